@@ -1,0 +1,110 @@
+"""ctypes binding of libcglgan_hip.so (the C ABI declared in include/cglgan.h).
+
+The library is the product: there is no Python or CPU fallback.  If the shared object is
+missing, importing this module raises immediately (build it with ``make -C cgl-gan_amd`` or
+``python -c "import __graft_entry__ as g; g.build()"``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libcglgan_hip.so")
+
+MAX_LAYERS = 8
+LOSS_CE2, LOSS_BCE = 0, 1
+WEIGHT_CAPGAN, WEIGHT_MEAN, WEIGHT_MIX_SINGLE, WEIGHT_MIX_DOUBLE, WEIGHT_CGLGAN = 0, 1, 2, 3, 4
+PHASE_ALL, PHASE_A, PHASE_B = 0, 1, 2
+MODEL_G, MODEL_D = 0, 1
+
+# every symbol include/cglgan.h declares (checked by tests/test_lib_exports.py)
+EXPORTS = [
+    "cgl_gan_param_count", "cgl_gan_param_tensor", "cgl_gan_running_count", "cgl_gan_workspace_bytes",
+    "cgl_gan_create", "cgl_gan_destroy", "cgl_gan_reset", "cgl_gan_run", "cgl_gan_run_graph",
+    "cgl_gan_alpha_scale", "cgl_gan_exchange_buffer", "cgl_gan_tensor", "cgl_gan_read_stats",
+    "cgl_gan_plan_info", "cgl_linear_fwd", "cgl_linear_bwd_data", "cgl_linear_bwd_weight", "cgl_adam_step",
+    "cgl_normal_fill", "cgl_op_workspace_bytes", "cgl_version",
+]
+
+
+class MlpSpec(ctypes.Structure):
+    _fields_ = [("n_layers", ctypes.c_int), ("dims", ctypes.c_int * (MAX_LAYERS + 1)),
+                ("bn", ctypes.c_int * MAX_LAYERS)]
+
+
+class GanConfig(ctypes.Structure):
+    _fields_ = [("g", MlpSpec), ("d", MlpSpec), ("batch", ctypes.c_int), ("batch_real", ctypes.c_int),
+                ("epoch", ctypes.c_int), ("loss", ctypes.c_int), ("weighting", ctypes.c_int),
+                ("n_workers", ctypes.c_int), ("rank", ctypes.c_int), ("exchange_layer", ctypes.c_int),
+                ("lr_g", ctypes.c_float), ("lr_d", ctypes.c_float), ("beta1", ctypes.c_float),
+                ("beta2", ctypes.c_float), ("adam_eps", ctypes.c_float), ("bn_eps", ctypes.c_float),
+                ("bn_momentum", ctypes.c_float), ("slope", ctypes.c_float), ("seed", ctypes.c_ulonglong),
+                ("gen_z", ctypes.c_int), ("sample_n", ctypes.c_int)]
+
+
+class GanBuffers(ctypes.Structure):
+    _fields_ = [("g_params", ctypes.c_void_p), ("g_grads", ctypes.c_void_p), ("g_m", ctypes.c_void_p),
+                ("g_v", ctypes.c_void_p), ("g_running", ctypes.c_void_p), ("d_params", ctypes.c_void_p),
+                ("d_grads", ctypes.c_void_p), ("d_m", ctypes.c_void_p), ("d_v", ctypes.c_void_p),
+                ("z", ctypes.c_void_p), ("real", ctypes.c_void_p), ("real_idx", ctypes.c_void_p),
+                ("losses_all", ctypes.c_void_p), ("workspace", ctypes.c_void_p),
+                ("workspace_bytes", ctypes.c_int64)]
+
+
+class GanStats(ctypes.Structure):
+    _fields_ = [("round", ctypes.c_int), ("d_loss", ctypes.c_float * 8), ("d_real", ctypes.c_float * 8),
+                ("d_fake", ctypes.c_float * 8), ("g_loss", ctypes.c_float), ("alpha", ctypes.c_float),
+                ("F", ctypes.c_float), ("lambda_", ctypes.c_float), ("bn_batches", ctypes.c_longlong)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libcglgan_hip.so not built ({LIB_PATH}); run `make -C cgl-gan_amd` "
+                          "(there is no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    P = ctypes.POINTER
+    vp, i64, ci, cf = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float
+    sig = {
+        "cgl_gan_param_count": (i64, [P(GanConfig), ci]),
+        "cgl_gan_param_tensor": (ci, [P(GanConfig), ci, ci, P(i64), P(ci), P(ci), P(ci), P(ci)]),
+        "cgl_gan_running_count": (i64, [P(GanConfig)]),
+        "cgl_gan_workspace_bytes": (i64, [P(GanConfig)]),
+        "cgl_gan_create": (ci, [P(GanConfig), P(GanBuffers), P(vp)]),
+        "cgl_gan_destroy": (ci, [vp]),
+        "cgl_gan_reset": (ci, [vp, P(cf), vp]),
+        "cgl_gan_run": (ci, [vp, ci, vp]),
+        "cgl_gan_run_graph": (ci, [vp, ci, vp]),
+        "cgl_gan_alpha_scale": (ci, [vp, vp]),
+        "cgl_gan_exchange_buffer": (ci, [vp, P(vp), P(i64)]),
+        "cgl_gan_tensor": (ci, [vp, ci, P(vp), P(i64)]),
+        "cgl_gan_read_stats": (ci, [vp, P(GanStats), vp]),
+        "cgl_gan_plan_info": (ci, [vp, ci, P(ci), P(ci), P(ctypes.c_double)]),
+        "cgl_linear_fwd": (ci, [vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, i64, vp]),
+        "cgl_linear_bwd_data": (ci, [vp, vp, vp, ci, ci, ci, vp, i64, vp]),
+        "cgl_linear_bwd_weight": (ci, [vp, vp, vp, vp, ci, ci, ci, vp, i64, vp]),
+        "cgl_adam_step": (ci, [vp, vp, vp, vp, i64, ci, cf, cf, cf, cf, vp, i64, vp]),
+        "cgl_normal_fill": (ci, [vp, i64, ctypes.c_ulonglong, ci, ci, vp]),
+        "cgl_op_workspace_bytes": (i64, []),
+        "cgl_version": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(rc, what="libcglgan_hip"):
+    """Turn a non-zero C-ABI return code into RuntimeError (include/cglgan.h conventions)."""
+    if rc != 0:
+        kinds = {-1: "invalid argument", -2: "bad call order", -3: "buffer too small"}
+        raise RuntimeError(f"{what} failed: rc={rc} ({kinds.get(rc, 'hipError')})")
+    return rc
+
+
+def version():
+    return lib.cgl_version().decode()

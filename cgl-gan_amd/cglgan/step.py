@@ -1,0 +1,226 @@
+"""One worker's fused GAN round on its own MI355X: the drop-in for the reference's
+Server.train + Worker.train pair (capgan.py:211-262 + :316-349, mixed-gan.py:238-292 + :355-392,
+MDGAN/MNIST/mdgan.py:180-207 + :266-297, CGLGAN/2DMG/main.py:225-278 + :344-375).
+
+All device memory is allocated here with torch (the caching allocator owns it); the HIP library
+borrows it.  Parameters live in one flat fp32 buffer per model (G, D) with the reference's
+state-dict keys exposed as views, so ``state_dict()`` / ``load_state_dict()`` interoperate with
+checkpoints written by the reference (``torch.save(net_g.state_dict())`` capgan.py:186).
+"""
+from __future__ import annotations
+
+import ctypes
+from collections import OrderedDict
+
+import torch
+
+from . import _lib as C
+from .specs import MlpModel
+
+_WEIGHTING = {"capgan": C.WEIGHT_CAPGAN, "mean": C.WEIGHT_MEAN, "mix_single": C.WEIGHT_MIX_SINGLE,
+              "mix_double": C.WEIGHT_MIX_DOUBLE, "cglgan": C.WEIGHT_CGLGAN}
+
+
+def _spec(m: MlpModel) -> C.MlpSpec:
+    s = C.MlpSpec()
+    s.n_layers = m.n_layers
+    for i, v in enumerate(m.dims):
+        s.dims[i] = v
+    for i, v in enumerate(m.bn):
+        s.bn[i] = v
+    return s
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class GanStep:
+    """Fused worker round.  ``run()`` = one communication round of one worker.
+
+    Knobs mirror the reference drivers' module globals: ``batch`` (batch_size, capgan.py:48),
+    ``epoch`` (local D steps, capgan.py:50), ``b1``/``b2`` (capgan.py:52-53), lr 2e-4 (:122).
+    """
+
+    def __init__(self, g: MlpModel, d: MlpModel, batch: int, batch_real: int = None, epoch: int = 1,
+                 loss: str = "ce", weighting: str = "capgan", n_workers: int = 1, rank: int = 0,
+                 exchange_layer: int = -1, lr_g: float = 2e-4, lr_d: float = 2e-4, betas=(0.5, 0.999),
+                 adam_eps: float = 1e-8, bn_eps: float = 0.8, bn_momentum: float = 0.1, slope: float = 0.2,
+                 seed: int = 20211212, gen_z: bool = False, real: torch.Tensor = None, sample_n: int = 0,
+                 real_idx: torch.Tensor = None, device="cuda"):
+        self.gm, self.dm = g, d
+        self.B = batch
+        self.Br = batch_real or batch
+        self.epoch = epoch
+        self.device = torch.device(device)
+        cfg = C.GanConfig()
+        cfg.g, cfg.d = _spec(g), _spec(d)
+        cfg.batch, cfg.batch_real, cfg.epoch = batch, self.Br, epoch
+        cfg.loss = C.LOSS_CE2 if loss == "ce" else C.LOSS_BCE
+        cfg.weighting = _WEIGHTING[weighting]
+        cfg.n_workers, cfg.rank, cfg.exchange_layer = n_workers, rank, exchange_layer
+        cfg.lr_g, cfg.lr_d = lr_g, lr_d
+        cfg.beta1, cfg.beta2, cfg.adam_eps = betas[0], betas[1], adam_eps
+        cfg.bn_eps, cfg.bn_momentum, cfg.slope = bn_eps, bn_momentum, slope
+        cfg.seed, cfg.gen_z, cfg.sample_n = seed, int(gen_z), sample_n
+        self.cfg = cfg
+        self.n_workers, self.rank = n_workers, rank
+
+        dev = self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        ng = C.lib.cgl_gan_param_count(ctypes.byref(cfg), C.MODEL_G)
+        nd = C.lib.cgl_gan_param_count(ctypes.byref(cfg), C.MODEL_D)
+        nr = C.lib.cgl_gan_running_count(ctypes.byref(cfg))
+        wsb = C.lib.cgl_gan_workspace_bytes(ctypes.byref(cfg))
+        if ng < 0 or nd < 0 or wsb < 0:
+            raise RuntimeError(f"invalid GAN configuration (rc={min(ng, nd, wsb)})")
+        self.g_params, self.g_grads = torch.zeros(ng, **f32), torch.zeros(ng, **f32)
+        self.g_m, self.g_v = torch.zeros(ng, **f32), torch.zeros(ng, **f32)
+        self.g_running = torch.zeros(max(nr, 1), **f32)
+        self.d_params, self.d_grads = torch.zeros(nd, **f32), torch.zeros(nd, **f32)
+        self.d_m, self.d_v = torch.zeros(nd, **f32), torch.zeros(nd, **f32)
+        self.z = torch.zeros(2 * batch, g.dims[0], **f32)
+        img = g.dims[-1]
+        if real is None:
+            real = torch.zeros(epoch * self.Br, img, **f32)
+        self.real = real
+        self.real_idx = real_idx
+        self.losses_all = torch.zeros(max(n_workers, 1), **f32)
+        self.workspace = torch.zeros(wsb, dtype=torch.uint8, device=dev)
+
+        bufs = C.GanBuffers()
+        for name in ("g_params", "g_grads", "g_m", "g_v", "g_running", "d_params", "d_grads", "d_m", "d_v", "z",
+                     "real", "losses_all", "workspace"):
+            setattr(bufs, name, self.__dict__[name].data_ptr())
+        bufs.real_idx = real_idx.data_ptr() if real_idx is not None else None
+        bufs.workspace_bytes = wsb
+        self._bufs = bufs
+        h = ctypes.c_void_p()
+        C.check(C.lib.cgl_gan_create(ctypes.byref(cfg), ctypes.byref(bufs), ctypes.byref(h)), "cgl_gan_create")
+        self._h = h
+        self.g_views = self._views(g, C.MODEL_G, self.g_params)
+        self.d_views = self._views(d, C.MODEL_D, self.d_params)
+        self.g_grad_views = self._views(g, C.MODEL_G, self.g_grads)
+        self.d_grad_views = self._views(d, C.MODEL_D, self.d_grads)
+        self._running_views()
+        self.reset()
+
+    # ------------------------------------------------------------------ layout views
+    def _views(self, m: MlpModel, which, flat):
+        keys = m.tensor_keys()
+        out = OrderedDict()
+        for i, k in enumerate(keys):
+            off, rows, cols, layer, kind = (ctypes.c_int64(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int(),
+                                            ctypes.c_int())
+            C.check(C.lib.cgl_gan_param_tensor(ctypes.byref(self.cfg), which, i, ctypes.byref(off), ctypes.byref(rows),
+                                               ctypes.byref(cols), ctypes.byref(layer), ctypes.byref(kind)))
+            n = rows.value * cols.value
+            v = flat[off.value:off.value + n]
+            out[k] = v.view(rows.value, cols.value) if kind.value == 0 else v
+        return out
+
+    def _running_views(self):
+        self.running = OrderedDict()
+        off = 0
+        al = lambda n: (n + 63) // 64 * 64
+        for l in self.gm.bn_layers():
+            n = self.gm.dims[l + 1]
+            k = self.gm.bn_keys[l]
+            self.running[k + ".running_mean"] = self.g_running[off:off + n]
+            off += al(n)
+            self.running[k + ".running_var"] = self.g_running[off:off + n]
+            off += al(n)
+
+    # ------------------------------------------------------------------ state
+    def reset(self, beta=None):
+        """Zero lambda / round counters, set beta (data-size weights, capgan.py:149-153)."""
+        b = beta if beta is not None else [1.0 / self.n_workers] * self.n_workers
+        arr = (ctypes.c_float * len(b))(*[float(x) for x in b])
+        C.check(C.lib.cgl_gan_reset(self._h, arr, _stream()), "cgl_gan_reset")
+        for k, v in self.running.items():
+            v.fill_(0.0 if k.endswith("running_mean") else 1.0)
+
+    @torch.no_grad()
+    def load_state_dicts(self, g_sd, d_sd):
+        for k, v in self.g_views.items():
+            v.copy_(g_sd[k].reshape(v.shape))
+        for k, v in self.d_views.items():
+            v.copy_(d_sd[k].reshape(v.shape))
+        for k, v in self.running.items():
+            if k in g_sd:
+                v.copy_(g_sd[k])
+        self.g_m.zero_(); self.g_v.zero_(); self.d_m.zero_(); self.d_v.zero_()
+
+    def g_state_dict(self):
+        sd = OrderedDict()
+        st = self.stats()
+        for k, v in self.g_views.items():
+            sd[k] = v.detach().clone()
+        for l in self.gm.bn_layers():
+            k = self.gm.bn_keys[l]
+            sd[k + ".running_mean"] = self.running[k + ".running_mean"].clone()
+            sd[k + ".running_var"] = self.running[k + ".running_var"].clone()
+            sd[k + ".num_batches_tracked"] = torch.tensor(st["bn_batches"], dtype=torch.long)
+        return sd
+
+    def d_state_dict(self):
+        return OrderedDict((k, v.detach().clone()) for k, v in self.d_views.items())
+
+    # ------------------------------------------------------------------ execution
+    def run(self, phase=C.PHASE_ALL, graph=False):
+        fn = C.lib.cgl_gan_run_graph if graph else C.lib.cgl_gan_run
+        C.check(fn(self._h, phase, _stream()), "cgl_gan_run")
+
+    def alpha_scale(self):
+        C.check(C.lib.cgl_gan_alpha_scale(self._h, _stream()), "cgl_gan_alpha_scale")
+
+    def exchange_buffer(self):
+        p, n = ctypes.c_void_p(), ctypes.c_int64()
+        C.check(C.lib.cgl_gan_exchange_buffer(self._h, ctypes.byref(p), ctypes.byref(n)))
+        return self._wrap(p.value, n.value)
+
+    def g_output(self):
+        """[2B, img] G output of the last round: rows < B = Xd, rows >= B = Xg."""
+        p, n = ctypes.c_void_p(), ctypes.c_int64()
+        C.check(C.lib.cgl_gan_tensor(self._h, 0, ctypes.byref(p), ctypes.byref(n)))
+        return self._wrap(p.value, n.value).view(2 * self.B, -1)
+
+    def own_loss(self):
+        p, n = ctypes.c_void_p(), ctypes.c_int64()
+        C.check(C.lib.cgl_gan_tensor(self._h, 1, ctypes.byref(p), ctypes.byref(n)))
+        return self._wrap(p.value, 1)
+
+    def _wrap(self, addr, n):
+        """View of a workspace region (the address lies inside self.workspace)."""
+        base = self.workspace.data_ptr()
+        off = addr - base
+        if addr == 0 or off < 0 or off + 4 * n > self.workspace.numel():
+            raise RuntimeError("address outside the context workspace")
+        return self.workspace[off:off + 4 * n].view(torch.float32)
+
+    def stats(self):
+        s = C.GanStats()
+        C.check(C.lib.cgl_gan_read_stats(self._h, ctypes.byref(s), _stream()), "cgl_gan_read_stats")
+        return {"round": s.round, "d_loss": list(s.d_loss)[:self.epoch], "d_real": list(s.d_real)[:self.epoch],
+                "d_fake": list(s.d_fake)[:self.epoch], "g_loss": s.g_loss, "alpha": s.alpha, "F": s.F,
+                "lambda": s.lambda_, "bn_batches": s.bn_batches}
+
+    def plan_info(self, phase=C.PHASE_ALL):
+        nl, ng, fl = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
+        C.check(C.lib.cgl_gan_plan_info(self._h, phase, ctypes.byref(nl), ctypes.byref(ng), ctypes.byref(fl)))
+        return {"launches": nl.value, "gemm_launches": ng.value, "gemm_flops": fl.value}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            C.lib.cgl_gan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,122 @@
+// Internal descriptors shared by the HIP kernels and the host runtime of libcglgan_hip.
+// Nothing here crosses the public C-ABI (include/cglgan.h); the runtime builds these
+// descriptors once per context, uploads them to device memory and replays them.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define CGL_WAVE 64
+#define CGL_GEMM_THREADS 256
+#define CGL_GEMM_KCHUNK 16           // k per MFMA chunk: 8 per lane half (k-permuted)
+#define CGL_TF_MAXK 1024             // max K for the in-LDS BatchNorm transform table
+
+enum { CGL_EPI_ACT_NONE = 0, CGL_EPI_ACT_LEAKY = 1, CGL_EPI_ACT_TANH = 2 };
+
+// Row source of a row-major operand whose rows are the non-contiguous index.
+// Row r < split comes from p0 (optionally through idx0[idx_off + r]), rows >= split from p1.
+struct CglRowSrc {
+  const float* p0;
+  const float* p1;
+  const int* idx0;        // optional gather for segment 0
+  const int* idx_off;     // optional device offset added to the gather position
+  int split;              // first row of segment 1 (INT32_MAX = single segment)
+  int ld;                 // row stride in floats (both segments)
+};
+
+// Forward-BatchNorm transform applied to the A operand as it is loaded (consumer side).
+// The producer GEMM wrote per-(row tile, group slot, feature) partials {sum, M2}.
+struct CglBnFwd {
+  const float* part;      // [ntiles][2][K][2]
+  int part_bm;            // producer rows per tile
+  int gr;                 // rows per BatchNorm group (one forward call of the reference)
+  int mtot;               // total rows in the producer output
+  const float* gamma;
+  const float* beta;
+  float eps, momentum, slope;
+  float* run_mean;        // updated by workgroup 0 (group 0 first, then 1), may be null
+  float* run_var;
+  float* save_mean;       // [ngroups][K] (workgroup 0), may be null
+  float* save_invstd;
+};
+
+struct CglGemmDesc {
+  int M, N, K;
+  int WM, WN, WK;         // wave arrangement, WM*WN*WK == 4
+  int tiles_m, tiles_n;
+  int wg_begin;           // first workgroup of this problem in a grouped launch
+  int layout;             // 0: NT (A[m][k], B[n][k]); 1: NN (A[m][k], B[k][n]); 2: TN (A[k][m], B[k][n])
+  int a_vec, b_vec;       // 16-byte vector loads allowed along k (kc operands)
+  CglRowSrc a, b;
+  // A transform (kc A only)
+  int a_tf;               // 0 none, 1 BatchNorm+LeakyReLU from producer partials
+  CglBnFwd bn;
+  float* a_copy;          // optional copy-out of the (transformed) A rows; rows >= a_copy_row0
+  int a_copy_ld, a_copy_row0;
+  // B extras
+  int b_ones_col;         // logical column N-1 of B is all ones (bias-gradient trick)
+  // epilogue
+  float* C; int ldc;
+  const float* bias;
+  int act; float slope;
+  const float* mask_ref; int mask_ld;     // v *= (ref > 0 ? 1 : slope)
+  const float* tanh_ref; int tanh_ld;     // v *= 1 - t*t
+  float* stat_part; int stat_gr;          // forward BatchNorm partials of the stored output
+  float* bias_out;                        // with b_ones_col: column N-1 of C goes here
+};
+
+// D output layer + adversarial loss (+ its backward into the last hidden layer).
+struct CglHeadDesc {
+  int M, F, C;            // rows, input features, logits (2: CE, 1: Sigmoid+BCE)
+  int loss;               // 0 CE, 1 BCE
+  const float* P; int ldp;        // last hidden activations (post-LeakyReLU) [M][F]
+  const float* W; const float* b; // [C][F], [C]
+  int split;              // rows < split: target t0 weight w0; others: t1, w1
+  int t0, t1;
+  float w0, w1;           // dlogit scale per segment (mean and the 0.5 of D_loss folded in)
+  float* dlogits;         // [M][C] (optional)
+  float* dP; int lddp;    // (dlogits . W) * leaky'(P)
+  float slope;
+  float* part;            // [nwg][2] per-workgroup loss sums per segment
+  unsigned int* counter;  // last-arriver ticket (zero at rest)
+  float* loss_out;        // [2]: mean loss of segment 0 and 1 (written by the last workgroup)
+  float combine;          // D_loss = (seg0 + seg1) * combine  (0.5: capgan.py:339, 1: CGLGAN/2DMG/main.py:364)
+  float* combine_out;     // optional
+  int rows_per_wg;
+};
+
+// BatchNorm1d backward for one layer, fused with the LeakyReLU mask of its output.
+struct CglBnBwdDesc {
+  int M, F;
+  const float* dA; int ld_da;     // gradient w.r.t. the LeakyReLU output
+  const float* post; int ld_post; // LeakyReLU output (mask source)
+  const float* Y; int ld_y;       // BatchNorm input (pre-BN)
+  const float* mean; const float* invstd; const float* gamma;
+  float* dZ; int ld_dz;           // gradient w.r.t. the BatchNorm input
+  float* g_gamma; float* g_beta;
+  float slope;
+};
+
+#define CGL_MAX_EPOCH 8
+#define CGL_MAX_WORKERS 64
+
+// Per-context device scalar block.  Written only by cgl_step_begin (counters, Adam bias
+// corrections), by the head kernels' last workgroup (losses), by cgl_alpha_scale and by
+// the scalar tail of the G Adam launch; every other kernel only reads it.
+struct CglStepState {
+  int round;                        // rounds started
+  int n_workers, rank, weighting;   // exchange configuration
+  float g_step_size, g_bc2sqrt;     // Adam bias corrections for this round's G update
+  float d_step_size[CGL_MAX_EPOCH], d_bc2sqrt[CGL_MAX_EPOCH];
+  float lambda;                     // CAPGAN / Mix-G / CGLGAN lambda
+  float d_loss_parts[CGL_MAX_EPOCH][2];  // mean real / fake loss of each local D step
+  float d_loss[CGL_MAX_EPOCH];
+  float g_loss_parts[2];            // [0] = own G loss (mean over rows)
+  float alpha;                      // weight applied to the own G-loss gradient
+  float F;                          // F_max reported by the reference's Server.train
+  float beta[CGL_MAX_WORKERS];      // data-size weights
+  float losses[CGL_MAX_WORKERS];    // gathered G losses (N > 1)
+  float alphas[CGL_MAX_WORKERS];
+  long long bn_batches;             // num_batches_tracked of every G BatchNorm layer
+};
+
+enum { CGL_W_CAPGAN = 0, CGL_W_MEAN = 1, CGL_W_MIX_SINGLE = 2, CGL_W_MIX_DOUBLE = 3, CGL_W_CGLGAN = 4 };

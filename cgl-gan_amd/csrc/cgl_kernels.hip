@@ -1,0 +1,369 @@
+// Non-GEMM kernels of the MLP GAN step (gfx950).
+//
+//  cgl_head_loss   D output layer (2 logits or 1 Sigmoid unit) + CrossEntropy / BCE loss, its
+//                  backward into the last hidden layer, and the batch-mean loss reduced by the
+//                  last-arriving workgroup (reference: nn.Linear(256,2) model/mnist_model.py:81,
+//                  nn.CrossEntropyLoss capgan.py:311, nn.BCELoss CGLGAN/2DMG/main.py:336).
+//  cgl_bn_bwd      BatchNorm1d(eps=0.8) train-mode backward fused with the LeakyReLU' mask of its
+//                  output (model/mnist_model.py:13-14; autograd in Server.train capgan.py:258).
+//  cgl_adam        flat multi-tensor Adam, op order of torch 2.10 _single_tensor_adam
+//                  (optim.Adam(lr=2e-4, betas=(0.5, 0.999)) capgan.py:158,312), plus the scalar
+//                  tail of the round (lambda SGD capgan.py:140-141,259; F_max :249).
+//  cgl_step_begin  per-round counters and Adam bias corrections (device-side, graph-replayable).
+//  cgl_normal      Philox4x32-10 + Box-Muller N(0,1) for z (capgan.py:216,219).
+//  cgl_alpha_scale lambda-weighting of gathered worker losses (capgan.py:247-248,
+//                  mixed-gan.py:276, MDGAN/MNIST/mdgan.py:203, CGLGAN/2DMG/main.py:261-264) and the
+//                  scaling of this worker's gradient contribution before the RCCL all-reduce.
+#include "cgl_internal.h"
+
+// ------------------------------------------------------------------------------------------
+// wave-level sum
+__device__ __forceinline__ float cgl_wave_sum(float x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
+__global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restrict__ hd) {
+  __shared__ float s_loss[4][2];
+  __shared__ int s_last;
+  const int M = hd->M, F = hd->F, C = hd->C;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int r0 = blockIdx.x * hd->rows_per_wg;
+  const int r1 = min(r0 + hd->rows_per_wg, M);
+  float lsum[2] = {0.f, 0.f};
+  for (int r = r0 + wave; r < r1; r += 4) {
+    const float* __restrict__ p = hd->P + (long)r * hd->ldp;
+    float z[2];
+    for (int c = 0; c < C; ++c) {
+      const float* __restrict__ w = hd->W + (long)c * F;
+      float s = 0.f;
+      for (int f = lane; f < F; f += 64) s = fmaf(p[f], w[f], s);
+      z[c] = cgl_wave_sum(s) + hd->b[c];
+    }
+    const int seg = r < hd->split ? 0 : 1;
+    const int t = seg ? hd->t1 : hd->t0;
+    const float wgt = seg ? hd->w1 : hd->w0;
+    float dl[2];
+    float lossv;
+    if (hd->loss == 0) {
+      // log_softmax over the 2 logits + NLL (torch: x - max - log(sum(exp(x - max))))
+      const float mx = fmaxf(z[0], z[1]);
+      const float se = expf(z[0] - mx) + expf(z[1] - mx);
+      const float lse = logf(se);
+      const float o0 = z[0] - mx - lse, o1 = z[1] - mx - lse;
+      lossv = -(t == 0 ? o0 : o1);
+      // NLL backward (-w at target) through log_softmax backward: g - exp(out) * sum(g)
+      dl[0] = (t == 0 ? -wgt : 0.f) + expf(o0) * wgt;
+      dl[1] = (t == 1 ? -wgt : 0.f) + expf(o1) * wgt;
+    } else {
+      // Sigmoid + BCELoss (log clamped at -100, EPSILON 1e-12 in the backward)
+      const float pr = 1.f / (1.f + expf(-z[0]));
+      const float y = (float)t;
+      const float lp = fmaxf(logf(pr), -100.f), l1p = fmaxf(logf(1.f - pr), -100.f);
+      lossv = -(y * lp + (1.f - y) * l1p);
+      const float gp = wgt * (pr - y) / fmaxf((1.f - pr) * pr, 1e-12f);
+      dl[0] = gp * (1.f - pr) * pr;
+      dl[1] = 0.f;
+    }
+    lsum[seg] += lossv;
+    if (hd->dlogits && lane < C) hd->dlogits[(long)r * C + lane] = dl[lane];
+    if (hd->dP) {
+      float* __restrict__ dp = hd->dP + (long)r * hd->lddp;
+      const float sl = hd->slope;
+      for (int f = lane; f < F; f += 64) {
+        float g = dl[0] * hd->W[f];
+        if (C == 2) g = fmaf(dl[1], hd->W[F + f], g);
+        dp[f] = p[f] > 0.f ? g : g * sl;
+      }
+    }
+  }
+  if (lane == 0) {
+    s_loss[wave][0] = lsum[0];
+    s_loss[wave][1] = lsum[1];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.f, b = 0.f;
+    for (int q = 0; q < 4; ++q) {
+      a += s_loss[q][0];
+      b += s_loss[q][1];
+    }
+    hd->part[blockIdx.x * 2 + 0] = a;
+    hd->part[blockIdx.x * 2 + 1] = b;
+    // last-arriver reduction (agent-scope release before the ticket, acquire after)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned int ticket =
+        __hip_atomic_fetch_add(hd->counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (ticket == gridDim.x - 1);
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      double s0 = 0.0, s1 = 0.0;
+      for (unsigned int q = 0; q < gridDim.x; ++q) {
+        s0 += (double)__hip_atomic_load(hd->part + q * 2 + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s1 += (double)__hip_atomic_load(hd->part + q * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const int n0 = min(hd->split, M), n1 = M - n0;
+      const float l0 = n0 > 0 ? (float)(s0 / n0) : 0.f;
+      const float l1 = n1 > 0 ? (float)(s1 / n1) : 0.f;
+      hd->loss_out[0] = l0;
+      hd->loss_out[1] = l1;
+      if (hd->combine_out) *hd->combine_out = (l0 + l1) * hd->combine;
+      __hip_atomic_store(hd->counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// BatchNorm1d backward (train) + LeakyReLU' mask.  One workgroup owns 32 features and all M
+// rows, so the per-feature reductions stay inside the workgroup (fixed order, double accum).
+__global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict__ bd) {
+  __shared__ double s_a[8][32], s_b[8][32];
+  const int M = bd->M, F = bd->F;
+  const int fl = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int f = blockIdx.x * 32 + fl;
+  const bool fok = f < F;
+  const float sl = bd->slope;
+  const float mean = fok ? bd->mean[f] : 0.f;
+  const float invstd = fok ? bd->invstd[f] : 0.f;
+  double sum = 0.0, dotp = 0.0;
+  if (fok) {
+    for (int r = rg; r < M; r += 8) {
+      const float da = bd->dA[(long)r * bd->ld_da + f];
+      const float po = bd->post[(long)r * bd->ld_post + f];
+      const float dy = po > 0.f ? da : da * sl;
+      const float y = bd->Y[(long)r * bd->ld_y + f];
+      sum += (double)dy;
+      dotp += (double)((y - mean) * dy);
+    }
+  }
+  s_a[rg][fl] = sum;
+  s_b[rg][fl] = dotp;
+  __syncthreads();
+  double S = 0.0, D = 0.0;
+  for (int q = 0; q < 8; ++q) {
+    S += s_a[q][fl];
+    D += s_b[q][fl];
+  }
+  if (!fok) return;
+  const float w = bd->gamma[f];
+  const float k = (float)D * invstd * invstd / M;
+  const float gmean = (float)(S / M);
+  for (int r = rg; r < M; r += 8) {
+    const float da = bd->dA[(long)r * bd->ld_da + f];
+    const float po = bd->post[(long)r * bd->ld_post + f];
+    const float dy = po > 0.f ? da : da * sl;
+    const float y = bd->Y[(long)r * bd->ld_y + f];
+    const float gi = (y - mean) * k;
+    bd->dZ[(long)r * bd->ld_dz + f] = (dy - gmean - gi) * invstd * w;
+  }
+  if (rg == 0) {
+    bd->g_gamma[f] = (float)(D * (double)invstd);
+    bd->g_beta[f] = (float)S;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+struct CglAdamArgs {
+  float* p; const float* g; float* m; float* v;
+  long n;
+  const float* step_size;   // device scalars (CglStepState fields)
+  const float* bc2sqrt;
+  float b2, w1, w2, eps;   // w1 = (float)(1 - beta1), w2 = (float)(1 - beta2) computed in double
+};
+
+__device__ __forceinline__ float cgl_lerp(float self, float end, float w) {
+  // at::lerp: |w| < 0.5 ? self + w * (end - self) : end - (end - self) * (1 - w)
+  return fabsf(w) < 0.5f ? self + w * (end - self) : end - (end - self) * (1.f - w);
+}
+
+__device__ __forceinline__ float cgl_softmax_at(const float* x, int n, int i) {
+  float mx = x[0];
+  for (int q = 1; q < n; ++q) mx = fmaxf(mx, x[q]);
+  float s = 0.f;
+  for (int q = 0; q < n; ++q) s += expf(x[q] - mx);
+  return expf(x[i] - mx) / s;
+}
+
+// alpha_i for every worker from the gathered losses (the reference's Server.train weighting).
+__device__ void cgl_weights(int mode, int N, float lam, const float* beta, const float* loss, float* alpha) {
+  float tmp[CGL_MAX_WORKERS], tmp2[CGL_MAX_WORKERS];
+  if (mode == CGL_W_MEAN) {
+    for (int i = 0; i < N; ++i) alpha[i] = 1.f / N;
+    return;
+  }
+  if (mode == CGL_W_MIX_SINGLE) {
+    for (int i = 0; i < N; ++i) tmp[i] = beta[i] * lam * loss[i];
+    for (int i = 0; i < N; ++i) alpha[i] = cgl_softmax_at(tmp, N, i);
+    return;
+  }
+  for (int i = 0; i < N; ++i) tmp[i] = lam * loss[i];
+  for (int i = 0; i < N; ++i) tmp2[i] = cgl_softmax_at(tmp, N, i);   // softmax(lambda * l)
+  if (mode == CGL_W_CGLGAN) {
+    for (int i = 0; i < N; ++i) alpha[i] = (beta[i] + tmp2[i]) * 0.5f;
+    return;
+  }
+  if (mode == CGL_W_CAPGAN) {
+    for (int i = 0; i < N; ++i) tmp[i] = tmp2[i] * beta[i];          // softmax(a * beta)
+  } else {  // CGL_W_MIX_DOUBLE
+    for (int i = 0; i < N; ++i) tmp[i] = beta[i] * tmp2[i];
+  }
+  for (int i = 0; i < N; ++i) alpha[i] = cgl_softmax_at(tmp, N, i);
+}
+
+__global__ __launch_bounds__(256) void cgl_adam(CglAdamArgs a, CglStepState* st, int tail) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const float ss = *a.step_size, bc = *a.bc2sqrt;
+  const float w1 = a.w1, w2 = a.w2;
+  if (i < a.n) {
+    const float g = a.g[i];
+    const float m = cgl_lerp(a.m[i], g, w1);
+    const float v = __fadd_rn(__fmul_rn(a.v[i], a.b2), __fmul_rn(__fmul_rn(w2, g), g));
+    a.m[i] = m;
+    a.v[i] = v;
+    const float denom = sqrtf(v) / bc + a.eps;
+    a.p[i] = a.p[i] + (-ss) * m / denom;
+  }
+  if (tail && i == 0) {
+    // scalar tail of Server.train: F_max and the lambda update (after every parameter read
+    // of this round, before the next round's step_begin).
+    const int N = st->n_workers;
+    const float lam = st->lambda;
+    float l[CGL_MAX_WORKERS];
+    if (N == 1) {
+      l[0] = st->g_loss_parts[0];
+    } else {
+      for (int q = 0; q < N; ++q) l[q] = st->losses[q];
+    }
+    float al[CGL_MAX_WORKERS];
+    cgl_weights(st->weighting, N, lam, st->beta, l, al);
+    if (st->weighting == CGL_W_MEAN) {
+      float s = 0.f;
+      for (int q = 0; q < N; ++q) s += l[q];
+      st->F = s / N;
+    } else if (st->weighting == CGL_W_CGLGAN) {
+      float fb = 0.f, fg = 0.f, g1 = 0.f, g2 = 0.f;
+      float gm[CGL_MAX_WORKERS], tmp[CGL_MAX_WORKERS];
+      for (int q = 0; q < N; ++q) tmp[q] = lam * l[q];
+      for (int q = 0; q < N; ++q) gm[q] = cgl_softmax_at(tmp, N, q);
+      for (int q = 0; q < N; ++q) {
+        fb += st->beta[q] * l[q];
+        fg += gm[q] * l[q];
+      }
+      st->F = (fb + fg) / 2.f;
+      for (int q = 0; q < N; ++q) {
+        g1 += l[q] * l[q] * gm[q];
+        g2 += l[q] * gm[q] * fg;
+      }
+      st->lambda = lam + 10.f * (g1 - g2);
+    } else {
+      float s = 0.f;
+      for (int q = 0; q < N; ++q) s += al[q] * l[q];
+      st->F = s - 0.001f * lam;
+      // optim.SGD([Lambda], lr=0.1): dF/dLambda = -0.001
+      st->lambda = lam + (-0.1f) * (-0.001f);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+struct CglBeginArgs {
+  CglStepState* st;
+  int epoch;
+  float lr_g, lr_d, b1, b2;
+  int bn_layers;
+};
+
+__global__ void cgl_step_begin(CglBeginArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  CglStepState* st = a.st;
+  const int r = st->round + 1;
+  st->round = r;
+  {
+    const double t = (double)r;
+    const double bc1 = 1.0 - pow((double)a.b1, t);
+    const double bc2 = 1.0 - pow((double)a.b2, t);
+    st->g_step_size = (float)((double)a.lr_g / bc1);
+    st->g_bc2sqrt = (float)pow(bc2, 0.5);
+  }
+  for (int e = 0; e < a.epoch; ++e) {
+    const double t = (double)((r - 1) * a.epoch + e + 1);
+    const double bc1 = 1.0 - pow((double)a.b1, t);
+    const double bc2 = 1.0 - pow((double)a.b2, t);
+    st->d_step_size[e] = (float)((double)a.lr_d / bc1);
+    st->d_bc2sqrt[e] = (float)pow(bc2, 0.5);
+  }
+  st->alpha = 1.f;
+  st->bn_batches += 2;
+}
+
+// ------------------------------------------------------------------------------------------
+// Philox4x32-10 counter-based RNG + Box-Muller: out[i] ~ N(0,1), fresh per round.
+__device__ __forceinline__ void cgl_philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)M0 * c[0], p1 = (uint64_t)M1 * c[2];
+    const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0;
+    const uint32_t h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+    const uint32_t n0 = h1 ^ c[1] ^ k0, n2 = h0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = l1; c[2] = n2; c[3] = l0;
+    k0 += W0; k1 += W1;
+  }
+}
+
+__global__ __launch_bounds__(256) void cgl_normal(float* out, long n, unsigned long long seed,
+                                                  const CglStepState* st, int stream_id) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;   // 4 outputs per thread
+  if (q * 4 >= n) return;
+  uint32_t c[4] = {(uint32_t)q, (uint32_t)(q >> 32), (uint32_t)(st ? st->round : 0), (uint32_t)stream_id};
+  cgl_philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const float inv = 2.3283064365386963e-10f;   // 2^-32
+  float z[4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float u1 = ((float)c[2 * j] + 1.0f) * inv;   // (0, 1]
+    const float u2 = (float)c[2 * j + 1] * inv;
+    const float rr = sqrtf(-2.0f * logf(u1));
+    float s, co;
+    sincosf(6.283185307179586f * u2, &s, &co);
+    z[2 * j] = rr * co;
+    z[2 * j + 1] = rr * s;
+  }
+  for (int j = 0; j < 4; ++j)
+    if (q * 4 + j < n) out[q * 4 + j] = z[j];
+}
+
+// ------------------------------------------------------------------------------------------
+// alpha from the gathered losses; scale this worker's gradient buffer by alpha[rank].
+__global__ __launch_bounds__(256) void cgl_alpha_scale(CglStepState* st, const float* losses, float* x,
+                                                       long n) {
+  __shared__ float s_alpha;
+  if (threadIdx.x == 0) {
+    const int N = st->n_workers;
+    float al[CGL_MAX_WORKERS];
+    cgl_weights(st->weighting, N, st->lambda, st->beta, losses, al);
+    s_alpha = al[st->rank];
+    if (blockIdx.x == 0) {
+      for (int q = 0; q < N; ++q) {
+        st->losses[q] = losses[q];
+        st->alphas[q] = al[q];
+      }
+      st->alpha = al[st->rank];
+    }
+  }
+  __syncthreads();
+  const float a = s_alpha;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    x[i] *= a;
+}
+
+// y[i] = sum over `parts` contiguous buffers (loopback reduction used by single-device
+// multi-worker rehearsal; the multi-GPU path uses RCCL instead)
+__global__ __launch_bounds__(256) void cgl_scale_inplace(float* x, long n, float a) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    x[i] *= a;
+}

@@ -1,0 +1,1090 @@
+// Host runtime of libcglgan_hip: plans one CGL-GAN communication round as a fixed list of
+// kernel launches over caller-owned buffers, and replays it eagerly or through a hipGraph.
+//
+// Replaces the reference's Python role loop: Server.train (capgan.py:211-262,
+// mixed-gan.py:238-292, MDGAN/MNIST/mdgan.py:180-207, CGLGAN/2DMG/main.py:225-278) and
+// Worker.train (capgan.py:316-349, mixed-gan.py:355-392, MDGAN/MNIST/mdgan.py:266-297,
+// CGLGAN/2DMG/main.py:344-375) -- on ONE device per worker, with G replicated per worker and
+// the reference's queue exchange turned into an all-reduce between phase A and phase B.
+//
+// Unity build: the kernels are compiled in this translation unit.
+#include "cgl_gemm.hip"
+#include "cgl_kernels.hip"
+#include "../../include/cglgan.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#define CGL_VERSION_STR "0.1.0 gfx950"
+
+namespace {
+
+inline int64_t al64(int64_t n) { return (n + 63) & ~int64_t(63); }
+
+struct TensorRec {
+  int64_t off;
+  int rows, cols, layer, kind;  // kind: 0 W, 1 b, 2 BN gamma, 3 BN beta
+};
+
+std::vector<TensorRec> param_layout(const cgl_mlp_spec& s, int64_t* total) {
+  std::vector<TensorRec> v;
+  int64_t off = 0;
+  for (int l = 0; l < s.n_layers; ++l) {
+    const int fo = s.dims[l + 1], fi = s.dims[l];
+    v.push_back({off, fo, fi, l, 0});
+    off += al64((int64_t)fo * fi);
+    v.push_back({off, fo, 1, l, 1});
+    off += al64(fo);
+    if (s.bn[l]) {
+      v.push_back({off, fo, 1, l, 2});
+      off += al64(fo);
+      v.push_back({off, fo, 1, l, 3});
+      off += al64(fo);
+    }
+  }
+  if (total) *total = off;
+  return v;
+}
+
+int64_t running_layout(const cgl_mlp_spec& s, int64_t* mean_off, int64_t* var_off) {
+  int64_t off = 0;
+  for (int l = 0; l < s.n_layers; ++l) {
+    if (mean_off) mean_off[l] = -1;
+    if (var_off) var_off[l] = -1;
+    if (!s.bn[l]) continue;
+    if (mean_off) mean_off[l] = off;
+    off += al64(s.dims[l + 1]);
+    if (var_off) var_off[l] = off;
+    off += al64(s.dims[l + 1]);
+  }
+  return off;
+}
+
+int validate(const cgl_gan_config* c) {
+  if (!c) return CGL_E_ARG;
+  const cgl_mlp_spec &g = c->g, &d = c->d;
+  if (g.n_layers < 1 || g.n_layers > CGL_MAX_LAYERS || d.n_layers < 2 || d.n_layers > CGL_MAX_LAYERS)
+    return CGL_E_ARG;
+  for (int l = 0; l <= g.n_layers; ++l)
+    if (g.dims[l] < 1) return CGL_E_ARG;
+  for (int l = 0; l <= d.n_layers; ++l)
+    if (d.dims[l] < 1) return CGL_E_ARG;
+  if (g.dims[g.n_layers] != d.dims[0]) return CGL_E_ARG;
+  if (g.bn[g.n_layers - 1]) return CGL_E_ARG;
+  for (int l = 0; l < d.n_layers; ++l)
+    if (d.bn[l]) return CGL_E_ARG;
+  for (int l = 0; l + 1 < g.n_layers; ++l)
+    if (g.bn[l] && g.dims[l + 1] > CGL_TF_MAXK) return CGL_E_ARG;
+  const int C = d.dims[d.n_layers];
+  if (c->loss == CGL_LOSS_CE2 && C != 2) return CGL_E_ARG;
+  if (c->loss == CGL_LOSS_BCE && C != 1) return CGL_E_ARG;
+  if (c->loss != CGL_LOSS_CE2 && c->loss != CGL_LOSS_BCE) return CGL_E_ARG;
+  if (c->batch < 2 || c->batch_real < 1 || c->epoch < 1 || c->epoch > CGL_MAX_EPOCH) return CGL_E_ARG;
+  if (c->n_workers < 1 || c->n_workers > CGL_MAX_WORKERS || c->rank < 0 || c->rank >= c->n_workers)
+    return CGL_E_ARG;
+  if (c->weighting < 0 || c->weighting > 4) return CGL_E_ARG;
+  if (c->exchange_layer != -1 && (c->exchange_layer < 1 || c->exchange_layer >= g.n_layers)) return CGL_E_ARG;
+  if (c->sample_n < 0 || (c->sample_n > 0 && c->sample_n % c->batch_real != 0)) return CGL_E_ARG;
+  return CGL_OK;
+}
+
+// ----------------------------------------------------------------------------------------
+// workspace carve (sizing pass with base == nullptr)
+struct Carve {
+  char* base;
+  int64_t off = 0;
+  explicit Carve(void* b) : base((char*)b) {}
+  template <class T>
+  T* take(int64_t count) {
+    const int64_t bytes = (count * (int64_t)sizeof(T) + 255) & ~int64_t(255);
+    T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+    off += bytes;
+    return p;
+  }
+};
+
+constexpr int kMaxGemmDescs = 128;
+constexpr int kMaxHeadDescs = 2 * CGL_MAX_EPOCH + 4;
+constexpr int kMaxBnDescs = 2 * CGL_MAX_LAYERS;
+constexpr int kHeadRows = 16;
+
+struct WS {
+  // G forward (2B rows)
+  float* gout[CGL_MAX_LAYERS];
+  float* gact[CGL_MAX_LAYERS];
+  float* gpart[CGL_MAX_LAYERS];
+  float* gmean[CGL_MAX_LAYERS];
+  float* ginvstd[CGL_MAX_LAYERS];
+  // D step (Md rows)
+  float* R;
+  float* P[CGL_MAX_LAYERS];
+  float* dQ[CGL_MAX_LAYERS];
+  float* dlog;
+  // D(Xg) (B rows)
+  float* S[CGL_MAX_LAYERS];
+  float* dS[CGL_MAX_LAYERS];
+  float* dYL;
+  // G backward (B rows)
+  float* gdA[CGL_MAX_LAYERS];
+  float* gG[CGL_MAX_LAYERS];
+  // misc
+  float* hpart;
+  unsigned int* counters;
+  CglStepState* st;
+  int* idx;       // sampler output when sample_n > 0
+  CglGemmDesc* gemm;
+  CglHeadDesc* head;
+  CglBnBwdDesc* bnb;
+  int64_t total;
+};
+
+WS carve_ws(const cgl_gan_config& c, void* base) {
+  WS w;
+  std::memset(&w, 0, sizeof(w));
+  Carve cv(base);
+  const cgl_mlp_spec &g = c.g, &d = c.d;
+  const int L = g.n_layers, J = d.n_layers;
+  const int B = c.batch, Md = c.batch_real + c.batch;
+  w.st = cv.take<CglStepState>(1);
+  w.counters = cv.take<unsigned int>(64);
+  w.gemm = cv.take<CglGemmDesc>(kMaxGemmDescs);
+  w.head = cv.take<CglHeadDesc>(kMaxHeadDescs);
+  w.bnb = cv.take<CglBnBwdDesc>(kMaxBnDescs);
+  for (int l = 0; l < L; ++l) {
+    const int f = g.dims[l + 1];
+    w.gout[l] = cv.take<float>((int64_t)2 * B * f);
+    if (l + 1 < L && g.bn[l]) {
+      w.gact[l] = cv.take<float>((int64_t)2 * B * f);
+      const int64_t tiles = (2 * B + 31) / 32;
+      w.gpart[l] = cv.take<float>(tiles * 2 * f * 2);
+      w.gmean[l] = cv.take<float>((int64_t)2 * f);
+      w.ginvstd[l] = cv.take<float>((int64_t)2 * f);
+      w.gdA[l] = cv.take<float>((int64_t)B * f);
+    }
+    if (l + 1 < L) w.gG[l] = cv.take<float>((int64_t)B * f);
+  }
+  w.R = cv.take<float>((int64_t)Md * d.dims[0]);
+  for (int j = 0; j + 1 < J; ++j) {
+    const int f = d.dims[j + 1];
+    w.P[j] = cv.take<float>((int64_t)Md * f);
+    w.dQ[j] = cv.take<float>((int64_t)Md * f);
+    w.S[j] = cv.take<float>((int64_t)B * f);
+    w.dS[j] = cv.take<float>((int64_t)B * f);
+  }
+  w.dlog = cv.take<float>((int64_t)Md * d.dims[J]);
+  w.dYL = cv.take<float>((int64_t)B * g.dims[L]);
+  w.hpart = cv.take<float>((int64_t)((Md + kHeadRows - 1) / kHeadRows) * 2);
+  w.idx = cv.take<int>((int64_t)c.epoch * c.batch_real);
+  w.total = cv.off;
+  return w;
+}
+
+// ----------------------------------------------------------------------------------------
+enum LaunchKind { K_GEMM, K_HEAD, K_BNBWD, K_ADAM, K_BEGIN, K_NORMAL, K_SAMPLE, K_ALPHA };
+
+struct Launch {
+  LaunchKind kind;
+  int grid = 1;
+  int first = 0, count = 0;  // descriptor range (host index)
+  CglAdamArgs adam{};
+  int tail = 0;
+  CglBeginArgs begin{};
+  float* nptr = nullptr;
+  long nn = 0;
+  int stream_id = 0;
+  double flops = 0.0;
+};
+
+void choose_tiles(CglGemmDesc& d, int force_wm = 0) {
+  static const int opts[4][3] = {{2, 2, 1}, {2, 1, 2}, {1, 2, 2}, {1, 1, 4}};
+  double best = 1e300;
+  for (auto& o : opts) {
+    if (force_wm && o[0] != force_wm) continue;
+    const int tm = (d.M + 32 * o[0] - 1) / (32 * o[0]);
+    const int tn = (d.N + 32 * o[1] - 1) / (32 * o[1]);
+    const double wgs = (double)tm * tn;
+    const int nch = (d.K + CGL_GEMM_KCHUNK - 1) / CGL_GEMM_KCHUNK;
+    const int per = (nch + o[2] - 1) / o[2];
+    const double t = (per * 8.0 + 24.0) * std::max(1.0, wgs / 256.0) + (o[2] - 1) * 6.0;
+    if (t < best - 1e-9) {
+      best = t;
+      d.WM = o[0];
+      d.WN = o[1];
+      d.WK = o[2];
+      d.tiles_m = tm;
+      d.tiles_n = tn;
+    }
+  }
+}
+
+CglGemmDesc make_gemm(int layout, int M, int N, int K) {
+  CglGemmDesc d;
+  std::memset(&d, 0, sizeof(d));
+  d.layout = layout;
+  d.M = M;
+  d.N = N;
+  d.K = K;
+  d.a.split = 0x7fffffff;
+  d.b.split = 0x7fffffff;
+  d.slope = 0.2f;
+  d.act = CGL_EPI_ACT_NONE;
+  choose_tiles(d);
+  return d;
+}
+
+CglRowSrc rows(const float* p, int ld) {
+  CglRowSrc r;
+  std::memset(&r, 0, sizeof(r));
+  r.p0 = p;
+  r.ld = ld;
+  r.split = 0x7fffffff;
+  return r;
+}
+
+inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+struct cgl_gan {
+  cgl_gan_config cfg;
+  cgl_gan_buffers bufs;
+  WS ws;
+  std::vector<CglGemmDesc> gemm;
+  std::vector<CglHeadDesc> head;
+  std::vector<CglBnBwdDesc> bnb;
+  std::vector<Launch> phA, phB;
+  hipGraphExec_t gexec[3] = {nullptr, nullptr, nullptr};
+  float* xchg = nullptr;
+  int64_t xchg_n = 0;
+  // parameter tensor pointers
+  std::vector<TensorRec> gl, dl;
+  int64_t run_mean_off[CGL_MAX_LAYERS], run_var_off[CGL_MAX_LAYERS];
+};
+
+namespace {
+
+const float* gparam(const cgl_gan* c, int layer, int kind) {
+  for (auto& t : c->gl)
+    if (t.layer == layer && t.kind == kind) return c->bufs.g_params + t.off;
+  return nullptr;
+}
+float* ggrad(const cgl_gan* c, int layer, int kind) {
+  for (auto& t : c->gl)
+    if (t.layer == layer && t.kind == kind) return c->bufs.g_grads + t.off;
+  return nullptr;
+}
+const float* dparam(const cgl_gan* c, int layer, int kind) {
+  for (auto& t : c->dl)
+    if (t.layer == layer && t.kind == kind) return c->bufs.d_params + t.off;
+  return nullptr;
+}
+float* dgrad(const cgl_gan* c, int layer, int kind) {
+  for (auto& t : c->dl)
+    if (t.layer == layer && t.kind == kind) return c->bufs.d_grads + t.off;
+  return nullptr;
+}
+
+// Add a grouped GEMM launch built from `descs` (workgroup offsets assigned here).
+void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> descs) {
+  Launch L;
+  L.kind = K_GEMM;
+  L.first = (int)c->gemm.size();
+  L.count = (int)descs.size();
+  int wg = 0;
+  for (auto& d : descs) {
+    d.wg_begin = wg;
+    wg += d.tiles_m * d.tiles_n;
+    const int nalg = d.b_ones_col ? d.N - 1 : d.N;
+    L.flops += 2.0 * d.M * (double)nalg * d.K;
+    c->gemm.push_back(d);
+  }
+  L.grid = wg;
+  ph.push_back(L);
+}
+
+void push_head(cgl_gan* c, std::vector<Launch>& ph, const CglHeadDesc& h) {
+  Launch L;
+  L.kind = K_HEAD;
+  L.first = (int)c->head.size();
+  L.count = 1;
+  L.grid = (h.M + kHeadRows - 1) / kHeadRows;
+  c->head.push_back(h);
+  ph.push_back(L);
+}
+
+void push_bnb(cgl_gan* c, std::vector<Launch>& ph, const CglBnBwdDesc& b) {
+  Launch L;
+  L.kind = K_BNBWD;
+  L.first = (int)c->bnb.size();
+  L.count = 1;
+  L.grid = (b.F + 31) / 32;
+  c->bnb.push_back(b);
+  ph.push_back(L);
+}
+
+void push_adam(cgl_gan* c, std::vector<Launch>& ph, float* p, const float* g, float* m, float* v, long n,
+               const float* ss, const float* bc, int tail) {
+  Launch L;
+  L.kind = K_ADAM;
+  L.adam.p = p;
+  L.adam.g = g;
+  L.adam.m = m;
+  L.adam.v = v;
+  L.adam.n = n;
+  L.adam.step_size = ss;
+  L.adam.bc2sqrt = bc;
+  L.adam.b2 = c->cfg.beta2;
+  L.adam.w1 = (float)(1.0 - (double)c->cfg.beta1);
+  L.adam.w2 = (float)(1.0 - (double)c->cfg.beta2);
+  L.adam.eps = c->cfg.adam_eps;
+  L.tail = tail;
+  L.grid = (int)((n + 255) / 256);
+  ph.push_back(L);
+}
+
+int build_plan(cgl_gan* c) {
+  const cgl_gan_config& cf = c->cfg;
+  const cgl_mlp_spec &g = cf.g, &d = cf.d;
+  const int L = g.n_layers, J = d.n_layers;
+  const int B = cf.batch, Br = cf.batch_real, Md = Br + B;
+  const int img = g.dims[L];
+  WS& w = c->ws;
+  CglStepState* st = w.st;
+  const float sl = cf.slope;
+
+  std::vector<Launch>& A = c->phA;
+  std::vector<Launch>& Bp = c->phB;
+
+  // ---- round prologue
+  {
+    Launch Lb;
+    Lb.kind = K_BEGIN;
+    Lb.begin.st = st;
+    Lb.begin.epoch = cf.epoch;
+    Lb.begin.lr_g = cf.lr_g;
+    Lb.begin.lr_d = cf.lr_d;
+    Lb.begin.b1 = cf.beta1;
+    Lb.begin.b2 = cf.beta2;
+    A.push_back(Lb);
+  }
+  if (cf.gen_z) {
+    Launch Ln;
+    Ln.kind = K_NORMAL;
+    Ln.nptr = c->bufs.z;
+    Ln.nn = (long)2 * B * g.dims[0];
+    Ln.grid = (int)((Ln.nn / 4 + 255) / 256 + 1);
+    A.push_back(Ln);
+  }
+  const int* real_idx = c->bufs.real_idx;
+  if (cf.sample_n > 0) {
+    Launch Ls;
+    Ls.kind = K_SAMPLE;
+    Ls.grid = (cf.epoch * Br + 255) / 256;
+    A.push_back(Ls);
+    real_idx = w.idx;
+  }
+
+  // ---- G forward on [z1; z2] (2B rows; BatchNorm statistics per B-row forward call)
+  int bm_prod[CGL_MAX_LAYERS] = {0};
+  for (int l = 0; l < L; ++l) {
+    const int fi = g.dims[l], fo = g.dims[l + 1];
+    CglGemmDesc e = make_gemm(0, 2 * B, fo, fi);
+    if (l + 1 < L && g.bn[l] && B < 64) choose_tiles(e, 1);  // keep producer tiles <= one call
+    if (l == 0) {
+      e.a = rows(c->bufs.z, fi);
+    } else {
+      e.a = rows(w.gout[l - 1], fi);
+      if (g.bn[l - 1]) {
+        e.a_tf = 1;
+        CglBnFwd& bn = e.bn;
+        bn.part = w.gpart[l - 1];
+        bn.part_bm = bm_prod[l - 1];
+        bn.gr = B;
+        bn.mtot = 2 * B;
+        bn.gamma = gparam(c, l - 1, 2);
+        bn.beta = gparam(c, l - 1, 3);
+        bn.eps = cf.bn_eps;
+        bn.momentum = cf.bn_momentum;
+        bn.slope = sl;
+        bn.run_mean = c->bufs.g_running + c->run_mean_off[l - 1];
+        bn.run_var = c->bufs.g_running + c->run_var_off[l - 1];
+        bn.save_mean = w.gmean[l - 1];
+        bn.save_invstd = w.ginvstd[l - 1];
+        e.a_copy = w.gact[l - 1];
+        e.a_copy_ld = fi;
+        e.a_copy_row0 = B;
+      }
+    }
+    e.a_vec = (fi % 4 == 0) && al16(e.a.p0);
+    e.b = rows(gparam(c, l, 0), fi);
+    e.b_vec = (fi % 4 == 0);
+    e.bias = gparam(c, l, 1);
+    if (l == L - 1) {
+      e.act = CGL_EPI_ACT_TANH;
+    } else if (g.bn[l]) {
+      e.act = CGL_EPI_ACT_NONE;
+      e.stat_part = w.gpart[l];
+      e.stat_gr = B;
+    } else {
+      e.act = CGL_EPI_ACT_LEAKY;
+    }
+    e.slope = sl;
+    e.C = w.gout[l];
+    e.ldc = fo;
+    bm_prod[l] = 32 * e.WM;
+    push_gemm(c, A, {e});
+  }
+  const float* Xd = w.gout[L - 1];
+  const float* Xg = w.gout[L - 1] + (int64_t)B * img;
+
+  // ---- local D steps (Worker.train capgan.py:324-341)
+  const int C = d.dims[J];
+  const float combine = cf.loss == CGL_LOSS_CE2 ? 0.5f : 1.0f;
+  for (int ep = 0; ep < cf.epoch; ++ep) {
+    for (int j = 0; j + 1 < J; ++j) {
+      const int fi = d.dims[j], fo = d.dims[j + 1];
+      CglGemmDesc e = make_gemm(0, Md, fo, fi);
+      if (j == 0) {
+        CglRowSrc r;
+        std::memset(&r, 0, sizeof(r));
+        if (real_idx) {
+          r.p0 = c->bufs.real;
+          r.idx0 = real_idx + (int64_t)ep * Br;
+        } else {
+          r.p0 = c->bufs.real + (int64_t)ep * Br * fi;
+        }
+        r.p1 = Xd;
+        r.split = Br;
+        r.ld = fi;
+        e.a = r;
+        e.a_vec = (fi % 4 == 0) && al16(c->bufs.real) && al16(Xd);
+        e.a_copy = w.R;
+        e.a_copy_ld = fi;
+        e.a_copy_row0 = 0;
+      } else {
+        e.a = rows(w.P[j - 1], fi);
+        e.a_vec = (fi % 4 == 0);
+      }
+      e.b = rows(dparam(c, j, 0), fi);
+      e.b_vec = (fi % 4 == 0);
+      e.bias = dparam(c, j, 1);
+      e.act = CGL_EPI_ACT_LEAKY;
+      e.slope = sl;
+      e.C = w.P[j];
+      e.ldc = fo;
+      push_gemm(c, A, {e});
+    }
+    CglHeadDesc h;
+    std::memset(&h, 0, sizeof(h));
+    h.M = Md;
+    h.F = d.dims[J - 1];
+    h.C = C;
+    h.loss = cf.loss;
+    h.P = w.P[J - 2];
+    h.ldp = d.dims[J - 1];
+    h.W = dparam(c, J - 1, 0);
+    h.b = dparam(c, J - 1, 1);
+    h.split = Br;
+    h.t0 = 1;
+    h.t1 = 0;
+    h.w0 = combine / Br;
+    h.w1 = combine / B;
+    h.dlogits = w.dlog;
+    h.dP = w.dQ[J - 2];
+    h.lddp = d.dims[J - 1];
+    h.slope = sl;
+    h.part = w.hpart;
+    h.counter = w.counters + ep;
+    h.loss_out = &st->d_loss_parts[ep][0];
+    h.combine = combine;
+    h.combine_out = &st->d_loss[ep];
+    h.rows_per_wg = kHeadRows;
+    push_head(c, A, h);
+    // backward: weight grads (TN, + bias column) and input grads (NN, LeakyReLU' mask)
+    for (int j = J - 1; j >= 0; --j) {
+      std::vector<CglGemmDesc> grp;
+      if (j == J - 1) {
+        // grad of the output layer: dlogits^T . P[J-2]
+        CglGemmDesc t = make_gemm(2, C, d.dims[J - 1] + 1, Md);
+        t.a = rows(w.dlog, C);
+        t.b = rows(w.P[J - 2], d.dims[J - 1]);
+        t.b_ones_col = 1;
+        t.C = dgrad(c, J - 1, 0);
+        t.ldc = d.dims[J - 1];
+        t.bias_out = dgrad(c, J - 1, 1);
+        grp.push_back(t);
+        --j;  // the layer below is handled in the same launch
+      }
+      {
+        const float* in = (j >= 1) ? w.P[j - 1] : w.R;
+        CglGemmDesc t = make_gemm(2, d.dims[j + 1], d.dims[j] + 1, Md);
+        t.a = rows(w.dQ[j], d.dims[j + 1]);
+        t.b = rows(in, d.dims[j]);
+        t.b_ones_col = 1;
+        t.C = dgrad(c, j, 0);
+        t.ldc = d.dims[j];
+        t.bias_out = dgrad(c, j, 1);
+        grp.push_back(t);
+      }
+      if (j >= 1) {
+        CglGemmDesc n = make_gemm(1, Md, d.dims[j], d.dims[j + 1]);
+        n.a = rows(w.dQ[j], d.dims[j + 1]);
+        n.a_vec = (d.dims[j + 1] % 4 == 0);
+        n.b = rows(dparam(c, j, 0), d.dims[j]);
+        n.mask_ref = w.P[j - 1];
+        n.mask_ld = d.dims[j];
+        n.slope = sl;
+        n.C = w.dQ[j - 1];
+        n.ldc = d.dims[j];
+        grp.push_back(n);
+      }
+      push_gemm(c, A, grp);
+    }
+    int64_t nd = 0;
+    param_layout(d, &nd);
+    push_adam(c, A, c->bufs.d_params, c->bufs.d_grads, c->bufs.d_m, c->bufs.d_v, (long)nd,
+              &st->d_step_size[ep], &st->d_bc2sqrt[ep], 0);
+  }
+
+  // ---- G loss through the updated D (capgan.py:343-347) and its input gradient
+  for (int j = 0; j + 1 < J; ++j) {
+    const int fi = d.dims[j], fo = d.dims[j + 1];
+    CglGemmDesc e = make_gemm(0, B, fo, fi);
+    e.a = rows(j == 0 ? Xg : w.S[j - 1], fi);
+    e.a_vec = (fi % 4 == 0);
+    e.b = rows(dparam(c, j, 0), fi);
+    e.b_vec = (fi % 4 == 0);
+    e.bias = dparam(c, j, 1);
+    e.act = CGL_EPI_ACT_LEAKY;
+    e.slope = sl;
+    e.C = w.S[j];
+    e.ldc = fo;
+    push_gemm(c, A, {e});
+  }
+  {
+    CglHeadDesc h;
+    std::memset(&h, 0, sizeof(h));
+    h.M = B;
+    h.F = d.dims[J - 1];
+    h.C = C;
+    h.loss = cf.loss;
+    h.P = w.S[J - 2];
+    h.ldp = d.dims[J - 1];
+    h.W = dparam(c, J - 1, 0);
+    h.b = dparam(c, J - 1, 1);
+    h.split = B;
+    h.t0 = 1;
+    h.t1 = 1;
+    h.w0 = 1.0f / B;
+    h.w1 = 1.0f / B;
+    h.dP = w.dS[J - 2];
+    h.lddp = d.dims[J - 1];
+    h.slope = sl;
+    h.part = w.hpart;
+    h.counter = w.counters + CGL_MAX_EPOCH;
+    h.loss_out = &st->g_loss_parts[0];
+    h.combine = 1.0f;
+    h.rows_per_wg = kHeadRows;
+    push_head(c, A, h);
+  }
+  for (int j = J - 2; j >= 0; --j) {
+    // dS[j-1] = (dS[j] V_j) * leaky'(S[j-1]);  j == 0: dXg = dS[0] V_0, then Tanh'
+    CglGemmDesc n = make_gemm(1, B, d.dims[j], d.dims[j + 1]);
+    n.a = rows(w.dS[j], d.dims[j + 1]);
+    n.a_vec = (d.dims[j + 1] % 4 == 0);
+    n.b = rows(dparam(c, j, 0), d.dims[j]);
+    n.slope = sl;
+    if (j >= 1) {
+      n.mask_ref = w.S[j - 1];
+      n.mask_ld = d.dims[j];
+      n.C = w.dS[j - 1];
+      n.ldc = d.dims[j];
+    } else {
+      n.tanh_ref = Xg;
+      n.tanh_ld = img;
+      n.C = w.dYL;
+      n.ldc = img;
+    }
+    push_gemm(c, A, {n});
+  }
+
+  // ---- G backward (Server.train: F_max.backward() capgan.py:258, on the Xg rows)
+  std::vector<Launch>* ph = &A;
+  if (cf.exchange_layer == -1) {
+    c->xchg = w.dYL;
+    c->xchg_n = (int64_t)B * img;
+    ph = &Bp;
+  }
+  auto gbuf = [&](int l) -> float* { return l == L - 1 ? w.dYL : w.gG[l]; };
+  for (int l = L - 1; l >= 0; --l) {
+    std::vector<CglGemmDesc> grp;
+    const int fi = g.dims[l], fo = g.dims[l + 1];
+    {
+      const float* prev;
+      if (l == 0)
+        prev = c->bufs.z + (int64_t)B * fi;
+      else if (g.bn[l - 1])
+        prev = w.gact[l - 1] + (int64_t)B * fi;
+      else
+        prev = w.gout[l - 1] + (int64_t)B * fi;
+      CglGemmDesc t = make_gemm(2, fo, fi + 1, B);
+      t.a = rows(gbuf(l), fo);
+      t.b = rows(prev, fi);
+      t.b_ones_col = 1;
+      t.C = ggrad(c, l, 0);
+      t.ldc = fi;
+      t.bias_out = ggrad(c, l, 1);
+      grp.push_back(t);
+    }
+    if (l >= 1) {
+      CglGemmDesc n = make_gemm(1, B, fi, fo);
+      n.a = rows(gbuf(l), fo);
+      n.a_vec = (fo % 4 == 0);
+      n.b = rows(gparam(c, l, 0), fi);
+      n.slope = sl;
+      n.ldc = fi;
+      if (g.bn[l - 1]) {
+        n.C = w.gdA[l - 1];
+      } else {
+        n.mask_ref = w.gout[l - 1] + (int64_t)B * fi;
+        n.mask_ld = fi;
+        n.C = w.gG[l - 1];
+      }
+      grp.push_back(n);
+    }
+    push_gemm(c, *ph, grp);
+    if (l >= 1 && cf.exchange_layer == l) {
+      c->xchg = g.bn[l - 1] ? w.gdA[l - 1] : w.gG[l - 1];
+      c->xchg_n = (int64_t)B * fi;
+      ph = &Bp;
+    }
+    if (l >= 1 && g.bn[l - 1]) {
+      CglBnBwdDesc b;
+      std::memset(&b, 0, sizeof(b));
+      b.M = B;
+      b.F = fi;
+      b.dA = w.gdA[l - 1];
+      b.ld_da = fi;
+      b.post = w.gact[l - 1] + (int64_t)B * fi;
+      b.ld_post = fi;
+      b.Y = w.gout[l - 1] + (int64_t)B * fi;
+      b.ld_y = fi;
+      b.mean = w.gmean[l - 1] + fi;        // group 1 = the Xg forward call
+      b.invstd = w.ginvstd[l - 1] + fi;
+      b.gamma = gparam(c, l - 1, 2);
+      b.dZ = w.gG[l - 1];
+      b.ld_dz = fi;
+      b.g_gamma = ggrad(c, l - 1, 2);
+      b.g_beta = ggrad(c, l - 1, 3);
+      b.slope = sl;
+      push_bnb(c, *ph, b);
+    }
+  }
+  int64_t ng = 0;
+  param_layout(g, &ng);
+  push_adam(c, *ph, c->bufs.g_params, c->bufs.g_grads, c->bufs.g_m, c->bufs.g_v, (long)ng, &st->g_step_size,
+            &st->g_bc2sqrt, 1);
+  if ((int)c->gemm.size() > kMaxGemmDescs || (int)c->head.size() > kMaxHeadDescs ||
+      (int)c->bnb.size() > kMaxBnDescs)
+    return CGL_E_SIZE;
+  return CGL_OK;
+}
+
+// Shuffle sampler: keyed Feistel permutation of [0, n) per data epoch (cycle walking).
+__device__ __forceinline__ uint32_t cgl_hash(uint32_t x, uint32_t k) {
+  x ^= k;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ uint32_t cgl_permute(uint32_t i, uint32_t n, uint32_t key) {
+  int bits = 2;
+  while ((1u << bits) < n) ++bits;
+  if (bits & 1) ++bits;
+  const int hb = bits / 2;
+  const uint32_t mask = (1u << hb) - 1;
+  uint32_t x = i;
+  do {
+    uint32_t l = x >> hb, r = x & mask;
+    for (int round = 0; round < 4; ++round) {
+      const uint32_t t = l ^ (cgl_hash(r, key + 0x9e3779b9u * (round + 1)) & mask);
+      l = r;
+      r = t;
+    }
+    x = (l << hb) | r;
+  } while (x >= n);
+  return x;
+}
+
+__global__ void cgl_sample(int* idx, const CglStepState* st, int epoch, int br, int n, unsigned long long seed) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= epoch * br) return;
+  const long pos = ((long)(st->round - 1) * epoch) * br + t;
+  const uint32_t ep = (uint32_t)(pos / n), j = (uint32_t)(pos % n);
+  idx[t] = (int)cgl_permute(j, (uint32_t)n, (uint32_t)seed ^ (ep * 0x85ebca6bu + 0x1234567u));
+}
+
+int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s) {
+  switch (L.kind) {
+    case K_GEMM:
+      hipLaunchKernelGGL(cgl_gemm_f32, dim3(L.grid), dim3(CGL_GEMM_THREADS), 0, s, c->ws.gemm + L.first, L.count);
+      break;
+    case K_HEAD:
+      hipLaunchKernelGGL(cgl_head_loss, dim3(L.grid), dim3(256), 0, s, c->ws.head + L.first);
+      break;
+    case K_BNBWD:
+      hipLaunchKernelGGL(cgl_bn_bwd, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
+      break;
+    case K_ADAM:
+      hipLaunchKernelGGL(cgl_adam, dim3(L.grid), dim3(256), 0, s, L.adam, c->ws.st, L.tail);
+      break;
+    case K_BEGIN:
+      hipLaunchKernelGGL(cgl_step_begin, dim3(1), dim3(64), 0, s, L.begin);
+      break;
+    case K_NORMAL:
+      hipLaunchKernelGGL(cgl_normal, dim3(L.grid), dim3(256), 0, s, L.nptr, L.nn, c->cfg.seed, c->ws.st, 0);
+      break;
+    case K_SAMPLE:
+      hipLaunchKernelGGL(cgl_sample, dim3(L.grid), dim3(256), 0, s, c->ws.idx, c->ws.st, c->cfg.epoch,
+                         c->cfg.batch_real, c->cfg.sample_n, c->cfg.seed ^ 0x5bd1e995ULL);
+      break;
+    default:
+      return CGL_E_STATE;
+  }
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+int run_phase(cgl_gan* c, int phase, hipStream_t s) {
+  if (phase == CGL_PHASE_ALL || phase == CGL_PHASE_A)
+    for (auto& L : c->phA) {
+      const int e = exec_launch(c, L, s);
+      if (e) return e;
+    }
+  if (phase == CGL_PHASE_ALL || phase == CGL_PHASE_B)
+    for (auto& L : c->phB) {
+      const int e = exec_launch(c, L, s);
+      if (e) return e;
+    }
+  return 0;
+}
+
+#define HIPCHK(x)                          \
+  do {                                     \
+    const hipError_t _e = (x);             \
+    if (_e != hipSuccess) return (int)_e;  \
+  } while (0)
+
+}  // namespace
+
+// ==========================================================================================
+extern "C" {
+
+const char* cgl_version(void) { return CGL_VERSION_STR; }
+
+int64_t cgl_gan_param_count(const cgl_gan_config* cfg, int model) {
+  if (!cfg || (model != CGL_MODEL_G && model != CGL_MODEL_D)) return CGL_E_ARG;
+  int64_t n = 0;
+  param_layout(model == CGL_MODEL_G ? cfg->g : cfg->d, &n);
+  return n;
+}
+
+int cgl_gan_param_tensor(const cgl_gan_config* cfg, int model, int idx, int64_t* offset, int* rows_, int* cols,
+                         int* layer, int* kind) {
+  if (!cfg || (model != CGL_MODEL_G && model != CGL_MODEL_D)) return CGL_E_ARG;
+  auto v = param_layout(model == CGL_MODEL_G ? cfg->g : cfg->d, nullptr);
+  if (idx < 0 || idx >= (int)v.size()) return CGL_E_ARG;
+  if (offset) *offset = v[idx].off;
+  if (rows_) *rows_ = v[idx].rows;
+  if (cols) *cols = v[idx].cols;
+  if (layer) *layer = v[idx].layer;
+  if (kind) *kind = v[idx].kind;
+  return CGL_OK;
+}
+
+int64_t cgl_gan_running_count(const cgl_gan_config* cfg) {
+  if (!cfg) return CGL_E_ARG;
+  return running_layout(cfg->g, nullptr, nullptr);
+}
+
+int64_t cgl_gan_workspace_bytes(const cgl_gan_config* cfg) {
+  const int v = validate(cfg);
+  if (v) return v;
+  return carve_ws(*cfg, nullptr).total;
+}
+
+int cgl_gan_create(const cgl_gan_config* cfg, const cgl_gan_buffers* bufs, cgl_gan** out) {
+  if (!out || !bufs) return CGL_E_ARG;
+  *out = nullptr;
+  const int v = validate(cfg);
+  if (v) return v;
+  if (!bufs->g_params || !bufs->g_grads || !bufs->g_m || !bufs->g_v || !bufs->d_params || !bufs->d_grads ||
+      !bufs->d_m || !bufs->d_v || !bufs->z || !bufs->real || !bufs->workspace)
+    return CGL_E_ARG;
+  int has_bn = 0;
+  for (int l = 0; l < cfg->g.n_layers; ++l) has_bn |= cfg->g.bn[l];
+  if (has_bn && !bufs->g_running) return CGL_E_ARG;
+  if (cfg->n_workers > 1 && !bufs->losses_all) return CGL_E_ARG;
+  const int64_t need = carve_ws(*cfg, nullptr).total;
+  if (bufs->workspace_bytes < need) return CGL_E_SIZE;
+  if (!al16(bufs->g_params) || !al16(bufs->d_params) || !al16(bufs->z) || !al16(bufs->workspace))
+    return CGL_E_ARG;
+
+  cgl_gan* c = new cgl_gan();
+  c->cfg = *cfg;
+  c->bufs = *bufs;
+  c->ws = carve_ws(*cfg, bufs->workspace);
+  c->gl = param_layout(cfg->g, nullptr);
+  c->dl = param_layout(cfg->d, nullptr);
+  running_layout(cfg->g, c->run_mean_off, c->run_var_off);
+  int e = build_plan(c);
+  if (e) {
+    delete c;
+    return e;
+  }
+  // upload descriptors, zero counters / state
+  hipError_t he = hipMemcpy(c->ws.gemm, c->gemm.data(), c->gemm.size() * sizeof(CglGemmDesc), hipMemcpyHostToDevice);
+  if (he == hipSuccess && !c->head.empty())
+    he = hipMemcpy(c->ws.head, c->head.data(), c->head.size() * sizeof(CglHeadDesc), hipMemcpyHostToDevice);
+  if (he == hipSuccess && !c->bnb.empty())
+    he = hipMemcpy(c->ws.bnb, c->bnb.data(), c->bnb.size() * sizeof(CglBnBwdDesc), hipMemcpyHostToDevice);
+  if (he == hipSuccess) he = hipMemset(c->ws.counters, 0, 64 * sizeof(unsigned int));
+  if (he == hipSuccess) he = hipMemset(c->ws.st, 0, sizeof(CglStepState));
+  if (he == hipSuccess) he = hipDeviceSynchronize();
+  if (he != hipSuccess) {
+    delete c;
+    return (int)he;
+  }
+  *out = c;
+  return CGL_OK;
+}
+
+int cgl_gan_destroy(cgl_gan* c) {
+  if (!c) return CGL_E_ARG;
+  for (auto& g : c->gexec)
+    if (g) (void)hipGraphExecDestroy(g);
+  delete c;
+  return CGL_OK;
+}
+
+int cgl_gan_reset(cgl_gan* c, const float* beta_host, void* stream) {
+  if (!c) return CGL_E_ARG;
+  CglStepState h;
+  std::memset(&h, 0, sizeof(h));
+  h.n_workers = c->cfg.n_workers;
+  h.rank = c->cfg.rank;
+  h.weighting = c->cfg.weighting;
+  h.alpha = 1.f;
+  for (int i = 0; i < c->cfg.n_workers; ++i) h.beta[i] = beta_host ? beta_host[i] : 1.f / c->cfg.n_workers;
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipMemcpyAsync(c->ws.st, &h, sizeof(h), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(c->ws.counters, 0, 64 * sizeof(unsigned int), s));
+  HIPCHK(hipStreamSynchronize(s));
+  return CGL_OK;
+}
+
+int cgl_gan_run(cgl_gan* c, int phase, void* stream) {
+  if (!c || phase < 0 || phase > 2) return CGL_E_ARG;
+  return run_phase(c, phase, (hipStream_t)stream);
+}
+
+int cgl_gan_run_graph(cgl_gan* c, int phase, void* stream) {
+  if (!c || phase < 0 || phase > 2) return CGL_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (!c->gexec[phase]) {
+    hipGraph_t graph;
+    HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    const int e = run_phase(c, phase, s);
+    hipGraph_t g2;
+    const hipError_t ec = hipStreamEndCapture(s, &g2);
+    if (e) return e;
+    HIPCHK(ec);
+    graph = g2;
+    hipGraphExec_t ex;
+    HIPCHK(hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0));
+    (void)hipGraphDestroy(graph);
+    c->gexec[phase] = ex;
+  }
+  HIPCHK(hipGraphLaunch(c->gexec[phase], s));
+  return CGL_OK;
+}
+
+int cgl_gan_alpha_scale(cgl_gan* c, void* stream) {
+  if (!c || !c->xchg) return CGL_E_STATE;
+  const long n = (long)c->xchg_n;
+  const int grid = (int)std::min<long>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(cgl_alpha_scale, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->ws.st,
+                     c->bufs.losses_all, c->xchg, n);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+int cgl_gan_exchange_buffer(cgl_gan* c, float** ptr, int64_t* n) {
+  if (!c || !ptr || !n) return CGL_E_ARG;
+  *ptr = c->xchg;
+  *n = c->xchg_n;
+  return CGL_OK;
+}
+
+int cgl_gan_tensor(cgl_gan* c, int which, float** ptr, int64_t* n) {
+  if (!c || !ptr || !n) return CGL_E_ARG;
+  const int L = c->cfg.g.n_layers;
+  if (which == 0) {
+    *ptr = c->ws.gout[L - 1];
+    *n = (int64_t)2 * c->cfg.batch * c->cfg.g.dims[L];
+  } else if (which == 1) {
+    *ptr = &c->ws.st->g_loss_parts[0];
+    *n = 1;
+  } else {
+    return CGL_E_ARG;
+  }
+  return CGL_OK;
+}
+
+int cgl_gan_read_stats(cgl_gan* c, cgl_gan_stats* out, void* stream) {
+  if (!c || !out) return CGL_E_ARG;
+  CglStepState h;
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipMemcpyAsync(&h, c->ws.st, sizeof(h), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  std::memset(out, 0, sizeof(*out));
+  out->round = h.round;
+  for (int e = 0; e < CGL_MAX_EPOCH; ++e) {
+    out->d_loss[e] = h.d_loss[e];
+    out->d_real[e] = h.d_loss_parts[e][0];
+    out->d_fake[e] = h.d_loss_parts[e][1];
+  }
+  out->g_loss = h.g_loss_parts[0];
+  out->alpha = h.alpha;
+  out->F = h.F;
+  out->lambda_ = h.lambda;
+  out->bn_batches = h.bn_batches;
+  return CGL_OK;
+}
+
+int cgl_gan_plan_info(cgl_gan* c, int phase, int* n_launches, int* n_gemm, double* flops) {
+  if (!c) return CGL_E_ARG;
+  int nl = 0, ngm = 0;
+  double f = 0;
+  auto acc = [&](const std::vector<Launch>& v) {
+    for (auto& L : v) {
+      ++nl;
+      if (L.kind == K_GEMM) {
+        ++ngm;
+        f += L.flops;
+      }
+    }
+  };
+  if (phase == CGL_PHASE_ALL || phase == CGL_PHASE_A) acc(c->phA);
+  if (phase == CGL_PHASE_ALL || phase == CGL_PHASE_B) acc(c->phB);
+  if (n_launches) *n_launches = nl;
+  if (n_gemm) *n_gemm = ngm;
+  if (flops) *flops = f;
+  return CGL_OK;
+}
+
+// ---------------- single ops -------------------------------------------------------------
+int64_t cgl_op_workspace_bytes(void) { return 4096; }
+
+static int single_gemm(CglGemmDesc& d, void* ws, int64_t wsb, hipStream_t s) {
+  if (!ws || wsb < (int64_t)sizeof(CglGemmDesc) || !al16(ws)) return CGL_E_ARG;
+  d.wg_begin = 0;
+  HIPCHK(hipMemcpyAsync(ws, &d, sizeof(d), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(cgl_gemm_f32, dim3(d.tiles_m * d.tiles_n), dim3(CGL_GEMM_THREADS), 0, s,
+                     (const CglGemmDesc*)ws, 1);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  // the descriptor lives in the caller's workspace: keep it alive until the kernel has read it
+  HIPCHK(hipStreamSynchronize(s));
+  return 0;
+}
+
+int cgl_linear_fwd(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, int act,
+                   float slope, void* ws, int64_t wsb, void* stream) {
+  if (!X || !W || !Y || M < 1 || N < 1 || K < 1 || act < 0 || act > 2) return CGL_E_ARG;
+  CglGemmDesc d = make_gemm(0, M, N, K);
+  d.a = rows(X, K);
+  d.a_vec = (K % 4 == 0) && al16(X);
+  d.b = rows(W, K);
+  d.b_vec = (K % 4 == 0) && al16(W);
+  d.bias = b;
+  d.act = act;
+  d.slope = slope;
+  d.C = Y;
+  d.ldc = N;
+  return single_gemm(d, ws, wsb, (hipStream_t)stream);
+}
+
+int cgl_linear_bwd_data(const float* dY, const float* W, float* dX, int M, int N, int K, void* ws, int64_t wsb,
+                        void* stream) {
+  if (!dY || !W || !dX || M < 1 || N < 1 || K < 1) return CGL_E_ARG;
+  CglGemmDesc d = make_gemm(1, M, K, N);
+  d.a = rows(dY, N);
+  d.a_vec = (N % 4 == 0) && al16(dY);
+  d.b = rows(W, K);
+  d.C = dX;
+  d.ldc = K;
+  return single_gemm(d, ws, wsb, (hipStream_t)stream);
+}
+
+int cgl_linear_bwd_weight(const float* dY, const float* X, float* dW, float* db, int M, int N, int K, void* ws,
+                          int64_t wsb, void* stream) {
+  if (!dY || !X || !dW || M < 1 || N < 1 || K < 1) return CGL_E_ARG;
+  CglGemmDesc d = make_gemm(2, N, K + (db ? 1 : 0), M);
+  d.a = rows(dY, N);
+  d.b = rows(X, K);
+  d.b_ones_col = db ? 1 : 0;
+  d.C = dW;
+  d.ldc = K;
+  d.bias_out = db;
+  return single_gemm(d, ws, wsb, (hipStream_t)stream);
+}
+
+int cgl_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int step, float lr, float beta1,
+                  float beta2, float eps, void* ws, int64_t wsb, void* stream) {
+  if (!p || !g || !m || !v || n < 0 || step < 1 || !ws || wsb < 8) return CGL_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  float sc[2];
+  const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+  sc[0] = (float)((double)lr / bc1);
+  sc[1] = (float)std::pow(bc2, 0.5);
+  HIPCHK(hipMemcpyAsync(ws, sc, sizeof(sc), hipMemcpyHostToDevice, s));
+  CglAdamArgs a;
+  a.p = p;
+  a.g = g;
+  a.m = m;
+  a.v = v;
+  a.n = (long)n;
+  a.step_size = (const float*)ws;
+  a.bc2sqrt = (const float*)ws + 1;
+  a.b2 = beta2;
+  a.w1 = (float)(1.0 - (double)beta1);
+  a.w2 = (float)(1.0 - (double)beta2);
+  a.eps = eps;
+  if (n > 0)
+    hipLaunchKernelGGL(cgl_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, (CglStepState*)nullptr, 0);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  HIPCHK(hipStreamSynchronize(s));
+  return 0;
+}
+
+int cgl_normal_fill(float* out, int64_t n, unsigned long long seed, int round, int stream_id, void* stream) {
+  if (!out || n < 0) return CGL_E_ARG;
+  (void)round;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(cgl_normal, dim3((unsigned)((n / 4 + 255) / 256 + 1)), dim3(256), 0, (hipStream_t)stream, out,
+                     (long)n, seed, (const CglStepState*)nullptr, stream_id);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+}  // extern "C"

@@ -1,0 +1,160 @@
+/* libcglgan_hip -- MI355X-native CGL-GAN worker step, C ABI.
+ *
+ * The reference (NetworkCommunication/CGL-GAN) has no native code and no FFI: its hot path
+ * is the per-worker GAN training step that the Python drivers run through PyTorch ops.
+ * Each entry point below replaces one piece of that path; the reference interface it
+ * stands in for is cited per function (paths relative to the reference repository root).
+ * The Python binding that calls this ABI is cgl-gan_amd/cglgan/_lib.py (ctypes); see
+ * INTEGRATION.md for how a reference driver binds it.
+ *
+ * Conventions: all pointers are device pointers unless stated; `stream` is a hipStream_t
+ * passed as void*; every function returns 0 on success, a positive hipError_t value on a
+ * HIP failure, or a negative CGL_E* code on an argument error.  The library never
+ * allocates device memory: the caller provides every buffer (sizes from the *_count /
+ * *_bytes queries) and keeps ownership.
+ */
+#ifndef CGLGAN_H
+#define CGLGAN_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CGL_MAX_LAYERS 8
+
+enum {
+  CGL_OK = 0,
+  CGL_E_ARG = -1,        /* invalid argument / unsupported shape */
+  CGL_E_STATE = -2,      /* call out of order (e.g. graph before create) */
+  CGL_E_SIZE = -3        /* a caller buffer is too small */
+};
+
+enum { CGL_LOSS_CE2 = 0, CGL_LOSS_BCE = 1 };
+enum {
+  CGL_WEIGHT_CAPGAN = 0,      /* alpha = softmax(beta * softmax(lambda * l))   capgan.py:247-248        */
+  CGL_WEIGHT_MEAN = 1,        /* alpha = 1/N                                   MDGAN/MNIST/mdgan.py:203 */
+  CGL_WEIGHT_MIX_SINGLE = 2,  /* alpha = softmax(beta * lambda * l)            mixed-gan.py:276         */
+  CGL_WEIGHT_MIX_DOUBLE = 3,  /* alpha = softmax(beta * softmax(lambda * l))   CAPGAN/MNIST/mixed-gan.py:276-278 */
+  CGL_WEIGHT_CGLGAN = 4       /* alpha = (beta + softmax(lambda * l)) / 2      CGLGAN/2DMG/main.py:261-264 */
+};
+enum { CGL_PHASE_ALL = 0, CGL_PHASE_A = 1, CGL_PHASE_B = 2 };
+enum { CGL_MODEL_G = 0, CGL_MODEL_D = 1 };
+
+/* One MLP: n_layers Linear layers, dims[0] -> ... -> dims[n_layers].
+ * Hidden layers are Linear -> [BatchNorm1d(eps, momentum) if bn[l]] -> LeakyReLU(slope)
+ * (block() of model/mnist_model.py:10-15).  G's last layer is followed by Tanh
+ * (model/mnist_model.py:22-23); D's last layer gives 2 logits (CE, :81) or one Sigmoid unit (BCE,
+ * MDGAN/MNIST/mnist_model.py:41-42, CGLGAN/2DMG/model.py:63-64). */
+typedef struct cgl_mlp_spec {
+  int n_layers;
+  int dims[CGL_MAX_LAYERS + 1];
+  int bn[CGL_MAX_LAYERS];
+} cgl_mlp_spec;
+
+typedef struct cgl_gan_config {
+  cgl_mlp_spec g, d;
+  int batch;            /* B: generated rows per forward call (batch_size, capgan.py:48)          */
+  int batch_real;       /* real rows per local D step                                            */
+  int epoch;            /* local D steps per round (epoch, capgan.py:50), <= 8                  */
+  int loss;             /* CGL_LOSS_*                                                            */
+  int weighting;        /* CGL_WEIGHT_*                                                          */
+  int n_workers, rank;  /* exchange group of this G replica (1: no exchange)                     */
+  int exchange_layer;   /* -1: exchange the G-output gradient (CAPGAN / MDGAN);
+                           k > 0: exchange the gradient of G layer k's input (Mix-G trunk/head
+                           split: layers >= k are this worker's head, mixed-gan.py:263-281)     */
+  float lr_g, lr_d, beta1, beta2, adam_eps;   /* 2e-4, 2e-4, 0.5, 0.999, 1e-8 (capgan.py:52-53,122) */
+  float bn_eps, bn_momentum, slope;           /* 0.8, 0.1, 0.2 (model/mnist_model.py:13-14)     */
+  unsigned long long seed;                    /* z RNG seed; identical across a server group     */
+  int gen_z;            /* 1: the step draws z on device (Philox) each round; 0: caller fills z   */
+  int sample_n;         /* >0: in-graph shuffle sampler over sample_n real rows (per-epoch keyed
+                           permutation, DataLoader(shuffle=True) capgan.py:282,326-330); 0: the
+                           caller provides the round's real rows / indices                      */
+} cgl_gan_config;
+
+typedef struct cgl_gan_buffers {
+  float* g_params; float* g_grads; float* g_m; float* g_v;  /* flat, cgl_gan_param_count(G)      */
+  float* g_running;     /* BatchNorm running_mean/running_var, cgl_gan_running_count()            */
+  float* d_params; float* d_grads; float* d_m; float* d_v;  /* flat, cgl_gan_param_count(D)      */
+  float* z;             /* [2*batch][g.dims[0]]: z1 (no-grad Xd call) then z2 (Xg call)           */
+  const float* real;    /* real rows, row stride g.dims[n_layers]                                 */
+  int* real_idx;        /* [epoch*batch_real] gather indices into `real`, or NULL: rows in order  */
+  float* losses_all;    /* [n_workers] gathered G losses (exchange), may be NULL when n_workers=1 */
+  void* workspace;  int64_t workspace_bytes;   /* cgl_gan_workspace_bytes()                      */
+} cgl_gan_buffers;
+
+typedef struct cgl_gan cgl_gan;
+
+/* Host-side scalars of the last round (cgl_gan_read_stats). */
+typedef struct cgl_gan_stats {
+  int round;
+  float d_loss[8];      /* D_loss of each local step  (capgan.py:339)                             */
+  float d_real[8], d_fake[8];
+  float g_loss;         /* this worker's G loss      (capgan.py:346)                             */
+  float alpha;          /* weight of this worker's G-loss gradient                               */
+  float F;              /* F_max                     (capgan.py:249)                             */
+  float lambda_;        /* Lambda after the round    (capgan.py:259)                             */
+  long long bn_batches; /* num_batches_tracked of G's BatchNorm layers                          */
+} cgl_gan_stats;
+
+/* ---------------- layout / sizing queries (host only, no device access) ---------------- */
+/* Number of floats of the flat parameter buffer of G or D (each tensor 256-byte aligned). */
+int64_t cgl_gan_param_count(const cgl_gan_config* cfg, int model);
+/* Tensor `idx` (reference state-dict order: Linear weight, bias, then BN weight, bias per layer)
+ * of G or D: offset in floats and shape.  Returns 0, or CGL_E_ARG past the last tensor. */
+int cgl_gan_param_tensor(const cgl_gan_config* cfg, int model, int idx, int64_t* offset, int* rows, int* cols,
+                         int* layer, int* kind /* 0 W, 1 b, 2 BN gamma, 3 BN beta */);
+int64_t cgl_gan_running_count(const cgl_gan_config* cfg);
+int64_t cgl_gan_workspace_bytes(const cgl_gan_config* cfg);
+
+/* ---------------- fused worker step (replaces Server.train + Worker.train) ---------------- */
+/* Validates cfg, plans every launch of a round and writes the launch descriptors into the
+ * workspace (capgan.py:211-262 + :316-349, mixed-gan.py:238-292 + :355-392,
+ * MDGAN/MNIST/mdgan.py:180-207 + :266-297, CGLGAN/2DMG/main.py:225-278 + :344-375). */
+int cgl_gan_create(const cgl_gan_config* cfg, const cgl_gan_buffers* bufs, cgl_gan** out);
+int cgl_gan_destroy(cgl_gan* ctx);
+/* Zero the round counters / lambda, set the data-size weights beta[n_workers]
+ * (capgan.py:149-153) -- host array. */
+int cgl_gan_reset(cgl_gan* ctx, const float* beta_host, void* stream);
+/* Run one round (CGL_PHASE_ALL) or its halves around the exchange: phase A ends with this
+ * worker's (unscaled) exchange gradient and G loss; phase B consumes the all-reduced one. */
+int cgl_gan_run(cgl_gan* ctx, int phase, void* stream);
+/* Same, through a captured hipGraph (captured on first use, replayed after). */
+int cgl_gan_run_graph(cgl_gan* ctx, int phase, void* stream);
+/* Exchange step: alpha from losses_all (already gathered), then scale this worker's exchange
+ * gradient by alpha[rank] in place, ready for an all-reduce(sum). */
+int cgl_gan_alpha_scale(cgl_gan* ctx, void* stream);
+/* The exchange gradient buffer (device pointer, float count). */
+int cgl_gan_exchange_buffer(cgl_gan* ctx, float** ptr, int64_t* n);
+/* Device pointer of an internal activation: 0 = G output [2B][img] (Xd rows then Xg rows),
+ * 1 = own G-loss scalar. */
+int cgl_gan_tensor(cgl_gan* ctx, int which, float** ptr, int64_t* n);
+/* Synchronous copy of the round scalars to the host. */
+int cgl_gan_read_stats(cgl_gan* ctx, cgl_gan_stats* out, void* stream);
+/* Launch / kernel counts of a phase (for roofline bookkeeping). */
+int cgl_gan_plan_info(cgl_gan* ctx, int phase, int* n_launches, int* n_gemm_launches, double* gemm_flops);
+
+/* ---------------- single ops (nn.Module boundary: model/mnist_model.py) ---------------- */
+/* Y[M,N] = act(X[M,K] W[N,K]^T + b)   act: 0 none, 1 LeakyReLU(slope), 2 Tanh  (nn.Linear fwd) */
+int cgl_linear_fwd(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, int act,
+                   float slope, void* workspace, int64_t ws_bytes, void* stream);
+/* dX[M,K] = dY[M,N] W[N,K]   (nn.Linear backward, input grad) */
+int cgl_linear_bwd_data(const float* dY, const float* W, float* dX, int M, int N, int K, void* workspace,
+                        int64_t ws_bytes, void* stream);
+/* dW[N,K] = dY^T X, db[N] = sum_rows dY   (nn.Linear backward, weight/bias grad) */
+int cgl_linear_bwd_weight(const float* dY, const float* X, float* dW, float* db, int M, int N, int K,
+                          void* workspace, int64_t ws_bytes, void* stream);
+/* Flat Adam step t (optim.Adam, torch _single_tensor_adam op order) */
+int cgl_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int step, float lr, float beta1,
+                  float beta2, float eps, void* workspace, int64_t ws_bytes, void* stream);
+/* N(0,1) fill (Philox4x32-10 + Box-Muller); counter = (index, round, stream_id) */
+int cgl_normal_fill(float* out, int64_t n, unsigned long long seed, int round, int stream_id, void* stream);
+int64_t cgl_op_workspace_bytes(void);
+
+/* Library identification: "<version> gfx950" */
+const char* cgl_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CGLGAN_H */

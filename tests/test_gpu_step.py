@@ -1,0 +1,115 @@
+"""HIP worker round vs the CPU oracle (which is pinned bitwise to the reference's own modules).
+
+Tolerances (written here): one round from identical state <= 1e-5 relative on the
+losses, the G gradients and the updated parameters; a free-running 10-round trajectory
+<= 1e-4 relative on the losses.
+"""
+import pytest
+import torch
+
+from parity_helpers import STEP_TOL, TRAJ_TOL, feed, inputs, make_pair, oracle_round, rel, rel_scalar
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _threads():
+    n = torch.get_num_threads()
+    torch.set_num_threads(1)
+    yield
+    torch.set_num_threads(n)
+
+
+def _one_round(kind, B, Br=None, epoch=1, graph=False):
+    Br = Br or B
+    srv, workers, step = make_pair(kind, B, Br, epoch)
+    z1, z2, reals = inputs(kind, B, Br, epoch, seed=7)
+    feed(step, z1, z2, reals)
+    step.run(graph=graph)
+    torch.cuda.synchronize()
+    r = oracle_round(kind, srv, workers, z1, z2, reals)
+    return srv, workers, step, r
+
+
+@pytest.mark.parametrize("kind,B,Br,epoch", [
+    ("capgan", 64, 64, 1), ("capgan", 256, 256, 1), ("capgan", 100, 100, 1), ("capgan", 64, 40, 2),
+    ("mdgan", 64, 64, 1), ("ring", 64, 64, 1), ("mixg1", 64, 64, 1)])
+def test_single_round_parity(kind, B, Br, epoch):
+    srv, workers, step, r = _one_round(kind, B, Br, epoch)
+    st = step.stats()
+    assert st["round"] == 1
+    # G output of the round (Xd rows then Xg rows)
+    out = step.g_output().cpu()
+    assert rel(out[:B], r["Xd"].reshape(B, -1)) <= STEP_TOL
+    assert rel(out[B:], r["Xg"].reshape(B, -1)) <= STEP_TOL
+    # losses
+    for e in range(epoch):
+        assert rel_scalar(st["d_loss"][e], r["d_losses"][e]) <= STEP_TOL, (e, st["d_loss"], r["d_losses"])
+    assert rel_scalar(st["g_loss"], r["g_losses"][0]) <= STEP_TOL
+    assert rel_scalar(st["F"], r["F"]) <= STEP_TOL
+    # G gradients of the round and updated parameters
+    G = srv.G
+    gp = dict(G.trunk.params) if hasattr(G, "trunk") else dict(G.params)
+    if hasattr(G, "heads"):
+        for h in G.heads:
+            gp.update(h.params)
+    for k, v in step.g_grad_views.items():
+        assert rel(v, gp[k].grad) <= STEP_TOL, k
+    for k, v in step.g_views.items():
+        assert rel(v, gp[k].detach()) <= STEP_TOL, k
+    for k, v in step.d_views.items():
+        assert rel(v, workers[0].D.params[k].detach()) <= STEP_TOL, k
+    # BatchNorm running statistics (two train-mode forward calls per round)
+    sd = G.state_dict()
+    for k, v in step.running.items():
+        assert rel(v, sd[k]) <= STEP_TOL, k
+    gsd = step.g_state_dict()
+    for k in sd:
+        if k.endswith("num_batches_tracked"):
+            assert int(gsd[k]) == int(sd[k]), k
+
+
+@pytest.mark.parametrize("kind,B", [("capgan", 64), ("capgan", 256), ("mdgan", 64), ("ring", 64)])
+def test_trajectory_10_rounds(kind, B):
+    srv, workers, step = make_pair(kind, B)
+    for t in range(10):
+        z1, z2, reals = inputs(kind, B, B, 1, seed=100 + t)
+        feed(step, z1, z2, reals)
+        step.run(graph=(t % 2 == 1))
+        st = step.stats()
+        r = oracle_round(kind, srv, workers, z1, z2, reals)
+        assert rel_scalar(st["d_loss"][0], r["d_losses"][0]) <= TRAJ_TOL, (t, st, r["d_losses"])
+        assert rel_scalar(st["g_loss"], r["g_losses"][0]) <= TRAJ_TOL, (t, st, r["g_losses"])
+        assert abs(st["lambda"] - float(r["lam"])) <= 1e-6 + TRAJ_TOL * abs(float(r["lam"]))
+
+
+def test_graph_replay_equals_eager():
+    """The hipGraph replay runs exactly the eager launch list: bitwise identical rounds."""
+    _, _, s1 = make_pair("capgan", 256)
+    _, _, s2 = make_pair("capgan", 256)
+    for t in range(3):
+        z1, z2, reals = inputs("capgan", 256, 256, 1, seed=300 + t)
+        feed(s1, z1, z2, reals)
+        feed(s2, z1, z2, reals)
+        s1.run(graph=False)
+        s2.run(graph=True)
+    torch.cuda.synchronize()
+    assert torch.equal(s1.g_params, s2.g_params)
+    assert torch.equal(s1.d_params, s2.d_params)
+    assert s1.stats()["d_loss"] == s2.stats()["d_loss"]
+
+
+def test_deterministic_replicas():
+    """Fixed-order reductions only: two replicas fed the same inputs stay bitwise identical
+    (the property that keeps replicated G identical across GPUs without a broadcast)."""
+    _, _, s1 = make_pair("capgan", 128)
+    _, _, s2 = make_pair("capgan", 128)
+    for t in range(3):
+        z1, z2, reals = inputs("capgan", 128, 128, 1, seed=500 + t)
+        feed(s1, z1, z2, reals)
+        feed(s2, z1, z2, reals)
+        s1.run(graph=True)
+        s2.run(graph=True)
+    torch.cuda.synchronize()
+    assert torch.equal(s1.g_params, s2.g_params)
+    assert torch.equal(s1.running["model.3.running_mean"], s2.running["model.3.running_mean"])

@@ -1,0 +1,134 @@
+"""The C-ABI library loads on CPU and exports every symbol include/cglgan.h declares.
+
+Only host-side (no-device) entry points are called here: layout / sizing queries and config
+validation.  Compute calls need a GPU and live in the ``-m gpu`` tests.
+"""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from cglgan import _lib as C
+from cglgan import specs
+from cglgan.step import _spec
+from oracle import gan_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "cglgan.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(cgl_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_symbols_exported():
+    decl = declared_symbols()
+    assert decl, "no declarations parsed"
+    assert sorted(C.EXPORTS) == decl
+    for name in decl:
+        assert hasattr(C.lib, name), name
+    assert C.version().endswith("gfx950")
+
+
+def test_nm_exports():
+    out = os.popen(f"nm -D --defined-only {C.LIB_PATH}").read()
+    for name in declared_symbols():
+        assert re.search(rf"\bT {name}$", out, re.M), name
+
+
+def _cfg(g, d, B=64, Br=None, loss=C.LOSS_CE2, epoch=1, n_workers=1, rank=0, xl=-1):
+    cfg = C.GanConfig()
+    cfg.g, cfg.d = _spec(g), _spec(d)
+    cfg.batch, cfg.batch_real, cfg.epoch = B, Br or B, epoch
+    cfg.loss, cfg.weighting = loss, 0
+    cfg.n_workers, cfg.rank, cfg.exchange_layer = n_workers, rank, xl
+    cfg.lr_g = cfg.lr_d = 2e-4
+    cfg.beta1, cfg.beta2, cfg.adam_eps = 0.5, 0.999, 1e-8
+    cfg.bn_eps, cfg.bn_momentum, cfg.slope = 0.8, 0.1, 0.2
+    return cfg
+
+
+def _layout(cfg, which, n):
+    out = []
+    for i in range(n):
+        off, r, c, l, k = ctypes.c_int64(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        assert C.lib.cgl_gan_param_tensor(ctypes.byref(cfg), which, i, ctypes.byref(off), ctypes.byref(r),
+                                          ctypes.byref(c), ctypes.byref(l), ctypes.byref(k)) == 0
+        out.append((off.value, r.value, c.value, l.value, k.value))
+    assert C.lib.cgl_gan_param_tensor(ctypes.byref(cfg), which, n, None, None, None, None, None) == C_E_ARG
+    return out
+
+
+C_E_ARG = -1
+
+
+@pytest.mark.parametrize("kind", ["capgan", "mixg", "mdgan", "ring"])
+def test_layout_matches_reference_state_dict(kind):
+    if kind == "capgan":
+        gm, dm = specs.mnist_generator(), specs.mnist_discriminator()
+        G, ws = O.build_capgan(1)
+        gsd, dsd = G.state_dict(), ws[0].D.state_dict()
+        loss = C.LOSS_CE2
+    elif kind == "mixg":
+        gm, dm = specs.mixgen_worker(1), specs.mnist_discriminator()
+        G, ws = O.build_mixg(2)
+        gsd, dsd = G.state_dict(), ws[1].D.state_dict()
+        loss = C.LOSS_CE2
+    elif kind == "mdgan":
+        gm, dm = specs.mnist_generator(), specs.mnist_discriminator(sigmoid=True)
+        G, ws = O.build_capgan(1, loss="bce")
+        gsd, dsd = G.state_dict(), ws[0].D.state_dict()
+        loss = C.LOSS_BCE
+    else:
+        gm, dm = specs.ring_generator(0), specs.ring_discriminator()
+        G, ws = O.build_ring(1, 1)
+        gsd, dsd = G.state_dict(), ws[0].D.state_dict()
+        loss = C.LOSS_BCE
+    cfg = _cfg(gm, dm, loss=loss)
+    for m, which, sd in ((gm, C.MODEL_G, gsd), (dm, C.MODEL_D, dsd)):
+        keys = m.tensor_keys()
+        lay = _layout(cfg, which, len(keys))
+        total = C.lib.cgl_gan_param_count(ctypes.byref(cfg), which)
+        prev_end = 0
+        for k, (off, r, c, l, kd) in zip(keys, lay):
+            assert k in sd, k
+            assert r * c == sd[k].numel(), k
+            if kd == 0:
+                assert list(sd[k].shape) == [r, c], k
+            assert off % 64 == 0 and off >= prev_end
+            prev_end = off + r * c
+        assert total >= prev_end
+    nr = C.lib.cgl_gan_running_count(ctypes.byref(cfg))
+    assert nr == sum(((gm.dims[l + 1] + 63) // 64 * 64) * 2 for l in gm.bn_layers())
+    assert C.lib.cgl_gan_workspace_bytes(ctypes.byref(cfg)) > 0
+
+
+def test_config_validation():
+    gm, dm = specs.mnist_generator(), specs.mnist_discriminator()
+    ok = _cfg(gm, dm)
+    assert C.lib.cgl_gan_workspace_bytes(ctypes.byref(ok)) > 0
+    bad = _cfg(gm, dm, loss=C.LOSS_BCE)          # BCE needs a 1-unit D head
+    assert C.lib.cgl_gan_workspace_bytes(ctypes.byref(bad)) == C_E_ARG
+    bad = _cfg(gm, specs.ring_discriminator())   # G output 784 != D input 2
+    assert C.lib.cgl_gan_workspace_bytes(ctypes.byref(bad)) == C_E_ARG
+    bad = _cfg(gm, dm, epoch=9)
+    assert C.lib.cgl_gan_workspace_bytes(ctypes.byref(bad)) == C_E_ARG
+    bad = _cfg(gm, dm, n_workers=2, rank=2)
+    assert C.lib.cgl_gan_workspace_bytes(ctypes.byref(bad)) == C_E_ARG
+    bad = _cfg(gm, dm, xl=5)
+    assert C.lib.cgl_gan_workspace_bytes(ctypes.byref(bad)) == C_E_ARG
+    okx = _cfg(gm, dm, xl=specs.MIXGEN_HEAD_LAYER, n_workers=4, rank=3)
+    assert C.lib.cgl_gan_workspace_bytes(ctypes.byref(okx)) > 0
+    # create() rejects null buffers without touching a device
+    h = ctypes.c_void_p()
+    bufs = C.GanBuffers()
+    assert C.lib.cgl_gan_create(ctypes.byref(ok), ctypes.byref(bufs), ctypes.byref(h)) == C_E_ARG
+
+
+def test_ops_reject_bad_args():
+    assert C.lib.cgl_linear_fwd(None, None, None, None, 1, 1, 1, 0, 0.2, None, 0, None) == C_E_ARG
+    assert C.lib.cgl_adam_step(None, None, None, None, 1, 1, 1e-3, 0.5, 0.999, 1e-8, None, 0, None) == C_E_ARG
+    assert C.lib.cgl_op_workspace_bytes() >= 64
