@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""Benchmark: images/s of the CGL-GAN worker round (G+D step) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Workload (BASELINE.json configs[1] at N=1, configs[2] at N>1):
+  * model/mnist_model.py MLP GAN (G 100-128-256-512-1024-784 with BatchNorm1d(eps .8), D 784-512-256-2),
+    fp32, batch 256, CAPGAN worker round: two train-mode G forwards (Xd, Xg), one local D step on a
+    real batch (CE, Adam), the G loss through the updated D, G backward, lambda SGD and Adam G
+    (capgan.py:211-262 + :316-349), captured as hipGraph(s) and replayed.
+  * inputs: z drawn on device each round (Philox); the real batch gathered each round from a
+    synthetic 28x28 dataset resident in HBM (59,904 rows = 234 full batches, uniform(-1,1)) through
+    the in-graph per-epoch shuffle sampler.
+  * N > 1: one worker per GPU (CAPGAN N workers, S=1, G replicated with a shared z stream): per
+    round all_gather(G losses) -> lambda-weighting -> all_reduce(sum) of the weighted G-output
+    gradient -> replicated G update, plus the E-share all_reduce(avg) of D every --E rounds (RCCL).
+A "step" is one round; value = images/s over all ranks = N * 256 * K / max-over-ranks time.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cgl-gan_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "images/sec (G+D step) MNIST bs256 at 1/2/4/8 MI355X; D-loss match vs CPU"
+PEAK_F32_MFMA = 157.3    # TFLOP/s, MI355X dense fp32 matrix (MI355X_MICROARCH.md)
+PEAK_HBM = 8000.0        # GB/s
+# algorithmic work per image (BASELINE.md / SURVEY 8d): FLOPs excluding the D weight-gradient of
+# the G-loss path that the reference computes and discards
+FLOP_PER_IMAGE_MIN = 18.95e6
+
+
+def args_():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--batch", type=int, default=256)
+    p.add_argument("--rows", type=int, default=59904, help="synthetic dataset rows per worker")
+    p.add_argument("--E", type=int, default=1, help="D-share all-reduce period (N > 1)")
+    p.add_argument("--eager", action="store_true", help="launch without hipGraph")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--profile-rounds", type=int, default=5)
+    return p.parse_args()
+
+
+def build_step(a, rank, world):
+    from cglgan import GanStep, specs
+    from cglgan.init import default_init
+    gm, dm = specs.mnist_generator(), specs.mnist_discriminator()
+    g = torch.Generator(device="cuda").manual_seed(1000 + rank)
+    data = torch.rand(a.rows, 784, device="cuda", generator=g) * 2 - 1
+    step = GanStep(gm, dm, batch=a.batch, batch_real=a.batch, epoch=1, loss="ce", weighting="capgan",
+                   n_workers=world, rank=rank, seed=20211212, gen_z=True, real=data, sample_n=a.rows)
+    torch.manual_seed(20211212)          # G identical on every replica (capgan.py:28,156)
+    default_init(gm, step.g_views)
+    torch.manual_seed(20211212 + 1 + rank)
+    default_init(dm, step.d_views)
+    step.reset(beta=[1.0 / world] * world)
+    return step, data
+
+
+def one_round(step, world, r, a):
+    from cglgan._lib import PHASE_A, PHASE_ALL, PHASE_B
+    graph = not a.eager
+    if world == 1:
+        step.run(PHASE_ALL, graph=graph)
+        return
+    step.run(PHASE_A, graph=graph)
+    dist.all_gather_into_tensor(step.losses_all, step.own_loss())
+    step.alpha_scale()
+    dist.all_reduce(step.exchange_buffer())
+    step.run(PHASE_B, graph=graph)
+    if a.E > 0 and (r + 1) % a.E == 0:
+        dist.all_reduce(step.d_params, op=dist.ReduceOp.AVG)
+
+
+def profile_launches(step, world, rounds):
+    """Per-launch device time with HIP events on the launch stream (eager replay of the plan)."""
+    from cglgan._lib import PHASE_A, PHASE_ALL, PHASE_B
+    phases = [PHASE_ALL] if world == 1 else [PHASE_A, PHASE_B]
+    per_kind = {}
+    gemm_ms, gemm_flops, gemm_n = 0.0, 0.0, 0
+    s = torch.cuda.current_stream()
+    for _ in range(rounds):
+        recs = []
+        for ph in phases:
+            info = step.launches(ph)
+            for i, (kind, flops, grid) in enumerate(info):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                step.launch_one(i, ph)
+                e1.record(s)
+                recs.append((kind, flops, e0, e1))
+        torch.cuda.synchronize()
+        for kind, flops, e0, e1 in recs:
+            ms = e0.elapsed_time(e1)
+            k = per_kind.setdefault(kind, [0.0, 0])
+            k[0] += ms
+            k[1] += 1
+            if kind == "gemm":
+                gemm_ms += ms
+                gemm_flops += flops
+                gemm_n += 1
+    return per_kind, gemm_ms / rounds, gemm_flops / rounds, gemm_n / rounds
+
+
+def cpu_baseline(a):
+    """The CPU oracle (torch-CPU restatement of the reference step) on this host's cores."""
+    sys.path.insert(0, ROOT)
+    from oracle import gan_oracle as O
+    threads = max(1, min(16, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    G, workers = O.build_capgan(1)
+    srv = O.CapganServer(G, torch.tensor([1.0]))
+    B = a.batch
+    n, t_total = 0, 0.0
+    warm = 3
+    while True:
+        z1, z2, reals = O.synthetic_inputs(B, 1, 1, seed=5000 + n)
+        t0 = time.perf_counter()
+        srv.round(workers, z1, z2, reals)
+        dt = time.perf_counter() - t0
+        n += 1
+        if n > warm:
+            t_total += dt
+        if (n > warm and t_total >= a.cpu_seconds) or n >= 2000:
+            break
+    rounds = n - warm
+    return {"value": round(B * rounds / t_total, 1), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{rounds} CAPGAN rounds (B={B}, N=1) of the torch-CPU oracle after {warm} warm-up "
+                      f"rounds, {t_total:.1f} s, torch {torch.__version__}"}
+
+
+def main():
+    a = args_()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus N > 1 needs torch.distributed.run with N processes")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        step, data = build_step(a, rank, world)
+        torch.cuda.synchronize()
+        for r in range(a.warmup):
+            one_round(step, world, r, a)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for r in range(a.steps):
+            one_round(step, world, a.warmup + r, a)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        st = step.stats()
+        per_kind, gemm_ms, gemm_flops, gemm_n = profile_launches(step, world, a.profile_rounds)
+        plan = step.plan_info()
+    ms_step = el / a.steps * 1e3
+    value = world * a.batch * a.steps / el
+    out = None
+    if rank == 0:
+        gemm_tf = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
+        step_tf = a.batch * FLOP_PER_IMAGE_MIN / (ms_step * 1e-3) / 1e12
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": ("C2: model/mnist_model.py MLP GAN, CAPGAN worker round (G fwd x2, D step, "
+                                    "G loss, G bwd, Adam G/D), 1 worker per GPU" if world == 1 else
+                                    f"C3: CAPGAN {world} workers (1 per GPU), S=1, lambda-weighted G-gradient "
+                                    f"all-reduce + E={a.E} D all-reduce over RCCL"),
+                       "global_batch": a.batch * world, "batch_per_worker": a.batch, "img": "28x28x1",
+                       "parallelism": f"workers{world}", "graph": not a.eager,
+                       "dataset_rows_per_worker": a.rows},
+            "roofline": {"bound": "mfma", "kernel": "cgl_gemm_f32 (all GEMM launches of the round)",
+                         "achieved": round(gemm_tf, 3), "peak": PEAK_F32_MFMA, "unit": "TFLOP/s",
+                         "frac": round(gemm_tf / PEAK_F32_MFMA, 4), "traffic": None,
+                         "gemm_launches_per_round": gemm_n, "gemm_flops_per_round": gemm_flops,
+                         "gemm_ms_per_round": round(gemm_ms, 4),
+                         "avg_gemm_launch_us": round(gemm_ms / max(gemm_n, 1) * 1e3, 3),
+                         "step_achieved_tflops": round(step_tf, 3),
+                         "step_frac_mfma": round(step_tf / PEAK_F32_MFMA, 4),
+                         "per_kind_ms_per_round": {k: round(v[0] / a.profile_rounds, 4) for k, v in per_kind.items()},
+                         "launches_per_round": plan["launches"]},
+            "losses": {"d_loss": st["d_loss"][0], "g_loss": st["g_loss"], "lambda": st["lambda"],
+                       "round": st["round"]},
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(a)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return out
+
+
+if __name__ == "__main__":
+    main()

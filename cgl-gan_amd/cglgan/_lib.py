@@ -23,7 +23,7 @@ EXPORTS = [
     "cgl_gan_param_count", "cgl_gan_param_tensor", "cgl_gan_running_count", "cgl_gan_workspace_bytes",
     "cgl_gan_create", "cgl_gan_destroy", "cgl_gan_reset", "cgl_gan_run", "cgl_gan_run_graph",
     "cgl_gan_alpha_scale", "cgl_gan_exchange_buffer", "cgl_gan_tensor", "cgl_gan_read_stats",
-    "cgl_gan_plan_info", "cgl_linear_fwd", "cgl_linear_bwd_data", "cgl_linear_bwd_weight", "cgl_adam_step",
+    "cgl_gan_plan_info", "cgl_gan_launch_count", "cgl_gan_launch_info", "cgl_gan_launch_one", "cgl_linear_fwd", "cgl_linear_bwd_data", "cgl_linear_bwd_weight", "cgl_adam_step",
     "cgl_normal_fill", "cgl_op_workspace_bytes", "cgl_version",
 ]
 
@@ -37,9 +37,9 @@ class GanConfig(ctypes.Structure):
     _fields_ = [("g", MlpSpec), ("d", MlpSpec), ("batch", ctypes.c_int), ("batch_real", ctypes.c_int),
                 ("epoch", ctypes.c_int), ("loss", ctypes.c_int), ("weighting", ctypes.c_int),
                 ("n_workers", ctypes.c_int), ("rank", ctypes.c_int), ("exchange_layer", ctypes.c_int),
-                ("lr_g", ctypes.c_float), ("lr_d", ctypes.c_float), ("beta1", ctypes.c_float),
-                ("beta2", ctypes.c_float), ("adam_eps", ctypes.c_float), ("bn_eps", ctypes.c_float),
-                ("bn_momentum", ctypes.c_float), ("slope", ctypes.c_float), ("seed", ctypes.c_ulonglong),
+                ("lr_g", ctypes.c_double), ("lr_d", ctypes.c_double), ("beta1", ctypes.c_double),
+                ("beta2", ctypes.c_double), ("adam_eps", ctypes.c_double), ("bn_eps", ctypes.c_double),
+                ("bn_momentum", ctypes.c_double), ("slope", ctypes.c_float), ("seed", ctypes.c_ulonglong),
                 ("gen_z", ctypes.c_int), ("sample_n", ctypes.c_int)]
 
 
@@ -64,7 +64,7 @@ def _load():
                           "(there is no CPU fallback)")
     lib = ctypes.CDLL(LIB_PATH)
     P = ctypes.POINTER
-    vp, i64, ci, cf = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float
+    vp, i64, ci, cf, cd = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_double
     sig = {
         "cgl_gan_param_count": (i64, [P(GanConfig), ci]),
         "cgl_gan_param_tensor": (ci, [P(GanConfig), ci, ci, P(i64), P(ci), P(ci), P(ci), P(ci)]),
@@ -80,10 +80,13 @@ def _load():
         "cgl_gan_tensor": (ci, [vp, ci, P(vp), P(i64)]),
         "cgl_gan_read_stats": (ci, [vp, P(GanStats), vp]),
         "cgl_gan_plan_info": (ci, [vp, ci, P(ci), P(ci), P(ctypes.c_double)]),
+        "cgl_gan_launch_count": (ci, [vp, ci]),
+        "cgl_gan_launch_info": (ci, [vp, ci, ci, P(ci), P(cd), P(ci)]),
+        "cgl_gan_launch_one": (ci, [vp, ci, ci, vp]),
         "cgl_linear_fwd": (ci, [vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, i64, vp]),
         "cgl_linear_bwd_data": (ci, [vp, vp, vp, ci, ci, ci, vp, i64, vp]),
         "cgl_linear_bwd_weight": (ci, [vp, vp, vp, vp, ci, ci, ci, vp, i64, vp]),
-        "cgl_adam_step": (ci, [vp, vp, vp, vp, i64, ci, cf, cf, cf, cf, vp, i64, vp]),
+        "cgl_adam_step": (ci, [vp, vp, vp, vp, i64, ci, cd, cd, cd, cd, vp, i64, vp]),
         "cgl_normal_fill": (ci, [vp, i64, ctypes.c_ulonglong, ci, ci, vp]),
         "cgl_op_workspace_bytes": (i64, []),
         "cgl_version": (ctypes.c_char_p, []),

@@ -189,6 +189,12 @@ class GanStep:
         C.check(C.lib.cgl_gan_tensor(self._h, 0, ctypes.byref(p), ctypes.byref(n)))
         return self._wrap(p.value, n.value).view(2 * self.B, -1)
 
+    def internal(self, which):
+        """Internal tensor by cgl_gan_tensor code (include/cglgan.h) as a flat float view."""
+        p, n = ctypes.c_void_p(), ctypes.c_int64()
+        C.check(C.lib.cgl_gan_tensor(self._h, which, ctypes.byref(p), ctypes.byref(n)), "cgl_gan_tensor")
+        return self._wrap(p.value, n.value)
+
     def own_loss(self):
         p, n = ctypes.c_void_p(), ctypes.c_int64()
         C.check(C.lib.cgl_gan_tensor(self._h, 1, ctypes.byref(p), ctypes.byref(n)))
@@ -213,6 +219,21 @@ class GanStep:
         nl, ng, fl = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
         C.check(C.lib.cgl_gan_plan_info(self._h, phase, ctypes.byref(nl), ctypes.byref(ng), ctypes.byref(fl)))
         return {"launches": nl.value, "gemm_launches": ng.value, "gemm_flops": fl.value}
+
+    LAUNCH_KINDS = {0: "gemm", 1: "head", 2: "bn_bwd", 3: "adam", 4: "begin", 5: "normal", 6: "sample"}
+
+    def launches(self, phase=C.PHASE_ALL):
+        """[(kind, flops, grid)] of the planned launches of a phase, in stream order."""
+        n = C.lib.cgl_gan_launch_count(self._h, phase)
+        out = []
+        for i in range(n):
+            k, f, g = ctypes.c_int(), ctypes.c_double(), ctypes.c_int()
+            C.check(C.lib.cgl_gan_launch_info(self._h, phase, i, ctypes.byref(k), ctypes.byref(f), ctypes.byref(g)))
+            out.append((self.LAUNCH_KINDS[k.value], f.value, g.value))
+        return out
+
+    def launch_one(self, idx, phase=C.PHASE_ALL):
+        C.check(C.lib.cgl_gan_launch_one(self._h, phase, idx, _stream()), "cgl_gan_launch_one")
 
     def close(self):
         if getattr(self, "_h", None):

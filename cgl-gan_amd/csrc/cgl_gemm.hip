@@ -111,7 +111,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
         double mean, m2;
         int n;
         cgl_bn_group_stats(bn, K, k, g, mean, m2, n);
-        const double invstd = 1.0 / sqrt(m2 / n + (double)bn.eps);
+        const double invstd = 1.0 / sqrt(m2 / n + bn.eps);
         const float sc = (float)invstd * bn.gamma[k];
         const float sh = bn.beta[k] - (float)mean * sc;
         s_tf[((g - g0) * CGL_TF_MAXK + k) * 2 + 0] = sc;
@@ -135,7 +135,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
           }
           if (bn.save_mean) {
             bn.save_mean[(long)g * K + k] = (float)mean;
-            bn.save_invstd[(long)g * K + k] = (float)(1.0 / sqrt(m2 / n + (double)bn.eps));
+            bn.save_invstd[(long)g * K + k] = (float)(1.0 / sqrt(m2 / n + bn.eps));
           }
         }
       }

@@ -32,7 +32,8 @@ struct CglBnFwd {
   int mtot;               // total rows in the producer output
   const float* gamma;
   const float* beta;
-  float eps, momentum, slope;
+  double eps, momentum;
+  float slope;
   float* run_mean;        // updated by workgroup 0 (group 0 first, then 1), may be null
   float* run_var;
   float* save_mean;       // [ngroups][K] (workgroup 0), may be null

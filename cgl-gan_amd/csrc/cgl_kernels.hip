@@ -273,7 +273,7 @@ __global__ __launch_bounds__(256) void cgl_adam(CglAdamArgs a, CglStepState* st,
 struct CglBeginArgs {
   CglStepState* st;
   int epoch;
-  float lr_g, lr_d, b1, b2;
+  double lr_g, lr_d, b1, b2;
   int bn_layers;
 };
 
@@ -284,16 +284,16 @@ __global__ void cgl_step_begin(CglBeginArgs a) {
   st->round = r;
   {
     const double t = (double)r;
-    const double bc1 = 1.0 - pow((double)a.b1, t);
-    const double bc2 = 1.0 - pow((double)a.b2, t);
-    st->g_step_size = (float)((double)a.lr_g / bc1);
+    const double bc1 = 1.0 - pow(a.b1, t);
+    const double bc2 = 1.0 - pow(a.b2, t);
+    st->g_step_size = (float)(a.lr_g / bc1);
     st->g_bc2sqrt = (float)pow(bc2, 0.5);
   }
   for (int e = 0; e < a.epoch; ++e) {
     const double t = (double)((r - 1) * a.epoch + e + 1);
-    const double bc1 = 1.0 - pow((double)a.b1, t);
-    const double bc2 = 1.0 - pow((double)a.b2, t);
-    st->d_step_size[e] = (float)((double)a.lr_d / bc1);
+    const double bc1 = 1.0 - pow(a.b1, t);
+    const double bc2 = 1.0 - pow(a.b2, t);
+    st->d_step_size[e] = (float)(a.lr_d / bc1);
     st->d_bc2sqrt[e] = (float)pow(bc2, 0.5);
   }
   st->alpha = 1.f;

@@ -258,6 +258,7 @@ struct cgl_gan {
   std::vector<CglBnBwdDesc> bnb;
   std::vector<Launch> phA, phB;
   hipGraphExec_t gexec[3] = {nullptr, nullptr, nullptr};
+  hipStream_t cap = nullptr;   // private capture stream (the legacy default stream cannot capture)
   float* xchg = nullptr;
   int64_t xchg_n = 0;
   // parameter tensor pointers
@@ -337,10 +338,10 @@ void push_adam(cgl_gan* c, std::vector<Launch>& ph, float* p, const float* g, fl
   L.adam.n = n;
   L.adam.step_size = ss;
   L.adam.bc2sqrt = bc;
-  L.adam.b2 = c->cfg.beta2;
-  L.adam.w1 = (float)(1.0 - (double)c->cfg.beta1);
-  L.adam.w2 = (float)(1.0 - (double)c->cfg.beta2);
-  L.adam.eps = c->cfg.adam_eps;
+  L.adam.b2 = (float)c->cfg.beta2;
+  L.adam.w1 = (float)(1.0 - c->cfg.beta1);
+  L.adam.w2 = (float)(1.0 - c->cfg.beta2);
+  L.adam.eps = (float)c->cfg.adam_eps;
   L.tail = tail;
   L.grid = (int)((n + 255) / 256);
   ph.push_back(L);
@@ -870,6 +871,7 @@ int cgl_gan_destroy(cgl_gan* c) {
   if (!c) return CGL_E_ARG;
   for (auto& g : c->gexec)
     if (g) (void)hipGraphExecDestroy(g);
+  if (c->cap) (void)hipStreamDestroy(c->cap);
   delete c;
   return CGL_OK;
 }
@@ -899,11 +901,13 @@ int cgl_gan_run_graph(cgl_gan* c, int phase, void* stream) {
   if (!c || phase < 0 || phase > 2) return CGL_E_ARG;
   hipStream_t s = (hipStream_t)stream;
   if (!c->gexec[phase]) {
+    if (!c->cap) HIPCHK(hipStreamCreateWithFlags(&c->cap, hipStreamNonBlocking));
+    HIPCHK(hipStreamSynchronize(s));
     hipGraph_t graph;
-    HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    const int e = run_phase(c, phase, s);
+    HIPCHK(hipStreamBeginCapture(c->cap, hipStreamCaptureModeThreadLocal));
+    const int e = run_phase(c, phase, c->cap);
     hipGraph_t g2;
-    const hipError_t ec = hipStreamEndCapture(s, &g2);
+    const hipError_t ec = hipStreamEndCapture(c->cap, &g2);
     if (e) return e;
     HIPCHK(ec);
     graph = g2;
@@ -936,15 +940,41 @@ int cgl_gan_exchange_buffer(cgl_gan* c, float** ptr, int64_t* n) {
 int cgl_gan_tensor(cgl_gan* c, int which, float** ptr, int64_t* n) {
   if (!c || !ptr || !n) return CGL_E_ARG;
   const int L = c->cfg.g.n_layers;
+  const int B = c->cfg.batch;
+  const cgl_mlp_spec& g = c->cfg.g;
+  *ptr = nullptr;
+  *n = 0;
   if (which == 0) {
     *ptr = c->ws.gout[L - 1];
-    *n = (int64_t)2 * c->cfg.batch * c->cfg.g.dims[L];
+    *n = (int64_t)2 * B * g.dims[L];
   } else if (which == 1) {
     *ptr = &c->ws.st->g_loss_parts[0];
     *n = 1;
+  } else if (which == 2) {
+    *ptr = c->ws.dYL;
+    *n = (int64_t)B * g.dims[L];
+  } else if (which >= 16 && which < 16 + L) {       // gdA[l]: grad w.r.t. BN+LeakyReLU output (Xg rows)
+    *ptr = c->ws.gdA[which - 16];
+    *n = (int64_t)B * g.dims[which - 16 + 1];
+  } else if (which >= 32 && which < 32 + L) {       // gG[l]: grad w.r.t. Linear output (Xg rows)
+    *ptr = c->ws.gG[which - 32];
+    *n = (int64_t)B * g.dims[which - 32 + 1];
+  } else if (which >= 48 && which < 48 + L) {       // gact[l]: BN+LeakyReLU output (2B rows)
+    *ptr = c->ws.gact[which - 48];
+    *n = (int64_t)2 * B * g.dims[which - 48 + 1];
+  } else if (which >= 64 && which < 64 + L) {       // gout[l]: Linear output (pre-BN) / activation (2B rows)
+    *ptr = c->ws.gout[which - 64];
+    *n = (int64_t)2 * B * g.dims[which - 64 + 1];
+  } else if (which >= 80 && which < 80 + L) {       // saved BN batch mean [2][dims[l+1]] (per forward call)
+    *ptr = c->ws.gmean[which - 80];
+    *n = (int64_t)2 * g.dims[which - 80 + 1];
+  } else if (which >= 96 && which < 96 + L) {       // saved BN invstd [2][dims[l+1]]
+    *ptr = c->ws.ginvstd[which - 96];
+    *n = (int64_t)2 * g.dims[which - 96 + 1];
   } else {
     return CGL_E_ARG;
   }
+  if (!*ptr) return CGL_E_ARG;
   return CGL_OK;
 }
 
@@ -988,6 +1018,41 @@ int cgl_gan_plan_info(cgl_gan* c, int phase, int* n_launches, int* n_gemm, doubl
   if (n_gemm) *n_gemm = ngm;
   if (flops) *flops = f;
   return CGL_OK;
+}
+
+static const std::vector<Launch>* phase_list(cgl_gan* c, int phase, int idx, int* local) {
+  // CGL_PHASE_ALL enumerates phase A then phase B
+  if (phase == CGL_PHASE_A || (phase == CGL_PHASE_ALL && idx < (int)c->phA.size())) {
+    *local = idx;
+    return &c->phA;
+  }
+  *local = phase == CGL_PHASE_ALL ? idx - (int)c->phA.size() : idx;
+  return &c->phB;
+}
+
+int cgl_gan_launch_count(cgl_gan* c, int phase) {
+  if (!c || phase < 0 || phase > 2) return CGL_E_ARG;
+  if (phase == CGL_PHASE_A) return (int)c->phA.size();
+  if (phase == CGL_PHASE_B) return (int)c->phB.size();
+  return (int)(c->phA.size() + c->phB.size());
+}
+
+int cgl_gan_launch_info(cgl_gan* c, int phase, int idx, int* kind, double* flops, int* grid) {
+  if (!c || phase < 0 || phase > 2 || idx < 0 || idx >= cgl_gan_launch_count(c, phase)) return CGL_E_ARG;
+  int li;
+  const std::vector<Launch>* v = phase_list(c, phase, idx, &li);
+  const Launch& L = (*v)[li];
+  if (kind) *kind = (int)L.kind;
+  if (flops) *flops = L.flops;
+  if (grid) *grid = L.grid;
+  return CGL_OK;
+}
+
+int cgl_gan_launch_one(cgl_gan* c, int phase, int idx, void* stream) {
+  if (!c || phase < 0 || phase > 2 || idx < 0 || idx >= cgl_gan_launch_count(c, phase)) return CGL_E_ARG;
+  int li;
+  const std::vector<Launch>* v = phase_list(c, phase, idx, &li);
+  return exec_launch(c, (*v)[li], (hipStream_t)stream);
 }
 
 // ---------------- single ops -------------------------------------------------------------
@@ -1047,14 +1112,14 @@ int cgl_linear_bwd_weight(const float* dY, const float* X, float* dW, float* db,
   return single_gemm(d, ws, wsb, (hipStream_t)stream);
 }
 
-int cgl_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int step, float lr, float beta1,
-                  float beta2, float eps, void* ws, int64_t wsb, void* stream) {
+int cgl_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int step, double lr, double beta1,
+                  double beta2, double eps, void* ws, int64_t wsb, void* stream) {
   if (!p || !g || !m || !v || n < 0 || step < 1 || !ws || wsb < 8) return CGL_E_ARG;
   hipStream_t s = (hipStream_t)stream;
   float sc[2];
-  const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
-  const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
-  sc[0] = (float)((double)lr / bc1);
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  sc[0] = (float)(lr / bc1);
   sc[1] = (float)std::pow(bc2, 0.5);
   HIPCHK(hipMemcpyAsync(ws, sc, sizeof(sc), hipMemcpyHostToDevice, s));
   CglAdamArgs a;
@@ -1065,10 +1130,10 @@ int cgl_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int s
   a.n = (long)n;
   a.step_size = (const float*)ws;
   a.bc2sqrt = (const float*)ws + 1;
-  a.b2 = beta2;
-  a.w1 = (float)(1.0 - (double)beta1);
-  a.w2 = (float)(1.0 - (double)beta2);
-  a.eps = eps;
+  a.b2 = (float)beta2;
+  a.w1 = (float)(1.0 - beta1);
+  a.w2 = (float)(1.0 - beta2);
+  a.eps = (float)eps;
   if (n > 0)
     hipLaunchKernelGGL(cgl_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, (CglStepState*)nullptr, 0);
   const hipError_t e = hipGetLastError();

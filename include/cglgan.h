@@ -63,8 +63,10 @@ typedef struct cgl_gan_config {
   int exchange_layer;   /* -1: exchange the G-output gradient (CAPGAN / MDGAN);
                            k > 0: exchange the gradient of G layer k's input (Mix-G trunk/head
                            split: layers >= k are this worker's head, mixed-gan.py:263-281)     */
-  float lr_g, lr_d, beta1, beta2, adam_eps;   /* 2e-4, 2e-4, 0.5, 0.999, 1e-8 (capgan.py:52-53,122) */
-  float bn_eps, bn_momentum, slope;           /* 0.8, 0.1, 0.2 (model/mnist_model.py:13-14)     */
+  double lr_g, lr_d, beta1, beta2, adam_eps;  /* 2e-4, 2e-4, 0.5, 0.999, 1e-8 (capgan.py:52-53,122);
+                                                 double like the Python floats torch.optim uses  */
+  double bn_eps, bn_momentum;                 /* 0.8, 0.1 (model/mnist_model.py:13)              */
+  float slope;                                /* 0.2 (model/mnist_model.py:14)                   */
   unsigned long long seed;                    /* z RNG seed; identical across a server group     */
   int gen_z;            /* 1: the step draws z on device (Philox) each round; 0: caller fills z   */
   int sample_n;         /* >0: in-graph shuffle sampler over sample_n real rows (per-epoch keyed
@@ -126,13 +128,21 @@ int cgl_gan_run_graph(cgl_gan* ctx, int phase, void* stream);
 int cgl_gan_alpha_scale(cgl_gan* ctx, void* stream);
 /* The exchange gradient buffer (device pointer, float count). */
 int cgl_gan_exchange_buffer(cgl_gan* ctx, float** ptr, int64_t* n);
-/* Device pointer of an internal activation: 0 = G output [2B][img] (Xd rows then Xg rows),
- * 1 = own G-loss scalar. */
+/* Device pointer of an internal tensor: 0 = G output [2B][img] (Xd rows then Xg rows),
+ * 1 = own G-loss scalar, 2 = gradient at the G output [B][img] (after Tanh'),
+ * 16+l / 32+l = gradient w.r.t. layer l's activation / Linear output [B][dims[l+1]] (Xg rows),
+ * 48+l / 64+l = layer l's BN+LeakyReLU output / Linear output [2B][dims[l+1]]. */
 int cgl_gan_tensor(cgl_gan* ctx, int which, float** ptr, int64_t* n);
 /* Synchronous copy of the round scalars to the host. */
 int cgl_gan_read_stats(cgl_gan* ctx, cgl_gan_stats* out, void* stream);
 /* Launch / kernel counts of a phase (for roofline bookkeeping). */
 int cgl_gan_plan_info(cgl_gan* ctx, int phase, int* n_launches, int* n_gemm_launches, double* gemm_flops);
+/* Per-launch access to the plan (instrumented timing: the caller brackets each launch with
+ * events on `stream`).  kind: 0 GEMM, 1 loss head, 2 BN backward, 3 Adam, 4 round begin,
+ * 5 normal RNG, 6 sampler.  flops = algorithmic GEMM flops of the launch (0 for others). */
+int cgl_gan_launch_count(cgl_gan* ctx, int phase);
+int cgl_gan_launch_info(cgl_gan* ctx, int phase, int idx, int* kind, double* flops, int* grid);
+int cgl_gan_launch_one(cgl_gan* ctx, int phase, int idx, void* stream);
 
 /* ---------------- single ops (nn.Module boundary: model/mnist_model.py) ---------------- */
 /* Y[M,N] = act(X[M,K] W[N,K]^T + b)   act: 0 none, 1 LeakyReLU(slope), 2 Tanh  (nn.Linear fwd) */
@@ -145,8 +155,8 @@ int cgl_linear_bwd_data(const float* dY, const float* W, float* dX, int M, int N
 int cgl_linear_bwd_weight(const float* dY, const float* X, float* dW, float* db, int M, int N, int K,
                           void* workspace, int64_t ws_bytes, void* stream);
 /* Flat Adam step t (optim.Adam, torch _single_tensor_adam op order) */
-int cgl_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int step, float lr, float beta1,
-                  float beta2, float eps, void* workspace, int64_t ws_bytes, void* stream);
+int cgl_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int step, double lr, double beta1,
+                  double beta2, double eps, void* workspace, int64_t ws_bytes, void* stream);
 /* N(0,1) fill (Philox4x32-10 + Box-Muller); counter = (index, round, stream_id) */
 int cgl_normal_fill(float* out, int64_t n, unsigned long long seed, int round, int stream_id, void* stream);
 int64_t cgl_op_workspace_bytes(void);

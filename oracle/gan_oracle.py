@@ -146,10 +146,14 @@ class SeqNet:
                     torch.nn.init.normal_(self.params[ent[1] + ".weight"], 1.0, 0.02, generator=generator)
                     torch.nn.init.constant_(self.params[ent[1] + ".bias"], 0)
 
-    def forward(self, x, train=True):
-        """nn.Sequential forward of the spec (train-mode BatchNorm updates running stats)."""
+    def forward(self, x, train=True, trace=None):
+        """nn.Sequential forward of the spec (train-mode BatchNorm updates running stats).
+
+        ``trace`` (a list) collects the input of every LeakyReLU (conditioning checks in tests)."""
         h = x.reshape(x.shape[0], -1)
         for ent in self.spec:
+            if trace is not None and ent[0] == "leaky":
+                trace.append(h.detach())
             kind = ent[0]
             if kind == "linear":
                 h = F.linear(h, self.params[ent[1] + ".weight"], self.params[ent[1] + ".bias"])
@@ -201,9 +205,9 @@ class MixNet:
         self.trunk = SeqNet(trunk_spec, generator=generator)
         self.heads = [SeqNet(s, generator=generator) for s in head_specs]
 
-    def forward(self, z, train=True):
-        h = self.trunk.forward(z, train)
-        return torch.cat([hd.forward(h, train) for hd in self.heads], dim=0)
+    def forward(self, z, train=True, trace=None):
+        h = self.trunk.forward(z, train, trace)
+        return torch.cat([hd.forward(h, train, trace) for hd in self.heads], dim=0)
 
     def apply_weights_init(self, generator=None):
         self.trunk.apply_weights_init(generator)

