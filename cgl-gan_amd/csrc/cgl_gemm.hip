@@ -27,32 +27,46 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ const float* cgl_row(const CglRowSrc& s, int r) {
   if (r < s.split) {
     int rr = r;
-    if (s.idx0) rr = s.idx0[(s.idx_off ? *s.idx_off : 0) + r];
+    if (s.idx0) rr = gldi(s.idx0 + (s.idx_off ? gldi(s.idx_off) : 0) + r);
     return s.p0 + (long)rr * s.ld;
   }
   return s.p1 + (long)(r - s.split) * s.ld;
 }
 
-// 8 consecutive k of one row (k-contiguous operand); zeros outside [0,K) or for invalid rows.
-__device__ __forceinline__ void cgl_load_kc(const float* __restrict__ rp, bool ok, int k, int K, int vec,
-                                            float v[8]) {
-  if (vec) {
-    float4 x = make_float4(0.f, 0.f, 0.f, 0.f), y = x;
-    if (ok && k + 3 < K) x = *reinterpret_cast<const float4*>(rp + k);
-    if (ok && k + 7 < K) y = *reinterpret_cast<const float4*>(rp + k + 4);
-    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-    v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+// Loads are issued UNCONDITIONALLY from clamped (always valid) addresses and masked only when
+// the values are consumed: a predicated "load or zero" compiles to a branch around every load
+// with a full vmcnt(0) drain, which serialises the memory pipeline (measured: one full memory
+// latency per 16-k chunk).
+
+// Operand pointers come out of the descriptor in memory, so the compiler cannot prove they are
+// global and would emit flat_load_* -- which return out of order and force
+// s_waitcnt vmcnt(0) lgkmcnt(0) at every use.  Casting to address space 1 gives global_load_*
+// with counted waits.
+// raw: 8 consecutive k of one row of a k-contiguous operand (k clamped into [0, K))
+template <int VEC>
+__device__ __forceinline__ void cgl_ld_kc(const float* __restrict__ rp_, int k, int K, float v[8]) {
+  gcfp rp = (gcfp)rp_;
+  if (VEC) {  // K % 4 == 0, 16-byte aligned rows
+    const f32x4 x = *(gcf4p)(rp + min(k, K - 4));
+    const f32x4 y = *(gcf4p)(rp + min(k + 4, K - 4));
+    v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
+    v[4] = y[0]; v[5] = y[1]; v[6] = y[2]; v[7] = y[3];
   } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (ok && k + j < K) ? rp[k + j] : 0.f;
+    for (int j = 0; j < 8; ++j) v[j] = rp[min(k + j, K - 1)];
   }
 }
 
-// rows k..k+7 at one column of a row-major [K][ld] operand (mn-contiguous operand).
-__device__ __forceinline__ void cgl_load_mn(const float* __restrict__ p, int ld, bool ok, int k, int K,
-                                            float v[8]) {
+// raw: rows k..k+7 (clamped) at one column of a row-major [K][ld] (mn-contiguous) operand
+__device__ __forceinline__ void cgl_ld_mn(const float* __restrict__ p_, int ld, int k, int K, float v[8]) {
+  gcfp p = (gcfp)p_;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = (ok && k + j < K) ? p[(long)(k + j) * ld] : 0.f;
+  for (int j = 0; j < 8; ++j) v[j] = p[(long)min(k + j, K - 1) * ld];
+}
+
+__device__ __forceinline__ void cgl_mask(float v[8], bool ok, int k, int K) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (ok && k + j < K) ? v[j] : 0.f;
 }
 
 // Mean / biased variance of BatchNorm group g for feature k from the producer partials
@@ -62,26 +76,48 @@ __device__ void cgl_bn_group_stats(const CglBnFwd& bn, int K, int k, int g, doub
   const int r0 = g * bn.gr, r1 = min(r0 + bn.gr, bn.mtot);
   n = r1 - r0;
   const int t0 = r0 / bn.part_bm, t1 = (r1 - 1) / bn.part_bm;
+  // each tile contributes one {sum, M2} pair; blocks of 8 independent loads in flight, then the
+  // exact parallel combination M2 = sum M2_t + n_t (mean_t - mean)^2 (fixed order)
+  const int nt = t1 - t0 + 1;
   double s = 0.0;
-  for (int t = t0; t <= t1; ++t) {
-    const int slot = g - (t * bn.part_bm) / bn.gr;
-    s += (double)bn.part[((long)(t * 2 + slot) * K + k) * 2 + 0];
+  for (int i0 = 0; i0 < nt; i0 += 8) {
+    float ps[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int t = t0 + min(i0 + j, nt - 1);
+      const int slot = g - (t * bn.part_bm) / bn.gr;
+      ps[j] = gld(bn.part + ((long)(t * 2 + slot) * K + k) * 2);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (i0 + j < nt) s += (double)ps[j];
   }
   mean = s / n;
   double q = 0.0;
-  for (int t = t0; t <= t1; ++t) {
-    const int slot = g - (t * bn.part_bm) / bn.gr;
-    const int a = max(t * bn.part_bm, r0), b = min((t + 1) * bn.part_bm, r1);
-    const int c = b - a;
-    const float* pp = bn.part + ((long)(t * 2 + slot) * K + k) * 2;
-    const double mt = (double)pp[0] / c;
-    const double d = mt - mean;
-    q += (double)pp[1] + c * d * d;
+  for (int i0 = 0; i0 < nt; i0 += 8) {
+    float ps[8], pq[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int t = t0 + min(i0 + j, nt - 1);
+      const int slot = g - (t * bn.part_bm) / bn.gr;
+      const float* pp = bn.part + ((long)(t * 2 + slot) * K + k) * 2;
+      ps[j] = gld(pp);
+      pq[j] = gld(pp + 1);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (i0 + j < nt) {
+        const int t = t0 + i0 + j;
+        const int c = min((t + 1) * bn.part_bm, r1) - max(t * bn.part_bm, r0);
+        const double dd = (double)ps[j] / c - mean;
+        q += (double)pq[j] + c * dd * dd;
+      }
+    }
   }
   m2 = q;
 }
 
-template <int LAYOUT>
+template <int LAYOUT, int VEC>
 __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d, int bid, float* __restrict__ s_tf,
                                               float* __restrict__ s_red, float* __restrict__ s_col) {
   const int M = d->M, N = d->N, K = d->K;
@@ -112,8 +148,8 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
         int n;
         cgl_bn_group_stats(bn, K, k, g, mean, m2, n);
         const double invstd = 1.0 / sqrt(m2 / n + bn.eps);
-        const float sc = (float)invstd * bn.gamma[k];
-        const float sh = bn.beta[k] - (float)mean * sc;
+        const float sc = (float)invstd * gld(bn.gamma + k);
+        const float sh = gld(bn.beta + k) - (float)mean * sc;
         s_tf[((g - g0) * CGL_TF_MAXK + k) * 2 + 0] = sc;
         s_tf[((g - g0) * CGL_TF_MAXK + k) * 2 + 1] = sh;
       }
@@ -129,13 +165,13 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
           cgl_bn_group_stats(bn, K, k, g, mean, m2, n);
           if (bn.run_mean) {
             const double mom = bn.momentum;
-            bn.run_mean[k] = (float)(mom * mean + (1.0 - mom) * (double)bn.run_mean[k]);
+            gst(bn.run_mean + k, (float)(mom * mean + (1.0 - mom) * (double)gld(bn.run_mean + k)));
             const double unb = m2 / (n - 1);
-            bn.run_var[k] = (float)(mom * unb + (1.0 - mom) * (double)bn.run_var[k]);
+            gst(bn.run_var + k, (float)(mom * unb + (1.0 - mom) * (double)gld(bn.run_var + k)));
           }
           if (bn.save_mean) {
-            bn.save_mean[(long)g * K + k] = (float)mean;
-            bn.save_invstd[(long)g * K + k] = (float)(1.0 / sqrt(m2 / n + bn.eps));
+            gst(bn.save_mean + (long)g * K + k, (float)mean);
+            gst(bn.save_invstd + (long)g * K + k, (float)(1.0 / sqrt(m2 / n + bn.eps)));
           }
         }
       }
@@ -151,14 +187,15 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   const int am = m0 + li;          // A row (kc) or A column (mn)
   const int bn_ = n0 + li;         // B row (NT) or B column (NN/TN)
   const bool a_ok = am < M;
-  const bool b_ok = bn_ < N;
-  const float* __restrict__ a_row = nullptr;
-  const float* __restrict__ b_row = nullptr;
-  if (LAYOUT != 2) a_row = a_ok ? cgl_row(d->a, am) : d->a.p0;
-  if (LAYOUT == 0) b_row = b_ok ? cgl_row(d->b, bn_) : d->b.p0;
-  const int a_vec = d->a_vec, b_vec = d->b_vec;
   const int b_ones = (LAYOUT != 0) ? d->b_ones_col : 0;
+  const int nmem = N - b_ones;     // columns of B actually in memory
+  const bool b_ok = bn_ < nmem;
   const bool b_is_ones = b_ones && (bn_ == N - 1);
+  // clamped (always dereferenceable) operand bases
+  const float* __restrict__ a_base = (LAYOUT != 2) ? cgl_row(d->a, min(am, M - 1)) : d->a.p0 + min(am, M - 1);
+  const float* __restrict__ b_base =
+      (LAYOUT == 0) ? cgl_row(d->b, min(bn_, N - 1)) : d->b.p0 + max(0, min(bn_, nmem - 1));
+  const int lda = d->a.ld, ldb = d->b.ld;
   const int gsel = a_tf ? (a_ok ? am / d->bn.gr - g0 : 0) : 0;
   const float slope_tf = d->bn.slope;
   float* __restrict__ a_copy = d->a_copy;
@@ -168,62 +205,60 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 
-  float av[8], bv[8];
   auto load_chunk = [&](int c, float* A_, float* B_) {
     const int k = c * CGL_GEMM_KCHUNK + 8 * lh;
-    if (LAYOUT == 2) {
-      cgl_load_mn(d->a.p0 + am, d->a.ld, a_ok, k, K, A_);
-    } else {
-      cgl_load_kc(a_row, a_ok, k, K, a_vec, A_);
-    }
-    if (LAYOUT == 0) {
-      cgl_load_kc(b_row, b_ok, k, K, b_vec, B_);
-    } else {
-      if (b_is_ones) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) B_[j] = (k + j < K) ? 1.f : 0.f;
-      } else {
-        cgl_load_mn(d->b.p0 + bn_, d->b.ld, b_ok, k, K, B_);
-      }
-    }
+    if (LAYOUT == 2)
+      cgl_ld_mn(a_base, lda, k, K, A_);
+    else
+      cgl_ld_kc<VEC>(a_base, k, K, A_);
+    if (LAYOUT == 0)
+      cgl_ld_kc<VEC>(b_base, k, K, B_);
+    else
+      cgl_ld_mn(b_base, ldb, k, K, B_);
   };
-
-  if (cb < ce) load_chunk(cb, av, bv);
-  for (int c = cb; c < ce; ++c) {
-    float an[8], bnx[8];
-    if (c + 1 < ce) load_chunk(c + 1, an, bnx);
+  auto compute_chunk = [&](int c, float* A_, float* B_) {
     const int k = c * CGL_GEMM_KCHUNK + 8 * lh;
+    cgl_mask(A_, a_ok, k, K);
+    if (b_is_ones) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) B_[j] = (k + j < K) ? 1.f : 0.f;
+    } else {
+      cgl_mask(B_, b_ok, k, K);
+    }
     if (a_tf) {
       const float* t = s_tf + (gsel * CGL_TF_MAXK) * 2;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        if (a_ok && k + j < K) {
-          float x = fmaf(av[j], t[(k + j) * 2 + 0], t[(k + j) * 2 + 1]);
-          av[j] = x > 0.f ? x : x * slope_tf;
-        } else {
-          av[j] = 0.f;
-        }
+        const int kk = min(k + j, K - 1);
+        const float x = fmaf(A_[j], t[kk * 2 + 0], t[kk * 2 + 1]);
+        A_[j] = (a_ok && k + j < K) ? (x > 0.f ? x : x * slope_tf) : 0.f;
       }
     }
     if (do_copy) {
       float* dst = a_copy + (long)am * d->a_copy_ld;
-      if (a_vec && k + 7 < K) {
-        *reinterpret_cast<float4*>(dst + k) = make_float4(av[0], av[1], av[2], av[3]);
-        *reinterpret_cast<float4*>(dst + k + 4) = make_float4(av[4], av[5], av[6], av[7]);
+      if (VEC && k + 7 < K) {
+        *(gf4p)(dst + k) = f32x4{A_[0], A_[1], A_[2], A_[3]};
+        *(gf4p)(dst + k + 4) = f32x4{A_[4], A_[5], A_[6], A_[7]};
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          if (k + j < K) dst[k + j] = av[j];
+          if (k + j < K) gst(dst + k + j, A_[j]);
       }
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], bv[j], acc, 0, 0, 0);
-    if (c + 1 < ce) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        av[j] = an[j];
-        bv[j] = bnx[j];
-      }
+    for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A_[j], B_[j], acc, 0, 0, 0);
+  };
+
+  // two register sets in ping-pong: the loads of chunk c+1 are in flight while chunk c's MFMAs
+  // run, and no register copy forces an early wait.  Tail loads are clamped re-loads.
+  if (cb < ce) {
+    float xa[8], xb[8], ya[8], yb[8];
+    load_chunk(cb, xa, xb);
+    for (int c = cb; c < ce; c += 2) {
+      load_chunk(min(c + 1, ce - 1), ya, yb);
+      compute_chunk(c, xa, xb);
+      load_chunk(min(c + 2, ce - 1), xa, xb);
+      if (c + 1 < ce) compute_chunk(c + 1, ya, yb);
     }
   }
 
@@ -256,7 +291,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 
   if (owner && colok && !ones_col) {
     if (d->bias) {
-      const float bb = d->bias[col];
+      const float bb = gld(d->bias + col);
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] += bb;
     }
@@ -270,24 +305,24 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     }
     if (d->mask_ref) {
       const float sl = d->slope;
+      float ref[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = rbase + (r & 3) + 8 * (r >> 2);
-        if (row < M) {
-          const float ref = d->mask_ref[(long)row * d->mask_ld + col];
-          v[r] = ref > 0.f ? v[r] : v[r] * sl;
-        }
+        const int row = min(rbase + (r & 3) + 8 * (r >> 2), M - 1);
+        ref[r] = gld(d->mask_ref + (long)row * d->mask_ld + col);
       }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = ref[r] > 0.f ? v[r] : v[r] * sl;
     }
     if (d->tanh_ref) {
+      float t[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = rbase + (r & 3) + 8 * (r >> 2);
-        if (row < M) {
-          const float t = d->tanh_ref[(long)row * d->tanh_ld + col];
-          v[r] = v[r] * (1.f - t * t);
-        }
+        const int row = min(rbase + (r & 3) + 8 * (r >> 2), M - 1);
+        t[r] = gld(d->tanh_ref + (long)row * d->tanh_ld + col);
       }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = v[r] * (1.f - t[r] * t[r]);
     }
   }
 
@@ -340,8 +375,8 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     if (owner && wm == 0 && lh == 0 && colok) {
       for (int s = 0; s < 2; ++s) {
         float* p = d->stat_part + ((long)(tm * 2 + s) * N + col) * 2;
-        p[0] = part[s][0];
-        p[1] = part[s][1];
+        gst(p, part[s][0]);
+        gst(p + 1, part[s][1]);
       }
     }
   }
@@ -352,7 +387,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = rbase + (r & 3) + 8 * (r >> 2);
-          if (row < M) d->bias_out[row] = v[r];
+          if (row < M) gst(d->bias_out + row, v[r]);
         }
       }
     } else {
@@ -361,7 +396,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = rbase + (r & 3) + 8 * (r >> 2);
-        if (row < M) C[(long)row * ldc + col] = v[r];
+        if (row < M) gst(C + (long)row * ldc + col, v[r]);
       }
     }
   }
@@ -379,10 +414,19 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
     if (bid >= descs[q].wg_begin) di = q;
   const CglGemmDesc* __restrict__ d = descs + di;
   const int layout = d->layout;
-  if (layout == 0)
-    cgl_gemm_body<0>(d, bid, s_tf, s_red, s_col);
-  else if (layout == 1)
-    cgl_gemm_body<1>(d, bid, s_tf, s_red, s_col);
-  else
-    cgl_gemm_body<2>(d, bid, s_tf, s_red, s_col);
+  // VEC: every k-contiguous operand allows 16-byte loads (K % 4 == 0, aligned rows)
+  const int vec = layout == 0 ? (d->a_vec && d->b_vec) : d->a_vec;
+  if (layout == 0) {
+    if (vec)
+      cgl_gemm_body<0, 1>(d, bid, s_tf, s_red, s_col);
+    else
+      cgl_gemm_body<0, 0>(d, bid, s_tf, s_red, s_col);
+  } else if (layout == 1) {
+    if (vec)
+      cgl_gemm_body<1, 1>(d, bid, s_tf, s_red, s_col);
+    else
+      cgl_gemm_body<1, 0>(d, bid, s_tf, s_red, s_col);
+  } else {
+    cgl_gemm_body<2, 0>(d, bid, s_tf, s_red, s_col);
+  }
 }

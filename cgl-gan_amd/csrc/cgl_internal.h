@@ -12,6 +12,20 @@
 
 enum { CGL_EPI_ACT_NONE = 0, CGL_EPI_ACT_LEAKY = 1, CGL_EPI_ACT_TANH = 2 };
 
+// Global-address-space accessors.  Pointers read out of a descriptor in memory are generic to
+// the compiler, which then emits flat_* instructions; flat loads return out of order and force
+// s_waitcnt vmcnt(0) lgkmcnt(0) at every use.  Every kernel accesses descriptor-borne buffers
+// through these so that global_* instructions with counted waits are generated.
+#define CGL_GLOBAL __attribute__((address_space(1)))
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef const CGL_GLOBAL float* gcfp;
+typedef CGL_GLOBAL float* gfp;
+typedef const CGL_GLOBAL f32x4* gcf4p;
+typedef CGL_GLOBAL f32x4* gf4p;
+__device__ __forceinline__ float gld(const float* p) { return *(gcfp)p; }
+__device__ __forceinline__ void gst(float* p, float v) { *(gfp)p = v; }
+__device__ __forceinline__ int gldi(const int* p) { return *(const CGL_GLOBAL int*)p; }
+
 // Row source of a row-major operand whose rows are the non-contiguous index.
 // Row r < split comes from p0 (optionally through idx0[idx_off + r]), rows >= split from p1.
 struct CglRowSrc {

@@ -25,6 +25,9 @@ __device__ __forceinline__ float cgl_wave_sum(float x) {
 }
 
 __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restrict__ hd) {
+  // Each wave owns rows r0 + wave + 4 i; a row is a dot product of F features (F % 4 == 0) done
+  // with 16-byte global loads, a 64-lane reduction, the loss and its gradient, then the
+  // gradient into the last hidden layer (dlogits . W) * LeakyReLU'(P).
   __shared__ float s_loss[4][2];
   __shared__ int s_last;
   const int M = hd->M, F = hd->F, C = hd->C;
@@ -32,15 +35,24 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
   const int lane = threadIdx.x & 63;
   const int r0 = blockIdx.x * hd->rows_per_wg;
   const int r1 = min(r0 + hd->rows_per_wg, M);
+  const float* __restrict__ Pb = hd->P;
+  const float* __restrict__ W = hd->W;
+  const int F4 = F >> 2;
   float lsum[2] = {0.f, 0.f};
   for (int r = r0 + wave; r < r1; r += 4) {
-    const float* __restrict__ p = hd->P + (long)r * hd->ldp;
-    float z[2];
+    const float* p = Pb + (long)r * hd->ldp;
+    float z[2] = {0.f, 0.f};
     for (int c = 0; c < C; ++c) {
-      const float* __restrict__ w = hd->W + (long)c * F;
       float s = 0.f;
-      for (int f = lane; f < F; f += 64) s = fmaf(p[f], w[f], s);
-      z[c] = cgl_wave_sum(s) + hd->b[c];
+      for (int q = lane; q < F4; q += 64) {
+        const f32x4 pv = *(gcf4p)(p + 4 * q);
+        const f32x4 wv = *(gcf4p)(W + (long)c * F + 4 * q);
+        s = fmaf(pv[0], wv[0], s);
+        s = fmaf(pv[1], wv[1], s);
+        s = fmaf(pv[2], wv[2], s);
+        s = fmaf(pv[3], wv[3], s);
+      }
+      z[c] = cgl_wave_sum(s) + gld(hd->b + c);
     }
     const int seg = r < hd->split ? 0 : 1;
     const int t = seg ? hd->t1 : hd->t0;
@@ -68,14 +80,24 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
       dl[1] = 0.f;
     }
     lsum[seg] += lossv;
-    if (hd->dlogits && lane < C) hd->dlogits[(long)r * C + lane] = dl[lane];
+    if (hd->dlogits && lane < C) gst(hd->dlogits + (long)r * C + lane, dl[lane]);
     if (hd->dP) {
-      float* __restrict__ dp = hd->dP + (long)r * hd->lddp;
+      float* dp = hd->dP + (long)r * hd->lddp;
       const float sl = hd->slope;
-      for (int f = lane; f < F; f += 64) {
-        float g = dl[0] * hd->W[f];
-        if (C == 2) g = fmaf(dl[1], hd->W[F + f], g);
-        dp[f] = p[f] > 0.f ? g : g * sl;
+      for (int q = lane; q < F4; q += 64) {
+        const f32x4 pv = *(gcf4p)(p + 4 * q);
+        const f32x4 w0 = *(gcf4p)(W + 4 * q);
+        f32x4 g = dl[0] * w0;
+        if (C == 2) {
+          const f32x4 w1 = *(gcf4p)(W + F + 4 * q);
+          g[0] = fmaf(dl[1], w1[0], g[0]);
+          g[1] = fmaf(dl[1], w1[1], g[1]);
+          g[2] = fmaf(dl[1], w1[2], g[2]);
+          g[3] = fmaf(dl[1], w1[3], g[3]);
+        }
+        f32x4 o;
+        for (int e = 0; e < 4; ++e) o[e] = pv[e] > 0.f ? g[e] : g[e] * sl;
+        *(gf4p)(dp + 4 * q) = o;
       }
     }
   }
@@ -90,8 +112,8 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
       a += s_loss[q][0];
       b += s_loss[q][1];
     }
-    hd->part[blockIdx.x * 2 + 0] = a;
-    hd->part[blockIdx.x * 2 + 1] = b;
+    gst(hd->part + blockIdx.x * 2 + 0, a);
+    gst(hd->part + blockIdx.x * 2 + 1, b);
     // last-arriver reduction (agent-scope release before the ticket, acquire after)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -109,9 +131,9 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
       const int n0 = min(hd->split, M), n1 = M - n0;
       const float l0 = n0 > 0 ? (float)(s0 / n0) : 0.f;
       const float l1 = n1 > 0 ? (float)(s1 / n1) : 0.f;
-      hd->loss_out[0] = l0;
-      hd->loss_out[1] = l1;
-      if (hd->combine_out) *hd->combine_out = (l0 + l1) * hd->combine;
+      gst(hd->loss_out, l0);
+      gst(hd->loss_out + 1, l1);
+      if (hd->combine_out) gst(hd->combine_out, (l0 + l1) * hd->combine);
       __hip_atomic_store(hd->counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -120,24 +142,38 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
 // ------------------------------------------------------------------------------------------
 // BatchNorm1d backward (train) + LeakyReLU' mask.  One workgroup owns 32 features and all M
 // rows, so the per-feature reductions stay inside the workgroup (fixed order, double accum).
+// Rows are processed in unrolled blocks of 8 so that 24 independent loads are in flight.
 __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict__ bd) {
   __shared__ double s_a[8][32], s_b[8][32];
   const int M = bd->M, F = bd->F;
   const int fl = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int f = blockIdx.x * 32 + fl;
   const bool fok = f < F;
+  const int fc = min(f, F - 1);
   const float sl = bd->slope;
-  const float mean = fok ? bd->mean[f] : 0.f;
-  const float invstd = fok ? bd->invstd[f] : 0.f;
+  const float mean = gld(bd->mean + fc);
+  const float invstd = gld(bd->invstd + fc);
+  const float* dA = bd->dA + fc;
+  const float* post = bd->post + fc;
+  const float* Y = bd->Y + fc;
+  const long lda = bd->ld_da, ldp = bd->ld_post, ldy = bd->ld_y;
   double sum = 0.0, dotp = 0.0;
-  if (fok) {
-    for (int r = rg; r < M; r += 8) {
-      const float da = bd->dA[(long)r * bd->ld_da + f];
-      const float po = bd->post[(long)r * bd->ld_post + f];
-      const float dy = po > 0.f ? da : da * sl;
-      const float y = bd->Y[(long)r * bd->ld_y + f];
-      sum += (double)dy;
-      dotp += (double)((y - mean) * dy);
+  for (int r0 = rg; r0 < M; r0 += 64) {
+    float da[8], po[8], y[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = min(r0 + 8 * j, M - 1);
+      da[j] = gld(dA + r * lda);
+      po[j] = gld(post + r * ldp);
+      y[j] = gld(Y + r * ldy);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (r0 + 8 * j < M) {
+        const float dy = po[j] > 0.f ? da[j] : da[j] * sl;
+        sum += (double)dy;
+        dotp += (double)((y[j] - mean) * dy);
+      }
     }
   }
   s_a[rg][fl] = sum;
@@ -149,20 +185,33 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
     D += s_b[q][fl];
   }
   if (!fok) return;
-  const float w = bd->gamma[f];
+  const float w = gld(bd->gamma + f);
   const float k = (float)D * invstd * invstd / M;
   const float gmean = (float)(S / M);
-  for (int r = rg; r < M; r += 8) {
-    const float da = bd->dA[(long)r * bd->ld_da + f];
-    const float po = bd->post[(long)r * bd->ld_post + f];
-    const float dy = po > 0.f ? da : da * sl;
-    const float y = bd->Y[(long)r * bd->ld_y + f];
-    const float gi = (y - mean) * k;
-    bd->dZ[(long)r * bd->ld_dz + f] = (dy - gmean - gi) * invstd * w;
+  float* dZ = bd->dZ + f;
+  const long ldz = bd->ld_dz;
+  for (int r0 = rg; r0 < M; r0 += 64) {
+    float da[8], po[8], y[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = min(r0 + 8 * j, M - 1);
+      da[j] = gld(dA + r * lda);
+      po[j] = gld(post + r * ldp);
+      y[j] = gld(Y + r * ldy);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = r0 + 8 * j;
+      if (r < M) {
+        const float dy = po[j] > 0.f ? da[j] : da[j] * sl;
+        const float gi = (y[j] - mean) * k;
+        gst(dZ + r * ldz, (dy - gmean - gi) * invstd * w);
+      }
+    }
   }
   if (rg == 0) {
-    bd->g_gamma[f] = (float)(D * (double)invstd);
-    bd->g_beta[f] = (float)S;
+    gst(bd->g_gamma + f, (float)(D * (double)invstd));
+    gst(bd->g_beta + f, (float)S);
   }
 }
 
@@ -216,16 +265,16 @@ __device__ void cgl_weights(int mode, int N, float lam, const float* beta, const
 
 __global__ __launch_bounds__(256) void cgl_adam(CglAdamArgs a, CglStepState* st, int tail) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const float ss = *a.step_size, bc = *a.bc2sqrt;
+  const float ss = gld(a.step_size), bc = gld(a.bc2sqrt);
   const float w1 = a.w1, w2 = a.w2;
   if (i < a.n) {
-    const float g = a.g[i];
-    const float m = cgl_lerp(a.m[i], g, w1);
-    const float v = __fadd_rn(__fmul_rn(a.v[i], a.b2), __fmul_rn(__fmul_rn(w2, g), g));
-    a.m[i] = m;
-    a.v[i] = v;
+    const float g = gld(a.g + i);
+    const float m = cgl_lerp(gld(a.m + i), g, w1);
+    const float v = __fadd_rn(__fmul_rn(gld(a.v + i), a.b2), __fmul_rn(__fmul_rn(w2, g), g));
+    gst(a.m + i, m);
+    gst(a.v + i, v);
     const float denom = sqrtf(v) / bc + a.eps;
-    a.p[i] = a.p[i] + (-ss) * m / denom;
+    gst(a.p + i, gld(a.p + i) + (-ss) * m / denom);
   }
   if (tail && i == 0) {
     // scalar tail of Server.train: F_max and the lambda update (after every parameter read

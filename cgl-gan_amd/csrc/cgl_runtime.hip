@@ -81,6 +81,7 @@ int validate(const cgl_gan_config* c) {
   const int C = d.dims[d.n_layers];
   if (c->loss == CGL_LOSS_CE2 && C != 2) return CGL_E_ARG;
   if (c->loss == CGL_LOSS_BCE && C != 1) return CGL_E_ARG;
+  if (d.dims[d.n_layers - 1] % 4 != 0) return CGL_E_ARG;  // loss head reads 16-byte vectors
   if (c->loss != CGL_LOSS_CE2 && c->loss != CGL_LOSS_BCE) return CGL_E_ARG;
   if (c->batch < 2 || c->batch_real < 1 || c->epoch < 1 || c->epoch > CGL_MAX_EPOCH) return CGL_E_ARG;
   if (c->n_workers < 1 || c->n_workers > CGL_MAX_WORKERS || c->rank < 0 || c->rank >= c->n_workers)
