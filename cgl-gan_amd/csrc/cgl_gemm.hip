@@ -14,12 +14,13 @@
 //    32x32x2 fragment is permuted so that lane half h owns 8 CONSECUTIVE k of every 16-k
 //    chunk: a k-contiguous operand is then two float4 loads per lane per 8 MFMAs;
 //  * prologue fusion: the A operand can be the pre-BatchNorm output of the previous layer;
-//    the workgroup reduces the producer's {sum, M2} partials into a per-feature scale/shift
-//    table in LDS and applies BatchNorm1d(train) + LeakyReLU while loading (the reference's
-//    BN/LeakyReLU kernels disappear), optionally writing the transformed rows out once;
+//    the workgroup stages the producer's per-feature scale/shift table in LDS and applies
+//    BatchNorm1d(train) + LeakyReLU while loading (the reference's BN/LeakyReLU kernels
+//    disappear), optionally writing the transformed rows out once;
 //  * epilogue fusion: bias, LeakyReLU / Tanh, LeakyReLU' mask, Tanh' (1 - t^2), the
 //    bias-gradient column (B's extra all-ones column), and per-column {sum, M2} partials of
-//    the stored output for the next layer's BatchNorm, grouped per forward call.
+//    the stored output for the next layer's BatchNorm, grouped per forward call; the last
+//    workgroup of each column tile combines them into the scale/shift table (cgl_bn_finalize).
 #include "cgl_internal.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -117,9 +118,273 @@ __device__ void cgl_bn_group_stats(const CglBnFwd& bn, int K, int k, int g, doub
   m2 = q;
 }
 
+// Last-arriver BatchNorm finalize of one column tile of a producer GEMM.  Every workgroup of
+// the column tile publishes its partials (agent-scope release: the workgroups of a launch span
+// all 8 XCDs and their L2s), then takes a ticket; the last one combines the partials of every
+// row tile in a fixed order (so the result does not depend on which workgroup is last) into
+//   scale = gamma * invstd, shift = beta - mean * scale  per (group, feature),
+// the saved mean / invstd for the backward pass and the running statistics, updated group by
+// group in the order of the reference's forward calls (Xd then Xg, capgan.py:215-220).
+__device__ void cgl_bn_finalize(const CglGemmDesc* __restrict__ d, int tn) {
+  __shared__ int s_last;
+  __shared__ double s_mean[2][64], s_m2[2][64];
+  __shared__ int s_n[2];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned int ticket =
+        __hip_atomic_fetch_add(d->stat_cnt + tn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (ticket == (unsigned int)d->tiles_m - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const CglBnFwd& bn = d->bn;
+  const int N = d->N;
+  const int ncol = 32 * d->WN;
+  const int c0 = tn * ncol;
+  const int ngroups = (bn.mtot + bn.gr - 1) / bn.gr;   // <= 2
+  const int tid = threadIdx.x;
+  for (int p = tid; p < ngroups * ncol; p += CGL_GEMM_THREADS) {
+    const int g = p / ncol, c = p % ncol, k = c0 + c;
+    if (k < N) {
+      double mean, m2;
+      int n;
+      cgl_bn_group_stats(bn, N, k, g, mean, m2, n);
+      s_mean[g][c] = mean;
+      s_m2[g][c] = m2;
+      if (c == 0) s_n[g] = n;
+      const double invstd = 1.0 / sqrt(m2 / n + bn.eps);
+      const float sc = (float)invstd * gld(bn.gamma + k);
+      const float sh = gld(bn.beta + k) - (float)mean * sc;
+      gst(d->stat_tab + ((long)g * N + k) * 2, sc);
+      gst(d->stat_tab + ((long)g * N + k) * 2 + 1, sh);
+      if (bn.save_mean) {
+        gst(bn.save_mean + (long)g * N + k, (float)mean);
+        gst(bn.save_invstd + (long)g * N + k, (float)invstd);
+      }
+    }
+  }
+  __syncthreads();
+  if (bn.run_mean && tid < ncol && c0 + tid < N) {
+    const int k = c0 + tid;
+    const double mom = bn.momentum;
+    float rm = gld(bn.run_mean + k), rv = gld(bn.run_var + k);
+    for (int g = 0; g < ngroups; ++g) {
+      rm = (float)(mom * s_mean[g][tid] + (1.0 - mom) * (double)rm);
+      rv = (float)(mom * (s_m2[g][tid] / (s_n[g] - 1)) + (1.0 - mom) * (double)rv);
+    }
+    gst(bn.run_mean + k, rm);
+    gst(bn.run_var + k, rv);
+  }
+  if (tid == 0) __hip_atomic_store(d->stat_cnt + tn, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------------------------------
+// LDS-staged main loop (PIPE == 1).
+//
+// Each k-group of WM x WN waves stages 32-deep k slices of its A panel (32*WM rows) and B panel
+// (32*WN columns) through LDS, double buffered: the coalesced global loads of slice s+1
+// (every wave-instruction reads whole 128-byte rows: 8 rows x 128 B for a k-contiguous operand)
+// are in flight while slice s is consumed from LDS, and each element is loaded once per
+// workgroup instead of once per wave that needs it.
+//   k-contiguous panel ([row][k], A of NT/NN and B of NT): rows padded to 36 floats, so the
+//     fragment reads (ds_read_b128 of 4 consecutive k for 32 rows) are bank-conflict free;
+//   mn-contiguous panel ([k][col], A of TN, B of NN/TN): rows of 32*W floats, fragment reads are
+//     ds_read_b32 of 32 consecutive columns (conflict free).
+// Tails (rows >= M, cols >= N, k >= K) are zero-filled at staging, so the MFMAs need no masks.
+// The BatchNorm+LeakyReLU transform of A and its copy-out are applied once, at staging.
+constexpr int CGL_BK = 32;
+constexpr int CGL_LDK = 36;
+
+__device__ __forceinline__ int cgl_lds_stage_floats(int WM, int WN) { return (32 * WM + 32 * WN) * CGL_LDK; }
+
 template <int LAYOUT, int VEC>
+__device__ __forceinline__ void cgl_mainloop_lds(const CglGemmDesc* __restrict__ d, f32x16& acc,
+                                                 const float* __restrict__ s_tf, float* __restrict__ s_stage,
+                                                 int M, int N, int K, int nmem, int b_ones, int WM, int WN, int WK,
+                                                 int wk, int wmn, int wm, int wn, int tm, int tn, int lane, int g0,
+                                                 int a_tf) {
+  const int gw = WM * WN;
+  const int BMr = 32 * WM, BNr = 32 * WN;
+  const int a_fl = BMr * CGL_LDK;
+  const int stage_fl = cgl_lds_stage_floats(WM, WN);
+  float* __restrict__ grp = s_stage + wk * 2 * stage_fl;
+  const int nst = (K + CGL_BK - 1) / CGL_BK;
+  const int nsg = (nst + WK - 1) / WK;
+  const int sb = (wk * nst) / WK, cnt = ((wk + 1) * nst) / WK - sb;
+  const int ninst = (4 * WM + 4 * WN) / gw;  // staging wave-instructions per wave per slice (4..8)
+  const int arow0 = tm * BMr;                 // first A row (kc) / column (mn) of the panel
+  const int bcol0 = tn * BNr;                 // first B row (NT) / column (NN, TN) of the panel
+  const int li = lane & 31, lh = lane >> 5;
+  const float slope_tf = d->tf_slope;
+  const int gr = a_tf ? d->tf_gr : 1;
+  float* __restrict__ a_copy = (LAYOUT != 2 && tn == 0) ? d->a_copy : nullptr;
+  const int a_copy_ld = d->a_copy_ld, a_copy_row0 = d->a_copy_row0;
+  const int lda = d->a.ld, ldb = d->b.ld;
+
+  f32x4 rg[8];  // staging registers (ninst <= 8)
+
+  // address of staging instruction q of this wave for slice s; fills rg[q]
+  auto stage_load = [&](int s, int q) {
+    const int t = wmn + q * gw;
+    const bool isA = t < 4 * WM;
+    const int u = isA ? t : t - 4 * WM;
+    const bool kc = isA ? (LAYOUT != 2) : (LAYOUT == 0);
+    f32x4 v;
+    if (kc) {
+      const int lrow = 8 * u + (lane >> 3);
+      const int k = s * CGL_BK + 4 * (lane & 7);
+      const int nrows = isA ? M : N;
+      const int grow = min((isA ? arow0 : bcol0) + lrow, nrows - 1);
+      const float* rp = cgl_row(isA ? d->a : d->b, grow);
+      if (VEC) {
+        v = *(gcf4p)(rp + min(k, K - 4));
+      } else {
+        gcfp g = (gcfp)rp;
+        v = f32x4{g[min(k, K - 1)], g[min(k + 1, K - 1)], g[min(k + 2, K - 1)], g[min(k + 3, K - 1)]};
+      }
+    } else {
+      const int R = isA ? BMr : BNr;
+      const int lpr = R >> 2;                 // lanes per k-row
+      const int rpi = 64 / lpr;               // k-rows per instruction
+      const int kl = u * rpi + lane / lpr;
+      const int col = (isA ? arow0 : bcol0) + 4 * (lane % lpr);
+      const int ncols = isA ? M : nmem;
+      const int k = min(s * CGL_BK + kl, K - 1);
+      const float* base = (isA ? d->a.p0 : d->b.p0) + (long)k * (isA ? lda : ldb);
+      if (VEC && ncols >= 4) {
+        v = *(gcf4p)(base + min(col, ncols - 4));
+      } else {
+        gcfp g = (gcfp)base;
+        const int cm = max(ncols - 1, 0);
+        v = f32x4{g[min(col, cm)], g[min(col + 1, cm)], g[min(col + 2, cm)], g[min(col + 3, cm)]};
+      }
+    }
+    rg[q] = v;
+  };
+
+  // mask / transform / copy-out, then write rg[q] into LDS buffer `buf`
+  auto stage_store = [&](int s, int q, float* buf) {
+    const int t = wmn + q * gw;
+    const bool isA = t < 4 * WM;
+    const int u = isA ? t : t - 4 * WM;
+    const bool kc = isA ? (LAYOUT != 2) : (LAYOUT == 0);
+    f32x4 v = rg[q];
+    if (kc) {
+      const int lrow = 8 * u + (lane >> 3);
+      const int k = s * CGL_BK + 4 * (lane & 7);
+      const int nrows = isA ? M : N;
+      const int growu = (isA ? arow0 : bcol0) + lrow;
+      const bool rok = growu < nrows;
+      if (isA && a_tf) {
+        const int gsel = rok ? growu / gr - g0 : 0;
+        const float* tb = s_tf + (gsel * CGL_TF_MAXK) * 2;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int kk = min(k + j, K - 1);
+          const float x = fmaf(v[j], tb[kk * 2 + 0], tb[kk * 2 + 1]);
+          v[j] = x > 0.f ? x : x * slope_tf;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (rok && k + j < K) ? v[j] : 0.f;
+      if (isA && a_copy && rok && growu >= a_copy_row0) {
+        float* dst = a_copy + (long)growu * a_copy_ld + k;
+        if (VEC && k + 3 < K) {
+          *(gf4p)dst = v;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (k + j < K) gst(dst + j, v[j]);
+        }
+      }
+      *reinterpret_cast<f32x4*>(buf + (isA ? 0 : a_fl) + lrow * CGL_LDK + 4 * (lane & 7)) = v;
+    } else {
+      const int R = isA ? BMr : BNr;
+      const int lpr = R >> 2;
+      const int rpi = 64 / lpr;
+      const int kl = u * rpi + lane / lpr;
+      const int cl = 4 * (lane % lpr);
+      const int col = (isA ? arow0 : bcol0) + cl;
+      const int ncols = isA ? M : nmem;
+      const bool kok = s * CGL_BK + kl < K;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (kok && col + j < ncols) ? v[j] : 0.f;
+      *reinterpret_cast<f32x4*>(buf + (isA ? 0 : a_fl) + kl * R + cl) = v;
+    }
+  };
+
+  // fragments of sub-chunk j2 (16 k) from LDS buffer `buf`, then 8 MFMAs
+  auto compute = [&](int s, const float* buf) {
+#pragma unroll
+    for (int j2 = 0; j2 < 2; ++j2) {
+      float av[8], bv[8];
+      const int kq = 16 * j2 + 8 * lh;
+      if (LAYOUT != 2) {
+        const float* p = buf + (wm * 32 + li) * CGL_LDK + kq;
+        const f32x4 x = *reinterpret_cast<const f32x4*>(p);
+        const f32x4 y = *reinterpret_cast<const f32x4*>(p + 4);
+        av[0] = x[0]; av[1] = x[1]; av[2] = x[2]; av[3] = x[3];
+        av[4] = y[0]; av[5] = y[1]; av[6] = y[2]; av[7] = y[3];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) av[j] = buf[(kq + j) * BMr + wm * 32 + li];
+      }
+      const float* bb = buf + a_fl;
+      if (LAYOUT == 0) {
+        const float* p = bb + (wn * 32 + li) * CGL_LDK + kq;
+        const f32x4 x = *reinterpret_cast<const f32x4*>(p);
+        const f32x4 y = *reinterpret_cast<const f32x4*>(p + 4);
+        bv[0] = x[0]; bv[1] = x[1]; bv[2] = x[2]; bv[3] = x[3];
+        bv[4] = y[0]; bv[5] = y[1]; bv[6] = y[2]; bv[7] = y[3];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bv[j] = bb[(kq + j) * BNr + wn * 32 + li];
+        if (b_ones && bcol0 + wn * 32 + li == N - 1) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bv[j] = (s * CGL_BK + kq + j < K) ? 1.f : 0.f;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], bv[j], acc, 0, 0, 0);
+    }
+  };
+
+  // (staging loops are fully unrolled to 8 with a uniform predicate so rg[] stays in VGPRs)
+  // prologue: slice sb into buffer 0
+  if (cnt > 0) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q < ninst) stage_load(sb, q);
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q < ninst) stage_store(sb, q, grp);
+  }
+  __syncthreads();
+  for (int i = 0; i < nsg; ++i) {
+    float* cur = grp + (i & 1) * stage_fl;
+    float* nxt = grp + ((i + 1) & 1) * stage_fl;
+    const bool more = i + 1 < cnt;
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (q < ninst) stage_load(sb + i + 1, q);
+    }
+    if (i < cnt) compute(sb + i, cur);
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (q < ninst) stage_store(sb + i + 1, q, nxt);
+    }
+    __syncthreads();
+  }
+}
+
+template <int LAYOUT, int VEC, int PIPE>
 __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d, int bid, float* __restrict__ s_tf,
-                                              float* __restrict__ s_red, float* __restrict__ s_col) {
+                                              float* __restrict__ s_stage, float* __restrict__ s_col) {
+  float* __restrict__ s_red = s_stage;   // split-K partials reuse the staging region after the loop
   const int M = d->M, N = d->N, K = d->K;
   const int WN = d->WN, WK = d->WK, WM = d->WM;
   const int tid = threadIdx.x;
@@ -128,58 +393,51 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   const int li = lane & 31, lh = lane >> 5;
   const int wk = wave % WK, wmn = wave / WK;
   const int wm = wmn / WN, wn = wmn % WN;
+  // XCD-aware tile order (blocks b and b+8 land on the same XCD): each XCD takes a contiguous
+  // range of tiles in n-major order, so its L2 holds ~1/8 of the B panels (the weights) plus
+  // the A panels, instead of all of both.  Bijective for any tile count (guide T1).
   const int local = bid - d->wg_begin;
-  const int tm = local / d->tiles_n, tn = local % d->tiles_n;
+  const int nwg = d->tiles_m * d->tiles_n;
+  int tile = local;
+  if (nwg >= 16) {
+    const int xcd = local & 7, pos = local >> 3, q = nwg >> 3, r = nwg & 7;
+    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+  }
+  const int tn = tile / d->tiles_m, tm = tile % d->tiles_m;
   const int BM = 32 * WM;
   const int m0 = tm * BM + wm * 32;
   const int n0 = (tn * WN + wn) * 32;
 
-  // ---------------- BatchNorm prologue: scale/shift table for the groups of this row tile
+  // ---------------- BatchNorm prologue: scale/shift pairs of the groups of this row tile
+  // (finalized by the last workgroups of the producer GEMM)
   const int a_tf = (LAYOUT != 2) ? d->a_tf : 0;
   int g0 = 0;
   if (a_tf) {
-    const CglBnFwd& bn = d->bn;
     const int rlast = min(tm * BM + BM, M) - 1;
-    g0 = (tm * BM) / bn.gr;
-    const int g1 = rlast / bn.gr;
-    for (int k = tid; k < K; k += CGL_GEMM_THREADS) {
-      for (int g = g0; g <= g1; ++g) {
-        double mean, m2;
-        int n;
-        cgl_bn_group_stats(bn, K, k, g, mean, m2, n);
-        const double invstd = 1.0 / sqrt(m2 / n + bn.eps);
-        const float sc = (float)invstd * gld(bn.gamma + k);
-        const float sh = gld(bn.beta + k) - (float)mean * sc;
-        s_tf[((g - g0) * CGL_TF_MAXK + k) * 2 + 0] = sc;
-        s_tf[((g - g0) * CGL_TF_MAXK + k) * 2 + 1] = sh;
-      }
-    }
-    if (local == 0 && (bn.run_mean || bn.save_mean)) {
-      // running statistics: every forward call (group) in order, like the reference's
-      // sequential Xd-then-Xg calls (capgan.py:215-220).
-      const int ngroups = (bn.mtot + bn.gr - 1) / bn.gr;
-      for (int k = tid; k < K; k += CGL_GEMM_THREADS) {
-        for (int g = 0; g < ngroups; ++g) {
-          double mean, m2;
-          int n;
-          cgl_bn_group_stats(bn, K, k, g, mean, m2, n);
-          if (bn.run_mean) {
-            const double mom = bn.momentum;
-            gst(bn.run_mean + k, (float)(mom * mean + (1.0 - mom) * (double)gld(bn.run_mean + k)));
-            const double unb = m2 / (n - 1);
-            gst(bn.run_var + k, (float)(mom * unb + (1.0 - mom) * (double)gld(bn.run_var + k)));
-          }
-          if (bn.save_mean) {
-            gst(bn.save_mean + (long)g * K + k, (float)mean);
-            gst(bn.save_invstd + (long)g * K + k, (float)(1.0 / sqrt(m2 / n + bn.eps)));
-          }
-        }
+    g0 = (tm * BM) / d->tf_gr;
+    const int g1 = rlast / d->tf_gr;
+    for (int g = g0; g <= g1; ++g) {
+      const float* src = d->tf_tab + (long)g * K * 2;
+      float* dst = s_tf + (g - g0) * CGL_TF_MAXK * 2;
+      for (int k2 = tid; k2 < K; k2 += CGL_GEMM_THREADS) {
+        dst[2 * k2] = gld(src + 2 * k2);
+        dst[2 * k2 + 1] = gld(src + 2 * k2 + 1);
       }
     }
     __syncthreads();
   }
 
   // ---------------- main loop
+  const int b_ones = (LAYOUT != 0) ? d->b_ones_col : 0;
+  const int nmem = N - b_ones;     // columns of B actually in memory
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+
+  if constexpr (PIPE == 1) {
+    cgl_mainloop_lds<LAYOUT, VEC>(d, acc, s_tf, s_stage, M, N, K, nmem, b_ones, WM, WN, WK, wk, wmn, wm, wn, tm, tn,
+                                  lane, g0, a_tf);
+  } else {
   const int nch = (K + CGL_GEMM_KCHUNK - 1) / CGL_GEMM_KCHUNK;
   const int cb = (wk * nch) / WK, ce = ((wk + 1) * nch) / WK;
 
@@ -187,8 +445,6 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   const int am = m0 + li;          // A row (kc) or A column (mn)
   const int bn_ = n0 + li;         // B row (NT) or B column (NN/TN)
   const bool a_ok = am < M;
-  const int b_ones = (LAYOUT != 0) ? d->b_ones_col : 0;
-  const int nmem = N - b_ones;     // columns of B actually in memory
   const bool b_ok = bn_ < nmem;
   const bool b_is_ones = b_ones && (bn_ == N - 1);
   // clamped (always dereferenceable) operand bases
@@ -196,14 +452,10 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   const float* __restrict__ b_base =
       (LAYOUT == 0) ? cgl_row(d->b, min(bn_, N - 1)) : d->b.p0 + max(0, min(bn_, nmem - 1));
   const int lda = d->a.ld, ldb = d->b.ld;
-  const int gsel = a_tf ? (a_ok ? am / d->bn.gr - g0 : 0) : 0;
-  const float slope_tf = d->bn.slope;
+  const int gsel = a_tf ? (a_ok ? am / d->tf_gr - g0 : 0) : 0;
+  const float slope_tf = d->tf_slope;
   float* __restrict__ a_copy = d->a_copy;
   const bool do_copy = (LAYOUT != 2) && a_copy && tn == 0 && wn == 0 && a_ok && am >= d->a_copy_row0;
-
-  f32x16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 
   auto load_chunk = [&](int c, float* A_, float* B_) {
     const int k = c * CGL_GEMM_KCHUNK + 8 * lh;
@@ -249,18 +501,23 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A_[j], B_[j], acc, 0, 0, 0);
   };
 
-  // two register sets in ping-pong: the loads of chunk c+1 are in flight while chunk c's MFMAs
-  // run, and no register copy forces an early wait.  Tail loads are clamped re-loads.
+  // three register sets in rotation: the loads of chunks c+1 and c+2 are in flight while chunk
+  // c's MFMAs run (~2 x 512 MFMA cycles of cover for an L2/MALL miss), and no register copy
+  // forces an early wait.  Tail loads are clamped re-loads.
   if (cb < ce) {
-    float xa[8], xb[8], ya[8], yb[8];
+    float xa[8], xb[8], ya[8], yb[8], za[8], zb[8];
     load_chunk(cb, xa, xb);
-    for (int c = cb; c < ce; c += 2) {
-      load_chunk(min(c + 1, ce - 1), ya, yb);
+    load_chunk(min(cb + 1, ce - 1), ya, yb);
+    for (int c = cb; c < ce; c += 3) {
+      load_chunk(min(c + 2, ce - 1), za, zb);
       compute_chunk(c, xa, xb);
-      load_chunk(min(c + 2, ce - 1), xa, xb);
+      load_chunk(min(c + 3, ce - 1), xa, xb);
       if (c + 1 < ce) compute_chunk(c + 1, ya, yb);
+      load_chunk(min(c + 4, ce - 1), ya, yb);
+      if (c + 2 < ce) compute_chunk(c + 2, za, zb);
     }
   }
+  }  // PIPE == 0
 
   // ---------------- split-K reduction (fixed order: wk = 1, 2, 3)
   if (WK > 1) {
@@ -379,6 +636,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
         gst(p + 1, part[s][1]);
       }
     }
+    if (d->stat_tab) cgl_bn_finalize(d, tn);
   }
 
   if (owner && colok) {
@@ -404,29 +662,49 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 
 // One kernel symbol for every GEMM of the step; a grouped launch may mix layouts (e.g. the
 // weight gradient (TN) and the input gradient (NN) of one layer run side by side).
-__global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDesc* __restrict__ descs, int ndesc) {
-  __shared__ float s_tf[2 * CGL_TF_MAXK * 2];   // BatchNorm scale/shift per (group, k)
-  __shared__ float s_red[3 * 16 * 64];          // split-K partial accumulators
+// Dynamic LDS: [tf_floats: BatchNorm scale/shift table (0 when no problem of the launch needs it)]
+//              [staging slices of every k-group, reused for the split-K partials after the loop]
+__global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDesc* __restrict__ descs, int ndesc,
+                                                                 int tf_floats) {
+  extern __shared__ float cgl_dyn_lds[];
   __shared__ float s_col[4 * 32 * 2];           // per-column reductions across waves
+  float* s_tf = cgl_dyn_lds;
+  float* s_stage = cgl_dyn_lds + tf_floats;
   const int bid = blockIdx.x;
   int di = 0;
   for (int q = 1; q < ndesc; ++q)
     if (bid >= descs[q].wg_begin) di = q;
   const CglGemmDesc* __restrict__ d = descs + di;
   const int layout = d->layout;
-  // VEC: every k-contiguous operand allows 16-byte loads (K % 4 == 0, aligned rows)
-  const int vec = layout == 0 ? (d->a_vec && d->b_vec) : d->a_vec;
-  if (layout == 0) {
-    if (vec)
-      cgl_gemm_body<0, 1>(d, bid, s_tf, s_red, s_col);
-    else
-      cgl_gemm_body<0, 0>(d, bid, s_tf, s_red, s_col);
-  } else if (layout == 1) {
-    if (vec)
-      cgl_gemm_body<1, 1>(d, bid, s_tf, s_red, s_col);
-    else
-      cgl_gemm_body<1, 0>(d, bid, s_tf, s_red, s_col);
-  } else {
-    cgl_gemm_body<2, 0>(d, bid, s_tf, s_red, s_col);
-  }
+  // VEC: every operand allows 16-byte loads along its contiguous dimension
+  const int vec = d->a_vec && d->b_vec;
+  const int pipe = d->pipe;
+#define CGL_BODY(L)                                             \
+  do {                                                          \
+    if (pipe) {                                                 \
+      if (vec)                                                  \
+        cgl_gemm_body<L, 1, 1>(d, bid, s_tf, s_stage, s_col);   \
+      else                                                      \
+        cgl_gemm_body<L, 0, 1>(d, bid, s_tf, s_stage, s_col);   \
+    } else {                                                    \
+      if (vec)                                                  \
+        cgl_gemm_body<L, 1, 0>(d, bid, s_tf, s_stage, s_col);   \
+      else                                                      \
+        cgl_gemm_body<L, 0, 0>(d, bid, s_tf, s_stage, s_col);   \
+    }                                                           \
+  } while (0)
+  if (layout == 0)
+    CGL_BODY(0);
+  else if (layout == 1)
+    CGL_BODY(1);
+  else
+    CGL_BODY(2);
+#undef CGL_BODY
+}
+
+// Host helper: dynamic LDS bytes of one problem (staging or split-K region; the table is extra).
+inline int cgl_gemm_stage_bytes(const CglGemmDesc& d) {
+  const int red = 3 * 16 * 64 * 4;
+  const int st = d.pipe ? d.WK * 2 * (32 * d.WM + 32 * d.WN) * CGL_LDK * 4 : 0;
+  return st > red ? st : red;
 }

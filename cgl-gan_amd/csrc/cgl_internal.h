@@ -37,8 +37,10 @@ struct CglRowSrc {
   int ld;                 // row stride in floats (both segments)
 };
 
-// Forward-BatchNorm transform applied to the A operand as it is loaded (consumer side).
-// The producer GEMM wrote per-(row tile, group slot, feature) partials {sum, M2}.
+// Forward-BatchNorm statistics of a producer GEMM's output.  Every workgroup writes per-(row
+// tile, group slot, feature) partials {sum, M2}; the last workgroup to finish a column tile
+// combines them (fixed order, double) into the per-group scale/shift table the consumer GEMM
+// applies to its A operand, the saved mean/invstd of the backward pass and the running stats.
 struct CglBnFwd {
   const float* part;      // [ntiles][2][K][2]
   int part_bm;            // producer rows per tile
@@ -60,12 +62,15 @@ struct CglGemmDesc {
   int tiles_m, tiles_n;
   int wg_begin;           // first workgroup of this problem in a grouped launch
   int layout;             // 0: NT (A[m][k], B[n][k]); 1: NN (A[m][k], B[k][n]); 2: TN (A[k][m], B[k][n])
-  int a_vec, b_vec;       // 16-byte vector loads allowed along k (kc operands)
+  int a_vec, b_vec;       // 16-byte vector loads allowed along each operand's contiguous dim
+  int pipe;               // 0: direct-to-register fragment loads; 1: LDS-staged slices
   CglRowSrc a, b;
   // A transform (kc A only)
-  int a_tf;               // 0 none, 1 BatchNorm+LeakyReLU from producer partials
-  CglBnFwd bn;
-  float* a_copy;          // optional copy-out of the (transformed) A rows; rows >= a_copy_row0
+  int a_tf;               // 0 none, 1 BatchNorm+LeakyReLU through the producer's table
+  const float* tf_tab;    // [ngroups][K][2] {scale, shift}
+  int tf_gr;              // rows per BatchNorm group
+  float tf_slope;
+  float* a_copy;         // optional copy-out of the (transformed) A rows; rows >= a_copy_row0
   int a_copy_ld, a_copy_row0;
   // B extras
   int b_ones_col;         // logical column N-1 of B is all ones (bias-gradient trick)
@@ -76,7 +81,10 @@ struct CglGemmDesc {
   const float* mask_ref; int mask_ld;     // v *= (ref > 0 ? 1 : slope)
   const float* tanh_ref; int tanh_ld;     // v *= 1 - t*t
   float* stat_part; int stat_gr;          // forward BatchNorm partials of the stored output
-  float* bias_out;                        // with b_ones_col: column N-1 of C goes here
+  CglBnFwd bn;                            // with stat_part: finalize by the last workgroup per column tile
+  float* stat_tab;                        // [ngroups][N][2] scale/shift output
+  unsigned int* stat_cnt;                 // [tiles_n] arrival tickets (zero at rest)
+  float* bias_out;                     // with b_ones_col: column N-1 of C goes here
 };
 
 // D output layer + adversarial loss (+ its backward into the last hidden layer).

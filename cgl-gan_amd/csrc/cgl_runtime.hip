@@ -111,6 +111,8 @@ constexpr int kMaxGemmDescs = 128;
 constexpr int kMaxHeadDescs = 2 * CGL_MAX_EPOCH + 4;
 constexpr int kMaxBnDescs = 2 * CGL_MAX_LAYERS;
 constexpr int kHeadRows = 16;
+constexpr int kBnCounter0 = 64;   // first BatchNorm ticket (64 per G layer)
+constexpr int kCounters = kBnCounter0 + 64 * CGL_MAX_LAYERS;
 
 struct WS {
   // G forward (2B rows)
@@ -133,7 +135,8 @@ struct WS {
   float* gG[CGL_MAX_LAYERS];
   // misc
   float* hpart;
-  unsigned int* counters;
+  unsigned int* counters;   // [kCounters]: head-loss tickets, then BatchNorm column-tile tickets
+  float* gtab[CGL_MAX_LAYERS];  // BatchNorm scale/shift table [2][f][2] of G layer l's output
   CglStepState* st;
   int* idx;       // sampler output when sample_n > 0
   CglGemmDesc* gemm;
@@ -150,7 +153,7 @@ WS carve_ws(const cgl_gan_config& c, void* base) {
   const int L = g.n_layers, J = d.n_layers;
   const int B = c.batch, Md = c.batch_real + c.batch;
   w.st = cv.take<CglStepState>(1);
-  w.counters = cv.take<unsigned int>(64);
+  w.counters = cv.take<unsigned int>(kCounters);
   w.gemm = cv.take<CglGemmDesc>(kMaxGemmDescs);
   w.head = cv.take<CglHeadDesc>(kMaxHeadDescs);
   w.bnb = cv.take<CglBnBwdDesc>(kMaxBnDescs);
@@ -162,6 +165,7 @@ WS carve_ws(const cgl_gan_config& c, void* base) {
       const int64_t tiles = (2 * B + 31) / 32;
       w.gpart[l] = cv.take<float>(tiles * 2 * f * 2);
       w.gmean[l] = cv.take<float>((int64_t)2 * f);
+      w.gtab[l] = cv.take<float>((int64_t)2 * f * 2);
       w.ginvstd[l] = cv.take<float>((int64_t)2 * f);
       w.gdA[l] = cv.take<float>((int64_t)B * f);
     }
@@ -197,7 +201,36 @@ struct Launch {
   long nn = 0;
   int stream_id = 0;
   double flops = 0.0;
+  int shmem = 0;        // dynamic LDS bytes (GEMM)
+  int tf_floats = 0;    // BatchNorm-table floats at the head of the dynamic LDS (GEMM)
 };
+
+// The LDS-staged GEMM needs up to ~90 KB of dynamic LDS per workgroup (> the 64 KB default).
+hipError_t gemm_lds_attr() {
+  static bool done = false;
+  if (!done) {
+    // the attribute is advisory on this platform (launches up to the per-CU LDS succeed); try
+    // the largest accepted value and never fail on it
+    for (int kb : {159, 150, 128, 96, 64}) {
+      const hipError_t e =
+          hipFuncSetAttribute((const void*)cgl_gemm_f32, hipFuncAttributeMaxDynamicSharedMemorySize, kb * 1024);
+      (void)hipGetLastError();
+      if (e == hipSuccess) break;
+    }
+    done = true;
+  }
+  return hipSuccess;
+}
+
+// GEMM main-loop selection (0 direct fragment loads, 1 LDS-staged); CGL_GEMM_PIPE overrides.
+int gemm_pipe_default() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CGL_GEMM_PIPE");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
 
 void choose_tiles(CglGemmDesc& d, int force_wm = 0) {
   static const int opts[4][3] = {{2, 2, 1}, {2, 1, 2}, {1, 2, 2}, {1, 1, 4}};
@@ -232,8 +265,30 @@ CglGemmDesc make_gemm(int layout, int M, int N, int K) {
   d.b.split = 0x7fffffff;
   d.slope = 0.2f;
   d.act = CGL_EPI_ACT_NONE;
+  d.pipe = gemm_pipe_default();
   choose_tiles(d);
   return d;
+}
+
+inline bool al16p(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// 16-byte loads are legal for an operand when every row start is 16-byte aligned and the
+// contiguous extent is a multiple of 4 floats (k for k-contiguous operands, columns otherwise).
+void set_vec(CglGemmDesc& d) {
+  auto src_ok = [](const CglRowSrc& r) {
+    return (r.ld % 4 == 0) && al16p(r.p0) && (r.p1 == nullptr || al16p(r.p1));
+  };
+  const int nmem = d.N - (d.layout != 0 ? d.b_ones_col : 0);
+  if (d.layout == 0) {
+    d.a_vec = (d.K % 4 == 0) && src_ok(d.a);
+    d.b_vec = (d.K % 4 == 0) && src_ok(d.b);
+  } else if (d.layout == 1) {
+    d.a_vec = (d.K % 4 == 0) && src_ok(d.a);
+    d.b_vec = (nmem % 4 == 0) && src_ok(d.b);
+  } else {
+    d.a_vec = (d.M % 4 == 0) && src_ok(d.a);
+    d.b_vec = (nmem % 4 == 0) && src_ok(d.b);
+  }
 }
 
 CglRowSrc rows(const float* p, int ld) {
@@ -296,15 +351,20 @@ void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
   L.kind = K_GEMM;
   L.first = (int)c->gemm.size();
   L.count = (int)descs.size();
-  int wg = 0;
+  int wg = 0, stage = 0, tf = 0;
   for (auto& d : descs) {
+    set_vec(d);
     d.wg_begin = wg;
     wg += d.tiles_m * d.tiles_n;
     const int nalg = d.b_ones_col ? d.N - 1 : d.N;
     L.flops += 2.0 * d.M * (double)nalg * d.K;
+    stage = std::max(stage, cgl_gemm_stage_bytes(d));
+    if (d.a_tf) tf = 2 * CGL_TF_MAXK * 2;
     c->gemm.push_back(d);
   }
   L.grid = wg;
+  L.tf_floats = tf;
+  L.shmem = stage + tf * 4;
   ph.push_back(L);
 }
 
@@ -391,7 +451,6 @@ int build_plan(cgl_gan* c) {
   }
 
   // ---- G forward on [z1; z2] (2B rows; BatchNorm statistics per B-row forward call)
-  int bm_prod[CGL_MAX_LAYERS] = {0};
   for (int l = 0; l < L; ++l) {
     const int fi = g.dims[l], fo = g.dims[l + 1];
     CglGemmDesc e = make_gemm(0, 2 * B, fo, fi);
@@ -402,20 +461,9 @@ int build_plan(cgl_gan* c) {
       e.a = rows(w.gout[l - 1], fi);
       if (g.bn[l - 1]) {
         e.a_tf = 1;
-        CglBnFwd& bn = e.bn;
-        bn.part = w.gpart[l - 1];
-        bn.part_bm = bm_prod[l - 1];
-        bn.gr = B;
-        bn.mtot = 2 * B;
-        bn.gamma = gparam(c, l - 1, 2);
-        bn.beta = gparam(c, l - 1, 3);
-        bn.eps = cf.bn_eps;
-        bn.momentum = cf.bn_momentum;
-        bn.slope = sl;
-        bn.run_mean = c->bufs.g_running + c->run_mean_off[l - 1];
-        bn.run_var = c->bufs.g_running + c->run_var_off[l - 1];
-        bn.save_mean = w.gmean[l - 1];
-        bn.save_invstd = w.ginvstd[l - 1];
+        e.tf_tab = w.gtab[l - 1];
+        e.tf_gr = B;
+        e.tf_slope = sl;
         e.a_copy = w.gact[l - 1];
         e.a_copy_ld = fi;
         e.a_copy_row0 = B;
@@ -431,13 +479,28 @@ int build_plan(cgl_gan* c) {
       e.act = CGL_EPI_ACT_NONE;
       e.stat_part = w.gpart[l];
       e.stat_gr = B;
+      CglBnFwd& bn = e.bn;
+      bn.part = w.gpart[l];
+      bn.part_bm = 32 * e.WM;
+      bn.gr = B;
+      bn.mtot = 2 * B;
+      bn.gamma = gparam(c, l, 2);
+      bn.beta = gparam(c, l, 3);
+      bn.eps = cf.bn_eps;
+      bn.momentum = cf.bn_momentum;
+      bn.slope = sl;
+      bn.run_mean = c->bufs.g_running + c->run_mean_off[l];
+      bn.run_var = c->bufs.g_running + c->run_var_off[l];
+      bn.save_mean = w.gmean[l];
+      bn.save_invstd = w.ginvstd[l];
+      e.stat_tab = w.gtab[l];
+      e.stat_cnt = w.counters + kBnCounter0 + 64 * l;
     } else {
       e.act = CGL_EPI_ACT_LEAKY;
     }
     e.slope = sl;
     e.C = w.gout[l];
     e.ldc = fo;
-    bm_prod[l] = 32 * e.WM;
     push_gemm(c, A, {e});
   }
   const float* Xd = w.gout[L - 1];
@@ -736,7 +799,8 @@ __global__ void cgl_sample(int* idx, const CglStepState* st, int epoch, int br, 
 int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s) {
   switch (L.kind) {
     case K_GEMM:
-      hipLaunchKernelGGL(cgl_gemm_f32, dim3(L.grid), dim3(CGL_GEMM_THREADS), 0, s, c->ws.gemm + L.first, L.count);
+      hipLaunchKernelGGL(cgl_gemm_f32, dim3(L.grid), dim3(CGL_GEMM_THREADS), L.shmem, s, c->ws.gemm + L.first,
+                         L.count, L.tf_floats);
       break;
     case K_HEAD:
       hipLaunchKernelGGL(cgl_head_loss, dim3(L.grid), dim3(256), 0, s, c->ws.head + L.first);
@@ -839,6 +903,10 @@ int cgl_gan_create(const cgl_gan_config* cfg, const cgl_gan_buffers* bufs, cgl_g
   if (!al16(bufs->g_params) || !al16(bufs->d_params) || !al16(bufs->z) || !al16(bufs->workspace))
     return CGL_E_ARG;
 
+  {
+    const hipError_t ea = gemm_lds_attr();
+    if (ea != hipSuccess) return (int)ea;
+  }
   cgl_gan* c = new cgl_gan();
   c->cfg = *cfg;
   c->bufs = *bufs;
@@ -857,7 +925,7 @@ int cgl_gan_create(const cgl_gan_config* cfg, const cgl_gan_buffers* bufs, cgl_g
     he = hipMemcpy(c->ws.head, c->head.data(), c->head.size() * sizeof(CglHeadDesc), hipMemcpyHostToDevice);
   if (he == hipSuccess && !c->bnb.empty())
     he = hipMemcpy(c->ws.bnb, c->bnb.data(), c->bnb.size() * sizeof(CglBnBwdDesc), hipMemcpyHostToDevice);
-  if (he == hipSuccess) he = hipMemset(c->ws.counters, 0, 64 * sizeof(unsigned int));
+  if (he == hipSuccess) he = hipMemset(c->ws.counters, 0, kCounters * sizeof(unsigned int));
   if (he == hipSuccess) he = hipMemset(c->ws.st, 0, sizeof(CglStepState));
   if (he == hipSuccess) he = hipDeviceSynchronize();
   if (he != hipSuccess) {
@@ -888,7 +956,7 @@ int cgl_gan_reset(cgl_gan* c, const float* beta_host, void* stream) {
   for (int i = 0; i < c->cfg.n_workers; ++i) h.beta[i] = beta_host ? beta_host[i] : 1.f / c->cfg.n_workers;
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(hipMemcpyAsync(c->ws.st, &h, sizeof(h), hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemsetAsync(c->ws.counters, 0, 64 * sizeof(unsigned int), s));
+  HIPCHK(hipMemsetAsync(c->ws.counters, 0, kCounters * sizeof(unsigned int), s));
   HIPCHK(hipStreamSynchronize(s));
   return CGL_OK;
 }
@@ -1061,10 +1129,12 @@ int64_t cgl_op_workspace_bytes(void) { return 4096; }
 
 static int single_gemm(CglGemmDesc& d, void* ws, int64_t wsb, hipStream_t s) {
   if (!ws || wsb < (int64_t)sizeof(CglGemmDesc) || !al16(ws)) return CGL_E_ARG;
+  HIPCHK(gemm_lds_attr());
   d.wg_begin = 0;
+  set_vec(d);
   HIPCHK(hipMemcpyAsync(ws, &d, sizeof(d), hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(cgl_gemm_f32, dim3(d.tiles_m * d.tiles_n), dim3(CGL_GEMM_THREADS), 0, s,
-                     (const CglGemmDesc*)ws, 1);
+  hipLaunchKernelGGL(cgl_gemm_f32, dim3(d.tiles_m * d.tiles_n), dim3(CGL_GEMM_THREADS), cgl_gemm_stage_bytes(d), s,
+                     (const CglGemmDesc*)ws, 1, 0);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   // the descriptor lives in the caller's workspace: keep it alive until the kernel has read it

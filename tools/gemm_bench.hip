@@ -4,6 +4,7 @@
 // launches (hipEvent over 200 launches) and the achieved fp32 TFLOP/s.
 #include "../cgl-gan_amd/csrc/cgl_gemm.hip"
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -23,6 +24,64 @@ struct Shape {
   int layout, M, N, K;
 };
 
+__global__ void empty_kernel(int* p) {
+  if (p && threadIdx.x == 9999) p[0] = 1;
+}
+
+static double time_desc(CglGemmDesc d, CglGemmDesc* dd, int reps) {
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipMemcpy(dd, &d, sizeof(d), hipMemcpyHostToDevice);
+  const int grid = d.tiles_m * d.tiles_n;
+  const int sh = cgl_gemm_stage_bytes(d);
+  for (int i = 0; i < 10; ++i) hipLaunchKernelGGL(cgl_gemm_f32, dim3(grid), dim3(256), sh, 0, dd, 1, 0);
+  (void)hipEventRecord(e0, 0);
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(cgl_gemm_f32, dim3(grid), dim3(256), sh, 0, dd, 1, 0);
+  (void)hipEventRecord(e1, 0);
+  (void)hipEventSynchronize(e1);
+  float ms;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  return ms * 1e3 / reps;
+}
+
+static void probes(float* A, float* B, float* C, float* bias, CglGemmDesc* dd, int reps) {
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  for (int grid : {1, 256, 1024}) {
+    for (int i = 0; i < 10; ++i) hipLaunchKernelGGL(empty_kernel, dim3(grid), dim3(256), 0, 0, (int*)nullptr);
+    (void)hipEventRecord(e0, 0);
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(empty_kernel, dim3(grid), dim3(256), 0, 0, (int*)nullptr);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    printf("probe empty kernel grid=%d: %.2f us/launch\n", grid, ms * 1e3 / reps);
+  }
+  // fixed tile count (NT 256x256 -> 64 WGs of (1,1,4)), growing K
+  for (int K : {16, 64, 256, 1024, 4096}) {
+    for (int wk : {1, 4}) {
+      CglGemmDesc d;
+      memset(&d, 0, sizeof(d));
+      d.layout = 0; d.M = 256; d.N = 256; d.K = K;
+      d.WM = 1; d.WN = (wk == 1) ? 4 : 1; d.WK = wk;
+      d.tiles_m = 8; d.tiles_n = (wk == 1) ? 2 : 8;
+      d.a.p0 = A; d.a.split = 0x7fffffff; d.a.ld = K;
+      d.b.p0 = B; d.b.split = 0x7fffffff; d.b.ld = K;
+      d.a_vec = d.b_vec = 1;
+      d.C = C; d.ldc = 256; d.slope = 0.2f;
+      d.pipe = 1;
+      const double us1 = time_desc(d, dd, reps);
+      d.pipe = 0;
+      const double us = time_desc(d, dd, reps);
+      printf("probe(LDS) NT 256x256 K=%5d WK=%d: %7.2f us (%.1f TF)\n", K, wk, us1, 2.0 * 256 * 256 * K / us1 * 1e-6);
+      printf("probe NT 256x256 K=%5d WK=%d WGs=%3d: %7.2f us  (%.1f TF, %d MFMA/wave)\n", K, wk,
+             d.tiles_m * d.tiles_n, us, 2.0 * 256 * 256 * K / us * 1e-6, (K / 16 / wk) * 8);
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 200;
   const Shape shapes[] = {
@@ -35,7 +94,15 @@ int main(int argc, char** argv) {
       {"G gW4", 2, 784, 1025, 256},  {"G gW3", 2, 1024, 513, 256},  {"G gW2", 2, 512, 257, 256},
       {"G gW1", 2, 256, 129, 256},   {"G gW0", 2, 128, 101, 256},
   };
-  const int cfgs[4][3] = {{2, 2, 1}, {2, 1, 2}, {1, 2, 2}, {1, 1, 4}};
+  const int cfgs[8][4] = {{2, 2, 1, 0}, {2, 1, 2, 0}, {1, 2, 2, 0}, {1, 1, 4, 0},
+                          {2, 2, 1, 1}, {2, 1, 2, 1}, {1, 2, 2, 1}, {1, 1, 4, 1}};
+  for (int kb : {160, 159, 150, 128, 96, 64}) {
+    const hipError_t e = hipFuncSetAttribute((const void*)cgl_gemm_f32, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             kb * 1024);
+    printf("hipFuncSetAttribute(MaxDynamicSharedMemorySize, %d KB): %s\n", kb, hipGetErrorString(e));
+    (void)hipGetLastError();
+    if (e == hipSuccess) break;
+  }
   const size_t big = 4u << 20;  // floats
   float *A, *B, *C, *bias;
   CK(hipMalloc(&A, big * 4));
@@ -52,9 +119,11 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
+  probes(A, B, C, bias, dd, reps);
+  if (argc > 2) return 0;
   double tot_best = 0, tot_flop = 0;
   printf("%-8s %-3s %5s %5s %5s |", "shape", "L", "M", "N", "K");
-  for (auto& c : cfgs) printf("  %d%d%d us  TF  |", c[0], c[1], c[2]);
+  for (auto& c : cfgs) printf(" %d%d%d%s us TF |", c[0], c[1], c[2], c[3] ? "L" : "d");
   printf(" best\n");
   for (const Shape& s : shapes) {
     printf("%-8s %-3d %5d %5d %5d |", s.name, s.layout, s.M, s.N, s.K);
@@ -71,6 +140,7 @@ int main(int argc, char** argv) {
       d.WK = c[2];
       d.tiles_m = (s.M + 32 * c[0] - 1) / (32 * c[0]);
       d.tiles_n = (s.N + 32 * c[1] - 1) / (32 * c[1]);
+      d.pipe = c[3];
       d.a.p0 = A;
       d.a.split = 0x7fffffff;
       d.b.p0 = B;
@@ -85,27 +155,41 @@ int main(int argc, char** argv) {
         d.a.ld = s.K;
         d.a_vec = (s.K % 4 == 0);
         d.b.ld = s.N;
+        d.b_vec = (s.N % 4 == 0);
       } else {
         d.a.ld = s.M;
         d.b.ld = s.N - 1;
+        d.a_vec = (s.M % 4 == 0);
+        d.b_vec = ((s.N - 1) % 4 == 0);
         d.b_ones_col = 1;
         d.bias_out = bias;
       }
       d.slope = 0.2f;
       d.C = C;
       d.ldc = s.layout == 2 ? s.N - 1 : s.N;
-      CK(hipMemcpy(dd, &d, sizeof(d), hipMemcpyHostToDevice));
-      const int grid = d.tiles_m * d.tiles_n;
-      for (int i = 0; i < 10; ++i) hipLaunchKernelGGL(cgl_gemm_f32, dim3(grid), dim3(256), 0, 0, dd, 1);
-      CK(hipEventRecord(e0, 0));
-      for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(cgl_gemm_f32, dim3(grid), dim3(256), 0, 0, dd, 1);
-      CK(hipEventRecord(e1, 0));
-      CK(hipEventSynchronize(e1));
-      float ms;
-      CK(hipEventElapsedTime(&ms, e0, e1));
-      const double us = ms * 1e3 / reps;
+      if (c[3] == 1) {  // verify against the direct path on the same inputs
+        const size_t n = (size_t)s.M * d.ldc;
+        std::vector<float> r0(n), r1(n);
+        CglGemmDesc d0 = d;
+        d0.pipe = 0;
+        CK(hipMemset(C, 0, n * 4));
+        (void)time_desc(d0, dd, 1);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(r0.data(), C, n * 4, hipMemcpyDeviceToHost));
+        CK(hipMemset(C, 0, n * 4));
+        (void)time_desc(d, dd, 1);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(r1.data(), C, n * 4, hipMemcpyDeviceToHost));
+        double num = 0, den = 0;
+        for (size_t i = 0; i < n; ++i) {
+          num += (double)(r1[i] - r0[i]) * (r1[i] - r0[i]);
+          den += (double)r0[i] * r0[i];
+        }
+        if (!(num <= 1e-10 * den)) printf(" [MISMATCH rel %.2e] ", sqrt(num / (den + 1e-30)));
+      }
+      const double us = time_desc(d, dd, reps);
       const double flop = 2.0 * s.M * s.N * s.K;
-      printf("  %6.2f %5.1f |", us, flop / us * 1e-6);
+      printf(" %6.2f %5.1f |", us, flop / us * 1e-6);
       if (us < best) best = us;
     }
     tot_best += best;
