@@ -14,13 +14,12 @@
 //    32x32x2 fragment is permuted so that lane half h owns 8 CONSECUTIVE k of every 16-k
 //    chunk: a k-contiguous operand is then two float4 loads per lane per 8 MFMAs;
 //  * prologue fusion: the A operand can be the pre-BatchNorm output of the previous layer;
-//    the workgroup stages the producer's per-feature scale/shift table in LDS and applies
+//    the workgroup combines the producer's {sum, M2} partials into a scale/shift table in LDS and applies
 //    BatchNorm1d(train) + LeakyReLU while loading (the reference's BN/LeakyReLU kernels
 //    disappear), optionally writing the transformed rows out once;
 //  * epilogue fusion: bias, LeakyReLU / Tanh, LeakyReLU' mask, Tanh' (1 - t^2), the
 //    bias-gradient column (B's extra all-ones column), and per-column {sum, M2} partials of
-//    the stored output for the next layer's BatchNorm, grouped per forward call; the last
-//    workgroup of each column tile combines them into the scale/shift table (cgl_bn_finalize).
+//    the stored output for the next layer's BatchNorm, grouped per forward call.
 #include "cgl_internal.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -70,114 +69,110 @@ __device__ __forceinline__ void cgl_mask(float v[8], bool ok, int k, int K) {
   for (int j = 0; j < 8; ++j) v[j] = (ok && k + j < K) ? v[j] : 0.f;
 }
 
-// Mean / biased variance of BatchNorm group g for feature k from the producer partials
-// (exact parallel combination of per-tile {sum, M2}, in double like torch's CPU kernel).
-__device__ void cgl_bn_group_stats(const CglBnFwd& bn, int K, int k, int g, double& mean, double& m2,
-                                   int& n) {
+// BatchNorm statistics of group g for Q features k[q] (k[q] < 0: unused) from the producer
+// partials: the exact parallel combination of per-tile {S_t, M2_t} over c_t rows, in double
+// like torch's CPU kernel and in a fixed tile order,
+//   mean = sum_t S_t / n,   M2 = sum_t (M2_t + c_t (S_t / c_t - mean)^2).
+// Fast path (<= 8 tiles per group): every {S_t, M2_t} pair of the Q features is loaded up front
+// as one 8-byte load, so the whole computation costs a single memory round trip.
+template <int Q>
+__device__ __forceinline__ void cgl_bn_stats(const CglBnFwd& bn, int K, const int (&k)[Q], int g, double (&mean)[Q],
+                                             double (&m2)[Q], int& n) {
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
   const int r0 = g * bn.gr, r1 = min(r0 + bn.gr, bn.mtot);
   n = r1 - r0;
   const int t0 = r0 / bn.part_bm, t1 = (r1 - 1) / bn.part_bm;
-  // each tile contributes one {sum, M2} pair; blocks of 8 independent loads in flight, then the
-  // exact parallel combination M2 = sum M2_t + n_t (mean_t - mean)^2 (fixed order)
   const int nt = t1 - t0 + 1;
-  double s = 0.0;
-  for (int i0 = 0; i0 < nt; i0 += 8) {
-    float ps[8];
+  if (nt <= 8) {
+    f32x2 pr[Q][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int t = t0 + min(i0 + j, nt - 1);
-      const int slot = g - (t * bn.part_bm) / bn.gr;
-      ps[j] = gld(bn.part + ((long)(t * 2 + slot) * K + k) * 2);
-    }
+    for (int q = 0; q < Q; ++q) {
+      const int kk = max(k[q], 0);
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (i0 + j < nt) s += (double)ps[j];
-  }
-  mean = s / n;
-  double q = 0.0;
-  for (int i0 = 0; i0 < nt; i0 += 8) {
-    float ps[8], pq[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int t = t0 + min(i0 + j, nt - 1);
-      const int slot = g - (t * bn.part_bm) / bn.gr;
-      const float* pp = bn.part + ((long)(t * 2 + slot) * K + k) * 2;
-      ps[j] = gld(pp);
-      pq[j] = gld(pp + 1);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (i0 + j < nt) {
-        const int t = t0 + i0 + j;
-        const int c = min((t + 1) * bn.part_bm, r1) - max(t * bn.part_bm, r0);
-        const double dd = (double)ps[j] / c - mean;
-        q += (double)pq[j] + c * dd * dd;
+      for (int j = 0; j < 8; ++j) {
+        const int t = t0 + min(j, nt - 1);
+        const int slot = (t * bn.part_bm < r0) ? 1 : 0;   // tile starts in the previous group
+        pr[q][j] = *(const CGL_GLOBAL f32x2*)(bn.part + ((long)(t * 2 + slot) * K + kk) * 2);
       }
     }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      double s = 0.0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j < nt) s += (double)pr[q][j][0];
+      const double mu = s / n;
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (j < nt) {
+          const int t = t0 + j;
+          const int c = min((t + 1) * bn.part_bm, r1) - max(t * bn.part_bm, r0);
+          const double dd = (double)pr[q][j][0] / c - mu;
+          acc += (double)pr[q][j][1] + c * dd * dd;
+        }
+      }
+      mean[q] = mu;
+      m2[q] = acc;
+    }
+    return;
   }
-  m2 = q;
+  for (int q = 0; q < Q; ++q) {
+    const int kk = max(k[q], 0);
+    double s = 0.0;
+    for (int t = t0; t <= t1; ++t) {
+      const int slot = (t * bn.part_bm < r0) ? 1 : 0;
+      s += (double)gld(bn.part + ((long)(t * 2 + slot) * K + kk) * 2);
+    }
+    const double mu = s / n;
+    double acc = 0.0;
+    for (int t = t0; t <= t1; ++t) {
+      const int slot = (t * bn.part_bm < r0) ? 1 : 0;
+      const float* pp = bn.part + ((long)(t * 2 + slot) * K + kk) * 2;
+      const int c = min((t + 1) * bn.part_bm, r1) - max(t * bn.part_bm, r0);
+      const double dd = (double)gld(pp) / c - mu;
+      acc += (double)gld(pp + 1) + c * dd * dd;
+    }
+    mean[q] = mu;
+    m2[q] = acc;
+  }
 }
 
-// Last-arriver BatchNorm finalize of one column tile of a producer GEMM.  Every workgroup of
-// the column tile publishes its partials (agent-scope release: the workgroups of a launch span
-// all 8 XCDs and their L2s), then takes a ticket; the last one combines the partials of every
-// row tile in a fixed order (so the result does not depend on which workgroup is last) into
-//   scale = gamma * invstd, shift = beta - mean * scale  per (group, feature),
-// the saved mean / invstd for the backward pass and the running statistics, updated group by
-// group in the order of the reference's forward calls (Xd then Xg, capgan.py:215-220).
-__device__ void cgl_bn_finalize(const CglGemmDesc* __restrict__ d, int tn) {
-  __shared__ int s_last;
+// Saved statistics (for the backward pass) and running statistics of the 64-feature block
+// `blk`, every group in the order of the reference's forward calls (Xd then Xg,
+// capgan.py:215-220): torch's momentum update with the unbiased variance.
+__device__ void cgl_bn_block_side(const CglBnFwd& bn, int K, int blk) {
   __shared__ double s_mean[2][64], s_m2[2][64];
   __shared__ int s_n[2];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned int ticket =
-        __hip_atomic_fetch_add(d->stat_cnt + tn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (ticket == (unsigned int)d->tiles_m - 1);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const CglBnFwd& bn = d->bn;
-  const int N = d->N;
-  const int ncol = 32 * d->WN;
-  const int c0 = tn * ncol;
   const int ngroups = (bn.mtot + bn.gr - 1) / bn.gr;   // <= 2
   const int tid = threadIdx.x;
-  for (int p = tid; p < ngroups * ncol; p += CGL_GEMM_THREADS) {
-    const int g = p / ncol, c = p % ncol, k = c0 + c;
-    if (k < N) {
-      double mean, m2;
-      int n;
-      cgl_bn_group_stats(bn, N, k, g, mean, m2, n);
-      s_mean[g][c] = mean;
-      s_m2[g][c] = m2;
-      if (c == 0) s_n[g] = n;
-      const double invstd = 1.0 / sqrt(m2 / n + bn.eps);
-      const float sc = (float)invstd * gld(bn.gamma + k);
-      const float sh = gld(bn.beta + k) - (float)mean * sc;
-      gst(d->stat_tab + ((long)g * N + k) * 2, sc);
-      gst(d->stat_tab + ((long)g * N + k) * 2 + 1, sh);
-      if (bn.save_mean) {
-        gst(bn.save_mean + (long)g * N + k, (float)mean);
-        gst(bn.save_invstd + (long)g * N + k, (float)invstd);
-      }
+  if (tid < 64 * ngroups) {
+    const int g = tid >> 6, c = tid & 63;
+    const int kk = blk * 64 + c;
+    const int k[1] = {kk < K ? kk : -1};
+    double mean[1], m2[1];
+    int n;
+    cgl_bn_stats<1>(bn, K, k, g, mean, m2, n);
+    s_mean[g][c] = mean[0];
+    s_m2[g][c] = m2[0];
+    if (c == 0) s_n[g] = n;
+    if (kk < K && bn.save_mean) {
+      gst(bn.save_mean + (long)g * K + kk, (float)mean[0]);
+      gst(bn.save_invstd + (long)g * K + kk, (float)(1.0 / sqrt(m2[0] / n + bn.eps)));
     }
   }
   __syncthreads();
-  if (bn.run_mean && tid < ncol && c0 + tid < N) {
-    const int k = c0 + tid;
+  const int kk = blk * 64 + tid;
+  if (bn.run_mean && tid < 64 && kk < K) {
     const double mom = bn.momentum;
-    float rm = gld(bn.run_mean + k), rv = gld(bn.run_var + k);
+    float rm = gld(bn.run_mean + kk), rv = gld(bn.run_var + kk);
     for (int g = 0; g < ngroups; ++g) {
       rm = (float)(mom * s_mean[g][tid] + (1.0 - mom) * (double)rm);
       rv = (float)(mom * (s_m2[g][tid] / (s_n[g] - 1)) + (1.0 - mom) * (double)rv);
     }
-    gst(bn.run_mean + k, rm);
-    gst(bn.run_var + k, rv);
+    gst(bn.run_mean + kk, rm);
+    gst(bn.run_var + kk, rv);
   }
-  if (tid == 0) __hip_atomic_store(d->stat_cnt + tn, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -217,8 +212,8 @@ __device__ __forceinline__ void cgl_mainloop_lds(const CglGemmDesc* __restrict__
   const int arow0 = tm * BMr;                 // first A row (kc) / column (mn) of the panel
   const int bcol0 = tn * BNr;                 // first B row (NT) / column (NN, TN) of the panel
   const int li = lane & 31, lh = lane >> 5;
-  const float slope_tf = d->tf_slope;
-  const int gr = a_tf ? d->tf_gr : 1;
+  const float slope_tf = d->bn.slope;
+  const int gr = a_tf ? d->bn.gr : 1;
   float* __restrict__ a_copy = (LAYOUT != 2 && tn == 0) ? d->a_copy : nullptr;
   const int a_copy_ld = d->a_copy_ld, a_copy_row0 = d->a_copy_row0;
   const int lda = d->a.ld, ldb = d->b.ld;
@@ -408,21 +403,46 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   const int m0 = tm * BM + wm * 32;
   const int n0 = (tn * WN + wn) * 32;
 
-  // ---------------- BatchNorm prologue: scale/shift pairs of the groups of this row tile
-  // (finalized by the last workgroups of the producer GEMM)
+  // ---------------- BatchNorm prologue: scale/shift pairs of the group(s) of this row tile,
+  // four features per thread with one memory round trip; pairs past K (up to the next
+  // multiple of 8) are zero, so the transform of a clamped tail load is 0
   const int a_tf = (LAYOUT != 2) ? d->a_tf : 0;
   int g0 = 0;
   if (a_tf) {
+    const CglBnFwd& bn = d->bn;
     const int rlast = min(tm * BM + BM, M) - 1;
-    g0 = (tm * BM) / d->tf_gr;
-    const int g1 = rlast / d->tf_gr;
+    g0 = (tm * BM) / bn.gr;
+    const int g1 = rlast / bn.gr;
+    const int Kp = (K + 7) & ~7;
     for (int g = g0; g <= g1; ++g) {
-      const float* src = d->tf_tab + (long)g * K * 2;
       float* dst = s_tf + (g - g0) * CGL_TF_MAXK * 2;
-      for (int k2 = tid; k2 < K; k2 += CGL_GEMM_THREADS) {
-        dst[2 * k2] = gld(src + 2 * k2);
-        dst[2 * k2 + 1] = gld(src + 2 * k2 + 1);
+      for (int kb = 0; kb < Kp; kb += 4 * CGL_GEMM_THREADS) {
+        int k[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) k[q] = (kb + q * CGL_GEMM_THREADS + tid < K) ? kb + q * CGL_GEMM_THREADS + tid : -1;
+        double mean[4], m2[4];
+        int n;
+        cgl_bn_stats<4>(bn, K, k, g, mean, m2, n);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int kk = kb + q * CGL_GEMM_THREADS + tid;
+          if (kk < Kp) {
+            float sc = 0.f, sh = 0.f;
+            if (k[q] >= 0) {
+              const double invstd = 1.0 / sqrt(m2[q] / n + bn.eps);
+              sc = (float)invstd * gld(bn.gamma + kk);
+              sh = gld(bn.beta + kk) - (float)mean[q] * sc;
+            }
+            dst[2 * kk] = sc;
+            dst[2 * kk + 1] = sh;
+          }
+        }
       }
+    }
+    // saved / running statistics: 64-feature blocks spread over the first workgroups
+    if (bn.run_mean || bn.save_mean) {
+      const int nblk = (K + 63) / 64;
+      for (int blk = local; blk < nblk; blk += nwg) cgl_bn_block_side(bn, K, blk);
     }
     __syncthreads();
   }
@@ -452,8 +472,8 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   const float* __restrict__ b_base =
       (LAYOUT == 0) ? cgl_row(d->b, min(bn_, N - 1)) : d->b.p0 + max(0, min(bn_, nmem - 1));
   const int lda = d->a.ld, ldb = d->b.ld;
-  const int gsel = a_tf ? (a_ok ? am / d->tf_gr - g0 : 0) : 0;
-  const float slope_tf = d->tf_slope;
+  const int gsel = a_tf ? (a_ok ? am / d->bn.gr - g0 : 0) : 0;
+  const float slope_tf = d->bn.slope;
   float* __restrict__ a_copy = d->a_copy;
   const bool do_copy = (LAYOUT != 2) && a_copy && tn == 0 && wn == 0 && a_ok && am >= d->a_copy_row0;
 
@@ -478,12 +498,15 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
       cgl_mask(B_, b_ok, k, K);
     }
     if (a_tf) {
-      const float* t = s_tf + (gsel * CGL_TF_MAXK) * 2;
+      // {scale, shift} of k..k+7 (k % 8 == 0): four 16-byte LDS reads, zero pairs past K
+      const f32x4* t4 = (const f32x4*)(s_tf + (gsel * CGL_TF_MAXK + k) * 2);
+      const f32x4 p0 = t4[0], p1 = t4[1], p2 = t4[2], p3 = t4[3];
+      const float sc[8] = {p0[0], p0[2], p1[0], p1[2], p2[0], p2[2], p3[0], p3[2]};
+      const float sh[8] = {p0[1], p0[3], p1[1], p1[3], p2[1], p2[3], p3[1], p3[3]};
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int kk = min(k + j, K - 1);
-        const float x = fmaf(A_[j], t[kk * 2 + 0], t[kk * 2 + 1]);
-        A_[j] = (a_ok && k + j < K) ? (x > 0.f ? x : x * slope_tf) : 0.f;
+        const float x = fmaf(A_[j], sc[j], sh[j]);
+        A_[j] = a_ok ? (x > 0.f ? x : x * slope_tf) : 0.f;
       }
     }
     if (do_copy) {
@@ -588,6 +611,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     const int gr = d->stat_gr;
     const int trow0 = tm * BM;
     const int gfirst = trow0 / gr;
+    const int gsplit = (gfirst + 1) * gr;   // first row of slot 1 (a tile spans <= 2 groups)
     float part[2][2];
     for (int s = 0; s < 2; ++s) {
       // pass 1: sum
@@ -596,7 +620,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = rbase + (r & 3) + 8 * (r >> 2);
-          if (row < M && row / gr - gfirst == s) sum += v[r];
+          if (row < M && (row >= gsplit) == (s == 1)) sum += v[r];
         }
       }
       sum += __shfl_xor(sum, 32);
@@ -614,7 +638,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = rbase + (r & 3) + 8 * (r >> 2);
-          if (row < M && row / gr - gfirst == s) {
+          if (row < M && (row >= gsplit) == (s == 1)) {
             const float dd = v[r] - mean;
             q2 += dd * dd;
           }
@@ -636,7 +660,6 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
         gst(p + 1, part[s][1]);
       }
     }
-    if (d->stat_tab) cgl_bn_finalize(d, tn);
   }
 
   if (owner && colok) {

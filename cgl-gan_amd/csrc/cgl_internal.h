@@ -37,10 +37,10 @@ struct CglRowSrc {
   int ld;                 // row stride in floats (both segments)
 };
 
-// Forward-BatchNorm statistics of a producer GEMM's output.  Every workgroup writes per-(row
-// tile, group slot, feature) partials {sum, M2}; the last workgroup to finish a column tile
-// combines them (fixed order, double) into the per-group scale/shift table the consumer GEMM
-// applies to its A operand, the saved mean/invstd of the backward pass and the running stats.
+// Forward-BatchNorm transform applied to the A operand as it is loaded (consumer side).
+// The producer GEMM wrote per-(row tile, group slot, feature) partials {sum, M2}; every consumer
+// workgroup combines them (fixed order, double) into the scale/shift pairs of its rows' group,
+// and a few workgroups also write the saved mean/invstd and update the running statistics.
 struct CglBnFwd {
   const float* part;      // [ntiles][2][K][2]
   int part_bm;            // producer rows per tile
@@ -50,9 +50,9 @@ struct CglBnFwd {
   const float* beta;
   double eps, momentum;
   float slope;
-  float* run_mean;        // updated by workgroup 0 (group 0 first, then 1), may be null
+  float* run_mean;        // per 64-feature block by one workgroup (group 0 first, then 1), may be null
   float* run_var;
-  float* save_mean;       // [ngroups][K] (workgroup 0), may be null
+  float* save_mean;       // [ngroups][K] (same workgroups), may be null
   float* save_invstd;
 };
 
@@ -66,10 +66,8 @@ struct CglGemmDesc {
   int pipe;               // 0: direct-to-register fragment loads; 1: LDS-staged slices
   CglRowSrc a, b;
   // A transform (kc A only)
-  int a_tf;               // 0 none, 1 BatchNorm+LeakyReLU through the producer's table
-  const float* tf_tab;    // [ngroups][K][2] {scale, shift}
-  int tf_gr;              // rows per BatchNorm group
-  float tf_slope;
+  int a_tf;               // 0 none, 1 BatchNorm+LeakyReLU from producer partials
+  CglBnFwd bn;
   float* a_copy;         // optional copy-out of the (transformed) A rows; rows >= a_copy_row0
   int a_copy_ld, a_copy_row0;
   // B extras
@@ -81,9 +79,6 @@ struct CglGemmDesc {
   const float* mask_ref; int mask_ld;     // v *= (ref > 0 ? 1 : slope)
   const float* tanh_ref; int tanh_ld;     // v *= 1 - t*t
   float* stat_part; int stat_gr;          // forward BatchNorm partials of the stored output
-  CglBnFwd bn;                            // with stat_part: finalize by the last workgroup per column tile
-  float* stat_tab;                        // [ngroups][N][2] scale/shift output
-  unsigned int* stat_cnt;                 // [tiles_n] arrival tickets (zero at rest)
   float* bias_out;                     // with b_ones_col: column N-1 of C goes here
 };
 

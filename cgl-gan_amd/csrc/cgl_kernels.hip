@@ -112,21 +112,23 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
       a += s_loss[q][0];
       b += s_loss[q][1];
     }
-    gst(hd->part + blockIdx.x * 2 + 0, a);
-    gst(hd->part + blockIdx.x * 2 + 1, b);
-    // last-arriver reduction (agent-scope release before the ticket, acquire after)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    // last-arriver reduction: partials are published with agent-coherent (sc1) stores and
+    // complete before the ticket is taken; the last workgroup reads them back coherently
+    __hip_atomic_store((CGL_GLOBAL float*)(hd->part + blockIdx.x * 2 + 0), a, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((CGL_GLOBAL float*)(hd->part + blockIdx.x * 2 + 1), b, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned int ticket =
         __hip_atomic_fetch_add(hd->counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = (ticket == gridDim.x - 1);
     if (s_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       double s0 = 0.0, s1 = 0.0;
       for (unsigned int q = 0; q < gridDim.x; ++q) {
-        s0 += (double)__hip_atomic_load(hd->part + q * 2 + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s1 += (double)__hip_atomic_load(hd->part + q * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s0 += (double)__hip_atomic_load((CGL_GLOBAL float*)(hd->part + q * 2 + 0), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+        s1 += (double)__hip_atomic_load((CGL_GLOBAL float*)(hd->part + q * 2 + 1), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
       }
       const int n0 = min(hd->split, M), n1 = M - n0;
       const float l0 = n0 > 0 ? (float)(s0 / n0) : 0.f;

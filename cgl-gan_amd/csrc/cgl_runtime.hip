@@ -111,8 +111,7 @@ constexpr int kMaxGemmDescs = 128;
 constexpr int kMaxHeadDescs = 2 * CGL_MAX_EPOCH + 4;
 constexpr int kMaxBnDescs = 2 * CGL_MAX_LAYERS;
 constexpr int kHeadRows = 16;
-constexpr int kBnCounter0 = 64;   // first BatchNorm ticket (64 per G layer)
-constexpr int kCounters = kBnCounter0 + 64 * CGL_MAX_LAYERS;
+constexpr int kCounters = 64;
 
 struct WS {
   // G forward (2B rows)
@@ -135,8 +134,7 @@ struct WS {
   float* gG[CGL_MAX_LAYERS];
   // misc
   float* hpart;
-  unsigned int* counters;   // [kCounters]: head-loss tickets, then BatchNorm column-tile tickets
-  float* gtab[CGL_MAX_LAYERS];  // BatchNorm scale/shift table [2][f][2] of G layer l's output
+  unsigned int* counters;   // [kCounters]: head-loss tickets
   CglStepState* st;
   int* idx;       // sampler output when sample_n > 0
   CglGemmDesc* gemm;
@@ -165,7 +163,6 @@ WS carve_ws(const cgl_gan_config& c, void* base) {
       const int64_t tiles = (2 * B + 31) / 32;
       w.gpart[l] = cv.take<float>(tiles * 2 * f * 2);
       w.gmean[l] = cv.take<float>((int64_t)2 * f);
-      w.gtab[l] = cv.take<float>((int64_t)2 * f * 2);
       w.ginvstd[l] = cv.take<float>((int64_t)2 * f);
       w.gdA[l] = cv.take<float>((int64_t)B * f);
     }
@@ -451,6 +448,7 @@ int build_plan(cgl_gan* c) {
   }
 
   // ---- G forward on [z1; z2] (2B rows; BatchNorm statistics per B-row forward call)
+  int bm_prod[CGL_MAX_LAYERS] = {0};
   for (int l = 0; l < L; ++l) {
     const int fi = g.dims[l], fo = g.dims[l + 1];
     CglGemmDesc e = make_gemm(0, 2 * B, fo, fi);
@@ -461,9 +459,20 @@ int build_plan(cgl_gan* c) {
       e.a = rows(w.gout[l - 1], fi);
       if (g.bn[l - 1]) {
         e.a_tf = 1;
-        e.tf_tab = w.gtab[l - 1];
-        e.tf_gr = B;
-        e.tf_slope = sl;
+        CglBnFwd& bn = e.bn;
+        bn.part = w.gpart[l - 1];
+        bn.part_bm = bm_prod[l - 1];
+        bn.gr = B;
+        bn.mtot = 2 * B;
+        bn.gamma = gparam(c, l - 1, 2);
+        bn.beta = gparam(c, l - 1, 3);
+        bn.eps = cf.bn_eps;
+        bn.momentum = cf.bn_momentum;
+        bn.slope = sl;
+        bn.run_mean = c->bufs.g_running + c->run_mean_off[l - 1];
+        bn.run_var = c->bufs.g_running + c->run_var_off[l - 1];
+        bn.save_mean = w.gmean[l - 1];
+        bn.save_invstd = w.ginvstd[l - 1];
         e.a_copy = w.gact[l - 1];
         e.a_copy_ld = fi;
         e.a_copy_row0 = B;
@@ -479,28 +488,13 @@ int build_plan(cgl_gan* c) {
       e.act = CGL_EPI_ACT_NONE;
       e.stat_part = w.gpart[l];
       e.stat_gr = B;
-      CglBnFwd& bn = e.bn;
-      bn.part = w.gpart[l];
-      bn.part_bm = 32 * e.WM;
-      bn.gr = B;
-      bn.mtot = 2 * B;
-      bn.gamma = gparam(c, l, 2);
-      bn.beta = gparam(c, l, 3);
-      bn.eps = cf.bn_eps;
-      bn.momentum = cf.bn_momentum;
-      bn.slope = sl;
-      bn.run_mean = c->bufs.g_running + c->run_mean_off[l];
-      bn.run_var = c->bufs.g_running + c->run_var_off[l];
-      bn.save_mean = w.gmean[l];
-      bn.save_invstd = w.ginvstd[l];
-      e.stat_tab = w.gtab[l];
-      e.stat_cnt = w.counters + kBnCounter0 + 64 * l;
     } else {
       e.act = CGL_EPI_ACT_LEAKY;
     }
     e.slope = sl;
     e.C = w.gout[l];
     e.ldc = fo;
+    bm_prod[l] = 32 * e.WM;
     push_gemm(c, A, {e});
   }
   const float* Xd = w.gout[L - 1];

@@ -34,10 +34,11 @@ static double time_desc(CglGemmDesc d, CglGemmDesc* dd, int reps) {
   (void)hipEventCreate(&e1);
   (void)hipMemcpy(dd, &d, sizeof(d), hipMemcpyHostToDevice);
   const int grid = d.tiles_m * d.tiles_n;
-  const int sh = cgl_gemm_stage_bytes(d);
-  for (int i = 0; i < 10; ++i) hipLaunchKernelGGL(cgl_gemm_f32, dim3(grid), dim3(256), sh, 0, dd, 1, 0);
+  const int tf = d.a_tf ? 2 * CGL_TF_MAXK * 2 : 0;
+  const int sh = cgl_gemm_stage_bytes(d) + tf * 4;
+  for (int i = 0; i < 10; ++i) hipLaunchKernelGGL(cgl_gemm_f32, dim3(grid), dim3(256), sh, 0, dd, 1, tf);
   (void)hipEventRecord(e0, 0);
-  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(cgl_gemm_f32, dim3(grid), dim3(256), sh, 0, dd, 1, 0);
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(cgl_gemm_f32, dim3(grid), dim3(256), sh, 0, dd, 1, tf);
   (void)hipEventRecord(e1, 0);
   (void)hipEventSynchronize(e1);
   float ms;
@@ -59,6 +60,31 @@ static void probes(float* A, float* B, float* C, float* bias, CglGemmDesc* dd, i
     (void)hipEventElapsedTime(&ms, e0, e1);
     printf("probe empty kernel grid=%d: %.2f us/launch\n", grid, ms * 1e3 / reps);
   }
+  // hipGraph replay of 28 dependent empty kernels (the per-node floor of a captured round)
+  {
+    hipStream_t cs;
+    CK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    hipGraph_t gr;
+    hipGraphExec_t ge;
+    for (int grid : {1, 256}) {
+      CK(hipStreamBeginCapture(cs, hipStreamCaptureModeGlobal));
+      for (int i = 0; i < 28; ++i) hipLaunchKernelGGL(empty_kernel, dim3(grid), dim3(256), 0, cs, (int*)nullptr);
+      CK(hipStreamEndCapture(cs, &gr));
+      CK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
+      for (int i = 0; i < 5; ++i) CK(hipGraphLaunch(ge, cs));
+      CK(hipStreamSynchronize(cs));
+      (void)hipEventRecord(e0, cs);
+      for (int i = 0; i < 50; ++i) CK(hipGraphLaunch(ge, cs));
+      (void)hipEventRecord(e1, cs);
+      (void)hipEventSynchronize(e1);
+      float ms;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      printf("probe graph of 28 empty kernels grid=%d: %.2f us/replay (%.2f us/kernel)\n", grid, ms * 1e3 / 50,
+             ms * 1e3 / 50 / 28);
+      CK(hipGraphExecDestroy(ge));
+      CK(hipGraphDestroy(gr));
+    }
+  }
   // fixed tile count (NT 256x256 -> 64 WGs of (1,1,4)), growing K
   for (int K : {16, 64, 256, 1024, 4096}) {
     for (int wk : {1, 4}) {
@@ -78,6 +104,50 @@ static void probes(float* A, float* B, float* C, float* bias, CglGemmDesc* dd, i
       printf("probe(LDS) NT 256x256 K=%5d WK=%d: %7.2f us (%.1f TF)\n", K, wk, us1, 2.0 * 256 * 256 * K / us1 * 1e-6);
       printf("probe NT 256x256 K=%5d WK=%d WGs=%3d: %7.2f us  (%.1f TF, %d MFMA/wave)\n", K, wk,
              d.tiles_m * d.tiles_n, us, 2.0 * 256 * 256 * K / us * 1e-6, (K / 16 / wk) * 8);
+    }
+  }
+}
+
+// Cost of each fused prologue/epilogue feature on the G-forward shapes (same tiles as the plan).
+static void fusion_costs(float* A, float* B, float* C, CglGemmDesc* dd, int reps) {
+  float *part, *vec, *cp;
+  CK(hipMalloc(&part, 64 * 2 * 1024 * 2 * 4));
+  CK(hipMemset(part, 0, 64 * 2 * 1024 * 2 * 4));
+  CK(hipMalloc(&vec, 16 * 1024 * 4));
+  CK(hipMalloc(&cp, 512 * 1024 * 4));
+  std::vector<float> h(16 * 1024, 1.f);
+  CK(hipMemcpy(vec, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+  const Shape fw[] = {{"G1 fwd", 0, 512, 256, 128}, {"G2 fwd", 0, 512, 512, 256}, {"G3 fwd", 0, 512, 1024, 512},
+                      {"G4 fwd", 0, 512, 784, 1024}};
+  const int cfg[4][3] = {{2, 2, 1}, {2, 1, 2}, {1, 2, 2}, {1, 1, 4}};
+  printf("fusion costs (us): plain | +stat partials | BN-transform A | both | both+copy\n");
+  for (const Shape& s : fw) {
+    for (auto& c : cfg) {
+      CglGemmDesc d;
+      memset(&d, 0, sizeof(d));
+      d.layout = 0; d.M = s.M; d.N = s.N; d.K = s.K;
+      d.WM = c[0]; d.WN = c[1]; d.WK = c[2];
+      d.tiles_m = (s.M + 32 * c[0] - 1) / (32 * c[0]);
+      d.tiles_n = (s.N + 32 * c[1] - 1) / (32 * c[1]);
+      d.a.p0 = A; d.a.split = 0x7fffffff; d.a.ld = s.K;
+      d.b.p0 = B; d.b.split = 0x7fffffff; d.b.ld = s.K;
+      d.a_vec = d.b_vec = 1;
+      d.C = C; d.ldc = s.N; d.slope = 0.2f; d.bias = vec;
+      const double t0 = time_desc(d, dd, reps);
+      d.stat_part = part; d.stat_gr = 256;
+      const double t1 = time_desc(d, dd, reps);
+      d.stat_part = nullptr;
+      d.a_tf = 1;
+      d.bn.part = part; d.bn.part_bm = 32; d.bn.gr = 256; d.bn.mtot = 512;
+      d.bn.gamma = vec; d.bn.beta = vec; d.bn.eps = 0.8; d.bn.momentum = 0.1; d.bn.slope = 0.2f;
+      d.bn.run_mean = vec + 4096; d.bn.run_var = vec + 8192; d.bn.save_mean = vec + 12288 - 2048;
+      d.bn.save_invstd = vec + 12288;
+      const double t2 = time_desc(d, dd, reps);
+      d.stat_part = part;
+      const double t3 = time_desc(d, dd, reps);
+      d.a_copy = cp; d.a_copy_ld = s.K; d.a_copy_row0 = 256;
+      const double t4 = time_desc(d, dd, reps);
+      printf("%-7s %d%d%d: %7.2f | %7.2f | %7.2f | %7.2f | %7.2f\n", s.name, c[0], c[1], c[2], t0, t1, t2, t3, t4);
     }
   }
 }
@@ -120,6 +190,7 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   probes(A, B, C, bias, dd, reps);
+  fusion_costs(A, B, C, dd, reps);
   if (argc > 2) return 0;
   double tot_best = 0, tot_flop = 0;
   printf("%-8s %-3s %5s %5s %5s |", "shape", "L", "M", "N", "K");
