@@ -69,19 +69,9 @@ def build_step(a, rank, world):
     return step, data
 
 
-def one_round(step, world, r, a):
-    from cglgan._lib import PHASE_A, PHASE_ALL, PHASE_B
-    graph = not a.eager
-    if world == 1:
-        step.run(PHASE_ALL, graph=graph)
-        return
-    step.run(PHASE_A, graph=graph)
-    dist.all_gather_into_tensor(step.losses_all, step.own_loss())
-    step.alpha_scale()
-    dist.all_reduce(step.exchange_buffer())
-    step.run(PHASE_B, graph=graph)
-    if a.E > 0 and (r + 1) % a.E == 0:
-        dist.all_reduce(step.d_params, op=dist.ReduceOp.AVG)
+def make_exchange(step, world, a):
+    from cglgan.exchange import DistComm, WorkerExchange
+    return WorkerExchange(step, DistComm() if world > 1 else None, share_every=a.E if world > 1 else 0)
 
 
 def profile_launches(step, world, rounds):
@@ -155,15 +145,17 @@ def main():
     stream = torch.cuda.Stream()
     with torch.cuda.stream(stream):
         step, data = build_step(a, rank, world)
+        ex = make_exchange(step, world, a)
+        graph = not a.eager
         torch.cuda.synchronize()
         for r in range(a.warmup):
-            one_round(step, world, r, a)
+            ex.round(r, graph=graph)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
         for r in range(a.steps):
-            one_round(step, world, a.warmup + r, a)
+            ex.round(a.warmup + r, graph=graph)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()

@@ -1,0 +1,138 @@
+"""Cross-worker exchange of one communication round, one worker per GPU.
+
+The reference runs every role as a thread on one device and passes tensors (with their
+autograd graph) through queue.Queue.  Here each worker is a process on its own
+GPU, G is replicated (identical init, identical z stream, deterministic kernels), and the
+round's queue traffic becomes collectives:
+
+  CAPGAN / MDGAN / CGLGAN (capgan.py:223-259):
+    phase A      local D step(s), G loss through the updated D, its gradient w.r.t. Xg
+    all_gather   the N scalar G losses                      (Worker -> Server, capgan.py:347,228-232)
+    alpha        lambda-weighting on device, own gradient scaled by alpha_rank (capgan.py:247-248)
+    all_reduce   sum of alpha_i dl_i/dXg  [B, 784]           (F_max.backward through every D, :258)
+    phase B      replicated G backward + Adam, lambda SGD    (:258-260)
+  Mix-G (mixed-gan.py:238-292): the same with the trunk-output gradient [B, 512] inside a
+    server group, plus the Cloud's data-size-weighted trunk average every cloud_epoch rounds
+    (mixed-gan.py:104-124, 193-200; the reference's load of it is a no-op, SURVEY F4, kept
+    reproducible with ``fedavg_compat_noop``).
+  E-share (new behaviour): mean of the D parameters every E rounds.
+
+``DistComm`` wraps torch.distributed (backend "nccl" = RCCL over xGMI on MI355X, "gloo" on
+CPU); ``LocalComm`` runs N workers of one process in lockstep (single-GPU rehearsal and
+tests).  Both expose the same three collectives, so ``WorkerExchange`` is written once.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import _lib as C
+
+
+class DistComm:
+    """Collectives of one process group (this process = one worker)."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.size = dist.get_world_size(group)
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor):
+        dist.all_gather_into_tensor(out, inp, group=self.group)
+
+    def all_reduce_sum(self, t: torch.Tensor):
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+
+    def all_reduce_mean(self, t: torch.Tensor, weights=None):
+        """sum_i w_i t_i (w = 1/N when None); identical result on every rank."""
+        if weights is not None:
+            t.mul_(float(weights[self.rank]))
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            t.div_(self.size)
+
+
+class WorkerExchange:
+    """One worker's communication round (phase A -> collectives -> phase B).
+
+    ``share_every`` > 0: E-share of the D parameters every that many rounds (a19).
+    ``cloud``/``cloud_every``: Mix-G Cloud FedAvg of the trunk across server groups (a18)
+    with data-size weights ``cloud_weights`` (one per member of the cloud group).
+    """
+
+    def __init__(self, step, comm=None, share_every: int = 0, cloud=None, cloud_every: int = 0,
+                 cloud_weights=None, fedavg_compat_noop: bool = False):
+        self.step = step
+        self.comm = comm
+        self.share_every = share_every
+        self.cloud, self.cloud_every = cloud, cloud_every
+        self.cloud_weights = cloud_weights
+        self.fedavg_compat_noop = fedavg_compat_noop
+        n = comm.size if comm is not None else 1
+        if n != step.n_workers:
+            raise ValueError(f"step planned for {step.n_workers} workers, group has {n}")
+
+    def round(self, r: int, graph: bool = True):
+        s = self.step
+        if self.comm is None or self.comm.size == 1:
+            s.run(C.PHASE_ALL, graph=graph)
+        else:
+            s.run(C.PHASE_A, graph=graph)
+            self.comm.all_gather(s.losses_all, s.own_loss())
+            s.alpha_scale()
+            self.comm.all_reduce_sum(s.exchange_buffer())
+            s.run(C.PHASE_B, graph=graph)
+        if self.comm is not None and self.share_every > 0 and (r + 1) % self.share_every == 0:
+            self.comm.all_reduce_mean(s.d_params)
+        if self.cloud is not None and self.cloud_every > 0 and (r + 1) % self.cloud_every == 0:
+            self.cloud_average()
+
+    def cloud_average(self):
+        """Data-size-weighted average of the shared trunk (+ its BatchNorm running stats) across
+        server groups, mixed-gan.py:104-124 (weights A_s = data_len_s / sum).  With
+        ``fedavg_compat_noop`` the reference's actual behaviour is reproduced: its load_state_dict
+        ignores every key, so the Cloud is only a barrier."""
+        if self.fedavg_compat_noop:
+            self.cloud.all_reduce_sum(torch.zeros(1, device=self.step.g_params.device))
+            return
+        p, r = self.step.trunk_slices()
+        self.cloud.all_reduce_mean(p, self.cloud_weights)
+        if r is not None:
+            self.cloud.all_reduce_mean(r, self.cloud_weights)
+
+
+class LocalComm:
+    """N in-process workers in lockstep: the collectives of ``WorkerExchange`` computed over the
+    workers' buffers with a fixed summation order (rank 0 .. N-1)."""
+
+    def __init__(self, steps):
+        self.steps = steps
+        self.size = len(steps)
+
+    def round(self, r: int, graph: bool = False, share_every: int = 0):
+        ss = self.steps
+        if self.size == 1:
+            ss[0].run(C.PHASE_ALL, graph=graph)
+            return
+        for s in ss:
+            s.run(C.PHASE_A, graph=graph)
+        losses = torch.cat([s.own_loss() for s in ss])
+        for s in ss:
+            s.losses_all.copy_(losses)
+            s.alpha_scale()
+        bufs = [s.exchange_buffer() for s in ss]
+        tot = bufs[0].clone()
+        for b in bufs[1:]:
+            tot += b
+        for b in bufs:
+            b.copy_(tot)
+        for s in ss:
+            s.run(C.PHASE_B, graph=graph)
+        if share_every > 0 and (r + 1) % share_every == 0:
+            tot = ss[0].d_params.clone()
+            for s in ss[1:]:
+                tot += s.d_params
+            tot /= self.size
+            for s in ss:
+                s.d_params.copy_(tot)

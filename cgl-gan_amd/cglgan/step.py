@@ -69,6 +69,7 @@ class GanStep:
         cfg.seed, cfg.gen_z, cfg.sample_n = seed, int(gen_z), sample_n
         self.cfg = cfg
         self.n_workers, self.rank = n_workers, rank
+        self.exchange_layer = exchange_layer
 
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
@@ -122,6 +123,27 @@ class GanStep:
             v = flat[off.value:off.value + n]
             out[k] = v.view(rows.value, cols.value) if kind.value == 0 else v
         return out
+
+    def trunk_slices(self):
+        """(flat G-parameter view, flat running-stat view or None) of the layers below
+        ``exchange_layer`` -- the Mix-G trunk shared by a server group (mixed-gan.py:193-200).
+        Both are contiguous prefixes of the flat buffers (state-dict order)."""
+        if self.exchange_layer <= 0:
+            raise RuntimeError("no trunk: the step was planned without a trunk/head split")
+        end = None
+        for i in range(len(self.gm.tensor_keys())):
+            off, rows, cols, layer, kind = (ctypes.c_int64(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int(),
+                                            ctypes.c_int())
+            C.check(C.lib.cgl_gan_param_tensor(ctypes.byref(self.cfg), C.MODEL_G, i, ctypes.byref(off),
+                                               ctypes.byref(rows), ctypes.byref(cols), ctypes.byref(layer),
+                                               ctypes.byref(kind)))
+            if layer.value >= self.exchange_layer:
+                end = off.value
+                break
+        p = self.g_params[:end]
+        al = lambda n: (n + 63) // 64 * 64
+        rend = sum(2 * al(self.gm.dims[l + 1]) for l in self.gm.bn_layers() if l < self.exchange_layer)
+        return p, (self.g_running[:rend] if rend > 0 else None)
 
     def _running_views(self):
         self.running = OrderedDict()
