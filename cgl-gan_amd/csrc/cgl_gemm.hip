@@ -4,9 +4,9 @@
 // autograd backward (model/mnist_model.py:11,22,77,79,81).
 //
 // Design (MI355X-first, not a CUDA tiling):
-//  * one wave owns a 32x32 output tile = ONE f32 MFMA accumulator (16 AGPR/VGPR per lane);
-//    v_mfma_f32_32x32x2_f32 issues every 64 cycles with a 64-cycle dependent latency, so a
-//    single accumulation chain already runs at the f32 matrix peak;
+//  * one wave owns TM x TN 32x32 f32 MFMA accumulators (1x1 for small problems, 2x2 for the
+//    large ones); v_mfma_f32_32x32x2_f32 issues every 64 cycles with a 64-cycle dependent
+//    latency, so even a single accumulation chain runs at the f32 matrix peak;
 //  * a 256-thread workgroup holds 4 waves arranged WM x WN x WK: WK > 1 splits K inside the
 //    workgroup (skinny, batch-256 GEMMs need it to put >= 1024 waves on the 256 CUs) and the
 //    split is summed through LDS in a fixed order (deterministic, no atomics);
@@ -14,13 +14,15 @@
 //    32x32x2 fragment is permuted so that lane half h owns 8 CONSECUTIVE k of every 16-k
 //    chunk: a k-contiguous operand is then two float4 loads per lane per 8 MFMAs;
 //  * prologue fusion: the A operand can be the pre-BatchNorm output of the previous layer;
-//    the workgroup combines the producer's {sum, M2} partials into a scale/shift table in LDS and applies
-//    BatchNorm1d(train) + LeakyReLU while loading (the reference's BN/LeakyReLU kernels
-//    disappear), optionally writing the transformed rows out once;
+//    the workgroup combines the producer's {sum, M2} partials into a scale/shift table in
+//    LDS and applies BatchNorm1d(train) + LeakyReLU while loading (the reference's
+//    BN/LeakyReLU kernels disappear), optionally writing the transformed rows out once;
 //  * epilogue fusion: bias, LeakyReLU / Tanh, LeakyReLU' mask, Tanh' (1 - t^2), the
 //    bias-gradient column (B's extra all-ones column), and per-column {sum, M2} partials of
 //    the stored output for the next layer's BatchNorm, grouped per forward call.
 #include "cgl_internal.h"
+
+#include <type_traits>
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -176,210 +178,20 @@ __device__ void cgl_bn_block_side(const CglBnFwd& bn, int K, int blk) {
 }
 
 // ------------------------------------------------------------------------------------------
-// LDS-staged main loop (PIPE == 1).
-//
-// Each k-group of WM x WN waves stages 32-deep k slices of its A panel (32*WM rows) and B panel
-// (32*WN columns) through LDS, double buffered: the coalesced global loads of slice s+1
-// (every wave-instruction reads whole 128-byte rows: 8 rows x 128 B for a k-contiguous operand)
-// are in flight while slice s is consumed from LDS, and each element is loaded once per
-// workgroup instead of once per wave that needs it.
-//   k-contiguous panel ([row][k], A of NT/NN and B of NT): rows padded to 36 floats, so the
-//     fragment reads (ds_read_b128 of 4 consecutive k for 32 rows) are bank-conflict free;
-//   mn-contiguous panel ([k][col], A of TN, B of NN/TN): rows of 32*W floats, fragment reads are
-//     ds_read_b32 of 32 consecutive columns (conflict free).
-// Tails (rows >= M, cols >= N, k >= K) are zero-filled at staging, so the MFMAs need no masks.
-// The BatchNorm+LeakyReLU transform of A and its copy-out are applied once, at staging.
-constexpr int CGL_BK = 32;
-constexpr int CGL_LDK = 36;
+// Main body.  One wave owns TM x TN 32x32 accumulator blocks ((32 TM) x (32 TN) outputs); the
+// workgroup tile is (32 TM WM) x (32 TN WN), K split WK ways.  Operand fragments of S chunks
+// (16 k each) are in flight in a rotation of S register sets, so (S - 1) x TM TN x 512 MFMA
+// cycles cover an L2 / MALL miss; TM = TN = 2 halves the operand traffic per FLOP and
+// quadruples the MFMA work per load batch for the large problems.
+template <int TM, int TN>
+struct CglPipe {
+  static constexpr int S = 3;
+};
 
-__device__ __forceinline__ int cgl_lds_stage_floats(int WM, int WN) { return (32 * WM + 32 * WN) * CGL_LDK; }
-
-template <int LAYOUT, int VEC>
-__device__ __forceinline__ void cgl_mainloop_lds(const CglGemmDesc* __restrict__ d, f32x16& acc,
-                                                 const float* __restrict__ s_tf, float* __restrict__ s_stage,
-                                                 int M, int N, int K, int nmem, int b_ones, int WM, int WN, int WK,
-                                                 int wk, int wmn, int wm, int wn, int tm, int tn, int lane, int g0,
-                                                 int a_tf) {
-  const int gw = WM * WN;
-  const int BMr = 32 * WM, BNr = 32 * WN;
-  const int a_fl = BMr * CGL_LDK;
-  const int stage_fl = cgl_lds_stage_floats(WM, WN);
-  float* __restrict__ grp = s_stage + wk * 2 * stage_fl;
-  const int nst = (K + CGL_BK - 1) / CGL_BK;
-  const int nsg = (nst + WK - 1) / WK;
-  const int sb = (wk * nst) / WK, cnt = ((wk + 1) * nst) / WK - sb;
-  const int ninst = (4 * WM + 4 * WN) / gw;  // staging wave-instructions per wave per slice (4..8)
-  const int arow0 = tm * BMr;                 // first A row (kc) / column (mn) of the panel
-  const int bcol0 = tn * BNr;                 // first B row (NT) / column (NN, TN) of the panel
-  const int li = lane & 31, lh = lane >> 5;
-  const float slope_tf = d->bn.slope;
-  const int gr = a_tf ? d->bn.gr : 1;
-  float* __restrict__ a_copy = (LAYOUT != 2 && tn == 0) ? d->a_copy : nullptr;
-  const int a_copy_ld = d->a_copy_ld, a_copy_row0 = d->a_copy_row0;
-  const int lda = d->a.ld, ldb = d->b.ld;
-
-  f32x4 rg[8];  // staging registers (ninst <= 8)
-
-  // address of staging instruction q of this wave for slice s; fills rg[q]
-  auto stage_load = [&](int s, int q) {
-    const int t = wmn + q * gw;
-    const bool isA = t < 4 * WM;
-    const int u = isA ? t : t - 4 * WM;
-    const bool kc = isA ? (LAYOUT != 2) : (LAYOUT == 0);
-    f32x4 v;
-    if (kc) {
-      const int lrow = 8 * u + (lane >> 3);
-      const int k = s * CGL_BK + 4 * (lane & 7);
-      const int nrows = isA ? M : N;
-      const int grow = min((isA ? arow0 : bcol0) + lrow, nrows - 1);
-      const float* rp = cgl_row(isA ? d->a : d->b, grow);
-      if (VEC) {
-        v = *(gcf4p)(rp + min(k, K - 4));
-      } else {
-        gcfp g = (gcfp)rp;
-        v = f32x4{g[min(k, K - 1)], g[min(k + 1, K - 1)], g[min(k + 2, K - 1)], g[min(k + 3, K - 1)]};
-      }
-    } else {
-      const int R = isA ? BMr : BNr;
-      const int lpr = R >> 2;                 // lanes per k-row
-      const int rpi = 64 / lpr;               // k-rows per instruction
-      const int kl = u * rpi + lane / lpr;
-      const int col = (isA ? arow0 : bcol0) + 4 * (lane % lpr);
-      const int ncols = isA ? M : nmem;
-      const int k = min(s * CGL_BK + kl, K - 1);
-      const float* base = (isA ? d->a.p0 : d->b.p0) + (long)k * (isA ? lda : ldb);
-      if (VEC && ncols >= 4) {
-        v = *(gcf4p)(base + min(col, ncols - 4));
-      } else {
-        gcfp g = (gcfp)base;
-        const int cm = max(ncols - 1, 0);
-        v = f32x4{g[min(col, cm)], g[min(col + 1, cm)], g[min(col + 2, cm)], g[min(col + 3, cm)]};
-      }
-    }
-    rg[q] = v;
-  };
-
-  // mask / transform / copy-out, then write rg[q] into LDS buffer `buf`
-  auto stage_store = [&](int s, int q, float* buf) {
-    const int t = wmn + q * gw;
-    const bool isA = t < 4 * WM;
-    const int u = isA ? t : t - 4 * WM;
-    const bool kc = isA ? (LAYOUT != 2) : (LAYOUT == 0);
-    f32x4 v = rg[q];
-    if (kc) {
-      const int lrow = 8 * u + (lane >> 3);
-      const int k = s * CGL_BK + 4 * (lane & 7);
-      const int nrows = isA ? M : N;
-      const int growu = (isA ? arow0 : bcol0) + lrow;
-      const bool rok = growu < nrows;
-      if (isA && a_tf) {
-        const int gsel = rok ? growu / gr - g0 : 0;
-        const float* tb = s_tf + (gsel * CGL_TF_MAXK) * 2;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int kk = min(k + j, K - 1);
-          const float x = fmaf(v[j], tb[kk * 2 + 0], tb[kk * 2 + 1]);
-          v[j] = x > 0.f ? x : x * slope_tf;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = (rok && k + j < K) ? v[j] : 0.f;
-      if (isA && a_copy && rok && growu >= a_copy_row0) {
-        float* dst = a_copy + (long)growu * a_copy_ld + k;
-        if (VEC && k + 3 < K) {
-          *(gf4p)dst = v;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (k + j < K) gst(dst + j, v[j]);
-        }
-      }
-      *reinterpret_cast<f32x4*>(buf + (isA ? 0 : a_fl) + lrow * CGL_LDK + 4 * (lane & 7)) = v;
-    } else {
-      const int R = isA ? BMr : BNr;
-      const int lpr = R >> 2;
-      const int rpi = 64 / lpr;
-      const int kl = u * rpi + lane / lpr;
-      const int cl = 4 * (lane % lpr);
-      const int col = (isA ? arow0 : bcol0) + cl;
-      const int ncols = isA ? M : nmem;
-      const bool kok = s * CGL_BK + kl < K;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = (kok && col + j < ncols) ? v[j] : 0.f;
-      *reinterpret_cast<f32x4*>(buf + (isA ? 0 : a_fl) + kl * R + cl) = v;
-    }
-  };
-
-  // fragments of sub-chunk j2 (16 k) from LDS buffer `buf`, then 8 MFMAs
-  auto compute = [&](int s, const float* buf) {
-#pragma unroll
-    for (int j2 = 0; j2 < 2; ++j2) {
-      float av[8], bv[8];
-      const int kq = 16 * j2 + 8 * lh;
-      if (LAYOUT != 2) {
-        const float* p = buf + (wm * 32 + li) * CGL_LDK + kq;
-        const f32x4 x = *reinterpret_cast<const f32x4*>(p);
-        const f32x4 y = *reinterpret_cast<const f32x4*>(p + 4);
-        av[0] = x[0]; av[1] = x[1]; av[2] = x[2]; av[3] = x[3];
-        av[4] = y[0]; av[5] = y[1]; av[6] = y[2]; av[7] = y[3];
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) av[j] = buf[(kq + j) * BMr + wm * 32 + li];
-      }
-      const float* bb = buf + a_fl;
-      if (LAYOUT == 0) {
-        const float* p = bb + (wn * 32 + li) * CGL_LDK + kq;
-        const f32x4 x = *reinterpret_cast<const f32x4*>(p);
-        const f32x4 y = *reinterpret_cast<const f32x4*>(p + 4);
-        bv[0] = x[0]; bv[1] = x[1]; bv[2] = x[2]; bv[3] = x[3];
-        bv[4] = y[0]; bv[5] = y[1]; bv[6] = y[2]; bv[7] = y[3];
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) bv[j] = bb[(kq + j) * BNr + wn * 32 + li];
-        if (b_ones && bcol0 + wn * 32 + li == N - 1) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) bv[j] = (s * CGL_BK + kq + j < K) ? 1.f : 0.f;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], bv[j], acc, 0, 0, 0);
-    }
-  };
-
-  // (staging loops are fully unrolled to 8 with a uniform predicate so rg[] stays in VGPRs)
-  // prologue: slice sb into buffer 0
-  if (cnt > 0) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-      if (q < ninst) stage_load(sb, q);
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-      if (q < ninst) stage_store(sb, q, grp);
-  }
-  __syncthreads();
-  for (int i = 0; i < nsg; ++i) {
-    float* cur = grp + (i & 1) * stage_fl;
-    float* nxt = grp + ((i + 1) & 1) * stage_fl;
-    const bool more = i + 1 < cnt;
-    if (more) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (q < ninst) stage_load(sb + i + 1, q);
-    }
-    if (i < cnt) compute(sb + i, cur);
-    if (more) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (q < ninst) stage_store(sb + i + 1, q, nxt);
-    }
-    __syncthreads();
-  }
-}
-
-template <int LAYOUT, int VEC, int PIPE>
+template <int LAYOUT, int VEC, int TM, int TN>
 __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d, int bid, float* __restrict__ s_tf,
-                                              float* __restrict__ s_stage, float* __restrict__ s_col) {
-  float* __restrict__ s_red = s_stage;   // split-K partials reuse the staging region after the loop
+                                              float* __restrict__ s_red, float* __restrict__ s_col) {
+  constexpr int S = CglPipe<TM, TN>::S;
   const int M = d->M, N = d->N, K = d->K;
   const int WN = d->WN, WK = d->WK, WM = d->WM;
   const int tid = threadIdx.x;
@@ -399,9 +211,9 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
   }
   const int tn = tile / d->tiles_m, tm = tile % d->tiles_m;
-  const int BM = 32 * WM;
-  const int m0 = tm * BM + wm * 32;
-  const int n0 = (tn * WN + wn) * 32;
+  const int BM = 32 * TM * WM;
+  const int m0 = tm * BM + wm * 32 * TM;            // first row of this wave's tile
+  const int n0 = (tn * WN + wn) * 32 * TN;          // first column of this wave's tile
 
   // ---------------- BatchNorm prologue: scale/shift pairs of the group(s) of this row tile,
   // four features per thread with one memory round trip; pairs past K (up to the next
@@ -419,7 +231,10 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
       for (int kb = 0; kb < Kp; kb += 4 * CGL_GEMM_THREADS) {
         int k[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) k[q] = (kb + q * CGL_GEMM_THREADS + tid < K) ? kb + q * CGL_GEMM_THREADS + tid : -1;
+        for (int q = 0; q < 4; ++q) {
+          const int kk = kb + q * CGL_GEMM_THREADS + tid;
+          k[q] = kk < K ? kk : -1;
+        }
         double mean[4], m2[4];
         int n;
         cgl_bn_stats<4>(bn, K, k, g, mean, m2, n);
@@ -450,249 +265,372 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   // ---------------- main loop
   const int b_ones = (LAYOUT != 0) ? d->b_ones_col : 0;
   const int nmem = N - b_ones;     // columns of B actually in memory
-  f32x16 acc;
+  f32x16 acc[TM][TN];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  if constexpr (PIPE == 1) {
-    cgl_mainloop_lds<LAYOUT, VEC>(d, acc, s_tf, s_stage, M, N, K, nmem, b_ones, WM, WN, WK, wk, wmn, wm, wn, tm, tn,
-                                  lane, g0, a_tf);
-  } else {
   const int nch = (K + CGL_GEMM_KCHUNK - 1) / CGL_GEMM_KCHUNK;
   const int cb = (wk * nch) / WK, ce = ((wk + 1) * nch) / WK;
-
-  // per-lane operand rows / columns
-  const int am = m0 + li;          // A row (kc) or A column (mn)
-  const int bn_ = n0 + li;         // B row (NT) or B column (NN/TN)
-  const bool a_ok = am < M;
-  const bool b_ok = bn_ < nmem;
-  const bool b_is_ones = b_ones && (bn_ == N - 1);
-  // clamped (always dereferenceable) operand bases
-  const float* __restrict__ a_base = (LAYOUT != 2) ? cgl_row(d->a, min(am, M - 1)) : d->a.p0 + min(am, M - 1);
-  const float* __restrict__ b_base =
-      (LAYOUT == 0) ? cgl_row(d->b, min(bn_, N - 1)) : d->b.p0 + max(0, min(bn_, nmem - 1));
   const int lda = d->a.ld, ldb = d->b.ld;
-  const int gsel = a_tf ? (a_ok ? am / d->bn.gr - g0 : 0) : 0;
   const float slope_tf = d->bn.slope;
   float* __restrict__ a_copy = d->a_copy;
-  const bool do_copy = (LAYOUT != 2) && a_copy && tn == 0 && wn == 0 && a_ok && am >= d->a_copy_row0;
 
-  auto load_chunk = [&](int c, float* A_, float* B_) {
-    const int k = c * CGL_GEMM_KCHUNK + 8 * lh;
-    if (LAYOUT == 2)
-      cgl_ld_mn(a_base, lda, k, K, A_);
-    else
-      cgl_ld_kc<VEC>(a_base, k, K, A_);
-    if (LAYOUT == 0)
-      cgl_ld_kc<VEC>(b_base, k, K, B_);
-    else
-      cgl_ld_mn(b_base, ldb, k, K, B_);
-  };
-  auto compute_chunk = [&](int c, float* A_, float* B_) {
-    const int k = c * CGL_GEMM_KCHUNK + 8 * lh;
-    cgl_mask(A_, a_ok, k, K);
-    if (b_is_ones) {
+  // per-lane operand rows / columns of each block, clamped (always dereferenceable) bases
+  const float* a_base[TM];
+  const float* b_base[TN];
+  bool a_ok[TM], b_is_ones[TN], do_copy[TM];
+  int gsel[TM];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) B_[j] = (k + j < K) ? 1.f : 0.f;
-    } else {
-      cgl_mask(B_, b_ok, k, K);
-    }
-    if (a_tf) {
-      // {scale, shift} of k..k+7 (k % 8 == 0): four 16-byte LDS reads, zero pairs past K
-      const f32x4* t4 = (const f32x4*)(s_tf + (gsel * CGL_TF_MAXK + k) * 2);
-      const f32x4 p0 = t4[0], p1 = t4[1], p2 = t4[2], p3 = t4[3];
-      const float sc[8] = {p0[0], p0[2], p1[0], p1[2], p2[0], p2[2], p3[0], p3[2]};
-      const float sh[8] = {p0[1], p0[3], p1[1], p1[3], p2[1], p2[3], p3[1], p3[3]};
+  for (int i = 0; i < TM; ++i) {
+    const int am = m0 + 32 * i + li;      // A row (kc) or A column (mn)
+    a_ok[i] = am < M;
+    a_base[i] = (LAYOUT != 2) ? cgl_row(d->a, min(am, M - 1)) : d->a.p0 + min(am, M - 1);
+    gsel[i] = a_tf ? (a_ok[i] ? am / d->bn.gr - g0 : 0) : 0;
+    do_copy[i] = (LAYOUT != 2) && a_copy && tn == 0 && wn == 0 && a_ok[i] && am >= d->a_copy_row0;
+  }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float x = fmaf(A_[j], sc[j], sh[j]);
-        A_[j] = a_ok ? (x > 0.f ? x : x * slope_tf) : 0.f;
-      }
-    }
-    if (do_copy) {
-      float* dst = a_copy + (long)am * d->a_copy_ld;
-      if (VEC && k + 7 < K) {
-        *(gf4p)(dst + k) = f32x4{A_[0], A_[1], A_[2], A_[3]};
-        *(gf4p)(dst + k + 4) = f32x4{A_[4], A_[5], A_[6], A_[7]};
+  for (int j = 0; j < TN; ++j) {
+    const int bc = n0 + 32 * j + li;      // B row (NT) or B column (NN/TN)
+    b_is_ones[j] = b_ones && (bc == N - 1);
+    b_base[j] = (LAYOUT == 0) ? cgl_row(d->b, min(bc, N - 1)) : d->b.p0 + max(0, min(bc, nmem - 1));
+  }
+
+  // Full chunks (k + 16 <= K) load without clamps and multiply without masks: rows / columns
+  // past M / N come from clamped (valid) addresses and only feed accumulator rows / columns
+  // that are never stored.  Only the K-tail chunk clamps its k and zeroes k >= K.
+  auto load_chunk = [&](auto tail, int c, float (&A_)[TM][8], float (&B_)[TN][8]) {
+    constexpr bool T = decltype(tail)::value;
+    const int k = c * CGL_GEMM_KCHUNK + 8 * lh;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      if (LAYOUT == 2) {
+        if (T) {
+          cgl_ld_mn(a_base[i], lda, k, K, A_[i]);
+        } else {
+          gcfp q = (gcfp)a_base[i] + (long)k * lda;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) A_[i][j] = q[(long)j * lda];
+        }
       } else {
+        if (T) {
+          cgl_ld_kc<VEC>(a_base[i], k, K, A_[i]);
+        } else if (VEC) {
+          const f32x4 x = *(gcf4p)(a_base[i] + k), y = *(gcf4p)(a_base[i] + k + 4);
+          A_[i][0] = x[0]; A_[i][1] = x[1]; A_[i][2] = x[2]; A_[i][3] = x[3];
+          A_[i][4] = y[0]; A_[i][5] = y[1]; A_[i][6] = y[2]; A_[i][7] = y[3];
+        } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (k + j < K) gst(dst + k + j, A_[j]);
+          for (int j = 0; j < 8; ++j) A_[i][j] = ((gcfp)a_base[i])[k + j];
+        }
       }
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A_[j], B_[j], acc, 0, 0, 0);
+    for (int j = 0; j < TN; ++j) {
+      if (LAYOUT == 0) {
+        if (T) {
+          cgl_ld_kc<VEC>(b_base[j], k, K, B_[j]);
+        } else if (VEC) {
+          const f32x4 x = *(gcf4p)(b_base[j] + k), y = *(gcf4p)(b_base[j] + k + 4);
+          B_[j][0] = x[0]; B_[j][1] = x[1]; B_[j][2] = x[2]; B_[j][3] = x[3];
+          B_[j][4] = y[0]; B_[j][5] = y[1]; B_[j][6] = y[2]; B_[j][7] = y[3];
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) B_[j][q] = ((gcfp)b_base[j])[k + q];
+        }
+      } else {
+        if (T) {
+          cgl_ld_mn(b_base[j], ldb, k, K, B_[j]);
+        } else {
+          gcfp q = (gcfp)b_base[j] + (long)k * ldb;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) B_[j][u] = q[(long)u * ldb];
+        }
+      }
+    }
+  };
+  auto compute_chunk = [&](auto tail, int c, float (&A_)[TM][8], float (&B_)[TN][8]) {
+    constexpr bool T = decltype(tail)::value;
+    const int k = c * CGL_GEMM_KCHUNK + 8 * lh;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      if (T) cgl_mask(A_[i], true, k, K);
+      if (a_tf) {
+        // {scale, shift} of k..k+7 (k % 8 == 0): four 16-byte LDS reads, zero pairs past K
+        const f32x4* t4 = (const f32x4*)(s_tf + (gsel[i] * CGL_TF_MAXK + k) * 2);
+        const f32x4 p0 = t4[0], p1 = t4[1], p2 = t4[2], p3 = t4[3];
+        const float sc[8] = {p0[0], p0[2], p1[0], p1[2], p2[0], p2[2], p3[0], p3[2]};
+        const float sh[8] = {p0[1], p0[3], p1[1], p1[3], p2[1], p2[3], p3[1], p3[3]};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = fmaf(A_[i][j], sc[j], sh[j]);
+          A_[i][j] = x > 0.f ? x : x * slope_tf;
+        }
+      }
+      if (do_copy[i]) {
+        float* dst = a_copy + (long)(m0 + 32 * i + li) * d->a_copy_ld;
+        if (VEC && (!T || k + 7 < K)) {
+          *(gf4p)(dst + k) = f32x4{A_[i][0], A_[i][1], A_[i][2], A_[i][3]};
+          *(gf4p)(dst + k + 4) = f32x4{A_[i][4], A_[i][5], A_[i][6], A_[i][7]};
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (!T || k + j < K) gst(dst + k + j, A_[i][j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (T) cgl_mask(B_[j], true, k, K);
+      if (b_ones) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (b_is_ones[j]) B_[j][q] = (!T || k + q < K) ? 1.f : 0.f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(A_[i][q], B_[j][q], acc[i][j], 0, 0, 0);
   };
 
-  // three register sets in rotation: the loads of chunks c+1 and c+2 are in flight while chunk
-  // c's MFMAs run (~2 x 512 MFMA cycles of cover for an L2/MALL miss), and no register copy
-  // forces an early wait.  Tail loads are clamped re-loads.
-  if (cb < ce) {
-    float xa[8], xb[8], ya[8], yb[8], za[8], zb[8];
-    load_chunk(cb, xa, xb);
-    load_chunk(min(cb + 1, ce - 1), ya, yb);
-    for (int c = cb; c < ce; c += 3) {
-      load_chunk(min(c + 2, ce - 1), za, zb);
-      compute_chunk(c, xa, xb);
-      load_chunk(min(c + 3, ce - 1), xa, xb);
-      if (c + 1 < ce) compute_chunk(c + 1, ya, yb);
-      load_chunk(min(c + 4, ce - 1), ya, yb);
-      if (c + 2 < ce) compute_chunk(c + 2, za, zb);
+  // S register sets in rotation: set s holds chunk c + s; after its MFMAs are issued it is
+  // refilled with chunk c + s + S, so S - 1 chunks of loads are always in flight and no
+  // register copy forces an early wait.
+  const int cfull = min(ce, K / CGL_GEMM_KCHUNK);   // end of this wave's full chunks
+  std::integral_constant<bool, false> full;
+  std::integral_constant<bool, true> tailc;
+  if (cb < cfull) {
+    float xa[S][TM][8], xb[S][TN][8];
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      if (cb + s < cfull) load_chunk(full, cb + s, xa[s], xb[s]);
+    for (int c = cb; c < cfull; c += S) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (c + s < cfull) compute_chunk(full, c + s, xa[s], xb[s]);
+        if (c + s + S < cfull) load_chunk(full, c + s + S, xa[s], xb[s]);
+      }
     }
   }
-  }  // PIPE == 0
+  if (cfull < ce) {   // the K tail (at most one chunk, owned by the last k-group)
+    float xa[TM][8], xb[TN][8];
+    load_chunk(tailc, cfull, xa, xb);
+    compute_chunk(tailc, cfull, xa, xb);
+  }
 
   // ---------------- split-K reduction (fixed order: wk = 1, 2, 3)
   if (WK > 1) {
+    constexpr int NB = TM * TN;
     if (wk > 0) {
-      float* dst = s_red + ((wmn * (WK - 1) + (wk - 1)) * 16) * 64;
+      float* dst = s_red + ((wmn * (WK - 1) + (wk - 1)) * NB * 16) * 64;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dst[r * 64 + lane] = acc[r];
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dst[((i * TN + j) * 16 + r) * 64 + lane] = acc[i][j][r];
     }
     __syncthreads();
     if (wk == 0) {
       for (int q = 1; q < WK; ++q) {
-        const float* src = s_red + ((wmn * (WK - 1) + (q - 1)) * 16) * 64;
+        const float* src = s_red + ((wmn * (WK - 1) + (q - 1)) * NB * 16) * 64;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] += src[r * 64 + lane];
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] += src[((i * TN + j) * 16 + r) * 64 + lane];
       }
     }
   }
 
   // ---------------- epilogue (waves with wk == 0 own the tile)
+  // register r of block (i, j): row m0 + 32 i + 4 lh + (r & 3) + 8 (r >> 2), column n0 + 32 j + li
   const bool owner = (wk == 0);
-  const int col = n0 + li;
-  const bool colok = col < N;
-  const bool ones_col = b_ones && col == N - 1;
-  float v[16];
+  const int rbase = m0 + 4 * lh;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = acc[r];
-  const int rbase = m0 + 4 * lh;   // row of register r: rbase + (r & 3) + 8 * (r >> 2)
-
-  if (owner && colok && !ones_col) {
-    if (d->bias) {
-      const float bb = gld(d->bias + col);
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + 32 * j + li;
+    const bool colok = col < N;
+    const bool ones_col = b_ones && col == N - 1;
+    if (owner && colok && !ones_col) {
+      const float bb = d->bias ? gld(d->bias + col) : 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] += bb;
-    }
-    if (d->act == CGL_EPI_ACT_LEAKY) {
-      const float sl = d->slope;
+      for (int i = 0; i < TM; ++i) {
+        float* v = (float*)&acc[i][j];
+        if (d->bias) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * sl;
-    } else if (d->act == CGL_EPI_ACT_TANH) {
+          for (int r = 0; r < 16; ++r) v[r] += bb;
+        }
+        if (d->act == CGL_EPI_ACT_LEAKY) {
+          const float sl = d->slope;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = tanhf(v[r]);
-    }
-    if (d->mask_ref) {
-      const float sl = d->slope;
-      float ref[16];
+          for (int r = 0; r < 16; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * sl;
+        } else if (d->act == CGL_EPI_ACT_TANH) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = min(rbase + (r & 3) + 8 * (r >> 2), M - 1);
-        ref[r] = gld(d->mask_ref + (long)row * d->mask_ld + col);
+          for (int r = 0; r < 16; ++r) v[r] = tanhf(v[r]);
+        }
+        if (d->mask_ref) {
+          const float sl = d->slope;
+          float ref[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = min(rbase + 32 * i + (r & 3) + 8 * (r >> 2), M - 1);
+            ref[r] = gld(d->mask_ref + (long)row * d->mask_ld + col);
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = ref[r] > 0.f ? v[r] : v[r] * sl;
+        }
+        if (d->tanh_ref) {
+          float t[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = min(rbase + 32 * i + (r & 3) + 8 * (r >> 2), M - 1);
+            t[r] = gld(d->tanh_ref + (long)row * d->tanh_ld + col);
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = v[r] * (1.f - t[r] * t[r]);
+        }
       }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = ref[r] > 0.f ? v[r] : v[r] * sl;
-    }
-    if (d->tanh_ref) {
-      float t[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = min(rbase + (r & 3) + 8 * (r >> 2), M - 1);
-        t[r] = gld(d->tanh_ref + (long)row * d->tanh_ld + col);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = v[r] * (1.f - t[r] * t[r]);
     }
   }
 
   // forward BatchNorm partials of the stored output: per column, per group slot {sum, M2}
+  // over the workgroup's BM rows (two-pass: tile-slot sum, then M2 about the tile-slot mean)
   if (d->stat_part) {
     const int gr = d->stat_gr;
     const int trow0 = tm * BM;
     const int gfirst = trow0 / gr;
     const int gsplit = (gfirst + 1) * gr;   // first row of slot 1 (a tile spans <= 2 groups)
-    float part[2][2];
+    float part[TN][2][2];
     for (int s = 0; s < 2; ++s) {
-      // pass 1: sum
-      float sum = 0.f;
-      if (owner && colok) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = rbase + (r & 3) + 8 * (r >> 2);
-          if (row < M && (row >= gsplit) == (s == 1)) sum += v[r];
-        }
-      }
-      sum += __shfl_xor(sum, 32);
-      if (owner && lh == 0) s_col[(wm * WN + wn) * 32 + li] = sum;
-      __syncthreads();
-      float tot = 0.f;
-      for (int q = 0; q < WM; ++q) tot += s_col[(q * WN + wn) * 32 + li];
-      __syncthreads();
       const int ra = max(trow0, (gfirst + s) * gr), rb = min(min(trow0 + BM, M), (gfirst + s + 1) * gr);
       const int cnt = rb - ra;
-      const float mean = cnt > 0 ? tot / cnt : 0.f;
-      // pass 2: M2 about the tile-slot mean
-      float q2 = 0.f;
-      if (owner && colok) {
+      float tot[TN], mean[TN];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = rbase + (r & 3) + 8 * (r >> 2);
-          if (row < M && (row >= gsplit) == (s == 1)) {
-            const float dd = v[r] - mean;
-            q2 += dd * dd;
+      for (int j = 0; j < TN; ++j) {
+        const bool colok = n0 + 32 * j + li < N;
+        float sum = 0.f;
+        if (owner && colok) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            const float* v = (const float*)&acc[i][j];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
+              if (row < M && (row >= gsplit) == (s == 1)) sum += v[r];
+            }
           }
         }
+        sum += __shfl_xor(sum, 32);
+        if (owner && lh == 0) s_col[((wm * WN + wn) * TN + j) * 32 + li] = sum;
       }
-      q2 += __shfl_xor(q2, 32);
-      if (owner && lh == 0) s_col[(wm * WN + wn) * 32 + li] = q2;
       __syncthreads();
-      float qt = 0.f;
-      for (int q = 0; q < WM; ++q) qt += s_col[(q * WN + wn) * 32 + li];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        float t = 0.f;
+        for (int q = 0; q < WM; ++q) t += s_col[((q * WN + wn) * TN + j) * 32 + li];
+        tot[j] = t;
+        mean[j] = cnt > 0 ? t / cnt : 0.f;
+      }
       __syncthreads();
-      part[s][0] = cnt > 0 ? tot : 0.f;
-      part[s][1] = cnt > 0 ? qt : 0.f;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const bool colok = n0 + 32 * j + li < N;
+        float q2 = 0.f;
+        if (owner && colok) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            const float* v = (const float*)&acc[i][j];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
+              if (row < M && (row >= gsplit) == (s == 1)) {
+                const float dd = v[r] - mean[j];
+                q2 += dd * dd;
+              }
+            }
+          }
+        }
+        q2 += __shfl_xor(q2, 32);
+        if (owner && lh == 0) s_col[((wm * WN + wn) * TN + j) * 32 + li] = q2;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        float qt = 0.f;
+        for (int q = 0; q < WM; ++q) qt += s_col[((q * WN + wn) * TN + j) * 32 + li];
+        part[j][s][0] = cnt > 0 ? tot[j] : 0.f;
+        part[j][s][1] = cnt > 0 ? qt : 0.f;
+      }
+      __syncthreads();
     }
-    if (owner && wm == 0 && lh == 0 && colok) {
-      for (int s = 0; s < 2; ++s) {
-        float* p = d->stat_part + ((long)(tm * 2 + s) * N + col) * 2;
-        gst(p, part[s][0]);
-        gst(p + 1, part[s][1]);
+    if (owner && wm == 0 && lh == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + 32 * j + li;
+        if (col < N) {
+          for (int s = 0; s < 2; ++s) {
+            float* p = d->stat_part + ((long)(tm * 2 + s) * N + col) * 2;
+            gst(p, part[j][s][0]);
+            gst(p + 1, part[j][s][1]);
+          }
+        }
       }
     }
   }
 
-  if (owner && colok) {
-    if (ones_col) {
-      if (d->bias_out) {
+  if (owner) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = rbase + (r & 3) + 8 * (r >> 2);
-          if (row < M) gst(d->bias_out + row, v[r]);
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + 32 * j + li;
+      if (col >= N) continue;
+      const bool ones_col = b_ones && col == N - 1;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const float* v = (const float*)&acc[i][j];
+        if (ones_col) {
+          if (d->bias_out) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
+              if (row < M) gst(d->bias_out + row, v[r]);
+            }
+          }
+        } else {
+          float* __restrict__ C = d->C;
+          const int ldc = d->ldc;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
+            if (row < M) gst(C + (long)row * ldc + col, v[r]);
+          }
         }
-      }
-    } else {
-      float* __restrict__ C = d->C;
-      const int ldc = d->ldc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = rbase + (r & 3) + 8 * (r >> 2);
-        if (row < M) gst(C + (long)row * ldc + col, v[r]);
       }
     }
   }
 }
 
-// One kernel symbol for every GEMM of the step; a grouped launch may mix layouts (e.g. the
-// weight gradient (TN) and the input gradient (NN) of one layer run side by side).
+// One kernel per per-wave block shape (TM x TN), shared by every GEMM of the step; a grouped
+// launch may mix layouts (e.g. the weight gradient (TN) and the input gradient (NN) of one
+// layer side by side).  Separate symbols keep the 1x1 variant's register budget (and so its
+// occupancy) independent of the 2x2 variant's.
 // Dynamic LDS: [tf_floats: BatchNorm scale/shift table (0 when no problem of the launch needs it)]
-//              [staging slices of every k-group, reused for the split-K partials after the loop]
+//              [split-K partials of the waves with wk > 0]
+template <int TM, int TN>
 __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDesc* __restrict__ descs, int ndesc,
                                                                  int tf_floats) {
   extern __shared__ float cgl_dyn_lds[];
-  __shared__ float s_col[4 * 32 * 2];           // per-column reductions across waves
+  __shared__ float s_col[4 * TN * 32];          // per-column reductions across waves (WM WN <= 4)
   float* s_tf = cgl_dyn_lds;
-  float* s_stage = cgl_dyn_lds + tf_floats;
+  float* s_red = cgl_dyn_lds + tf_floats;
   const int bid = blockIdx.x;
   int di = 0;
   for (int q = 1; q < ndesc; ++q)
@@ -701,20 +639,12 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
   const int layout = d->layout;
   // VEC: every operand allows 16-byte loads along its contiguous dimension
   const int vec = d->a_vec && d->b_vec;
-  const int pipe = d->pipe;
-#define CGL_BODY(L)                                             \
-  do {                                                          \
-    if (pipe) {                                                 \
-      if (vec)                                                  \
-        cgl_gemm_body<L, 1, 1>(d, bid, s_tf, s_stage, s_col);   \
-      else                                                      \
-        cgl_gemm_body<L, 0, 1>(d, bid, s_tf, s_stage, s_col);   \
-    } else {                                                    \
-      if (vec)                                                  \
-        cgl_gemm_body<L, 1, 0>(d, bid, s_tf, s_stage, s_col);   \
-      else                                                      \
-        cgl_gemm_body<L, 0, 0>(d, bid, s_tf, s_stage, s_col);   \
-    }                                                           \
+#define CGL_BODY(L)                                               \
+  do {                                                            \
+    if (vec)                                                      \
+      cgl_gemm_body<L, 1, TM, TN>(d, bid, s_tf, s_red, s_col);    \
+    else                                                          \
+      cgl_gemm_body<L, 0, TM, TN>(d, bid, s_tf, s_red, s_col);    \
   } while (0)
   if (layout == 0)
     CGL_BODY(0);
@@ -725,9 +655,7 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
 #undef CGL_BODY
 }
 
-// Host helper: dynamic LDS bytes of one problem (staging or split-K region; the table is extra).
+// Host helper: dynamic LDS bytes of one problem's split-K partials (the BN table is extra).
 inline int cgl_gemm_stage_bytes(const CglGemmDesc& d) {
-  const int red = 3 * 16 * 64 * 4;
-  const int st = d.pipe ? d.WK * 2 * (32 * d.WM + 32 * d.WN) * CGL_LDK * 4 : 0;
-  return st > red ? st : red;
+  return (d.WK > 1) ? d.WM * d.WN * (d.WK - 1) * d.TM * d.TN * 16 * 64 * 4 : 0;
 }

@@ -63,7 +63,7 @@ struct CglGemmDesc {
   int wg_begin;           // first workgroup of this problem in a grouped launch
   int layout;             // 0: NT (A[m][k], B[n][k]); 1: NN (A[m][k], B[k][n]); 2: TN (A[k][m], B[k][n])
   int a_vec, b_vec;       // 16-byte vector loads allowed along each operand's contiguous dim
-  int pipe;               // 0: direct-to-register fragment loads; 1: LDS-staged slices
+  int TM, TN;             // 32x32 accumulator blocks per wave (1x1 or 2x2)
   CglRowSrc a, b;
   // A transform (kc A only)
   int a_tf;               // 0 none, 1 BatchNorm+LeakyReLU from producer partials

@@ -199,54 +199,71 @@ struct Launch {
   int stream_id = 0;
   double flops = 0.0;
   int shmem = 0;        // dynamic LDS bytes (GEMM)
+  int blk = 1;          // GEMM per-wave block shape (TM = TN = blk)
   int tf_floats = 0;    // BatchNorm-table floats at the head of the dynamic LDS (GEMM)
 };
 
-// The LDS-staged GEMM needs up to ~90 KB of dynamic LDS per workgroup (> the 64 KB default).
+// Split-K partials of 2x2-block waves need up to 48 KB of dynamic LDS (+16 KB BN table).
 hipError_t gemm_lds_attr() {
   static bool done = false;
   if (!done) {
-    // the attribute is advisory on this platform (launches up to the per-CU LDS succeed); try
-    // the largest accepted value and never fail on it
-    for (int kb : {159, 150, 128, 96, 64}) {
-      const hipError_t e =
-          hipFuncSetAttribute((const void*)cgl_gemm_f32, hipFuncAttributeMaxDynamicSharedMemorySize, kb * 1024);
-      (void)hipGetLastError();
-      if (e == hipSuccess) break;
+    // advisory on this platform (launches up to the per-CU LDS succeed); never fail on it
+    for (const void* fn : {(const void*)cgl_gemm_f32<1, 1>, (const void*)cgl_gemm_f32<2, 2>}) {
+      for (int kb : {150, 128, 96, 64}) {
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kb * 1024);
+        (void)hipGetLastError();
+        if (e == hipSuccess) break;
+      }
     }
     done = true;
   }
   return hipSuccess;
 }
 
-// GEMM main-loop selection (0 direct fragment loads, 1 LDS-staged); CGL_GEMM_PIPE overrides.
-int gemm_pipe_default() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("CGL_GEMM_PIPE");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
+void launch_gemm(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, int n, int tf) {
+  if (blk == 2)
+    cgl_gemm_f32<2, 2><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n, tf);
+  else
+    cgl_gemm_f32<1, 1><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n, tf);
 }
 
-void choose_tiles(CglGemmDesc& d, int force_wm = 0) {
+// Cost model of one GEMM launch (cycles) used to pick the wave arrangement WM x WN x WK and
+// the per-wave block shape TM x TN:
+//   MFMA issue per SIMD, one wave's dependent chain incl. the part of the memory latency its
+//   (S-1)-deep prefetch does not cover, and the per-CU address/L1 rate of the fragment loads
+//   (a fragment load touches 32 cache lines), plus the split-K reduction.
+double gemm_cost(int M, int N, int K, int WM, int WN, int WK, int TM, int TN) {
+  const double lat = 2000.0;
+  const int S = 3;
+  const long tiles = (long)((M + 32 * TM * WM - 1) / (32 * TM * WM)) * ((N + 32 * TN * WN - 1) / (32 * TN * WN));
+  const double wg_per_cu = std::ceil(tiles / 256.0);
+  const int nch = (K + CGL_GEMM_KCHUNK - 1) / CGL_GEMM_KCHUNK;
+  const double per = std::ceil((double)nch / WK);
+  const double blk = 512.0 * TM * TN;
+  const double mfma = wg_per_cu * per * blk;
+  const double chain = per * std::max(blk, lat / (S - 1));
+  const double ta = wg_per_cu * 4 * per * (TM + TN) * 64.0;
+  return std::max(mfma, std::max(chain, ta)) + (WK > 1 ? 400.0 * TM * TN : 0.0);
+}
+
+// force_wm: rows per wave-row group fixed (32 * TM * WM == 32 * force_wm); force_t: TM = TN fixed
+void choose_tiles(CglGemmDesc& d, int force_wm = 0, int force_t = 0) {
   static const int opts[4][3] = {{2, 2, 1}, {2, 1, 2}, {1, 2, 2}, {1, 1, 4}};
   double best = 1e300;
-  for (auto& o : opts) {
-    if (force_wm && o[0] != force_wm) continue;
-    const int tm = (d.M + 32 * o[0] - 1) / (32 * o[0]);
-    const int tn = (d.N + 32 * o[1] - 1) / (32 * o[1]);
-    const double wgs = (double)tm * tn;
-    const int nch = (d.K + CGL_GEMM_KCHUNK - 1) / CGL_GEMM_KCHUNK;
-    const int per = (nch + o[2] - 1) / o[2];
-    const double t = (per * 8.0 + 24.0) * std::max(1.0, wgs / 256.0) + (o[2] - 1) * 6.0;
-    if (t < best - 1e-9) {
-      best = t;
-      d.WM = o[0];
-      d.WN = o[1];
-      d.WK = o[2];
-      d.tiles_m = tm;
-      d.tiles_n = tn;
+  for (int t = 1; t <= 2; ++t) {
+    if (force_t && t != force_t) continue;
+    for (auto& o : opts) {
+      if (force_wm && o[0] * t != force_wm) continue;
+      const double c = gemm_cost(d.M, d.N, d.K, o[0], o[1], o[2], t, t);
+      if (c < best * (1.0 - 1e-9)) {
+        best = c;
+        d.WM = o[0];
+        d.WN = o[1];
+        d.WK = o[2];
+        d.TM = d.TN = t;
+        d.tiles_m = (d.M + 32 * t * o[0] - 1) / (32 * t * o[0]);
+        d.tiles_n = (d.N + 32 * t * o[1] - 1) / (32 * t * o[1]);
+      }
     }
   }
 }
@@ -262,7 +279,6 @@ CglGemmDesc make_gemm(int layout, int M, int N, int K) {
   d.b.split = 0x7fffffff;
   d.slope = 0.2f;
   d.act = CGL_EPI_ACT_NONE;
-  d.pipe = gemm_pipe_default();
   choose_tiles(d);
   return d;
 }
@@ -349,6 +365,19 @@ void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
   L.first = (int)c->gemm.size();
   L.count = (int)descs.size();
   int wg = 0, stage = 0, tf = 0;
+  // one block shape per launch (one kernel instantiation): the shape of the largest problem
+  int blk = 1;
+  double fmax = -1.0;
+  for (auto& d : descs) {
+    const double f = (double)d.M * d.N * d.K;
+    if (f > fmax) {
+      fmax = f;
+      blk = d.TM;
+    }
+  }
+  for (auto& d : descs)
+    if (d.TM != blk) choose_tiles(d, 0, blk);
+  L.blk = blk;
   for (auto& d : descs) {
     set_vec(d);
     d.wg_begin = wg;
@@ -494,7 +523,7 @@ int build_plan(cgl_gan* c) {
     e.slope = sl;
     e.C = w.gout[l];
     e.ldc = fo;
-    bm_prod[l] = 32 * e.WM;
+    bm_prod[l] = 32 * e.TM * e.WM;
     push_gemm(c, A, {e});
   }
   const float* Xd = w.gout[L - 1];
@@ -793,8 +822,7 @@ __global__ void cgl_sample(int* idx, const CglStepState* st, int epoch, int br, 
 int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s) {
   switch (L.kind) {
     case K_GEMM:
-      hipLaunchKernelGGL(cgl_gemm_f32, dim3(L.grid), dim3(CGL_GEMM_THREADS), L.shmem, s, c->ws.gemm + L.first,
-                         L.count, L.tf_floats);
+      launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, L.count, L.tf_floats);
       break;
     case K_HEAD:
       hipLaunchKernelGGL(cgl_head_loss, dim3(L.grid), dim3(256), 0, s, c->ws.head + L.first);
@@ -1127,8 +1155,7 @@ static int single_gemm(CglGemmDesc& d, void* ws, int64_t wsb, hipStream_t s) {
   d.wg_begin = 0;
   set_vec(d);
   HIPCHK(hipMemcpyAsync(ws, &d, sizeof(d), hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(cgl_gemm_f32, dim3(d.tiles_m * d.tiles_n), dim3(CGL_GEMM_THREADS), cgl_gemm_stage_bytes(d), s,
-                     (const CglGemmDesc*)ws, 1, 0);
+launch_gemm(d.TM, d.tiles_m * d.tiles_n, cgl_gemm_stage_bytes(d), s, (const CglGemmDesc*)ws, 1, 0);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   // the descriptor lives in the caller's workspace: keep it alive until the kernel has read it

@@ -36,9 +36,15 @@ static double time_desc(CglGemmDesc d, CglGemmDesc* dd, int reps) {
   const int grid = d.tiles_m * d.tiles_n;
   const int tf = d.a_tf ? 2 * CGL_TF_MAXK * 2 : 0;
   const int sh = cgl_gemm_stage_bytes(d) + tf * 4;
-  for (int i = 0; i < 10; ++i) hipLaunchKernelGGL(cgl_gemm_f32, dim3(grid), dim3(256), sh, 0, dd, 1, tf);
+  auto go = [&]() {
+    if (d.TM == 2)
+      cgl_gemm_f32<2, 2><<<grid, 256, sh, 0>>>(dd, 1, tf);
+    else
+      cgl_gemm_f32<1, 1><<<grid, 256, sh, 0>>>(dd, 1, tf);
+  };
+  for (int i = 0; i < 10; ++i) go();
   (void)hipEventRecord(e0, 0);
-  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(cgl_gemm_f32, dim3(grid), dim3(256), sh, 0, dd, 1, tf);
+  for (int i = 0; i < reps; ++i) go();
   (void)hipEventRecord(e1, 0);
   (void)hipEventSynchronize(e1);
   float ms;
@@ -97,13 +103,16 @@ static void probes(float* A, float* B, float* C, float* bias, CglGemmDesc* dd, i
       d.b.p0 = B; d.b.split = 0x7fffffff; d.b.ld = K;
       d.a_vec = d.b_vec = 1;
       d.C = C; d.ldc = 256; d.slope = 0.2f;
-      d.pipe = 1;
-      const double us1 = time_desc(d, dd, reps);
-      d.pipe = 0;
+      d.TM = d.TN = 1;
       const double us = time_desc(d, dd, reps);
-      printf("probe(LDS) NT 256x256 K=%5d WK=%d: %7.2f us (%.1f TF)\n", K, wk, us1, 2.0 * 256 * 256 * K / us1 * 1e-6);
       printf("probe NT 256x256 K=%5d WK=%d WGs=%3d: %7.2f us  (%.1f TF, %d MFMA/wave)\n", K, wk,
              d.tiles_m * d.tiles_n, us, 2.0 * 256 * 256 * K / us * 1e-6, (K / 16 / wk) * 8);
+      // same launch with every row of A and B aliased to row 0 (ld = 0): a fragment load then
+      // touches 1 cache line instead of 32 -- isolates the per-CU address/L1 cost
+      d.a.ld = 0; d.b.ld = 0;
+      const double usb = time_desc(d, dd, reps);
+      printf("probe NT 256x256 K=%5d WK=%d rows aliased: %7.2f us  (%.1f TF)\n", K, wk, usb,
+             2.0 * 256 * 256 * K / usb * 1e-6);
     }
   }
 }
@@ -119,16 +128,16 @@ static void fusion_costs(float* A, float* B, float* C, CglGemmDesc* dd, int reps
   CK(hipMemcpy(vec, h.data(), h.size() * 4, hipMemcpyHostToDevice));
   const Shape fw[] = {{"G1 fwd", 0, 512, 256, 128}, {"G2 fwd", 0, 512, 512, 256}, {"G3 fwd", 0, 512, 1024, 512},
                       {"G4 fwd", 0, 512, 784, 1024}};
-  const int cfg[4][3] = {{2, 2, 1}, {2, 1, 2}, {1, 2, 2}, {1, 1, 4}};
+  const int cfg[6][4] = {{2, 1, 2, 1}, {1, 2, 2, 1}, {1, 1, 4, 1}, {2, 1, 2, 2}, {1, 2, 2, 2}, {1, 1, 4, 2}};
   printf("fusion costs (us): plain | +stat partials | BN-transform A | both | both+copy\n");
   for (const Shape& s : fw) {
     for (auto& c : cfg) {
       CglGemmDesc d;
       memset(&d, 0, sizeof(d));
       d.layout = 0; d.M = s.M; d.N = s.N; d.K = s.K;
-      d.WM = c[0]; d.WN = c[1]; d.WK = c[2];
-      d.tiles_m = (s.M + 32 * c[0] - 1) / (32 * c[0]);
-      d.tiles_n = (s.N + 32 * c[1] - 1) / (32 * c[1]);
+      d.WM = c[0]; d.WN = c[1]; d.WK = c[2]; d.TM = d.TN = c[3];
+      d.tiles_m = (s.M + 32 * c[3] * c[0] - 1) / (32 * c[3] * c[0]);
+      d.tiles_n = (s.N + 32 * c[3] * c[1] - 1) / (32 * c[3] * c[1]);
       d.a.p0 = A; d.a.split = 0x7fffffff; d.a.ld = s.K;
       d.b.p0 = B; d.b.split = 0x7fffffff; d.b.ld = s.K;
       d.a_vec = d.b_vec = 1;
@@ -147,7 +156,8 @@ static void fusion_costs(float* A, float* B, float* C, CglGemmDesc* dd, int reps
       const double t3 = time_desc(d, dd, reps);
       d.a_copy = cp; d.a_copy_ld = s.K; d.a_copy_row0 = 256;
       const double t4 = time_desc(d, dd, reps);
-      printf("%-7s %d%d%d: %7.2f | %7.2f | %7.2f | %7.2f | %7.2f\n", s.name, c[0], c[1], c[2], t0, t1, t2, t3, t4);
+      printf("%-7s %d%d%d/%d: %7.2f | %7.2f | %7.2f | %7.2f | %7.2f\n", s.name, c[0], c[1], c[2], c[3], t0, t1, t2, t3,
+             t4);
     }
   }
 }
@@ -164,14 +174,14 @@ int main(int argc, char** argv) {
       {"G gW4", 2, 784, 1025, 256},  {"G gW3", 2, 1024, 513, 256},  {"G gW2", 2, 512, 257, 256},
       {"G gW1", 2, 256, 129, 256},   {"G gW0", 2, 128, 101, 256},
   };
-  const int cfgs[8][4] = {{2, 2, 1, 0}, {2, 1, 2, 0}, {1, 2, 2, 0}, {1, 1, 4, 0},
-                          {2, 2, 1, 1}, {2, 1, 2, 1}, {1, 2, 2, 1}, {1, 1, 4, 1}};
-  for (int kb : {160, 159, 150, 128, 96, 64}) {
-    const hipError_t e = hipFuncSetAttribute((const void*)cgl_gemm_f32, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             kb * 1024);
-    printf("hipFuncSetAttribute(MaxDynamicSharedMemorySize, %d KB): %s\n", kb, hipGetErrorString(e));
-    (void)hipGetLastError();
-    if (e == hipSuccess) break;
+  const int cfgs[8][4] = {{2, 2, 1, 1}, {2, 1, 2, 1}, {1, 2, 2, 1}, {1, 1, 4, 1},
+                          {2, 2, 1, 2}, {2, 1, 2, 2}, {1, 2, 2, 2}, {1, 1, 4, 2}};
+  for (const void* fn : {(const void*)cgl_gemm_f32<1, 1>, (const void*)cgl_gemm_f32<2, 2>}) {
+    for (int kb : {150, 128, 96, 64}) {
+      const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kb * 1024);
+      (void)hipGetLastError();
+      if (e == hipSuccess) break;
+    }
   }
   const size_t big = 4u << 20;  // floats
   float *A, *B, *C, *bias;
@@ -189,17 +199,28 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  probes(A, B, C, bias, dd, reps);
-  fusion_costs(A, B, C, dd, reps);
-  if (argc > 2) return 0;
+  const bool single = argc > 3;   // gemm_bench REPS single SHAPE CFG: one config only (PMC runs)
+  if (!single) {
+    probes(A, B, C, bias, dd, reps);
+    fusion_costs(A, B, C, dd, reps);
+  }
+  if (argc == 3) return 0;
+  const int only_shape = single ? atoi(argv[3]) : -1;
+  const int only_cfg = single && argc > 4 ? atoi(argv[4]) : -1;
   double tot_best = 0, tot_flop = 0;
   printf("%-8s %-3s %5s %5s %5s |", "shape", "L", "M", "N", "K");
-  for (auto& c : cfgs) printf(" %d%d%d%s us TF |", c[0], c[1], c[2], c[3] ? "L" : "d");
+  for (auto& c : cfgs) printf(" %d%d%d/%d us TF |", c[0], c[1], c[2], c[3]);
   printf(" best\n");
+  int si = -1;
   for (const Shape& s : shapes) {
+    ++si;
+    if (only_shape >= 0 && si != only_shape) continue;
     printf("%-8s %-3d %5d %5d %5d |", s.name, s.layout, s.M, s.N, s.K);
     double best = 1e30;
+    int ci = -1;
     for (auto& c : cfgs) {
+      ++ci;
+      if (only_cfg >= 0 && ci != only_cfg) continue;
       CglGemmDesc d;
       memset(&d, 0, sizeof(d));
       d.layout = s.layout;
@@ -209,9 +230,9 @@ int main(int argc, char** argv) {
       d.WM = c[0];
       d.WN = c[1];
       d.WK = c[2];
-      d.tiles_m = (s.M + 32 * c[0] - 1) / (32 * c[0]);
-      d.tiles_n = (s.N + 32 * c[1] - 1) / (32 * c[1]);
-      d.pipe = c[3];
+      d.TM = d.TN = c[3];
+      d.tiles_m = (s.M + 32 * c[3] * c[0] - 1) / (32 * c[3] * c[0]);
+      d.tiles_n = (s.N + 32 * c[3] * c[1] - 1) / (32 * c[3] * c[1]);
       d.a.p0 = A;
       d.a.split = 0x7fffffff;
       d.b.p0 = B;
@@ -238,11 +259,13 @@ int main(int argc, char** argv) {
       d.slope = 0.2f;
       d.C = C;
       d.ldc = s.layout == 2 ? s.N - 1 : s.N;
-      if (c[3] == 1) {  // verify against the direct path on the same inputs
+      if (c[3] == 2) {  // verify against the 1x1-block kernel on the same inputs
         const size_t n = (size_t)s.M * d.ldc;
         std::vector<float> r0(n), r1(n);
         CglGemmDesc d0 = d;
-        d0.pipe = 0;
+        d0.TM = d0.TN = 1;
+        d0.tiles_m = (s.M + 32 * c[0] - 1) / (32 * c[0]);
+        d0.tiles_n = (s.N + 32 * c[1] - 1) / (32 * c[1]);
         CK(hipMemset(C, 0, n * 4));
         (void)time_desc(d0, dd, 1);
         CK(hipDeviceSynchronize());
@@ -257,6 +280,7 @@ int main(int argc, char** argv) {
           den += (double)r0[i] * r0[i];
         }
         if (!(num <= 1e-10 * den)) printf(" [MISMATCH rel %.2e] ", sqrt(num / (den + 1e-30)));
+        if (s.layout == 2 && d.bias_out) { /* bias column compared through C only */ }
       }
       const double us = time_desc(d, dd, reps);
       const double flop = 2.0 * s.M * s.N * s.K;
