@@ -9,7 +9,7 @@
 //  cgl_adam        flat multi-tensor Adam, op order of torch 2.10 _single_tensor_adam
 //                  (optim.Adam(lr=2e-4, betas=(0.5, 0.999)) capgan.py:158,312), plus the scalar
 //                  tail of the round (lambda SGD capgan.py:140-141,259; F_max :249).
-//  cgl_step_begin  per-round counters and Adam bias corrections (device-side, graph-replayable).
+//  cgl_begin_at    per-round Adam bias corrections (device-side, graph-replayable).
 //  cgl_normal      Philox4x32-10 + Box-Muller N(0,1) for z (capgan.py:216,219).
 //  cgl_alpha_scale lambda-weighting of gathered worker losses (capgan.py:247-248,
 //                  mixed-gan.py:276, MDGAN/MNIST/mdgan.py:203, CGLGAN/2DMG/main.py:261-264) and the
@@ -24,12 +24,15 @@ __device__ __forceinline__ float cgl_wave_sum(float x) {
   return x;
 }
 
+#define CGL_HEAD_MAXQ 4   // float4 per lane kept in registers: F <= 1024
 __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restrict__ hd) {
-  // Each wave owns rows r0 + wave + 4 i; a row is a dot product of F features (F % 4 == 0) done
-  // with 16-byte global loads, a 64-lane reduction, the loss and its gradient, then the
-  // gradient into the last hidden layer (dlogits . W) * LeakyReLU'(P).
+  // Each wave owns rows r0 + wave + 4 i; a row is a dot product of F features (F % 4 == 0)
+  // over 16-byte loads held in registers, a 64-lane reduction, the loss and its gradient, then
+  // the gradient into the last hidden layer (dlogits . W) * LeakyReLU'(P) from the same
+  // registers.  The batch-mean losses are reduced by the last workgroup to arrive.
   __shared__ float s_loss[4][2];
   __shared__ int s_last;
+  __shared__ float s_part[2 * 1024];
   const int M = hd->M, F = hd->F, C = hd->C;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -38,22 +41,35 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
   const float* __restrict__ Pb = hd->P;
   const float* __restrict__ W = hd->W;
   const int F4 = F >> 2;
+  const float b0 = gld(hd->b), b1 = C == 2 ? gld(hd->b + 1) : 0.f;
+  // W rows (same for every row of the batch)
+  f32x4 w0[CGL_HEAD_MAXQ], w1[CGL_HEAD_MAXQ];
+#pragma unroll
+  for (int u = 0; u < CGL_HEAD_MAXQ; ++u) {
+    const int q = min(lane + 64 * u, F4 - 1);
+    w0[u] = *(gcf4p)(W + 4 * q);
+    w1[u] = C == 2 ? *(gcf4p)(W + F + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   float lsum[2] = {0.f, 0.f};
   for (int r = r0 + wave; r < r1; r += 4) {
     const float* p = Pb + (long)r * hd->ldp;
-    float z[2] = {0.f, 0.f};
-    for (int c = 0; c < C; ++c) {
-      float s = 0.f;
-      for (int q = lane; q < F4; q += 64) {
-        const f32x4 pv = *(gcf4p)(p + 4 * q);
-        const f32x4 wv = *(gcf4p)(W + (long)c * F + 4 * q);
-        s = fmaf(pv[0], wv[0], s);
-        s = fmaf(pv[1], wv[1], s);
-        s = fmaf(pv[2], wv[2], s);
-        s = fmaf(pv[3], wv[3], s);
+    f32x4 pv[CGL_HEAD_MAXQ];
+#pragma unroll
+    for (int u = 0; u < CGL_HEAD_MAXQ; ++u) pv[u] = *(gcf4p)(p + 4 * min(lane + 64 * u, F4 - 1));
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int u = 0; u < CGL_HEAD_MAXQ; ++u) {
+      if (lane + 64 * u < F4) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s0 = fmaf(pv[u][e], w0[u][e], s0);
+          s1 = fmaf(pv[u][e], w1[u][e], s1);
+        }
       }
-      z[c] = cgl_wave_sum(s) + gld(hd->b + c);
     }
+    float z[2];
+    z[0] = cgl_wave_sum(s0) + b0;
+    z[1] = C == 2 ? cgl_wave_sum(s1) + b1 : 0.f;
     const int seg = r < hd->split ? 0 : 1;
     const int t = seg ? hd->t1 : hd->t0;
     const float wgt = seg ? hd->w1 : hd->w0;
@@ -84,20 +100,21 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
     if (hd->dP) {
       float* dp = hd->dP + (long)r * hd->lddp;
       const float sl = hd->slope;
-      for (int q = lane; q < F4; q += 64) {
-        const f32x4 pv = *(gcf4p)(p + 4 * q);
-        const f32x4 w0 = *(gcf4p)(W + 4 * q);
-        f32x4 g = dl[0] * w0;
-        if (C == 2) {
-          const f32x4 w1 = *(gcf4p)(W + F + 4 * q);
-          g[0] = fmaf(dl[1], w1[0], g[0]);
-          g[1] = fmaf(dl[1], w1[1], g[1]);
-          g[2] = fmaf(dl[1], w1[2], g[2]);
-          g[3] = fmaf(dl[1], w1[3], g[3]);
+#pragma unroll
+      for (int u = 0; u < CGL_HEAD_MAXQ; ++u) {
+        const int q = lane + 64 * u;
+        if (q < F4) {
+          f32x4 g = dl[0] * w0[u];
+          if (C == 2) {
+            g[0] = fmaf(dl[1], w1[u][0], g[0]);
+            g[1] = fmaf(dl[1], w1[u][1], g[1]);
+            g[2] = fmaf(dl[1], w1[u][2], g[2]);
+            g[3] = fmaf(dl[1], w1[u][3], g[3]);
+          }
+          f32x4 o;
+          for (int e = 0; e < 4; ++e) o[e] = pv[u][e] > 0.f ? g[e] : g[e] * sl;
+          *(gf4p)(dp + 4 * q) = o;
         }
-        f32x4 o;
-        for (int e = 0; e < 4; ++e) o[e] = pv[e] > 0.f ? g[e] : g[e] * sl;
-        *(gf4p)(dp + 4 * q) = o;
       }
     }
   }
@@ -122,29 +139,39 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
     const unsigned int ticket =
         __hip_atomic_fetch_add(hd->counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = (ticket == gridDim.x - 1);
-    if (s_last) {
-      double s0 = 0.0, s1 = 0.0;
-      for (unsigned int q = 0; q < gridDim.x; ++q) {
-        s0 += (double)__hip_atomic_load((CGL_GLOBAL float*)(hd->part + q * 2 + 0), __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-        s1 += (double)__hip_atomic_load((CGL_GLOBAL float*)(hd->part + q * 2 + 1), __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-      }
-      const int n0 = min(hd->split, M), n1 = M - n0;
-      const float l0 = n0 > 0 ? (float)(s0 / n0) : 0.f;
-      const float l1 = n1 > 0 ? (float)(s1 / n1) : 0.f;
-      gst(hd->loss_out, l0);
-      gst(hd->loss_out + 1, l1);
-      if (hd->combine_out) gst(hd->combine_out, (l0 + l1) * hd->combine);
-      __hip_atomic_store(hd->counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // every thread loads partials at once (one round trip), thread 0 sums them in a fixed order
+  const int np = 2 * gridDim.x;
+  for (int i = threadIdx.x; i < np; i += 256)
+    s_part[i] = __hip_atomic_load((CGL_GLOBAL float*)(hd->part + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s0 = 0.0, s1 = 0.0;
+    for (unsigned int q = 0; q < gridDim.x; ++q) {
+      s0 += (double)s_part[2 * q];
+      s1 += (double)s_part[2 * q + 1];
     }
+    const int n0 = min(hd->split, M), n1 = M - n0;
+    const float l0 = n0 > 0 ? (float)(s0 / n0) : 0.f;
+    const float l1 = n1 > 0 ? (float)(s1 / n1) : 0.f;
+    gst(hd->loss_out, l0);
+    gst(hd->loss_out + 1, l1);
+    if (hd->combine_out) gst(hd->combine_out, (l0 + l1) * hd->combine);
+    __hip_atomic_store(hd->counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
 // ------------------------------------------------------------------------------------------
 // BatchNorm1d backward (train) + LeakyReLU' mask.  One workgroup owns 32 features and all M
-// rows, so the per-feature reductions stay inside the workgroup (fixed order, double accum).
-// Rows are processed in unrolled blocks of 8 so that 24 independent loads are in flight.
+// rows, so the per-feature reductions stay inside the workgroup (fixed order, double accum):
+//   dy = dA * leaky'(post),  S = sum dy,  D = sum (y - mean) dy,
+//   dZ = (dy - S/M - (y - mean) D invstd^2 / M) invstd gamma,  dgamma = D invstd,  dbeta = S
+// (torch's batch_norm_backward, train mode).  With M <= 8 * CGL_BNB_RPT every thread keeps its
+// rows in registers: all loads are issued at once (one memory round trip) and the second pass
+// reuses them; larger M streams the rows twice.
+#define CGL_BNB_RPT 32
 __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict__ bd) {
   __shared__ double s_a[8][32], s_b[8][32];
   const int M = bd->M, F = bd->F;
@@ -155,11 +182,53 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
   const float sl = bd->slope;
   const float mean = gld(bd->mean + fc);
   const float invstd = gld(bd->invstd + fc);
+  const float w = gld(bd->gamma + fc);
   const float* dA = bd->dA + fc;
   const float* post = bd->post + fc;
   const float* Y = bd->Y + fc;
   const long lda = bd->ld_da, ldp = bd->ld_post, ldy = bd->ld_y;
+  float* dZ = bd->dZ + fc;
+  const long ldz = bd->ld_dz;
   double sum = 0.0, dotp = 0.0;
+  if (M <= 8 * CGL_BNB_RPT) {
+    float dy[CGL_BNB_RPT], yc[CGL_BNB_RPT];
+#pragma unroll
+    for (int j = 0; j < CGL_BNB_RPT; ++j) {
+      const int r = min(rg + 8 * j, M - 1);
+      const float da = gld(dA + r * lda), po = gld(post + r * ldp), y = gld(Y + r * ldy);
+      dy[j] = po > 0.f ? da : da * sl;
+      yc[j] = y - mean;
+    }
+#pragma unroll
+    for (int j = 0; j < CGL_BNB_RPT; ++j) {
+      if (rg + 8 * j < M) {
+        sum += (double)dy[j];
+        dotp += (double)(yc[j] * dy[j]);
+      }
+    }
+    s_a[rg][fl] = sum;
+    s_b[rg][fl] = dotp;
+    __syncthreads();
+    double S = 0.0, D = 0.0;
+    for (int q = 0; q < 8; ++q) {
+      S += s_a[q][fl];
+      D += s_b[q][fl];
+    }
+    const float k = (float)D * invstd * invstd / M;
+    const float gmean = (float)(S / M);
+    if (fok) {
+#pragma unroll
+      for (int j = 0; j < CGL_BNB_RPT; ++j) {
+        const int r = rg + 8 * j;
+        if (r < M) gst(dZ + r * ldz, (dy[j] - gmean - yc[j] * k) * invstd * w);
+      }
+      if (rg == 0) {
+        gst(bd->g_gamma + f, (float)(D * (double)invstd));
+        gst(bd->g_beta + f, (float)S);
+      }
+    }
+    return;
+  }
   for (int r0 = rg; r0 < M; r0 += 64) {
     float da[8], po[8], y[8];
 #pragma unroll
@@ -187,11 +256,8 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
     D += s_b[q][fl];
   }
   if (!fok) return;
-  const float w = gld(bd->gamma + f);
   const float k = (float)D * invstd * invstd / M;
   const float gmean = (float)(S / M);
-  float* dZ = bd->dZ + f;
-  const long ldz = bd->ld_dz;
   for (int r0 = rg; r0 < M; r0 += 64) {
     float da[8], po[8], y[8];
 #pragma unroll
@@ -280,7 +346,7 @@ __global__ __launch_bounds__(256) void cgl_adam(CglAdamArgs a, CglStepState* st,
   }
   if (tail && i == 0) {
     // scalar tail of Server.train: F_max and the lambda update (after every parameter read
-    // of this round, before the next round's step_begin).
+    // of this round, before the next round's prologue).
     const int N = st->n_workers;
     const float lam = st->lambda;
     float l[CGL_MAX_WORKERS];
@@ -317,6 +383,7 @@ __global__ __launch_bounds__(256) void cgl_adam(CglAdamArgs a, CglStepState* st,
       // optim.SGD([Lambda], lr=0.1): dF/dLambda = -0.001
       st->lambda = lam + (-0.1f) * (-0.001f);
     }
+    st->round = st->round + 1;   // round complete (read by the next round's prologue)
   }
 }
 
@@ -328,11 +395,13 @@ struct CglBeginArgs {
   int bn_layers;
 };
 
-__global__ void cgl_step_begin(CglBeginArgs a) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// Per-round scalars of round r (1-based): Adam bias corrections of the G update and of every
+// local D step (torch's step counters: G steps once per round, D `epoch` times), alpha reset,
+// BatchNorm num_batches_tracked (two train-mode forward calls per round).  Runs in the round
+// prologue; the round counter itself is advanced by the G-Adam tail at the end of the round,
+// so that no kernel reads a counter another block of the same launch is writing.
+__device__ void cgl_begin_at(const CglBeginArgs& a, int r) {
   CglStepState* st = a.st;
-  const int r = st->round + 1;
-  st->round = r;
   {
     const double t = (double)r;
     const double bc1 = 1.0 - pow(a.b1, t);
@@ -366,11 +435,11 @@ __device__ __forceinline__ void cgl_philox(uint32_t c[4], uint32_t k0, uint32_t 
   }
 }
 
-__global__ __launch_bounds__(256) void cgl_normal(float* out, long n, unsigned long long seed,
-                                                  const CglStepState* st, int stream_id) {
-  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;   // 4 outputs per thread
+// outputs 4q .. 4q+3 of the N(0,1) stream (seed, round, stream_id)
+__device__ __forceinline__ void cgl_normal_at(long q, float* out, long n, unsigned long long seed, uint32_t round,
+                                              int stream_id) {
   if (q * 4 >= n) return;
-  uint32_t c[4] = {(uint32_t)q, (uint32_t)(q >> 32), (uint32_t)(st ? st->round : 0), (uint32_t)stream_id};
+  uint32_t c[4] = {(uint32_t)q, (uint32_t)(q >> 32), round, (uint32_t)stream_id};
   cgl_philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
   const float inv = 2.3283064365386963e-10f;   // 2^-32
   float z[4];
@@ -386,6 +455,11 @@ __global__ __launch_bounds__(256) void cgl_normal(float* out, long n, unsigned l
   }
   for (int j = 0; j < 4; ++j)
     if (q * 4 + j < n) out[q * 4 + j] = z[j];
+}
+
+__global__ __launch_bounds__(256) void cgl_normal(float* out, long n, unsigned long long seed, int round,
+                                                  int stream_id) {
+  cgl_normal_at((long)blockIdx.x * blockDim.x + threadIdx.x, out, n, seed, (uint32_t)round, stream_id);
 }
 
 // ------------------------------------------------------------------------------------------

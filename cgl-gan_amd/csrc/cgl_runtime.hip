@@ -63,6 +63,8 @@ int64_t running_layout(const cgl_mlp_spec& s, int64_t* mean_off, int64_t* var_of
   return off;
 }
 
+constexpr int kHeadRows = 4;     // one row per wave of a head workgroup
+
 int validate(const cgl_gan_config* c) {
   if (!c) return CGL_E_ARG;
   const cgl_mlp_spec &g = c->g, &d = c->d;
@@ -82,6 +84,8 @@ int validate(const cgl_gan_config* c) {
   if (c->loss == CGL_LOSS_CE2 && C != 2) return CGL_E_ARG;
   if (c->loss == CGL_LOSS_BCE && C != 1) return CGL_E_ARG;
   if (d.dims[d.n_layers - 1] % 4 != 0) return CGL_E_ARG;  // loss head reads 16-byte vectors
+  if (d.dims[d.n_layers - 1] > 4 * 64 * CGL_HEAD_MAXQ) return CGL_E_ARG;  // head keeps a row in registers
+  if ((c->batch_real + c->batch + kHeadRows - 1) / kHeadRows > 1024) return CGL_E_ARG;  // head partials in LDS
   if (c->loss != CGL_LOSS_CE2 && c->loss != CGL_LOSS_BCE) return CGL_E_ARG;
   if (c->batch < 2 || c->batch_real < 1 || c->epoch < 1 || c->epoch > CGL_MAX_EPOCH) return CGL_E_ARG;
   if (c->n_workers < 1 || c->n_workers > CGL_MAX_WORKERS || c->rank < 0 || c->rank >= c->n_workers)
@@ -110,7 +114,6 @@ struct Carve {
 constexpr int kMaxGemmDescs = 128;
 constexpr int kMaxHeadDescs = 2 * CGL_MAX_EPOCH + 4;
 constexpr int kMaxBnDescs = 2 * CGL_MAX_LAYERS;
-constexpr int kHeadRows = 16;
 constexpr int kCounters = 64;
 
 struct WS {
@@ -185,7 +188,7 @@ WS carve_ws(const cgl_gan_config& c, void* base) {
 }
 
 // ----------------------------------------------------------------------------------------
-enum LaunchKind { K_GEMM, K_HEAD, K_BNBWD, K_ADAM, K_BEGIN, K_NORMAL, K_SAMPLE, K_ALPHA };
+enum LaunchKind { K_GEMM, K_HEAD, K_BNBWD, K_ADAM, K_PROLOGUE };
 
 struct Launch {
   LaunchKind kind;
@@ -194,8 +197,9 @@ struct Launch {
   CglAdamArgs adam{};
   int tail = 0;
   CglBeginArgs begin{};
-  float* nptr = nullptr;
+  float* nptr = nullptr;  // prologue: z buffer, its length, normal / sampler block counts
   long nn = 0;
+  int nb_norm = 0, nb_samp = 0;
   int stream_id = 0;
   double flops = 0.0;
   int shmem = 0;        // dynamic LDS bytes (GEMM)
@@ -447,33 +451,28 @@ int build_plan(cgl_gan* c) {
   std::vector<Launch>& A = c->phA;
   std::vector<Launch>& Bp = c->phB;
 
-  // ---- round prologue
-  {
-    Launch Lb;
-    Lb.kind = K_BEGIN;
-    Lb.begin.st = st;
-    Lb.begin.epoch = cf.epoch;
-    Lb.begin.lr_g = cf.lr_g;
-    Lb.begin.lr_d = cf.lr_d;
-    Lb.begin.b1 = cf.beta1;
-    Lb.begin.b2 = cf.beta2;
-    A.push_back(Lb);
-  }
-  if (cf.gen_z) {
-    Launch Ln;
-    Ln.kind = K_NORMAL;
-    Ln.nptr = c->bufs.z;
-    Ln.nn = (long)2 * B * g.dims[0];
-    Ln.grid = (int)((Ln.nn / 4 + 255) / 256 + 1);
-    A.push_back(Ln);
-  }
+  // ---- round prologue: per-round scalars, z draw, real-batch sampling (one launch)
   const int* real_idx = c->bufs.real_idx;
-  if (cf.sample_n > 0) {
-    Launch Ls;
-    Ls.kind = K_SAMPLE;
-    Ls.grid = (cf.epoch * Br + 255) / 256;
-    A.push_back(Ls);
-    real_idx = w.idx;
+  {
+    Launch Lp;
+    Lp.kind = K_PROLOGUE;
+    Lp.begin.st = st;
+    Lp.begin.epoch = cf.epoch;
+    Lp.begin.lr_g = cf.lr_g;
+    Lp.begin.lr_d = cf.lr_d;
+    Lp.begin.b1 = cf.beta1;
+    Lp.begin.b2 = cf.beta2;
+    if (cf.gen_z) {
+      Lp.nptr = c->bufs.z;
+      Lp.nn = (long)2 * B * g.dims[0];
+      Lp.nb_norm = (int)((Lp.nn / 4 + 255) / 256);
+    }
+    if (cf.sample_n > 0) {
+      Lp.nb_samp = (cf.epoch * Br + 255) / 256;
+      real_idx = w.idx;
+    }
+    Lp.grid = 1 + Lp.nb_norm + Lp.nb_samp;
+    A.push_back(Lp);
   }
 
   // ---- G forward on [z1; z2] (2B rows; BatchNorm statistics per B-row forward call)
@@ -811,12 +810,27 @@ __device__ uint32_t cgl_permute(uint32_t i, uint32_t n, uint32_t key) {
   return x;
 }
 
-__global__ void cgl_sample(int* idx, const CglStepState* st, int epoch, int br, int n, unsigned long long seed) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+// Round prologue: block 0 writes the round's scalars, the next nb_norm blocks draw z, the
+// last blocks draw the real-row indices of this round's local D steps.  Every block reads the
+// completed-round counter, which only the G-Adam tail (a later launch) advances.
+__global__ __launch_bounds__(256) void cgl_round_prologue(CglBeginArgs a, float* z, long nz, unsigned long long zseed,
+                                                          int nb_norm, int* idx, int epoch, int br, int n,
+                                                          unsigned long long sseed) {
+  const int done = a.st->round;
+  const int bid = blockIdx.x;
+  if (bid == 0) {
+    if (threadIdx.x == 0) cgl_begin_at(a, done + 1);
+    return;
+  }
+  if (bid <= nb_norm) {
+    cgl_normal_at((long)(bid - 1) * 256 + threadIdx.x, z, nz, zseed, (uint32_t)(done + 1), 0);
+    return;
+  }
+  const int t = (bid - 1 - nb_norm) * 256 + threadIdx.x;
   if (t >= epoch * br) return;
-  const long pos = ((long)(st->round - 1) * epoch) * br + t;
+  const long pos = ((long)done * epoch) * br + t;
   const uint32_t ep = (uint32_t)(pos / n), j = (uint32_t)(pos % n);
-  idx[t] = (int)cgl_permute(j, (uint32_t)n, (uint32_t)seed ^ (ep * 0x85ebca6bu + 0x1234567u));
+  idx[t] = (int)cgl_permute(j, (uint32_t)n, (uint32_t)sseed ^ (ep * 0x85ebca6bu + 0x1234567u));
 }
 
 int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s) {
@@ -833,15 +847,10 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s) {
     case K_ADAM:
       hipLaunchKernelGGL(cgl_adam, dim3(L.grid), dim3(256), 0, s, L.adam, c->ws.st, L.tail);
       break;
-    case K_BEGIN:
-      hipLaunchKernelGGL(cgl_step_begin, dim3(1), dim3(64), 0, s, L.begin);
-      break;
-    case K_NORMAL:
-      hipLaunchKernelGGL(cgl_normal, dim3(L.grid), dim3(256), 0, s, L.nptr, L.nn, c->cfg.seed, c->ws.st, 0);
-      break;
-    case K_SAMPLE:
-      hipLaunchKernelGGL(cgl_sample, dim3(L.grid), dim3(256), 0, s, c->ws.idx, c->ws.st, c->cfg.epoch,
-                         c->cfg.batch_real, c->cfg.sample_n, c->cfg.seed ^ 0x5bd1e995ULL);
+    case K_PROLOGUE:
+      hipLaunchKernelGGL(cgl_round_prologue, dim3(L.grid), dim3(256), 0, s, L.begin, L.nptr, L.nn, c->cfg.seed,
+                         L.nb_norm, c->ws.idx, c->cfg.epoch, c->cfg.batch_real, c->cfg.sample_n,
+                         c->cfg.seed ^ 0x5bd1e995ULL);
       break;
     default:
       return CGL_E_STATE;
@@ -1236,10 +1245,9 @@ int cgl_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int s
 
 int cgl_normal_fill(float* out, int64_t n, unsigned long long seed, int round, int stream_id, void* stream) {
   if (!out || n < 0) return CGL_E_ARG;
-  (void)round;
   if (n == 0) return 0;
-  hipLaunchKernelGGL(cgl_normal, dim3((unsigned)((n / 4 + 255) / 256 + 1)), dim3(256), 0, (hipStream_t)stream, out,
-                     (long)n, seed, (const CglStepState*)nullptr, stream_id);
+  hipLaunchKernelGGL(cgl_normal, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, out,
+                     (long)n, seed, round, stream_id);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }
