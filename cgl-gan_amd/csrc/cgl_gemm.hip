@@ -13,13 +13,12 @@
 //  * operands are loaded straight into the MFMA fragment registers.  The k index of the
 //    32x32x2 fragment is permuted so that lane half h owns 8 CONSECUTIVE k of every 16-k
 //    chunk: a k-contiguous operand is then two float4 loads per lane per 8 MFMAs;
-//  * prologue fusion: the A operand can be the pre-BatchNorm output of the previous layer;
-//    the workgroup combines the producer's {sum, M2} partials into a scale/shift table in
-//    LDS and applies BatchNorm1d(train) + LeakyReLU while loading (the reference's
-//    BN/LeakyReLU kernels disappear), optionally writing the transformed rows out once;
+//  * prologue fusion: the A operand rows can be gathered through an index list (the sampled
+//    real batch) from two sources (real rows, then generated rows) and written out once;
 //  * epilogue fusion: bias, LeakyReLU / Tanh, LeakyReLU' mask, Tanh' (1 - t^2), the
 //    bias-gradient column (B's extra all-ones column), and per-column {sum, M2} partials of
-//    the stored output for the next layer's BatchNorm, grouped per forward call.
+//    the stored output for the next layer's BatchNorm, grouped per forward call (combined by
+//    cgl_bn_apply, cgl_kernels.hip).
 #include "cgl_internal.h"
 
 #include <type_traits>
@@ -71,112 +70,6 @@ __device__ __forceinline__ void cgl_mask(float v[8], bool ok, int k, int K) {
   for (int j = 0; j < 8; ++j) v[j] = (ok && k + j < K) ? v[j] : 0.f;
 }
 
-// BatchNorm statistics of group g for Q features k[q] (k[q] < 0: unused) from the producer
-// partials: the exact parallel combination of per-tile {S_t, M2_t} over c_t rows, in double
-// like torch's CPU kernel and in a fixed tile order,
-//   mean = sum_t S_t / n,   M2 = sum_t (M2_t + c_t (S_t / c_t - mean)^2).
-// Fast path (<= 8 tiles per group): every {S_t, M2_t} pair of the Q features is loaded up front
-// as one 8-byte load, so the whole computation costs a single memory round trip.
-template <int Q>
-__device__ __forceinline__ void cgl_bn_stats(const CglBnFwd& bn, int K, const int (&k)[Q], int g, double (&mean)[Q],
-                                             double (&m2)[Q], int& n) {
-  typedef float f32x2 __attribute__((ext_vector_type(2)));
-  const int r0 = g * bn.gr, r1 = min(r0 + bn.gr, bn.mtot);
-  n = r1 - r0;
-  const int t0 = r0 / bn.part_bm, t1 = (r1 - 1) / bn.part_bm;
-  const int nt = t1 - t0 + 1;
-  if (nt <= 8) {
-    f32x2 pr[Q][8];
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int kk = max(k[q], 0);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int t = t0 + min(j, nt - 1);
-        const int slot = (t * bn.part_bm < r0) ? 1 : 0;   // tile starts in the previous group
-        pr[q][j] = *(const CGL_GLOBAL f32x2*)(bn.part + ((long)(t * 2 + slot) * K + kk) * 2);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      double s = 0.0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j < nt) s += (double)pr[q][j][0];
-      const double mu = s / n;
-      double acc = 0.0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (j < nt) {
-          const int t = t0 + j;
-          const int c = min((t + 1) * bn.part_bm, r1) - max(t * bn.part_bm, r0);
-          const double dd = (double)pr[q][j][0] / c - mu;
-          acc += (double)pr[q][j][1] + c * dd * dd;
-        }
-      }
-      mean[q] = mu;
-      m2[q] = acc;
-    }
-    return;
-  }
-  for (int q = 0; q < Q; ++q) {
-    const int kk = max(k[q], 0);
-    double s = 0.0;
-    for (int t = t0; t <= t1; ++t) {
-      const int slot = (t * bn.part_bm < r0) ? 1 : 0;
-      s += (double)gld(bn.part + ((long)(t * 2 + slot) * K + kk) * 2);
-    }
-    const double mu = s / n;
-    double acc = 0.0;
-    for (int t = t0; t <= t1; ++t) {
-      const int slot = (t * bn.part_bm < r0) ? 1 : 0;
-      const float* pp = bn.part + ((long)(t * 2 + slot) * K + kk) * 2;
-      const int c = min((t + 1) * bn.part_bm, r1) - max(t * bn.part_bm, r0);
-      const double dd = (double)gld(pp) / c - mu;
-      acc += (double)gld(pp + 1) + c * dd * dd;
-    }
-    mean[q] = mu;
-    m2[q] = acc;
-  }
-}
-
-// Saved statistics (for the backward pass) and running statistics of the 64-feature block
-// `blk`, every group in the order of the reference's forward calls (Xd then Xg,
-// capgan.py:215-220): torch's momentum update with the unbiased variance.
-__device__ void cgl_bn_block_side(const CglBnFwd& bn, int K, int blk) {
-  __shared__ double s_mean[2][64], s_m2[2][64];
-  __shared__ int s_n[2];
-  const int ngroups = (bn.mtot + bn.gr - 1) / bn.gr;   // <= 2
-  const int tid = threadIdx.x;
-  if (tid < 64 * ngroups) {
-    const int g = tid >> 6, c = tid & 63;
-    const int kk = blk * 64 + c;
-    const int k[1] = {kk < K ? kk : -1};
-    double mean[1], m2[1];
-    int n;
-    cgl_bn_stats<1>(bn, K, k, g, mean, m2, n);
-    s_mean[g][c] = mean[0];
-    s_m2[g][c] = m2[0];
-    if (c == 0) s_n[g] = n;
-    if (kk < K && bn.save_mean) {
-      gst(bn.save_mean + (long)g * K + kk, (float)mean[0]);
-      gst(bn.save_invstd + (long)g * K + kk, (float)(1.0 / sqrt(m2[0] / n + bn.eps)));
-    }
-  }
-  __syncthreads();
-  const int kk = blk * 64 + tid;
-  if (bn.run_mean && tid < 64 && kk < K) {
-    const double mom = bn.momentum;
-    float rm = gld(bn.run_mean + kk), rv = gld(bn.run_var + kk);
-    for (int g = 0; g < ngroups; ++g) {
-      rm = (float)(mom * s_mean[g][tid] + (1.0 - mom) * (double)rm);
-      rv = (float)(mom * (s_m2[g][tid] / (s_n[g] - 1)) + (1.0 - mom) * (double)rv);
-    }
-    gst(bn.run_mean + kk, rm);
-    gst(bn.run_var + kk, rv);
-  }
-}
-
 // ------------------------------------------------------------------------------------------
 // Main body.  One wave owns TM x TN 32x32 accumulator blocks ((32 TM) x (32 TN) outputs); the
 // workgroup tile is (32 TM WM) x (32 TN WN), K split WK ways.  Operand fragments of S chunks
@@ -189,8 +82,8 @@ struct CglPipe {
 };
 
 template <int LAYOUT, int VEC, int TM, int TN>
-__device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d, int bid, float* __restrict__ s_tf,
-                                              float* __restrict__ s_red, float* __restrict__ s_col) {
+__device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d, int bid, float* __restrict__ s_red,
+                                              float* __restrict__ s_col) {
   constexpr int S = CglPipe<TM, TN>::S;
   const int M = d->M, N = d->N, K = d->K;
   const int WN = d->WN, WK = d->WK, WM = d->WM;
@@ -215,53 +108,6 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   const int m0 = tm * BM + wm * 32 * TM;            // first row of this wave's tile
   const int n0 = (tn * WN + wn) * 32 * TN;          // first column of this wave's tile
 
-  // ---------------- BatchNorm prologue: scale/shift pairs of the group(s) of this row tile,
-  // four features per thread with one memory round trip; pairs past K (up to the next
-  // multiple of 8) are zero, so the transform of a clamped tail load is 0
-  const int a_tf = (LAYOUT != 2) ? d->a_tf : 0;
-  int g0 = 0;
-  if (a_tf) {
-    const CglBnFwd& bn = d->bn;
-    const int rlast = min(tm * BM + BM, M) - 1;
-    g0 = (tm * BM) / bn.gr;
-    const int g1 = rlast / bn.gr;
-    const int Kp = (K + 7) & ~7;
-    for (int g = g0; g <= g1; ++g) {
-      float* dst = s_tf + (g - g0) * CGL_TF_MAXK * 2;
-      for (int kb = 0; kb < Kp; kb += 4 * CGL_GEMM_THREADS) {
-        int k[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int kk = kb + q * CGL_GEMM_THREADS + tid;
-          k[q] = kk < K ? kk : -1;
-        }
-        double mean[4], m2[4];
-        int n;
-        cgl_bn_stats<4>(bn, K, k, g, mean, m2, n);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int kk = kb + q * CGL_GEMM_THREADS + tid;
-          if (kk < Kp) {
-            float sc = 0.f, sh = 0.f;
-            if (k[q] >= 0) {
-              const double invstd = 1.0 / sqrt(m2[q] / n + bn.eps);
-              sc = (float)invstd * gld(bn.gamma + kk);
-              sh = gld(bn.beta + kk) - (float)mean[q] * sc;
-            }
-            dst[2 * kk] = sc;
-            dst[2 * kk + 1] = sh;
-          }
-        }
-      }
-    }
-    // saved / running statistics: 64-feature blocks spread over the first workgroups
-    if (bn.run_mean || bn.save_mean) {
-      const int nblk = (K + 63) / 64;
-      for (int blk = local; blk < nblk; blk += nwg) cgl_bn_block_side(bn, K, blk);
-    }
-    __syncthreads();
-  }
-
   // ---------------- main loop
   const int b_ones = (LAYOUT != 0) ? d->b_ones_col : 0;
   const int nmem = N - b_ones;     // columns of B actually in memory
@@ -276,21 +122,17 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   const int nch = (K + CGL_GEMM_KCHUNK - 1) / CGL_GEMM_KCHUNK;
   const int cb = (wk * nch) / WK, ce = ((wk + 1) * nch) / WK;
   const int lda = d->a.ld, ldb = d->b.ld;
-  const float slope_tf = d->bn.slope;
   float* __restrict__ a_copy = d->a_copy;
 
   // per-lane operand rows / columns of each block, clamped (always dereferenceable) bases
   const float* a_base[TM];
   const float* b_base[TN];
-  bool a_ok[TM], b_is_ones[TN], do_copy[TM];
-  int gsel[TM];
+  bool b_is_ones[TN], do_copy[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int am = m0 + 32 * i + li;      // A row (kc) or A column (mn)
-    a_ok[i] = am < M;
     a_base[i] = (LAYOUT != 2) ? cgl_row(d->a, min(am, M - 1)) : d->a.p0 + min(am, M - 1);
-    gsel[i] = a_tf ? (a_ok[i] ? am / d->bn.gr - g0 : 0) : 0;
-    do_copy[i] = (LAYOUT != 2) && a_copy && tn == 0 && wn == 0 && a_ok[i] && am >= d->a_copy_row0;
+    do_copy[i] = (LAYOUT != 2) && a_copy && tn == 0 && wn == 0 && am < M && am >= d->a_copy_row0;
   }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -358,18 +200,6 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       if (T) cgl_mask(A_[i], true, k, K);
-      if (a_tf) {
-        // {scale, shift} of k..k+7 (k % 8 == 0): four 16-byte LDS reads, zero pairs past K
-        const f32x4* t4 = (const f32x4*)(s_tf + (gsel[i] * CGL_TF_MAXK + k) * 2);
-        const f32x4 p0 = t4[0], p1 = t4[1], p2 = t4[2], p3 = t4[3];
-        const float sc[8] = {p0[0], p0[2], p1[0], p1[2], p2[0], p2[2], p3[0], p3[2]};
-        const float sh[8] = {p0[1], p0[3], p1[1], p1[3], p2[1], p2[3], p3[1], p3[3]};
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float x = fmaf(A_[i][j], sc[j], sh[j]);
-          A_[i][j] = x > 0.f ? x : x * slope_tf;
-        }
-      }
       if (do_copy[i]) {
         float* dst = a_copy + (long)(m0 + 32 * i + li) * d->a_copy_ld;
         if (VEC && (!T || k + 7 < K)) {
@@ -622,15 +452,12 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 // launch may mix layouts (e.g. the weight gradient (TN) and the input gradient (NN) of one
 // layer side by side).  Separate symbols keep the 1x1 variant's register budget (and so its
 // occupancy) independent of the 2x2 variant's.
-// Dynamic LDS: [tf_floats: BatchNorm scale/shift table (0 when no problem of the launch needs it)]
-//              [split-K partials of the waves with wk > 0]
+// Dynamic LDS: split-K partials of the waves with wk > 0.
 template <int TM, int TN>
-__global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDesc* __restrict__ descs, int ndesc,
-                                                                 int tf_floats) {
+__global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDesc* __restrict__ descs, int ndesc) {
   extern __shared__ float cgl_dyn_lds[];
   __shared__ float s_col[4 * TN * 32];          // per-column reductions across waves (WM WN <= 4)
-  float* s_tf = cgl_dyn_lds;
-  float* s_red = cgl_dyn_lds + tf_floats;
+  float* s_red = cgl_dyn_lds;
   const int bid = blockIdx.x;
   int di = 0;
   for (int q = 1; q < ndesc; ++q)
@@ -642,9 +469,9 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
 #define CGL_BODY(L)                                               \
   do {                                                            \
     if (vec)                                                      \
-      cgl_gemm_body<L, 1, TM, TN>(d, bid, s_tf, s_red, s_col);    \
+      cgl_gemm_body<L, 1, TM, TN>(d, bid, s_red, s_col);    \
     else                                                          \
-      cgl_gemm_body<L, 0, TM, TN>(d, bid, s_tf, s_red, s_col);    \
+      cgl_gemm_body<L, 0, TM, TN>(d, bid, s_red, s_col);    \
   } while (0)
   if (layout == 0)
     CGL_BODY(0);
@@ -655,7 +482,7 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
 #undef CGL_BODY
 }
 
-// Host helper: dynamic LDS bytes of one problem's split-K partials (the BN table is extra).
+// Host helper: dynamic LDS bytes of one problem's split-K partials.
 inline int cgl_gemm_stage_bytes(const CglGemmDesc& d) {
   return (d.WK > 1) ? d.WM * d.WN * (d.WK - 1) * d.TM * d.TN * 16 * 64 * 4 : 0;
 }

@@ -8,7 +8,7 @@
 #define CGL_WAVE 64
 #define CGL_GEMM_THREADS 256
 #define CGL_GEMM_KCHUNK 16           // k per MFMA chunk: 8 per lane half (k-permuted)
-#define CGL_TF_MAXK 1024             // max K for the in-LDS BatchNorm transform table
+#define CGL_BN_MAXF 1024             // max features of a G BatchNorm layer
 
 enum { CGL_EPI_ACT_NONE = 0, CGL_EPI_ACT_LEAKY = 1, CGL_EPI_ACT_TANH = 2 };
 
@@ -37,10 +37,10 @@ struct CglRowSrc {
   int ld;                 // row stride in floats (both segments)
 };
 
-// Forward-BatchNorm transform applied to the A operand as it is loaded (consumer side).
-// The producer GEMM wrote per-(row tile, group slot, feature) partials {sum, M2}; every consumer
-// workgroup combines them (fixed order, double) into the scale/shift pairs of its rows' group,
-// and a few workgroups also write the saved mean/invstd and update the running statistics.
+// Forward BatchNorm of one G layer.  The producer GEMM wrote per-(row tile, group slot,
+// feature) partials {sum, M2}; cgl_bn_apply combines them (fixed order, double) into the
+// per-group mean / invstd, applies BatchNorm1d(train) + LeakyReLU, and updates the saved and
+// running statistics.
 struct CglBnFwd {
   const float* part;      // [ntiles][2][K][2]
   int part_bm;            // producer rows per tile
@@ -50,9 +50,9 @@ struct CglBnFwd {
   const float* beta;
   double eps, momentum;
   float slope;
-  float* run_mean;        // per 64-feature block by one workgroup (group 0 first, then 1), may be null
+  float* run_mean;        // updated group 0 first, then 1 (the reference's call order), may be null
   float* run_var;
-  float* save_mean;       // [ngroups][K] (same workgroups), may be null
+  float* save_mean;       // [ngroups][K], may be null
   float* save_invstd;
 };
 
@@ -65,9 +65,7 @@ struct CglGemmDesc {
   int a_vec, b_vec;       // 16-byte vector loads allowed along each operand's contiguous dim
   int TM, TN;             // 32x32 accumulator blocks per wave (1x1 or 2x2)
   CglRowSrc a, b;
-  // A transform (kc A only)
-  int a_tf;               // 0 none, 1 BatchNorm+LeakyReLU from producer partials
-  CglBnFwd bn;
+  // A copy-out (kc A only)
   float* a_copy;         // optional copy-out of the (transformed) A rows; rows >= a_copy_row0
   int a_copy_ld, a_copy_row0;
   // B extras
@@ -80,6 +78,14 @@ struct CglGemmDesc {
   const float* tanh_ref; int tanh_ld;     // v *= 1 - t*t
   float* stat_part; int stat_gr;          // forward BatchNorm partials of the stored output
   float* bias_out;                     // with b_ones_col: column N-1 of C goes here
+};
+
+// BatchNorm1d(train) + LeakyReLU over the whole [mtot][F] output of one G layer.
+struct CglBnApplyDesc {
+  int F;
+  const float* Y; int ld_y;       // pre-BN (Linear output)
+  float* act; int ld_act;         // post-LeakyReLU
+  CglBnFwd bn;
 };
 
 // D output layer + adversarial loss (+ its backward into the last hidden layer).

@@ -163,6 +163,141 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
   }
 }
 
+// BatchNorm statistics of group g for Q features k[q] (k[q] < 0: unused) from the producer
+// partials: the exact parallel combination of per-tile {S_t, M2_t} over c_t rows, in double
+// like torch's CPU kernel and in a fixed tile order,
+//   mean = sum_t S_t / n,   M2 = sum_t (M2_t + c_t (S_t / c_t - mean)^2).
+// Fast path (<= 8 tiles per group): every {S_t, M2_t} pair of the Q features is loaded up front
+// as one 8-byte load, so the whole computation costs a single memory round trip.
+template <int Q>
+__device__ __forceinline__ void cgl_bn_stats(const CglBnFwd& bn, int K, const int (&k)[Q], int g, double (&mean)[Q],
+                                             double (&m2)[Q], int& n) {
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  const int r0 = g * bn.gr, r1 = min(r0 + bn.gr, bn.mtot);
+  n = r1 - r0;
+  const int t0 = r0 / bn.part_bm, t1 = (r1 - 1) / bn.part_bm;
+  const int nt = t1 - t0 + 1;
+  if (nt <= 8) {
+    f32x2 pr[Q][8];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int kk = max(k[q], 0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int t = t0 + min(j, nt - 1);
+        const int slot = (t * bn.part_bm < r0) ? 1 : 0;   // tile starts in the previous group
+        pr[q][j] = *(const CGL_GLOBAL f32x2*)(bn.part + ((long)(t * 2 + slot) * K + kk) * 2);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      double s = 0.0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j < nt) s += (double)pr[q][j][0];
+      const double mu = s / n;
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (j < nt) {
+          const int t = t0 + j;
+          const int c = min((t + 1) * bn.part_bm, r1) - max(t * bn.part_bm, r0);
+          const double dd = (double)pr[q][j][0] / c - mu;
+          acc += (double)pr[q][j][1] + c * dd * dd;
+        }
+      }
+      mean[q] = mu;
+      m2[q] = acc;
+    }
+    return;
+  }
+  for (int q = 0; q < Q; ++q) {
+    const int kk = max(k[q], 0);
+    double s = 0.0;
+    for (int t = t0; t <= t1; ++t) {
+      const int slot = (t * bn.part_bm < r0) ? 1 : 0;
+      s += (double)gld(bn.part + ((long)(t * 2 + slot) * K + kk) * 2);
+    }
+    const double mu = s / n;
+    double acc = 0.0;
+    for (int t = t0; t <= t1; ++t) {
+      const int slot = (t * bn.part_bm < r0) ? 1 : 0;
+      const float* pp = bn.part + ((long)(t * 2 + slot) * K + kk) * 2;
+      const int c = min((t + 1) * bn.part_bm, r1) - max(t * bn.part_bm, r0);
+      const double dd = (double)gld(pp) / c - mu;
+      acc += (double)gld(pp + 1) + c * dd * dd;
+    }
+    mean[q] = mu;
+    m2[q] = acc;
+  }
+}
+
+// BatchNorm1d(train) + LeakyReLU of one G layer's [mtot][F] output, torch's arithmetic:
+//   invstd = 1 / sqrt(var_biased + eps),  scale = invstd * gamma,  shift = beta - mean * scale,
+//   act = leaky(fma(y, scale, shift))
+// per forward call (group of gr rows).  A workgroup owns 64 features x CGL_BNA_ROWS rows; its
+// first 64 x ngroups threads combine the producer partials of its features (one memory round
+// trip), the row-block-0 workgroups also write the saved mean / invstd for the backward pass and
+// update the running statistics (momentum, unbiased variance) group by group in the order of the
+// reference's forward calls (Xd then Xg, capgan.py:215-220).
+#define CGL_BNA_ROWS 32
+__global__ __launch_bounds__(256) void cgl_bn_apply(const CglBnApplyDesc* __restrict__ ad) {
+  __shared__ float s_sc[2][64], s_sh[2][64];
+  __shared__ double s_mean[2][64], s_m2[2][64];
+  __shared__ int s_n[2];
+  const CglBnFwd& bn = ad->bn;
+  const int F = ad->F, mtot = bn.mtot;
+  const int ngroups = (mtot + bn.gr - 1) / bn.gr;   // <= 2
+  const int tid = threadIdx.x, fl = tid & 63, rl = tid >> 6;
+  const int f0 = blockIdx.x * 64, r0 = blockIdx.y * CGL_BNA_ROWS;
+  const int f = f0 + fl, fc = min(f, F - 1);
+  // this thread's rows, loaded before the statistics are ready
+  constexpr int RPT = CGL_BNA_ROWS / 4;
+  float y[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) y[i] = gld(ad->Y + (long)min(r0 + rl + 4 * i, mtot - 1) * ad->ld_y + fc);
+  if (tid < 64 * ngroups) {
+    const int g = tid >> 6;
+    const int k[1] = {f < F ? f : -1};
+    double mean[1], m2[1];
+    int n;
+    cgl_bn_stats<1>(bn, F, k, g, mean, m2, n);
+    const double invstd = 1.0 / sqrt(m2[0] / n + bn.eps);
+    const float sc = (float)invstd * gld(bn.gamma + fc);
+    s_sc[g][fl] = sc;
+    s_sh[g][fl] = gld(bn.beta + fc) - (float)mean[0] * sc;
+    s_mean[g][fl] = mean[0];
+    s_m2[g][fl] = m2[0];
+    if (fl == 0) s_n[g] = n;
+    if (blockIdx.y == 0 && f < F && bn.save_mean) {
+      gst(bn.save_mean + (long)g * F + f, (float)mean[0]);
+      gst(bn.save_invstd + (long)g * F + f, (float)invstd);
+    }
+  }
+  __syncthreads();
+  if (blockIdx.y == 0 && bn.run_mean && tid < 64 && f < F) {
+    const double mom = bn.momentum;
+    float rm = gld(bn.run_mean + f), rv = gld(bn.run_var + f);
+    for (int g = 0; g < ngroups; ++g) {
+      rm = (float)(mom * s_mean[g][fl] + (1.0 - mom) * (double)rm);
+      rv = (float)(mom * (s_m2[g][fl] / (s_n[g] - 1)) + (1.0 - mom) * (double)rv);
+    }
+    gst(bn.run_mean + f, rm);
+    gst(bn.run_var + f, rv);
+  }
+  if (f >= F) return;
+  const float sl = bn.slope;
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int r = r0 + rl + 4 * i;
+    if (r < mtot) {
+      const int g = r >= bn.gr ? 1 : 0;
+      const float x = fmaf(y[i], s_sc[g][fl], s_sh[g][fl]);
+      gst(ad->act + (long)r * ad->ld_act + f, x > 0.f ? x : x * sl);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // BatchNorm1d backward (train) + LeakyReLU' mask.  One workgroup owns 32 features and all M
 // rows, so the per-feature reductions stay inside the workgroup (fixed order, double accum):

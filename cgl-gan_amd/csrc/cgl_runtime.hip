@@ -78,8 +78,6 @@ int validate(const cgl_gan_config* c) {
   if (g.bn[g.n_layers - 1]) return CGL_E_ARG;
   for (int l = 0; l < d.n_layers; ++l)
     if (d.bn[l]) return CGL_E_ARG;
-  for (int l = 0; l + 1 < g.n_layers; ++l)
-    if (g.bn[l] && g.dims[l + 1] > CGL_TF_MAXK) return CGL_E_ARG;
   const int C = d.dims[d.n_layers];
   if (c->loss == CGL_LOSS_CE2 && C != 2) return CGL_E_ARG;
   if (c->loss == CGL_LOSS_BCE && C != 1) return CGL_E_ARG;
@@ -143,6 +141,7 @@ struct WS {
   CglGemmDesc* gemm;
   CglHeadDesc* head;
   CglBnBwdDesc* bnb;
+  CglBnApplyDesc* bna;
   int64_t total;
 };
 
@@ -158,6 +157,7 @@ WS carve_ws(const cgl_gan_config& c, void* base) {
   w.gemm = cv.take<CglGemmDesc>(kMaxGemmDescs);
   w.head = cv.take<CglHeadDesc>(kMaxHeadDescs);
   w.bnb = cv.take<CglBnBwdDesc>(kMaxBnDescs);
+  w.bna = cv.take<CglBnApplyDesc>(kMaxBnDescs);
   for (int l = 0; l < L; ++l) {
     const int f = g.dims[l + 1];
     w.gout[l] = cv.take<float>((int64_t)2 * B * f);
@@ -188,11 +188,12 @@ WS carve_ws(const cgl_gan_config& c, void* base) {
 }
 
 // ----------------------------------------------------------------------------------------
-enum LaunchKind { K_GEMM, K_HEAD, K_BNBWD, K_ADAM, K_PROLOGUE };
+enum LaunchKind { K_GEMM, K_HEAD, K_BNBWD, K_ADAM, K_PROLOGUE, K_BNAPPLY };
 
 struct Launch {
   LaunchKind kind;
   int grid = 1;
+  int grid_y = 1;
   int first = 0, count = 0;  // descriptor range (host index)
   CglAdamArgs adam{};
   int tail = 0;
@@ -204,7 +205,6 @@ struct Launch {
   double flops = 0.0;
   int shmem = 0;        // dynamic LDS bytes (GEMM)
   int blk = 1;          // GEMM per-wave block shape (TM = TN = blk)
-  int tf_floats = 0;    // BatchNorm-table floats at the head of the dynamic LDS (GEMM)
 };
 
 // Split-K partials of 2x2-block waves need up to 48 KB of dynamic LDS (+16 KB BN table).
@@ -224,11 +224,11 @@ hipError_t gemm_lds_attr() {
   return hipSuccess;
 }
 
-void launch_gemm(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, int n, int tf) {
+void launch_gemm(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, int n) {
   if (blk == 2)
-    cgl_gemm_f32<2, 2><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n, tf);
+    cgl_gemm_f32<2, 2><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
   else
-    cgl_gemm_f32<1, 1><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n, tf);
+    cgl_gemm_f32<1, 1><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
 }
 
 // Cost model of one GEMM launch (cycles) used to pick the wave arrangement WM x WN x WK and
@@ -329,6 +329,7 @@ struct cgl_gan {
   std::vector<CglGemmDesc> gemm;
   std::vector<CglHeadDesc> head;
   std::vector<CglBnBwdDesc> bnb;
+  std::vector<CglBnApplyDesc> bna;
   std::vector<Launch> phA, phB;
   hipGraphExec_t gexec[3] = {nullptr, nullptr, nullptr};
   hipStream_t cap = nullptr;   // private capture stream (the legacy default stream cannot capture)
@@ -368,7 +369,7 @@ void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
   L.kind = K_GEMM;
   L.first = (int)c->gemm.size();
   L.count = (int)descs.size();
-  int wg = 0, stage = 0, tf = 0;
+  int wg = 0, stage = 0;
   // one block shape per launch (one kernel instantiation): the shape of the largest problem
   int blk = 1;
   double fmax = -1.0;
@@ -389,12 +390,10 @@ void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
     const int nalg = d.b_ones_col ? d.N - 1 : d.N;
     L.flops += 2.0 * d.M * (double)nalg * d.K;
     stage = std::max(stage, cgl_gemm_stage_bytes(d));
-    if (d.a_tf) tf = 2 * CGL_TF_MAXK * 2;
     c->gemm.push_back(d);
   }
   L.grid = wg;
-  L.tf_floats = tf;
-  L.shmem = stage + tf * 4;
+  L.shmem = stage;
   ph.push_back(L);
 }
 
@@ -405,6 +404,17 @@ void push_head(cgl_gan* c, std::vector<Launch>& ph, const CglHeadDesc& h) {
   L.count = 1;
   L.grid = (h.M + kHeadRows - 1) / kHeadRows;
   c->head.push_back(h);
+  ph.push_back(L);
+}
+
+void push_bna(cgl_gan* c, std::vector<Launch>& ph, const CglBnApplyDesc& b) {
+  Launch L;
+  L.kind = K_BNAPPLY;
+  L.first = (int)c->bna.size();
+  L.count = 1;
+  L.grid = (b.F + 63) / 64;
+  L.grid_y = (b.bn.mtot + CGL_BNA_ROWS - 1) / CGL_BNA_ROWS;
+  c->bna.push_back(b);
   ph.push_back(L);
 }
 
@@ -476,7 +486,6 @@ int build_plan(cgl_gan* c) {
   }
 
   // ---- G forward on [z1; z2] (2B rows; BatchNorm statistics per B-row forward call)
-  int bm_prod[CGL_MAX_LAYERS] = {0};
   for (int l = 0; l < L; ++l) {
     const int fi = g.dims[l], fo = g.dims[l + 1];
     CglGemmDesc e = make_gemm(0, 2 * B, fo, fi);
@@ -485,26 +494,7 @@ int build_plan(cgl_gan* c) {
       e.a = rows(c->bufs.z, fi);
     } else {
       e.a = rows(w.gout[l - 1], fi);
-      if (g.bn[l - 1]) {
-        e.a_tf = 1;
-        CglBnFwd& bn = e.bn;
-        bn.part = w.gpart[l - 1];
-        bn.part_bm = bm_prod[l - 1];
-        bn.gr = B;
-        bn.mtot = 2 * B;
-        bn.gamma = gparam(c, l - 1, 2);
-        bn.beta = gparam(c, l - 1, 3);
-        bn.eps = cf.bn_eps;
-        bn.momentum = cf.bn_momentum;
-        bn.slope = sl;
-        bn.run_mean = c->bufs.g_running + c->run_mean_off[l - 1];
-        bn.run_var = c->bufs.g_running + c->run_var_off[l - 1];
-        bn.save_mean = w.gmean[l - 1];
-        bn.save_invstd = w.ginvstd[l - 1];
-        e.a_copy = w.gact[l - 1];
-        e.a_copy_ld = fi;
-        e.a_copy_row0 = B;
-      }
+      if (g.bn[l - 1]) e.a = rows(w.gact[l - 1], fi);   // BatchNorm + LeakyReLU applied by cgl_bn_apply
     }
     e.a_vec = (fi % 4 == 0) && al16(e.a.p0);
     e.b = rows(gparam(c, l, 0), fi);
@@ -522,8 +512,31 @@ int build_plan(cgl_gan* c) {
     e.slope = sl;
     e.C = w.gout[l];
     e.ldc = fo;
-    bm_prod[l] = 32 * e.TM * e.WM;
     push_gemm(c, A, {e});
+    if (l + 1 < L && g.bn[l]) {
+      CglBnApplyDesc ap;
+      std::memset(&ap, 0, sizeof(ap));
+      ap.F = fo;
+      ap.Y = w.gout[l];
+      ap.ld_y = fo;
+      ap.act = w.gact[l];
+      ap.ld_act = fo;
+      CglBnFwd& bn = ap.bn;
+      bn.part = w.gpart[l];
+      bn.part_bm = 32 * e.TM * e.WM;
+      bn.gr = B;
+      bn.mtot = 2 * B;
+      bn.gamma = gparam(c, l, 2);
+      bn.beta = gparam(c, l, 3);
+      bn.eps = cf.bn_eps;
+      bn.momentum = cf.bn_momentum;
+      bn.slope = sl;
+      bn.run_mean = c->bufs.g_running + c->run_mean_off[l];
+      bn.run_var = c->bufs.g_running + c->run_var_off[l];
+      bn.save_mean = w.gmean[l];
+      bn.save_invstd = w.ginvstd[l];
+      push_bna(c, A, ap);
+    }
   }
   const float* Xd = w.gout[L - 1];
   const float* Xg = w.gout[L - 1] + (int64_t)B * img;
@@ -776,7 +789,7 @@ int build_plan(cgl_gan* c) {
   push_adam(c, *ph, c->bufs.g_params, c->bufs.g_grads, c->bufs.g_m, c->bufs.g_v, (long)ng, &st->g_step_size,
             &st->g_bc2sqrt, 1);
   if ((int)c->gemm.size() > kMaxGemmDescs || (int)c->head.size() > kMaxHeadDescs ||
-      (int)c->bnb.size() > kMaxBnDescs)
+      (int)c->bnb.size() > kMaxBnDescs || (int)c->bna.size() > kMaxBnDescs)
     return CGL_E_SIZE;
   return CGL_OK;
 }
@@ -836,10 +849,13 @@ __global__ __launch_bounds__(256) void cgl_round_prologue(CglBeginArgs a, float*
 int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s) {
   switch (L.kind) {
     case K_GEMM:
-      launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, L.count, L.tf_floats);
+      launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, L.count);
       break;
     case K_HEAD:
       hipLaunchKernelGGL(cgl_head_loss, dim3(L.grid), dim3(256), 0, s, c->ws.head + L.first);
+      break;
+    case K_BNAPPLY:
+      hipLaunchKernelGGL(cgl_bn_apply, dim3(L.grid, L.grid_y), dim3(256), 0, s, c->ws.bna + L.first);
       break;
     case K_BNBWD:
       hipLaunchKernelGGL(cgl_bn_bwd, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
@@ -954,6 +970,8 @@ int cgl_gan_create(const cgl_gan_config* cfg, const cgl_gan_buffers* bufs, cgl_g
   hipError_t he = hipMemcpy(c->ws.gemm, c->gemm.data(), c->gemm.size() * sizeof(CglGemmDesc), hipMemcpyHostToDevice);
   if (he == hipSuccess && !c->head.empty())
     he = hipMemcpy(c->ws.head, c->head.data(), c->head.size() * sizeof(CglHeadDesc), hipMemcpyHostToDevice);
+  if (he == hipSuccess && !c->bna.empty())
+    he = hipMemcpy(c->ws.bna, c->bna.data(), c->bna.size() * sizeof(CglBnApplyDesc), hipMemcpyHostToDevice);
   if (he == hipSuccess && !c->bnb.empty())
     he = hipMemcpy(c->ws.bnb, c->bnb.data(), c->bnb.size() * sizeof(CglBnBwdDesc), hipMemcpyHostToDevice);
   if (he == hipSuccess) he = hipMemset(c->ws.counters, 0, kCounters * sizeof(unsigned int));
@@ -1164,7 +1182,7 @@ static int single_gemm(CglGemmDesc& d, void* ws, int64_t wsb, hipStream_t s) {
   d.wg_begin = 0;
   set_vec(d);
   HIPCHK(hipMemcpyAsync(ws, &d, sizeof(d), hipMemcpyHostToDevice, s));
-launch_gemm(d.TM, d.tiles_m * d.tiles_n, cgl_gemm_stage_bytes(d), s, (const CglGemmDesc*)ws, 1, 0);
+launch_gemm(d.TM, d.tiles_m * d.tiles_n, cgl_gemm_stage_bytes(d), s, (const CglGemmDesc*)ws, 1);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   // the descriptor lives in the caller's workspace: keep it alive until the kernel has read it

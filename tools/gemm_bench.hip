@@ -34,13 +34,12 @@ static double time_desc(CglGemmDesc d, CglGemmDesc* dd, int reps) {
   (void)hipEventCreate(&e1);
   (void)hipMemcpy(dd, &d, sizeof(d), hipMemcpyHostToDevice);
   const int grid = d.tiles_m * d.tiles_n;
-  const int tf = d.a_tf ? 2 * CGL_TF_MAXK * 2 : 0;
-  const int sh = cgl_gemm_stage_bytes(d) + tf * 4;
+  const int sh = cgl_gemm_stage_bytes(d);
   auto go = [&]() {
     if (d.TM == 2)
-      cgl_gemm_f32<2, 2><<<grid, 256, sh, 0>>>(dd, 1, tf);
+      cgl_gemm_f32<2, 2><<<grid, 256, sh, 0>>>(dd, 1);
     else
-      cgl_gemm_f32<1, 1><<<grid, 256, sh, 0>>>(dd, 1, tf);
+      cgl_gemm_f32<1, 1><<<grid, 256, sh, 0>>>(dd, 1);
   };
   for (int i = 0; i < 10; ++i) go();
   (void)hipEventRecord(e0, 0);
@@ -129,7 +128,7 @@ static void fusion_costs(float* A, float* B, float* C, CglGemmDesc* dd, int reps
   const Shape fw[] = {{"G1 fwd", 0, 512, 256, 128}, {"G2 fwd", 0, 512, 512, 256}, {"G3 fwd", 0, 512, 1024, 512},
                       {"G4 fwd", 0, 512, 784, 1024}};
   const int cfg[6][4] = {{2, 1, 2, 1}, {1, 2, 2, 1}, {1, 1, 4, 1}, {2, 1, 2, 2}, {1, 2, 2, 2}, {1, 1, 4, 2}};
-  printf("fusion costs (us): plain | +stat partials | BN-transform A | both | both+copy\n");
+  printf("fusion costs (us): plain | +stat partials | +A copy-out\n");
   for (const Shape& s : fw) {
     for (auto& c : cfg) {
       CglGemmDesc d;
@@ -145,19 +144,9 @@ static void fusion_costs(float* A, float* B, float* C, CglGemmDesc* dd, int reps
       const double t0 = time_desc(d, dd, reps);
       d.stat_part = part; d.stat_gr = 256;
       const double t1 = time_desc(d, dd, reps);
-      d.stat_part = nullptr;
-      d.a_tf = 1;
-      d.bn.part = part; d.bn.part_bm = 32; d.bn.gr = 256; d.bn.mtot = 512;
-      d.bn.gamma = vec; d.bn.beta = vec; d.bn.eps = 0.8; d.bn.momentum = 0.1; d.bn.slope = 0.2f;
-      d.bn.run_mean = vec + 4096; d.bn.run_var = vec + 8192; d.bn.save_mean = vec + 12288 - 2048;
-      d.bn.save_invstd = vec + 12288;
-      const double t2 = time_desc(d, dd, reps);
-      d.stat_part = part;
-      const double t3 = time_desc(d, dd, reps);
       d.a_copy = cp; d.a_copy_ld = s.K; d.a_copy_row0 = 256;
-      const double t4 = time_desc(d, dd, reps);
-      printf("%-7s %d%d%d/%d: %7.2f | %7.2f | %7.2f | %7.2f | %7.2f\n", s.name, c[0], c[1], c[2], c[3], t0, t1, t2, t3,
-             t4);
+      const double t2 = time_desc(d, dd, reps);
+      printf("%-7s %d%d%d/%d: %7.2f | %7.2f | %7.2f\n", s.name, c[0], c[1], c[2], c[3], t0, t1, t2);
     }
   }
 }
