@@ -78,7 +78,10 @@ __device__ __forceinline__ void cgl_mask(float v[8], bool ok, int k, int K) {
 // quadruples the MFMA work per load batch for the large problems.
 template <int TM, int TN>
 struct CglPipe {
-  static constexpr int S = 3;
+#ifndef CGL_GEMM_STAGES
+#define CGL_GEMM_STAGES 3
+#endif
+  static constexpr int S = CGL_GEMM_STAGES;
 };
 
 template <int LAYOUT, int VEC, int TM, int TN>
@@ -231,23 +234,27 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   };
 
   // S register sets in rotation: set s holds chunk c + s; after its MFMAs are issued it is
-  // refilled with chunk c + s + S, so S - 1 chunks of loads are always in flight and no
-  // register copy forces an early wait.
+  // refilled with chunk c + s + S, so S - 1 chunks of loads are always in flight.  The bulk
+  // loop body is branch-free (refills past the end re-load the last full chunk, harmlessly), so
+  // every s_waitcnt waits for exactly the set it consumes.
   const int cfull = min(ce, K / CGL_GEMM_KCHUNK);   // end of this wave's full chunks
   std::integral_constant<bool, false> full;
   std::integral_constant<bool, true> tailc;
   if (cb < cfull) {
     float xa[S][TM][8], xb[S][TN][8];
 #pragma unroll
-    for (int s = 0; s < S; ++s)
-      if (cb + s < cfull) load_chunk(full, cb + s, xa[s], xb[s]);
-    for (int c = cb; c < cfull; c += S) {
+    for (int s = 0; s < S; ++s) load_chunk(full, min(cb + s, cfull - 1), xa[s], xb[s]);
+    int c = cb;
+    for (; c + S <= cfull; c += S) {
 #pragma unroll
       for (int s = 0; s < S; ++s) {
-        if (c + s < cfull) compute_chunk(full, c + s, xa[s], xb[s]);
-        if (c + s + S < cfull) load_chunk(full, c + s + S, xa[s], xb[s]);
+        compute_chunk(full, c + s, xa[s], xb[s]);
+        load_chunk(full, min(c + s + S, cfull - 1), xa[s], xb[s]);
       }
     }
+#pragma unroll
+    for (int s = 0; s < S - 1; ++s)
+      if (c + s < cfull) compute_chunk(full, c + s, xa[s], xb[s]);
   }
   if (cfull < ce) {   // the K tail (at most one chunk, owned by the last k-group)
     float xa[TM][8], xb[TN][8];
