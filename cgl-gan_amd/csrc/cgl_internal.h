@@ -102,9 +102,11 @@ struct CglHeadDesc {
   float slope;
   float* part;            // [nwg][2] per-workgroup loss sums per segment
   unsigned int* counter;  // last-arriver ticket (zero at rest)
-  float* loss_out;        // [2]: mean loss of segment 0 and 1 (written by the last workgroup)
+  float* loss_out0;       // mean loss of segment 0 / 1 (written by the last workgroup), may be null
+  float* loss_out1;
   float combine;          // D_loss = (seg0 + seg1) * combine  (0.5: capgan.py:339, 1: CGLGAN/2DMG/main.py:364)
   float* combine_out;     // optional
+  const float* combine_in0;  // segment-0 mean computed by another launch (when this one has no segment 0)
   int rows_per_wg;
 };
 

@@ -154,10 +154,10 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
       s1 += (double)s_part[2 * q + 1];
     }
     const int n0 = min(hd->split, M), n1 = M - n0;
-    const float l0 = n0 > 0 ? (float)(s0 / n0) : 0.f;
+    const float l0 = n0 > 0 ? (float)(s0 / n0) : (hd->combine_in0 ? gld(hd->combine_in0) : 0.f);
     const float l1 = n1 > 0 ? (float)(s1 / n1) : 0.f;
-    gst(hd->loss_out, l0);
-    gst(hd->loss_out + 1, l1);
+    if (hd->loss_out0 && n0 > 0) gst(hd->loss_out0, l0);
+    if (hd->loss_out1 && n1 > 0) gst(hd->loss_out1, l1);
     if (hd->combine_out) gst(hd->combine_out, (l0 + l1) * hd->combine);
     __hip_atomic_store(hd->counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }

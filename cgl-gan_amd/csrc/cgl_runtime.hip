@@ -135,6 +135,7 @@ struct WS {
   float* gG[CGL_MAX_LAYERS];
   // misc
   float* hpart;
+  float* hpart2;
   unsigned int* counters;   // [kCounters]: head-loss tickets
   CglStepState* st;
   int* idx;       // sampler output when sample_n > 0
@@ -182,6 +183,7 @@ WS carve_ws(const cgl_gan_config& c, void* base) {
   w.dlog = cv.take<float>((int64_t)Md * d.dims[J]);
   w.dYL = cv.take<float>((int64_t)B * g.dims[L]);
   w.hpart = cv.take<float>((int64_t)((Md + kHeadRows - 1) / kHeadRows) * 2);
+  w.hpart2 = cv.take<float>((int64_t)((Md + kHeadRows - 1) / kHeadRows) * 2);
   w.idx = cv.take<int>((int64_t)c.epoch * c.batch_real);
   w.total = cv.off;
   return w;
@@ -203,6 +205,9 @@ struct Launch {
   int nb_norm = 0, nb_samp = 0;
   int stream_id = 0;
   double flops = 0.0;
+  int stream = 0;       // 0: the caller's stream, 1: the context's side stream
+  int wait_ev = -1;     // event waited on before the launch / recorded after it
+  int record_ev = -1;
   int shmem = 0;        // dynamic LDS bytes (GEMM)
   int blk = 1;          // GEMM per-wave block shape (TM = TN = blk)
 };
@@ -333,11 +338,22 @@ struct cgl_gan {
   std::vector<Launch> phA, phB;
   hipGraphExec_t gexec[3] = {nullptr, nullptr, nullptr};
   hipStream_t cap = nullptr;   // private capture stream (the legacy default stream cannot capture)
+  hipStream_t side = nullptr;  // second stream: the real-row D chain of the first local D step
+  hipEvent_t ev[2] = {nullptr, nullptr};   // fork (after the prologue), join (before the D-step head)
+  bool two_streams = false;
   float* xchg = nullptr;
   int64_t xchg_n = 0;
   // parameter tensor pointers
   std::vector<TensorRec> gl, dl;
   int64_t run_mean_off[CGL_MAX_LAYERS], run_var_off[CGL_MAX_LAYERS];
+  ~cgl_gan() {
+    for (auto& g : gexec)
+      if (g) (void)hipGraphExecDestroy(g);
+    if (cap) (void)hipStreamDestroy(cap);
+    if (side) (void)hipStreamDestroy(side);
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+  }
 };
 
 namespace {
@@ -482,6 +498,7 @@ int build_plan(cgl_gan* c) {
       real_idx = w.idx;
     }
     Lp.grid = 1 + Lp.nb_norm + Lp.nb_samp;
+    Lp.record_ev = c->two_streams ? 0 : -1;   // fork point of the side stream
     A.push_back(Lp);
   }
 
@@ -544,29 +561,40 @@ int build_plan(cgl_gan* c) {
   // ---- local D steps (Worker.train capgan.py:324-341)
   const int C = d.dims[J];
   const float combine = cf.loss == CGL_LOSS_CE2 ? 0.5f : 1.0f;
-  for (int ep = 0; ep < cf.epoch; ++ep) {
+  // hidden-layer forwards of the D-step input rows [row0, row0 + nrows): part 0 = real rows
+  // (through the sampler's index list), part 1 = Xd rows, part 2 = both (one 2-segment GEMM)
+  auto d_forward = [&](int ep, int part, int stream, int wait_ev) {
+    const int row0 = part == 1 ? Br : 0;
+    const int nrows = part == 0 ? Br : part == 1 ? B : Md;
     for (int j = 0; j + 1 < J; ++j) {
       const int fi = d.dims[j], fo = d.dims[j + 1];
-      CglGemmDesc e = make_gemm(0, Md, fo, fi);
+      CglGemmDesc e = make_gemm(0, nrows, fo, fi);
       if (j == 0) {
         CglRowSrc r;
         std::memset(&r, 0, sizeof(r));
-        if (real_idx) {
-          r.p0 = c->bufs.real;
-          r.idx0 = real_idx + (int64_t)ep * Br;
-        } else {
-          r.p0 = c->bufs.real + (int64_t)ep * Br * fi;
-        }
-        r.p1 = Xd;
-        r.split = Br;
+        r.split = 0x7fffffff;
         r.ld = fi;
+        if (part == 1) {
+          r.p0 = Xd;
+        } else {
+          if (real_idx) {
+            r.p0 = c->bufs.real;
+            r.idx0 = real_idx + (int64_t)ep * Br;
+          } else {
+            r.p0 = c->bufs.real + (int64_t)ep * Br * fi;
+          }
+          if (part == 2) {
+            r.p1 = Xd;
+            r.split = Br;
+          }
+        }
         e.a = r;
         e.a_vec = (fi % 4 == 0) && al16(c->bufs.real) && al16(Xd);
-        e.a_copy = w.R;
+        e.a_copy = w.R + (int64_t)row0 * fi;
         e.a_copy_ld = fi;
         e.a_copy_row0 = 0;
       } else {
-        e.a = rows(w.P[j - 1], fi);
+        e.a = rows(w.P[j - 1] + (int64_t)row0 * fi, fi);
         e.a_vec = (fi % 4 == 0);
       }
       e.b = rows(dparam(c, j, 0), fi);
@@ -574,36 +602,66 @@ int build_plan(cgl_gan* c) {
       e.bias = dparam(c, j, 1);
       e.act = CGL_EPI_ACT_LEAKY;
       e.slope = sl;
-      e.C = w.P[j];
+      e.C = w.P[j] + (int64_t)row0 * fo;
       e.ldc = fo;
       push_gemm(c, A, {e});
+      A.back().stream = stream;
+      if (j == 0) A.back().wait_ev = wait_ev;
     }
+  };
+  // the loss head of a part: CE/BCE on the logits, dlogits and the gradient into the last
+  // hidden layer; real rows are segment 0 (target valid), Xd rows segment 1 (target fake)
+  auto d_head = [&](int ep, int part, int stream, int wait_ev, int record_ev) {
+    const int row0 = part == 1 ? Br : 0;
+    const int nrows = part == 0 ? Br : part == 1 ? B : Md;
+    const int F = d.dims[J - 1];
     CglHeadDesc h;
     std::memset(&h, 0, sizeof(h));
-    h.M = Md;
-    h.F = d.dims[J - 1];
+    h.M = nrows;
+    h.F = F;
     h.C = C;
     h.loss = cf.loss;
-    h.P = w.P[J - 2];
-    h.ldp = d.dims[J - 1];
+    h.P = w.P[J - 2] + (int64_t)row0 * F;
+    h.ldp = F;
     h.W = dparam(c, J - 1, 0);
     h.b = dparam(c, J - 1, 1);
-    h.split = Br;
+    h.split = part == 0 ? Br : part == 1 ? 0 : Br;
     h.t0 = 1;
     h.t1 = 0;
     h.w0 = combine / Br;
     h.w1 = combine / B;
-    h.dlogits = w.dlog;
-    h.dP = w.dQ[J - 2];
-    h.lddp = d.dims[J - 1];
+    h.dlogits = w.dlog + (int64_t)row0 * C;
+    h.dP = w.dQ[J - 2] + (int64_t)row0 * F;
+    h.lddp = F;
     h.slope = sl;
-    h.part = w.hpart;
-    h.counter = w.counters + ep;
-    h.loss_out = &st->d_loss_parts[ep][0];
+    h.part = part == 0 ? w.hpart2 : w.hpart;
+    h.counter = w.counters + (part == 0 ? 16 : ep);
+    h.loss_out0 = &st->d_loss_parts[ep][0];
+    h.loss_out1 = &st->d_loss_parts[ep][1];
     h.combine = combine;
-    h.combine_out = &st->d_loss[ep];
+    h.combine_out = part == 0 ? nullptr : &st->d_loss[ep];
+    h.combine_in0 = part == 1 ? &st->d_loss_parts[ep][0] : nullptr;
     h.rows_per_wg = kHeadRows;
     push_head(c, A, h);
+    A.back().stream = stream;
+    A.back().wait_ev = wait_ev;
+    A.back().record_ev = record_ev;
+  };
+  for (int ep = 0; ep < cf.epoch; ++ep) {
+    if (ep == 0 && c->two_streams) {
+      // the real rows of the first local D step do not depend on G: their forward and loss
+      // head run on the side stream concurrently with the G forward (forked after the
+      // prologue, joined before the Xd head, whose D_loss combines both segments)
+      d_forward(0, 0, 1, 0);
+      d_head(0, 0, 1, -1, 1);
+      // (the G forward was pushed before; move the side chain in front of it in list order so
+      // that a single-stream replay of the list is still a valid order)
+      d_forward(0, 1, 0, -1);
+      d_head(0, 1, 0, 1, -1);
+    } else {
+      d_forward(ep, 2, 0, -1);
+      d_head(ep, 2, 0, -1, -1);
+    }
     // backward: weight grads (TN, + bias column) and input grads (NN, LeakyReLU' mask)
     for (int j = J - 1; j >= 0; --j) {
       std::vector<CglGemmDesc> grp;
@@ -686,7 +744,7 @@ int build_plan(cgl_gan* c) {
     h.slope = sl;
     h.part = w.hpart;
     h.counter = w.counters + CGL_MAX_EPOCH;
-    h.loss_out = &st->g_loss_parts[0];
+    h.loss_out0 = &st->g_loss_parts[0];
     h.combine = 1.0f;
     h.rows_per_wg = kHeadRows;
     push_head(c, A, h);
@@ -846,7 +904,15 @@ __global__ __launch_bounds__(256) void cgl_round_prologue(CglBeginArgs a, float*
   idx[t] = (int)cgl_permute(j, (uint32_t)n, (uint32_t)sseed ^ (ep * 0x85ebca6bu + 0x1234567u));
 }
 
-int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s) {
+int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = true) {
+  hipStream_t s = s_main;
+  if (events && c->two_streams) {
+    if (L.stream == 1) s = c->side;
+    if (L.wait_ev >= 0) {
+      const hipError_t ew = hipStreamWaitEvent(s, c->ev[L.wait_ev], 0);
+      if (ew != hipSuccess) return (int)ew;
+    }
+  }
   switch (L.kind) {
     case K_GEMM:
       launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, L.count);
@@ -871,7 +937,8 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s) {
     default:
       return CGL_E_STATE;
   }
-  const hipError_t e = hipGetLastError();
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && events && c->two_streams && L.record_ev >= 0) e = hipEventRecord(c->ev[L.record_ev], s);
   return e == hipSuccess ? 0 : (int)e;
 }
 
@@ -956,6 +1023,21 @@ int cgl_gan_create(const cgl_gan_config* cfg, const cgl_gan_buffers* bufs, cgl_g
   }
   cgl_gan* c = new cgl_gan();
   c->cfg = *cfg;
+  {
+    // measured slower on MI355X (0.299 vs 0.264 ms per B=256 round: the concurrent chains slow
+    // each other and the fork / join add latency), so opt-in only
+    const char* e2 = getenv("CGL_TWO_STREAMS");
+    c->two_streams = e2 && atoi(e2) != 0 && cfg->d.n_layers >= 2;
+  }
+  if (c->two_streams) {
+    hipError_t es = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+    if (es == hipSuccess) es = hipEventCreateWithFlags(&c->ev[0], hipEventDisableTiming);
+    if (es == hipSuccess) es = hipEventCreateWithFlags(&c->ev[1], hipEventDisableTiming);
+    if (es != hipSuccess) {
+      delete c;
+      return (int)es;
+    }
+  }
   c->bufs = *bufs;
   c->ws = carve_ws(*cfg, bufs->workspace);
   c->gl = param_layout(cfg->g, nullptr);
@@ -987,9 +1069,6 @@ int cgl_gan_create(const cgl_gan_config* cfg, const cgl_gan_buffers* bufs, cgl_g
 
 int cgl_gan_destroy(cgl_gan* c) {
   if (!c) return CGL_E_ARG;
-  for (auto& g : c->gexec)
-    if (g) (void)hipGraphExecDestroy(g);
-  if (c->cap) (void)hipStreamDestroy(c->cap);
   delete c;
   return CGL_OK;
 }
@@ -1170,7 +1249,7 @@ int cgl_gan_launch_one(cgl_gan* c, int phase, int idx, void* stream) {
   if (!c || phase < 0 || phase > 2 || idx < 0 || idx >= cgl_gan_launch_count(c, phase)) return CGL_E_ARG;
   int li;
   const std::vector<Launch>* v = phase_list(c, phase, idx, &li);
-  return exec_launch(c, (*v)[li], (hipStream_t)stream);
+  return exec_launch(c, (*v)[li], (hipStream_t)stream, false);
 }
 
 // ---------------- single ops -------------------------------------------------------------
