@@ -49,7 +49,7 @@ def args_():
     p.add_argument("--eager", action="store_true", help="launch without hipGraph")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
-    p.add_argument("--profile-rounds", type=int, default=5)
+    p.add_argument("--profile-reps", type=int, default=20, help="back-to-back replays per launch when timing launches")
     return p.parse_args()
 
 
@@ -74,34 +74,49 @@ def make_exchange(step, world, a):
     return WorkerExchange(step, DistComm() if world > 1 else None, share_every=a.E if world > 1 else 0)
 
 
-def profile_launches(step, world, rounds):
-    """Per-launch device time with HIP events on the launch stream (eager replay of the plan)."""
+def profile_launches(step, world, reps):
+    """Device time per launch of the round's plan: each launch is replayed `reps` times
+    back-to-back between two HIP events on the launch stream (the launches are idempotent up to
+    optimizer state, and this runs after the timed region), so the figure is the kernel's own
+    duration plus the back-to-back dispatch gap -- the quantity rocprofv3's kernel trace
+    reports as its average duration."""
     from cglgan._lib import PHASE_A, PHASE_ALL, PHASE_B
     phases = [PHASE_ALL] if world == 1 else [PHASE_A, PHASE_B]
     per_kind = {}
-    gemm_ms, gemm_flops, gemm_n = 0.0, 0.0, 0
+    gemm_us, gemm_flops, gemm_n = [], 0.0, 0
     s = torch.cuda.current_stream()
-    for _ in range(rounds):
-        recs = []
-        for ph in phases:
-            info = step.launches(ph)
-            for i, (kind, flops, grid) in enumerate(info):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(s)
+    for ph in phases:
+        info = step.launches(ph)
+        for i, (kind, flops, grid) in enumerate(info):
+            step.launch_one(i, ph)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(reps):
                 step.launch_one(i, ph)
-                e1.record(s)
-                recs.append((kind, flops, e0, e1))
-        torch.cuda.synchronize()
-        for kind, flops, e0, e1 in recs:
-            ms = e0.elapsed_time(e1)
+            e1.record(s)
+            e1.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / reps
             k = per_kind.setdefault(kind, [0.0, 0])
-            k[0] += ms
+            k[0] += us
             k[1] += 1
             if kind == "gemm":
-                gemm_ms += ms
+                gemm_us.append(us)
                 gemm_flops += flops
                 gemm_n += 1
-    return per_kind, gemm_ms / rounds, gemm_flops / rounds, gemm_n / rounds
+    return per_kind, gemm_us, gemm_flops, gemm_n
+
+
+def traffic_per_gemm_launch():
+    """HBM-side bytes per GEMM dispatch from the committed PMC passes of this build
+    (profiles/r01_traffic.json, made by tools/pmc_traffic.py; None when absent)."""
+    path = os.path.join(ROOT, "profiles", "r01_traffic.json")
+    if not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    for k, v in d.items():
+        if "cgl_gemm_f32" in k:
+            return round(v["bytes_per_dispatch"])
+    return None
 
 
 def cpu_baseline(a):
@@ -165,13 +180,14 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
         st = step.stats()
-        per_kind, gemm_ms, gemm_flops, gemm_n = profile_launches(step, world, a.profile_rounds)
+        per_kind, gemm_us, gemm_flops, gemm_n = profile_launches(step, world, a.profile_reps)
         plan = step.plan_info()
     ms_step = el / a.steps * 1e3
     value = world * a.batch * a.steps / el
     out = None
     if rank == 0:
-        gemm_tf = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
+        gemm_s = sum(gemm_us) * 1e-6
+        gemm_tf = gemm_flops / gemm_s / 1e12 if gemm_s > 0 else 0.0
         step_tf = a.batch * FLOP_PER_IMAGE_MIN / (ms_step * 1e-3) / 1e12
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": a.steps,
@@ -184,15 +200,18 @@ def main():
                        "global_batch": a.batch * world, "batch_per_worker": a.batch, "img": "28x28x1",
                        "parallelism": f"workers{world}", "graph": not a.eager,
                        "dataset_rows_per_worker": a.rows},
-            "roofline": {"bound": "mfma", "kernel": "cgl_gemm_f32 (all GEMM launches of the round)",
+            "roofline": {"bound": "mfma", "kernel": "cgl_gemm_f32 (the round's GEMM launches)",
                          "achieved": round(gemm_tf, 3), "peak": PEAK_F32_MFMA, "unit": "TFLOP/s",
-                         "frac": round(gemm_tf / PEAK_F32_MFMA, 4), "traffic": None,
+                         "frac": round(gemm_tf / PEAK_F32_MFMA, 4),
+                         "traffic": traffic_per_gemm_launch(),
+                         "traffic_unit": "bytes per GEMM launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/r01_traffic.json)",
                          "gemm_launches_per_round": gemm_n, "gemm_flops_per_round": gemm_flops,
-                         "gemm_ms_per_round": round(gemm_ms, 4),
-                         "avg_gemm_launch_us": round(gemm_ms / max(gemm_n, 1) * 1e3, 3),
+                         "flops_per_gemm_launch": gemm_flops / max(gemm_n, 1),
+                         "avg_gemm_launch_us": round(sum(gemm_us) / max(gemm_n, 1), 3),
+                         "gemm_launch_us": [round(u, 2) for u in gemm_us],
                          "step_achieved_tflops": round(step_tf, 3),
                          "step_frac_mfma": round(step_tf / PEAK_F32_MFMA, 4),
-                         "per_kind_ms_per_round": {k: round(v[0] / a.profile_rounds, 4) for k, v in per_kind.items()},
+                         "per_kind_us_per_round": {k: round(v[0], 2) for k, v in per_kind.items()},
                          "launches_per_round": plan["launches"]},
             "losses": {"d_loss": st["d_loss"][0], "g_loss": st["g_loss"], "lambda": st["lambda"],
                        "round": st["round"]},
