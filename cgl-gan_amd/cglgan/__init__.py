@@ -8,6 +8,7 @@ from ._lib import version
 from .specs import (MIXGEN_HEAD_LAYER, RING_HEAD_LAYER, MlpModel, mixgen_worker, mnist_discriminator,
                     mnist_generator, ring_discriminator, ring_generator)
 from .step import GanStep
+from . import model
 
 __all__ = ["GanStep", "MlpModel", "mnist_generator", "mnist_discriminator", "mixgen_worker", "ring_generator",
-           "ring_discriminator", "MIXGEN_HEAD_LAYER", "RING_HEAD_LAYER", "version"]
+           "ring_discriminator", "MIXGEN_HEAD_LAYER", "RING_HEAD_LAYER", "version", "model"]

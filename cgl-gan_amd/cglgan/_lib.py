@@ -24,7 +24,8 @@ EXPORTS = [
     "cgl_gan_create", "cgl_gan_destroy", "cgl_gan_reset", "cgl_gan_run", "cgl_gan_run_graph",
     "cgl_gan_alpha_scale", "cgl_gan_exchange_buffer", "cgl_gan_tensor", "cgl_gan_read_stats",
     "cgl_gan_plan_info", "cgl_gan_launch_count", "cgl_gan_launch_info", "cgl_gan_launch_one", "cgl_linear_fwd", "cgl_linear_bwd_data", "cgl_linear_bwd_weight", "cgl_adam_step",
-    "cgl_normal_fill", "cgl_op_workspace_bytes", "cgl_version",
+    "cgl_normal_fill", "cgl_op_workspace_bytes", "cgl_version", "cgl_act_fwd", "cgl_act_bwd", "cgl_bn1d_fwd",
+    "cgl_bn1d_bwd",
 ]
 
 
@@ -88,6 +89,10 @@ def _load():
         "cgl_linear_bwd_weight": (ci, [vp, vp, vp, vp, ci, ci, ci, vp, i64, vp]),
         "cgl_adam_step": (ci, [vp, vp, vp, vp, i64, ci, cd, cd, cd, cd, vp, i64, vp]),
         "cgl_normal_fill": (ci, [vp, i64, ctypes.c_ulonglong, ci, ci, vp]),
+        "cgl_act_fwd": (ci, [vp, i64, ci, cf, vp, vp]),
+        "cgl_act_bwd": (ci, [vp, vp, i64, ci, cf, vp, vp]),
+        "cgl_bn1d_fwd": (ci, [vp, ci, ci, ci, vp, vp, cd, cd, vp, vp, ci, ci, cf, vp, vp, vp, vp, i64, vp]),
+        "cgl_bn1d_bwd": (ci, [vp, vp, vp, ci, ci, vp, vp, vp, ci, cf, vp, vp, vp, vp, i64, vp]),
         "cgl_op_workspace_bytes": (i64, []),
         "cgl_version": (ctypes.c_char_p, []),
     }

@@ -189,6 +189,19 @@ class GanStep:
             sd[k + ".num_batches_tracked"] = torch.tensor(st["bn_batches"], dtype=torch.long)
         return sd
 
+    def modules(self, img_shape=(1, 28, 28)):
+        """(Generator, Discriminator) nn.Modules of cglgan.model holding a copy of this worker's
+        current state (reference keys), e.g. for sampling G(fixed_z) in eval mode
+        (capgan.py:203-209) or for checkpointing as the reference does."""
+        from . import model as M
+        if self.gm.name != "mnist_generator" or not self.dm.name.startswith("mnist_discriminator"):
+            raise NotImplementedError("module export is provided for the model/mnist_model.py G / D")
+        g = M.Generator(img_shape).to(self.device)
+        d = M.Discriminator(img_shape, sigmoid=self.dm.name.endswith("sigmoid")).to(self.device)
+        g.load_state_dict(self.g_state_dict())
+        d.load_state_dict(self.d_state_dict())
+        return g, d
+
     def d_state_dict(self):
         return OrderedDict((k, v.detach().clone()) for k, v in self.d_views.items())
 

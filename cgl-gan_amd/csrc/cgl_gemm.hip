@@ -313,6 +313,9 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
         } else if (d->act == CGL_EPI_ACT_TANH) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) v[r] = tanhf(v[r]);
+        } else if (d->act == CGL_EPI_ACT_SIGMOID) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = 1.f / (1.f + expf(-v[r]));
         }
         if (d->mask_ref) {
           const float sl = d->slope;

@@ -10,7 +10,7 @@
 #define CGL_GEMM_KCHUNK 16           // k per MFMA chunk: 8 per lane half (k-permuted)
 #define CGL_BN_MAXF 1024             // max features of a G BatchNorm layer
 
-enum { CGL_EPI_ACT_NONE = 0, CGL_EPI_ACT_LEAKY = 1, CGL_EPI_ACT_TANH = 2 };
+enum { CGL_EPI_ACT_NONE = 0, CGL_EPI_ACT_LEAKY = 1, CGL_EPI_ACT_TANH = 2, CGL_EPI_ACT_SIGMOID = 3 };
 
 // Global-address-space accessors.  Pointers read out of a descriptor in memory are generic to
 // the compiler, which then emits flat_* instructions; flat loads return out of order and force
@@ -110,7 +110,18 @@ struct CglHeadDesc {
   int rows_per_wg;
 };
 
-// BatchNorm1d backward for one layer, fused with the LeakyReLU mask of its output.
+// Standalone BatchNorm1d forward (nn.Module path): batch or running statistics, optional LeakyReLU.
+struct CglBn1dDesc {
+  int M, F, ldx, train, act;
+  const float* X; float* Y;
+  const float* gamma; const float* beta;
+  double eps, momentum;
+  float slope;
+  float* run_mean; float* run_var; float* save_mean; float* save_invstd;
+};
+
+// BatchNorm1d backward for one layer, fused with the LeakyReLU mask of its output (post may be
+// null: no activation).
 struct CglBnBwdDesc {
   int M, F;
   const float* dA; int ld_da;     // gradient w.r.t. the LeakyReLU output

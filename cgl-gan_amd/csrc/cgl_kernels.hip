@@ -319,7 +319,8 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
   const float invstd = gld(bd->invstd + fc);
   const float w = gld(bd->gamma + fc);
   const float* dA = bd->dA + fc;
-  const float* post = bd->post + fc;
+  const bool post_on = bd->post != nullptr;
+  const float* post = post_on ? bd->post + fc : bd->Y + fc;   // (any valid address when unused)
   const float* Y = bd->Y + fc;
   const long lda = bd->ld_da, ldp = bd->ld_post, ldy = bd->ld_y;
   float* dZ = bd->dZ + fc;
@@ -330,7 +331,7 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
 #pragma unroll
     for (int j = 0; j < CGL_BNB_RPT; ++j) {
       const int r = min(rg + 8 * j, M - 1);
-      const float da = gld(dA + r * lda), po = gld(post + r * ldp), y = gld(Y + r * ldy);
+      const float da = gld(dA + r * lda), po = post_on ? gld(post + r * ldp) : 1.f, y = gld(Y + r * ldy);
       dy[j] = po > 0.f ? da : da * sl;
       yc[j] = y - mean;
     }
@@ -370,7 +371,7 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
     for (int j = 0; j < 8; ++j) {
       const int r = min(r0 + 8 * j, M - 1);
       da[j] = gld(dA + r * lda);
-      po[j] = gld(post + r * ldp);
+      po[j] = post_on ? gld(post + r * ldp) : 1.f;
       y[j] = gld(Y + r * ldy);
     }
 #pragma unroll
@@ -399,7 +400,7 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
     for (int j = 0; j < 8; ++j) {
       const int r = min(r0 + 8 * j, M - 1);
       da[j] = gld(dA + r * lda);
-      po[j] = gld(post + r * ldp);
+      po[j] = post_on ? gld(post + r * ldp) : 1.f;
       y[j] = gld(Y + r * ldy);
     }
 #pragma unroll
@@ -415,6 +416,126 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
   if (rg == 0) {
     gst(bd->g_gamma + f, (float)(D * (double)invstd));
     gst(bd->g_beta + f, (float)S);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Standalone BatchNorm1d (+ LeakyReLU) forward, train or eval, for the nn.Module path.  One
+// workgroup owns 32 features x all M rows (8 row groups): column sums in double, fixed order;
+// rows stay in registers when M <= 8 * CGL_BNB_RPT (one memory round trip), else are streamed.
+__device__ __forceinline__ void cgl_bn1d_apply_row(const CglBn1dDesc* bd, int r, int f, float x, float sc, float sh) {
+  float y = fmaf(x, sc, sh);
+  if (bd->act == CGL_EPI_ACT_LEAKY) y = y > 0.f ? y : y * bd->slope;
+  gst(bd->Y + (long)r * bd->F + f, y);
+}
+
+__global__ __launch_bounds__(256) void cgl_bn1d_fwd_k(const CglBn1dDesc* __restrict__ bd) {
+  __shared__ double s_a[8][32];
+  __shared__ float s_sc[32], s_sh[32];
+  const int M = bd->M, F = bd->F;
+  const int fl = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int f = blockIdx.x * 32 + fl;
+  const bool fok = f < F;
+  const int fc = min(f, F - 1);
+  const float* X = bd->X + fc;
+  const long ldx = bd->ldx;
+  const bool regs = M <= 8 * CGL_BNB_RPT;
+  float xv[CGL_BNB_RPT];
+  if (regs) {
+#pragma unroll
+    for (int j = 0; j < CGL_BNB_RPT; ++j) xv[j] = gld(X + (long)min(rg + 8 * j, M - 1) * ldx);
+  }
+  if (bd->train) {
+    double sum = 0.0;
+    if (regs) {
+#pragma unroll
+      for (int j = 0; j < CGL_BNB_RPT; ++j)
+        if (rg + 8 * j < M) sum += (double)xv[j];
+    } else {
+      for (int r = rg; r < M; r += 8) sum += (double)gld(X + (long)r * ldx);
+    }
+    s_a[rg][fl] = sum;
+    __syncthreads();
+    double S = 0.0;
+    for (int q = 0; q < 8; ++q) S += s_a[q][fl];
+    const double mean = S / M;
+    __syncthreads();
+    double q2 = 0.0;
+    if (regs) {
+#pragma unroll
+      for (int j = 0; j < CGL_BNB_RPT; ++j)
+        if (rg + 8 * j < M) {
+          const double dd = (double)xv[j] - mean;
+          q2 += dd * dd;
+        }
+    } else {
+      for (int r = rg; r < M; r += 8) {
+        const double dd = (double)gld(X + (long)r * ldx) - mean;
+        q2 += dd * dd;
+      }
+    }
+    s_a[rg][fl] = q2;
+    __syncthreads();
+    if (rg == 0) {
+      double Q = 0.0;
+      for (int q = 0; q < 8; ++q) Q += s_a[q][fl];
+      const double var = Q / M;
+      const double invstd = 1.0 / sqrt(var + bd->eps);
+      const float sc = (float)invstd * gld(bd->gamma + fc);
+      s_sc[fl] = sc;
+      s_sh[fl] = gld(bd->beta + fc) - (float)mean * sc;
+      if (fok) {
+        if (bd->save_mean) {
+          gst(bd->save_mean + f, (float)mean);
+          gst(bd->save_invstd + f, (float)invstd);
+        }
+        if (bd->run_mean) {
+          const double mom = bd->momentum;
+          gst(bd->run_mean + f, (float)(mom * mean + (1.0 - mom) * (double)gld(bd->run_mean + f)));
+          const double unb = M > 1 ? Q / (M - 1) : var;
+          gst(bd->run_var + f, (float)(mom * unb + (1.0 - mom) * (double)gld(bd->run_var + f)));
+        }
+      }
+    }
+  } else if (rg == 0) {
+    const double invstd = 1.0 / sqrt((double)gld(bd->run_var + fc) + bd->eps);
+    const float sc = (float)invstd * gld(bd->gamma + fc);
+    s_sc[fl] = sc;
+    s_sh[fl] = gld(bd->beta + fc) - gld(bd->run_mean + fc) * sc;
+  }
+  __syncthreads();
+  if (!fok) return;
+  const float sc = s_sc[fl], sh = s_sh[fl];
+  if (regs) {
+#pragma unroll
+    for (int j = 0; j < CGL_BNB_RPT; ++j)
+      if (rg + 8 * j < M) cgl_bn1d_apply_row(bd, rg + 8 * j, f, xv[j], sc, sh);
+  } else {
+    for (int r = rg; r < M; r += 8) cgl_bn1d_apply_row(bd, r, f, gld(X + (long)r * ldx), sc, sh);
+  }
+}
+
+// elementwise activation forward / backward (act: 1 LeakyReLU, 2 Tanh, 3 Sigmoid)
+__global__ __launch_bounds__(256) void cgl_act_fwd_k(const float* X, long n, int act, float slope, float* Y) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float x = gld(X + i);
+    float y = x;
+    if (act == CGL_EPI_ACT_LEAKY) y = x > 0.f ? x : x * slope;
+    else if (act == CGL_EPI_ACT_TANH) y = tanhf(x);
+    else if (act == CGL_EPI_ACT_SIGMOID) y = 1.f / (1.f + expf(-x));
+    gst(Y + i, y);
+  }
+}
+
+__global__ __launch_bounds__(256) void cgl_act_bwd_k(const float* dY, const float* Y, long n, int act, float slope,
+                                                     float* dX) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float g = gld(dY + i), y = gld(Y + i);
+    float d = g;
+    if (act == CGL_EPI_ACT_LEAKY) d = y > 0.f ? g : g * slope;
+    else if (act == CGL_EPI_ACT_TANH) d = g * (1.f - y * y);
+    else if (act == CGL_EPI_ACT_SIGMOID) d = g * (y * (1.f - y));
+    gst(dX + i, d);
   }
 }
 

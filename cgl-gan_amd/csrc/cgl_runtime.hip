@@ -1253,7 +1253,7 @@ int cgl_gan_launch_one(cgl_gan* c, int phase, int idx, void* stream) {
 }
 
 // ---------------- single ops -------------------------------------------------------------
-int64_t cgl_op_workspace_bytes(void) { return 4096; }
+int64_t cgl_op_workspace_bytes(void) { return 1 << 16; }   // descriptor + BN scratch (F <= 8000)
 
 static int single_gemm(CglGemmDesc& d, void* ws, int64_t wsb, hipStream_t s) {
   if (!ws || wsb < (int64_t)sizeof(CglGemmDesc) || !al16(ws)) return CGL_E_ARG;
@@ -1271,7 +1271,7 @@ launch_gemm(d.TM, d.tiles_m * d.tiles_n, cgl_gemm_stage_bytes(d), s, (const CglG
 
 int cgl_linear_fwd(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, int act,
                    float slope, void* ws, int64_t wsb, void* stream) {
-  if (!X || !W || !Y || M < 1 || N < 1 || K < 1 || act < 0 || act > 2) return CGL_E_ARG;
+  if (!X || !W || !Y || M < 1 || N < 1 || K < 1 || act < 0 || act > 3) return CGL_E_ARG;
   CglGemmDesc d = make_gemm(0, M, N, K);
   d.a = rows(X, K);
   d.a_vec = (K % 4 == 0) && al16(X);
@@ -1308,6 +1308,76 @@ int cgl_linear_bwd_weight(const float* dY, const float* X, float* dW, float* db,
   d.ldc = K;
   d.bias_out = db;
   return single_gemm(d, ws, wsb, (hipStream_t)stream);
+}
+
+int cgl_act_fwd(const float* X, int64_t n, int act, float slope, float* Y, void* stream) {
+  if (!X || !Y || n < 0 || act < 0 || act > 3) return CGL_E_ARG;
+  if (n == 0) return 0;
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(cgl_act_fwd_k, dim3(grid), dim3(256), 0, (hipStream_t)stream, X, (long)n, act, slope, Y);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+int cgl_act_bwd(const float* dY, const float* Y, int64_t n, int act, float slope, float* dX, void* stream) {
+  if (!dY || !Y || !dX || n < 0 || act < 0 || act > 3) return CGL_E_ARG;
+  if (n == 0) return 0;
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(cgl_act_bwd_k, dim3(grid), dim3(256), 0, (hipStream_t)stream, dY, Y, (long)n, act, slope, dX);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+int cgl_bn1d_fwd(const float* X, int M, int F, int ldx, const float* gamma, const float* beta, double eps,
+                 double momentum, float* running_mean, float* running_var, int train, int act, float slope, float* Y,
+                 float* save_mean, float* save_invstd, void* ws, int64_t wsb, void* stream) {
+  if (!X || !Y || !gamma || !beta || M < 1 || F < 1 || ldx < F || (act != 0 && act != 1)) return CGL_E_ARG;
+  if (!train && (!running_mean || !running_var)) return CGL_E_ARG;
+  if (train && M < 2) return CGL_E_ARG;   // torch: "Expected more than 1 value per channel when training"
+  if ((running_mean == nullptr) != (running_var == nullptr)) return CGL_E_ARG;
+  if ((save_mean == nullptr) != (save_invstd == nullptr)) return CGL_E_ARG;
+  if (!ws || wsb < (int64_t)sizeof(CglBn1dDesc) || !al16(ws)) return CGL_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  CglBn1dDesc d;
+  std::memset(&d, 0, sizeof(d));
+  d.M = M; d.F = F; d.ldx = ldx; d.train = train; d.act = act;
+  d.X = X; d.Y = Y; d.gamma = gamma; d.beta = beta; d.eps = eps; d.momentum = momentum; d.slope = slope;
+  d.run_mean = running_mean; d.run_var = running_var; d.save_mean = save_mean; d.save_invstd = save_invstd;
+  HIPCHK(hipMemcpyAsync(ws, &d, sizeof(d), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(cgl_bn1d_fwd_k, dim3((F + 31) / 32), dim3(256), 0, s, (const CglBn1dDesc*)ws);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  HIPCHK(hipStreamSynchronize(s));   // the descriptor lives in the caller's workspace
+  return 0;
+}
+
+int cgl_bn1d_bwd(const float* dY, const float* Y, const float* X, int M, int F, const float* save_mean,
+                 const float* save_invstd, const float* gamma, int act, float slope, float* dX, float* dgamma,
+                 float* dbeta, void* ws, int64_t wsb, void* stream) {
+  if (!dY || !X || !save_mean || !save_invstd || !gamma || !dX || M < 1 || F < 1) return CGL_E_ARG;
+  if ((act != 0 && act != 1) || (act == 1 && !Y)) return CGL_E_ARG;
+  if (!ws || wsb < (int64_t)sizeof(CglBnBwdDesc) + 2 * 4 * (int64_t)F || !al16(ws)) return CGL_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  // gamma / beta grads land in the workspace when the caller does not want them
+  float* scratch = (float*)((char*)ws + ((sizeof(CglBnBwdDesc) + 255) & ~size_t(255)));
+  if (wsb < (int64_t)((sizeof(CglBnBwdDesc) + 255) & ~size_t(255)) + 2 * 4 * (int64_t)F) return CGL_E_ARG;
+  CglBnBwdDesc b;
+  std::memset(&b, 0, sizeof(b));
+  b.M = M; b.F = F;
+  b.dA = dY; b.ld_da = F;
+  b.post = act == 1 ? Y : nullptr; b.ld_post = F;
+  b.Y = X; b.ld_y = F;
+  b.mean = save_mean; b.invstd = save_invstd; b.gamma = gamma;
+  b.dZ = dX; b.ld_dz = F;
+  b.g_gamma = dgamma ? dgamma : scratch;
+  b.g_beta = dbeta ? dbeta : scratch + F;
+  b.slope = slope;
+  HIPCHK(hipMemcpyAsync(ws, &b, sizeof(b), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(cgl_bn_bwd, dim3((F + 31) / 32), dim3(256), 0, s, (const CglBnBwdDesc*)ws);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  HIPCHK(hipStreamSynchronize(s));
+  return 0;
 }
 
 int cgl_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int step, double lr, double beta1,

@@ -138,14 +138,16 @@ int cgl_gan_read_stats(cgl_gan* ctx, cgl_gan_stats* out, void* stream);
 /* Launch / kernel counts of a phase (for roofline bookkeeping). */
 int cgl_gan_plan_info(cgl_gan* ctx, int phase, int* n_launches, int* n_gemm_launches, double* gemm_flops);
 /* Per-launch access to the plan (instrumented timing: the caller brackets each launch with
- * events on `stream`).  kind: 0 GEMM, 1 loss head, 2 BN backward, 3 Adam, 4 round begin,
- * 5 normal RNG, 6 sampler.  flops = algorithmic GEMM flops of the launch (0 for others). */
+ * events on `stream`).  kind: 0 GEMM, 1 loss head, 2 BN backward, 3 Adam, 4 round prologue
+ * (scalars, z RNG, sampler), 5 BN forward apply.  flops = algorithmic GEMM flops (0 for others). */
 int cgl_gan_launch_count(cgl_gan* ctx, int phase);
 int cgl_gan_launch_info(cgl_gan* ctx, int phase, int idx, int* kind, double* flops, int* grid);
 int cgl_gan_launch_one(cgl_gan* ctx, int phase, int idx, void* stream);
 
 /* ---------------- single ops (nn.Module boundary: model/mnist_model.py) ---------------- */
-/* Y[M,N] = act(X[M,K] W[N,K]^T + b)   act: 0 none, 1 LeakyReLU(slope), 2 Tanh  (nn.Linear fwd) */
+/* Y[M,N] = act(X[M,K] W[N,K]^T + b)   act: 0 none, 1 LeakyReLU(slope), 2 Tanh, 3 Sigmoid
+ * (nn.Linear + the activation module that follows it: model/mnist_model.py:11-14,22-23,77-81,
+ * MDGAN/MNIST/mnist_model.py:41-42) */
 int cgl_linear_fwd(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, int act,
                    float slope, void* workspace, int64_t ws_bytes, void* stream);
 /* dX[M,K] = dY[M,N] W[N,K]   (nn.Linear backward, input grad) */
@@ -154,6 +156,22 @@ int cgl_linear_bwd_data(const float* dY, const float* W, float* dX, int M, int N
 /* dW[N,K] = dY^T X, db[N] = sum_rows dY   (nn.Linear backward, weight/bias grad) */
 int cgl_linear_bwd_weight(const float* dY, const float* X, float* dW, float* db, int M, int N, int K,
                           void* workspace, int64_t ws_bytes, void* stream);
+/* dX[n] = dY[n] * act'(Y[n]) given the activation OUTPUT Y (LeakyReLU / Tanh / Sigmoid backward) */
+int cgl_act_bwd(const float* dY, const float* Y, int64_t n, int act, float slope, float* dX, void* stream);
+/* Y[n] = act(X[n])  (a standalone nn.LeakyReLU / nn.Tanh / nn.Sigmoid) */
+int cgl_act_fwd(const float* X, int64_t n, int act, float slope, float* Y, void* stream);
+/* nn.BatchNorm1d(F, eps, momentum) [+ LeakyReLU(slope) when act == 1] on X[M,F] (row stride ldx):
+ * train != 0: batch statistics (biased variance for the output, unbiased for running_var),
+ * running stats updated, save_mean / save_invstd written (may be null);
+ * train == 0: running statistics (eval mode, capgan.py:204-208).  (model/mnist_model.py:13) */
+int cgl_bn1d_fwd(const float* X, int M, int F, int ldx, const float* gamma, const float* beta, double eps,
+                 double momentum, float* running_mean, float* running_var, int train, int act, float slope, float* Y,
+                 float* save_mean, float* save_invstd, void* workspace, int64_t ws_bytes, void* stream);
+/* Train-mode backward of the above: dY = grad of the (activated) output Y (row stride F);
+ * act == 1 applies LeakyReLU' from Y.  dX[M,F] = grad of X; dgamma, dbeta (may be null). */
+int cgl_bn1d_bwd(const float* dY, const float* Y, const float* X, int M, int F, const float* save_mean,
+                 const float* save_invstd, const float* gamma, int act, float slope, float* dX, float* dgamma,
+                 float* dbeta, void* workspace, int64_t ws_bytes, void* stream);
 /* Flat Adam step t (optim.Adam, torch _single_tensor_adam op order) */
 int cgl_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int step, double lr, double beta1,
                   double beta2, double eps, void* workspace, int64_t ws_bytes, void* stream);
