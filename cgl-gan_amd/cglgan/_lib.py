@@ -26,7 +26,14 @@ EXPORTS = [
     "cgl_gan_plan_info", "cgl_gan_launch_count", "cgl_gan_launch_info", "cgl_gan_launch_one", "cgl_linear_fwd", "cgl_linear_bwd_data", "cgl_linear_bwd_weight", "cgl_adam_step",
     "cgl_normal_fill", "cgl_op_workspace_bytes", "cgl_version", "cgl_act_fwd", "cgl_act_bwd", "cgl_bn1d_fwd",
     "cgl_bn1d_bwd",
+    # conv GAN path (model/lsgan.py)
+    "cgl_conv3x3_workspace_bytes", "cgl_conv3x3_fwd", "cgl_conv3x3_bwd_data", "cgl_conv3x3_bwd_weight",
+    "cgl_bn2d_workspace_bytes", "cgl_bn2d_fwd", "cgl_bn2d_bwd", "cgl_act_drop_bwd", "cgl_dropout2d_mask",
+    "cgl_nchw_to_nhwc", "cgl_nhwc_to_nchw", "cgl_adv_loss", "cgl_adam_multi", "cgl_dense_workspace_bytes",
+    "cgl_dense_fwd", "cgl_dense_bwd_data", "cgl_dense_bwd_weight", "cgl_gather_rows",
 ]
+
+LOSS_OP_CE2, LOSS_OP_BCE, LOSS_OP_MSE, LOSS_OP_BCE_LOGIT = 0, 1, 2, 3
 
 
 class MlpSpec(ctypes.Structure):
@@ -94,6 +101,24 @@ def _load():
         "cgl_bn1d_fwd": (ci, [vp, ci, ci, ci, vp, vp, cd, cd, vp, vp, ci, ci, cf, vp, vp, vp, vp, i64, vp]),
         "cgl_bn1d_bwd": (ci, [vp, vp, vp, ci, ci, vp, vp, vp, ci, cf, vp, vp, vp, vp, i64, vp]),
         "cgl_op_workspace_bytes": (i64, []),
+        "cgl_conv3x3_workspace_bytes": (i64, [ci] * 7),
+        "cgl_conv3x3_fwd": (ci, [vp, vp, vp, vp] + [ci] * 9 + [cf, vp, vp, i64, vp]),
+        "cgl_conv3x3_bwd_data": (ci, [vp, vp, vp] + [ci] * 7 + [vp, i64, vp]),
+        "cgl_conv3x3_bwd_weight": (ci, [vp, vp, vp, vp] + [ci] * 7 + [vp, i64, vp]),
+        "cgl_bn2d_workspace_bytes": (i64, [ci] * 4),
+        "cgl_bn2d_fwd": (ci, [vp, ci, ci, ci, ci, vp, vp, cd, cd, vp, vp, ci, ci, cf, vp, vp, vp, vp, i64, vp]),
+        "cgl_bn2d_bwd": (ci, [vp, vp, vp, ci, ci, ci, ci, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, i64, vp]),
+        "cgl_act_drop_bwd": (ci, [vp, vp, vp, ci, ci, ci, cf, ci, vp, vp]),
+        "cgl_dropout2d_mask": (ci, [vp, ci, ci, cd, ctypes.c_ulonglong, ctypes.c_ulonglong, vp]),
+        "cgl_nchw_to_nhwc": (ci, [vp, vp, ci, ci, ci, vp]),
+        "cgl_nhwc_to_nchw": (ci, [vp, vp, ci, ci, ci, vp]),
+        "cgl_adv_loss": (ci, [vp, ci, ci, ci, ci, cd, vp, vp, vp]),
+        "cgl_dense_workspace_bytes": (i64, [ci] * 3),
+        "cgl_dense_fwd": (ci, [vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, i64, vp]),
+        "cgl_dense_bwd_data": (ci, [vp, vp, vp, ci, ci, ci, vp, i64, vp]),
+        "cgl_dense_bwd_weight": (ci, [vp, vp, vp, vp, ci, ci, ci, vp, i64, vp]),
+        "cgl_gather_rows": (ci, [vp, vp, i64, ci, ci, vp, vp]),
+        "cgl_adam_multi": (ci, [ci, P(vp), P(vp), P(vp), P(vp), P(i64), ci, cd, cd, cd, cd, vp]),
         "cgl_version": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():

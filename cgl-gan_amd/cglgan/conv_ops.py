@@ -1,0 +1,189 @@
+"""Checked Python wrappers of the conv-path C ABI (include/cglgan.h, "conv GAN ops").
+
+Tensors are float32 CUDA (ROCm) tensors; activations are NHWC -- a logically NCHW tensor in
+``torch.channels_last`` memory, or a plain contiguous [n, h, w, c] tensor -- and weights keep the
+reference nn.Conv2d layout [cout][cin][3][3].  Every call is stream-ordered on the current torch
+stream (no host synchronisation) and raises on a non-zero return code; there is no fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib as C
+
+ACT_NONE, ACT_LEAKY, ACT_TANH, ACT_SIGMOID = 0, 1, 2, 3
+LOSS = {"ce": C.LOSS_OP_CE2, "bce_prob": C.LOSS_OP_BCE, "mse": C.LOSS_OP_MSE, "bce": C.LOSS_OP_BCE_LOGIT}
+
+_WS = {}
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _s():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def workspace(nbytes: int, device) -> torch.Tensor:
+    """Per-device scratch owned by the caching allocator (grown on demand; ops on one stream are
+    ordered, so one buffer serves every op)."""
+    dev = torch.device(device)
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    w = _WS.get(key)
+    if w is None or w.numel() < nbytes:
+        w = torch.empty(max(int(nbytes), 1 << 20), dtype=torch.uint8, device=dev)
+        _WS[key] = w
+    return w
+
+
+def _chk(*ts):
+    for t in ts:
+        if t is not None and (not t.is_cuda or t.dtype != torch.float32):
+            raise RuntimeError("cglgan conv ops compute on the GPU only: expected float32 CUDA (ROCm) tensors")
+
+
+def conv_out_hw(h, w, stride, up):
+    return ((h << up) - 1) // stride + 1, ((w << up) - 1) // stride + 1
+
+
+def conv_ws_bytes(n, h, w, cin, cout, stride, up):
+    b = C.lib.cgl_conv3x3_workspace_bytes(n, h, w, cin, cout, stride, up)
+    if b < 0:
+        raise RuntimeError(f"conv3x3: bad geometry (rc={b})")
+    return b
+
+
+def conv3x3_fwd(x, w, b, y, n, h, wd, cin, cout, stride=1, up=0, act=ACT_NONE, slope=0.2, drop=None):
+    _chk(x, w, b, y, drop)
+    ws = workspace(conv_ws_bytes(n, h, wd, cin, cout, stride, up), x.device)
+    C.check(C.lib.cgl_conv3x3_fwd(_p(x), _p(w), _p(b), _p(y), n, h, wd, cin, cout, stride, up, act, float(slope),
+                                  _p(drop), _p(ws), ws.numel(), _s()), "cgl_conv3x3_fwd")
+    return y
+
+
+def conv3x3_bwd_data(dy, w, dx, n, h, wd, cin, cout, stride=1, up=0):
+    _chk(dy, w, dx)
+    ws = workspace(conv_ws_bytes(n, h, wd, cin, cout, stride, up), dy.device)
+    C.check(C.lib.cgl_conv3x3_bwd_data(_p(dy), _p(w), _p(dx), n, h, wd, cin, cout, stride, up, _p(ws), ws.numel(),
+                                       _s()), "cgl_conv3x3_bwd_data")
+    return dx
+
+
+def conv3x3_bwd_weight(dy, x, dw, db, n, h, wd, cin, cout, stride=1, up=0):
+    _chk(dy, x, dw, db)
+    ws = workspace(conv_ws_bytes(n, h, wd, cin, cout, stride, up), dy.device)
+    C.check(C.lib.cgl_conv3x3_bwd_weight(_p(dy), _p(x), _p(dw), _p(db), n, h, wd, cin, cout, stride, up, _p(ws),
+                                         ws.numel(), _s()), "cgl_conv3x3_bwd_weight")
+    return dw
+
+
+def dense_ws_bytes(M, K, N):
+    b = C.lib.cgl_dense_workspace_bytes(M, K, N)
+    if b < 0:
+        raise RuntimeError(f"dense: bad geometry (rc={b})")
+    return b
+
+
+def dense_fwd(x, w, b, y, M, K, N, act=ACT_NONE, slope=0.2):
+    _chk(x, w, b, y)
+    ws = workspace(dense_ws_bytes(M, K, N), x.device)
+    C.check(C.lib.cgl_dense_fwd(_p(x), _p(w), _p(b), _p(y), M, K, N, act, float(slope), _p(ws), ws.numel(), _s()),
+            "cgl_dense_fwd")
+    return y
+
+
+def dense_bwd_data(dy, w, dx, M, K, N):
+    _chk(dy, w, dx)
+    ws = workspace(dense_ws_bytes(M, K, N), dy.device)
+    C.check(C.lib.cgl_dense_bwd_data(_p(dy), _p(w), _p(dx), M, K, N, _p(ws), ws.numel(), _s()), "cgl_dense_bwd_data")
+    return dx
+
+
+def dense_bwd_weight(dy, x, dw, db, M, K, N):
+    _chk(dy, x, dw, db)
+    ws = workspace(dense_ws_bytes(M, K, N), dy.device)
+    C.check(C.lib.cgl_dense_bwd_weight(_p(dy), _p(x), _p(dw), _p(db), M, K, N, _p(ws), ws.numel(), _s()),
+            "cgl_dense_bwd_weight")
+    return dw
+
+
+def gather_rows(src, idx, row0, nrows, row_floats, dst):
+    _chk(src, dst)
+    if idx is not None and (not idx.is_cuda or idx.dtype != torch.int32):
+        raise RuntimeError("gather_rows: idx must be an int32 CUDA tensor")
+    C.check(C.lib.cgl_gather_rows(_p(src), _p(idx), int(row0), nrows, row_floats, _p(dst), _s()), "cgl_gather_rows")
+    return dst
+
+
+def bn2d_ws_bytes(n, hw, c, groups):
+    b = C.lib.cgl_bn2d_workspace_bytes(n, hw, c, groups)
+    if b < 0:
+        raise RuntimeError(f"bn2d: bad geometry (rc={b})")
+    return b
+
+
+def bn2d_fwd(x, n, hw, c, gamma, beta, y, groups=1, eps=0.8, momentum=0.1, running_mean=None, running_var=None,
+             train=True, act=ACT_NONE, slope=0.2, save_mean=None, save_invstd=None):
+    _chk(x, gamma, beta, y, running_mean, running_var, save_mean, save_invstd)
+    ws = workspace(bn2d_ws_bytes(n, hw, c, groups), x.device)
+    C.check(C.lib.cgl_bn2d_fwd(_p(x), n, hw, c, groups, _p(gamma), _p(beta), float(eps), float(momentum),
+                               _p(running_mean), _p(running_var), int(train), act, float(slope), _p(y), _p(save_mean),
+                               _p(save_invstd), _p(ws), ws.numel(), _s()), "cgl_bn2d_fwd")
+    return y
+
+
+def bn2d_bwd(dy, x, n, hw, c, save_mean, save_invstd, gamma, dx, groups=1, post=None, post_out=None, drop=None,
+             dgamma=None, dbeta=None, slope=0.2):
+    _chk(dy, x, save_mean, save_invstd, gamma, dx, post, post_out, drop, dgamma, dbeta)
+    ws = workspace(bn2d_ws_bytes(n, hw, c, groups), dy.device)
+    C.check(C.lib.cgl_bn2d_bwd(_p(dy), _p(post), _p(x), n, hw, c, groups, _p(save_mean), _p(save_invstd), _p(gamma),
+                               float(slope), _p(post_out), _p(drop), _p(dx), _p(dgamma), _p(dbeta), _p(ws), ws.numel(),
+                               _s()), "cgl_bn2d_bwd")
+    return dx
+
+
+def act_drop_bwd(dy, post, drop, n, hw, c, dx, slope=0.2, tanh_y=False):
+    _chk(dy, post, drop, dx)
+    C.check(C.lib.cgl_act_drop_bwd(_p(dy), _p(post), _p(drop), n, hw, c, float(slope), int(tanh_y), _p(dx), _s()),
+            "cgl_act_drop_bwd")
+    return dx
+
+
+def dropout2d_mask(mask, n, c, p, seed, counter):
+    _chk(mask)
+    C.check(C.lib.cgl_dropout2d_mask(_p(mask), n, c, float(p), int(seed) & (2 ** 64 - 1), int(counter) & (2 ** 64 - 1),
+                                     _s()), "cgl_dropout2d_mask")
+    return mask
+
+
+def nchw_to_nhwc(x, y, n, c, hw):
+    _chk(x, y)
+    C.check(C.lib.cgl_nchw_to_nhwc(_p(x), _p(y), n, c, hw, _s()), "cgl_nchw_to_nhwc")
+    return y
+
+
+def nhwc_to_nchw(x, y, n, c, hw):
+    _chk(x, y)
+    C.check(C.lib.cgl_nhwc_to_nchw(_p(x), _p(y), n, c, hw, _s()), "cgl_nhwc_to_nchw")
+    return y
+
+
+def adv_loss(x, M, Cc, kind, target, weight, loss_out=None, grad=None):
+    _chk(x, loss_out, grad)
+    C.check(C.lib.cgl_adv_loss(_p(x), M, Cc, LOSS[kind], int(target), float(weight), _p(loss_out), _p(grad), _s()),
+            "cgl_adv_loss")
+
+
+def adam_multi(params, grads, ms, vs, step, lr=2e-4, betas=(0.5, 0.999), eps=1e-8):
+    """One optim.Adam step over up to 32 tensors per launch (chunks larger lists)."""
+    for i in range(0, len(params), 32):
+        ps, gs, mm, vv = params[i:i + 32], grads[i:i + 32], ms[i:i + 32], vs[i:i + 32]
+        _chk(*ps, *gs, *mm, *vv)
+        nt = len(ps)
+        arr = lambda ts: (ctypes.c_void_p * nt)(*[t.data_ptr() for t in ts])
+        ns = (ctypes.c_int64 * nt)(*[t.numel() for t in ps])
+        C.check(C.lib.cgl_adam_multi(nt, arr(ps), arr(gs), arr(mm), arr(vv), ns, int(step), float(lr), float(betas[0]),
+                                     float(betas[1]), float(eps), _s()), "cgl_adam_multi")

@@ -1,0 +1,1554 @@
+// Conv GAN path of model/lsgan.py on gfx950: 3x3 convolutions as implicit GEMMs on NHWC
+// activations (fp32 MFMA), BatchNorm2d, Dropout2d masks, the adversarial losses, NCHW<->NHWC
+// layout changes and a multi-tensor Adam -- every op the reference runs implicitly through
+// PyTorch for its conv generator / discriminator:
+//
+//   nn.Upsample(scale_factor=2) + nn.Conv2d(c, c', 3, 1, 1)       model/lsgan.py:11-12, 15-16
+//   nn.Conv2d(64, 1, 3, 1, 1) + nn.Tanh                          model/lsgan.py:19-20
+//   nn.Conv2d(c, c', 3, 2, 1) + LeakyReLU(0.2) + Dropout2d(0.25) model/lsgan.py:78
+//   nn.BatchNorm2d(c, 0.8)                                       model/lsgan.py:13, 17, 80
+//   out.view(B, 128, 8, 8) / out.view(B, -1)                     model/lsgan.py:25, 96 (layout only)
+//
+// Design (MI355X-first):
+//  * Activations are NHWC ("channels_last"): a pixel's channels are contiguous, so an implicit
+//    im2col row segment of 8 consecutive k (one tap, 8 channels) is two 16-byte loads.
+//  * One MFMA kernel (v_mfma_f32_32x32x2_f32, exact f32) computes every forward and input-gradient
+//    convolution from a TAP TABLE: output pixels are enumerated on a (possibly strided) grid,
+//    each tap reads the input at (oy*isy + dy[t], ox*isx + dx[t]), and the weights are packed per
+//    call into B[n][t*Cin + c] (k-contiguous).  Nearest-neighbour x2 upsampling followed by a 3x3
+//    convolution is computed in PHASE form: each of the 4 output parities is a 2x2 convolution of
+//    the low-resolution input with combined weights (e.g. W[1]+W[2]), and its input gradient is one
+//    4x4-tap convolution of the output gradient at stride 2 -- 16 instead of 36 MACs per
+//    (pixel, cin, cout), and neither the upsampled tensor nor its gradient is ever materialised.
+//    The stride-2 discriminator convolutions' input gradients are likewise 4 parity problems with
+//    1, 2, 2 and 4 taps.  Up to 4 problems share one launch (grouped, XCD-aware tile order).
+//  * Weight gradients use the same tap tables: an MFMA GEMM over pixels (the reduction dim)
+//    split across workgroups, partial tiles reduced in a fixed order (deterministic, no atomics)
+//    and folded back onto the 3x3 OIHW weights.
+//  * BatchNorm2d statistics: per-chunk {sum, M2} partials in double, Chan-combined per forward
+//    call (group) in a fixed order, torch's formulas (biased variance for the output, unbiased for
+//    running_var); backward as torch's batch_norm_backward.  Dropout2d masks come from
+//    Philox4x32-10 per (image, channel).
+//  * Every launch takes its descriptor by value (kernel arguments): no uploads, no host syncs, so
+//    the ops are stream-ordered and capturable in a hipGraph.
+//
+// Unity build: included by cgl_runtime.hip (shares cgl_internal.h, cgl_philox, cgl_lerp, HIPCHK).
+
+#define CGL_CONV_MAXP 4
+#define CGL_AS4 __attribute__((address_space(4)))
+
+struct CglConvProb {
+  int M, N, K, Kp;           // enumerated output pixels, output channels, K = taps * Cin, packed row length
+  int OH, OW;                // enumerated output grid per image
+  int osy, osx, ooy, oox;    // stored output position (oy * osy + ooy, ox * osx + oox)
+  int YH, YW, ldy;           // stored output dims and channel count (pixel stride)
+  int isy, isx;              // input step per enumerated output pixel
+  int IH, IW, ish;           // virtual input bounds; stored input is read at (iy >> ish, ix >> ish)
+  int XH, XW, Cin;           // stored input dims / channels
+  int Ty, Tx;                // tap grid, t = ty * Tx + tx
+  int dy[4], dx[4];          // tap offsets
+  int ym[4], xm[4];          // kernel rows / columns combined into each tap (bitmask of kh / kw)
+  int wg_begin, tiles_m, tiles_n, splits;
+  const float* X;
+  const float* Wp;           // packed weights [N][Kp]
+  float* Y;                  // output (fwd), or the output gradient dY (wgrad, read only)
+  float* part;               // wgrad partials [splits][N][Kp]
+};
+
+struct CglConvLaunch {
+  CglConvProb p[CGL_CONV_MAXP];
+  int np, WM, WN;
+  const float* bias;         // [N] or null
+  int act;                   // CGL_EPI_ACT_*
+  float slope;
+  const float* drop;         // Dropout2d scale per (image, channel) [img][ldy], or null
+};
+
+typedef const CGL_AS4 CglConvLaunch* CglKL;
+typedef const CGL_AS4 CglConvProb* CglKP;
+
+// The launch descriptor is the kernel's first (by-value) argument: read it through the kernarg
+// segment pointer so that uniform-indexed fields become scalar loads (a dynamically indexed
+// by-value struct would otherwise be copied to scratch).
+__device__ __forceinline__ CglKL cgl_conv_args() { return (CglKL)__builtin_amdgcn_kernarg_segment_ptr(); }
+
+__device__ __forceinline__ int cgl_conv_prob(CglKL L, int bid) {
+  int pi = 0;
+  for (int q = 1; q < L->np; ++q)
+    if (bid >= L->p[q].wg_begin) pi = q;
+  return pi;
+}
+
+__device__ __forceinline__ void cgl_conv_pix(CglKP P, int m, int& img, int& oy, int& ox) {
+  const int hw = P->OH * P->OW;
+  img = m / hw;
+  const int r = m - img * hw;
+  oy = r / P->OW;
+  ox = r - oy * P->OW;
+}
+
+__device__ __forceinline__ int cgl_xcd_tile(int local, int nwg) {
+  if (nwg < 16) return local;
+  const int xcd = local & 7, pos = local >> 3, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+}
+
+// ------------------------------------------------------------------------------------------
+// Forward / input-gradient convolution: C[m][n] = sum_k A[m][k] Wp[n][k] with the implicit A of
+// the tap table.  One wave owns TM x TN 32x32 accumulators; WM x WN waves per workgroup.
+// FAST: Cin % 16 == 0, so a 16-k chunk lies inside one tap (uniform tap, 2 x 16-byte loads per
+// lane and block).  Otherwise each k is decoded per element (tiny-K layers: Cin = 1).
+template <int TM, int TN, bool FAST>
+__device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local) {
+  constexpr int S = 3;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, li = lane & 31, lh = lane >> 5;
+  const int WN = L->WN, WM = L->WM;
+  const int wm = wave / WN, wn = wave - wm * WN;
+  const int tiles_n = P->tiles_n;
+  const int tile = cgl_xcd_tile(local, P->tiles_m * tiles_n);
+  const int tn = tile % tiles_n, tm = tile / tiles_n;
+  const int M = P->M, N = P->N, K = P->K, Kp = P->Kp, Cin = P->Cin;
+  const int IH = P->IH, IW = P->IW, ish = P->ish, XW = P->XW, Tx = P->Tx;
+  const int m0 = tm * 32 * TM * WM + wm * 32 * TM;
+  const int n0 = (tn * WN + wn) * 32 * TN;
+  const float* __restrict__ X = P->X;
+
+  int ay[TM], ax[TM];
+  long aoff[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int img, oy, ox;
+    cgl_conv_pix(P, min(m0 + 32 * i + li, M - 1), img, oy, ox);
+    ay[i] = oy * P->isy;
+    ax[i] = ox * P->isx;
+    aoff[i] = (long)img * P->XH * XW * Cin;
+  }
+  const float* brow[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) brow[j] = P->Wp + (long)min(n0 + 32 * j + li, N - 1) * Kp;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto load = [&](int c, float (&A)[TM][8], float (&B)[TN][8], int& okm) {
+    const int k0 = c * 16;
+    okm = 0;
+    if (FAST) {
+      const int t = k0 / Cin;   // uniform: the chunk lies inside one tap
+      const int ci = k0 - t * Cin + 8 * lh;
+      const int ty = t / Tx, tx = t - ty * Tx;
+      const int dyv = P->dy[ty], dxv = P->dx[tx];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int iy = ay[i] + dyv, ix = ax[i] + dxv;
+        const bool ok = (unsigned)iy < (unsigned)IH && (unsigned)ix < (unsigned)IW;
+        okm |= ok ? (1 << i) : 0;
+        const int cy = min(max(iy, 0), IH - 1) >> ish, cx = min(max(ix, 0), IW - 1) >> ish;
+        gcfp p = (gcfp)(X + aoff[i] + ((long)cy * XW + cx) * Cin + ci);
+        const f32x4 u = *(gcf4p)p, w = *(gcf4p)(p + 4);
+        A[i][0] = u[0]; A[i][1] = u[1]; A[i][2] = u[2]; A[i][3] = u[3];
+        A[i][4] = w[0]; A[i][5] = w[1]; A[i][6] = w[2]; A[i][7] = w[3];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int k = k0 + 8 * lh + q;
+          const int kk = min(k, K - 1);
+          const int t = kk / Cin, ci = kk - t * Cin;
+          const int ty = t / Tx, tx = t - ty * Tx;
+          const int iy = ay[i] + P->dy[ty], ix = ax[i] + P->dx[tx];
+          const bool ok = k < K && (unsigned)iy < (unsigned)IH && (unsigned)ix < (unsigned)IW;
+          okm |= ok ? (1 << (i * 8 + q)) : 0;
+          const int cy = min(max(iy, 0), IH - 1) >> ish, cx = min(max(ix, 0), IW - 1) >> ish;
+          A[i][q] = ((gcfp)X)[aoff[i] + ((long)cy * XW + cx) * Cin + ci];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      gcfp p = (gcfp)(brow[j] + k0 + 8 * lh);
+      const f32x4 u = *(gcf4p)p, w = *(gcf4p)(p + 4);
+      B[j][0] = u[0]; B[j][1] = u[1]; B[j][2] = u[2]; B[j][3] = u[3];
+      B[j][4] = w[0]; B[j][5] = w[1]; B[j][6] = w[2]; B[j][7] = w[3];
+    }
+  };
+  auto compute = [&](float (&A)[TM][8], float (&B)[TN][8], int okm) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      if (FAST) {
+        const bool ok = (okm >> i) & 1;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) A[i][q] = ok ? A[i][q] : 0.f;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) A[i][q] = ((okm >> (i * 8 + q)) & 1) ? A[i][q] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[i][q], B[j][q], acc[i][j], 0, 0, 0);
+  };
+
+  // S register sets in rotation (S - 1 chunks of loads in flight); Kp % 16 == 0, no K tail
+  const int nch = Kp >> 4;
+  float xa[S][TM][8], xb[S][TN][8];
+  int okm[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) load(min(s, nch - 1), xa[s], xb[s], okm[s]);
+  int c = 0;
+  for (; c + S <= nch; c += S) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      compute(xa[s], xb[s], okm[s]);
+      load(min(c + s + S, nch - 1), xa[s], xb[s], okm[s]);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (c + s < nch) compute(xa[s], xb[s], okm[s]);
+
+  // epilogue: bias, activation, Dropout2d scale, NHWC store at the mapped position
+  const int ldy = P->ldy, YH = P->YH, YW = P->YW;
+  const int osy = P->osy, osx = P->osx, ooy = P->ooy, oox = P->oox;
+  const float* __restrict__ bias = L->bias;
+  const float* __restrict__ drop = L->drop;
+  const int act = L->act;
+  const float sl = L->slope;
+  float* __restrict__ Y = P->Y;
+  float bj[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = min(n0 + 32 * j + li, N - 1);
+    bj[j] = bias ? gld(bias + col) : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = m0 + 32 * i + 4 * lh + (r & 3) + 8 * (r >> 2);
+      if (row >= M) continue;
+      int img, oy, ox;
+      cgl_conv_pix(P, row, img, oy, ox);
+      const long pix = ((long)img * YH + oy * osy + ooy) * YW + ox * osx + oox;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + 32 * j + li;
+        if (col >= N) continue;
+        float v = acc[i][j][r] + bj[j];
+        if (act == CGL_EPI_ACT_LEAKY) v = v > 0.f ? v : v * sl;
+        else if (act == CGL_EPI_ACT_TANH) v = tanhf(v);
+        else if (act == CGL_EPI_ACT_SIGMOID) v = 1.f / (1.f + expf(-v));
+        if (drop) v *= gld(drop + (long)img * ldy + col);
+        gst(Y + pix * ldy + col, v);
+      }
+    }
+  }
+}
+
+template <int TM, int TN, bool FAST>
+__global__ __launch_bounds__(256) void cgl_conv_fwd(CglConvLaunch args) {
+  (void)args;
+  CglKL L = cgl_conv_args();
+  const int bid = blockIdx.x;
+  const int pi = cgl_conv_prob(L, bid);
+  CglKP P = &L->p[pi];
+  cgl_conv_fwd_body<TM, TN, FAST>(L, P, bid - P->wg_begin);
+}
+
+// ------------------------------------------------------------------------------------------
+// Weight gradient: part[s][n][k] = sum over the pixels m of split s of dY[pos(m)][n] * A[m][k]
+// (A = the tap table's implicit im2col of X).  Rows of the result tile are output channels
+// (operand A = dY, 32 consecutive channels of one pixel per lane group: coalesced), columns are
+// im2col columns (operand B, consecutive channels of one tap: coalesced); each lane half takes 8
+// consecutive pixels of a 16-pixel chunk (the MFMA k permutation of cgl_gemm.hip).
+// Work unit = one wave: (tile, split) with a (32 TM) x (32 TN) result tile; a workgroup runs 4
+// consecutive units (no LDS, no barriers), so small layers (Conv2d(1, 16): 16 x 9 results) do not
+// pay for a large workgroup tile.
+template <int TM, int TN>
+__device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local) {
+  constexpr int S = 2;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, li = lane & 31, lh = lane >> 5;
+  const int tiles = P->tiles_m * P->tiles_n;
+  const int unit = local * 4 + wave;
+  if (unit >= tiles * P->splits) return;
+  const int split = unit / tiles;
+  const int tile = unit - split * tiles;
+  const int tn = tile % P->tiles_n, tm = tile / P->tiles_n;
+  const int M = P->M, N = P->N, K = P->K, Kp = P->Kp, Cin = P->Cin;
+  const int IH = P->IH, IW = P->IW, ish = P->ish, XW = P->XW, XH = P->XH, Tx = P->Tx;
+  const int n0 = tm * 32 * TM;
+  const int k0c = tn * 32 * TN;
+  const float* __restrict__ X = P->X;
+  const float* __restrict__ dY = P->Y;
+  const int ldy = P->ldy, YH = P->YH, YW = P->YW;
+  const int osy = P->osy, osx = P->osx, ooy = P->ooy, oox = P->oox, isy = P->isy, isx = P->isx;
+
+  int rch[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) rch[i] = min(n0 + 32 * i + li, N - 1);
+  int cdy[TN], cdx[TN], cci[TN];
+  bool cok[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int kc = k0c + 32 * j + li;
+    cok[j] = kc < K;
+    const int kk = min(kc, K - 1);
+    const int t = kk / Cin;
+    cci[j] = kk - t * Cin;
+    const int ty = t / Tx, tx = t - ty * Tx;
+    cdy[j] = P->dy[ty];
+    cdx[j] = P->dx[tx];
+  }
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // masks: bit q (A, pixel valid), bit 8 + j * 8 + q (B, tap in bounds)
+  auto load = [&](int c, float (&A)[TM][8], float (&B)[TN][8], int& okm) {
+    okm = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int m = c * 16 + 8 * lh + q;
+      const bool mv = m < M;
+      int img, oy, ox;
+      cgl_conv_pix(P, min(m, M - 1), img, oy, ox);
+      const long ya = (((long)img * YH + oy * osy + ooy) * YW + ox * osx + oox) * ldy;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) A[i][q] = ((gcfp)dY)[ya + rch[i]];
+      okm |= mv ? (1 << q) : 0;
+      const long xo = (long)img * XH * XW * Cin;
+      const int iyb = oy * isy, ixb = ox * isx;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int iy = iyb + cdy[j], ix = ixb + cdx[j];
+        const bool ok = mv && cok[j] && (unsigned)iy < (unsigned)IH && (unsigned)ix < (unsigned)IW;
+        okm |= ok ? (1 << (8 + j * 8 + q)) : 0;
+        const int cy = min(max(iy, 0), IH - 1) >> ish, cx = min(max(ix, 0), IW - 1) >> ish;
+        B[j][q] = ((gcfp)X)[xo + ((long)cy * XW + cx) * Cin + cci[j]];
+      }
+    }
+  };
+  auto compute = [&](float (&A)[TM][8], float (&B)[TN][8], int okm) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const bool mv = (okm >> q) & 1;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) A[i][q] = mv ? A[i][q] : 0.f;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) B[j][q] = ((okm >> (8 + j * 8 + q)) & 1) ? B[j][q] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[i][q], B[j][q], acc[i][j], 0, 0, 0);
+  };
+
+  const int nchk = (M + 15) >> 4;
+  const int splits = P->splits;
+  const int cb = (int)(((long)split * nchk) / splits), ce = (int)(((long)(split + 1) * nchk) / splits);
+  if (cb < ce) {
+    float xa[S][TM][8], xb[S][TN][8];
+    int okm[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) load(min(cb + s, ce - 1), xa[s], xb[s], okm[s]);
+    int c = cb;
+    for (; c + S <= ce; c += S) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        compute(xa[s], xb[s], okm[s]);
+        load(min(c + s + S, ce - 1), xa[s], xb[s], okm[s]);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < S - 1; ++s)
+      if (c + s < ce) compute(xa[s], xb[s], okm[s]);
+  }
+
+  float* __restrict__ part = P->part + (long)split * N * Kp;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int kc = k0c + 32 * j + li;
+    if (kc >= K) continue;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = n0 + 32 * i + 4 * lh + (r & 3) + 8 * (r >> 2);
+        if (n < N) gst(part + (long)n * Kp + kc, acc[i][j][r]);
+      }
+  }
+}
+
+template <int TM, int TN>
+__global__ __launch_bounds__(256) void cgl_conv_wgrad(CglConvLaunch args) {
+  (void)args;
+  CglKL L = cgl_conv_args();
+  const int bid = blockIdx.x;
+  const int pi = cgl_conv_prob(L, bid);
+  CglKP P = &L->p[pi];
+  cgl_conv_wgrad_body<TM, TN>(L, P, bid - P->wg_begin);
+}
+
+// ------------------------------------------------------------------------------------------
+// One-output-channel convolution on the vector ALUs (N == 1: Conv2d(64, 1) of the generator's
+// last layer, and the input gradient of the discriminator's Conv2d(1, 16)) -- an MFMA tile would
+// waste 31 of its 32 columns.  One thread per enumerated output pixel; Cin % 4 == 0.
+__global__ __launch_bounds__(256) void cgl_conv_n1(CglConvLaunch args) {
+  (void)args;
+  CglKL L = cgl_conv_args();
+  const int bid = blockIdx.x;
+  const int pi = cgl_conv_prob(L, bid);
+  CglKP P = &L->p[pi];
+  const int m = (bid - P->wg_begin) * 256 + threadIdx.x;
+  if (m >= P->M) return;
+  int img, oy, ox;
+  cgl_conv_pix(P, m, img, oy, ox);
+  const int Cin = P->Cin, Tx = P->Tx, T = P->Ty * P->Tx;
+  const int IH = P->IH, IW = P->IW, ish = P->ish, XW = P->XW;
+  const float* __restrict__ X = P->X + (long)img * P->XH * XW * Cin;
+  const float* __restrict__ Wp = P->Wp;
+  float acc = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const int ty = t / Tx, tx = t - ty * Tx;
+    const int iy = oy * P->isy + P->dy[ty], ix = ox * P->isx + P->dx[tx];
+    if ((unsigned)iy >= (unsigned)IH || (unsigned)ix >= (unsigned)IW) continue;
+    gcfp xp = (gcfp)(X + ((long)(iy >> ish) * XW + (ix >> ish)) * Cin);
+    gcfp wp = (gcfp)(Wp + t * Cin);
+    for (int c = 0; c < Cin; c += 4) {
+      const f32x4 v = *(gcf4p)(xp + c);
+      acc = fmaf(v[0], wp[c], acc);
+      acc = fmaf(v[1], wp[c + 1], acc);
+      acc = fmaf(v[2], wp[c + 2], acc);
+      acc = fmaf(v[3], wp[c + 3], acc);
+    }
+  }
+  float v = acc + (L->bias ? gld(L->bias) : 0.f);
+  if (L->act == CGL_EPI_ACT_LEAKY) v = v > 0.f ? v : v * L->slope;
+  else if (L->act == CGL_EPI_ACT_TANH) v = tanhf(v);
+  else if (L->act == CGL_EPI_ACT_SIGMOID) v = 1.f / (1.f + expf(-v));
+  if (L->drop) v *= gld(L->drop + (long)img * P->ldy);
+  gst(P->Y + (((long)img * P->YH + oy * P->osy + P->ooy) * P->YW + ox * P->osx + P->oox) * P->ldy, v);
+}
+
+// ------------------------------------------------------------------------------------------
+// Weight packing: Wp_p[n][k] = sum over the kernel taps combined into packed tap t of W (OIHW),
+// (co, ci) = (n, c) for a forward problem, (c, n) for an input-gradient problem (transpose);
+// zero for k >= K (row padding to a multiple of 16).
+struct CglPackArgs {
+  const float* W;            // [cout][cin][ks][ks]
+  int cout, cin, transpose, np, ks;
+  float* dst[CGL_CONV_MAXP];
+  int N[CGL_CONV_MAXP], Kp[CGL_CONV_MAXP], Cg[CGL_CONV_MAXP], Tx[CGL_CONV_MAXP], T[CGL_CONV_MAXP];
+  int ym[CGL_CONV_MAXP][4], xm[CGL_CONV_MAXP][4];
+  int begin[CGL_CONV_MAXP + 1];  // element offsets of each problem in the grid
+};
+
+__global__ __launch_bounds__(256) void cgl_conv_pack(CglPackArgs a) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= a.begin[a.np]) return;
+  int p = 0;
+  for (int q = 1; q < a.np; ++q)
+    if (e >= a.begin[q]) p = q;
+  const int local = e - a.begin[p];
+  const int Kp = a.Kp[p], Cg = a.Cg[p];
+  const int n = local / Kp, k = local - n * Kp;
+  float v = 0.f;
+  if (k < a.T[p] * Cg) {
+    const int t = k / Cg, c = k - t * Cg;
+    const int ty = t / a.Tx[p], tx = t - ty * a.Tx[p];
+    const int co = a.transpose ? c : n, ci = a.transpose ? n : c;
+    const int ks = a.ks;
+    const float* w = a.W + ((long)co * a.cin + ci) * ks * ks;
+    const int ymk = a.ym[p][ty], xmk = a.xm[p][tx];
+    for (int kh = 0; kh < ks; ++kh) {
+      if (!((ymk >> kh) & 1)) continue;
+      for (int kw = 0; kw < ks; ++kw)
+        if ((xmk >> kw) & 1) v += gld(w + kh * ks + kw);
+    }
+  }
+  gst(a.dst[p] + local, v);
+}
+
+// Weight-gradient reduction: dW[co][ci][kh][kw] = sum over problems, taps containing (kh, kw) and
+// splits (fixed order, double) of the partial tiles.  Thread e = ((co * 3 + kh) * 3 + kw) * cin + ci
+// (consecutive ci: coalesced partial reads).
+struct CglWgradReduceArgs {
+  float* dW;
+  int cout, cin, np, ks;
+  const float* part[CGL_CONV_MAXP];
+  int Kp[CGL_CONV_MAXP], splits[CGL_CONV_MAXP], Tx[CGL_CONV_MAXP], Ty[CGL_CONV_MAXP];
+  int ym[CGL_CONV_MAXP][4], xm[CGL_CONV_MAXP][4];
+};
+
+__global__ __launch_bounds__(256) void cgl_conv_wgrad_reduce(CglWgradReduceArgs a) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int cin = a.cin, ks = a.ks;
+  if (e >= a.cout * ks * ks * cin) return;
+  const int ci = e % cin;
+  const int rest = e / cin;
+  const int kw = rest % ks, kh = (rest / ks) % ks, co = rest / (ks * ks);
+  double acc = 0.0;
+  for (int p = 0; p < a.np; ++p) {
+    const int Kp = a.Kp[p], Tx = a.Tx[p], Ty = a.Ty[p], S = a.splits[p];
+    const long sstride = (long)a.cout * Kp;
+    for (int ty = 0; ty < Ty; ++ty) {
+      if (!((a.ym[p][ty] >> kh) & 1)) continue;
+      for (int tx = 0; tx < Tx; ++tx) {
+        if (!((a.xm[p][tx] >> kw) & 1)) continue;
+        const float* src = a.part[p] + (long)co * Kp + (ty * Tx + tx) * cin + ci;
+        for (int s = 0; s < S; ++s) acc += (double)gld(src + s * sstride);
+      }
+    }
+  }
+  gst(a.dW + ((long)co * cin + ci) * ks * ks + kh * ks + kw, (float)acc);
+}
+
+// ------------------------------------------------------------------------------------------
+// Per-channel reductions over an NHWC tensor [rows][C] (C a power of two <= 256), one chunk of R
+// rows per workgroup, double accumulation, fixed order:
+//   mode 0  {sum x, M2 about the chunk mean}                            (BatchNorm2d statistics)
+//   mode 1  {sum g, sum g (x - mean_group)},  g = dY * leaky'(post)      (BatchNorm2d backward)
+//   mode 2  {sum x, 0}                                                  (bias gradient)
+struct CglChanArgs {
+  const float* X; int rows, C, R, mode, hw, gr;
+  const float* dY; const float* post; float slope;
+  const float* mean;         // [groups][C] (mode 1)
+  double* part;              // [nchunks][C][2]
+};
+
+__global__ __launch_bounds__(256) void cgl_chan_reduce(CglChanArgs a) {
+  __shared__ double s0[256], s1[256];
+  const int C = a.C, rp = 256 / C;
+  const int c = threadIdx.x % C, rl = threadIdx.x / C;
+  const int r0 = blockIdx.x * a.R, r1 = min(r0 + a.R, a.rows);
+  double x0 = 0.0, x1 = 0.0;
+  if (a.mode == 1) {
+    const float mu = gld(a.mean + (long)(r0 / a.gr) * C + c);
+    for (int r = r0 + rl; r < r1; r += rp) {
+      const long o = (long)r * C + c;
+      float g = gld(a.dY + o);
+      if (a.post) g = gld(a.post + o) > 0.f ? g : g * a.slope;
+      x0 += (double)g;
+      x1 += (double)(g * (gld(a.X + o) - mu));
+    }
+  } else {
+    for (int r = r0 + rl; r < r1; r += rp) x0 += (double)gld(a.X + (long)r * C + c);
+  }
+  s0[threadIdx.x] = x0;
+  s1[threadIdx.x] = x1;
+  __syncthreads();
+  if (a.mode == 0) {
+    if (rl == 0) {
+      double t = 0.0;
+      for (int q = 0; q < rp; ++q) t += s0[q * C + c];
+      s0[c] = t;
+    }
+    __syncthreads();
+    const double mean = s0[c] / (r1 - r0);
+    double m2 = 0.0;
+    for (int r = r0 + rl; r < r1; r += rp) {
+      const double d = (double)gld(a.X + (long)r * C + c) - mean;
+      m2 += d * d;
+    }
+    __syncthreads();
+    s1[threadIdx.x] = m2;
+    __syncthreads();
+    if (rl == 0) {
+      double t = 0.0;
+      for (int q = 0; q < rp; ++q) t += s1[q * C + c];
+      a.part[((long)blockIdx.x * C + c) * 2] = s0[c];
+      a.part[((long)blockIdx.x * C + c) * 2 + 1] = t;
+    }
+    return;
+  }
+  if (rl == 0) {
+    double t0 = 0.0, t1 = 0.0;
+    for (int q = 0; q < rp; ++q) {
+      t0 += s0[q * C + c];
+      t1 += s1[q * C + c];
+    }
+    a.part[((long)blockIdx.x * C + c) * 2] = t0;
+    a.part[((long)blockIdx.x * C + c) * 2 + 1] = t1;
+  }
+}
+
+// Column sums of X [rows][C] per chunk of R rows (any C): part[chunk][c][0] (double).
+__global__ __launch_bounds__(256) void cgl_colsum_k(const float* X, int rows, int C, int R, double* part) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const int r0 = blockIdx.y * R, r1 = min(r0 + R, rows);
+  double t = 0.0;
+  for (int r = r0; r < r1; ++r) t += (double)gld(X + (long)r * C + c);
+  part[((long)blockIdx.y * C + c) * 2] = t;
+  part[((long)blockIdx.y * C + c) * 2 + 1] = 0.0;
+}
+
+// BatchNorm2d finalize, one thread per channel, groups in the reference's call order.
+//   fwd (mode 0): mean / biased var per group from the chunk partials (Chan), save_mean / invstd,
+//                 scale = invstd * gamma, shift = beta - mean * scale, running stats (momentum,
+//                 unbiased variance) group by group; eval: the same from running stats.
+//   bwd (mode 1): per group gm = S / n, k = D invstd^2 / n; dgamma = sum_g D invstd, dbeta = sum_g S.
+//   bias (mode 2): out = sum of every chunk.
+struct CglBnFinArgs {
+  const double* part; int C, groups, chunks_per_group, R, gr, mode, train;
+  const float* gamma; const float* beta;
+  double eps, momentum;
+  float* run_mean; float* run_var;
+  float* save_mean; float* save_invstd;     // [groups][C]
+  float* coef0; float* coef1;               // [groups][C]: fwd scale, shift; bwd gm, k
+  float* dgamma; float* dbeta;              // bwd, or bias out (mode 2: dgamma)
+};
+
+__global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int C = a.C;
+  if (c >= C) return;
+  if (a.mode == 2) {
+    double t = 0.0;
+    const int nch = a.groups * a.chunks_per_group;
+    for (int q = 0; q < nch; ++q) t += a.part[((long)q * C + c) * 2];
+    gst(a.dgamma + c, (float)t);
+    return;
+  }
+  const float w = a.gamma ? gld(a.gamma + c) : 1.f;
+  if (a.mode == 1) {
+    double dg = 0.0, db = 0.0;
+    for (int g = 0; g < a.groups; ++g) {
+      double S = 0.0, D = 0.0;
+      for (int q = 0; q < a.chunks_per_group; ++q) {
+        const long o = ((long)(g * a.chunks_per_group + q) * C + c) * 2;
+        S += a.part[o];
+        D += a.part[o + 1];
+      }
+      const float invstd = gld(a.save_invstd + (long)g * C + c);
+      gst(a.coef0 + (long)g * C + c, (float)(S / a.gr));
+      gst(a.coef1 + (long)g * C + c, (float)D * invstd * invstd / a.gr);
+      dg += D * (double)invstd;
+      db += S;
+    }
+    if (a.dgamma) gst(a.dgamma + c, (float)dg);
+    if (a.dbeta) gst(a.dbeta + c, (float)db);
+    return;
+  }
+  const float b = a.beta ? gld(a.beta + c) : 0.f;
+  if (!a.train) {
+    const double invstd = 1.0 / sqrt((double)gld(a.run_var + c) + a.eps);
+    const float sc = (float)invstd * w;
+    for (int g = 0; g < a.groups; ++g) {
+      gst(a.coef0 + (long)g * C + c, sc);
+      gst(a.coef1 + (long)g * C + c, b - gld(a.run_mean + c) * sc);
+    }
+    return;
+  }
+  float rm = a.run_mean ? gld(a.run_mean + c) : 0.f, rv = a.run_var ? gld(a.run_var + c) : 0.f;
+  for (int g = 0; g < a.groups; ++g) {
+    double s = 0.0;
+    for (int q = 0; q < a.chunks_per_group; ++q) s += a.part[((long)(g * a.chunks_per_group + q) * C + c) * 2];
+    const double n = a.gr;
+    const double mu = s / n;
+    double m2 = 0.0;
+    for (int q = 0; q < a.chunks_per_group; ++q) {
+      const long o = ((long)(g * a.chunks_per_group + q) * C + c) * 2;
+      const double cnt = a.R;
+      const double dd = a.part[o] / cnt - mu;
+      m2 += a.part[o + 1] + cnt * dd * dd;
+    }
+    const double invstd = 1.0 / sqrt(m2 / n + a.eps);
+    const float sc = (float)invstd * w;
+    gst(a.coef0 + (long)g * C + c, sc);
+    gst(a.coef1 + (long)g * C + c, b - (float)mu * sc);
+    if (a.save_mean) {
+      gst(a.save_mean + (long)g * C + c, (float)mu);
+      gst(a.save_invstd + (long)g * C + c, (float)invstd);
+    }
+    if (a.run_mean) {
+      const double mom = a.momentum;
+      rm = (float)(mom * mu + (1.0 - mom) * (double)rm);
+      rv = (float)(mom * (n > 1 ? m2 / (n - 1) : m2 / n) + (1.0 - mom) * (double)rv);
+    }
+  }
+  if (a.run_mean) {
+    gst(a.run_mean + c, rm);
+    gst(a.run_var + c, rv);
+  }
+}
+
+// Elementwise NHWC passes (float4 over channels; C % 4 == 0):
+//   mode 0  Y = act(X * coef0[g][c] + coef1[g][c])                               (BatchNorm2d apply)
+//   mode 1  dX = (g - coef0[g][c] - (X - mean[g][c]) coef1[g][c]) invstd[g][c] gamma[c],
+//           g = dY * leaky'(post)  (BatchNorm2d backward apply), then * drop * leaky'(post_out)
+//   mode 2  dX = dY * leaky'(post_out) * drop                      (Dropout2d + LeakyReLU backward)
+//   mode 3  dX = dY * (1 - Y^2)                                                  (Tanh backward)
+struct CglEltArgs {
+  int mode, rows, C, gr, hw, act;
+  float slope;
+  const float* X; const float* dY; const float* post;
+  const float* coef0; const float* coef1; const float* mean; const float* invstd; const float* gamma;
+  const float* post_out; const float* drop;
+  float* out;
+};
+
+__global__ __launch_bounds__(256) void cgl_eltwise(CglEltArgs a) {
+  const long n4 = (long)a.rows * a.C / 4;
+  const int C = a.C;
+  const float sl = a.slope;
+  for (long q = (long)blockIdx.x * 256 + threadIdx.x; q < n4; q += (long)gridDim.x * 256) {
+    const long e = q * 4;
+    const int r = (int)(e / C), c = (int)(e - (long)r * C);
+    const int g = r / a.gr;
+    const long gc = (long)g * C + c;
+    f32x4 o;
+    if (a.mode == 0) {
+      const f32x4 x = *(gcf4p)(a.X + e);
+      const f32x4 s = *(gcf4p)(a.coef0 + gc), h = *(gcf4p)(a.coef1 + gc);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v = fmaf(x[j], s[j], h[j]);
+        if (a.act == CGL_EPI_ACT_LEAKY) v = v > 0.f ? v : v * sl;
+        o[j] = v;
+      }
+    } else if (a.mode == 1) {
+      const f32x4 x = *(gcf4p)(a.X + e), dy = *(gcf4p)(a.dY + e);
+      const f32x4 gm = *(gcf4p)(a.coef0 + gc), kk = *(gcf4p)(a.coef1 + gc);
+      const f32x4 mu = *(gcf4p)(a.mean + gc), is = *(gcf4p)(a.invstd + gc), w = *(gcf4p)(a.gamma + c);
+      f32x4 p = dy;
+      if (a.post) p = *(gcf4p)(a.post + e);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float gg = a.post ? (p[j] > 0.f ? dy[j] : dy[j] * sl) : dy[j];
+        o[j] = (gg - gm[j] - (x[j] - mu[j]) * kk[j]) * is[j] * w[j];
+      }
+      if (a.post_out) {
+        const f32x4 po = *(gcf4p)(a.post_out + e);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = po[j] > 0.f ? o[j] : o[j] * sl;
+      }
+      if (a.drop) {
+        const f32x4 dm = *(gcf4p)(a.drop + (long)(r / a.hw) * C + c);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] *= dm[j];
+      }
+    } else if (a.mode == 2) {
+      const f32x4 dy = *(gcf4p)(a.dY + e);
+      o = dy;
+      if (a.post_out) {
+        const f32x4 po = *(gcf4p)(a.post_out + e);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = po[j] > 0.f ? o[j] : o[j] * sl;
+      }
+      if (a.drop) {
+        const f32x4 dm = *(gcf4p)(a.drop + (long)(r / a.hw) * C + c);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] *= dm[j];
+      }
+    } else {
+      const f32x4 dy = *(gcf4p)(a.dY + e), y = *(gcf4p)(a.X + e);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = dy[j] * (1.f - y[j] * y[j]);
+    }
+    *(gf4p)(a.out + e) = o;
+  }
+}
+
+// Scalar fallback of mode 2 / 3 for C % 4 != 0 (single-channel tensors: the generator image).
+__global__ __launch_bounds__(256) void cgl_eltwise1(CglEltArgs a) {
+  const long n = (long)a.rows * a.C;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int r = (int)(e / a.C), c = (int)(e - (long)r * a.C);
+    float o = gld(a.dY + e);
+    if (a.mode == 3) {
+      const float y = gld(a.X + e);
+      o *= 1.f - y * y;
+    } else {
+      if (a.post_out) o = gld(a.post_out + e) > 0.f ? o : o * a.slope;
+      if (a.drop) o *= gld(a.drop + (long)(r / a.hw) * a.C + c);
+    }
+    gst(a.out + e, o);
+  }
+}
+
+// Dropout2d(p) scale per (image, channel): 1/(1-p) with probability 1-p, else 0 (torch:
+// bernoulli_(1 - p) then div_(1 - p)).  Philox4x32-10 keyed by seed, counter = (index, ctr).
+__global__ __launch_bounds__(256) void cgl_dropout_mask_k(float* mask, long n, float keep, float scale,
+                                                          unsigned long long seed, unsigned long long ctr) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  uint32_t c[4] = {(uint32_t)i, (uint32_t)(i >> 32), (uint32_t)ctr, (uint32_t)(ctr >> 32) ^ 0x5bd1e995u};
+  cgl_philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const float u = (float)(c[0] >> 8) * (1.0f / 16777216.0f);   // [0, 1), 24 bits
+  gst(mask + i, u < keep ? scale : 0.f);
+}
+
+// NCHW <-> NHWC for one batch: X [n][c][hw] -> Y [n][hw][c] (to_nhwc) or back.  32x32 tiles in LDS.
+__global__ __launch_bounds__(256) void cgl_transpose_k(const float* X, float* Y, int rows, int cols) {
+  // per image: X [rows][cols] -> Y [cols][rows]
+  __shared__ float t[32][33];
+  const long base = (long)blockIdx.z * rows * cols;
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int k = ty; k < 32; k += 8) {
+    const int r = r0 + k, c = c0 + tx;
+    if (r < rows && c < cols) t[k][tx] = gld(X + base + (long)r * cols + c);
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int c = c0 + k, r = r0 + tx;
+    if (r < rows && c < cols) gst(Y + base + (long)c * rows + r, t[tx][k]);
+  }
+}
+
+// Adversarial loss of one forward call (mean over M rows) and its gradient, one workgroup,
+// fixed-order double reduction:
+//   0 CE2:  nn.CrossEntropyLoss on 2 logits (capgan.py:311)
+//   1 BCE:  nn.BCELoss on probabilities, log clamped at -100 (CGLGAN/2DMG/main.py:336)
+//   2 MSE:  nn.MSELoss (LSGAN objective for the model/lsgan.py discriminator; parity vs torch)
+//   3 BCE on logits through nn.Sigmoid (Sigmoid + BCELoss, for the model/lsgan.py logit)
+// grad = weight * d(mean loss)/dx, written when non-null.
+__global__ __launch_bounds__(256) void cgl_adv_loss_k(const float* x, int M, int C, int loss, int target,
+                                                      float weight, float* loss_out, float* grad) {
+  __shared__ double s[256];
+  double acc = 0.0;
+  const float invM = 1.f / (float)M;
+  for (int r = threadIdx.x; r < M; r += 256) {
+    float l, g0 = 0.f, g1 = 0.f;
+    if (loss == 0) {
+      const float z0 = gld(x + 2 * r), z1 = gld(x + 2 * r + 1);
+      const float mx = fmaxf(z0, z1);
+      const float lse = logf(expf(z0 - mx) + expf(z1 - mx));
+      const float o0 = z0 - mx - lse, o1 = z1 - mx - lse;
+      l = -(target == 0 ? o0 : o1);
+      const float w = weight * invM;
+      g0 = (target == 0 ? -w : 0.f) + expf(o0) * w;
+      g1 = (target == 1 ? -w : 0.f) + expf(o1) * w;
+    } else if (loss == 2) {
+      const float z = gld(x + r);
+      const float d = z - (float)target;
+      l = d * d;
+      g0 = weight * (2.f * d * invM);
+    } else {
+      const float z = gld(x + r);
+      const float pr = loss == 3 ? 1.f / (1.f + expf(-z)) : z;
+      const float y = (float)target;
+      const float lp = fmaxf(logf(pr), -100.f), l1p = fmaxf(logf(1.f - pr), -100.f);
+      l = -(y * lp + (1.f - y) * l1p);
+      const float gp = weight * invM * (pr - y) / fmaxf((1.f - pr) * pr, 1e-12f);
+      g0 = loss == 3 ? gp * (1.f - pr) * pr : gp;
+    }
+    acc += (double)l;
+    if (grad) {
+      if (loss == 0) {
+        gst(grad + 2 * r, g0);
+        gst(grad + 2 * r + 1, g1);
+      } else {
+        gst(grad + r, g0);
+      }
+    }
+  }
+  s[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int q = 0; q < 256; ++q) t += s[q];
+    if (loss_out) gst(loss_out, (float)(t / M));
+  }
+}
+
+// Multi-tensor Adam (torch 2.10 _single_tensor_adam op order, see cgl_adam in cgl_kernels.hip);
+// bias corrections are launch arguments, so no upload and no host sync.
+#define CGL_ADAM_MAXT 32
+struct CglAdamMulti {
+  int nt;
+  float* p[CGL_ADAM_MAXT];
+  const float* g[CGL_ADAM_MAXT];
+  float* m[CGL_ADAM_MAXT];
+  float* v[CGL_ADAM_MAXT];
+  long n[CGL_ADAM_MAXT];
+  int blk[CGL_ADAM_MAXT + 1];
+  float step_size, bc2sqrt, b2, w1, w2, eps;
+};
+
+__global__ __launch_bounds__(256) void cgl_adam_multi_k(CglAdamMulti a) {
+  const int b = blockIdx.x;
+  int t = 0;
+  for (int q = 1; q < a.nt; ++q)
+    if (b >= a.blk[q]) t = q;
+  const long i = (long)(b - a.blk[t]) * 256 + threadIdx.x;
+  if (i >= a.n[t]) return;
+  float* p = a.p[t];
+  float* m = a.m[t];
+  float* v = a.v[t];
+  const float g = gld(a.g[t] + i);
+  const float mm = cgl_lerp(gld(m + i), g, a.w1);
+  const float vv = __fadd_rn(__fmul_rn(gld(v + i), a.b2), __fmul_rn(__fmul_rn(a.w2, g), g));
+  gst(m + i, mm);
+  gst(v + i, vv);
+  const float denom = sqrtf(vv) / a.bc2sqrt + a.eps;
+  gst(p + i, gld(p + i) + (-a.step_size) * mm / denom);
+}
+
+// Real-batch gather of the worker's sampler: dst[r] = src[idx ? idx[r] : row0 + r] (rows of
+// row_floats floats; DataLoader(shuffle=True) over a device-resident shard, capgan.py:282,326-332).
+__global__ __launch_bounds__(256) void cgl_gather_rows_k(const float* src, const int* idx, long row0, int nrows,
+                                                         int rowf, float* dst) {
+  const long n = (long)nrows * rowf;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int r = (int)(e / rowf), c = (int)(e - (long)r * rowf);
+    const long sr = idx ? (long)gldi(idx + r) : row0 + r;
+    gst(dst + e, gld(src + sr * rowf + c));
+  }
+}
+
+// ==========================================================================================
+// Host side: tap tables, launch planning, C ABI.
+namespace {
+
+struct ConvGeom {
+  int n, h, w, cin, cout, stride, up, ks;   // ks: kernel size 3 (padding 1) or 1 (dense layer)
+  int hv, wv, ho, wo;        // virtual (upsampled) input dims, output dims
+};
+
+int conv_geom(int n, int h, int w, int cin, int cout, int stride, int up, ConvGeom& g, int ks = 3) {
+  if (n < 1 || h < 1 || w < 1 || cin < 1 || cout < 1 || (stride != 1 && stride != 2) || (up != 0 && up != 1))
+    return CGL_E_ARG;
+  if (up && stride != 1) return CGL_E_ARG;   // the reference only upsamples before stride-1 convs
+  if (ks != 3 && (ks != 1 || stride != 1 || up)) return CGL_E_ARG;
+  if (cin > 65536 || cout > 65536) return CGL_E_ARG;
+  g.n = n; g.h = h; g.w = w; g.cin = cin; g.cout = cout; g.stride = stride; g.up = up; g.ks = ks;
+  g.hv = h << up;
+  g.wv = w << up;
+  g.ho = (g.hv - 1) / stride + 1;
+  g.wo = (g.wv - 1) / stride + 1;
+  if ((long)n * g.ho * g.wo > (1L << 30) || (long)n * h * w > (1L << 30)) return CGL_E_ARG;
+  return 0;
+}
+
+// one spatial dimension of a tap table: offsets and the kernel taps combined into each
+struct Taps1 {
+  int T, off[4], mask[4];
+};
+
+// forward, output parity ph of a 2x upsample + 3x3 conv (phase form), on the low-res input
+Taps1 taps_up_fwd(int ph) {
+  Taps1 t;
+  t.T = 2;
+  if (ph == 0) { t.off[0] = -1; t.mask[0] = 1; t.off[1] = 0; t.mask[1] = 6; }
+  else { t.off[0] = 0; t.mask[0] = 3; t.off[1] = 1; t.mask[1] = 4; }
+  return t;
+}
+Taps1 taps_1x1() {
+  Taps1 t;
+  t.T = 1; t.off[0] = 0; t.mask[0] = 1;
+  return t;
+}
+Taps1 taps_direct(int sign) {   // sign +1: forward (offset kh - 1); -1: input gradient (offset 1 - kh)
+  Taps1 t;
+  t.T = 3;
+  for (int k = 0; k < 3; ++k) { t.off[k] = sign * (k - 1); t.mask[k] = 1 << k; }
+  return t;
+}
+// input gradient of a 2x upsample + 3x3 conv: dX[y] = sum_o dY[2y + o] Wc[o], o = -1..2
+Taps1 taps_up_bwd() {
+  Taps1 t;
+  t.T = 4;
+  const int off[4] = {-1, 0, 1, 2}, mask[4] = {4, 6, 3, 1};
+  for (int k = 0; k < 4; ++k) { t.off[k] = off[k]; t.mask[k] = mask[k]; }
+  return t;
+}
+// input gradient of a stride-2 3x3 conv, input parity p: dX[2y + p] = sum dY[y + o] W[kh]
+Taps1 taps_s2_bwd(int p) {
+  Taps1 t;
+  if (p == 0) { t.T = 1; t.off[0] = 0; t.mask[0] = 2; }
+  else { t.T = 2; t.off[0] = 0; t.mask[0] = 4; t.off[1] = 1; t.mask[1] = 1; }
+  return t;
+}
+
+// Fill the geometry of one problem (everything but tiles / pointers).
+void set_prob(CglConvProb& P, int nimg, int OH, int OW, int osy, int osx, int ooy, int oox, int YH, int YW, int ldy,
+              int isy, int isx, int IH, int IW, int ish, int XH, int XW, int Cin, int N, const Taps1& ty,
+              const Taps1& tx) {
+  std::memset(&P, 0, sizeof(P));
+  P.M = nimg * OH * OW;
+  P.N = N;
+  P.K = ty.T * tx.T * Cin;
+  P.Kp = (P.K + 15) & ~15;
+  P.OH = OH; P.OW = OW;
+  P.osy = osy; P.osx = osx; P.ooy = ooy; P.oox = oox;
+  P.YH = YH; P.YW = YW; P.ldy = ldy;
+  P.isy = isy; P.isx = isx;
+  P.IH = IH; P.IW = IW; P.ish = ish;
+  P.XH = XH; P.XW = XW; P.Cin = Cin;
+  P.Ty = ty.T; P.Tx = tx.T;
+  for (int k = 0; k < 4; ++k) {
+    P.dy[k] = k < ty.T ? ty.off[k] : 0;
+    P.ym[k] = k < ty.T ? ty.mask[k] : 0;
+    P.dx[k] = k < tx.T ? tx.off[k] : 0;
+    P.xm[k] = k < tx.T ? tx.mask[k] : 0;
+  }
+}
+
+// Problems of a forward conv (output = Y [n][ho][wo][cout], input X [n][h][w][cin]).
+int fwd_probs(const ConvGeom& g, CglConvProb* P) {
+  if (g.ks == 1) {
+    set_prob(P[0], g.n, g.h, g.w, 1, 1, 0, 0, g.h, g.w, g.cout, 1, 1, g.h, g.w, 0, g.h, g.w, g.cin, g.cout, taps_1x1(),
+             taps_1x1());
+    return 1;
+  }
+  if (g.up) {
+    int np = 0;
+    for (int ph = 0; ph < 2; ++ph)
+      for (int pw = 0; pw < 2; ++pw)
+        set_prob(P[np++], g.n, g.h, g.w, 2, 2, ph, pw, g.ho, g.wo, g.cout, 1, 1, g.h, g.w, 0, g.h, g.w, g.cin, g.cout,
+                 taps_up_fwd(ph), taps_up_fwd(pw));
+    return np;
+  }
+  set_prob(P[0], g.n, g.ho, g.wo, 1, 1, 0, 0, g.ho, g.wo, g.cout, g.stride, g.stride, g.h, g.w, 0, g.h, g.w, g.cin,
+           g.cout, taps_direct(1), taps_direct(1));
+  return 1;
+}
+
+// Problems of the input gradient (output = dX [n][h][w][cin], input dY [n][ho][wo][cout]).
+int bwd_probs(const ConvGeom& g, CglConvProb* P) {
+  if (g.ks == 1) {
+    set_prob(P[0], g.n, g.h, g.w, 1, 1, 0, 0, g.h, g.w, g.cin, 1, 1, g.h, g.w, 0, g.h, g.w, g.cout, g.cin, taps_1x1(),
+             taps_1x1());
+    return 1;
+  }
+  if (g.up) {
+    set_prob(P[0], g.n, g.h, g.w, 1, 1, 0, 0, g.h, g.w, g.cin, 2, 2, g.ho, g.wo, 0, g.ho, g.wo, g.cout, g.cin,
+             taps_up_bwd(), taps_up_bwd());
+    return 1;
+  }
+  if (g.stride == 1) {
+    set_prob(P[0], g.n, g.h, g.w, 1, 1, 0, 0, g.h, g.w, g.cin, 1, 1, g.ho, g.wo, 0, g.ho, g.wo, g.cout, g.cin,
+             taps_direct(-1), taps_direct(-1));
+    return 1;
+  }
+  int np = 0;
+  for (int py = 0; py < 2; ++py)
+    for (int px = 0; px < 2; ++px) {
+      const int OH = (g.h - py + 1) / 2, OW = (g.w - px + 1) / 2;
+      if (OH < 1 || OW < 1) continue;
+      set_prob(P[np++], g.n, OH, OW, 2, 2, py, px, g.h, g.w, g.cin, 1, 1, g.ho, g.wo, 0, g.ho, g.wo, g.cout, g.cin,
+               taps_s2_bwd(py), taps_s2_bwd(px));
+    }
+  return np;
+}
+
+inline int64_t al256(int64_t b) { return (b + 255) & ~int64_t(255); }
+
+// MFMA tiling of a forward / input-gradient launch: 2x2 blocks per wave; waves along N when N > 64.
+struct ConvTiling { int TM, TN, WM, WN; };
+ConvTiling conv_tiling(int N) {
+  if (N > 64) return {2, 2, 2, 2};      // 128 x 128
+  if (N > 32) return {2, 2, 4, 1};      // 256 x 64
+  return {2, 1, 4, 1};                  // 256 x 32
+}
+
+int64_t packed_floats(const CglConvProb* P, int np) {
+  int64_t t = 0;
+  for (int i = 0; i < np; ++i) t += al256((int64_t)P[i].N * P[i].Kp * 4) / 4;
+  return t;
+}
+
+struct WgradPlan {
+  CglConvProb P[CGL_CONV_MAXP];
+  int np;
+  ConvTiling t;
+  int64_t part_floats;
+};
+
+// Weight-gradient plan: per-wave result tiles of (32 TM) x (32 TN) (rows = cout, cols = im2col
+// columns); pixel splits so that all problems together give ~4096 wave units, each covering >= 32
+// chunks of 16 pixels, with the partial tiles capped at 8M floats (32 MB).
+WgradPlan wgrad_plan(const ConvGeom& g) {
+  WgradPlan w;
+  w.np = fwd_probs(g, w.P);
+  w.t = ConvTiling{g.cout > 32 ? 2 : 1, w.P[0].K > 32 ? 2 : 1, 1, 1};
+  int tiles_total = 0;
+  int64_t nk_total = 0;
+  for (int i = 0; i < w.np; ++i) {
+    CglConvProb& P = w.P[i];
+    P.tiles_m = (P.N + 32 * w.t.TM - 1) / (32 * w.t.TM);
+    P.tiles_n = (P.K + 32 * w.t.TN - 1) / (32 * w.t.TN);
+    tiles_total += P.tiles_m * P.tiles_n;
+    nk_total += (int64_t)P.N * P.Kp;
+  }
+  int s = std::max(1, 4096 / std::max(1, tiles_total));
+  s = (int)std::min<int64_t>(s, std::max<int64_t>(1, (8 << 20) / std::max<int64_t>(1, nk_total)));
+  w.part_floats = 0;
+  for (int i = 0; i < w.np; ++i) {
+    CglConvProb& P = w.P[i];
+    const int nchk = (P.M + 15) / 16;
+    P.splits = std::max(1, std::min(std::min(s, nchk / 32), 1024));
+    w.part_floats += al256((int64_t)P.splits * P.N * P.Kp * 4) / 4;
+  }
+  return w;
+}
+
+int64_t conv_ws_bytes(const ConvGeom& g) {
+  CglConvProb P[CGL_CONV_MAXP];
+  int64_t a = packed_floats(P, fwd_probs(g, P));
+  int64_t b = packed_floats(P, bwd_probs(g, P));
+  WgradPlan w = wgrad_plan(g);
+  const int64_t bias_part = al256((int64_t)((g.n * g.ho * g.wo + 255) / 256) * g.cout * 16) / 4 + 64;
+  return 4 * (std::max(a, b) + w.part_floats + 2 * bias_part) + 4096;
+}
+
+int launch_pack(const float* W, const ConvGeom& g, int transpose, CglConvProb* P, int np, float* dst,
+                hipStream_t s) {
+  CglPackArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.W = W;
+  a.cout = g.cout;
+  a.cin = g.cin;
+  a.transpose = transpose;
+  a.np = np;
+  a.ks = g.ks;
+  int64_t off = 0;
+  int64_t e = 0;
+  for (int i = 0; i < np; ++i) {
+    a.dst[i] = dst + off;
+    P[i].Wp = dst + off;
+    off += al256((int64_t)P[i].N * P[i].Kp * 4) / 4;
+    a.N[i] = P[i].N;
+    a.Kp[i] = P[i].Kp;
+    a.Cg[i] = P[i].Cin;
+    a.Tx[i] = P[i].Tx;
+    a.T[i] = P[i].Ty * P[i].Tx;
+    for (int k = 0; k < 4; ++k) { a.ym[i][k] = P[i].ym[k]; a.xm[i][k] = P[i].xm[k]; }
+    a.begin[i] = (int)e;
+    e += (int64_t)P[i].N * P[i].Kp;
+  }
+  a.begin[np] = (int)e;
+  hipLaunchKernelGGL(cgl_conv_pack, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float slope, const float* drop,
+                    hipStream_t s) {
+  const int N = P[0].N;
+  CglConvLaunch L;
+  std::memset(&L, 0, sizeof(L));
+  L.np = np;
+  L.bias = bias;
+  L.act = act;
+  L.slope = slope;
+  L.drop = drop;
+  if (N == 1) {
+    int wg = 0;
+    for (int i = 0; i < np; ++i) {
+      P[i].wg_begin = wg;
+      wg += (P[i].M + 255) / 256;
+      L.p[i] = P[i];
+    }
+    hipLaunchKernelGGL(cgl_conv_n1, dim3(wg), dim3(256), 0, s, L);
+    return (int)hipGetLastError();
+  }
+  const ConvTiling t = conv_tiling(N);
+  L.WM = t.WM;
+  L.WN = t.WN;
+  bool fast = true;
+  int wg = 0;
+  for (int i = 0; i < np; ++i) {
+    P[i].tiles_m = (P[i].M + 32 * t.TM * t.WM - 1) / (32 * t.TM * t.WM);
+    P[i].tiles_n = (P[i].N + 32 * t.TN * t.WN - 1) / (32 * t.TN * t.WN);
+    P[i].wg_begin = wg;
+    wg += P[i].tiles_m * P[i].tiles_n;
+    fast = fast && (P[i].Cin % 16 == 0);
+    L.p[i] = P[i];
+  }
+  if (t.TN == 2) {
+    if (fast) hipLaunchKernelGGL((cgl_conv_fwd<2, 2, true>), dim3(wg), dim3(256), 0, s, L);
+    else hipLaunchKernelGGL((cgl_conv_fwd<2, 2, false>), dim3(wg), dim3(256), 0, s, L);
+  } else {
+    if (fast) hipLaunchKernelGGL((cgl_conv_fwd<2, 1, true>), dim3(wg), dim3(256), 0, s, L);
+    else hipLaunchKernelGGL((cgl_conv_fwd<2, 1, false>), dim3(wg), dim3(256), 0, s, L);
+  }
+  return (int)hipGetLastError();
+}
+
+
+int chan_chunk(int64_t gr) {
+  int R = 256;
+  while (R > 1 && gr % R != 0) R >>= 1;
+  return R;
+}
+
+bool pow2_le256(int C) { return C >= 1 && C <= 256 && (C & (C - 1)) == 0; }
+
+// per-column sum of X [rows][C] into out[C] (bias gradient): chunk partials (double), then a
+// fixed-order sum over chunks (cgl_bn_finalize mode 2)
+int col_sum(const float* X, int64_t rows, int C, double* part, float* out, hipStream_t s) {
+  const int R = 256;
+  const int nch = (int)((rows + R - 1) / R);
+  hipLaunchKernelGGL(cgl_colsum_k, dim3((C + 255) / 256, nch), dim3(256), 0, s, X, (int)rows, C, R, part);
+  CglBnFinArgs f;
+  std::memset(&f, 0, sizeof(f));
+  f.part = part; f.C = C; f.groups = 1; f.chunks_per_group = nch; f.mode = 2; f.dgamma = out;
+  hipLaunchKernelGGL(cgl_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, s, f);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+namespace {
+
+int conv_fwd_impl(const ConvGeom& g, const float* X, const float* W, const float* bias, float* Y, int act, float slope,
+                  const float* drop, void* ws, int64_t wsb, hipStream_t s) {
+  if (!X || !W || !Y || !ws || act < 0 || act > 3 || !al16(ws)) return CGL_E_ARG;
+  if (wsb < conv_ws_bytes(g)) return CGL_E_SIZE;
+  if ((g.cin % 16 == 0 || g.cout == 1) && !al16(X)) return CGL_E_ARG;
+  if (g.cout == 1 && g.cin % 4 != 0) return CGL_E_ARG;
+  CglConvProb P[CGL_CONV_MAXP];
+  const int np = fwd_probs(g, P);
+  for (int i = 0; i < np; ++i) {
+    P[i].X = X;
+    P[i].Y = Y;
+  }
+  int rc;
+  if ((rc = launch_pack(W, g, 0, P, np, (float*)ws, s))) return rc;
+  return launch_conv_mma(P, np, bias, act, slope, drop, s);
+}
+
+int conv_bwd_data_impl(const ConvGeom& g, const float* dY, const float* W, float* dX, void* ws, int64_t wsb,
+                       hipStream_t s) {
+  if (!dY || !W || !dX || !ws || !al16(ws)) return CGL_E_ARG;
+  if (wsb < conv_ws_bytes(g)) return CGL_E_SIZE;
+  if ((g.cout % 16 == 0 || g.cin == 1) && !al16(dY)) return CGL_E_ARG;
+  if (g.cin == 1 && g.cout % 4 != 0) return CGL_E_ARG;
+  CglConvProb P[CGL_CONV_MAXP];
+  const int np = bwd_probs(g, P);
+  for (int i = 0; i < np; ++i) {
+    P[i].X = dY;
+    P[i].Y = dX;
+  }
+  int rc;
+  if ((rc = launch_pack(W, g, 1, P, np, (float*)ws, s))) return rc;
+  return launch_conv_mma(P, np, nullptr, CGL_EPI_ACT_NONE, 0.f, nullptr, s);
+}
+
+int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, float* dW, float* db, void* ws,
+                         int64_t wsb, hipStream_t s) {
+  if (!dY || !X || !dW || !ws || !al16(ws)) return CGL_E_ARG;
+  if (wsb < conv_ws_bytes(g)) return CGL_E_SIZE;
+  WgradPlan pl = wgrad_plan(g);
+  CglConvLaunch L;
+  std::memset(&L, 0, sizeof(L));
+  L.np = pl.np;
+  L.WM = 1;
+  L.WN = 1;
+  float* part = (float*)ws;
+  int wg = 0;
+  CglWgradReduceArgs r;
+  std::memset(&r, 0, sizeof(r));
+  r.dW = dW;
+  r.cout = g.cout;
+  r.cin = g.cin;
+  r.np = pl.np;
+  r.ks = g.ks;
+  for (int i = 0; i < pl.np; ++i) {
+    CglConvProb& P = pl.P[i];
+    P.X = X;
+    P.Y = (float*)dY;
+    P.part = part;
+    part += al256((int64_t)P.splits * P.N * P.Kp * 4) / 4;
+    P.wg_begin = wg;
+    wg += (P.tiles_m * P.tiles_n * P.splits + 3) / 4;   // 4 wave units per workgroup
+    L.p[i] = P;
+    r.part[i] = P.part;
+    r.Kp[i] = P.Kp;
+    r.splits[i] = P.splits;
+    r.Tx[i] = P.Tx;
+    r.Ty[i] = P.Ty;
+    for (int k = 0; k < 4; ++k) { r.ym[i][k] = P.ym[k]; r.xm[i][k] = P.xm[k]; }
+  }
+  if (pl.t.TM == 2 && pl.t.TN == 2) hipLaunchKernelGGL((cgl_conv_wgrad<2, 2>), dim3(wg), dim3(256), 0, s, L);
+  else if (pl.t.TN == 2) hipLaunchKernelGGL((cgl_conv_wgrad<1, 2>), dim3(wg), dim3(256), 0, s, L);
+  else if (pl.t.TM == 2) hipLaunchKernelGGL((cgl_conv_wgrad<2, 1>), dim3(wg), dim3(256), 0, s, L);
+  else hipLaunchKernelGGL((cgl_conv_wgrad<1, 1>), dim3(wg), dim3(256), 0, s, L);
+  int rc;
+  if ((rc = (int)hipGetLastError())) return rc;
+  const long nred = (long)g.cout * g.ks * g.ks * g.cin;
+  hipLaunchKernelGGL(cgl_conv_wgrad_reduce, dim3((unsigned)((nred + 255) / 256)), dim3(256), 0, s, r);
+  if ((rc = (int)hipGetLastError())) return rc;
+  if (db) {
+    double* bp = (double*)(((uintptr_t)part + 255) & ~(uintptr_t)255);
+    if ((rc = col_sum(dY, (int64_t)g.n * g.ho * g.wo, g.cout, bp, db, s))) return rc;
+  }
+  return 0;
+}
+
+}  // namespace
+
+// ==========================================================================================
+extern "C" {
+
+int64_t cgl_conv3x3_workspace_bytes(int n, int h, int w, int cin, int cout, int stride, int up) {
+  ConvGeom g;
+  const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
+  if (rc) return rc;
+  return conv_ws_bytes(g);
+}
+
+int cgl_conv3x3_fwd(const float* X, const float* W, const float* bias, float* Y, int n, int h, int w, int cin,
+                    int cout, int stride, int up, int act, float slope, const float* drop, void* ws, int64_t wsb,
+                    void* stream) {
+  ConvGeom g;
+  const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
+  if (rc) return rc;
+  return conv_fwd_impl(g, X, W, bias, Y, act, slope, drop, ws, wsb, (hipStream_t)stream);
+}
+
+int cgl_conv3x3_bwd_data(const float* dY, const float* W, float* dX, int n, int h, int w, int cin, int cout,
+                         int stride, int up, void* ws, int64_t wsb, void* stream) {
+  ConvGeom g;
+  const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
+  if (rc) return rc;
+  return conv_bwd_data_impl(g, dY, W, dX, ws, wsb, (hipStream_t)stream);
+}
+
+int cgl_conv3x3_bwd_weight(const float* dY, const float* X, float* dW, float* db, int n, int h, int w, int cin,
+                           int cout, int stride, int up, void* ws, int64_t wsb, void* stream) {
+  ConvGeom g;
+  const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
+  if (rc) return rc;
+  return conv_bwd_weight_impl(g, dY, X, dW, db, ws, wsb, (hipStream_t)stream);
+}
+
+int64_t cgl_dense_workspace_bytes(int M, int K, int N) {
+  ConvGeom g;
+  const int rc = conv_geom(M, 1, 1, K, N, 1, 0, g, 1);
+  if (rc) return rc;
+  return conv_ws_bytes(g);
+}
+
+int cgl_dense_fwd(const float* X, const float* W, const float* b, float* Y, int M, int K, int N, int act, float slope,
+                  void* ws, int64_t wsb, void* stream) {
+  ConvGeom g;
+  const int rc = conv_geom(M, 1, 1, K, N, 1, 0, g, 1);
+  if (rc) return rc;
+  return conv_fwd_impl(g, X, W, b, Y, act, slope, nullptr, ws, wsb, (hipStream_t)stream);
+}
+
+int cgl_dense_bwd_data(const float* dY, const float* W, float* dX, int M, int K, int N, void* ws, int64_t wsb,
+                       void* stream) {
+  ConvGeom g;
+  const int rc = conv_geom(M, 1, 1, K, N, 1, 0, g, 1);
+  if (rc) return rc;
+  return conv_bwd_data_impl(g, dY, W, dX, ws, wsb, (hipStream_t)stream);
+}
+
+int cgl_dense_bwd_weight(const float* dY, const float* X, float* dW, float* db, int M, int K, int N, void* ws,
+                         int64_t wsb, void* stream) {
+  ConvGeom g;
+  const int rc = conv_geom(M, 1, 1, K, N, 1, 0, g, 1);
+  if (rc) return rc;
+  return conv_bwd_weight_impl(g, dY, X, dW, db, ws, wsb, (hipStream_t)stream);
+}
+
+int64_t cgl_bn2d_workspace_bytes(int n, int hw, int C, int groups) {
+  if (n < 1 || hw < 1 || C < 1 || groups < 1 || n % groups) return CGL_E_ARG;
+  const int64_t gr = (int64_t)(n / groups) * hw;
+  const int R = chan_chunk(gr);
+  const int64_t nch = (int64_t)n * hw / R;
+  return al256(nch * C * 16) + 4 * al256((int64_t)groups * C * 4) + 256;
+}
+
+int cgl_bn2d_fwd(const float* X, int n, int hw, int C, int groups, const float* gamma, const float* beta, double eps,
+                 double momentum, float* running_mean, float* running_var, int train, int act, float slope, float* Y,
+                 float* save_mean, float* save_invstd, void* ws, int64_t wsb, void* stream) {
+  if (!X || !Y || !gamma || !beta || !ws || !al16(ws) || !al16(X) || !al16(Y)) return CGL_E_ARG;
+  if (n < 1 || hw < 1 || C % 4 != 0 || !pow2_le256(C) || groups < 1 || n % groups || (act != 0 && act != 1))
+    return CGL_E_ARG;
+  if ((running_mean == nullptr) != (running_var == nullptr)) return CGL_E_ARG;
+  if ((save_mean == nullptr) != (save_invstd == nullptr)) return CGL_E_ARG;
+  if (!train && !running_mean) return CGL_E_ARG;
+  const int64_t gr = (int64_t)(n / groups) * hw;
+  if (train && gr < 2) return CGL_E_ARG;   // torch: "Expected more than 1 value per channel when training"
+  if (wsb < cgl_bn2d_workspace_bytes(n, hw, C, groups)) return CGL_E_SIZE;
+  hipStream_t s = (hipStream_t)stream;
+  const int R = chan_chunk(gr);
+  const int64_t rows = (int64_t)n * hw;
+  const int nch = (int)(rows / R);
+  double* part = (double*)ws;
+  float* coef = (float*)((char*)ws + al256((int64_t)nch * C * 16));
+  float* c0 = coef;
+  float* c1 = coef + al256((int64_t)groups * C * 4) / 4;
+  if (train) {
+    CglChanArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.X = X; a.rows = (int)rows; a.C = C; a.R = R; a.mode = 0; a.gr = (int)gr; a.part = part;
+    hipLaunchKernelGGL(cgl_chan_reduce, dim3(nch), dim3(256), 0, s, a);
+  }
+  CglBnFinArgs f;
+  std::memset(&f, 0, sizeof(f));
+  f.part = part; f.C = C; f.groups = groups; f.chunks_per_group = (int)(gr / R); f.R = R; f.gr = (int)gr;
+  f.mode = 0; f.train = train; f.gamma = gamma; f.beta = beta; f.eps = eps; f.momentum = momentum;
+  f.run_mean = running_mean; f.run_var = running_var; f.save_mean = save_mean; f.save_invstd = save_invstd;
+  f.coef0 = c0; f.coef1 = c1;
+  hipLaunchKernelGGL(cgl_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, s, f);
+  CglEltArgs e;
+  std::memset(&e, 0, sizeof(e));
+  e.mode = 0; e.rows = (int)rows; e.C = C; e.gr = (int)gr; e.hw = hw; e.act = act; e.slope = slope;
+  e.X = X; e.coef0 = c0; e.coef1 = c1; e.out = Y;
+  const long n4 = rows * C / 4;
+  hipLaunchKernelGGL(cgl_eltwise, dim3((unsigned)std::min<long>((n4 + 255) / 256, 8192)), dim3(256), 0, s, e);
+  return (int)hipGetLastError();
+}
+
+int cgl_bn2d_bwd(const float* dY, const float* post, const float* X, int n, int hw, int C, int groups,
+                 const float* save_mean, const float* save_invstd, const float* gamma, float slope,
+                 const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta, void* ws,
+                 int64_t wsb, void* stream) {
+  if (!dY || !X || !save_mean || !save_invstd || !gamma || !dX || !ws || !al16(ws)) return CGL_E_ARG;
+  if (!al16(dY) || !al16(X) || !al16(dX) || (post && !al16(post)) || (post_out && !al16(post_out))) return CGL_E_ARG;
+  if (!al16(save_mean) || !al16(save_invstd) || !al16(gamma) || (drop && !al16(drop))) return CGL_E_ARG;
+  if (n < 1 || hw < 1 || C % 4 != 0 || !pow2_le256(C) || groups < 1 || n % groups) return CGL_E_ARG;
+  if (wsb < cgl_bn2d_workspace_bytes(n, hw, C, groups)) return CGL_E_SIZE;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t gr = (int64_t)(n / groups) * hw;
+  const int R = chan_chunk(gr);
+  const int64_t rows = (int64_t)n * hw;
+  const int nch = (int)(rows / R);
+  double* part = (double*)ws;
+  float* coef = (float*)((char*)ws + al256((int64_t)nch * C * 16));
+  float* c0 = coef;
+  float* c1 = coef + al256((int64_t)groups * C * 4) / 4;
+  CglChanArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.X = X; a.rows = (int)rows; a.C = C; a.R = R; a.mode = 1; a.gr = (int)gr; a.part = part;
+  a.dY = dY; a.post = post; a.slope = slope; a.mean = save_mean;
+  hipLaunchKernelGGL(cgl_chan_reduce, dim3(nch), dim3(256), 0, s, a);
+  CglBnFinArgs f;
+  std::memset(&f, 0, sizeof(f));
+  f.part = part; f.C = C; f.groups = groups; f.chunks_per_group = (int)(gr / R); f.R = R; f.gr = (int)gr;
+  f.mode = 1; f.gamma = gamma; f.save_invstd = const_cast<float*>(save_invstd); f.coef0 = c0; f.coef1 = c1;
+  f.dgamma = dgamma; f.dbeta = dbeta;
+  hipLaunchKernelGGL(cgl_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, s, f);
+  CglEltArgs e;
+  std::memset(&e, 0, sizeof(e));
+  e.mode = 1; e.rows = (int)rows; e.C = C; e.gr = (int)gr; e.hw = hw; e.slope = slope;
+  e.X = X; e.dY = dY; e.post = post; e.coef0 = c0; e.coef1 = c1; e.mean = save_mean; e.invstd = save_invstd;
+  e.gamma = gamma; e.post_out = post_out; e.drop = drop; e.out = dX;
+  const long n4 = rows * C / 4;
+  hipLaunchKernelGGL(cgl_eltwise, dim3((unsigned)std::min<long>((n4 + 255) / 256, 8192)), dim3(256), 0, s, e);
+  return (int)hipGetLastError();
+}
+
+int cgl_act_drop_bwd(const float* dY, const float* post, const float* drop, int n, int hw, int C, float slope,
+                     int tanh_y, float* dX, void* stream) {
+  if (!dY || !dX || n < 1 || hw < 1 || C < 1) return CGL_E_ARG;
+  if (tanh_y && !post) return CGL_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  CglEltArgs e;
+  std::memset(&e, 0, sizeof(e));
+  e.mode = tanh_y ? 3 : 2;
+  e.rows = n * hw; e.C = C; e.gr = n * hw; e.hw = hw; e.slope = slope;
+  e.dY = dY; e.out = dX;
+  if (tanh_y) e.X = post;
+  else e.post_out = post;
+  e.drop = drop;
+  const long tot = (long)n * hw * C;
+  const bool v4 = C % 4 == 0 && al16(dY) && al16(dX) && (!post || al16(post)) && (!drop || al16(drop));
+  if (v4)
+    hipLaunchKernelGGL(cgl_eltwise, dim3((unsigned)std::min<long>((tot / 4 + 255) / 256, 8192)), dim3(256), 0, s, e);
+  else
+    hipLaunchKernelGGL(cgl_eltwise1, dim3((unsigned)std::min<long>((tot + 255) / 256, 8192)), dim3(256), 0, s, e);
+  return (int)hipGetLastError();
+}
+
+int cgl_dropout2d_mask(float* mask, int n, int C, double p, unsigned long long seed, unsigned long long counter,
+                       void* stream) {
+  if (!mask || n < 1 || C < 1 || !(p >= 0.0 && p < 1.0)) return CGL_E_ARG;
+  const long tot = (long)n * C;
+  const float keep = (float)(1.0 - p);
+  const float scale = 1.0f / keep;
+  hipLaunchKernelGGL(cgl_dropout_mask_k, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream, mask,
+                     tot, keep, scale, seed, counter);
+  return (int)hipGetLastError();
+}
+
+int cgl_nchw_to_nhwc(const float* X, float* Y, int n, int c, int hw, void* stream) {
+  if (!X || !Y || n < 1 || c < 1 || hw < 1) return CGL_E_ARG;
+  hipLaunchKernelGGL(cgl_transpose_k, dim3((hw + 31) / 32, (c + 31) / 32, n), dim3(256), 0, (hipStream_t)stream, X, Y,
+                     c, hw);
+  return (int)hipGetLastError();
+}
+
+int cgl_nhwc_to_nchw(const float* X, float* Y, int n, int c, int hw, void* stream) {
+  if (!X || !Y || n < 1 || c < 1 || hw < 1) return CGL_E_ARG;
+  hipLaunchKernelGGL(cgl_transpose_k, dim3((c + 31) / 32, (hw + 31) / 32, n), dim3(256), 0, (hipStream_t)stream, X, Y,
+                     hw, c);
+  return (int)hipGetLastError();
+}
+
+int cgl_adv_loss(const float* x, int M, int C, int loss, int target, double weight, float* loss_out, float* grad,
+                 void* stream) {
+  if (!x || M < 1 || loss < 0 || loss > 3 || (target != 0 && target != 1)) return CGL_E_ARG;
+  if ((loss == 0) != (C == 2) || (loss != 0 && C != 1)) return CGL_E_ARG;
+  hipLaunchKernelGGL(cgl_adv_loss_k, dim3(1), dim3(256), 0, (hipStream_t)stream, x, M, C, loss, target,
+                     (float)weight, loss_out, grad);
+  return (int)hipGetLastError();
+}
+
+int cgl_gather_rows(const float* src, const int* idx, int64_t row0, int nrows, int row_floats, float* dst,
+                    void* stream) {
+  if (!src || !dst || nrows < 0 || row_floats < 1 || row0 < 0) return CGL_E_ARG;
+  if (nrows == 0) return 0;
+  const long n = (long)nrows * row_floats;
+  hipLaunchKernelGGL(cgl_gather_rows_k, dim3((unsigned)std::min<long>((n + 255) / 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, src, idx, (long)row0, nrows, row_floats, dst);
+  return (int)hipGetLastError();
+}
+
+int cgl_adam_multi(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
+                   const int64_t* n, int step, double lr, double beta1, double beta2, double eps, void* stream) {
+  if (nt < 1 || nt > CGL_ADAM_MAXT || !p || !g || !m || !v || !n || step < 1) return CGL_E_ARG;
+  CglAdamMulti a;
+  std::memset(&a, 0, sizeof(a));
+  a.nt = nt;
+  int blk = 0;
+  for (int i = 0; i < nt; ++i) {
+    if (!p[i] || !g[i] || !m[i] || !v[i] || n[i] < 0) return CGL_E_ARG;
+    a.p[i] = p[i]; a.g[i] = g[i]; a.m[i] = m[i]; a.v[i] = v[i]; a.n[i] = (long)n[i];
+    a.blk[i] = blk;
+    blk += (int)((n[i] + 255) / 256);
+  }
+  a.blk[nt] = blk;
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  a.step_size = (float)(lr / bc1);
+  a.bc2sqrt = (float)std::pow(bc2, 0.5);
+  a.b2 = (float)beta2;
+  a.w1 = (float)(1.0 - beta1);
+  a.w2 = (float)(1.0 - beta2);
+  a.eps = (float)eps;
+  if (blk == 0) return 0;
+  hipLaunchKernelGGL(cgl_adam_multi_k, dim3(blk), dim3(256), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

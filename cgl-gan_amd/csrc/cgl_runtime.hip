@@ -1420,3 +1420,6 @@ int cgl_normal_fill(float* out, int64_t n, unsigned long long seed, int round, i
 }
 
 }  // extern "C"
+
+// conv GAN path (model/lsgan.py): implicit-GEMM convolutions, BatchNorm2d, losses, Adam
+#include "cgl_conv.hip"

@@ -179,6 +179,83 @@ int cgl_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int s
 int cgl_normal_fill(float* out, int64_t n, unsigned long long seed, int round, int stream_id, void* stream);
 int64_t cgl_op_workspace_bytes(void);
 
+/* ---------------- conv GAN ops (model/lsgan.py) ----------------
+ * Activations are NHWC (torch channels_last memory of the reference's NCHW tensors); weights are
+ * the reference's nn.Conv2d layout [cout][cin][3][3].  No op allocates or synchronises: every
+ * launch is stream-ordered (hipGraph-capturable); scratch comes from the caller's workspace. */
+
+/* Workspace bytes for the three conv3x3 ops of one geometry (negative on a bad geometry). */
+int64_t cgl_conv3x3_workspace_bytes(int n, int h, int w, int cin, int cout, int stride, int up);
+/* Y[n][ho][wo][cout] = drop(act(conv3x3(up2(X)) + bias)): nn.Conv2d(cin, cout, 3, stride, 1)
+ * (model/lsgan.py:12,16,19,78), optionally preceded by nn.Upsample(scale_factor=2) (up = 1,
+ * stride 1; model/lsgan.py:11,15) and followed by the activation (act: 0 none, 1 LeakyReLU(slope),
+ * 2 Tanh, 3 Sigmoid; :14,18,20,78) and the nn.Dropout2d scale drop[n][cout] (may be null; :78).
+ * X [n][h][w][cin] is the stored (pre-upsample) input; ho = ((h << up) - 1) / stride + 1. */
+int cgl_conv3x3_fwd(const float* X, const float* W, const float* bias, float* Y, int n, int h, int w, int cin,
+                    int cout, int stride, int up, int act, float slope, const float* drop, void* workspace,
+                    int64_t ws_bytes, void* stream);
+/* dX[n][h][w][cin] = gradient of the above w.r.t. X (through the upsample when up = 1), from the
+ * gradient dY[n][ho][wo][cout] of the convolution output (autograd of model/lsgan.py's convs). */
+int cgl_conv3x3_bwd_data(const float* dY, const float* W, float* dX, int n, int h, int w, int cin, int cout,
+                         int stride, int up, void* workspace, int64_t ws_bytes, void* stream);
+/* dW[cout][cin][3][3] and db[cout] (may be null) of the convolution from dY and its input X. */
+int cgl_conv3x3_bwd_weight(const float* dY, const float* X, float* dW, float* db, int n, int h, int w, int cin,
+                           int cout, int stride, int up, void* workspace, int64_t ws_bytes, void* stream);
+
+/* Stream-ordered dense layer on the same implicit-GEMM kernels (a 1x1 convolution of M "pixels"):
+ * Y[M][N] = act(X[M][K] W[N][K]^T + b) -- nn.Linear of model/lsgan.py:8 (l1, 100 -> 8192) and
+ * :92 (adv_layer, 512 -> 1) -- its input gradient dX = dY W and weight gradient dW = dY^T X,
+ * db = column sums of dY.  Unlike cgl_linear_* these never synchronise the stream. */
+int64_t cgl_dense_workspace_bytes(int M, int K, int N);
+int cgl_dense_fwd(const float* X, const float* W, const float* b, float* Y, int M, int K, int N, int act, float slope,
+                  void* workspace, int64_t ws_bytes, void* stream);
+int cgl_dense_bwd_data(const float* dY, const float* W, float* dX, int M, int K, int N, void* workspace,
+                       int64_t ws_bytes, void* stream);
+int cgl_dense_bwd_weight(const float* dY, const float* X, float* dW, float* db, int M, int K, int N, void* workspace,
+                         int64_t ws_bytes, void* stream);
+
+/* nn.BatchNorm2d(C, eps, momentum) [+ LeakyReLU(slope) when act == 1] on NHWC X[n][hw][C]
+ * (model/lsgan.py:13,17,80).  `groups` independent forward calls are stacked along n (statistics
+ * per group, running stats updated group by group in call order); save_mean / save_invstd are
+ * [groups][C] (may be null).  train == 0: running statistics (eval). */
+int64_t cgl_bn2d_workspace_bytes(int n, int hw, int C, int groups);
+int cgl_bn2d_fwd(const float* X, int n, int hw, int C, int groups, const float* gamma, const float* beta, double eps,
+                 double momentum, float* running_mean, float* running_var, int train, int act, float slope, float* Y,
+                 float* save_mean, float* save_invstd, void* workspace, int64_t ws_bytes, void* stream);
+/* Train-mode backward: dY is the gradient of the BatchNorm output, or of LeakyReLU(output) when
+ * `post` (that activation's output) is given.  The result is optionally multiplied by
+ * LeakyReLU'(post_out) and the Dropout2d scale drop[n][C] (the Conv -> LeakyReLU -> Dropout2d ->
+ * BatchNorm2d block of model/lsgan.py:78-80, backward in one pass).  dgamma / dbeta may be null. */
+int cgl_bn2d_bwd(const float* dY, const float* post, const float* X, int n, int hw, int C, int groups,
+                 const float* save_mean, const float* save_invstd, const float* gamma, float slope,
+                 const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta, void* workspace,
+                 int64_t ws_bytes, void* stream);
+/* dX = dY * LeakyReLU'(post) * drop[n][C] (Dropout2d + LeakyReLU backward; post / drop may be
+ * null), or with tanh_y != 0: dX = dY * (1 - post^2) (Tanh backward, post = the Tanh output). */
+int cgl_act_drop_bwd(const float* dY, const float* post, const float* drop, int n, int hw, int C, float slope,
+                     int tanh_y, float* dX, void* stream);
+/* nn.Dropout2d(p) scales per (image, channel): 1/(1-p) with probability 1-p, else 0
+ * (Philox4x32-10, counter-based: (seed, counter) selects the stream). */
+int cgl_dropout2d_mask(float* mask, int n, int C, double p, unsigned long long seed, unsigned long long counter,
+                       void* stream);
+/* Layout changes of model/lsgan.py:25 (view(B,128,8,8) of the Linear output) and :96 (view(B,-1)). */
+int cgl_nchw_to_nhwc(const float* X, float* Y, int n, int c, int hw, void* stream);
+int cgl_nhwc_to_nchw(const float* X, float* Y, int n, int c, int hw, void* stream);
+/* Mean adversarial loss of one forward call and weight * its gradient (grad may be null):
+ * loss 0 CrossEntropy on 2 logits (capgan.py:311), 1 BCELoss on probabilities
+ * (CGLGAN/2DMG/main.py:336), 2 MSELoss (LSGAN objective of model/lsgan.py's D), 3 Sigmoid + BCELoss
+ * on logits.  target 0 (fake) or 1 (valid); loss_out: device scalar. */
+int cgl_adv_loss(const float* x, int M, int C, int loss, int target, double weight, float* loss_out, float* grad,
+                 void* stream);
+/* dst[r] = src[idx ? idx[r] : row0 + r] for r < nrows (rows of row_floats floats; idx: device int32):
+ * the worker's real-batch sampler over a device-resident shard (capgan.py:282,326-332). */
+int cgl_gather_rows(const float* src, const int* idx, int64_t row0, int nrows, int row_floats, float* dst,
+                    void* stream);
+/* optim.Adam step `step` over nt (<= 32) tensors (torch _single_tensor_adam op order), host pointer
+ * arrays; no host synchronisation. */
+int cgl_adam_multi(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
+                   const int64_t* n, int step, double lr, double beta1, double beta2, double eps, void* stream);
+
 /* Library identification: "<version> gfx950" */
 const char* cgl_version(void);
 

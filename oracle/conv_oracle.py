@@ -1,0 +1,172 @@
+"""torch-CPU restatement of the model/lsgan.py conv GAN and its worker round (TEST INFRASTRUCTURE ONLY).
+
+See ``oracle/__init__.py``: only tests, ``__graft_entry__.smoke`` and bench.py's ``cpu_baseline`` leg
+use this module; the product path never imports it.
+
+Models (reference model/lsgan.py, paths relative to the reference root):
+  * ``Generator``      :3-27  -- l1 = Linear(100, 128*8*8), view(B,128,8,8) (:25), conv_blocks =
+    Upsample(2) Conv(128,128) BN2d(128,.8) LReLU(.2) Upsample(2) Conv(128,64) BN2d(64,.8) LReLU
+    Conv(64,1) Tanh (:10-21)
+  * ``Discriminator``  :73-99 -- 4 x [Conv(k3,s2,p1) LReLU(.2) Dropout2d(.25) (BN2d(.8) but block 1)]
+    (:77-88), view(B,-1) (:96), adv_layer = Linear(128*2*2, 1) (:92,97)
+  * ``MixGenerator``   :37-70 -- the intended trunk/heads split (the reference's forward cannot run:
+    ``self.img_shape`` is never set, :68) -- parity unpinned by the reference.
+
+The functional forward takes the Dropout2d scales explicitly (``masks``: one [B, C] tensor per
+Dropout2d, value 0 or 1/(1-p)); ``draw_masks`` reproduces torch's own draw (``_dropout_impl``:
+``empty(n, c, 1, 1).bernoulli_(1 - p).div_(1 - p)``) so that a reference module run under the same
+seed and this oracle agree bit for bit (tests/golden/make_golden.py pins it).
+
+The worker round restates capgan.py:211-262 (Server.train) + :316-349 (Worker.train) with these
+models.  The reference never trains model/lsgan.py; the losses offered are the
+LSGAN objective (MSELoss; north_star "LSGAN/BCE adversarial loss") and Sigmoid + BCELoss on the
+logit -- both parity-unpinned by the reference, pinned against torch's own loss modules.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import torch
+import torch.nn.functional as F
+
+from .gan_oracle import ADAM_EPS, B1, B2, BN_EPS, BN_MOMENTUM, LAMBDA_LR, LAMBDA_REG, LR, SLOPE, Adam
+
+DROP_P = 0.25   # nn.Dropout2d(0.25) model/lsgan.py:78
+
+# (key, kind, shape) in the reference's construction (= state-dict) order
+G_SPEC = [
+    ("l1.0", "linear", (128 * 8 * 8, 100)),
+    ("conv_blocks.1", "conv", (128, 128)),
+    ("conv_blocks.2", "bn", 128),
+    ("conv_blocks.5", "conv", (64, 128)),
+    ("conv_blocks.6", "bn", 64),
+    ("conv_blocks.8", "conv", (1, 64)),
+]
+D_SPEC = [
+    ("model.0", "conv", (16, 1)),
+    ("model.3", "conv", (32, 16)),
+    ("model.6", "bn", 32),
+    ("model.7", "conv", (64, 32)),
+    ("model.10", "bn", 64),
+    ("model.11", "conv", (128, 64)),
+    ("model.14", "bn", 128),
+    ("adv_layer", "linear", (1, 128 * 2 * 2)),
+]
+D_CHANNELS = [16, 32, 64, 128]
+
+
+def init_params(spec, generator=None):
+    """nn.Linear / nn.Conv2d reset_parameters (kaiming_uniform_(a=sqrt(5)), bias U(+-1/sqrt(fan_in)))
+    and BatchNorm (1, 0; running 0 / 1), drawn in construction order from the torch CPU RNG, so that
+    ``torch.manual_seed(s); init_params(G_SPEC)`` equals ``torch.manual_seed(s); Generator(ims)``."""
+    params, buffers = OrderedDict(), OrderedDict()
+    for key, kind, shp in spec:
+        if kind in ("linear", "conv"):
+            w = torch.empty(*shp) if kind == "linear" else torch.empty(shp[0], shp[1], 3, 3)
+            b = torch.empty(shp[0])
+            torch.nn.init.kaiming_uniform_(w, a=math.sqrt(5), generator=generator)
+            fan_in = w[0].numel()
+            bound = 1.0 / math.sqrt(fan_in)
+            torch.nn.init.uniform_(b, -bound, bound, generator=generator)
+            params[key + ".weight"], params[key + ".bias"] = w, b
+        else:
+            params[key + ".weight"], params[key + ".bias"] = torch.ones(shp), torch.zeros(shp)
+            buffers[key + ".running_mean"] = torch.zeros(shp)
+            buffers[key + ".running_var"] = torch.ones(shp)
+            buffers[key + ".num_batches_tracked"] = torch.tensor(0, dtype=torch.long)
+    return params, buffers
+
+
+def draw_masks(n, channels=D_CHANNELS, p=DROP_P):
+    """torch's Dropout2d noise for one D forward call, in call order (one bernoulli per block)."""
+    return [torch.empty(n, c, 1, 1).bernoulli_(1 - p).div_(1 - p).view(n, c) for c in channels]
+
+
+def _bn(x, P, Bf, key, train):
+    if train:
+        Bf[key + ".num_batches_tracked"].add_(1)
+    return F.batch_norm(x, Bf[key + ".running_mean"], Bf[key + ".running_var"], P[key + ".weight"],
+                        P[key + ".bias"], train, BN_MOMENTUM, BN_EPS)
+
+
+def g_forward(P, Bf, z, train=True):
+    """Generator.forward model/lsgan.py:23-27 (+ conv_blocks :10-21)."""
+    out = F.linear(z, P["l1.0.weight"], P["l1.0.bias"])
+    x = out.view(out.shape[0], 128, 8, 8)
+    x = F.interpolate(x, scale_factor=2, mode="nearest")
+    x = F.conv2d(x, P["conv_blocks.1.weight"], P["conv_blocks.1.bias"], 1, 1)
+    x = F.leaky_relu(_bn(x, P, Bf, "conv_blocks.2", train), SLOPE)
+    x = F.interpolate(x, scale_factor=2, mode="nearest")
+    x = F.conv2d(x, P["conv_blocks.5.weight"], P["conv_blocks.5.bias"], 1, 1)
+    x = F.leaky_relu(_bn(x, P, Bf, "conv_blocks.6", train), SLOPE)
+    x = F.conv2d(x, P["conv_blocks.8.weight"], P["conv_blocks.8.bias"], 1, 1)
+    return torch.tanh(x)
+
+
+def d_forward(P, Bf, img, masks=None, train=True):
+    """Discriminator.forward model/lsgan.py:94-99; ``masks`` = the 4 Dropout2d scales [B, C]
+    (None in eval mode: Dropout2d is the identity)."""
+    x = img
+    convs = ["model.0", "model.3", "model.7", "model.11"]
+    bns = [None, "model.6", "model.10", "model.14"]
+    for i, (ck, bk) in enumerate(zip(convs, bns)):
+        x = F.conv2d(x, P[ck + ".weight"], P[ck + ".bias"], 2, 1)
+        x = F.leaky_relu(x, SLOPE)
+        if train:
+            x = x * masks[i].to(x.dtype)[:, :, None, None]
+        if bk is not None:
+            x = _bn(x, P, Bf, bk, train)
+    out = x.reshape(x.shape[0], -1)
+    return F.linear(out, P["adv_layer.weight"], P["adv_layer.bias"])
+
+
+def adv_loss(v, target, kind):
+    """LSGAN MSELoss (kind "mse") or nn.Sigmoid + nn.BCELoss (kind "bce") on the D logit."""
+    t = torch.full_like(v, float(target))
+    if kind == "mse":
+        return F.mse_loss(v, t)
+    return F.binary_cross_entropy(torch.sigmoid(v), t)
+
+
+class ConvGan:
+    """One CAPGAN worker + its server on the conv GAN (N = 1: alpha = 1, capgan.py:247-249)."""
+
+    def __init__(self, gp, gb, dp, db, loss="mse", dtype=torch.float64):
+        cv = lambda d: OrderedDict((k, v.detach().clone().to(dtype if v.is_floating_point() else v.dtype))
+                                   for k, v in d.items())
+        self.gp, self.gb, self.dp, self.db = cv(gp), cv(gb), cv(dp), cv(db)
+        for p in list(self.gp.values()) + list(self.dp.values()):
+            p.requires_grad_(True)
+        self.loss = loss
+        self.opt_g = Adam(list(self.gp.values()), LR, (B1, B2), ADAM_EPS)
+        self.opt_d = Adam(list(self.dp.values()), LR, (B1, B2), ADAM_EPS)
+        self.lam = 0.0
+        self.dtype = dtype
+
+    def round(self, z1, z2, real, masks_real, masks_fake, masks_g):
+        """capgan.py:215-260 with one worker (capgan.py:324-347), explicit inputs and masks."""
+        dt = self.dtype
+        z1, z2, real = z1.to(dt), z2.to(dt), real.to(dt)
+        with torch.no_grad():
+            Xd = g_forward(self.gp, self.gb, z1)
+        Xg = g_forward(self.gp, self.gb, z2)
+        half = 0.5 if self.loss == "mse" else 1.0
+        for p in self.dp.values():
+            p.grad = None
+        real_loss = adv_loss(d_forward(self.dp, self.db, real, masks_real), 1, self.loss)
+        fake_loss = adv_loss(d_forward(self.dp, self.db, Xd.detach(), masks_fake), 0, self.loss)
+        d_loss = (real_loss + fake_loss) * half
+        d_loss.backward()
+        d_grads = OrderedDict((k, p.grad.detach().clone()) for k, p in self.dp.items())
+        self.opt_d.step()
+        for p in self.gp.values():
+            p.grad = None
+        g_loss = adv_loss(d_forward(self.dp, self.db, Xg, masks_g), 1, self.loss)
+        F_max = g_loss - LAMBDA_REG * self.lam
+        F_max.backward()
+        g_grads = OrderedDict((k, p.grad.detach().clone()) for k, p in self.gp.items())
+        self.lam = self.lam + LAMBDA_LR * LAMBDA_REG   # SGD on Lambda: dF/dLambda = -0.001
+        self.opt_g.step()
+        return dict(Xd=Xd.detach(), Xg=Xg.detach(), d_loss=float(d_loss), d_real=float(real_loss),
+                    d_fake=float(fake_loss), g_loss=float(g_loss), d_grads=d_grads, g_grads=g_grads)
