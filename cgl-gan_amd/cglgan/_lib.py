@@ -102,7 +102,7 @@ def _load():
         "cgl_bn1d_bwd": (ci, [vp, vp, vp, ci, ci, vp, vp, vp, ci, cf, vp, vp, vp, vp, i64, vp]),
         "cgl_op_workspace_bytes": (i64, []),
         "cgl_conv3x3_workspace_bytes": (i64, [ci] * 7),
-        "cgl_conv3x3_fwd": (ci, [vp, vp, vp, vp] + [ci] * 9 + [cf, vp, vp, i64, vp]),
+        "cgl_conv3x3_fwd": (ci, [vp, vp, vp, vp] + [ci] * 8 + [cf, vp, vp, i64, vp]),
         "cgl_conv3x3_bwd_data": (ci, [vp, vp, vp] + [ci] * 7 + [vp, i64, vp]),
         "cgl_conv3x3_bwd_weight": (ci, [vp, vp, vp, vp] + [ci] * 7 + [vp, i64, vp]),
         "cgl_bn2d_workspace_bytes": (i64, [ci] * 4),

@@ -1,0 +1,353 @@
+"""One worker's CAPGAN round on the model/lsgan.py conv GAN, on its own MI355X.
+
+The drop-in for the reference's Server.train + Worker.train pair (capgan.py:211-262 + :316-349)
+with the conv Generator / Discriminator of model/lsgan.py:3-27, 73-99.  Every tensor operation is
+a libcglgan_hip kernel (cglgan.conv_ops, stream-ordered, no host synchronisation inside a round);
+the host only sequences launches.  The reference never trains these models, so the
+adversarial objective is a knob: ``loss="mse"`` (LSGAN, D_loss = 0.5 (real + fake)) or ``"bce"``
+(Sigmoid + BCELoss on the logit, D_loss = real + fake as in the BCE drivers).
+
+Data layout (HBM, all NHWC fp32):
+  G  (2B rows: the no-grad Xd call on z1, then the Xg call on z2 -- one launch chain, BatchNorm
+     statistics per call):  z [2B,100] -> h [2B,8192] -> h0 [2B,8,8,128] -> y1/a1 [2B,16,16,128]
+     -> y2/a2 [2B,32,32,64] -> x3[B:3B] (images, Tanh)
+  x3 [3B,32,32,1]: rows [0,B) the sampled real batch, [B,2B) Xd, [2B,3B) Xg, so the D step reads
+     [real; Xd] and the G-loss pass reads Xg without copies.
+  D  (2B rows in the D step: the real call and the fake call, statistics and Dropout2d masks per
+     call; B rows in the G-loss pass): q1..q4 (Conv -> LeakyReLU -> Dropout2d), r2..r4 (BN2d),
+     flat [.,512] (NCHW flatten, model/lsgan.py:96), v [.,1]
+Parameters: one flat buffer per model (+ grads, Adam m, v), 256-byte aligned tensors in
+state-dict order, exposed as views under the reference's keys (``l1.0.weight``,
+``conv_blocks.2.running_var``, ``model.14.bias``, ``adv_layer.weight`` ...).
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import torch
+
+from . import _lib as C
+from . import conv_ops as O
+
+# (key, kind, shape) in construction (= state-dict) order, model/lsgan.py
+LSGAN_G = [("l1.0", "linear", (128 * 8 * 8, 100)), ("conv_blocks.1", "conv", (128, 128)), ("conv_blocks.2", "bn", 128),
+           ("conv_blocks.5", "conv", (64, 128)), ("conv_blocks.6", "bn", 64), ("conv_blocks.8", "conv", (1, 64))]
+LSGAN_D = [("model.0", "conv", (16, 1)), ("model.3", "conv", (32, 16)), ("model.6", "bn", 32),
+           ("model.7", "conv", (64, 32)), ("model.10", "bn", 64), ("model.11", "conv", (128, 64)),
+           ("model.14", "bn", 128), ("adv_layer", "linear", (1, 128 * 2 * 2))]
+D_CONVS = [("model.0", None, 1, 16, 32), ("model.3", "model.6", 16, 32, 16), ("model.7", "model.10", 32, 64, 8),
+           ("model.11", "model.14", 64, 128, 4)]   # (conv, bn, cin, cout, input h = w)
+DROP_P = 0.25
+BN_EPS, BN_MOM, SLOPE = 0.8, 0.1, 0.2
+_AL = 64   # floats: 256-byte tensor alignment
+
+
+def tensor_shapes(spec):
+    for key, kind, shp in spec:
+        if kind == "linear":
+            yield key + ".weight", tuple(shp), kind
+            yield key + ".bias", (shp[0],), kind
+        elif kind == "conv":
+            yield key + ".weight", (shp[0], shp[1], 3, 3), kind
+            yield key + ".bias", (shp[0],), kind
+        else:
+            yield key + ".weight", (shp,), kind
+            yield key + ".bias", (shp,), kind
+
+
+class FlatModel:
+    """Flat parameter / grad / Adam-state buffers of one model with reference-keyed views."""
+
+    def __init__(self, spec, device):
+        self.spec = spec
+        offs, off = [], 0
+        for k, shp, _ in tensor_shapes(spec):
+            n = math.prod(shp)
+            offs.append((k, shp, off, n))
+            off += (n + _AL - 1) // _AL * _AL
+        f32 = dict(dtype=torch.float32, device=device)
+        self.p, self.g = torch.zeros(off, **f32), torch.zeros(off, **f32)
+        self.m, self.v = torch.zeros(off, **f32), torch.zeros(off, **f32)
+        self.layout = offs
+        self.params = OrderedDict((k, self.p[o:o + n].view(shp)) for k, shp, o, n in offs)
+        self.grads = OrderedDict((k, self.g[o:o + n].view(shp)) for k, shp, o, n in offs)
+        self._m = [self.m[o:o + n] for _, _, o, n in offs]
+        self._v = [self.v[o:o + n] for _, _, o, n in offs]
+        self.running = OrderedDict()
+        self.batches = OrderedDict()
+        for key, kind, shp in spec:
+            if kind == "bn":
+                self.running[key + ".running_mean"] = torch.zeros(shp, **f32)
+                self.running[key + ".running_var"] = torch.ones(shp, **f32)
+                self.batches[key] = 0
+        self.step = 0
+
+    def adam(self, lr, betas, eps):
+        self.step += 1
+        ps = [self.params[k].view(-1) for k, _, _, _ in self.layout]
+        gs = [self.grads[k].view(-1) for k, _, _, _ in self.layout]
+        O.adam_multi(ps, gs, self._m, self._v, self.step, lr, betas, eps)
+
+    def state_dict(self):
+        sd = OrderedDict()
+        for key, kind, _ in self.spec:
+            sd[key + ".weight"] = self.params[key + ".weight"].detach().clone()
+            sd[key + ".bias"] = self.params[key + ".bias"].detach().clone()
+            if kind == "bn":
+                sd[key + ".running_mean"] = self.running[key + ".running_mean"].clone()
+                sd[key + ".running_var"] = self.running[key + ".running_var"].clone()
+                sd[key + ".num_batches_tracked"] = torch.tensor(self.batches[key], dtype=torch.long)
+        return sd
+
+    @torch.no_grad()
+    def load_state_dict(self, sd):
+        for k, v in self.params.items():
+            v.copy_(sd[k].reshape(v.shape))
+        for k, v in self.running.items():
+            if k in sd:
+                v.copy_(sd[k])
+        for key in self.batches:
+            if key + ".num_batches_tracked" in sd:
+                self.batches[key] = int(sd[key + ".num_batches_tracked"])
+        self.m.zero_()
+        self.v.zero_()
+        self.step = 0
+
+
+@torch.no_grad()
+def default_init(fm: FlatModel, generator=None):
+    """nn.Linear / nn.Conv2d reset_parameters (kaiming_uniform_(a=sqrt(5)); bias U(+-1/sqrt(fan_in))) and
+    BatchNorm2d (1, 0), drawn from the torch CPU RNG in construction order: torch.manual_seed(s) then
+    this equals torch.manual_seed(s); Generator(ims) / Discriminator(ims) of model/lsgan.py."""
+    for key, kind, shp in fm.spec:
+        w, b = fm.params[key + ".weight"], fm.params[key + ".bias"]
+        if kind == "bn":
+            w.fill_(1.0)
+            b.fill_(0.0)
+            continue
+        wc = torch.empty(w.shape)
+        bc = torch.empty(b.shape)
+        torch.nn.init.kaiming_uniform_(wc, a=math.sqrt(5), generator=generator)
+        bound = 1.0 / math.sqrt(wc[0].numel())
+        torch.nn.init.uniform_(bc, -bound, bound, generator=generator)
+        w.copy_(wc)
+        b.copy_(bc)
+
+
+class ConvGanStep:
+    """Fused CAPGAN worker round of the model/lsgan.py GAN (see module docstring)."""
+
+    def __init__(self, batch, loss="mse", data=None, seed=20211212, n_workers=1, rank=0, weighting="capgan",
+                 lr=2e-4, betas=(0.5, 0.999), adam_eps=1e-8, gen_z=True, device="cuda"):
+        if loss not in ("mse", "bce"):
+            raise ValueError("loss must be 'mse' (LSGAN) or 'bce' (Sigmoid + BCELoss)")
+        if batch < 2:
+            raise ValueError("BatchNorm in train mode needs batch >= 2")
+        dev = torch.device(device)
+        self.device, self.B, self.loss = dev, batch, loss
+        self.lr, self.betas, self.eps = lr, betas, adam_eps
+        self.seed, self.gen_z = seed, gen_z
+        self.n_workers, self.rank, self.weighting = n_workers, rank, weighting
+        self.G, self.D = FlatModel(LSGAN_G, dev), FlatModel(LSGAN_D, dev)
+        B, B2 = batch, 2 * batch
+        e = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)
+        self.z = e(B2, 100)
+        self.h, self.h0 = e(B2, 8192), e(B2, 8, 8, 128)
+        self.y1, self.a1 = e(B2, 16, 16, 128), e(B2, 16, 16, 128)
+        self.y2, self.a2 = e(B2, 32, 32, 64), e(B2, 32, 32, 64)
+        self.x3 = e(3 * B, 32, 32, 1)
+        self.g_save = {k: (e(2, c), e(2, c)) for k, c in (("conv_blocks.2", 128), ("conv_blocks.6", 64))}
+        # D activations (2B rows: D step; first B rows reused by the G-loss pass)
+        self.q = [e(B2, hw // 2, hw // 2, co) for _, _, _, co, hw in D_CONVS]
+        self.r = [None] + [e(B2, hw // 2, hw // 2, co) for _, _, _, co, hw in D_CONVS[1:]]
+        self.flat, self.v = e(B2, 512), e(B2, 1)
+        self.d_save = {bn: (e(2, co), e(2, co)) for _, bn, _, co, _ in D_CONVS if bn}
+        self.mask_d = [e(B2, co) for _, _, _, co, _ in D_CONVS]    # D step masks (real rows, then fake rows)
+        self.mask_g = [e(B, co) for _, _, _, co, _ in D_CONVS]     # G-loss pass masks
+        # gradients
+        self.dv, self.dflat = e(B2, 1), e(B2, 512)
+        self.dr = [None] + [e(B2, hw // 2, hw // 2, co) for _, _, _, co, hw in D_CONVS[1:]]
+        self.dc = [e(B2, hw // 2, hw // 2, co) for _, _, _, co, hw in D_CONVS]
+        self.dq1 = e(B2, 16, 16, 16)
+        self.dimg, self.dc3g = e(B, 32, 32, 1), e(B, 32, 32, 1)
+        self.da2, self.dy2 = e(B, 32, 32, 64), e(B, 32, 32, 64)
+        self.da1, self.dy1 = e(B, 16, 16, 128), e(B, 16, 16, 128)
+        self.dh0, self.dh = e(B, 8, 8, 128), e(B, 8192)
+        self.lbuf = e(8)                       # d_real, d_fake, g_loss
+        self.losses_all = e(max(n_workers, 1))
+        self.lam = 0.0
+        self.beta = [1.0 / n_workers] * n_workers
+        self.round = 0
+        # sampler over a device-resident real shard [n, 1024] (DataLoader(shuffle=True), capgan.py:282)
+        self.data = data
+        self._perm, self._pos = None, 0
+        self._gen = torch.Generator().manual_seed(seed + 1 + rank)
+        if data is not None:
+            if data.dim() != 2 or data.shape[1] != 1024 or data.shape[0] < B:
+                raise ValueError("data must be a [n >= batch, 1024] tensor of 32x32 images")
+            if not data.is_cuda or data.dtype != torch.float32:
+                raise ValueError("data must be float32 on the GPU")
+
+    # ------------------------------------------------------------------ state
+    def init_default(self, seed_g=20211212, seed_d=None):
+        """capgan.py:28,156,309: torch.manual_seed(seed) then G (and D) constructed."""
+        torch.manual_seed(seed_g)
+        default_init(self.G)
+        if seed_d is not None:
+            torch.manual_seed(seed_d)
+        default_init(self.D)
+
+    # ------------------------------------------------------------------ pieces
+    def _sample_real(self):
+        B = self.B
+        n = self.data.shape[0]
+        if self._perm is None or self._pos + B > n:
+            self._perm = torch.randperm(n, generator=self._gen).to(torch.int32).to(self.device, non_blocking=True)
+            self._pos = 0
+        O.gather_rows(self.data, self._perm[self._pos:self._pos + B], 0, B, 1024, self.x3)
+        self._pos += B
+
+    def _g_forward(self):
+        P, B2 = self.G.params, 2 * self.B
+        O.dense_fwd(self.z, P["l1.0.weight"], P["l1.0.bias"], self.h, B2, 100, 8192)
+        O.nchw_to_nhwc(self.h, self.h0, B2, 128, 64)      # out.view(B, 128, 8, 8), model/lsgan.py:25
+        O.conv3x3_fwd(self.h0, P["conv_blocks.1.weight"], P["conv_blocks.1.bias"], self.y1, B2, 8, 8, 128, 128, 1, 1)
+        self._g_bn("conv_blocks.2", self.y1, self.a1, 256, 128)
+        O.conv3x3_fwd(self.a1, P["conv_blocks.5.weight"], P["conv_blocks.5.bias"], self.y2, B2, 16, 16, 128, 64, 1, 1)
+        self._g_bn("conv_blocks.6", self.y2, self.a2, 1024, 64)
+        O.conv3x3_fwd(self.a2, P["conv_blocks.8.weight"], P["conv_blocks.8.bias"], self.x3[self.B:], B2, 32, 32, 64, 1,
+                      1, 0, act=O.ACT_TANH)
+
+    def _g_bn(self, key, x, y, hw, c):
+        P, R = self.G.params, self.G.running
+        sm, si = self.g_save[key]
+        O.bn2d_fwd(x, 2 * self.B, hw, c, P[key + ".weight"], P[key + ".bias"], y, groups=2, eps=BN_EPS,
+                   momentum=BN_MOM, running_mean=R[key + ".running_mean"], running_var=R[key + ".running_var"],
+                   train=True, act=O.ACT_LEAKY, slope=SLOPE, save_mean=sm, save_invstd=si)
+        self.G.batches[key] += 2
+
+    def _masks(self, masks, n, call):
+        for k, (_, _, _, co, _) in enumerate(D_CONVS):
+            O.dropout2d_mask(masks[k], n, co, DROP_P, self.seed * 7919 + self.rank, (self.round * 2 + call) * 4 + k)
+
+    def _d_forward(self, x, n, groups, masks):
+        P, R = self.D.params, self.D.running
+        inp = x
+        for k, (ck, bk, ci, co, hw) in enumerate(D_CONVS):
+            O.conv3x3_fwd(inp, P[ck + ".weight"], P[ck + ".bias"], self.q[k], n, hw, hw, ci, co, 2, 0, act=O.ACT_LEAKY,
+                          slope=SLOPE, drop=masks[k])
+            inp = self.q[k]
+            if bk:
+                sm, si = self.d_save[bk]
+                O.bn2d_fwd(self.q[k], n, (hw // 2) ** 2, co, P[bk + ".weight"], P[bk + ".bias"], self.r[k], groups=groups,
+                           eps=BN_EPS, momentum=BN_MOM, running_mean=R[bk + ".running_mean"],
+                           running_var=R[bk + ".running_var"], train=True, act=O.ACT_NONE, save_mean=sm, save_invstd=si)
+                self.D.batches[bk] += groups
+                inp = self.r[k]
+        O.nhwc_to_nchw(self.r[3], self.flat, n, 128, 4)    # out.view(B, -1), model/lsgan.py:96
+        O.dense_fwd(self.flat, P["adv_layer.weight"], P["adv_layer.bias"], self.v, n, 512, 1)
+
+    def _d_backward(self, x, n, groups, masks, wgrad, dx):
+        P, G = self.D.params, self.D.grads
+        O.dense_bwd_data(self.dv, P["adv_layer.weight"], self.dflat, n, 512, 1)
+        if wgrad:
+            O.dense_bwd_weight(self.dv, self.flat, G["adv_layer.weight"], G["adv_layer.bias"], n, 512, 1)
+        O.nchw_to_nhwc(self.dflat, self.dr[3], n, 128, 4)
+        for k in (3, 2, 1, 0):
+            ck, bk, ci, co, hw = D_CONVS[k]
+            ho = hw // 2
+            if bk:
+                sm, si = self.d_save[bk]
+                O.bn2d_bwd(self.dr[k], self.q[k], n, ho * ho, co, sm, si, P[bk + ".weight"], self.dc[k], groups=groups,
+                           post_out=self.q[k], drop=masks[k], dgamma=G[bk + ".weight"] if wgrad else None,
+                           dbeta=G[bk + ".bias"] if wgrad else None, slope=SLOPE)
+            else:
+                O.act_drop_bwd(self.dq1, self.q[0], masks[0], n, ho * ho, co, self.dc[0], slope=SLOPE)
+            inp = x if k == 0 else (self.q[0] if k == 1 else self.r[k - 1])
+            if wgrad:
+                O.conv3x3_bwd_weight(self.dc[k], inp, G[ck + ".weight"], G[ck + ".bias"], n, hw, hw, ci, co, 2, 0)
+            if k > 0:
+                O.conv3x3_bwd_data(self.dc[k], P[ck + ".weight"], self.dr[k - 1] if k > 1 else self.dq1, n, hw, hw, ci, co,
+                                   2, 0)
+            elif dx is not None:
+                O.conv3x3_bwd_data(self.dc[0], P[ck + ".weight"], dx, n, hw, hw, ci, co, 2, 0)
+
+    def _g_backward(self):
+        P, G, B = self.G.params, self.G.grads, self.B
+        O.act_drop_bwd(self.dimg, self.x3[2 * B:], None, B, 1024, 1, self.dc3g, tanh_y=True)
+        O.conv3x3_bwd_weight(self.dc3g, self.a2[B:], G["conv_blocks.8.weight"], G["conv_blocks.8.bias"], B, 32, 32, 64,
+                             1, 1, 0)
+        O.conv3x3_bwd_data(self.dc3g, P["conv_blocks.8.weight"], self.da2, B, 32, 32, 64, 1, 1, 0)
+        sm, si = self.g_save["conv_blocks.6"]
+        O.bn2d_bwd(self.da2, self.y2[B:], B, 1024, 64, sm[1], si[1], P["conv_blocks.6.weight"], self.dy2,
+                   post=self.a2[B:], dgamma=G["conv_blocks.6.weight"], dbeta=G["conv_blocks.6.bias"], slope=SLOPE)
+        O.conv3x3_bwd_weight(self.dy2, self.a1[B:], G["conv_blocks.5.weight"], G["conv_blocks.5.bias"], B, 16, 16, 128,
+                             64, 1, 1)
+        O.conv3x3_bwd_data(self.dy2, P["conv_blocks.5.weight"], self.da1, B, 16, 16, 128, 64, 1, 1)
+        sm, si = self.g_save["conv_blocks.2"]
+        O.bn2d_bwd(self.da1, self.y1[B:], B, 256, 128, sm[1], si[1], P["conv_blocks.2.weight"], self.dy1,
+                   post=self.a1[B:], dgamma=G["conv_blocks.2.weight"], dbeta=G["conv_blocks.2.bias"], slope=SLOPE)
+        O.conv3x3_bwd_weight(self.dy1, self.h0[B:], G["conv_blocks.1.weight"], G["conv_blocks.1.bias"], B, 8, 8, 128,
+                             128, 1, 1)
+        O.conv3x3_bwd_data(self.dy1, P["conv_blocks.1.weight"], self.dh0, B, 8, 8, 128, 128, 1, 1)
+        O.nhwc_to_nchw(self.dh0, self.dh, B, 128, 64)
+        O.dense_bwd_weight(self.dh, self.z[B:], G["l1.0.weight"], G["l1.0.bias"], B, 100, 8192)
+
+    # ------------------------------------------------------------------ round
+    def phase_a(self, real=None):
+        """G forward (Xd, Xg), the local D step, the G loss through the updated D and its gradient
+        w.r.t. Xg (capgan.py:215-225, 322-347).  Ends with ``dimg`` = d l_rank / d Xg."""
+        B = self.B
+        if self.gen_z:
+            C.check(C.lib.cgl_normal_fill(ctypes_ptr(self.z), self.z.numel(), self.seed, self.round, 0,
+                                          O._s()), "cgl_normal_fill")
+        if real is not None:
+            O.gather_rows(real.reshape(-1, 1024), None, 0, B, 1024, self.x3)
+        elif self.data is not None:
+            self._sample_real()
+        self._g_forward()
+        # local D step on [real; Xd]: two forward calls (statistics, masks per call), one backward
+        half = 0.5 if self.loss == "mse" else 1.0
+        self._masks(self.mask_d, 2 * B, 0)
+        self._d_forward(self.x3, 2 * B, 2, self.mask_d)
+        O.adv_loss(self.v[:B], B, 1, self.loss, 1, half, self.lbuf[0:1], self.dv[:B])
+        O.adv_loss(self.v[B:2 * B], B, 1, self.loss, 0, half, self.lbuf[1:2], self.dv[B:2 * B])
+        self._d_backward(self.x3, 2 * B, 2, self.mask_d, wgrad=True, dx=None)
+        self.D.adam(self.lr, self.betas, self.eps)
+        # G loss through the updated D (its D weight gradient is discarded by the reference: skipped)
+        self._masks(self.mask_g, B, 1)
+        self._d_forward(self.x3[2 * B:], B, 1, self.mask_g)
+        O.adv_loss(self.v[:B], B, 1, self.loss, 1, 1.0, self.lbuf[2:3], self.dv[:B])
+        self._d_backward(self.x3[2 * B:], B, 1, self.mask_g, wgrad=False, dx=self.dimg)
+
+    def phase_b(self):
+        """Replicated G backward from the (exchanged) image gradient, lambda SGD, Adam G (capgan.py:258-260)."""
+        self._g_backward()
+        self.G.adam(self.lr, self.betas, self.eps)
+        self.lam += 0.1 * 0.001   # optim.SGD([Lambda], lr=0.1) with dF/dLambda = -0.001 (capgan.py:249,259)
+        self.round += 1
+
+    def run(self, real=None):
+        """One round with N = 1 (alpha = 1 exactly, capgan.py:247-248)."""
+        if self.n_workers != 1:
+            raise RuntimeError("n_workers > 1: use cglgan.exchange.ConvExchange")
+        self.phase_a(real)
+        self.phase_b()
+
+    def stats(self):
+        l = self.lbuf.cpu()
+        half = 0.5 if self.loss == "mse" else 1.0
+        return {"round": self.round, "d_real": float(l[0]), "d_fake": float(l[1]),
+                "d_loss": float((l[0] + l[1]) * half), "g_loss": float(l[2]), "lambda": self.lam}
+
+    def xd(self):
+        return self.x3[self.B:2 * self.B]
+
+    def xg(self):
+        return self.x3[2 * self.B:]
+
+
+def ctypes_ptr(t):
+    import ctypes
+    return ctypes.c_void_p(t.data_ptr())

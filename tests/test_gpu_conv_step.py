@@ -1,0 +1,117 @@
+"""Parity of the fused conv-GAN worker round (cglgan.ConvGanStep, model/lsgan.py) with the CPU oracle.
+
+The HIP round and oracle/conv_oracle.py start from the same parameters and consume the same
+inputs: z (drawn on device, read back), the real batch, and the Dropout2d scales the round drew
+(read back and injected into the oracle).  The oracle runs twice, in float64 (truth) and in float32
+(the reference's own CPU arithmetic); per tensor the HIP result must satisfy
+
+    ||hip - fp64|| <= max(STEP_TOL * ||fp64||, 4 * ||fp32 - fp64||)          (1e-5)
+
+i.e. it is within 1e-5 relative of exact, or at least as close to exact as (4x) the reference's
+fp32 computation -- the yardstick for quantities that fp32 itself cannot resolve (LeakyReLU
+kinks hit by rounding, the analytically-zero gradient of a conv bias that feeds BatchNorm2d).
+"""
+import pytest
+import torch
+
+from oracle import conv_oracle as CO
+
+pytestmark = pytest.mark.gpu
+STEP_TOL = 1e-5
+PRE_BN_BIAS = {"conv_blocks.1.bias", "conv_blocks.5.bias"}   # gradient == 0 analytically
+
+
+def _err(a, b):
+    return float((a.detach().double().cpu() - b.detach().double().cpu()).norm())
+
+
+def _check(name, hip, o64, o32, fails, tol=STEP_TOL):
+    e = _err(hip, o64)
+    bound = max(tol * float(o64.detach().double().norm()), 4 * _err(o32, o64), 1e-12)
+    if e > bound:
+        fails.append(f"{name}: err {e:.3e} > bound {bound:.3e} (fp32 oracle err {_err(o32, o64):.3e})")
+
+
+def _run(B, loss, seed=3, rounds=1):
+    from cglgan.conv_step import ConvGanStep
+    torch.set_num_threads(4)
+    st = ConvGanStep(B, loss=loss, seed=seed)
+    st.init_default(20211212, 20211213)
+    gp0, dp0 = st.G.state_dict(), st.D.state_dict()
+    split = lambda sd: ({k: v.cpu() for k, v in sd.items() if "running" not in k and "num_batches" not in k},
+                        {k: v.cpu() for k, v in sd.items() if "running" in k or "num_batches" in k})
+    gp, gb = split(gp0)
+    dp, db = split(dp0)
+    o64 = CO.ConvGan(gp, gb, dp, db, loss=loss, dtype=torch.float64)
+    o32 = CO.ConvGan(gp, gb, dp, db, loss=loss, dtype=torch.float32)
+    g = torch.Generator().manual_seed(seed)
+    outs = []
+    for r in range(rounds):
+        real = torch.rand(B, 1, 32, 32, generator=g) * 2 - 1
+        st.run(real=real.cuda())
+        torch.cuda.synchronize()
+        z = st.z.cpu()
+        mr = [m[:B].cpu() for m in st.mask_d]
+        mf = [m[B:].cpu() for m in st.mask_d]
+        mg = [m.cpu() for m in st.mask_g]
+        r64 = o64.round(z[:B], z[B:], real, mr, mf, mg)
+        r32 = o32.round(z[:B], z[B:], real, mr, mf, mg)
+        outs.append((st.stats(), r64, r32, st.G.grads, st.D.grads))
+    return st, o64, o32, outs
+
+
+@pytest.mark.parametrize("loss", ["mse", "bce"])
+def test_conv_round_parity(loss):
+    B = 8
+    st, o64, o32, outs = _run(B, loss)
+    s, r64, r32, gg, dg = outs[0]
+    fails = []
+    for k in ("d_real", "d_fake", "g_loss"):
+        _check(k, torch.tensor(s[k]), torch.tensor(r64[k]), torch.tensor(r32[k]), fails)
+    _check("Xd", st.xd().permute(0, 3, 1, 2), r64["Xd"], r32["Xd"], fails)
+    _check("Xg", st.xg().permute(0, 3, 1, 2), r64["Xg"], r32["Xg"], fails)
+    for k, v in r64["g_grads"].items():
+        if k in PRE_BN_BIAS:
+            continue
+        _check("G grad " + k, gg[k], v, r32["g_grads"][k], fails)
+    for k, v in r64["d_grads"].items():
+        _check("D grad " + k, dg[k], v, r32["d_grads"][k], fails)
+    p0g = {k: v.detach() for k, v in o64.gp.items()}
+    for k, v in st.G.params.items():
+        if k in PRE_BN_BIAS:   # Adam step of a rounding-noise gradient: bounded by lr
+            assert float((v.cpu().double() - o64.gp[k].detach()).abs().max()) <= 2 * 2e-4 + 1e-6, k
+            continue
+        _check("G param " + k, v, o64.gp[k], o32.gp[k], fails)
+    for k, v in st.D.params.items():
+        _check("D param " + k, v, o64.dp[k], o32.dp[k], fails)
+    for k, v in st.G.running.items():
+        _check("G " + k, v, o64.gb[k], o32.gb[k], fails)
+    for k, v in st.D.running.items():
+        _check("D " + k, v, o64.db[k], o32.db[k], fails)
+    assert all(st.G.batches[k] == int(o64.gb[k + ".num_batches_tracked"]) for k in st.G.batches)
+    assert all(st.D.batches[k] == int(o64.db[k + ".num_batches_tracked"]) for k in st.D.batches)
+    assert not fails, "\n".join(fails)
+
+
+def test_conv_trajectory_5_rounds():
+    """Free-running 5 rounds: losses within 1e-4 relative of the fp64 oracle."""
+    B = 8
+    st, o64, o32, outs = _run(B, "mse", seed=5, rounds=5)
+    for s, r64, r32, _, _ in outs:
+        for k in ("d_real", "d_fake", "g_loss"):
+            ref = r64[k]
+            bound = max(1e-4 * abs(ref), 4 * abs(r32[k] - ref))
+            assert abs(s[k] - ref) <= bound, (k, s[k], ref)
+
+
+def test_conv_round_deterministic():
+    """Two replicas with identical state and inputs produce bitwise identical results."""
+    from cglgan.conv_step import ConvGanStep
+    a, b = ConvGanStep(8, seed=11), ConvGanStep(8, seed=11)
+    a.init_default(1, 2)
+    b.init_default(1, 2)
+    real = torch.rand(8, 1, 32, 32, device="cuda") * 2 - 1
+    for _ in range(2):
+        a.run(real=real)
+        b.run(real=real)
+    assert torch.equal(a.G.p, b.G.p) and torch.equal(a.D.p, b.D.p)
