@@ -50,6 +50,10 @@ def args_():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--profile-reps", type=int, default=20, help="back-to-back replays per launch when timing launches")
+    p.add_argument("--model", choices=["mlp", "lsgan"], default="mlp",
+                   help="mlp: model/mnist_model.py (BASELINE configs[1], the default workload); "
+                        "lsgan: the model/lsgan.py conv GAN round (32x32, MSE/LSGAN loss)")
+    p.add_argument("--loss", choices=["mse", "bce"], default="mse", help="conv GAN objective (--model lsgan)")
     return p.parse_args()
 
 
@@ -146,6 +150,165 @@ def cpu_baseline(a):
                       f"rounds, {t_total:.1f} s, torch {torch.__version__}"}
 
 
+# ------------------------------------------------------------------------------------------
+# conv GAN (model/lsgan.py) round
+def conv_flops(n, h, w, cin, cout, stride, up, which):
+    """(executed, reference-formulation) FLOPs of one conv3x3 op of cglgan.conv_ops.
+    Executed = the MFMA work of the tap tables (phase-form upsampling: 2x2 taps per output parity,
+    4x4 taps at stride 2 for its input gradient; stride-2 input gradients by input parity);
+    reference = the direct 9-tap convolution on the upsampled input that torch runs."""
+    ho, wo = ((h << up) - 1) // stride + 1, ((w << up) - 1) // stride + 1
+    ref = 2.0 * n * ho * wo * cout * 9 * cin
+    if which in ("fwd", "wgrad"):
+        exe = 2.0 * n * ho * wo * cout * 4 * cin if up else ref
+    elif up:
+        exe = 2.0 * n * h * w * cin * 16 * cout
+    elif stride == 1:
+        exe = ref
+    else:
+        t = lambda d: sum(((d - p + 1) // 2) * (1 if p == 0 else 2) for p in (0, 1))
+        exe = 2.0 * n * cin * cout * t(h) * t(w)
+    return exe, ref
+
+
+def profile_conv_round(step, real=None):
+    """One extra round with every conv op bracketed by HIP events on the launch stream: per-op
+    device time (pack + MFMA kernel, + fixed-order reduction for weight gradients) and FLOPs."""
+    from cglgan import conv_ops as CO
+    s = torch.cuda.current_stream()
+    recs = []
+    orig = {k: getattr(CO, k) for k in ("conv3x3_fwd", "conv3x3_bwd_data", "conv3x3_bwd_weight")}
+    kinds = {"conv3x3_fwd": "fwd", "conv3x3_bwd_data": "bwd_data", "conv3x3_bwd_weight": "wgrad"}
+
+    def wrap(name):
+        fn = orig[name]
+
+        def f(*args, **kw):
+            geo = args[4:11] if name == "conv3x3_bwd_weight" else (args[3:10] if name == "conv3x3_bwd_data"
+                                                                     else args[4:11])
+            n, h, w, cin, cout, stride, up = (list(geo) + [1, 0])[:7]
+            if name == "conv3x3_fwd":
+                stride = kw.get("stride", stride)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            out = fn(*args, **kw)
+            e1.record(s)
+            exe, ref = conv_flops(n, h, w, cin, cout, stride, up, kinds[name])
+            recs.append((kinds[name], (n, h, w, cin, cout, stride, up), e0, e1, exe, ref))
+            return out
+        return f
+
+    for k in orig:
+        setattr(CO, k, wrap(k))
+    try:
+        step.run(real=real)
+    finally:
+        for k, f in orig.items():
+            setattr(CO, k, f)
+    torch.cuda.synchronize()
+    out = []
+    for kind, geo, e0, e1, exe, ref in recs:
+        out.append({"op": kind, "geom": geo, "us": e0.elapsed_time(e1) * 1e3, "exec_flops": exe, "ref_flops": ref})
+    return out
+
+
+def conv_cpu_baseline(a):
+    """The conv oracle (torch-CPU restatement of the model/lsgan.py round) on this host's cores."""
+    sys.path.insert(0, ROOT)
+    from oracle import conv_oracle as CV
+    threads = max(1, min(16, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    torch.manual_seed(20211212)
+    gp, gb = CV.init_params(CV.G_SPEC)
+    dp, db = CV.init_params(CV.D_SPEC)
+    o = CV.ConvGan(gp, gb, dp, db, loss=a.loss, dtype=torch.float32)
+    B = a.batch
+    g = torch.Generator().manual_seed(5)
+    n, t_total, warm = 0, 0.0, 1
+    while True:
+        z = torch.randn(2 * B, 100, generator=g)
+        real = torch.rand(B, 1, 32, 32, generator=g) * 2 - 1
+        m = [CV.draw_masks(B) for _ in range(3)]
+        t0 = time.perf_counter()
+        o.round(z[:B], z[B:], real, *m)
+        dt = time.perf_counter() - t0
+        n += 1
+        if n > warm:
+            t_total += dt
+        if (n > warm and t_total >= a.cpu_seconds) or n >= 200:
+            break
+    rounds = n - warm
+    return {"value": round(B * rounds / t_total, 2), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{rounds} conv-GAN CAPGAN rounds (model/lsgan.py, B={B}, N=1, {a.loss}) of the torch-CPU "
+                      f"oracle after {warm} warm-up round, {t_total:.1f} s, torch {torch.__version__}"}
+
+
+def main_lsgan(a, world, rank, local):
+    from cglgan.conv_step import ConvGanStep
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        g = torch.Generator(device="cuda").manual_seed(1000 + rank)
+        rows = (a.rows // a.batch) * a.batch
+        data = torch.rand(rows, 1024, device="cuda", generator=g) * 2 - 1
+        step = ConvGanStep(a.batch, loss=a.loss, data=data, seed=20211212, rank=rank)
+        step.init_default(20211212, 20211212 + 1 + rank)
+        torch.cuda.synchronize()
+        for _ in range(a.warmup):
+            step.run()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step.run()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        st = step.stats()
+        ops = profile_conv_round(step)
+    ms_step = el / a.steps * 1e3
+    value = world * a.batch * a.steps / el
+    if rank != 0:
+        return None
+    mma = [o for o in ops]
+    mma_us = sum(o["us"] for o in mma)
+    exe = sum(o["exec_flops"] for o in mma)
+    ref = sum(o["ref_flops"] for o in mma)
+    tf = exe / (mma_us * 1e-6) / 1e12
+    dom = max(mma, key=lambda o: o["us"])
+    out = {
+        "metric": METRIC + " [conv GAN model/lsgan.py variant]", "value": round(value, 1), "unit": "images/s",
+        "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"model/lsgan.py conv GAN, CAPGAN worker round (G fwd x2, D step, G loss, G bwd, "
+                               f"Adam G/D), {a.loss} objective, 32x32x1, 1 worker per GPU",
+                   "global_batch": a.batch * world, "batch_per_worker": a.batch, "img": "32x32x1",
+                   "parallelism": f"workers{world}", "dataset_rows_per_worker": rows},
+        "roofline": {"bound": "mfma", "kernel": "cgl_conv_fwd + cgl_conv_wgrad (+ pack / reduce), every conv op of "
+                                                "one round", "achieved": round(tf, 3), "peak": PEAK_F32_MFMA,
+                     "unit": "TFLOP/s", "frac": round(tf / PEAK_F32_MFMA, 4), "traffic": None,
+                     "conv_exec_gflop_per_round": round(exe / 1e9, 3),
+                     "conv_ref_gflop_per_round": round(ref / 1e9, 3),
+                     "conv_us_per_round": round(mma_us, 1),
+                     "effective_ref_tflops": round(ref / (mma_us * 1e-6) / 1e12, 3),
+                     "step_exec_tflops": round(exe / (ms_step * 1e-3) / 1e12, 3),
+                     "dominant_op": {"op": dom["op"], "geom": dom["geom"], "us": round(dom["us"], 1),
+                                     "tflops": round(dom["exec_flops"] / (dom["us"] * 1e-6) / 1e12, 2)},
+                     "ops": [{"op": o["op"], "geom": o["geom"], "us": round(o["us"], 1),
+                              "tflops": round(o["exec_flops"] / (o["us"] * 1e-6) / 1e12, 2)} for o in ops]},
+        "losses": {"d_loss": st["d_loss"], "g_loss": st["g_loss"], "round": st["round"]},
+    }
+    if world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = conv_cpu_baseline(a)
+    print(json.dumps(out), flush=True)
+    return out
+
+
 def main():
     a = args_()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -157,6 +320,12 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if a.model == "lsgan":
+        out = main_lsgan(a, world, rank, local)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return out
     stream = torch.cuda.Stream()
     with torch.cuda.stream(stream):
         step, data = build_step(a, rank, world)

@@ -57,7 +57,7 @@ struct CglConvProb {
 
 struct CglConvLaunch {
   CglConvProb p[CGL_CONV_MAXP];
-  int np, WM, WN;
+  int np, WM, WN, WK;        // waves per workgroup: WM x WN output blocks x WK k-splits
   const float* bias;         // [N] or null
   int act;                   // CGL_EPI_ACT_*
   float slope;
@@ -99,13 +99,14 @@ __device__ __forceinline__ int cgl_xcd_tile(int local, int nwg) {
 // FAST: Cin % 16 == 0, so a 16-k chunk lies inside one tap (uniform tap, 2 x 16-byte loads per
 // lane and block).  Otherwise each k is decoded per element (tiny-K layers: Cin = 1).
 template <int TM, int TN, bool FAST>
-__device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local) {
+__device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, float* s_red) {
   constexpr int S = 3;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, li = lane & 31, lh = lane >> 5;
-  const int WN = L->WN, WM = L->WM;
-  const int wm = wave / WN, wn = wave - wm * WN;
+  const int WN = L->WN, WM = L->WM, WK = L->WK;
+  const int wk = wave % WK, wmn = wave / WK;
+  const int wm = wmn / WN, wn = wmn - wm * WN;
   const int tiles_n = P->tiles_n;
   const int tile = cgl_xcd_tile(local, P->tiles_m * tiles_n);
   const int tn = tile % tiles_n, tm = tile / tiles_n;
@@ -202,23 +203,51 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[i][q], B[j][q], acc[i][j], 0, 0, 0);
   };
 
-  // S register sets in rotation (S - 1 chunks of loads in flight); Kp % 16 == 0, no K tail
+  // S register sets in rotation (S - 1 chunks of loads in flight); Kp % 16 == 0, no K tail.
+  // This wave's k-split: chunks [cb, ce).
   const int nch = Kp >> 4;
-  float xa[S][TM][8], xb[S][TN][8];
-  int okm[S];
+  const int cb = (wk * nch) / WK, ce = ((wk + 1) * nch) / WK;
+  if (cb < ce) {
+    float xa[S][TM][8], xb[S][TN][8];
+    int okm[S];
 #pragma unroll
-  for (int s = 0; s < S; ++s) load(min(s, nch - 1), xa[s], xb[s], okm[s]);
-  int c = 0;
-  for (; c + S <= nch; c += S) {
+    for (int s = 0; s < S; ++s) load(min(cb + s, ce - 1), xa[s], xb[s], okm[s]);
+    int c = cb;
+    for (; c + S <= ce; c += S) {
 #pragma unroll
-    for (int s = 0; s < S; ++s) {
-      compute(xa[s], xb[s], okm[s]);
-      load(min(c + s + S, nch - 1), xa[s], xb[s], okm[s]);
+      for (int s = 0; s < S; ++s) {
+        compute(xa[s], xb[s], okm[s]);
+        load(min(c + s + S, ce - 1), xa[s], xb[s], okm[s]);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < S - 1; ++s)
+      if (c + s < ce) compute(xa[s], xb[s], okm[s]);
+  }
+  // k-split reduction through LDS in a fixed order (wk = 1, 2, 3 added to wk = 0): deterministic
+  if (WK > 1) {
+    constexpr int NB = TM * TN;
+    if (wk > 0) {
+      float* dst = s_red + ((wmn * (WK - 1) + (wk - 1)) * NB * 16) * 64;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dst[((i * TN + j) * 16 + r) * 64 + lane] = acc[i][j][r];
+    }
+    __syncthreads();
+    if (wk > 0) return;
+    for (int q = 1; q < WK; ++q) {
+      const float* src = s_red + ((wmn * (WK - 1) + (q - 1)) * NB * 16) * 64;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] += src[((i * TN + j) * 16 + r) * 64 + lane];
     }
   }
-#pragma unroll
-  for (int s = 0; s < S - 1; ++s)
-    if (c + s < nch) compute(xa[s], xb[s], okm[s]);
 
   // epilogue: bias, activation, Dropout2d scale, NHWC store at the mapped position
   const int ldy = P->ldy, YH = P->YH, YW = P->YW;
@@ -261,11 +290,12 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local) {
 template <int TM, int TN, bool FAST>
 __global__ __launch_bounds__(256) void cgl_conv_fwd(CglConvLaunch args) {
   (void)args;
+  extern __shared__ float cgl_conv_lds[];
   CglKL L = cgl_conv_args();
   const int bid = blockIdx.x;
   const int pi = cgl_conv_prob(L, bid);
   CglKP P = &L->p[pi];
-  cgl_conv_fwd_body<TM, TN, FAST>(L, P, bid - P->wg_begin);
+  cgl_conv_fwd_body<TM, TN, FAST>(L, P, bid - P->wg_begin, cgl_conv_lds);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -415,42 +445,166 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad(CglConvLaunch args) {
 // ------------------------------------------------------------------------------------------
 // One-output-channel convolution on the vector ALUs (N == 1: Conv2d(64, 1) of the generator's
 // last layer, and the input gradient of the discriminator's Conv2d(1, 16)) -- an MFMA tile would
-// waste 31 of its 32 columns.  One thread per enumerated output pixel; Cin % 4 == 0.
+// waste 31 of its 32 columns.  Channels run across lanes: L = Cin / 4 lanes own one pixel (one
+// float4 of channels each, so a wave's load covers 64 / L whole pixel vectors, fully coalesced),
+// the lane's slice of every tap's weights stays in registers, and the L partial sums are combined
+// by an xor tree (fixed order).  Requires Cin % 4 == 0, Cin / 4 a power of two <= 64, <= 16 taps.
 __global__ __launch_bounds__(256) void cgl_conv_n1(CglConvLaunch args) {
   (void)args;
   CglKL L = cgl_conv_args();
   const int bid = blockIdx.x;
   const int pi = cgl_conv_prob(L, bid);
   CglKP P = &L->p[pi];
-  const int m = (bid - P->wg_begin) * 256 + threadIdx.x;
-  if (m >= P->M) return;
-  int img, oy, ox;
-  cgl_conv_pix(P, m, img, oy, ox);
   const int Cin = P->Cin, Tx = P->Tx, T = P->Ty * P->Tx;
+  const int c4 = Cin >> 2;
+  const int lanes = c4 < 64 ? c4 : 64;         // lanes per pixel (power of two)
+  const int nb = c4 / lanes;                   // float4 blocks per lane and tap (T * nb <= 16)
+  const int TB = T * nb;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane & (lanes - 1), slot = lane / lanes, ppw = 64 / lanes;
   const int IH = P->IH, IW = P->IW, ish = P->ish, XW = P->XW;
-  const float* __restrict__ X = P->X + (long)img * P->XH * XW * Cin;
-  const float* __restrict__ Wp = P->Wp;
-  float acc = 0.f;
-  for (int t = 0; t < T; ++t) {
-    const int ty = t / Tx, tx = t - ty * Tx;
-    const int iy = oy * P->isy + P->dy[ty], ix = ox * P->isx + P->dx[tx];
-    if ((unsigned)iy >= (unsigned)IH || (unsigned)ix >= (unsigned)IW) continue;
-    gcfp xp = (gcfp)(X + ((long)(iy >> ish) * XW + (ix >> ish)) * Cin);
-    gcfp wp = (gcfp)(Wp + t * Cin);
-    for (int c = 0; c < Cin; c += 4) {
-      const f32x4 v = *(gcf4p)(xp + c);
-      acc = fmaf(v[0], wp[c], acc);
-      acc = fmaf(v[1], wp[c + 1], acc);
-      acc = fmaf(v[2], wp[c + 2], acc);
-      acc = fmaf(v[3], wp[c + 3], acc);
+  f32x4 w[16];
+#pragma unroll
+  for (int tb = 0; tb < 16; ++tb) {
+    const int t = tb / nb, b = tb - t * nb;
+    w[tb] = tb < TB ? *(gcf4p)(P->Wp + t * Cin + 4 * (q + b * lanes)) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const float bias = L->bias ? gld(L->bias) : 0.f;
+  const int M = P->M;
+  const int per_wg = 4 * ppw * 8;              // 8 iterations of every wave per workgroup
+  const int m_begin = (bid - P->wg_begin) * per_wg;
+  for (int it = 0; it < 8; ++it) {
+    const int m = m_begin + (it * 4 + wave) * ppw + slot;
+    const bool mv = m < M;
+    int img, oy, ox;
+    cgl_conv_pix(P, min(m, M - 1), img, oy, ox);
+    const float* __restrict__ X = P->X + (long)img * P->XH * XW * Cin + 4 * q;
+    f32x4 v[16];
+#pragma unroll
+    for (int tb = 0; tb < 16; ++tb) {
+      if (tb < TB) {
+        const int t = tb / nb, b = tb - t * nb;
+        const int ty = t / Tx, tx = t - ty * Tx;
+        const int iy = oy * P->isy + P->dy[ty], ix = ox * P->isx + P->dx[tx];
+        const bool ok = (unsigned)iy < (unsigned)IH && (unsigned)ix < (unsigned)IW;
+        const int cy = min(max(iy, 0), IH - 1) >> ish, cx = min(max(ix, 0), IW - 1) >> ish;
+        v[tb] = *(gcf4p)(X + ((long)cy * XW + cx) * Cin + 4 * b * lanes);
+        if (!ok) v[tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    float acc = 0.f;
+#pragma unroll
+    for (int tb = 0; tb < 16; ++tb) {
+      if (tb < TB) {
+        acc = fmaf(v[tb][0], w[tb][0], acc);
+        acc = fmaf(v[tb][1], w[tb][1], acc);
+        acc = fmaf(v[tb][2], w[tb][2], acc);
+        acc = fmaf(v[tb][3], w[tb][3], acc);
+      }
+    }
+    for (int o = 1; o < lanes; o <<= 1) acc += __shfl_xor(acc, o);
+    if (mv && q == 0) {
+      float y = acc + bias;
+      if (L->act == CGL_EPI_ACT_LEAKY) y = y > 0.f ? y : y * L->slope;
+      else if (L->act == CGL_EPI_ACT_TANH) y = tanhf(y);
+      else if (L->act == CGL_EPI_ACT_SIGMOID) y = 1.f / (1.f + expf(-y));
+      if (L->drop) y *= gld(L->drop + (long)img * P->ldy);
+      gst(P->Y + (((long)img * P->YH + oy * P->osy + P->ooy) * P->YW + ox * P->osx + P->oox) * P->ldy, y);
     }
   }
-  float v = acc + (L->bias ? gld(L->bias) : 0.f);
-  if (L->act == CGL_EPI_ACT_LEAKY) v = v > 0.f ? v : v * L->slope;
-  else if (L->act == CGL_EPI_ACT_TANH) v = tanhf(v);
-  else if (L->act == CGL_EPI_ACT_SIGMOID) v = 1.f / (1.f + expf(-v));
-  if (L->drop) v *= gld(L->drop + (long)img * P->ldy);
-  gst(P->Y + (((long)img * P->YH + oy * P->osy + P->ooy) * P->YW + ox * P->osx + P->oox) * P->ldy, v);
+}
+
+// Weight gradient of a one-output-channel convolution (Conv2d(64, 1): 576 results reduced over every
+// output pixel) on the vector ALUs: thread = one im2col column k, pixels of the split in order, 8
+// loads in flight; partials part[split][0][k] for the fixed-order reduction.
+__global__ __launch_bounds__(256) void cgl_conv_wgrad_n1(CglConvLaunch args) {
+  (void)args;
+  CglKL L = cgl_conv_args();
+  CglKP P = &L->p[0];
+  const int K = P->K, Cin = P->Cin, Tx = P->Tx;
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  const int split = blockIdx.y, splits = P->splits;
+  const int M = P->M;
+  const int mb = (int)(((long)split * M) / splits), me = (int)(((long)(split + 1) * M) / splits);
+  const int kk = min(k, K - 1);
+  const int t = kk / Cin, c = kk - t * Cin;
+  const int ty = t / Tx, tx = t - ty * Tx;
+  const int dyv = P->dy[ty], dxv = P->dx[tx];
+  const int IH = P->IH, IW = P->IW, ish = P->ish, XW = P->XW, XH = P->XH;
+  float acc = 0.f;
+  for (int m0 = mb; m0 < me; m0 += 8) {
+    float d[8], x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = min(m0 + i, me - 1);
+      int img, oy, ox;
+      cgl_conv_pix(P, m, img, oy, ox);
+      d[i] = gld(P->Y + (((long)img * P->YH + oy * P->osy + P->ooy) * P->YW + ox * P->osx + P->oox) * P->ldy);
+      const int iy = oy * P->isy + dyv, ix = ox * P->isx + dxv;
+      const bool ok = (unsigned)iy < (unsigned)IH && (unsigned)ix < (unsigned)IW;
+      const int cy = min(max(iy, 0), IH - 1) >> ish, cx = min(max(ix, 0), IW - 1) >> ish;
+      x[i] = gld(P->X + (((long)img * XH + cy) * XW + cx) * Cin + c);
+      if (!ok || m0 + i >= me) x[i] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc = fmaf(d[i], x[i], acc);
+  }
+  if (k < K) gst(P->part + (long)split * P->Kp + k, acc);
+}
+
+// Input-stationary weight gradient of a stride-1 one-output-channel convolution (Conv2d(64, 1, 3, 1, 1)):
+// L = Cin / 4 lanes own one INPUT pixel (a float4 of channels each, loaded once, coalesced); every
+// tap t pairs it with the output-gradient pixel q - off_t (a broadcast scalar).  9 x 4 accumulators
+// per lane; the 256 / L pixel slots of a block are combined through LDS in a fixed order, giving
+// part[block][t * Cin + c] for the fixed-order split reduction.
+__global__ __launch_bounds__(256) void cgl_conv_wgrad_n1t(CglConvLaunch args) {
+  (void)args;
+  __shared__ float red[16384];
+  CglKL L = cgl_conv_args();
+  CglKP P = &L->p[0];
+  const int Cin = P->Cin, Tx = P->Tx, T = P->Ty * P->Tx;
+  const int lanes = Cin >> 2, slots = 256 / lanes;
+  const int q4 = threadIdx.x & (lanes - 1), slot = threadIdx.x / lanes;
+  const int XH = P->XH, XW = P->XW, OH = P->OH, OW = P->OW;
+  const int hw = XH * XW;
+  const long Min = (long)(P->M / (OH * OW)) * hw;
+  const int splits = P->splits;
+  const long qb = (blockIdx.x * Min) / splits, qe = ((blockIdx.x + 1) * Min) / splits;
+  f32x4 acc[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* __restrict__ dY = P->Y;
+  for (long qq = qb + slot; qq < qe; qq += slots) {
+    const int img = (int)(qq / hw);
+    const int r = (int)(qq - (long)img * hw);
+    const int iy = r / XW, ix = r - iy * XW;
+    const f32x4 x = *(gcf4p)(P->X + qq * Cin + 4 * q4);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      if (t < T) {
+        const int ty = t / Tx, tx = t - ty * Tx;
+        const int oy = iy - P->dy[ty], ox = ix - P->dx[tx];
+        const bool ok = (unsigned)oy < (unsigned)OH && (unsigned)ox < (unsigned)OW;
+        const float d = gld(dY + (((long)img * P->YH + min(max(oy, 0), OH - 1)) * P->YW + min(max(ox, 0), OW - 1)) *
+                                     P->ldy);
+        const float dd = ok ? d : 0.f;
+        acc[t][0] = fmaf(x[0], dd, acc[t][0]);
+        acc[t][1] = fmaf(x[1], dd, acc[t][1]);
+        acc[t][2] = fmaf(x[2], dd, acc[t][2]);
+        acc[t][3] = fmaf(x[3], dd, acc[t][3]);
+      }
+    }
+  }
+  const int K = T * Cin;
+#pragma unroll
+  for (int t = 0; t < 16; ++t)
+    if (t < T) *(f32x4*)&red[slot * K + t * Cin + 4 * q4] = acc[t];
+  __syncthreads();
+  for (int k = threadIdx.x; k < K; k += 256) {
+    float v = 0.f;
+    for (int sl = 0; sl < slots; ++sl) v += red[sl * K + k];
+    gst(P->part + (long)blockIdx.x * P->Kp + k, v);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -493,22 +647,28 @@ __global__ __launch_bounds__(256) void cgl_conv_pack(CglPackArgs a) {
 }
 
 // Weight-gradient reduction: dW[co][ci][kh][kw] = sum over problems, taps containing (kh, kw) and
-// splits (fixed order, double) of the partial tiles.  Thread e = ((co * 3 + kh) * 3 + kw) * cin + ci
-// (consecutive ci: coalesced partial reads).
+// splits of the partial tiles.  A block covers EB consecutive elements
+// e = ((co * ks + kh) * ks + kw) * cin + ci (consecutive ci: coalesced partial reads) x SG
+// split-groups (split-group g sums splits g, g + SG, ... in order, 8 loads in flight); the SG
+// partial sums are combined through LDS in a fixed order (deterministic).
 struct CglWgradReduceArgs {
   float* dW;
-  int cout, cin, np, ks;
+  int cout, cin, np, ks, EB, SG;
   const float* part[CGL_CONV_MAXP];
   int Kp[CGL_CONV_MAXP], splits[CGL_CONV_MAXP], Tx[CGL_CONV_MAXP], Ty[CGL_CONV_MAXP];
   int ym[CGL_CONV_MAXP][4], xm[CGL_CONV_MAXP][4];
 };
 
 __global__ __launch_bounds__(256) void cgl_conv_wgrad_reduce(CglWgradReduceArgs a) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
+  __shared__ double red[256];
+  const int EB = a.EB, SG = a.SG;
+  const int el = threadIdx.x % EB, sg = threadIdx.x / EB;
+  const int e = blockIdx.x * EB + el;
   const int cin = a.cin, ks = a.ks;
-  if (e >= a.cout * ks * ks * cin) return;
-  const int ci = e % cin;
-  const int rest = e / cin;
+  const int E = a.cout * ks * ks * cin;
+  const int ee = min(e, E - 1);
+  const int ci = ee % cin;
+  const int rest = ee / cin;
   const int kw = rest % ks, kh = (rest / ks) % ks, co = rest / (ks * ks);
   double acc = 0.0;
   for (int p = 0; p < a.np; ++p) {
@@ -519,11 +679,24 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad_reduce(CglWgradReduceArgs 
       for (int tx = 0; tx < Tx; ++tx) {
         if (!((a.xm[p][tx] >> kw) & 1)) continue;
         const float* src = a.part[p] + (long)co * Kp + (ty * Tx + tx) * cin + ci;
-        for (int s = 0; s < S; ++s) acc += (double)gld(src + s * sstride);
+        for (int s0 = sg; s0 < S; s0 += 8 * SG) {
+          float v[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[i] = gld(src + (long)min(s0 + i * SG, S - 1) * sstride);
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if (s0 + i * SG < S) acc += (double)v[i];
+        }
       }
     }
   }
-  gst(a.dW + ((long)co * cin + ci) * ks * ks + kh * ks + kw, (float)acc);
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (sg == 0 && e < E) {
+    double t = 0.0;
+    for (int g = 0; g < SG; ++g) t += red[g * EB + el];
+    gst(a.dW + ((long)co * cin + ci) * ks * ks + kh * ks + kw, (float)t);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -545,17 +718,35 @@ __global__ __launch_bounds__(256) void cgl_chan_reduce(CglChanArgs a) {
   const int c = threadIdx.x % C, rl = threadIdx.x / C;
   const int r0 = blockIdx.x * a.R, r1 = min(r0 + a.R, a.rows);
   double x0 = 0.0, x1 = 0.0;
+  // rows r0 + rl + rp * i, issued 8 at a time (independent loads in flight), summed in order
   if (a.mode == 1) {
     const float mu = gld(a.mean + (long)(r0 / a.gr) * C + c);
-    for (int r = r0 + rl; r < r1; r += rp) {
-      const long o = (long)r * C + c;
-      float g = gld(a.dY + o);
-      if (a.post) g = gld(a.post + o) > 0.f ? g : g * a.slope;
-      x0 += (double)g;
-      x1 += (double)(g * (gld(a.X + o) - mu));
+    for (int rb = r0 + rl; rb < r1; rb += 8 * rp) {
+      float g[8], xv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = min(rb + i * rp, r1 - 1);
+        const long o = (long)r * C + c;
+        g[i] = gld(a.dY + o);
+        if (a.post) g[i] = gld(a.post + o) > 0.f ? g[i] : g[i] * a.slope;
+        xv[i] = gld(a.X + o);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (rb + i * rp < r1) {
+          x0 += (double)g[i];
+          x1 += (double)(g[i] * (xv[i] - mu));
+        }
     }
   } else {
-    for (int r = r0 + rl; r < r1; r += rp) x0 += (double)gld(a.X + (long)r * C + c);
+    for (int rb = r0 + rl; rb < r1; rb += 8 * rp) {
+      float xv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) xv[i] = gld(a.X + (long)min(rb + i * rp, r1 - 1) * C + c);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (rb + i * rp < r1) x0 += (double)xv[i];
+    }
   }
   s0[threadIdx.x] = x0;
   s1[threadIdx.x] = x1;
@@ -569,9 +760,16 @@ __global__ __launch_bounds__(256) void cgl_chan_reduce(CglChanArgs a) {
     __syncthreads();
     const double mean = s0[c] / (r1 - r0);
     double m2 = 0.0;
-    for (int r = r0 + rl; r < r1; r += rp) {
-      const double d = (double)gld(a.X + (long)r * C + c) - mean;
-      m2 += d * d;
+    for (int rb = r0 + rl; rb < r1; rb += 8 * rp) {
+      float xv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) xv[i] = gld(a.X + (long)min(rb + i * rp, r1 - 1) * C + c);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (rb + i * rp < r1) {
+          const double d = (double)xv[i] - mean;
+          m2 += d * d;
+        }
     }
     __syncthreads();
     s1[threadIdx.x] = m2;
@@ -595,18 +793,28 @@ __global__ __launch_bounds__(256) void cgl_chan_reduce(CglChanArgs a) {
   }
 }
 
-// Column sums of X [rows][C] per chunk of R rows (any C): part[chunk][c][0] (double).
+// Column sums of X [rows][C] per chunk of R rows (any C): part[chunk][c][0] (double); 8 loads in
+// flight per thread, summed in row order.
 __global__ __launch_bounds__(256) void cgl_colsum_k(const float* X, int rows, int C, int R, double* part) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
   const int r0 = blockIdx.y * R, r1 = min(r0 + R, rows);
   double t = 0.0;
-  for (int r = r0; r < r1; ++r) t += (double)gld(X + (long)r * C + c);
+  for (int rb = r0; rb < r1; rb += 8) {
+    float xv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) xv[i] = gld(X + (long)min(rb + i, r1 - 1) * C + c);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (rb + i < r1) t += (double)xv[i];
+  }
   part[((long)blockIdx.y * C + c) * 2] = t;
   part[((long)blockIdx.y * C + c) * 2 + 1] = 0.0;
 }
 
-// BatchNorm2d finalize, one thread per channel, groups in the reference's call order.
+// BatchNorm2d finalize: ONE WAVE PER CHANNEL, lanes over the chunk partials (lane l takes chunks
+// l, l + 64, ... in order, then a fixed xor-tree across lanes: deterministic), groups in the
+// reference's call order.
 //   fwd (mode 0): mean / biased var per group from the chunk partials (Chan), save_mean / invstd,
 //                 scale = invstd * gamma, shift = beta - mean * scale, running stats (momentum,
 //                 unbiased variance) group by group; eval: the same from running stats.
@@ -622,39 +830,56 @@ struct CglBnFinArgs {
   float* dgamma; float* dbeta;              // bwd, or bias out (mode 2: dgamma)
 };
 
+__device__ __forceinline__ double cgl_wave_sum_d(double x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
 __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int C = a.C;
   if (c >= C) return;
+  const double* part = a.part;
   if (a.mode == 2) {
     double t = 0.0;
     const int nch = a.groups * a.chunks_per_group;
-    for (int q = 0; q < nch; ++q) t += a.part[((long)q * C + c) * 2];
-    gst(a.dgamma + c, (float)t);
+    for (int q = lane; q < nch; q += 64) t += part[((long)q * C + c) * 2];
+    t = cgl_wave_sum_d(t);
+    if (lane == 0) gst(a.dgamma + c, (float)t);
     return;
   }
   const float w = a.gamma ? gld(a.gamma + c) : 1.f;
+  const int cpg = a.chunks_per_group;
   if (a.mode == 1) {
     double dg = 0.0, db = 0.0;
     for (int g = 0; g < a.groups; ++g) {
       double S = 0.0, D = 0.0;
-      for (int q = 0; q < a.chunks_per_group; ++q) {
-        const long o = ((long)(g * a.chunks_per_group + q) * C + c) * 2;
-        S += a.part[o];
-        D += a.part[o + 1];
+      for (int q = lane; q < cpg; q += 64) {
+        const long o = ((long)(g * cpg + q) * C + c) * 2;
+        S += part[o];
+        D += part[o + 1];
       }
+      S = cgl_wave_sum_d(S);
+      D = cgl_wave_sum_d(D);
       const float invstd = gld(a.save_invstd + (long)g * C + c);
-      gst(a.coef0 + (long)g * C + c, (float)(S / a.gr));
-      gst(a.coef1 + (long)g * C + c, (float)D * invstd * invstd / a.gr);
+      if (lane == 0) {
+        gst(a.coef0 + (long)g * C + c, (float)(S / a.gr));
+        gst(a.coef1 + (long)g * C + c, (float)D * invstd * invstd / a.gr);
+      }
       dg += D * (double)invstd;
       db += S;
     }
-    if (a.dgamma) gst(a.dgamma + c, (float)dg);
-    if (a.dbeta) gst(a.dbeta + c, (float)db);
+    if (lane == 0) {
+      if (a.dgamma) gst(a.dgamma + c, (float)dg);
+      if (a.dbeta) gst(a.dbeta + c, (float)db);
+    }
     return;
   }
   const float b = a.beta ? gld(a.beta + c) : 0.f;
   if (!a.train) {
+    if (lane != 0) return;
     const double invstd = 1.0 / sqrt((double)gld(a.run_var + c) + a.eps);
     const float sc = (float)invstd * w;
     for (int g = 0; g < a.groups; ++g) {
@@ -666,23 +891,27 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
   float rm = a.run_mean ? gld(a.run_mean + c) : 0.f, rv = a.run_var ? gld(a.run_var + c) : 0.f;
   for (int g = 0; g < a.groups; ++g) {
     double s = 0.0;
-    for (int q = 0; q < a.chunks_per_group; ++q) s += a.part[((long)(g * a.chunks_per_group + q) * C + c) * 2];
+    for (int q = lane; q < cpg; q += 64) s += part[((long)(g * cpg + q) * C + c) * 2];
+    s = cgl_wave_sum_d(s);
     const double n = a.gr;
     const double mu = s / n;
     double m2 = 0.0;
-    for (int q = 0; q < a.chunks_per_group; ++q) {
-      const long o = ((long)(g * a.chunks_per_group + q) * C + c) * 2;
+    for (int q = lane; q < cpg; q += 64) {
+      const long o = ((long)(g * cpg + q) * C + c) * 2;
       const double cnt = a.R;
-      const double dd = a.part[o] / cnt - mu;
-      m2 += a.part[o + 1] + cnt * dd * dd;
+      const double dd = part[o] / cnt - mu;
+      m2 += part[o + 1] + cnt * dd * dd;
     }
+    m2 = cgl_wave_sum_d(m2);
     const double invstd = 1.0 / sqrt(m2 / n + a.eps);
     const float sc = (float)invstd * w;
-    gst(a.coef0 + (long)g * C + c, sc);
-    gst(a.coef1 + (long)g * C + c, b - (float)mu * sc);
-    if (a.save_mean) {
-      gst(a.save_mean + (long)g * C + c, (float)mu);
-      gst(a.save_invstd + (long)g * C + c, (float)invstd);
+    if (lane == 0) {
+      gst(a.coef0 + (long)g * C + c, sc);
+      gst(a.coef1 + (long)g * C + c, b - (float)mu * sc);
+      if (a.save_mean) {
+        gst(a.save_mean + (long)g * C + c, (float)mu);
+        gst(a.save_invstd + (long)g * C + c, (float)invstd);
+      }
     }
     if (a.run_mean) {
       const double mom = a.momentum;
@@ -690,7 +919,7 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
       rv = (float)(mom * (n > 1 ? m2 / (n - 1) : m2 / n) + (1.0 - mom) * (double)rv);
     }
   }
-  if (a.run_mean) {
+  if (a.run_mean && lane == 0) {
     gst(a.run_mean + c, rm);
     gst(a.run_var + c, rv);
   }
@@ -1059,12 +1288,31 @@ int bwd_probs(const ConvGeom& g, CglConvProb* P) {
 
 inline int64_t al256(int64_t b) { return (b + 255) & ~int64_t(255); }
 
-// MFMA tiling of a forward / input-gradient launch: 2x2 blocks per wave; waves along N when N > 64.
-struct ConvTiling { int TM, TN, WM, WN; };
+// MFMA tiling of a forward / input-gradient launch: (TM, TN) 32x32 blocks per wave, WM x WN waves
+// over the output tile, WK waves splitting K.  Large problems: 2x2 blocks, waves along N when
+// N > 64; problems that would give fewer than ~512 workgroups shrink the tile and split K inside
+// the workgroup (LDS reduction) so every CU gets work.
+struct ConvTiling { int TM, TN, WM, WN, WK; };
 ConvTiling conv_tiling(int N) {
-  if (N > 64) return {2, 2, 2, 2};      // 128 x 128
-  if (N > 32) return {2, 2, 4, 1};      // 256 x 64
-  return {2, 1, 4, 1};                  // 256 x 32
+  if (N > 64) return {2, 2, 2, 2, 1};      // 128 x 128
+  if (N > 32) return {2, 2, 4, 1, 1};      // 256 x 64
+  return {2, 1, 4, 1, 1};                  // 256 x 32
+}
+
+long conv_wgs(const CglConvProb* P, int np, const ConvTiling& t) {
+  long wg = 0;
+  for (int i = 0; i < np; ++i)
+    wg += (long)((P[i].M + 32 * t.TM * t.WM - 1) / (32 * t.TM * t.WM)) *
+          ((P[i].N + 32 * t.TN * t.WN - 1) / (32 * t.TN * t.WN));
+  return wg;
+}
+
+ConvTiling conv_tiling_for(const CglConvProb* P, int np) {
+  ConvTiling t = conv_tiling(P[0].N);
+  if (conv_wgs(P, np, t) >= 512) return t;
+  const ConvTiling mid = {2, P[0].N > 32 ? 2 : 1, 1, 1, 4};   // 64 x 64 (64 x 32), K split 4 ways
+  if (conv_wgs(P, np, mid) >= 512) return mid;
+  return {1, 1, 1, 1, 4};                                    // 32 x 32, K split 4 ways
 }
 
 int64_t packed_floats(const CglConvProb* P, int np) {
@@ -1083,10 +1331,17 @@ struct WgradPlan {
 // Weight-gradient plan: per-wave result tiles of (32 TM) x (32 TN) (rows = cout, cols = im2col
 // columns); pixel splits so that all problems together give ~4096 wave units, each covering >= 32
 // chunks of 16 pixels, with the partial tiles capped at 8M floats (32 MB).
+// the input-stationary one-output-channel weight gradient (cgl_conv_wgrad_n1t) applies
+bool wgrad_n1t_ok(const ConvGeom& g, const CglConvProb& P0) {
+  const int c4 = P0.Cin / 4;
+  return g.cout == 1 && g.stride == 1 && !g.up && P0.Cin % 4 == 0 && c4 >= 1 && c4 <= 64 && (c4 & (c4 - 1)) == 0 &&
+         P0.Ty * P0.Tx <= 16 && (256 / c4) * P0.Ty * P0.Tx * P0.Cin <= 16384;
+}
+
 WgradPlan wgrad_plan(const ConvGeom& g) {
   WgradPlan w;
   w.np = fwd_probs(g, w.P);
-  w.t = ConvTiling{g.cout > 32 ? 2 : 1, w.P[0].K > 32 ? 2 : 1, 1, 1};
+  w.t = ConvTiling{g.cout > 32 ? 2 : 1, w.P[0].K > 32 ? 2 : 1, 1, 1, 1};
   int tiles_total = 0;
   int64_t nk_total = 0;
   for (int i = 0; i < w.np; ++i) {
@@ -1096,13 +1351,15 @@ WgradPlan wgrad_plan(const ConvGeom& g) {
     tiles_total += P.tiles_m * P.tiles_n;
     nk_total += (int64_t)P.N * P.Kp;
   }
-  int s = std::max(1, 4096 / std::max(1, tiles_total));
+  int s = std::max(1, 2048 / std::max(1, tiles_total));
   s = (int)std::min<int64_t>(s, std::max<int64_t>(1, (8 << 20) / std::max<int64_t>(1, nk_total)));
   w.part_floats = 0;
   for (int i = 0; i < w.np; ++i) {
     CglConvProb& P = w.P[i];
     const int nchk = (P.M + 15) / 16;
-    P.splits = std::max(1, std::min(std::min(s, nchk / 32), 1024));
+    P.splits = std::max(1, std::min(std::min(s, nchk / 8), 1024));
+    if (g.cout == 1 && w.np == 1)   // vector kernels: >= 256 (input-stationary) / 32 pixels per split
+      P.splits = std::max(1, std::min(1024, P.M / (wgrad_n1t_ok(g, P) ? 256 : 32)));
     w.part_floats += al256((int64_t)P.splits * P.N * P.Kp * 4) / 4;
   }
   return w;
@@ -1113,7 +1370,7 @@ int64_t conv_ws_bytes(const ConvGeom& g) {
   int64_t a = packed_floats(P, fwd_probs(g, P));
   int64_t b = packed_floats(P, bwd_probs(g, P));
   WgradPlan w = wgrad_plan(g);
-  const int64_t bias_part = al256((int64_t)((g.n * g.ho * g.wo + 255) / 256) * g.cout * 16) / 4 + 64;
+  const int64_t bias_part = al256(((int64_t)g.n * g.ho * g.wo + 31) / 32 * g.cout * 16) / 4 + 64;
   return 4 * (std::max(a, b) + w.part_floats + 2 * bias_part) + 4096;
 }
 
@@ -1147,6 +1404,19 @@ int launch_pack(const float* W, const ConvGeom& g, int transpose, CglConvProb* P
   return (int)hipGetLastError();
 }
 
+// the vector one-output-channel kernel: Cin % 4 == 0, Cin / 4 a power of two (or a multiple of 64),
+// at most 16 (tap, float4-block) pairs per lane
+bool n1_ok(const CglConvProb* P, int np) {
+  for (int i = 0; i < np; ++i) {
+    const int c4 = P[i].Cin / 4;
+    if (P[i].Cin % 4 || c4 < 1) return false;
+    const int lanes = c4 < 64 ? c4 : 64;
+    if ((lanes & (lanes - 1)) || c4 % lanes) return false;
+    if (P[i].Ty * P[i].Tx * (c4 / lanes) > 16) return false;
+  }
+  return true;
+}
+
 int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float slope, const float* drop,
                     hipStream_t s) {
   const int N = P[0].N;
@@ -1157,19 +1427,23 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
   L.act = act;
   L.slope = slope;
   L.drop = drop;
-  if (N == 1) {
+  if (N == 1 && n1_ok(P, np)) {
     int wg = 0;
     for (int i = 0; i < np; ++i) {
+      const int c4 = P[i].Cin / 4, lanes = c4 < 64 ? c4 : 64;
+      const int per_wg = 4 * (64 / lanes) * 8;
       P[i].wg_begin = wg;
-      wg += (P[i].M + 255) / 256;
+      wg += (P[i].M + per_wg - 1) / per_wg;
       L.p[i] = P[i];
     }
     hipLaunchKernelGGL(cgl_conv_n1, dim3(wg), dim3(256), 0, s, L);
     return (int)hipGetLastError();
   }
-  const ConvTiling t = conv_tiling(N);
+  const ConvTiling t = conv_tiling_for(P, np);
   L.WM = t.WM;
   L.WN = t.WN;
+  L.WK = t.WK;
+  const int lds = t.WK > 1 ? (t.WK - 1) * t.WM * t.WN * t.TM * t.TN * 16 * 64 * 4 : 0;
   bool fast = true;
   int wg = 0;
   for (int i = 0; i < np; ++i) {
@@ -1180,19 +1454,22 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
     fast = fast && (P[i].Cin % 16 == 0);
     L.p[i] = P[i];
   }
-  if (t.TN == 2) {
-    if (fast) hipLaunchKernelGGL((cgl_conv_fwd<2, 2, true>), dim3(wg), dim3(256), 0, s, L);
-    else hipLaunchKernelGGL((cgl_conv_fwd<2, 2, false>), dim3(wg), dim3(256), 0, s, L);
+  if (t.TM == 2 && t.TN == 2) {
+    if (fast) hipLaunchKernelGGL((cgl_conv_fwd<2, 2, true>), dim3(wg), dim3(256), lds, s, L);
+    else hipLaunchKernelGGL((cgl_conv_fwd<2, 2, false>), dim3(wg), dim3(256), lds, s, L);
+  } else if (t.TM == 2) {
+    if (fast) hipLaunchKernelGGL((cgl_conv_fwd<2, 1, true>), dim3(wg), dim3(256), lds, s, L);
+    else hipLaunchKernelGGL((cgl_conv_fwd<2, 1, false>), dim3(wg), dim3(256), lds, s, L);
   } else {
-    if (fast) hipLaunchKernelGGL((cgl_conv_fwd<2, 1, true>), dim3(wg), dim3(256), 0, s, L);
-    else hipLaunchKernelGGL((cgl_conv_fwd<2, 1, false>), dim3(wg), dim3(256), 0, s, L);
+    if (fast) hipLaunchKernelGGL((cgl_conv_fwd<1, 1, true>), dim3(wg), dim3(256), lds, s, L);
+    else hipLaunchKernelGGL((cgl_conv_fwd<1, 1, false>), dim3(wg), dim3(256), lds, s, L);
   }
   return (int)hipGetLastError();
 }
 
 
 int chan_chunk(int64_t gr) {
-  int R = 256;
+  int R = 64;
   while (R > 1 && gr % R != 0) R >>= 1;
   return R;
 }
@@ -1202,13 +1479,23 @@ bool pow2_le256(int C) { return C >= 1 && C <= 256 && (C & (C - 1)) == 0; }
 // per-column sum of X [rows][C] into out[C] (bias gradient): chunk partials (double), then a
 // fixed-order sum over chunks (cgl_bn_finalize mode 2)
 int col_sum(const float* X, int64_t rows, int C, double* part, float* out, hipStream_t s) {
-  const int R = 256;
-  const int nch = (int)((rows + R - 1) / R);
-  hipLaunchKernelGGL(cgl_colsum_k, dim3((C + 255) / 256, nch), dim3(256), 0, s, X, (int)rows, C, R, part);
+  int nch;
+  if (pow2_le256(C)) {
+    const int R = 64;
+    nch = (int)((rows + R - 1) / R);
+    CglChanArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.X = X; a.rows = (int)rows; a.C = C; a.R = R; a.mode = 2; a.gr = (int)rows; a.part = part;
+    hipLaunchKernelGGL(cgl_chan_reduce, dim3(nch), dim3(256), 0, s, a);
+  } else {
+    const int R = 32;
+    nch = (int)((rows + R - 1) / R);
+    hipLaunchKernelGGL(cgl_colsum_k, dim3((C + 255) / 256, nch), dim3(256), 0, s, X, (int)rows, C, R, part);
+  }
   CglBnFinArgs f;
   std::memset(&f, 0, sizeof(f));
   f.part = part; f.C = C; f.groups = 1; f.chunks_per_group = nch; f.mode = 2; f.dgamma = out;
-  hipLaunchKernelGGL(cgl_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, s, f);
+  hipLaunchKernelGGL(cgl_bn_finalize, dim3((C + 3) / 4), dim3(256), 0, s, f);
   return (int)hipGetLastError();
 }
 
@@ -1220,8 +1507,7 @@ int conv_fwd_impl(const ConvGeom& g, const float* X, const float* W, const float
                   const float* drop, void* ws, int64_t wsb, hipStream_t s) {
   if (!X || !W || !Y || !ws || act < 0 || act > 3 || !al16(ws)) return CGL_E_ARG;
   if (wsb < conv_ws_bytes(g)) return CGL_E_SIZE;
-  if ((g.cin % 16 == 0 || g.cout == 1) && !al16(X)) return CGL_E_ARG;
-  if (g.cout == 1 && g.cin % 4 != 0) return CGL_E_ARG;
+  if ((g.cin % 4 == 0) && !al16(X)) return CGL_E_ARG;
   CglConvProb P[CGL_CONV_MAXP];
   const int np = fwd_probs(g, P);
   for (int i = 0; i < np; ++i) {
@@ -1237,8 +1523,7 @@ int conv_bwd_data_impl(const ConvGeom& g, const float* dY, const float* W, float
                        hipStream_t s) {
   if (!dY || !W || !dX || !ws || !al16(ws)) return CGL_E_ARG;
   if (wsb < conv_ws_bytes(g)) return CGL_E_SIZE;
-  if ((g.cout % 16 == 0 || g.cin == 1) && !al16(dY)) return CGL_E_ARG;
-  if (g.cin == 1 && g.cout % 4 != 0) return CGL_E_ARG;
+  if ((g.cout % 4 == 0) && !al16(dY)) return CGL_E_ARG;
   CglConvProb P[CGL_CONV_MAXP];
   const int np = bwd_probs(g, P);
   for (int i = 0; i < np; ++i) {
@@ -1260,7 +1545,10 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
   L.np = pl.np;
   L.WM = 1;
   L.WN = 1;
+  L.WK = 1;
   float* part = (float*)ws;
+  const bool valu = g.cout == 1 && pl.np == 1;   // cgl_conv_wgrad_n1 (splits set by wgrad_plan)
+  const bool n1t = valu && wgrad_n1t_ok(g, pl.P[0]);
   int wg = 0;
   CglWgradReduceArgs r;
   std::memset(&r, 0, sizeof(r));
@@ -1285,14 +1573,23 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
     r.Ty[i] = P.Ty;
     for (int k = 0; k < 4; ++k) { r.ym[i][k] = P.ym[k]; r.xm[i][k] = P.xm[k]; }
   }
-  if (pl.t.TM == 2 && pl.t.TN == 2) hipLaunchKernelGGL((cgl_conv_wgrad<2, 2>), dim3(wg), dim3(256), 0, s, L);
+  if (n1t)
+    hipLaunchKernelGGL(cgl_conv_wgrad_n1t, dim3(pl.P[0].splits), dim3(256), 0, s, L);
+  else if (valu)
+    hipLaunchKernelGGL(cgl_conv_wgrad_n1, dim3((pl.P[0].K + 255) / 256, pl.P[0].splits), dim3(256), 0, s, L);
+  else if (pl.t.TM == 2 && pl.t.TN == 2) hipLaunchKernelGGL((cgl_conv_wgrad<2, 2>), dim3(wg), dim3(256), 0, s, L);
   else if (pl.t.TN == 2) hipLaunchKernelGGL((cgl_conv_wgrad<1, 2>), dim3(wg), dim3(256), 0, s, L);
   else if (pl.t.TM == 2) hipLaunchKernelGGL((cgl_conv_wgrad<2, 1>), dim3(wg), dim3(256), 0, s, L);
   else hipLaunchKernelGGL((cgl_conv_wgrad<1, 1>), dim3(wg), dim3(256), 0, s, L);
   int rc;
   if ((rc = (int)hipGetLastError())) return rc;
   const long nred = (long)g.cout * g.ks * g.ks * g.cin;
-  hipLaunchKernelGGL(cgl_conv_wgrad_reduce, dim3((unsigned)((nred + 255) / 256)), dim3(256), 0, s, r);
+  // elements per block: >= ~512 blocks when possible; the rest of the block's threads split the splits
+  int EB = 64;
+  while (EB > 4 && (nred + EB - 1) / EB < 512) EB >>= 1;
+  r.EB = EB;
+  r.SG = 256 / EB;
+  hipLaunchKernelGGL(cgl_conv_wgrad_reduce, dim3((unsigned)((nred + EB - 1) / EB)), dim3(256), 0, s, r);
   if ((rc = (int)hipGetLastError())) return rc;
   if (db) {
     double* bp = (double*)(((uintptr_t)part + 255) & ~(uintptr_t)255);
@@ -1409,7 +1706,7 @@ int cgl_bn2d_fwd(const float* X, int n, int hw, int C, int groups, const float* 
   f.mode = 0; f.train = train; f.gamma = gamma; f.beta = beta; f.eps = eps; f.momentum = momentum;
   f.run_mean = running_mean; f.run_var = running_var; f.save_mean = save_mean; f.save_invstd = save_invstd;
   f.coef0 = c0; f.coef1 = c1;
-  hipLaunchKernelGGL(cgl_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, s, f);
+  hipLaunchKernelGGL(cgl_bn_finalize, dim3((C + 3) / 4), dim3(256), 0, s, f);
   CglEltArgs e;
   std::memset(&e, 0, sizeof(e));
   e.mode = 0; e.rows = (int)rows; e.C = C; e.gr = (int)gr; e.hw = hw; e.act = act; e.slope = slope;
@@ -1447,7 +1744,7 @@ int cgl_bn2d_bwd(const float* dY, const float* post, const float* X, int n, int 
   f.part = part; f.C = C; f.groups = groups; f.chunks_per_group = (int)(gr / R); f.R = R; f.gr = (int)gr;
   f.mode = 1; f.gamma = gamma; f.save_invstd = const_cast<float*>(save_invstd); f.coef0 = c0; f.coef1 = c1;
   f.dgamma = dgamma; f.dbeta = dbeta;
-  hipLaunchKernelGGL(cgl_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, s, f);
+  hipLaunchKernelGGL(cgl_bn_finalize, dim3((C + 3) / 4), dim3(256), 0, s, f);
   CglEltArgs e;
   std::memset(&e, 0, sizeof(e));
   e.mode = 1; e.rows = (int)rows; e.C = C; e.gr = (int)gr; e.hw = hw; e.slope = slope;
