@@ -327,6 +327,7 @@ __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local)
   const float* __restrict__ dY = P->Y;
   const int ldy = P->ldy, YH = P->YH, YW = P->YW;
   const int osy = P->osy, osx = P->osx, ooy = P->ooy, oox = P->oox, isy = P->isy, isx = P->isx;
+  const int OH = P->OH, OW = P->OW;
 
   int rch[TM];
 #pragma unroll
@@ -356,12 +357,23 @@ __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local)
   // masks: bit q (A, pixel valid), bit 8 + j * 8 + q (B, tap in bounds)
   auto load = [&](int c, float (&A)[TM][8], float (&B)[TN][8], int& okm) {
     okm = 0;
+    // decode the first pixel of this lane half once, then step along the row (wrapping)
+    int img, oy, ox;
+    cgl_conv_pix(P, min(c * 16 + 8 * lh, M - 1), img, oy, ox);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int m = c * 16 + 8 * lh + q;
       const bool mv = m < M;
-      int img, oy, ox;
-      cgl_conv_pix(P, min(m, M - 1), img, oy, ox);
+      if (q > 0) {
+        if (++ox == OW) {
+          ox = 0;
+          if (++oy == OH) {
+            oy = 0;
+            ++img;
+          }
+        }
+        if (!mv) { img = 0; oy = 0; ox = 0; }
+      }
       const long ya = (((long)img * YH + oy * osy + ooy) * YW + ox * osx + oox) * ldy;
 #pragma unroll
       for (int i = 0; i < TM; ++i) A[i][q] = ((gcfp)dY)[ya + rch[i]];
@@ -510,6 +522,71 @@ __global__ __launch_bounds__(256) void cgl_conv_n1(CglConvLaunch args) {
       else if (L->act == CGL_EPI_ACT_SIGMOID) y = 1.f / (1.f + expf(-y));
       if (L->drop) y *= gld(L->drop + (long)img * P->ldy);
       gst(P->Y + (((long)img * P->YH + oy * P->osy + P->ooy) * P->YW + ox * P->osx + P->oox) * P->ldy, y);
+    }
+  }
+}
+
+// LDS-tiled variant for a stride-1 3x3 one-output-channel convolution (Conv2d(64, 1, 3, 1, 1) +
+// Tanh, model/lsgan.py:19-20): a workgroup stages the (TH + 2) x (W + 2) input halo of TH output
+// rows of one image in LDS (coalesced 16-byte loads, zero padding written explicitly), so every
+// input pixel is read from memory once per tile instead of once per tap; then L = Cin / 4 lanes per
+// output pixel read their channel slice of the 9 taps from LDS and combine by an xor tree.
+#define CGL_N1T_TH 4
+__global__ __launch_bounds__(256) void cgl_conv_n1_tile(CglConvLaunch args) {
+  (void)args;
+  extern __shared__ float cgl_conv_lds[];
+  CglKL L = cgl_conv_args();
+  CglKP P = &L->p[0];
+  const int Cin = P->Cin, W = P->OW, H = P->OH;
+  const int c4 = Cin >> 2, lanes = c4;          // c4 <= 64, power of two
+  const int tiles_y = (H + CGL_N1T_TH - 1) / CGL_N1T_TH;
+  const int img = blockIdx.x / tiles_y, y0 = (blockIdx.x - img * tiles_y) * CGL_N1T_TH;
+  const int HR = CGL_N1T_TH + 2, WR = W + 2;
+  const float* __restrict__ X = P->X + (long)img * P->XH * P->XW * Cin;
+  // stage rows y0-1 .. y0+TH, cols -1 .. W (zero outside the image)
+  const int tot4 = HR * WR * c4;
+  for (int e = threadIdx.x; e < tot4; e += 256) {
+    const int q = e % c4, pix = e / c4;
+    const int ry = pix / WR, rx = pix - ry * WR;
+    const int iy = y0 - 1 + ry, ix = rx - 1;
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if ((unsigned)iy < (unsigned)P->XH && (unsigned)ix < (unsigned)P->XW)
+      v = *(gcf4p)(X + ((long)iy * P->XW + ix) * Cin + 4 * q);
+    *(f32x4*)&cgl_conv_lds[(long)pix * Cin + 4 * q] = v;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int q = lane & (lanes - 1);
+  const int slot = threadIdx.x / lanes, nslot = 256 / lanes;
+  f32x4 w[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) w[t] = *(gcf4p)(P->Wp + t * Cin + 4 * q);
+  const float bias = L->bias ? gld(L->bias) : 0.f;
+  const int npix = CGL_N1T_TH * W;
+  const int iters = (npix + nslot - 1) / nslot;   // uniform across the workgroup (xor tree below)
+  for (int it = 0; it < iters; ++it) {
+    const int pp = it * nslot + slot;
+    const bool valid = pp < npix;
+    const int p = valid ? pp : npix - 1;
+    const int ty = p / W, tx = p - ty * W;
+    float acc = 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ky = t / 3, kx = t - 3 * ky;
+      const f32x4 v = *(const f32x4*)&cgl_conv_lds[((long)(ty + ky) * WR + tx + kx) * Cin + 4 * q];
+      acc = fmaf(v[0], w[t][0], acc);
+      acc = fmaf(v[1], w[t][1], acc);
+      acc = fmaf(v[2], w[t][2], acc);
+      acc = fmaf(v[3], w[t][3], acc);
+    }
+    for (int o = 1; o < lanes; o <<= 1) acc += __shfl_xor(acc, o);
+    if (valid && q == 0 && y0 + ty < H) {
+      float yv = acc + bias;
+      if (L->act == CGL_EPI_ACT_LEAKY) yv = yv > 0.f ? yv : yv * L->slope;
+      else if (L->act == CGL_EPI_ACT_TANH) yv = tanhf(yv);
+      else if (L->act == CGL_EPI_ACT_SIGMOID) yv = 1.f / (1.f + expf(-yv));
+      if (L->drop) yv *= gld(L->drop + (long)img * P->ldy);
+      gst(P->Y + (((long)img * P->YH + y0 + ty) * P->YW + tx) * P->ldy, yv);
     }
   }
 }
@@ -1427,6 +1504,17 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
   L.act = act;
   L.slope = slope;
   L.drop = drop;
+  if (N == 1 && np == 1 && P[0].Ty == 3 && P[0].Tx == 3 && P[0].isy == 1 && P[0].isx == 1 && P[0].ish == 0 &&
+      P[0].osy == 1 && P[0].osx == 1 && P[0].dy[0] == -1 && P[0].dx[0] == -1 && P[0].Cin % 4 == 0 &&
+      P[0].Cin <= 256 && ((P[0].Cin / 4) & (P[0].Cin / 4 - 1)) == 0 && P[0].XH == P[0].OH && P[0].XW == P[0].OW &&
+      (CGL_N1T_TH + 2) * (P[0].OW + 2) * P[0].Cin * 4 <= 65536) {
+    const int tiles_y = (P[0].OH + CGL_N1T_TH - 1) / CGL_N1T_TH;
+    const int nimg = P[0].M / (P[0].OH * P[0].OW);
+    L.p[0] = P[0];
+    const int lds = (CGL_N1T_TH + 2) * (P[0].OW + 2) * P[0].Cin * 4;
+    hipLaunchKernelGGL(cgl_conv_n1_tile, dim3(nimg * tiles_y), dim3(256), lds, s, L);
+    return (int)hipGetLastError();
+  }
   if (N == 1 && n1_ok(P, np)) {
     int wg = 0;
     for (int i = 0; i < np; ++i) {
