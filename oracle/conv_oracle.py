@@ -121,6 +121,33 @@ def d_forward(P, Bf, img, masks=None, train=True):
     return F.linear(out, P["adv_layer.weight"], P["adv_layer.bias"])
 
 
+MIX_TRUNK_SPEC = [("model.0.0", "linear", (128 * 8 * 8, 100)), ("model.3", "conv", (128, 128)), ("model.4", "bn", 128),
+                  ("model.7", "conv", (64, 128))]
+
+
+def mix_head_spec(h):
+    """One head of model/lsgan.py:53-60: BatchNorm2d(64, 0.8), LeakyReLU, Conv2d(64, 1), Tanh."""
+    return [(f"paths.{h}.0", "bn", 64), (f"paths.{h}.2", "conv", (1, 64))]
+
+
+def mixg_forward(P, Bf, z, n_heads, train=True):
+    """MixGenerator.forward as model/lsgan.py:63-70 intends it (the reference's own forward raises at
+    :68, ``self.img_shape`` unset -- parity unpinned by the reference): trunk once, every head on the
+    same hidden tensor, heads concatenated on the batch dimension."""
+    out = F.linear(z, P["model.0.0.weight"], P["model.0.0.bias"])
+    x = out.view(out.shape[0], 128, 8, 8)
+    x = F.interpolate(x, scale_factor=2, mode="nearest")
+    x = F.conv2d(x, P["model.3.weight"], P["model.3.bias"], 1, 1)
+    x = F.leaky_relu(_bn(x, P, Bf, "model.4", train), SLOPE)
+    x = F.interpolate(x, scale_factor=2, mode="nearest")
+    hidden = F.conv2d(x, P["model.7.weight"], P["model.7.bias"], 1, 1)
+    imgs = []
+    for h in range(n_heads):
+        y = F.leaky_relu(_bn(hidden, P, Bf, f"paths.{h}.0", train), SLOPE)
+        imgs.append(torch.tanh(F.conv2d(y, P[f"paths.{h}.2.weight"], P[f"paths.{h}.2.bias"], 1, 1)))
+    return torch.cat(imgs, dim=0)
+
+
 def adv_loss(v, target, kind):
     """LSGAN MSELoss (kind "mse") or nn.Sigmoid + nn.BCELoss (kind "bce") on the D logit."""
     t = torch.full_like(v, float(target))
@@ -168,5 +195,5 @@ class ConvGan:
         g_grads = OrderedDict((k, p.grad.detach().clone()) for k, p in self.gp.items())
         self.lam = self.lam + LAMBDA_LR * LAMBDA_REG   # SGD on Lambda: dF/dLambda = -0.001
         self.opt_g.step()
-        return dict(Xd=Xd.detach(), Xg=Xg.detach(), d_loss=float(d_loss), d_real=float(real_loss),
-                    d_fake=float(fake_loss), g_loss=float(g_loss), d_grads=d_grads, g_grads=g_grads)
+        return dict(Xd=Xd.detach(), Xg=Xg.detach(), d_loss=float(d_loss.detach()), d_real=float(real_loss.detach()),
+                    d_fake=float(fake_loss.detach()), g_loss=float(g_loss.detach()), d_grads=d_grads, g_grads=g_grads)

@@ -47,6 +47,7 @@ md_model = _load("MDGAN/MNIST/mnist_model.py", "ref_mdgan_model")
 ring_model = _load("CGLGAN/2DMG/model.py", "ref_ring_model")
 
 IMS = (1, 28, 28)
+lsgan_model = _load("model/lsgan.py", "ref_lsgan_model")
 
 
 def sha(t):
@@ -294,6 +295,87 @@ def ring_run(B, steps, n_points_per_class=2000):
             "final_D": summarize(net_d.state_dict(), full=True)}
 
 
+# --------------------------------------------------------------------------------------------
+# model/lsgan.py conv GAN: module structure, forward / backward, and a CAPGAN-shaped round
+# (capgan.py:211-262 + 316-349 restated with the conv models and an LSGAN MSE or Sigmoid+BCE
+# objective; the reference never trains these models).  Dropout2d draws from the
+# global torch RNG exactly as in the reference module (torch.manual_seed before the round).
+# --------------------------------------------------------------------------------------------
+def lsgan_fixtures():
+    out = {}
+    torch.manual_seed(SEED)
+    g = lsgan_model.Generator(None)
+    d = lsgan_model.Discriminator(None)
+    out["keys_G"] = [[k, list(v.shape)] for k, v in g.state_dict().items()]
+    out["keys_D"] = [[k, list(v.shape)] for k, v in d.state_dict().items()]
+    out["init_G"] = summarize(g.state_dict())
+    out["init_D"] = summarize(d.state_dict())
+    # forward / backward at B=4 (train mode), full tensors
+    gen = torch.Generator().manual_seed(77)
+    z = torch.randn(4, 100, generator=gen)
+    img = g(z)
+    dy = torch.randn(img.shape, generator=gen)
+    (img * dy).sum().backward()
+    out["g_fwd"] = {"z_seed": 77, "img": summarize({"img": img.detach()}, full=True)["img"],
+                    "grads": summarize({k: p.grad for k, p in g.named_parameters()}),
+                    "running": summarize({k: v for k, v in g.state_dict().items() if "running" in k}, full=True)}
+    torch.manual_seed(1234)
+    real = torch.rand(4, 1, 32, 32, generator=gen) * 2 - 1
+    v = d(real)
+    (v.sum()).backward()
+    out["d_fwd"] = {"rng_seed": 1234, "v": [float(x) for x in v.detach().flatten().tolist()],
+                    "grads": summarize({k: p.grad for k, p in d.named_parameters()})}
+    g.eval()
+    with torch.no_grad():
+        out["g_eval"] = summarize({"img": g(z)}, full=True)["img"]
+    # 3 CAPGAN rounds (N = 1), B = 8, per objective
+    for kind in ("mse", "bce"):
+        torch.manual_seed(SEED)
+        net_g = lsgan_model.Generator(None)
+        net_d = lsgan_model.Discriminator(None)
+        opti_g = optim.Adam(net_g.parameters(), lr=0.0002, betas=(0.5, 0.999))
+        opti_d = optim.Adam(net_d.parameters(), lr=0.0002, betas=(0.5, 0.999))
+        Lambda = torch.tensor(0., requires_grad=True)
+        opti_L = optim.SGD([Lambda], lr=0.1)
+        crit = nn.MSELoss() if kind == "mse" else nn.BCELoss()
+        post = (lambda x: x) if kind == "mse" else torch.sigmoid
+        half = 0.5 if kind == "mse" else 1.0
+        rec = {"d_loss": [], "g_loss": [], "lambda": []}
+        for step in range(3):
+            gg = torch.Generator().manual_seed(4000 + step)
+            z1 = torch.randn(8, 100, generator=gg)
+            z2 = torch.randn(8, 100, generator=gg)
+            real = torch.rand(8, 1, 32, 32, generator=gg) * 2 - 1
+            torch.manual_seed(5000 + step)    # Dropout2d stream of this round's three D calls
+            with torch.no_grad():
+                Xd = net_g(z1)
+            z2.requires_grad_(True)
+            Xg = net_g(z2)
+            opti_d.zero_grad()
+            real_loss = crit(post(net_d(real)), torch.ones(8, 1))
+            fake_loss = crit(post(net_d(Xd.detach())), torch.zeros(8, 1))
+            D_loss = (real_loss + fake_loss) * half
+            D_loss.backward()
+            opti_d.step()
+            opti_g.zero_grad()
+            loss = torch.zeros(1)
+            loss[0] = crit(post(net_d(Xg.clone())), torch.ones(8, 1)).clone()
+            opti_L.zero_grad()
+            alpha = F.softmax(Lambda.detach() * loss.detach(), dim=0)
+            alpha = F.softmax(alpha * torch.tensor([1.0]), dim=0)
+            F_max = (alpha * loss).sum() - 0.001 * Lambda
+            F_max.backward()
+            opti_L.step()
+            opti_g.step()
+            rec["d_loss"].append(float(D_loss.item()))
+            rec["g_loss"].append(float(loss[0].item()))
+            rec["lambda"].append(float(Lambda.item()))
+        out[f"round_{kind}"] = {"trajectory": rec, "final_G": summarize(net_g.state_dict()),
+                                "final_D": summarize(net_d.state_dict()),
+                                "config": {"B": 8, "steps": 3, "input_seed0": 4000, "rng_seed0": 5000}}
+    return out
+
+
 def init_hashes():
     """Initial-parameter recipe pins (torch.manual_seed(SEED); Generator; Discriminator)."""
     torch.manual_seed(SEED)
@@ -318,6 +400,7 @@ def main():
         "mixg_b64_n2": mixg_run(64, 2, 3, beta_sizes=[300, 100]),
         "mixg_b64_n2_double": mixg_run(64, 2, 2, beta_sizes=[300, 100], double_softmax=True),
         "ring_b64": ring_run(64, 10),
+        "lsgan": lsgan_fixtures(),
     }
     meta = {"torch": torch.__version__, "threads": torch.get_num_threads(), "seed": SEED,
             "generator": "tests/golden/make_golden.py"}
