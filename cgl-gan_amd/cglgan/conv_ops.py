@@ -187,3 +187,15 @@ def adam_multi(params, grads, ms, vs, step, lr=2e-4, betas=(0.5, 0.999), eps=1e-
         ns = (ctypes.c_int64 * nt)(*[t.numel() for t in ps])
         C.check(C.lib.cgl_adam_multi(nt, arr(ps), arr(gs), arr(mm), arr(vv), ns, int(step), float(lr), float(betas[0]),
                                      float(betas[1]), float(eps), _s()), "cgl_adam_multi")
+
+
+WEIGHTING = {"capgan": 0, "mean": 1, "mix_single": 2, "mix_double": 3, "cglgan": 4}
+
+
+def weights_scale(weighting, lam, beta, losses, rank, x=None, alpha_out=None):
+    """alpha = the reference's lambda-weighting of the gathered losses; x *= alpha[rank] in place."""
+    _chk(losses, x, alpha_out)
+    n = losses.numel()
+    arr = (ctypes.c_float * n)(*[float(b) for b in beta])
+    C.check(C.lib.cgl_weights_scale(WEIGHTING[weighting], n, rank, float(lam), arr, _p(losses), _p(x),
+                                    x.numel() if x is not None else 0, _p(alpha_out), _s()), "cgl_weights_scale")

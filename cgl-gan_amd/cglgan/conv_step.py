@@ -25,6 +25,7 @@ from __future__ import annotations
 import math
 from collections import OrderedDict
 
+import numpy as np
 import torch
 
 from . import _lib as C
@@ -325,13 +326,15 @@ class ConvGanStep:
         """Replicated G backward from the (exchanged) image gradient, lambda SGD, Adam G (capgan.py:258-260)."""
         self._g_backward()
         self.G.adam(self.lr, self.betas, self.eps)
-        self.lam += 0.1 * 0.001   # optim.SGD([Lambda], lr=0.1) with dF/dLambda = -0.001 (capgan.py:249,259)
+        # optim.SGD([Lambda], lr=0.1) with dF/dLambda = -0.001 (capgan.py:249,259), in the fp32
+        # arithmetic of the reference's 0-d tensor (the MLP path's cgl_adam tail does the same)
+        self.lam = float(np.float32(self.lam) + np.float32(-0.1) * np.float32(-0.001))
         self.round += 1
 
     def run(self, real=None):
         """One round with N = 1 (alpha = 1 exactly, capgan.py:247-248)."""
         if self.n_workers != 1:
-            raise RuntimeError("n_workers > 1: use cglgan.exchange.ConvExchange")
+            raise RuntimeError("n_workers > 1: use cglgan.exchange.ConvWorkerExchange")
         self.phase_a(real)
         self.phase_b()
 

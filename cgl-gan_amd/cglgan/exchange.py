@@ -16,12 +16,17 @@ round's queue traffic becomes collectives:
     (mixed-gan.py:104-124, 193-200; the reference's load of it is a no-op, SURVEY F4, kept
     reproducible with ``fedavg_compat_noop``).
   E-share (new behaviour): mean of the D parameters every E rounds.
+  D-swap (MD-GAN, MDGAN/MNIST/mdgan.py:158-164, 258-262 -- commented out in the reference, parity
+    unpinned): every E rounds the server shuffles the N discriminators with Random(server + 100) and
+    worker i continues with D_{perm[i]}; here one point-to-point send/recv pair per rank over RCCL.
 
 ``DistComm`` wraps torch.distributed (backend "nccl" = RCCL over xGMI on MI355X, "gloo" on
 CPU); ``LocalComm`` runs N workers of one process in lockstep (single-GPU rehearsal and
 tests).  Both expose the same three collectives, so ``WorkerExchange`` is written once.
 """
 from __future__ import annotations
+
+import random
 
 import torch
 import torch.distributed as dist
@@ -52,6 +57,38 @@ class DistComm:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
             t.div_(self.size)
 
+    def swap(self, tensors, perm):
+        """tensors <- the same tensors of rank perm[rank] (one isend / irecv pair per tensor)."""
+        src, dst = perm[self.rank], perm.index(self.rank)
+        if src == self.rank:
+            return
+        bufs = [torch.empty_like(t) for t in tensors]
+        g = lambda r: dist.get_global_rank(self.group, r) if self.group is not None else r
+        ops = []
+        for t, b in zip(tensors, bufs):
+            ops.append(dist.P2POp(dist.isend, t.contiguous(), g(dst), self.group))
+            ops.append(dist.P2POp(dist.irecv, b, g(src), self.group))
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        for t, b in zip(tensors, bufs):
+            t.copy_(b)
+
+
+class DSwap:
+    """The MD-GAN server's D shuffle (MDGAN/MNIST/mdgan.py:122-123,158-164): Random() seeded with
+    server_rank + 100, ``shuffle`` of the N workers' discriminators; worker i receives D_{perm[i]}.
+    Every rank holds the same seeded generator, so all ranks agree on perm without communication."""
+
+    def __init__(self, n, server_rank=0):
+        self.n = n
+        self.rd = random.Random()
+        self.rd.seed(server_rank + 100)
+
+    def next_perm(self):
+        p = list(range(self.n))
+        self.rd.shuffle(p)
+        return p
+
 
 class WorkerExchange:
     """One worker's communication round (phase A -> collectives -> phase B).
@@ -62,10 +99,12 @@ class WorkerExchange:
     """
 
     def __init__(self, step, comm=None, share_every: int = 0, cloud=None, cloud_every: int = 0,
-                 cloud_weights=None, fedavg_compat_noop: bool = False):
+                 cloud_weights=None, fedavg_compat_noop: bool = False, swap_every: int = 0):
         self.step = step
         self.comm = comm
         self.share_every = share_every
+        self.swap_every = swap_every
+        self.dswap = DSwap(comm.size) if (comm is not None and swap_every > 0) else None
         self.cloud, self.cloud_every = cloud, cloud_every
         self.cloud_weights = cloud_weights
         self.fedavg_compat_noop = fedavg_compat_noop
@@ -85,6 +124,8 @@ class WorkerExchange:
             s.run(C.PHASE_B, graph=graph)
         if self.comm is not None and self.share_every > 0 and (r + 1) % self.share_every == 0:
             self.comm.all_reduce_mean(s.d_params)
+        if self.dswap is not None and (r + 1) % self.swap_every == 0:
+            self.comm.swap([s.d_params], self.dswap.next_perm())
         if self.cloud is not None and self.cloud_every > 0 and (r + 1) % self.cloud_every == 0:
             self.cloud_average()
 
@@ -136,3 +177,38 @@ class LocalComm:
             tot /= self.size
             for s in ss:
                 s.d_params.copy_(tot)
+
+
+class ConvWorkerExchange:
+    """The same round for the conv GAN (cglgan.conv_step.ConvGanStep, model/lsgan.py): the exchange
+    tensor is the image gradient dl/dXg [B, 32, 32, 1]; E-share averages D's parameters and its
+    BatchNorm running statistics; D-swap moves both (the reference's copy_parameters keeps every
+    non-scalar state-dict entry, MDGAN/MNIST/mdgan.py:233-238)."""
+
+    def __init__(self, step, comm=None, share_every: int = 0, swap_every: int = 0):
+        self.step, self.comm = step, comm
+        self.share_every, self.swap_every = share_every, swap_every
+        n = comm.size if comm is not None else 1
+        if n != step.n_workers:
+            raise ValueError(f"step planned for {step.n_workers} workers, group has {n}")
+        self.dswap = DSwap(n) if (comm is not None and swap_every > 0) else None
+
+    def _d_state(self):
+        return [self.step.D.p] + list(self.step.D.running.values())
+
+    def round(self, r: int, real=None):
+        from . import conv_ops as O
+        s = self.step
+        if self.comm is None or self.comm.size == 1:
+            s.run(real)
+        else:
+            s.phase_a(real)
+            self.comm.all_gather(s.losses_all, s.lbuf[2:3])
+            O.weights_scale(s.weighting, s.lam, s.beta, s.losses_all, s.rank, s.dimg)
+            self.comm.all_reduce_sum(s.dimg)
+            s.phase_b()
+        if self.comm is not None and self.share_every > 0 and (r + 1) % self.share_every == 0:
+            for t in self._d_state():
+                self.comm.all_reduce_mean(t)
+        if self.dswap is not None and (r + 1) % self.swap_every == 0:
+            self.comm.swap(self._d_state(), self.dswap.next_perm())

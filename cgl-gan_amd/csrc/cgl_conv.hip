@@ -1227,6 +1227,34 @@ __global__ __launch_bounds__(256) void cgl_gather_rows_k(const float* src, const
   }
 }
 
+// lambda-weighting of the gathered worker losses (cgl_weights of cgl_kernels.hip: capgan.py:247-248,
+// mixed-gan.py:276, MDGAN/MNIST/mdgan.py:203, CGLGAN/2DMG/main.py:261-264) and scaling of this
+// worker's exchange gradient by its alpha, before the all-reduce(sum) of the exchange.
+struct CglWeightsArgs {
+  int mode, n, rank;
+  float lam;
+  float beta[CGL_MAX_WORKERS];
+  const float* losses;
+  float* x;
+  long nx;
+  float* alpha_out;           // [n] (written by block 0), may be null
+};
+
+__global__ __launch_bounds__(256) void cgl_weights_scale_k(CglWeightsArgs a) {
+  __shared__ float s_alpha;
+  if (threadIdx.x == 0) {
+    float l[CGL_MAX_WORKERS], al[CGL_MAX_WORKERS];
+    for (int q = 0; q < a.n; ++q) l[q] = gld(a.losses + q);
+    cgl_weights(a.mode, a.n, a.lam, a.beta, l, al);
+    s_alpha = al[a.rank];
+    if (blockIdx.x == 0 && a.alpha_out)
+      for (int q = 0; q < a.n; ++q) gst(a.alpha_out + q, al[q]);
+  }
+  __syncthreads();
+  const float al = s_alpha;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < a.nx; i += (long)gridDim.x * 256) gst(a.x + i, gld(a.x + i) * al);
+}
+
 // ==========================================================================================
 // Host side: tap tables, launch planning, C ABI.
 namespace {
@@ -1896,6 +1924,21 @@ int cgl_adv_loss(const float* x, int M, int C, int loss, int target, double weig
   if ((loss == 0) != (C == 2) || (loss != 0 && C != 1)) return CGL_E_ARG;
   hipLaunchKernelGGL(cgl_adv_loss_k, dim3(1), dim3(256), 0, (hipStream_t)stream, x, M, C, loss, target,
                      (float)weight, loss_out, grad);
+  return (int)hipGetLastError();
+}
+
+int cgl_weights_scale(int weighting, int n, int rank, float lam, const float* beta_host, const float* losses,
+                      float* x, int64_t nx, float* alpha_out, void* stream) {
+  if (weighting < 0 || weighting > 4 || n < 1 || n > CGL_MAX_WORKERS || rank < 0 || rank >= n || !beta_host ||
+      !losses || (nx > 0 && !x) || nx < 0)
+    return CGL_E_ARG;
+  CglWeightsArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.mode = weighting; a.n = n; a.rank = rank; a.lam = lam;
+  for (int q = 0; q < n; ++q) a.beta[q] = beta_host[q];
+  a.losses = losses; a.x = x; a.nx = (long)nx; a.alpha_out = alpha_out;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((nx + 255) / 256, 1024));
+  hipLaunchKernelGGL(cgl_weights_scale_k, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 

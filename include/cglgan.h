@@ -247,6 +247,12 @@ int cgl_nhwc_to_nchw(const float* X, float* Y, int n, int c, int hw, void* strea
  * on logits.  target 0 (fake) or 1 (valid); loss_out: device scalar. */
 int cgl_adv_loss(const float* x, int M, int C, int loss, int target, double weight, float* loss_out, float* grad,
                  void* stream);
+/* Exchange weighting: alpha = weights(weighting, lambda, beta, losses[n]) (CGL_WEIGHT_*, the
+ * reference's Server.train formulas), then x[0:nx] *= alpha[rank] in place (this worker's
+ * contribution before the all-reduce(sum)); alpha_out[n] (device, may be null) receives every alpha.
+ * beta_host: host array of n data-size weights (capgan.py:149-153). */
+int cgl_weights_scale(int weighting, int n, int rank, float lam, const float* beta_host, const float* losses,
+                      float* x, int64_t nx, float* alpha_out, void* stream);
 /* dst[r] = src[idx ? idx[r] : row0 + r] for r < nrows (rows of row_floats floats; idx: device int32):
  * the worker's real-batch sampler over a device-resident shard (capgan.py:282,326-332). */
 int cgl_gather_rows(const float* src, const int* idx, int64_t row0, int nrows, int row_floats, float* dst,
