@@ -328,7 +328,8 @@ class ConvGanStep:
         self.G.adam(self.lr, self.betas, self.eps)
         # optim.SGD([Lambda], lr=0.1) with dF/dLambda = -0.001 (capgan.py:249,259), in the fp32
         # arithmetic of the reference's 0-d tensor (the MLP path's cgl_adam tail does the same)
-        self.lam = float(np.float32(self.lam) + np.float32(-0.1) * np.float32(-0.001))
+        if self.weighting != "mean":     # MD-GAN's server has no lambda (MDGAN/MNIST/mdgan.py:203-205)
+            self.lam = float(np.float32(self.lam) + np.float32(-0.1) * np.float32(-0.001))
         self.round += 1
 
     def run(self, real=None):

@@ -212,3 +212,42 @@ class ConvWorkerExchange:
                 self.comm.all_reduce_mean(t)
         if self.dswap is not None and (r + 1) % self.swap_every == 0:
             self.comm.swap(self._d_state(), self.dswap.next_perm())
+
+
+class ConvLocalComm:
+    """N conv-GAN workers (cglgan.conv_step.ConvGanStep) of one process in lockstep -- the single-GPU
+    rehearsal of ConvWorkerExchange: the same phase A / all-gather / alpha / sum / phase B sequence,
+    the sums taken over the workers' buffers in a fixed order (rank 0 .. N-1)."""
+
+    def __init__(self, steps):
+        self.steps = steps
+        self.size = len(steps)
+
+    def round(self, r: int, reals=None, share_every: int = 0):
+        from . import conv_ops as O
+        ss = self.steps
+        reals = reals if reals is not None else [None] * self.size
+        if self.size == 1:
+            ss[0].run(reals[0])
+            return
+        for s, x in zip(ss, reals):
+            s.phase_a(x)
+        losses = torch.cat([s.lbuf[2:3] for s in ss])
+        for s in ss:
+            s.losses_all.copy_(losses)
+            O.weights_scale(s.weighting, s.lam, s.beta, s.losses_all, s.rank, s.dimg)
+        tot = ss[0].dimg.clone()
+        for s in ss[1:]:
+            tot += s.dimg
+        for s in ss:
+            s.dimg.copy_(tot)
+            s.phase_b()
+        if share_every > 0 and (r + 1) % share_every == 0:
+            for i in range(1 + len(ss[0].D.running)):
+                ts = [s.D.p if i == 0 else list(s.D.running.values())[i - 1] for s in ss]
+                tot = ts[0].clone()
+                for t in ts[1:]:
+                    tot += t
+                tot /= self.size
+                for t in ts:
+                    t.copy_(tot)

@@ -197,3 +197,68 @@ class ConvGan:
         self.opt_g.step()
         return dict(Xd=Xd.detach(), Xg=Xg.detach(), d_loss=float(d_loss.detach()), d_real=float(real_loss.detach()),
                     d_fake=float(fake_loss.detach()), g_loss=float(g_loss.detach()), d_grads=d_grads, g_grads=g_grads)
+
+
+class ConvCapgan:
+    """N CAPGAN workers + their server on the conv GAN: capgan.py:211-262 (Server.train: Xd / Xg once,
+    the N worker losses gathered, alpha = softmax(softmax(lambda l) * beta), F = sum alpha l - 0.001 lambda,
+    F.backward() through every worker's D into the shared G, SGD on lambda, Adam G) with each worker's
+    Worker.train (:316-349) on its own D and real batch.  ``weighting="mean"``: MDGAN/MNIST/mdgan.py:203-205
+    (F = mean l, no lambda term)."""
+
+    def __init__(self, gp, gb, dps, dbs, beta, loss="mse", weighting="capgan", dtype=torch.float64):
+        from .gan_oracle import capgan_alpha
+        self._alpha = capgan_alpha
+        cv = lambda d: OrderedDict((k, v.detach().clone().to(dtype if v.is_floating_point() else v.dtype))
+                                   for k, v in d.items())
+        self.gp, self.gb = cv(gp), cv(gb)
+        self.dps, self.dbs = [cv(d) for d in dps], [cv(d) for d in dbs]
+        for p in list(self.gp.values()) + [p for d in self.dps for p in d.values()]:
+            p.requires_grad_(True)
+        self.loss, self.weighting, self.dtype = loss, weighting, dtype
+        self.beta = torch.tensor([float(b) for b in beta], dtype=dtype)
+        self.opt_g = Adam(list(self.gp.values()), LR, (B1, B2), ADAM_EPS)
+        self.opt_d = [Adam(list(d.values()), LR, (B1, B2), ADAM_EPS) for d in self.dps]
+        self.lam = 0.0
+
+    def round(self, z1, z2, reals, masks):
+        """``reals[i]`` worker i's real batch, ``masks[i]`` = (real-call, fake-call, G-loss-call) Dropout2d scales."""
+        dt = self.dtype
+        z1, z2 = z1.to(dt), z2.to(dt)
+        with torch.no_grad():
+            Xd = g_forward(self.gp, self.gb, z1)
+        Xg = g_forward(self.gp, self.gb, z2)
+        half = 0.5 if self.loss == "mse" else 1.0
+        losses, d_grads = [], []
+        for i, (dp, db) in enumerate(zip(self.dps, self.dbs)):
+            mr, mf, mg = masks[i]
+            for p in dp.values():
+                p.grad = None
+            d_loss = (adv_loss(d_forward(dp, db, reals[i].to(dt), mr), 1, self.loss) +
+                      adv_loss(d_forward(dp, db, Xd.detach(), mf), 0, self.loss)) * half
+            d_loss.backward()
+            d_grads.append(OrderedDict((k, p.grad.detach().clone()) for k, p in dp.items()))
+            self.opt_d[i].step()
+            losses.append(adv_loss(d_forward(dp, db, Xg, mg), 1, self.loss))
+        l = torch.stack(losses)
+        lam = torch.tensor(self.lam, dtype=dt)
+        n = len(self.dps)
+        if self.weighting == "capgan":
+            alpha = self._alpha(lam, l.detach(), self.beta)
+            F_max = (alpha * l).sum() - LAMBDA_REG * lam
+        elif self.weighting == "mean":
+            alpha = torch.full((n,), 1.0 / n, dtype=dt)
+            F_max = l.mean()
+        else:
+            raise ValueError(self.weighting)
+        for p in self.gp.values():
+            p.grad = None
+        F_max.backward()
+        g_grads = OrderedDict((k, p.grad.detach().clone()) for k, p in self.gp.items())
+        if self.weighting == "capgan":
+            # optim.SGD step on the fp32 0-d Lambda: p + (-lr) * grad, grad = -0.001 (capgan.py:141,249,259)
+            f32 = lambda x: torch.tensor(x, dtype=torch.float32)
+            self.lam = float(f32(self.lam) + f32(-LAMBDA_LR) * f32(-LAMBDA_REG))
+        self.opt_g.step()
+        return dict(Xd=Xd.detach(), Xg=Xg.detach(), losses=l.detach(), alpha=alpha.detach(), g_grads=g_grads,
+                    d_grads=d_grads)
