@@ -86,7 +86,7 @@ struct CglPipe {
 
 template <int LAYOUT, int VEC, int TM, int TN>
 __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d, int bid, float* __restrict__ s_red,
-                                              float* __restrict__ s_col) {
+                                              float* __restrict__ s_col, int* __restrict__ s_flag) {
   constexpr int S = CglPipe<TM, TN>::S;
   const int M = d->M, N = d->N, K = d->K;
   const int WN = d->WN, WK = d->WK, WM = d->WM;
@@ -97,15 +97,19 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   const int wk = wave % WK, wmn = wave / WK;
   const int wm = wmn / WN, wn = wmn % WN;
   // XCD-aware tile order (blocks b and b+8 land on the same XCD): each XCD takes a contiguous
-  // range of tiles in n-major order, so its L2 holds ~1/8 of the B panels (the weights) plus
-  // the A panels, instead of all of both.  Bijective for any tile count (guide T1).
+  // range of (tile, k-slice) units in n-major order, so its L2 holds ~1/8 of the B panels (the
+  // weights) plus the A panels, instead of all of both, and the k-slices of one tile share an XCD
+  // (their partials stay XCD-local).  Bijective for any count (guide T1).
+  const int KS = d->ksplit > 1 ? d->ksplit : 1;
   const int local = bid - d->wg_begin;
-  const int nwg = d->tiles_m * d->tiles_n;
-  int tile = local;
+  const int ntile = d->tiles_m * d->tiles_n;
+  const int nwg = ntile * KS;
+  int unit = local;
   if (nwg >= 16) {
     const int xcd = local & 7, pos = local >> 3, q = nwg >> 3, r = nwg & 7;
-    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+    unit = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
   }
+  const int tile = unit / KS, kslice = unit - tile * KS;
   const int tn = tile / d->tiles_m, tm = tile % d->tiles_m;
   const int BM = 32 * TM * WM;
   const int m0 = tm * BM + wm * 32 * TM;            // first row of this wave's tile
@@ -123,7 +127,9 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int nch = (K + CGL_GEMM_KCHUNK - 1) / CGL_GEMM_KCHUNK;
-  const int cb = (wk * nch) / WK, ce = ((wk + 1) * nch) / WK;
+  // chunk range of this wave: slice kslice * WK + wk of KS * WK equal slices of the K chunks
+  const int nsl = KS * WK, sl = kslice * WK + wk;
+  const int cb = (sl * nch) / nsl, ce = ((sl + 1) * nch) / nsl;
   const int lda = d->a.ld, ldb = d->b.ld;
   float* __restrict__ a_copy = d->a_copy;
 
@@ -286,6 +292,67 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
             for (int r = 0; r < 16; ++r) acc[i][j][r] += src[((i * TN + j) * 16 + r) * 64 + lane];
       }
     }
+  }
+
+  // ---------------- cross-workgroup split-K combine (ksplit > 1)
+  // Every k-slice workgroup publishes its tile partial with 16-byte write-through (sc1) buffer
+  // stores, drains them (vmcnt(0) in every storing wave, then the workgroup barrier) and takes a
+  // ticket (relaxed agent-scope atomic); the workgroup drawing ticket KS-1 reads all KS partials
+  // back with sc1 loads, sums them in slice order (deterministic: replicas stay bitwise equal)
+  // and continues into the epilogue; the others exit.  The ticket is re-zeroed by the reducer.
+  // (cdna_hip_programming.md Guideline 16 / "In-launch split-K reduction", sc1 form.)
+  if (KS > 1) {
+    constexpr int NB = TM * TN;
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    const int wt = WM * WN;
+    const long slab = (long)NB * 16 * 64;                      // floats per wave-tile partial
+    const long per_slice = (long)ntile * wt * slab;
+    auto rs = __builtin_amdgcn_make_buffer_rsrc(d->kpart, (short)0, (int)(per_slice * KS * 4), 0x00020000);
+    if (wk == 0) {
+      const long off0 = (long)kslice * per_slice + ((long)tile * wt + wmn) * slab;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x4 v = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+            const int off = (int)((off0 + (((i * TN + j) * 4 + q) * 64 + lane) * 4) * 4);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rs, off, 0, 16);
+          }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+      s_flag[0] = (__hip_atomic_fetch_add(d->kcount + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   (unsigned)(KS - 1));
+    __syncthreads();
+    if (!s_flag[0]) return;
+    if (wk == 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int ksl = 0; ksl < KS; ++ksl) {
+        const long off0 = (long)ksl * per_slice + ((long)tile * wt + wmn) * slab;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int off = (int)((off0 + (((i * TN + j) * 4 + q) * 64 + lane) * 4) * 4);
+              const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
+              acc[i][j][4 * q] += v[0];
+              acc[i][j][4 * q + 1] += v[1];
+              acc[i][j][4 * q + 2] += v[2];
+              acc[i][j][4 * q + 3] += v[3];
+            }
+      }
+    }
+    if (tid == 0) __hip_atomic_store(d->kcount + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 
   // ---------------- epilogue (waves with wk == 0 own the tile)
@@ -467,6 +534,7 @@ template <int TM, int TN>
 __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDesc* __restrict__ descs, int ndesc) {
   extern __shared__ float cgl_dyn_lds[];
   __shared__ float s_col[4 * TN * 32];          // per-column reductions across waves (WM WN <= 4)
+  __shared__ int s_flag[1];                     // split-K: this workgroup reduces its tile
   float* s_red = cgl_dyn_lds;
   const int bid = blockIdx.x;
   int di = 0;
@@ -479,9 +547,9 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
 #define CGL_BODY(L)                                               \
   do {                                                            \
     if (vec)                                                      \
-      cgl_gemm_body<L, 1, TM, TN>(d, bid, s_red, s_col);    \
+      cgl_gemm_body<L, 1, TM, TN>(d, bid, s_red, s_col, s_flag);    \
     else                                                          \
-      cgl_gemm_body<L, 0, TM, TN>(d, bid, s_red, s_col);    \
+      cgl_gemm_body<L, 0, TM, TN>(d, bid, s_red, s_col, s_flag);    \
   } while (0)
   if (layout == 0)
     CGL_BODY(0);
@@ -495,4 +563,10 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
 // Host helper: dynamic LDS bytes of one problem's split-K partials.
 inline int cgl_gemm_stage_bytes(const CglGemmDesc& d) {
   return (d.WK > 1) ? d.WM * d.WN * (d.WK - 1) * d.TM * d.TN * 16 * 64 * 4 : 0;
+}
+
+// Host helpers: workgroups of one problem, and the split-K partial floats it needs.
+inline int cgl_gemm_wgs(const CglGemmDesc& d) { return d.tiles_m * d.tiles_n * (d.ksplit > 1 ? d.ksplit : 1); }
+inline long cgl_gemm_kpart_floats(const CglGemmDesc& d) {
+  return d.ksplit > 1 ? (long)d.ksplit * d.tiles_m * d.tiles_n * d.WM * d.WN * d.TM * d.TN * 16 * 64 : 0;
 }

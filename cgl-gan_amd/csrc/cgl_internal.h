@@ -78,6 +78,13 @@ struct CglGemmDesc {
   const float* tanh_ref; int tanh_ld;     // v *= 1 - t*t
   float* stat_part; int stat_gr;          // forward BatchNorm partials of the stored output
   float* bias_out;                     // with b_ones_col: column N-1 of C goes here
+  // cross-workgroup split-K (ksplit > 1): the K range is cut into ksplit slices, one workgroup per
+  // (tile, slice); every slice stores its tile partial write-through (sc1) to kpart, the workgroup
+  // that draws the last ticket of kcount[tile] sums the partials in slice order (deterministic),
+  // runs the epilogue and re-zeroes the ticket
+  int ksplit;
+  float* kpart;                        // [ksplit][tiles][WM*WN][TM*TN][16][64] floats
+  unsigned int* kcount;                // [tiles], zero at rest
 };
 
 // BatchNorm1d(train) + LeakyReLU over the whole [mtot][F] output of one G layer.

@@ -112,7 +112,9 @@ struct Carve {
 constexpr int kMaxGemmDescs = 128;
 constexpr int kMaxHeadDescs = 2 * CGL_MAX_EPOCH + 4;
 constexpr int kMaxBnDescs = 2 * CGL_MAX_LAYERS;
-constexpr int kCounters = 64;
+constexpr int kSplitKCounters = 8192;           // split-K tickets (one per tile of a launch)
+constexpr int kCounters = 64 + kSplitKCounters;  // [0, 64): head-loss tickets
+constexpr int64_t kSplitKFloats = 4 << 20;       // split-K partials of one launch (16 MiB)
 
 struct WS {
   // G forward (2B rows)
@@ -136,7 +138,8 @@ struct WS {
   // misc
   float* hpart;
   float* hpart2;
-  unsigned int* counters;   // [kCounters]: head-loss tickets
+  unsigned int* counters;   // [kCounters]: head-loss tickets, then split-K tickets
+  float* kpart;             // [kSplitKFloats]: split-K partials (reused by every launch)
   CglStepState* st;
   int* idx;       // sampler output when sample_n > 0
   CglGemmDesc* gemm;
@@ -185,6 +188,7 @@ WS carve_ws(const cgl_gan_config& c, void* base) {
   w.hpart = cv.take<float>((int64_t)((Md + kHeadRows - 1) / kHeadRows) * 2);
   w.hpart2 = cv.take<float>((int64_t)((Md + kHeadRows - 1) / kHeadRows) * 2);
   w.idx = cv.take<int>((int64_t)c.epoch * c.batch_real);
+  w.kpart = cv.take<float>(kSplitKFloats);
   w.total = cv.off;
   return w;
 }
@@ -241,18 +245,53 @@ void launch_gemm(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc*
 //   MFMA issue per SIMD, one wave's dependent chain incl. the part of the memory latency its
 //   (S-1)-deep prefetch does not cover, and the per-CU address/L1 rate of the fragment loads
 //   (a fragment load touches 32 cache lines), plus the split-K reduction.
-double gemm_cost(int M, int N, int K, int WM, int WN, int WK, int TM, int TN) {
+//   KS > 1: cross-workgroup split-K -- KS times the workgroups, 1 / KS of the chunks each, plus
+//   the combine (publish, ticket, the reducer's read of KS partials).
+double gemm_cost(int M, int N, int K, int WM, int WN, int WK, int TM, int TN, int KS = 1) {
   const double lat = 2000.0;
   const int S = 3;
   const long tiles = (long)((M + 32 * TM * WM - 1) / (32 * TM * WM)) * ((N + 32 * TN * WN - 1) / (32 * TN * WN));
-  const double wg_per_cu = std::ceil(tiles / 256.0);
+  const double wg_per_cu = std::ceil(tiles * KS / 256.0);
   const int nch = (K + CGL_GEMM_KCHUNK - 1) / CGL_GEMM_KCHUNK;
-  const double per = std::ceil((double)nch / WK);
+  const double per = std::ceil((double)nch / (WK * KS));
   const double blk = 512.0 * TM * TN;
   const double mfma = wg_per_cu * per * blk;
   const double chain = per * std::max(blk, lat / (S - 1));
   const double ta = wg_per_cu * 4 * per * (TM + TN) * 64.0;
-  return std::max(mfma, std::max(chain, ta)) + (WK > 1 ? 400.0 * TM * TN : 0.0);
+  return std::max(mfma, std::max(chain, ta)) + (WK > 1 ? 400.0 * TM * TN : 0.0) +
+         (KS > 1 ? 2400.0 + 300.0 * KS * TM * TN : 0.0);
+}
+
+// Cross-workgroup split-K factor for a chosen tile shape (CGL_SPLITK=0 disables, =N forces N):
+// KS in {1, 2, 4} with >= 2 chunks per wave and a partial slab of <= 16 KB per tile.
+int gemm_splitk_env() {
+  static int v = -2;
+  if (v == -2) {
+    const char* e = getenv("CGL_SPLITK");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+void choose_ks(CglGemmDesc& d) {
+  d.ksplit = 1;
+  // Measured on MI355X (tools/gemm_bench REPS 2, profiles/r01_gemm_microbench_v8_splitk.txt): the
+  // combine (publish + ticket + the reducer's read, ~2-3 us) outweighs the shorter k-loop on every
+  // GEMM of the B=256 round, so split-K is opt-in (CGL_SPLITK=N forces N; -1 = cost model).
+  const int env = gemm_splitk_env();
+  if (env == 0) return;
+  const int nch = (d.K + CGL_GEMM_KCHUNK - 1) / CGL_GEMM_KCHUNK;
+  const long slab = (long)d.WM * d.WN * d.TM * d.TN * 4096;
+  if (slab > 16384) return;
+  double best = gemm_cost(d.M, d.N, d.K, d.WM, d.WN, d.WK, d.TM, d.TN, 1);
+  for (int ks : {2, 4}) {
+    if (nch < 2 * d.WK * ks) break;
+    if (env > 0 && ks != env) continue;
+    const double c = gemm_cost(d.M, d.N, d.K, d.WM, d.WN, d.WK, d.TM, d.TN, ks);
+    if (env > 0 || c < best * 0.97) {
+      best = c;
+      d.ksplit = ks;
+    }
+  }
 }
 
 // force_wm: rows per wave-row group fixed (32 * TM * WM == 32 * force_wm); force_t: TM = TN fixed
@@ -399,10 +438,26 @@ void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
   for (auto& d : descs)
     if (d.TM != blk) choose_tiles(d, 0, blk);
   L.blk = blk;
+  long kp = 0;
+  unsigned int kc = 64;
   for (auto& d : descs) {
     set_vec(d);
+    // split-K: only on the single-stream plan (the partial / ticket regions are per launch)
+    d.ksplit = 1;
+    if (!c->two_streams) {
+      choose_ks(d);
+      if (d.ksplit > 1 && (kp + cgl_gemm_kpart_floats(d) > kSplitKFloats ||
+                           kc + d.tiles_m * d.tiles_n > (unsigned)kCounters))
+        d.ksplit = 1;
+      if (d.ksplit > 1) {
+        d.kpart = c->ws.kpart + kp;
+        d.kcount = c->ws.counters + kc;
+        kp += cgl_gemm_kpart_floats(d);
+        kc += d.tiles_m * d.tiles_n;
+      }
+    }
     d.wg_begin = wg;
-    wg += d.tiles_m * d.tiles_n;
+    wg += cgl_gemm_wgs(d);
     const int nalg = d.b_ones_col ? d.N - 1 : d.N;
     L.flops += 2.0 * d.M * (double)nalg * d.K;
     stage = std::max(stage, cgl_gemm_stage_bytes(d));
@@ -1261,7 +1316,8 @@ static int single_gemm(CglGemmDesc& d, void* ws, int64_t wsb, hipStream_t s) {
   d.wg_begin = 0;
   set_vec(d);
   HIPCHK(hipMemcpyAsync(ws, &d, sizeof(d), hipMemcpyHostToDevice, s));
-launch_gemm(d.TM, d.tiles_m * d.tiles_n, cgl_gemm_stage_bytes(d), s, (const CglGemmDesc*)ws, 1);
+  d.ksplit = 1;
+  launch_gemm(d.TM, cgl_gemm_wgs(d), cgl_gemm_stage_bytes(d), s, (const CglGemmDesc*)ws, 1);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   // the descriptor lives in the caller's workspace: keep it alive until the kernel has read it

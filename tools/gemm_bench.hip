@@ -33,7 +33,7 @@ static double time_desc(CglGemmDesc d, CglGemmDesc* dd, int reps) {
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   (void)hipMemcpy(dd, &d, sizeof(d), hipMemcpyHostToDevice);
-  const int grid = d.tiles_m * d.tiles_n;
+  const int grid = cgl_gemm_wgs(d);
   const int sh = cgl_gemm_stage_bytes(d);
   auto go = [&]() {
     if (d.TM == 2)
@@ -151,6 +151,78 @@ static void fusion_costs(float* A, float* B, float* C, CglGemmDesc* dd, int reps
   }
 }
 
+// Cross-workgroup split-K: per shape, the (WM,WN,WK)/T arrangements 114/1, 122/1 and 212/1 at
+// KS = 1, 2, 4 (results checked against KS = 1).
+static void splitk_table(float* A, float* B, float* C, float* bias, CglGemmDesc* dd, int reps) {
+  float* kpart;
+  unsigned int* kcount;
+  CK(hipMalloc(&kpart, (size_t)(4 << 20) * 4));
+  CK(hipMalloc(&kcount, 8192 * 4));
+  CK(hipMemset(kcount, 0, 8192 * 4));
+  const Shape shapes[] = {
+      {"G3 fwd", 0, 512, 1024, 512}, {"G4 fwd", 0, 512, 784, 1024}, {"D0 fwd", 0, 512, 512, 784},
+      {"D1 fwd", 0, 512, 256, 512},  {"E0 fwd", 0, 256, 512, 784},  {"E1 fwd", 0, 256, 256, 512},
+      {"E dXg", 1, 256, 784, 512},   {"G4 dA", 1, 256, 1024, 784},  {"G3 dA", 1, 256, 512, 1024},
+      {"G2 dA", 1, 256, 256, 512},   {"D gV1", 2, 256, 513, 512},   {"D gV0", 2, 512, 785, 512},
+      {"G gW4", 2, 784, 1025, 256},  {"G gW3", 2, 1024, 513, 256},  {"G gW2", 2, 512, 257, 256},
+      {"G gW1", 2, 256, 129, 256},
+  };
+  const int cfgs[3][4] = {{1, 1, 4, 1}, {1, 2, 2, 1}, {2, 1, 2, 1}};
+  printf("split-K   shape      M     N     K |");
+  for (auto& c : cfgs) printf(" %d%d%d/%d ks1  ks2  ks4 |", c[0], c[1], c[2], c[3]);
+  printf("\n");
+  for (const Shape& s : shapes) {
+    printf("split-K %-7s %5d %5d %5d |", s.name, s.M, s.N, s.K);
+    for (auto& c : cfgs) {
+      for (int ks : {1, 2, 4}) {
+        CglGemmDesc d;
+        memset(&d, 0, sizeof(d));
+        d.layout = s.layout; d.M = s.M; d.N = s.N; d.K = s.K;
+        d.WM = c[0]; d.WN = c[1]; d.WK = c[2]; d.TM = d.TN = c[3];
+        d.tiles_m = (s.M + 32 * c[3] * c[0] - 1) / (32 * c[3] * c[0]);
+        d.tiles_n = (s.N + 32 * c[3] * c[1] - 1) / (32 * c[3] * c[1]);
+        d.a.p0 = A; d.a.split = 0x7fffffff; d.b.p0 = B; d.b.split = 0x7fffffff;
+        if (s.layout == 0) {
+          d.a.ld = s.K; d.b.ld = s.K; d.a_vec = d.b_vec = (s.K % 4 == 0); d.bias = bias; d.act = CGL_EPI_ACT_LEAKY;
+        } else if (s.layout == 1) {
+          d.a.ld = s.K; d.a_vec = (s.K % 4 == 0); d.b.ld = s.N; d.b_vec = (s.N % 4 == 0);
+        } else {
+          d.a.ld = s.M; d.b.ld = s.N - 1; d.a_vec = (s.M % 4 == 0); d.b_vec = ((s.N - 1) % 4 == 0);
+          d.b_ones_col = 1; d.bias_out = bias;
+        }
+        d.slope = 0.2f; d.C = C; d.ldc = s.layout == 2 ? s.N - 1 : s.N;
+        d.ksplit = ks; d.kpart = kpart; d.kcount = kcount;
+        const int nch = (s.K + 15) / 16;
+        if (ks > 1 && (nch < 2 * c[2] * ks || cgl_gemm_kpart_floats(d) > (4 << 20))) {
+          printf("    -");
+          continue;
+        }
+        const size_t n = (size_t)s.M * d.ldc;
+        static std::vector<float> r0;
+        std::vector<float> r1(n);
+        CK(hipMemset(C, 0, n * 4));
+        (void)time_desc(d, dd, 1);
+        CK(hipDeviceSynchronize());
+        if (ks == 1) {
+          r0.resize(n);
+          CK(hipMemcpy(r0.data(), C, n * 4, hipMemcpyDeviceToHost));
+        } else {
+          CK(hipMemcpy(r1.data(), C, n * 4, hipMemcpyDeviceToHost));
+          double num = 0, den = 0;
+          for (size_t i = 0; i < n; ++i) {
+            num += (double)(r1[i] - r0[i]) * (r1[i] - r0[i]);
+            den += (double)r0[i] * r0[i];
+          }
+          if (!(num <= 1e-10 * den)) printf(" [MISMATCH %.1e]", sqrt(num / (den + 1e-30)));
+        }
+        printf(" %5.2f", time_desc(d, dd, reps));
+      }
+      printf(" |");
+    }
+    printf("\n");
+  }
+}
+
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 200;
   const Shape shapes[] = {
@@ -189,6 +261,10 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const bool single = argc > 3;   // gemm_bench REPS single SHAPE CFG: one config only (PMC runs)
+  if (argc == 3 && atoi(argv[2]) == 2) {   // gemm_bench REPS 2: the split-K table only
+    splitk_table(A, B, C, bias, dd, reps);
+    return 0;
+  }
   if (!single) {
     probes(A, B, C, bias, dd, reps);
     fusion_costs(A, B, C, dd, reps);
