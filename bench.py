@@ -171,7 +171,7 @@ def conv_flops(n, h, w, cin, cout, stride, up, which):
     return exe, ref
 
 
-def profile_conv_round(step, real=None):
+def profile_conv_round(run_round):
     """One extra round with every conv op bracketed by HIP events on the launch stream: per-op
     device time (pack + MFMA kernel, + fixed-order reduction for weight gradients) and FLOPs."""
     from cglgan import conv_ops as CO
@@ -201,7 +201,7 @@ def profile_conv_round(step, real=None):
     for k in orig:
         setattr(CO, k, wrap(k))
     try:
-        step.run(real=real)
+        run_round()
     finally:
         for k, f in orig.items():
             setattr(CO, k, f)
@@ -245,22 +245,28 @@ def conv_cpu_baseline(a):
 
 def main_lsgan(a, world, rank, local):
     from cglgan.conv_step import ConvGanStep
+    from cglgan.exchange import ConvWorkerExchange, DistComm
     stream = torch.cuda.Stream()
     with torch.cuda.stream(stream):
         g = torch.Generator(device="cuda").manual_seed(1000 + rank)
         rows = (a.rows // a.batch) * a.batch
         data = torch.rand(rows, 1024, device="cuda", generator=g) * 2 - 1
-        step = ConvGanStep(a.batch, loss=a.loss, data=data, seed=20211212, rank=rank)
+        # one worker per GPU: G replicated (same init and z stream), D and real shard per rank
+        step = ConvGanStep(a.batch, loss=a.loss, data=data, seed=20211212, n_workers=world, rank=rank)
         step.init_default(20211212, 20211212 + 1 + rank)
+        ex = ConvWorkerExchange(step, DistComm() if world > 1 else None, share_every=a.E if world > 1 else 0)
         torch.cuda.synchronize()
+        r = 0
         for _ in range(a.warmup):
-            step.run()
+            ex.round(r)
+            r += 1
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
         for _ in range(a.steps):
-            step.run()
+            ex.round(r)
+            r += 1
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -270,7 +276,7 @@ def main_lsgan(a, world, rank, local):
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
         st = step.stats()
-        ops = profile_conv_round(step)
+        ops = profile_conv_round(lambda: ex.round(r))
     ms_step = el / a.steps * 1e3
     value = world * a.batch * a.steps / el
     if rank != 0:
@@ -286,7 +292,9 @@ def main_lsgan(a, world, rank, local):
         "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": f"model/lsgan.py conv GAN, CAPGAN worker round (G fwd x2, D step, G loss, G bwd, "
-                               f"Adam G/D), {a.loss} objective, 32x32x1, 1 worker per GPU",
+                               f"Adam G/D), {a.loss} objective, 32x32x1, 1 worker per GPU"
+                               + (f", {world} workers: loss all-gather, alpha-weighted image-gradient "
+                                  f"all-reduce, E={a.E} D all-reduce over RCCL" if world > 1 else ""),
                    "global_batch": a.batch * world, "batch_per_worker": a.batch, "img": "32x32x1",
                    "parallelism": f"workers{world}", "dataset_rows_per_worker": rows},
         "roofline": {"bound": "mfma", "kernel": "cgl_conv_fwd + cgl_conv_wgrad (+ pack / reduce), every conv op of "

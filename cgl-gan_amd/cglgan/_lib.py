@@ -31,6 +31,8 @@ EXPORTS = [
     "cgl_bn2d_workspace_bytes", "cgl_bn2d_fwd", "cgl_bn2d_bwd", "cgl_act_drop_bwd", "cgl_dropout2d_mask",
     "cgl_nchw_to_nhwc", "cgl_nhwc_to_nchw", "cgl_adv_loss", "cgl_adam_multi", "cgl_dense_workspace_bytes",
     "cgl_dense_fwd", "cgl_dense_bwd_data", "cgl_dense_bwd_weight", "cgl_gather_rows", "cgl_weights_scale",
+    # evaluation (CGLGAN/2DMG/main.py plot_2d KL score)
+    "cgl_kl_score",
 ]
 
 LOSS_OP_CE2, LOSS_OP_BCE, LOSS_OP_MSE, LOSS_OP_BCE_LOGIT = 0, 1, 2, 3
@@ -119,6 +121,7 @@ def _load():
         "cgl_dense_bwd_weight": (ci, [vp, vp, vp, vp, ci, ci, ci, vp, i64, vp]),
         "cgl_gather_rows": (ci, [vp, vp, i64, ci, ci, vp, vp]),
         "cgl_weights_scale": (ci, [ci, ci, ci, cf, P(cf), vp, vp, i64, vp, vp]),
+        "cgl_kl_score": (ci, [vp, i64, i64, vp, i64, i64, ci, cd, cd, cd, cd, vp, vp, vp]),
         "cgl_adam_multi": (ci, [ci, P(vp), P(vp), P(vp), P(vp), P(i64), ci, cd, cd, cd, cd, vp]),
         "cgl_version": (ctypes.c_char_p, []),
     }

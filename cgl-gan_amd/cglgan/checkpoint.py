@@ -1,0 +1,52 @@
+"""Checkpoint files in the reference drivers' format.
+
+Server.run writes, every 5000 rounds and at the end (capgan.py:185-200; mixed-gan.py likewise;
+MDGAN/MNIST/mdgan.py:168-170 with its own 3-tuple):
+
+  ``torch.save(net_g.state_dict(), "<dir>/<name>.pt")``   -- the generator state dict under the
+      reference's keys (model.0.weight, model.3.running_var, paths.i.4.bias ...), CPU tensors
+  ``pkl.dump((client_list, beta, lambda_list, [], gen_data, betas, gammas), f)`` -- "config<name>.pkl"
+
+``save_server`` writes both from a fused step (cglgan.GanStep / ConvGanStep, whose state dicts carry
+the reference's keys) or any module; ``load_generator`` reads a .pt back with torch.load(weights_only=
+True), so reference checkpoints load into cglgan.model modules and vice versa.
+"""
+from __future__ import annotations
+
+import os
+import pickle
+
+import torch
+
+
+def _cpu_state(sd):
+    return {k: (v.detach().cpu().clone() if torch.is_tensor(v) else v) for k, v in sd.items()}
+
+
+def generator_state(obj):
+    """The reference-keyed generator state dict of a GanStep (g_state_dict), ConvGanStep (G) or module."""
+    if hasattr(obj, "g_state_dict"):
+        return obj.g_state_dict()
+    if hasattr(obj, "G") and hasattr(obj.G, "state_dict"):
+        return obj.G.state_dict()
+    return obj.state_dict()
+
+
+def save_server(obj, directory: str, name: str, client_list, beta, lambda_list=(), gen_data=(), betas=(),
+                gammas=()):
+    """capgan.py:198-200: ``<name>.pt`` (generator state dict) + ``config<name>.pkl`` (7-tuple)."""
+    os.makedirs(directory, exist_ok=True)
+    pt = os.path.join(directory, f"{name}.pt")
+    torch.save(_cpu_state(generator_state(obj)), pt)
+    cfg = os.path.join(directory, f"config{name}.pkl")
+    beta_t = beta.detach().cpu() if torch.is_tensor(beta) else torch.tensor([float(b) for b in beta])
+    tup = (list(client_list), beta_t, list(lambda_list), [], [g.detach().cpu() if torch.is_tensor(g) else g
+                                                             for g in gen_data], list(betas), list(gammas))
+    with open(cfg, "wb") as f:
+        pickle.dump(tup, f)
+    return pt, cfg
+
+
+def load_generator(path: str):
+    """A generator checkpoint (``torch.save(state_dict)``) -- tensors only, loaded without unpickling code."""
+    return torch.load(path, map_location="cpu", weights_only=True)

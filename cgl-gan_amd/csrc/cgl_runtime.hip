@@ -1479,3 +1479,4 @@ int cgl_normal_fill(float* out, int64_t n, unsigned long long seed, int round, i
 
 // conv GAN path (model/lsgan.py): implicit-GEMM convolutions, BatchNorm2d, losses, Adam
 #include "cgl_conv.hip"
+#include "cgl_eval.hip"

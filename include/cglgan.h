@@ -262,6 +262,15 @@ int cgl_gather_rows(const float* src, const int* idx, int64_t row0, int nrows, i
 int cgl_adam_multi(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
                    const int64_t* n, int step, double lr, double beta1, double beta2, double eps, void* stream);
 
+/* ---- evaluation ------------------------------------------------------------------------------
+ * KL score of generated 2-D samples (CGLGAN/2DMG/main.py:63-101 plot_2d): np.histogram2d of the
+ * real points (rows r * real_stride of real [., 2]) and of the generated points over
+ * bins x bins bins of [lo0, hi0] x [lo1, hi1]; counts[2][bins][bins] (real, generated; device int32,
+ * may be null) and kl[0] (device double, may be null) = scipy.stats.entropy(gen, real) over the bins
+ * whose real count is non-zero.  bins <= 32; one workgroup, stream-ordered. */
+int cgl_kl_score(const float* real, int64_t nr, int64_t real_stride, const float* gen, int64_t ng, int64_t gen_stride,
+                 int bins, double lo0, double hi0, double lo1, double hi1, int* counts, double* kl, void* stream);
+
 /* Library identification: "<version> gfx950" */
 const char* cgl_version(void);
 
