@@ -889,9 +889,9 @@ __global__ __launch_bounds__(256) void cgl_colsum_k(const float* X, int rows, in
   part[((long)blockIdx.y * C + c) * 2 + 1] = 0.0;
 }
 
-// BatchNorm2d finalize: ONE WAVE PER CHANNEL, lanes over the chunk partials (lane l takes chunks
-// l, l + 64, ... in order, then a fixed xor-tree across lanes: deterministic), groups in the
-// reference's call order.
+// BatchNorm2d finalize: ONE WORKGROUP PER CHANNEL, threads over the chunk partials (thread t takes
+// chunks t, t + 256, ... in order, then a fixed xor-tree in each wave and the 4 wave sums in wave
+// order: deterministic), groups in the reference's call order.
 //   fwd (mode 0): mean / biased var per group from the chunk partials (Chan), save_mean / invstd,
 //                 scale = invstd * gamma, shift = beta - mean * scale, running stats (momentum,
 //                 unbiased variance) group by group; eval: the same from running stats.
@@ -913,17 +913,26 @@ __device__ __forceinline__ double cgl_wave_sum_d(double x) {
   return x;
 }
 
+// sum over the 256 threads of a workgroup, returned to every thread (every thread must call it)
+__device__ __forceinline__ double cgl_block_sum_d(double x, double* red) {
+  x = cgl_wave_sum_d(x);
+  __syncthreads();                       // red[] free (a previous call may still be reading it)
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ double red[4];
+  const int lane = threadIdx.x;          // thread index within the channel's workgroup
+  const int c = blockIdx.x;
   const int C = a.C;
-  if (c >= C) return;
   const double* part = a.part;
   if (a.mode == 2) {
     double t = 0.0;
     const int nch = a.groups * a.chunks_per_group;
-    for (int q = lane; q < nch; q += 64) t += part[((long)q * C + c) * 2];
-    t = cgl_wave_sum_d(t);
+    for (int q = lane; q < nch; q += 256) t += part[((long)q * C + c) * 2];
+    t = cgl_block_sum_d(t, red);
     if (lane == 0) gst(a.dgamma + c, (float)t);
     return;
   }
@@ -933,13 +942,13 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
     double dg = 0.0, db = 0.0;
     for (int g = 0; g < a.groups; ++g) {
       double S = 0.0, D = 0.0;
-      for (int q = lane; q < cpg; q += 64) {
+      for (int q = lane; q < cpg; q += 256) {
         const long o = ((long)(g * cpg + q) * C + c) * 2;
         S += part[o];
         D += part[o + 1];
       }
-      S = cgl_wave_sum_d(S);
-      D = cgl_wave_sum_d(D);
+      S = cgl_block_sum_d(S, red);
+      D = cgl_block_sum_d(D, red);
       const float invstd = gld(a.save_invstd + (long)g * C + c);
       if (lane == 0) {
         gst(a.coef0 + (long)g * C + c, (float)(S / a.gr));
@@ -968,18 +977,18 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
   float rm = a.run_mean ? gld(a.run_mean + c) : 0.f, rv = a.run_var ? gld(a.run_var + c) : 0.f;
   for (int g = 0; g < a.groups; ++g) {
     double s = 0.0;
-    for (int q = lane; q < cpg; q += 64) s += part[((long)(g * cpg + q) * C + c) * 2];
-    s = cgl_wave_sum_d(s);
+    for (int q = lane; q < cpg; q += 256) s += part[((long)(g * cpg + q) * C + c) * 2];
+    s = cgl_block_sum_d(s, red);
     const double n = a.gr;
     const double mu = s / n;
     double m2 = 0.0;
-    for (int q = lane; q < cpg; q += 64) {
+    for (int q = lane; q < cpg; q += 256) {
       const long o = ((long)(g * cpg + q) * C + c) * 2;
       const double cnt = a.R;
       const double dd = part[o] / cnt - mu;
       m2 += part[o + 1] + cnt * dd * dd;
     }
-    m2 = cgl_wave_sum_d(m2);
+    m2 = cgl_block_sum_d(m2, red);
     const double invstd = 1.0 / sqrt(m2 / n + a.eps);
     const float sc = (float)invstd * w;
     if (lane == 0) {
@@ -1585,7 +1594,7 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
 
 
 int chan_chunk(int64_t gr) {
-  int R = 64;
+  int R = 256;
   while (R > 1 && gr % R != 0) R >>= 1;
   return R;
 }
@@ -1597,7 +1606,7 @@ bool pow2_le256(int C) { return C >= 1 && C <= 256 && (C & (C - 1)) == 0; }
 int col_sum(const float* X, int64_t rows, int C, double* part, float* out, hipStream_t s) {
   int nch;
   if (pow2_le256(C)) {
-    const int R = 64;
+    const int R = 256;
     nch = (int)((rows + R - 1) / R);
     CglChanArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -1611,7 +1620,7 @@ int col_sum(const float* X, int64_t rows, int C, double* part, float* out, hipSt
   CglBnFinArgs f;
   std::memset(&f, 0, sizeof(f));
   f.part = part; f.C = C; f.groups = 1; f.chunks_per_group = nch; f.mode = 2; f.dgamma = out;
-  hipLaunchKernelGGL(cgl_bn_finalize, dim3((C + 3) / 4), dim3(256), 0, s, f);
+  hipLaunchKernelGGL(cgl_bn_finalize, dim3(C), dim3(256), 0, s, f);
   return (int)hipGetLastError();
 }
 
@@ -1822,7 +1831,7 @@ int cgl_bn2d_fwd(const float* X, int n, int hw, int C, int groups, const float* 
   f.mode = 0; f.train = train; f.gamma = gamma; f.beta = beta; f.eps = eps; f.momentum = momentum;
   f.run_mean = running_mean; f.run_var = running_var; f.save_mean = save_mean; f.save_invstd = save_invstd;
   f.coef0 = c0; f.coef1 = c1;
-  hipLaunchKernelGGL(cgl_bn_finalize, dim3((C + 3) / 4), dim3(256), 0, s, f);
+  hipLaunchKernelGGL(cgl_bn_finalize, dim3(C), dim3(256), 0, s, f);
   CglEltArgs e;
   std::memset(&e, 0, sizeof(e));
   e.mode = 0; e.rows = (int)rows; e.C = C; e.gr = (int)gr; e.hw = hw; e.act = act; e.slope = slope;
@@ -1860,7 +1869,7 @@ int cgl_bn2d_bwd(const float* dY, const float* post, const float* X, int n, int 
   f.part = part; f.C = C; f.groups = groups; f.chunks_per_group = (int)(gr / R); f.R = R; f.gr = (int)gr;
   f.mode = 1; f.gamma = gamma; f.save_invstd = const_cast<float*>(save_invstd); f.coef0 = c0; f.coef1 = c1;
   f.dgamma = dgamma; f.dbeta = dbeta;
-  hipLaunchKernelGGL(cgl_bn_finalize, dim3((C + 3) / 4), dim3(256), 0, s, f);
+  hipLaunchKernelGGL(cgl_bn_finalize, dim3(C), dim3(256), 0, s, f);
   CglEltArgs e;
   std::memset(&e, 0, sizeof(e));
   e.mode = 1; e.rows = (int)rows; e.C = C; e.gr = (int)gr; e.hw = hw; e.slope = slope;
