@@ -84,7 +84,7 @@ struct CglPipe {
   static constexpr int S = CGL_GEMM_STAGES;
 };
 
-template <int LAYOUT, int VEC, int TM, int TN>
+template <int LAYOUT, int VEC, int TM, int TN, bool SK>
 __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d, int bid, float* __restrict__ s_red,
                                               float* __restrict__ s_col, int* __restrict__ s_flag) {
   constexpr int S = CglPipe<TM, TN>::S;
@@ -100,7 +100,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   // range of (tile, k-slice) units in n-major order, so its L2 holds ~1/8 of the B panels (the
   // weights) plus the A panels, instead of all of both, and the k-slices of one tile share an XCD
   // (their partials stay XCD-local).  Bijective for any count (guide T1).
-  const int KS = d->ksplit > 1 ? d->ksplit : 1;
+  const int KS = (SK && d->ksplit > 1) ? d->ksplit : 1;   // SK: the split-K instantiation
   const int local = bid - d->wg_begin;
   const int ntile = d->tiles_m * d->tiles_n;
   const int nwg = ntile * KS;
@@ -301,7 +301,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   // back with sc1 loads, sums them in slice order (deterministic: replicas stay bitwise equal)
   // and continues into the epilogue; the others exit.  The ticket is re-zeroed by the reducer.
   // (cdna_hip_programming.md Guideline 16 / "In-launch split-K reduction", sc1 form.)
-  if (KS > 1) {
+  if (SK && KS > 1) {
     constexpr int NB = TM * TN;
     typedef int i32x4 __attribute__((ext_vector_type(4)));
     const int wt = WM * WN;
@@ -530,7 +530,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 // layer side by side).  Separate symbols keep the 1x1 variant's register budget (and so its
 // occupancy) independent of the 2x2 variant's.
 // Dynamic LDS: split-K partials of the waves with wk > 0.
-template <int TM, int TN>
+template <int TM, int TN, bool SK = false>
 __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDesc* __restrict__ descs, int ndesc) {
   extern __shared__ float cgl_dyn_lds[];
   __shared__ float s_col[4 * TN * 32];          // per-column reductions across waves (WM WN <= 4)
@@ -547,9 +547,9 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
 #define CGL_BODY(L)                                               \
   do {                                                            \
     if (vec)                                                      \
-      cgl_gemm_body<L, 1, TM, TN>(d, bid, s_red, s_col, s_flag);    \
+      cgl_gemm_body<L, 1, TM, TN, SK>(d, bid, s_red, s_col, s_flag);    \
     else                                                          \
-      cgl_gemm_body<L, 0, TM, TN>(d, bid, s_red, s_col, s_flag);    \
+      cgl_gemm_body<L, 0, TM, TN, SK>(d, bid, s_red, s_col, s_flag);    \
   } while (0)
   if (layout == 0)
     CGL_BODY(0);

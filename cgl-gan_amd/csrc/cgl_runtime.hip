@@ -214,6 +214,7 @@ struct Launch {
   int record_ev = -1;
   int shmem = 0;        // dynamic LDS bytes (GEMM)
   int blk = 1;          // GEMM per-wave block shape (TM = TN = blk)
+  bool sk = false;      // GEMM launch holds a split-K problem
 };
 
 // Split-K partials of 2x2-block waves need up to 48 KB of dynamic LDS (+16 KB BN table).
@@ -221,7 +222,8 @@ hipError_t gemm_lds_attr() {
   static bool done = false;
   if (!done) {
     // advisory on this platform (launches up to the per-CU LDS succeed); never fail on it
-    for (const void* fn : {(const void*)cgl_gemm_f32<1, 1>, (const void*)cgl_gemm_f32<2, 2>}) {
+    for (const void* fn : {(const void*)cgl_gemm_f32<1, 1>, (const void*)cgl_gemm_f32<2, 2>,
+                           (const void*)cgl_gemm_f32<1, 1, true>, (const void*)cgl_gemm_f32<2, 2, true>}) {
       for (int kb : {150, 128, 96, 64}) {
         const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kb * 1024);
         (void)hipGetLastError();
@@ -233,11 +235,17 @@ hipError_t gemm_lds_attr() {
   return hipSuccess;
 }
 
-void launch_gemm(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, int n) {
-  if (blk == 2)
+void launch_gemm(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, int n, bool sk = false) {
+  if (sk) {   // a launch with a split-K problem: the instantiation carrying the combine
+    if (blk == 2)
+      cgl_gemm_f32<2, 2, true><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+    else
+      cgl_gemm_f32<1, 1, true><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+  } else if (blk == 2) {
     cgl_gemm_f32<2, 2><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
-  else
+  } else {
     cgl_gemm_f32<1, 1><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+  }
 }
 
 // Cost model of one GEMM launch (cycles) used to pick the wave arrangement WM x WN x WK and
@@ -458,6 +466,7 @@ void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
     }
     d.wg_begin = wg;
     wg += cgl_gemm_wgs(d);
+    L.sk = L.sk || d.ksplit > 1;
     const int nalg = d.b_ones_col ? d.N - 1 : d.N;
     L.flops += 2.0 * d.M * (double)nalg * d.K;
     stage = std::max(stage, cgl_gemm_stage_bytes(d));
@@ -970,7 +979,7 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
   }
   switch (L.kind) {
     case K_GEMM:
-      launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, L.count);
+      launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, L.count, L.sk);
       break;
     case K_HEAD:
       hipLaunchKernelGGL(cgl_head_loss, dim3(L.grid), dim3(256), 0, s, c->ws.head + L.first);

@@ -36,10 +36,16 @@ static double time_desc(CglGemmDesc d, CglGemmDesc* dd, int reps) {
   const int grid = cgl_gemm_wgs(d);
   const int sh = cgl_gemm_stage_bytes(d);
   auto go = [&]() {
-    if (d.TM == 2)
+    if (d.ksplit > 1) {
+      if (d.TM == 2)
+        cgl_gemm_f32<2, 2, true><<<grid, 256, sh, 0>>>(dd, 1);
+      else
+        cgl_gemm_f32<1, 1, true><<<grid, 256, sh, 0>>>(dd, 1);
+    } else if (d.TM == 2) {
       cgl_gemm_f32<2, 2><<<grid, 256, sh, 0>>>(dd, 1);
-    else
+    } else {
       cgl_gemm_f32<1, 1><<<grid, 256, sh, 0>>>(dd, 1);
+    }
   };
   for (int i = 0; i < 10; ++i) go();
   (void)hipEventRecord(e0, 0);
@@ -237,7 +243,8 @@ int main(int argc, char** argv) {
   };
   const int cfgs[8][4] = {{2, 2, 1, 1}, {2, 1, 2, 1}, {1, 2, 2, 1}, {1, 1, 4, 1},
                           {2, 2, 1, 2}, {2, 1, 2, 2}, {1, 2, 2, 2}, {1, 1, 4, 2}};
-  for (const void* fn : {(const void*)cgl_gemm_f32<1, 1>, (const void*)cgl_gemm_f32<2, 2>}) {
+  for (const void* fn : {(const void*)cgl_gemm_f32<1, 1>, (const void*)cgl_gemm_f32<2, 2>,
+                         (const void*)cgl_gemm_f32<1, 1, true>, (const void*)cgl_gemm_f32<2, 2, true>}) {
     for (int kb : {150, 128, 96, 64}) {
       const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kb * 1024);
       (void)hipGetLastError();
