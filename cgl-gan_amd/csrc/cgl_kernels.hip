@@ -331,7 +331,10 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
 #pragma unroll
     for (int j = 0; j < CGL_BNB_RPT; ++j) {
       const int r = min(rg + 8 * j, M - 1);
-      const float da = gld(dA + r * lda), po = post_on ? gld(post + r * ldp) : 1.f, y = gld(Y + r * ldy);
+      // unconditional load (post aliases Y when unused), select after: a predicated load compiles
+      // to a branch with a full vmcnt(0) drain per row
+      const float da = gld(dA + r * lda), pr = gld(post + r * ldp), y = gld(Y + r * ldy);
+      const float po = post_on ? pr : 1.f;
       dy[j] = po > 0.f ? da : da * sl;
       yc[j] = y - mean;
     }
@@ -371,13 +374,13 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
     for (int j = 0; j < 8; ++j) {
       const int r = min(r0 + 8 * j, M - 1);
       da[j] = gld(dA + r * lda);
-      po[j] = post_on ? gld(post + r * ldp) : 1.f;
+      po[j] = gld(post + r * ldp);
       y[j] = gld(Y + r * ldy);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       if (r0 + 8 * j < M) {
-        const float dy = po[j] > 0.f ? da[j] : da[j] * sl;
+        const float dy = (!post_on || po[j] > 0.f) ? da[j] : da[j] * sl;
         sum += (double)dy;
         dotp += (double)((y[j] - mean) * dy);
       }
@@ -400,14 +403,14 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
     for (int j = 0; j < 8; ++j) {
       const int r = min(r0 + 8 * j, M - 1);
       da[j] = gld(dA + r * lda);
-      po[j] = post_on ? gld(post + r * ldp) : 1.f;
+      po[j] = gld(post + r * ldp);
       y[j] = gld(Y + r * ldy);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int r = r0 + 8 * j;
       if (r < M) {
-        const float dy = po[j] > 0.f ? da[j] : da[j] * sl;
+        const float dy = (!post_on || po[j] > 0.f) ? da[j] : da[j] * sl;
         const float gi = (y[j] - mean) * k;
         gst(dZ + r * ldz, (dy - gmean - gi) * invstd * w);
       }

@@ -113,7 +113,7 @@ constexpr int kMaxGemmDescs = 128;
 constexpr int kMaxHeadDescs = 2 * CGL_MAX_EPOCH + 4;
 constexpr int kMaxBnDescs = 2 * CGL_MAX_LAYERS;
 constexpr int kSplitKCounters = 8192;           // split-K tickets (one per tile of a launch)
-constexpr int kCounters = 64 + kSplitKCounters;  // [0, 64): head-loss tickets
+constexpr int kCounters = 64;                    // head-loss tickets
 constexpr int64_t kSplitKFloats = 4 << 20;       // split-K partials of one launch (16 MiB)
 
 struct WS {
@@ -138,8 +138,9 @@ struct WS {
   // misc
   float* hpart;
   float* hpart2;
-  unsigned int* counters;   // [kCounters]: head-loss tickets, then split-K tickets
+  unsigned int* counters;   // [kCounters]: head-loss tickets
   float* kpart;             // [kSplitKFloats]: split-K partials (reused by every launch)
+  unsigned int* kcount;     // [kSplitKCounters]: split-K tickets (zero at rest)
   CglStepState* st;
   int* idx;       // sampler output when sample_n > 0
   CglGemmDesc* gemm;
@@ -188,7 +189,9 @@ WS carve_ws(const cgl_gan_config& c, void* base) {
   w.hpart = cv.take<float>((int64_t)((Md + kHeadRows - 1) / kHeadRows) * 2);
   w.hpart2 = cv.take<float>((int64_t)((Md + kHeadRows - 1) / kHeadRows) * 2);
   w.idx = cv.take<int>((int64_t)c.epoch * c.batch_real);
+  // split-K scratch last, so that the layout of everything the default plan touches is unchanged
   w.kpart = cv.take<float>(kSplitKFloats);
+  w.kcount = cv.take<unsigned int>(kSplitKCounters);
   w.total = cv.off;
   return w;
 }
@@ -447,7 +450,7 @@ void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
     if (d.TM != blk) choose_tiles(d, 0, blk);
   L.blk = blk;
   long kp = 0;
-  unsigned int kc = 64;
+  unsigned int kc = 0;
   for (auto& d : descs) {
     set_vec(d);
     // split-K: only on the single-stream plan (the partial / ticket regions are per launch)
@@ -455,11 +458,11 @@ void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
     if (!c->two_streams) {
       choose_ks(d);
       if (d.ksplit > 1 && (kp + cgl_gemm_kpart_floats(d) > kSplitKFloats ||
-                           kc + d.tiles_m * d.tiles_n > (unsigned)kCounters))
+                           kc + d.tiles_m * d.tiles_n > (unsigned)kSplitKCounters))
         d.ksplit = 1;
       if (d.ksplit > 1) {
         d.kpart = c->ws.kpart + kp;
-        d.kcount = c->ws.counters + kc;
+        d.kcount = c->ws.kcount + kc;
         kp += cgl_gemm_kpart_floats(d);
         kc += d.tiles_m * d.tiles_n;
       }
@@ -1121,6 +1124,7 @@ int cgl_gan_create(const cgl_gan_config* cfg, const cgl_gan_buffers* bufs, cgl_g
   if (he == hipSuccess && !c->bnb.empty())
     he = hipMemcpy(c->ws.bnb, c->bnb.data(), c->bnb.size() * sizeof(CglBnBwdDesc), hipMemcpyHostToDevice);
   if (he == hipSuccess) he = hipMemset(c->ws.counters, 0, kCounters * sizeof(unsigned int));
+  if (he == hipSuccess) he = hipMemset(c->ws.kcount, 0, kSplitKCounters * sizeof(unsigned int));
   if (he == hipSuccess) he = hipMemset(c->ws.st, 0, sizeof(CglStepState));
   if (he == hipSuccess) he = hipDeviceSynchronize();
   if (he != hipSuccess) {
@@ -1149,6 +1153,7 @@ int cgl_gan_reset(cgl_gan* c, const float* beta_host, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(hipMemcpyAsync(c->ws.st, &h, sizeof(h), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemsetAsync(c->ws.counters, 0, kCounters * sizeof(unsigned int), s));
+  HIPCHK(hipMemsetAsync(c->ws.kcount, 0, kSplitKCounters * sizeof(unsigned int), s));
   HIPCHK(hipStreamSynchronize(s));
   return CGL_OK;
 }
