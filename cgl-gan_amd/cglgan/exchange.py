@@ -94,12 +94,18 @@ class WorkerExchange:
     """One worker's communication round (phase A -> collectives -> phase B).
 
     ``share_every`` > 0: E-share of the D parameters every that many rounds (a19).
-    ``cloud``/``cloud_every``: Mix-G Cloud FedAvg of the trunk across server groups (a18)
-    with data-size weights ``cloud_weights`` (one per member of the cloud group).
+    ``cloud``/``cloud_every``: Cloud FedAvg across server groups (a18) with data-size weights
+    ``cloud_weights`` (one per member of the cloud group), after every ``cloud_every``-th round;
+    or, with ``cloud_due(r)`` (see ``mixg_cloud_due`` / ``capgan_cloud_due``), before round r as the
+    reference's Server.run does.  ``cloud_scope``: "trunk" -- the Mix-G trunk parameters + running
+    statistics (mixed-gan.py:193-200); "all" -- every G parameter, no buffers (CAPGAN's fedlab
+    serialize_model / fedavg_aggregate / deserialize_model, capgan.py:169-175).  ``segema``: the
+    result is segema * own + (1 - segema) * average (capgan.py:174, mixed-gan.py:198-199).
     """
 
     def __init__(self, step, comm=None, share_every: int = 0, cloud=None, cloud_every: int = 0,
-                 cloud_weights=None, fedavg_compat_noop: bool = False, swap_every: int = 0):
+                 cloud_weights=None, fedavg_compat_noop: bool = False, swap_every: int = 0,
+                 cloud_scope: str = "trunk", segema: float = 0.0, cloud_due=None):
         self.step = step
         self.comm = comm
         self.share_every = share_every
@@ -108,12 +114,17 @@ class WorkerExchange:
         self.cloud, self.cloud_every = cloud, cloud_every
         self.cloud_weights = cloud_weights
         self.fedavg_compat_noop = fedavg_compat_noop
+        if cloud_scope not in ("trunk", "all"):
+            raise ValueError("cloud_scope must be 'trunk' (Mix-G) or 'all' (CAPGAN)")
+        self.cloud_scope, self.segema, self.cloud_due = cloud_scope, float(segema), cloud_due
         n = comm.size if comm is not None else 1
         if n != step.n_workers:
             raise ValueError(f"step planned for {step.n_workers} workers, group has {n}")
 
     def round(self, r: int, graph: bool = True):
         s = self.step
+        if self.cloud is not None and self.cloud_due is not None and self.cloud_due(r):
+            self.cloud_average()
         if self.comm is None or self.comm.size == 1:
             s.run(C.PHASE_ALL, graph=graph)
         else:
@@ -126,7 +137,8 @@ class WorkerExchange:
             self.comm.all_reduce_mean(s.d_params)
         if self.dswap is not None and (r + 1) % self.swap_every == 0:
             self.comm.swap([s.d_params], self.dswap.next_perm())
-        if self.cloud is not None and self.cloud_every > 0 and (r + 1) % self.cloud_every == 0:
+        if (self.cloud is not None and self.cloud_due is None and self.cloud_every > 0 and
+                (r + 1) % self.cloud_every == 0):
             self.cloud_average()
 
     def cloud_average(self):
@@ -137,10 +149,32 @@ class WorkerExchange:
         if self.fedavg_compat_noop:
             self.cloud.all_reduce_sum(torch.zeros(1, device=self.step.g_params.device))
             return
-        p, r = self.step.trunk_slices()
-        self.cloud.all_reduce_mean(p, self.cloud_weights)
-        if r is not None:
-            self.cloud.all_reduce_mean(r, self.cloud_weights)
+        if self.cloud_scope == "trunk":
+            p, r = self.step.trunk_slices()
+        else:
+            p, r = self.step.g_params, None
+        for t in (p, r):
+            if t is None:
+                continue
+            own = t.clone() if self.segema != 0.0 else None
+            self.cloud.all_reduce_mean(t, self.cloud_weights)
+            if own is not None:     # segema * self_p + (1 - segema) * recv_p, in that order
+                torch.add(own * self.segema, t * (1.0 - self.segema), out=t)
+
+
+def mixg_cloud_due(num_communication: int, cloud_epoch: int):
+    """mixed-gan.py:193: the Cloud step runs before round r when t = num_communication - r satisfies
+    ``cloud_epoch != 0 and t % cloud_epoch == 0``."""
+    return lambda r: cloud_epoch != 0 and (num_communication - r) % cloud_epoch == 0
+
+
+def capgan_cloud_due(num_communication: int, data_len: float, cloud_epoch: int, batch_size: int):
+    """capgan.py:169: ``t % (self.data_len * cloud_epoch / batch_size) == 0`` with data_len the float32
+    tensor sum of the shard sizes (Server.run :152) -- evaluated in the same float32 arithmetic, so a
+    period that is not an integer never fires, as in the reference."""
+    period = torch.tensor(float(data_len), dtype=torch.float32) * cloud_epoch / batch_size
+    return lambda r: bool(torch.remainder(torch.tensor(float(num_communication - r), dtype=torch.float32),
+                                          period) == 0)
 
 
 class LocalComm:

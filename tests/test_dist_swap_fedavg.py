@@ -129,3 +129,51 @@ def test_cloud_fedavg_compat_noop():
     for r in res:
         tk = [k for k in r["sd"] if "running" not in k]
         assert torch.equal(r["p"], torch.cat([r["sd"][k].flatten() for k in tk]))
+
+
+class _GStep:
+    """CAPGAN server surface: every G parameter in one flat buffer (fedlab serialize_model order)."""
+
+    def __init__(self, G):
+        self.g_params = torch.cat([p.detach().flatten() for p in G.parameters()]).clone()
+        self.n_workers = 1
+
+    def run(self, *a, **k):
+        pass
+
+
+def _capgan_cloud_worker(rank, world, port, outdir, sizes, segema):
+    _init(rank, world, port)
+    try:
+        from cglgan.exchange import DistComm, WorkerExchange, capgan_cloud_due
+        G, _ = O.build_capgan(1, seed=300 + rank)
+        step = _GStep(G)
+        own = step.g_params.clone()
+        A = [s / sum(sizes) for s in sizes]
+        due = capgan_cloud_due(20, 400.0, 1, 100)    # period 4 rounds: fires before r = 0, 4, 8, ...
+        ex = WorkerExchange(step, None, cloud=DistComm(), cloud_weights=A, cloud_scope="all", segema=segema,
+                            cloud_due=due)
+        fired = []
+        for r in range(3):
+            before = step.g_params.clone()
+            ex.round(r)
+            fired.append(not torch.equal(before, step.g_params))
+        torch.save({"p": step.g_params, "own": own, "fired": fired}, os.path.join(outdir, f"r{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_capgan_cloud_fedavg_all_params_segema():
+    """capgan.py:169-175: fedavg_aggregate of every G parameter (data-size weights), mixed with segema,
+    before the rounds where t % (data_len * cloud_epoch / batch_size) == 0."""
+    world, sizes, segema = 2, [300, 100], 0.25
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(_capgan_cloud_worker, args=(world, _free_port(), td, sizes, segema), nprocs=world, join=True)
+        res = [torch.load(os.path.join(td, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    w = torch.tensor(sizes, dtype=torch.float32)
+    w = w / w.sum()
+    avg = res[0]["own"] * w[0] + res[1]["own"] * w[1]
+    for r in res:
+        assert r["fired"] == [True, False, False]
+        exp = segema * r["own"] + (1 - segema) * avg
+        assert torch.allclose(r["p"], exp, rtol=1e-6, atol=1e-7)
