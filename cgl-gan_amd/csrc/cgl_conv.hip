@@ -531,28 +531,43 @@ __global__ __launch_bounds__(256) void cgl_conv_n1(CglConvLaunch args) {
 // rows of one image in LDS (coalesced 16-byte loads, zero padding written explicitly), so every
 // input pixel is read from memory once per tile instead of once per tap; then L = Cin / 4 lanes per
 // output pixel read their channel slice of the 9 taps from LDS and combine by an xor tree.
+// C4T / WT: compile-time channel-quads / width (0: read from the descriptor) -- the G's Conv2d(64, 1)
+// at 32x32 runs the specialised instance, whose index arithmetic is shifts and constant divisions.
 #define CGL_N1T_TH 4
+template <int C4T, int WT>
 __global__ __launch_bounds__(256) void cgl_conv_n1_tile(CglConvLaunch args) {
   (void)args;
   extern __shared__ float cgl_conv_lds[];
   CglKL L = cgl_conv_args();
   CglKP P = &L->p[0];
-  const int Cin = P->Cin, W = P->OW, H = P->OH;
-  const int c4 = Cin >> 2, lanes = c4;          // c4 <= 64, power of two
+  const int W = WT ? WT : P->OW, H = P->OH;
+  const int c4 = C4T ? C4T : (P->Cin >> 2), lanes = c4;   // c4 <= 64, power of two
+  const int Cin = 4 * c4;
   const int tiles_y = (H + CGL_N1T_TH - 1) / CGL_N1T_TH;
   const int img = blockIdx.x / tiles_y, y0 = (blockIdx.x - img * tiles_y) * CGL_N1T_TH;
   const int HR = CGL_N1T_TH + 2, WR = W + 2;
   const float* __restrict__ X = P->X + (long)img * P->XH * P->XW * Cin;
-  // stage rows y0-1 .. y0+TH, cols -1 .. W (zero outside the image)
+  // stage rows y0-1 .. y0+TH, cols -1 .. W (zero outside the image): every load of the thread is
+  // issued first from a clamped (valid) address and zero-selected afterwards -- a load under a
+  // branch drains vmcnt per element and serialises the staging (tot4 <= 16 * 256 by the launch
+  // condition: LDS <= 64 KB)
   const int tot4 = HR * WR * c4;
-  for (int e = threadIdx.x; e < tot4; e += 256) {
-    const int q = e % c4, pix = e / c4;
+  f32x4 v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = min((int)threadIdx.x + 256 * k, tot4 - 1);
+    const int q = e & (c4 - 1), pix = e / c4;
     const int ry = pix / WR, rx = pix - ry * WR;
     const int iy = y0 - 1 + ry, ix = rx - 1;
-    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-    if ((unsigned)iy < (unsigned)P->XH && (unsigned)ix < (unsigned)P->XW)
-      v = *(gcf4p)(X + ((long)iy * P->XW + ix) * Cin + 4 * q);
-    *(f32x4*)&cgl_conv_lds[(long)pix * Cin + 4 * q] = v;
+    const bool ok = (unsigned)iy < (unsigned)P->XH && (unsigned)ix < (unsigned)P->XW;
+    const int cy = min(max(iy, 0), P->XH - 1), cx = min(max(ix, 0), P->XW - 1);
+    v[k] = *(gcf4p)(X + ((long)cy * P->XW + cx) * Cin + 4 * q);
+    if (!ok) v[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = (int)threadIdx.x + 256 * k;
+    if (e < tot4) *(f32x4*)&cgl_conv_lds[(long)(e / c4) * Cin + 4 * (e & (c4 - 1))] = v[k];
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -634,15 +649,17 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad_n1(CglConvLaunch args) {
 // tap t pairs it with the output-gradient pixel q - off_t (a broadcast scalar).  9 x 4 accumulators
 // per lane; the 256 / L pixel slots of a block are combined through LDS in a fixed order, giving
 // part[block][t * Cin + c] for the fixed-order split reduction.
+// C4T / XWT / XHT: compile-time channel quads and input width / height (0: from the descriptor).
+template <int C4T, int XWT, int XHT>
 __global__ __launch_bounds__(256) void cgl_conv_wgrad_n1t(CglConvLaunch args) {
   (void)args;
   __shared__ float red[16384];
   CglKL L = cgl_conv_args();
   CglKP P = &L->p[0];
-  const int Cin = P->Cin, Tx = P->Tx, T = P->Ty * P->Tx;
-  const int lanes = Cin >> 2, slots = 256 / lanes;
+  const int lanes = C4T ? C4T : (P->Cin >> 2), slots = 256 / lanes;
+  const int Cin = 4 * lanes, Tx = P->Tx, T = P->Ty * P->Tx;
   const int q4 = threadIdx.x & (lanes - 1), slot = threadIdx.x / lanes;
-  const int XH = P->XH, XW = P->XW, OH = P->OH, OW = P->OW;
+  const int XH = XHT ? XHT : P->XH, XW = XWT ? XWT : P->XW, OH = P->OH, OW = P->OW;
   const int hw = XH * XW;
   const long Min = (long)(P->M / (OH * OW)) * hw;
   const int splits = P->splits;
@@ -651,26 +668,41 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad_n1t(CglConvLaunch args) {
 #pragma unroll
   for (int t = 0; t < 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   const float* __restrict__ dY = P->Y;
-  for (long qq = qb + slot; qq < qe; qq += slots) {
-    const int img = (int)(qq / hw);
-    const int r = (int)(qq - (long)img * hw);
-    const int iy = r / XW, ix = r - iy * XW;
-    const f32x4 x = *(gcf4p)(P->X + qq * Cin + 4 * q4);
+  // two input pixels per step: both pixels' loads (1 float4 + T gathers each) are in flight before
+  // the first FMA; the pixels of a step are accumulated in order (fixed summation order)
+  for (long q0 = qb + slot; q0 < qe; q0 += 2 * slots) {
+    f32x4 x[2];
+    float d[2][16];
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      if (t < T) {
-        const int ty = t / Tx, tx = t - ty * Tx;
-        const int oy = iy - P->dy[ty], ox = ix - P->dx[tx];
-        const bool ok = (unsigned)oy < (unsigned)OH && (unsigned)ox < (unsigned)OW;
-        const float d = gld(dY + (((long)img * P->YH + min(max(oy, 0), OH - 1)) * P->YW + min(max(ox, 0), OW - 1)) *
-                                     P->ldy);
-        const float dd = ok ? d : 0.f;
-        acc[t][0] = fmaf(x[0], dd, acc[t][0]);
-        acc[t][1] = fmaf(x[1], dd, acc[t][1]);
-        acc[t][2] = fmaf(x[2], dd, acc[t][2]);
-        acc[t][3] = fmaf(x[3], dd, acc[t][3]);
+    for (int u = 0; u < 2; ++u) {
+      const long qq = min(q0 + u * slots, qe - 1);
+      const int img = (int)(qq / hw);
+      const int r = (int)(qq - (long)img * hw);
+      const int iy = r / XW, ix = r - iy * XW;
+      x[u] = *(gcf4p)(P->X + qq * Cin + 4 * q4);
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        if (t < T) {
+          const int ty = t / Tx, tx = t - ty * Tx;
+          const int oy = iy - P->dy[ty], ox = ix - P->dx[tx];
+          const bool ok = (unsigned)oy < (unsigned)OH && (unsigned)ox < (unsigned)OW && q0 + u * slots < qe;
+          const float dv = gld(dY + (((long)img * P->YH + min(max(oy, 0), OH - 1)) * P->YW +
+                                     min(max(ox, 0), OW - 1)) * P->ldy);
+          d[u][t] = ok ? dv : 0.f;
+        }
       }
     }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        if (t < T) {
+          acc[t][0] = fmaf(x[u][0], d[u][t], acc[t][0]);
+          acc[t][1] = fmaf(x[u][1], d[u][t], acc[t][1]);
+          acc[t][2] = fmaf(x[u][2], d[u][t], acc[t][2]);
+          acc[t][3] = fmaf(x[u][3], d[u][t], acc[t][3]);
+        }
+      }
   }
   const int K = T * Cin;
 #pragma unroll
@@ -1549,7 +1581,10 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
     const int nimg = P[0].M / (P[0].OH * P[0].OW);
     L.p[0] = P[0];
     const int lds = (CGL_N1T_TH + 2) * (P[0].OW + 2) * P[0].Cin * 4;
-    hipLaunchKernelGGL(cgl_conv_n1_tile, dim3(nimg * tiles_y), dim3(256), lds, s, L);
+    if (P[0].Cin == 64 && P[0].OW == 32)
+      hipLaunchKernelGGL((cgl_conv_n1_tile<16, 32>), dim3(nimg * tiles_y), dim3(256), lds, s, L);
+    else
+      hipLaunchKernelGGL((cgl_conv_n1_tile<0, 0>), dim3(nimg * tiles_y), dim3(256), lds, s, L);
     return (int)hipGetLastError();
   }
   if (N == 1 && n1_ok(P, np)) {
@@ -1699,7 +1734,12 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
     for (int k = 0; k < 4; ++k) { r.ym[i][k] = P.ym[k]; r.xm[i][k] = P.xm[k]; }
   }
   if (n1t)
-    hipLaunchKernelGGL(cgl_conv_wgrad_n1t, dim3(pl.P[0].splits), dim3(256), 0, s, L);
+  {
+    if (pl.P[0].Cin == 64 && pl.P[0].XW == 32 && pl.P[0].XH == 32)
+      hipLaunchKernelGGL((cgl_conv_wgrad_n1t<16, 32, 32>), dim3(pl.P[0].splits), dim3(256), 0, s, L);
+    else
+      hipLaunchKernelGGL((cgl_conv_wgrad_n1t<0, 0, 0>), dim3(pl.P[0].splits), dim3(256), 0, s, L);
+  }
   else if (valu)
     hipLaunchKernelGGL(cgl_conv_wgrad_n1, dim3((pl.P[0].K + 255) / 256, pl.P[0].splits), dim3(256), 0, s, L);
   else if (pl.t.TM == 2 && pl.t.TN == 2) hipLaunchKernelGGL((cgl_conv_wgrad<2, 2>), dim3(wg), dim3(256), 0, s, L);
