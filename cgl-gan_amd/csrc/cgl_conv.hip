@@ -307,6 +307,13 @@ __global__ __launch_bounds__(256) void cgl_conv_fwd(CglConvLaunch args) {
 // Work unit = one wave: (tile, split) with a (32 TM) x (32 TN) result tile; a workgroup runs 4
 // consecutive units (no LDS, no barriers), so small layers (Conv2d(1, 16): 16 x 9 results) do not
 // pay for a large workgroup tile.
+// Read-only zeros: operand loads of padded taps / pixels past M point here instead of being masked
+// after the load (saves the mask bookkeeping and the per-MFMA-operand selects of the k-loop).  The
+// loads index it with an output channel (< N) or an input channel (< Cin), so it covers
+// CGL_ZERO_PAGE floats; conv_bwd_weight_impl refuses larger layers (dense layers reach N = 8192).
+#define CGL_ZERO_PAGE 65536
+__device__ float cgl_zero_page[CGL_ZERO_PAGE];
+
 template <int TM, int TN>
 __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local) {
   constexpr int S = 2;
@@ -354,7 +361,8 @@ __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // masks: bit q (A, pixel valid), bit 8 + j * 8 + q (B, tap in bounds)
+  // operands of invalid pixels / out-of-bounds taps are loaded from cgl_zero_page (no masks)
+  const float* __restrict__ zp = cgl_zero_page;
   auto load = [&](int c, float (&A)[TM][8], float (&B)[TN][8], int& okm) {
     okm = 0;
     // decode the first pixel of this lane half once, then step along the row (wrapping)
@@ -375,30 +383,22 @@ __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local)
         if (!mv) { img = 0; oy = 0; ox = 0; }
       }
       const long ya = (((long)img * YH + oy * osy + ooy) * YW + ox * osx + oox) * ldy;
+      const float* ab = mv ? dY + ya : zp;
 #pragma unroll
-      for (int i = 0; i < TM; ++i) A[i][q] = ((gcfp)dY)[ya + rch[i]];
-      okm |= mv ? (1 << q) : 0;
+      for (int i = 0; i < TM; ++i) A[i][q] = ((gcfp)ab)[rch[i]];
       const long xo = (long)img * XH * XW * Cin;
       const int iyb = oy * isy, ixb = ox * isx;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int iy = iyb + cdy[j], ix = ixb + cdx[j];
         const bool ok = mv && cok[j] && (unsigned)iy < (unsigned)IH && (unsigned)ix < (unsigned)IW;
-        okm |= ok ? (1 << (8 + j * 8 + q)) : 0;
-        const int cy = min(max(iy, 0), IH - 1) >> ish, cx = min(max(ix, 0), IW - 1) >> ish;
-        B[j][q] = ((gcfp)X)[xo + ((long)cy * XW + cx) * Cin + cci[j]];
+        const float* bb = ok ? X + xo + ((long)(iy >> ish) * XW + (ix >> ish)) * Cin : zp;
+        B[j][q] = ((gcfp)bb)[cci[j]];
       }
     }
   };
   auto compute = [&](float (&A)[TM][8], float (&B)[TN][8], int okm) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const bool mv = (okm >> q) & 1;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) A[i][q] = mv ? A[i][q] : 0.f;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) B[j][q] = ((okm >> (8 + j * 8 + q)) & 1) ? B[j][q] : 0.f;
-    }
+    (void)okm;
 #pragma unroll
     for (int q = 0; q < 8; ++q)
 #pragma unroll
@@ -1699,6 +1699,7 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
                          int64_t wsb, hipStream_t s) {
   if (!dY || !X || !dW || !ws || !al16(ws)) return CGL_E_ARG;
   if (wsb < conv_ws_bytes(g)) return CGL_E_SIZE;
+  if (g.cout > CGL_ZERO_PAGE || g.cin > CGL_ZERO_PAGE) return CGL_E_ARG;   // cgl_zero_page bound
   WgradPlan pl = wgrad_plan(g);
   CglConvLaunch L;
   std::memset(&L, 0, sizeof(L));
