@@ -1629,7 +1629,7 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
 
 
 int chan_chunk(int64_t gr) {
-  int R = 256;
+  int R = 128;
   while (R > 1 && gr % R != 0) R >>= 1;
   return R;
 }
