@@ -22,7 +22,8 @@ def _threads():
 
 @pytest.mark.parametrize("kind,B,Br,epoch", [
     ("capgan", 64, 64, 1), ("capgan", 256, 256, 1), ("capgan", 100, 100, 1), ("capgan", 64, 40, 2),
-    ("mdgan", 64, 64, 1), ("ring", 64, 64, 1), ("mixg1", 64, 64, 1), ("mixg1", 256, 256, 1)])
+    ("mdgan", 64, 64, 1), ("mdgan", 512, 512, 1), ("ring", 64, 64, 1), ("mixg1", 64, 64, 1),
+    ("mixg1", 256, 256, 1)])
 def test_single_round_parity(kind, B, Br, epoch):
     """One round from identical state, judged against the fp64 oracle (see parity_helpers)."""
     failures, _ = check_single_round(kind, B, Br, epoch)
