@@ -314,7 +314,10 @@ __global__ __launch_bounds__(256) void cgl_conv_fwd(CglConvLaunch args) {
 #define CGL_ZERO_PAGE 65536
 __device__ float cgl_zero_page[CGL_ZERO_PAGE];
 
-template <int TM, int TN>
+// ROW: every problem of the launch has OW % 8 == 0 and M % 16 == 0, so the 8 pixels of a lane
+// half are always valid and lie in one output row: one pixel decode per chunk, constant address
+// strides along the row, the tap's row bounds checked once (a fraction of the generic path's VALU).
+template <int TM, int TN, bool ROW>
 __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local) {
   constexpr int S = 2;
   const int tid = threadIdx.x;
@@ -365,6 +368,31 @@ __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local)
   const float* __restrict__ zp = cgl_zero_page;
   auto load = [&](int c, float (&A)[TM][8], float (&B)[TN][8], int& okm) {
     okm = 0;
+    if (ROW) {
+      int img, oy, ox;
+      cgl_conv_pix(P, c * 16 + 8 * lh, img, oy, ox);
+      const float* ya0 = dY + (((long)img * YH + oy * osy + ooy) * YW + ox * osx + oox) * ldy;
+      const long ystep = (long)osx * ldy;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) A[i][q] = ((gcfp)(ya0 + q * ystep))[rch[i]];
+      const float* ximg = X + (long)img * XH * XW * Cin;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int iy = oy * isy + cdy[j];
+        const bool rowok = cok[j] && (unsigned)iy < (unsigned)IH;
+        const float* rb = ximg + (long)(rowok ? (iy >> ish) : 0) * XW * Cin + cci[j];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int ix = (ox + q) * isx + cdx[j];
+          const bool ok = rowok && (unsigned)ix < (unsigned)IW;
+          const float* bb = ok ? rb + (long)(ix >> ish) * Cin : zp + cci[j];
+          B[j][q] = *(gcfp)bb;
+        }
+      }
+      return;
+    }
     // decode the first pixel of this lane half once, then step along the row (wrapping)
     int img, oy, ox;
     cgl_conv_pix(P, min(c * 16 + 8 * lh, M - 1), img, oy, ox);
@@ -444,14 +472,14 @@ __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local)
   }
 }
 
-template <int TM, int TN>
+template <int TM, int TN, bool ROW = false>
 __global__ __launch_bounds__(256) void cgl_conv_wgrad(CglConvLaunch args) {
   (void)args;
   CglKL L = cgl_conv_args();
   const int bid = blockIdx.x;
   const int pi = cgl_conv_prob(L, bid);
   CglKP P = &L->p[pi];
-  cgl_conv_wgrad_body<TM, TN>(L, P, bid - P->wg_begin);
+  cgl_conv_wgrad_body<TM, TN, ROW>(L, P, bid - P->wg_begin);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1695,6 +1723,13 @@ int conv_bwd_data_impl(const ConvGeom& g, const float* dY, const float* W, float
   return launch_conv_mma(P, np, nullptr, CGL_EPI_ACT_NONE, 0.f, nullptr, s);
 }
 
+// the ROW fast path of cgl_conv_wgrad_body: whole 8-pixel row segments in every problem
+bool wgrad_row_ok(const WgradPlan& pl) {
+  for (int i = 0; i < pl.np; ++i)
+    if (pl.P[i].OW % 8 != 0 || pl.P[i].M % 16 != 0) return false;
+  return true;
+}
+
 int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, float* dW, float* db, void* ws,
                          int64_t wsb, hipStream_t s) {
   if (!dY || !X || !dW || !ws || !al16(ws)) return CGL_E_ARG;
@@ -1743,6 +1778,8 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
   }
   else if (valu)
     hipLaunchKernelGGL(cgl_conv_wgrad_n1, dim3((pl.P[0].K + 255) / 256, pl.P[0].splits), dim3(256), 0, s, L);
+  else if (pl.t.TM == 2 && pl.t.TN == 2 && wgrad_row_ok(pl))
+    hipLaunchKernelGGL((cgl_conv_wgrad<2, 2, true>), dim3(wg), dim3(256), 0, s, L);
   else if (pl.t.TM == 2 && pl.t.TN == 2) hipLaunchKernelGGL((cgl_conv_wgrad<2, 2>), dim3(wg), dim3(256), 0, s, L);
   else if (pl.t.TN == 2) hipLaunchKernelGGL((cgl_conv_wgrad<1, 2>), dim3(wg), dim3(256), 0, s, L);
   else if (pl.t.TM == 2) hipLaunchKernelGGL((cgl_conv_wgrad<2, 1>), dim3(wg), dim3(256), 0, s, L);
