@@ -1778,8 +1778,12 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
   }
   else if (valu)
     hipLaunchKernelGGL(cgl_conv_wgrad_n1, dim3((pl.P[0].K + 255) / 256, pl.P[0].splits), dim3(256), 0, s, L);
-  else if (pl.t.TM == 2 && pl.t.TN == 2 && wgrad_row_ok(pl))
-    hipLaunchKernelGGL((cgl_conv_wgrad<2, 2, true>), dim3(wg), dim3(256), 0, s, L);
+  else if (wgrad_row_ok(pl)) {
+    if (pl.t.TM == 2 && pl.t.TN == 2) hipLaunchKernelGGL((cgl_conv_wgrad<2, 2, true>), dim3(wg), dim3(256), 0, s, L);
+    else if (pl.t.TN == 2) hipLaunchKernelGGL((cgl_conv_wgrad<1, 2, true>), dim3(wg), dim3(256), 0, s, L);
+    else if (pl.t.TM == 2) hipLaunchKernelGGL((cgl_conv_wgrad<2, 1, true>), dim3(wg), dim3(256), 0, s, L);
+    else hipLaunchKernelGGL((cgl_conv_wgrad<1, 1, true>), dim3(wg), dim3(256), 0, s, L);
+  }
   else if (pl.t.TM == 2 && pl.t.TN == 2) hipLaunchKernelGGL((cgl_conv_wgrad<2, 2>), dim3(wg), dim3(256), 0, s, L);
   else if (pl.t.TN == 2) hipLaunchKernelGGL((cgl_conv_wgrad<1, 2>), dim3(wg), dim3(256), 0, s, L);
   else if (pl.t.TM == 2) hipLaunchKernelGGL((cgl_conv_wgrad<2, 1>), dim3(wg), dim3(256), 0, s, L);
