@@ -634,6 +634,84 @@ __global__ __launch_bounds__(256) void cgl_conv_n1_tile(CglConvLaunch args) {
   }
 }
 
+// Tap-partial form of the stride-1 3x3 Conv2d(64, 1) + Tanh at 32x32 (model/lsgan.py:19-20): the
+// input is read once per tile as a stream and each pixel is contracted with all 9 taps at once,
+// s_t(i) = sum_c X(i, c) W[0][c][t], leaving 9 floats per pixel in LDS; an output pixel is then
+// y(o) = sum_t s_t(o + d_t) (zero outside the image).  4 lanes own one input pixel (16 channels =
+// four 16-byte loads each; a wave's loads cover 16 whole pixels), so the channel reduction is two
+// xor steps; every load of a lane is issued before its first FMA.  A workgroup covers TH = 8 output
+// rows of one image: (TH + 2) / TH = 1.25 reads per input pixel, 12 KB of LDS.
+#define CGL_N1P_TH 8
+__global__ __launch_bounds__(256) void cgl_conv_n1_part(CglConvLaunch args) {
+  (void)args;
+  constexpr int W = 32, C = 64, TH = CGL_N1P_TH, HR = TH + 2, WR = W + 2, NP = HR * W / 64;
+  __shared__ float part[9][HR * WR];
+  CglKL L = cgl_conv_args();
+  CglKP P = &L->p[0];
+  const int H = P->OH;
+  const int tiles_y = (H + TH - 1) / TH;
+  const int img = blockIdx.x / tiles_y, y0 = (blockIdx.x - img * tiles_y) * TH;
+  const float* __restrict__ X = P->X + (long)img * H * W * C;
+  const int j = threadIdx.x & 3, g = threadIdx.x >> 2;       // lane in the pixel group, group 0..63
+  f32x4 x[NP][4];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int pix = k * 64 + g, ry = pix / W, rx = pix - ry * W;
+    const int iy = min(max(y0 - 1 + ry, 0), H - 1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[k][i] = *(gcf4p)(X + ((long)iy * W + rx) * C + 16 * j + 4 * i);
+  }
+  if (threadIdx.x < 2 * HR) {                                 // zero padding columns -1 and W
+    const int r = threadIdx.x >> 1, col = (threadIdx.x & 1) ? WR - 1 : 0;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) part[t][r * WR + col] = 0.f;
+  }
+  f32x4 w[9][4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[t][i] = *(gcf4p)(P->Wp + t * C + 16 * j + 4 * i);
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int pix = k * 64 + g, ry = pix / W, rx = pix - ry * W;
+    const bool ok = (unsigned)(y0 - 1 + ry) < (unsigned)H;
+    float sv[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      // pairwise over the lane's 16 channels (4 independent 4-term chains), then the 4-lane tree
+      float a4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a4[i] = x[k][i][0] * w[t][i][0];
+        a4[i] = fmaf(x[k][i][1], w[t][i][1], a4[i]);
+        a4[i] = fmaf(x[k][i][2], w[t][i][2], a4[i]);
+        a4[i] = fmaf(x[k][i][3], w[t][i][3], a4[i]);
+      }
+      float a = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+      a += __shfl_xor(a, 1);
+      a += __shfl_xor(a, 2);
+      sv[t] = ok ? a : 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+      if ((t & 3) == j) part[t][ry * WR + rx + 1] = sv[t];
+  }
+  __syncthreads();
+  const int ty = threadIdx.x / W, tx = threadIdx.x - ty * W;  // one output pixel per thread
+  float st[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) st[t] = part[t][(ty + t / 3) * WR + tx + t % 3];
+  const float acc = (((st[0] + st[1]) + (st[2] + st[3])) + ((st[4] + st[5]) + (st[6] + st[7]))) + st[8];
+  if (y0 + ty < H) {
+    float yv = acc + (L->bias ? gld(L->bias) : 0.f);
+    if (L->act == CGL_EPI_ACT_LEAKY) yv = yv > 0.f ? yv : yv * L->slope;
+    else if (L->act == CGL_EPI_ACT_TANH) yv = tanhf(yv);
+    else if (L->act == CGL_EPI_ACT_SIGMOID) yv = 1.f / (1.f + expf(-yv));
+    if (L->drop) yv *= gld(L->drop + (long)img * P->ldy);
+    gst(P->Y + (((long)img * P->YH + y0 + ty) * P->YW + tx) * P->ldy, yv);
+  }
+}
+
 // Weight gradient of a one-output-channel convolution (Conv2d(64, 1): 576 results reduced over every
 // output pixel) on the vector ALUs: thread = one im2col column k, pixels of the split in order, 8
 // loads in flight; partials part[split][0][k] for the fixed-order reduction.
@@ -678,10 +756,17 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad_n1(CglConvLaunch args) {
 // per lane; the 256 / L pixel slots of a block are combined through LDS in a fixed order, giving
 // part[block][t * Cin + c] for the fixed-order split reduction.
 // C4T / XWT / XHT: compile-time channel quads and input width / height (0: from the descriptor).
-template <int C4T, int XWT, int XHT>
+// The specialised instance (3x3 taps, host-checked) sizes its LDS reduction to 256 / L slots x 9 taps x
+// Cin = 36 KB (four workgroups per CU instead of two with the generic 64 KB) and keeps 4 input pixels
+// per slot in flight -- the kernel is a stream of X, so bytes in flight per CU set its rate.
+// STG > 0: the output-gradient window of the block's pixel range (linear dY indices qb - OW - 1 ..
+// qe + OW, host-checked to fit STG floats, dY dense with the input's height / width) is staged in LDS
+// once, so the T per-pixel gathers are LDS broadcasts instead of vector-memory instructions.
+template <int C4T, int XWT, int XHT, int CGL_N1T_PX, int REDN, int STG>
 __global__ __launch_bounds__(256) void cgl_conv_wgrad_n1t(CglConvLaunch args) {
   (void)args;
-  __shared__ float red[16384];
+  __shared__ float red[REDN];
+  __shared__ float win[STG ? STG : 1];
   CglKL L = cgl_conv_args();
   CglKP P = &L->p[0];
   const int lanes = C4T ? C4T : (P->Cin >> 2), slots = 256 / lanes;
@@ -696,13 +781,23 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad_n1t(CglConvLaunch args) {
 #pragma unroll
   for (int t = 0; t < 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   const float* __restrict__ dY = P->Y;
-  // two input pixels per step: both pixels' loads (1 float4 + T gathers each) are in flight before
-  // the first FMA; the pixels of a step are accumulated in order (fixed summation order)
-  for (long q0 = qb + slot; q0 < qe; q0 += 2 * slots) {
-    f32x4 x[2];
-    float d[2][16];
+  const long wb = qb - OW - 1;
+  if (STG) {
+    const long wl = (qe - qb) + 2 * OW + 2, Mo = P->M;
+    for (int i = threadIdx.x; i < wl; i += 256) {
+      const long lin = wb + i;
+      const float v = gld(dY + min(max(lin, 0L), Mo - 1));
+      win[i] = (lin >= 0 && lin < Mo) ? v : 0.f;
+    }
+    __syncthreads();
+  }
+  // CGL_N1T_PX input pixels per step: every pixel's loads (1 float4 + T gathers each) are in flight
+  // before the first FMA; the pixels of a step are accumulated in order (fixed summation order)
+  for (long q0 = qb + slot; q0 < qe; q0 += CGL_N1T_PX * slots) {
+    f32x4 x[CGL_N1T_PX];
+    float d[CGL_N1T_PX][16];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < CGL_N1T_PX; ++u) {
       const long qq = min(q0 + u * slots, qe - 1);
       const int img = (int)(qq / hw);
       const int r = (int)(qq - (long)img * hw);
@@ -714,14 +809,18 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad_n1t(CglConvLaunch args) {
           const int ty = t / Tx, tx = t - ty * Tx;
           const int oy = iy - P->dy[ty], ox = ix - P->dx[tx];
           const bool ok = (unsigned)oy < (unsigned)OH && (unsigned)ox < (unsigned)OW && q0 + u * slots < qe;
-          const float dv = gld(dY + (((long)img * P->YH + min(max(oy, 0), OH - 1)) * P->YW +
-                                     min(max(ox, 0), OW - 1)) * P->ldy);
+          float dv;
+          if (STG)
+            dv = win[(int)(qq - wb) - P->dy[ty] * OW - P->dx[tx]];
+          else
+            dv = gld(dY + (((long)img * P->YH + min(max(oy, 0), OH - 1)) * P->YW + min(max(ox, 0), OW - 1)) *
+                              P->ldy);
           d[u][t] = ok ? dv : 0.f;
         }
       }
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < CGL_N1T_PX; ++u)
 #pragma unroll
       for (int t = 0; t < 16; ++t) {
         if (t < T) {
@@ -741,6 +840,52 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad_n1t(CglConvLaunch args) {
     float v = 0.f;
     for (int sl = 0; sl < slots; ++sl) v += red[sl * K + k];
     gst(P->part + (long)blockIdx.x * P->Kp + k, v);
+  }
+}
+
+// Input gradient of a stride-1 3x3 one-output-channel convolution (Conv2d(64, 1, 3, 1, 1) + Tanh,
+// model/lsgan.py:19-20): dX(i, c) = sum_t dY(i - d_t) W[0][c][t], 9 FMAs per written element, so the
+// op is a write stream of dX.  C4 = Cin / 4 lanes own one input pixel (a float4 of channels: a wave's
+// stores cover 64 / C4 consecutive pixels, fully coalesced); the lane's 9 weight quads are read from
+// the reference's OIHW W once (no packing launch) and stay in registers; the 9 dY scalars are
+// broadcast reads of a 4 KB image (L1 / L2 hits).  Taps are summed in (ky, kx) order.
+#define CGL_BN1_PPT 8
+template <int C4>
+__global__ __launch_bounds__(256) void cgl_conv_bwd_n1(const float* __restrict__ dY, const float* __restrict__ W,
+                                                       float* __restrict__ dX, int npix, int H, int Wd) {
+  const int q = threadIdx.x & (C4 - 1);
+  f32x4 w[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[t][j] = gld(W + (4 * q + j) * 9 + t);
+  // CGL_BN1_PPT pixels per lane group (the weight loads amortised over them), consecutive groups of a
+  // workgroup on consecutive pixels
+#pragma unroll 2
+  for (int k = 0; k < CGL_BN1_PPT; ++k) {
+  const int p = (blockIdx.x * CGL_BN1_PPT + k) * (256 / C4) + (int)threadIdx.x / C4;
+  const int pc = min(p, npix - 1);
+  const int hw = H * Wd;
+  const int img = pc / hw, r = pc - img * hw;
+  const int y = r / Wd, x = r - y * Wd;
+  const float* __restrict__ d = dY + (long)img * hw;
+  float dv[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int oy = y + 1 - t / 3, ox = x + 1 - t % 3;
+    const bool ok = (unsigned)oy < (unsigned)H && (unsigned)ox < (unsigned)Wd;
+    const float v = gld(d + min(max(oy, 0), H - 1) * Wd + min(max(ox, 0), Wd - 1));
+    dv[t] = ok ? v : 0.f;
+  }
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    acc[0] = fmaf(dv[t], w[t][0], acc[0]);
+    acc[1] = fmaf(dv[t], w[t][1], acc[1]);
+    acc[2] = fmaf(dv[t], w[t][2], acc[2]);
+    acc[3] = fmaf(dv[t], w[t][3], acc[3]);
+  }
+  if (p < npix) *(gf4p)(dX + (long)p * (4 * C4) + 4 * q) = acc;
   }
 }
 
@@ -1609,6 +1754,10 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
     const int nimg = P[0].M / (P[0].OH * P[0].OW);
     L.p[0] = P[0];
     const int lds = (CGL_N1T_TH + 2) * (P[0].OW + 2) * P[0].Cin * 4;
+    if (P[0].Cin == 64 && P[0].OW == 32 && P[0].YW == 32 && P[0].YH == P[0].OH && !getenv("CGL_N1_TILE")) {
+      hipLaunchKernelGGL(cgl_conv_n1_part, dim3(nimg * ((P[0].OH + CGL_N1P_TH - 1) / CGL_N1P_TH)), dim3(256), 0, s, L);
+      return (int)hipGetLastError();
+    }
     if (P[0].Cin == 64 && P[0].OW == 32)
       hipLaunchKernelGGL((cgl_conv_n1_tile<16, 32>), dim3(nimg * tiles_y), dim3(256), lds, s, L);
     else
@@ -1712,6 +1861,12 @@ int conv_bwd_data_impl(const ConvGeom& g, const float* dY, const float* W, float
   if (!dY || !W || !dX || !ws || !al16(ws)) return CGL_E_ARG;
   if (wsb < conv_ws_bytes(g)) return CGL_E_SIZE;
   if ((g.cout % 4 == 0) && !al16(dY)) return CGL_E_ARG;
+  if (g.cout == 1 && g.cin == 64 && g.ks == 3 && g.stride == 1 && !g.up && al16(dX) &&
+      (int64_t)g.n * g.h * g.w < (int64_t)1 << 30) {
+    const int npix = g.n * g.h * g.w;
+    hipLaunchKernelGGL((cgl_conv_bwd_n1<16>), dim3((npix + 16 * CGL_BN1_PPT - 1) / (16 * CGL_BN1_PPT)), dim3(256), 0, s, dY, W, dX, npix, g.h, g.w);
+    return (int)hipGetLastError();
+  }
   CglConvProb P[CGL_CONV_MAXP];
   const int np = bwd_probs(g, P);
   for (int i = 0; i < np; ++i) {
@@ -1771,10 +1926,19 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
   }
   if (n1t)
   {
-    if (pl.P[0].Cin == 64 && pl.P[0].XW == 32 && pl.P[0].XH == 32)
-      hipLaunchKernelGGL((cgl_conv_wgrad_n1t<16, 32, 32>), dim3(pl.P[0].splits), dim3(256), 0, s, L);
+    if (pl.P[0].Cin == 64 && pl.P[0].XW == 32 && pl.P[0].XH == 32 && pl.P[0].Ty * pl.P[0].Tx == 9)
+    {
+      const CglConvProb& P0 = pl.P[0];
+      const long per_block = ((long)(P0.M / (P0.OH * P0.OW)) * P0.XH * P0.XW + P0.splits - 1) / P0.splits;
+      const bool stage = P0.YH == P0.OH && P0.YW == P0.OW && P0.ldy == 1 && P0.OH == 32 && P0.OW == 32 &&
+                         per_block + 2 * P0.OW + 2 <= 512;
+      // one pixel per slot and step, dY window in LDS: 105 -> 57 us for the B=256 G Conv2d(64, 1)
+      // (two / four pixels per step: 77 / 119 us; no staging: 90 us)
+      if (stage) hipLaunchKernelGGL((cgl_conv_wgrad_n1t<16, 32, 32, 1, 9216, 512>), dim3(P0.splits), dim3(256), 0, s, L);
+      else hipLaunchKernelGGL((cgl_conv_wgrad_n1t<16, 32, 32, 1, 9216, 0>), dim3(P0.splits), dim3(256), 0, s, L);
+    }
     else
-      hipLaunchKernelGGL((cgl_conv_wgrad_n1t<0, 0, 0>), dim3(pl.P[0].splits), dim3(256), 0, s, L);
+      hipLaunchKernelGGL((cgl_conv_wgrad_n1t<0, 0, 0, 2, 16384, 0>), dim3(pl.P[0].splits), dim3(256), 0, s, L);
   }
   else if (valu)
     hipLaunchKernelGGL(cgl_conv_wgrad_n1, dim3((pl.P[0].K + 255) / 256, pl.P[0].splits), dim3(256), 0, s, L);

@@ -61,6 +61,8 @@ CONV_CASES = [
     (2, 7, 7, 32, 64, 2, 0, 1),       # D on 28x28 inputs (odd sizes 7 -> 4)
     (2, 9, 7, 32, 48, 1, 0, 0),       # generic stride 1, ragged tiles
     (1, 5, 3, 16, 16, 1, 1, 1),       # ragged upsample
+    (3, 7, 9, 64, 1, 1, 0, 2),        # one-output-channel conv, ragged (189 pixels: partial workgroups)
+    (2, 20, 32, 64, 1, 1, 0, 2),      # tap-partial Conv2d(64, 1) with a partial 8-row tile
 ]
 
 
