@@ -489,6 +489,9 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad(CglConvLaunch args) {
 // float4 of channels each, so a wave's load covers 64 / L whole pixel vectors, fully coalesced),
 // the lane's slice of every tap's weights stays in registers, and the L partial sums are combined
 // by an xor tree (fixed order).  Requires Cin % 4 == 0, Cin / 4 a power of two <= 64, <= 16 taps.
+// iterations per wave: each iteration's loads wait on the previous one's, so the D Conv2d(1, 16) input
+// gradient (512 workgroups at 8) ran latency-serialised; 2 gives 4x the workgroups
+#define CGL_N1_IT 2
 __global__ __launch_bounds__(256) void cgl_conv_n1(CglConvLaunch args) {
   (void)args;
   CglKL L = cgl_conv_args();
@@ -511,9 +514,9 @@ __global__ __launch_bounds__(256) void cgl_conv_n1(CglConvLaunch args) {
   }
   const float bias = L->bias ? gld(L->bias) : 0.f;
   const int M = P->M;
-  const int per_wg = 4 * ppw * 8;              // 8 iterations of every wave per workgroup
+  const int per_wg = 4 * ppw * CGL_N1_IT;      // CGL_N1_IT iterations of every wave per workgroup
   const int m_begin = (bid - P->wg_begin) * per_wg;
-  for (int it = 0; it < 8; ++it) {
+  for (int it = 0; it < CGL_N1_IT; ++it) {
     const int m = m_begin + (it * 4 + wave) * ppw + slot;
     const bool mv = m < M;
     int img, oy, ox;
@@ -1899,7 +1902,7 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
     int wg = 0;
     for (int i = 0; i < np; ++i) {
       const int c4 = P[i].Cin / 4, lanes = c4 < 64 ? c4 : 64;
-      const int per_wg = 4 * (64 / lanes) * 8;
+      const int per_wg = 4 * (64 / lanes) * CGL_N1_IT;
       P[i].wg_begin = wg;
       wg += (P[i].M + per_wg - 1) / per_wg;
       L.p[i] = P[i];
