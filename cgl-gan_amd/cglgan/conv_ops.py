@@ -28,10 +28,12 @@ def _s():
 
 
 def workspace(nbytes: int, device) -> torch.Tensor:
-    """Per-device scratch owned by the caching allocator (grown on demand; ops on one stream are
-    ordered, so one buffer serves every op)."""
+    """Scratch owned by the caching allocator, one buffer per (device, stream): ops issued on one
+    stream are ordered, so they share it; ops on another stream (a side-stream round beside the
+    drop-in modules, two-stream overlap) get their own and never race on it.  Grown on demand."""
     dev = torch.device(device)
-    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    key = (idx, torch.cuda.current_stream(idx).cuda_stream)
     w = _WS.get(key)
     if w is None or w.numel() < nbytes:
         w = torch.empty(max(int(nbytes), 1 << 20), dtype=torch.uint8, device=dev)

@@ -140,7 +140,7 @@ class ConvGanStep:
     """Fused CAPGAN worker round of the model/lsgan.py GAN (see module docstring)."""
 
     def __init__(self, batch, loss="mse", data=None, seed=20211212, n_workers=1, rank=0, weighting="capgan",
-                 lr=2e-4, betas=(0.5, 0.999), adam_eps=1e-8, gen_z=True, device="cuda"):
+                 lr=2e-4, betas=(0.5, 0.999), adam_eps=1e-8, gen_z=True, beta=None, device="cuda"):
         if loss not in ("mse", "bce"):
             raise ValueError("loss must be 'mse' (LSGAN) or 'bce' (Sigmoid + BCELoss)")
         if batch < 2:
@@ -178,7 +178,8 @@ class ConvGanStep:
         self.lbuf = e(8)                       # d_real, d_fake, g_loss
         self.losses_all = e(max(n_workers, 1))
         self.lam = 0.0
-        self.beta = [1.0 / n_workers] * n_workers
+        self.beta = None
+        self.set_beta(beta)
         self.round = 0
         # sampler over a device-resident real shard [n, 1024] (DataLoader(shuffle=True), capgan.py:282)
         self.data = data
@@ -191,6 +192,14 @@ class ConvGanStep:
                 raise ValueError("data must be float32 on the GPU")
 
     # ------------------------------------------------------------------ state
+    def set_beta(self, beta=None):
+        """Data-size weights of the CAPGAN alpha (capgan.py:149-153: beta_c = len(shard_c) / sum; see
+        cglgan.data.beta_weights); None = equal shards (1 / N each)."""
+        b = [1.0 / self.n_workers] * self.n_workers if beta is None else [float(x) for x in beta]
+        if len(b) != self.n_workers:
+            raise ValueError(f"beta needs one weight per worker ({self.n_workers})")
+        self.beta = b
+
     def init_default(self, seed_g=20211212, seed_d=None):
         """capgan.py:28,156,309: torch.manual_seed(seed) then G (and D) constructed."""
         torch.manual_seed(seed_g)

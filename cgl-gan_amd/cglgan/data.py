@@ -133,6 +133,71 @@ def eval_subsample(x: torch.Tensor, num_sample: int):
     return x[::max(1, x.shape[0] // num_sample)]
 
 
+def gmm(num_class: int = 5, x: int = 10000, np_seed: int = SEED, generator: torch.Generator | None = None,
+        device=None):
+    """The 2-D Gaussian-mixture ring of CGLGAN/2DMG/data.py:5-38 (``gmm(n_class, x).data / .targets``):
+    ``num_class`` modes at theta = linspace(0, 2 pi (1 - 1/n), n) on the unit circle (x = sin, y = cos),
+    std 0.01, ``x * num_class`` points whose modes are drawn one by one with numpy's legacy generator
+    (the reference seeds numpy's global generator with 20211212 at import, data.py:4 -- reproduced by
+    ``np_seed``) and whose coordinates are one ``torch.normal`` call of 2 values per point from the
+    torch CPU generator (the global one, as the reference, unless ``generator`` is given); then sorted by
+    label with ``torch.sort``.  Returns ``(data [n, 2] float32, targets [n] float32)``.
+
+    The draws are made on the host because their order IS the format (the same points as the
+    reference for the same seeds: pinned by the sha256 in tests/golden/golden_steps.json ``ring_b64``);
+    the result is moved to ``device`` once.  Generation is init-time work, not the round's hot path."""
+    rs = np.random.RandomState(np_seed)
+    thetas = np.linspace(0, 2 * (1 - 1 / num_class) * np.pi, num_class)
+    xs, ys = np.sin(thetas), np.cos(thetas)
+    n = x * num_class
+    data = torch.zeros(n, 2)
+    labels = torch.zeros(n)
+    std = 0.01 * torch.ones(1, 2)
+    means = [torch.Tensor([xs[c], ys[c]]) for c in range(num_class)]
+    for i in range(n):
+        coin = rs.randint(0, num_class)
+        data[i, :] = torch.normal(mean=means[coin], std=std, generator=generator)
+        labels[i] = coin
+    targets, order = torch.sort(labels)
+    data = data[order]
+    if device is not None:
+        data, targets = data.to(device), targets.to(device)
+    return data, targets
+
+
+def synthetic_mnist(n: int, num_class: int = 10, seed: int = 1, noise: float = 0.35, img_dim: int = 784,
+                    device=None):
+    """A labelled MNIST-shaped dataset for the driver and the benchmarks (there is no MNIST on these
+    hosts): ``num_class`` fixed random prototype images, each sample = its class prototype
+    + uniform noise, clamped to [-1, 1] (the range Normalize([0.5], [0.5]) gives, capgan.py:469).
+    Labels are uniform, so ``allocate_dataset`` produces the reference's IID / non-IID shard shapes
+    (SURVEY 8d C5).  Returns ``(images [n, img_dim] float32, labels [n] int64)``."""
+    g = torch.Generator().manual_seed(seed)
+    protos = torch.rand(num_class, img_dim, generator=g) * 2 - 1
+    labels = torch.randint(0, num_class, (n,), generator=g)
+    imgs = (protos[labels] + noise * (torch.rand(n, img_dim, generator=g) * 2 - 1)).clamp_(-1.0, 1.0)
+    if device is not None:
+        imgs, labels = imgs.to(device), labels.to(device)
+    return imgs, labels
+
+
+def sample_batches(shard: torch.Tensor, batch: int, count: int, seed: int):
+    """``count`` real batches of ``batch`` rows drawn from a shard with DataLoader(shuffle=True,
+    drop_last=False) semantics (capgan.py:282, 326-332): a fresh permutation per pass over the shard,
+    the pass's last batch possibly short.  Host-side helper for explicit-input rounds (tests, driver
+    replays); the fused round samples on the device."""
+    g = torch.Generator().manual_seed(seed)
+    n = shard.shape[0]
+    out, perm, pos = [], torch.randperm(n, generator=g), 0
+    while len(out) < count:
+        if pos >= n:
+            perm, pos = torch.randperm(n, generator=g), 0
+        idx = perm[pos:pos + batch]
+        pos += batch
+        out.append(shard[idx.to(shard.device)])
+    return out
+
+
 def device_shard(images: torch.Tensor, idx, device="cuda") -> torch.Tensor:
     """One worker's shard resident in HBM as the fused rounds read it: [len, features] float32 rows
     of ``images`` (any [n, ...] tensor) in shard order, gathered once (the rounds then sample it

@@ -179,31 +179,40 @@ def capgan_cloud_due(num_communication: int, data_len: float, cloud_epoch: int, 
 
 class LocalComm:
     """N in-process workers in lockstep: the collectives of ``WorkerExchange`` computed over the
-    workers' buffers with a fixed summation order (rank 0 .. N-1)."""
+    workers' buffers with a fixed summation order (rank 0 .. N-1) -- the single-GPU rehearsal of a
+    server group.  ``share_every``: E-share of D (a19); ``swap_every``: the MD-GAN D-swap
+    with the server's ``DSwap`` permutation (MDGAN/MNIST/mdgan.py:158-164), moving the D parameters
+    only, as ``WorkerExchange`` does (each worker keeps its own Adam state)."""
 
-    def __init__(self, steps):
+    def __init__(self, steps, share_every: int = 0, swap_every: int = 0, server_rank: int = 0):
         self.steps = steps
         self.size = len(steps)
+        self.share_every, self.swap_every = share_every, swap_every
+        self.dswap = DSwap(self.size, server_rank) if swap_every > 0 else None
+        for s in steps:
+            if s.n_workers != self.size:
+                raise ValueError(f"step planned for {s.n_workers} workers, group has {self.size}")
 
-    def round(self, r: int, graph: bool = False, share_every: int = 0):
+    def round(self, r: int, graph: bool = False, share_every: int = None):
         ss = self.steps
+        share_every = self.share_every if share_every is None else share_every
         if self.size == 1:
             ss[0].run(C.PHASE_ALL, graph=graph)
-            return
-        for s in ss:
-            s.run(C.PHASE_A, graph=graph)
-        losses = torch.cat([s.own_loss() for s in ss])
-        for s in ss:
-            s.losses_all.copy_(losses)
-            s.alpha_scale()
-        bufs = [s.exchange_buffer() for s in ss]
-        tot = bufs[0].clone()
-        for b in bufs[1:]:
-            tot += b
-        for b in bufs:
-            b.copy_(tot)
-        for s in ss:
-            s.run(C.PHASE_B, graph=graph)
+        else:
+            for s in ss:
+                s.run(C.PHASE_A, graph=graph)
+            losses = torch.cat([s.own_loss() for s in ss])
+            for s in ss:
+                s.losses_all.copy_(losses)
+                s.alpha_scale()
+            bufs = [s.exchange_buffer() for s in ss]
+            tot = bufs[0].clone()
+            for b in bufs[1:]:
+                tot += b
+            for b in bufs:
+                b.copy_(tot)
+            for s in ss:
+                s.run(C.PHASE_B, graph=graph)
         if share_every > 0 and (r + 1) % share_every == 0:
             tot = ss[0].d_params.clone()
             for s in ss[1:]:
@@ -211,6 +220,37 @@ class LocalComm:
             tot /= self.size
             for s in ss:
                 s.d_params.copy_(tot)
+        if self.dswap is not None and (r + 1) % self.swap_every == 0:
+            perm = self.dswap.next_perm()
+            old = [s.d_params.clone() for s in ss]
+            for i, s in enumerate(ss):      # worker i continues with D_{perm[i]}
+                s.d_params.copy_(old[perm[i]])
+            return perm
+        return None
+
+
+def local_cloud_average(steps, weights, cloud_scope: str = "trunk", segema: float = 0.0,
+                        fedavg_compat_noop: bool = False):
+    """``WorkerExchange.cloud_average`` over in-process workers (the cloud group = ``steps``, one
+    weight per member, e.g. A_s / group size for every replica of server s's trunk): every member
+    ends with sum_i w_i t_i (fixed order 0 .. n-1), mixed with segema as mixed-gan.py:198-199."""
+    if fedavg_compat_noop:
+        return
+    if len(weights) != len(steps):
+        raise ValueError("one cloud weight per member")
+    parts = [s.trunk_slices() if cloud_scope == "trunk" else (s.g_params, None) for s in steps]
+    for which in (0, 1):
+        ts = [p[which] for p in parts]
+        if ts[0] is None:
+            continue
+        tot = ts[0] * float(weights[0])
+        for w, t in zip(weights[1:], ts[1:]):
+            tot += t * float(w)
+        for t in ts:
+            if segema != 0.0:
+                torch.add(t * segema, tot * (1.0 - segema), out=t)
+            else:
+                t.copy_(tot)
 
 
 class ConvWorkerExchange:

@@ -44,3 +44,80 @@ def weights_init(model: MlpModel, views, generator=None):
             torch.nn.init.normal_(g, 1.0, 0.02, generator=generator)
             views[model.bn_keys[l] + ".weight"].copy_(g)
             views[model.bn_keys[l] + ".bias"].fill_(0.0)
+
+
+def _views_of(model: MlpModel, out=None):
+    """CPU tensors, one per state-dict key of ``model`` (shapes of cgl_gan_param_tensor)."""
+    out = {} if out is None else out
+    for l in range(model.n_layers):
+        fo, fi = model.dims[l + 1], model.dims[l]
+        out.setdefault(model.linear_keys[l] + ".weight", torch.zeros(fo, fi))
+        out.setdefault(model.linear_keys[l] + ".bias", torch.zeros(fo))
+        if model.bn[l]:
+            out.setdefault(model.bn_keys[l] + ".weight", torch.zeros(fo))
+            out.setdefault(model.bn_keys[l] + ".bias", torch.zeros(fo))
+    return out
+
+
+def _trunk_and_heads(n_heads, img_dim, z_dim):
+    from .specs import MIXGEN_HEAD_LAYER, mixgen_worker
+    trunk = mixgen_worker(0, img_dim, z_dim)
+    cut = MIXGEN_HEAD_LAYER
+    t = MlpModel("mixgen_trunk", trunk.dims[:cut + 1], trunk.bn[:cut], trunk.linear_keys[:cut], trunk.bn_keys[:cut])
+    heads = []
+    for h in range(n_heads):
+        w = mixgen_worker(h, img_dim, z_dim)
+        heads.append(MlpModel(f"mixgen_head{h}", w.dims[cut:], w.bn[cut:], w.linear_keys[cut:], w.bn_keys[cut:]))
+    return t, heads
+
+
+def capgan_state(n_workers: int = 1, seed: int = 20211212, sigmoid: bool = False, img_dim: int = 784,
+                 z_dim: int = 100):
+    """``torch.manual_seed(seed); net_g = Generator(ims)`` then one ``Discriminator(ims)`` per worker
+    with torch's default init (capgan.py:28,156,309; MDGAN/MNIST/mdgan.py for ``sigmoid``), drawn from
+    the global CPU generator in construction order.  Returns ``(G params, [D params])`` keyed by the
+    reference's state-dict keys (BatchNorm buffers start at 0 / 1, which ``GanStep.reset`` sets)."""
+    from .specs import mnist_discriminator, mnist_generator
+    torch.manual_seed(seed)
+    gm = mnist_generator(img_dim, z_dim)
+    g = _views_of(gm)
+    default_init(gm, g)
+    ds = []
+    for _ in range(n_workers):
+        dm = mnist_discriminator(img_dim, sigmoid)
+        d = _views_of(dm)
+        default_init(dm, d)
+        ds.append(d)
+    return g, ds
+
+
+def mixgen_state(n_heads: int, seed: int = 20211212, img_dim: int = 784, z_dim: int = 100,
+                 n_discriminators: int = 0):
+    """``torch.manual_seed(seed); net_g = MixGenerator(ims, N); net_g.apply(weights_init)``
+    (mixed-gan.py:34,180-181; model/mnist_model.py:32-56): the full generator (trunk ``model.*`` +
+    every head ``paths.h.*``) with the reference's draw order -- nn.Linear's default draws at
+    construction (trunk layers, then head 0, 1, ...), then weights_init's draws in Module.apply's
+    post-order, which visits the same layers in the same order.  With ``n_discriminators`` > 0 the
+    workers' ``Discriminator(ims).apply(weights_init)`` (mixed-gan.py:347-348) follow, each default-
+    constructed then re-initialised.  Returns ``(G params, [D params])``; a worker's ``mixgen_worker(h)``
+    step loads the trunk and its own head from the G dict."""
+    from .specs import mnist_discriminator
+    torch.manual_seed(seed)
+    trunk, heads = _trunk_and_heads(n_heads, img_dim, z_dim)
+    g = _views_of(trunk)
+    for h in heads:
+        _views_of(h, g)
+    default_init(trunk, g)
+    for h in heads:
+        default_init(h, g)
+    weights_init(trunk, g)
+    for h in heads:
+        weights_init(h, g)
+    ds = []
+    for _ in range(n_discriminators):
+        dm = mnist_discriminator(img_dim)
+        d = _views_of(dm)
+        default_init(dm, d)
+        weights_init(dm, d)
+        ds.append(d)
+    return g, ds

@@ -40,8 +40,10 @@ _WS = {}
 
 
 def _ws(dev):
-    """Per-device op workspace (descriptor upload area) owned by the caching allocator."""
-    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    """Op workspace (descriptor upload area) owned by the caching allocator, one per (device, stream):
+    stream-ordered ops share it, ops on another stream never race on it."""
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    key = (idx, torch.cuda.current_stream(idx).cuda_stream)
     w = _WS.get(key)
     if w is None:
         w = torch.empty(C.lib.cgl_op_workspace_bytes(), dtype=torch.uint8, device=dev)

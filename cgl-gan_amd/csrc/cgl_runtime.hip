@@ -1237,6 +1237,14 @@ int cgl_gan_tensor(cgl_gan* c, int which, float** ptr, int64_t* n) {
   } else if (which >= 96 && which < 96 + L) {       // saved BN invstd [2][dims[l+1]]
     *ptr = c->ws.ginvstd[which - 96];
     *n = (int64_t)2 * g.dims[which - 96 + 1];
+  } else if (which >= 112 && which < 112 + c->cfg.d.n_layers - 1) {   // D-step hidden activation P[j]
+    const int j = which - 112;                                        // (Br + B rows, last local D step)
+    *ptr = c->ws.P[j];
+    *n = (int64_t)(c->cfg.batch_real + B) * c->cfg.d.dims[j + 1];
+  } else if (which >= 128 && which < 128 + c->cfg.d.n_layers - 1) {   // G-loss pass hidden activation S[j]
+    const int j = which - 128;                                        // (B rows, through the updated D)
+    *ptr = c->ws.S[j];
+    *n = (int64_t)B * c->cfg.d.dims[j + 1];
   } else {
     return CGL_E_ARG;
   }

@@ -131,7 +131,10 @@ int cgl_gan_exchange_buffer(cgl_gan* ctx, float** ptr, int64_t* n);
 /* Device pointer of an internal tensor: 0 = G output [2B][img] (Xd rows then Xg rows),
  * 1 = own G-loss scalar, 2 = gradient at the G output [B][img] (after Tanh'),
  * 16+l / 32+l = gradient w.r.t. layer l's activation / Linear output [B][dims[l+1]] (Xg rows),
- * 48+l / 64+l = layer l's BN+LeakyReLU output / Linear output [2B][dims[l+1]]. */
+ * 48+l / 64+l = layer l's BN+LeakyReLU output / Linear output [2B][dims[l+1]],
+ * 80+l / 96+l = saved BN batch mean / invstd [2][dims[l+1]],
+ * 112+j = D hidden layer j's LeakyReLU output of the (last) local D step [Br+B][d.dims[j+1]],
+ * 128+j = the same for the G-loss pass through the updated D [B][d.dims[j+1]]. */
 int cgl_gan_tensor(cgl_gan* ctx, int which, float** ptr, int64_t* n);
 /* Synchronous copy of the round scalars to the host. */
 int cgl_gan_read_stats(cgl_gan* ctx, cgl_gan_stats* out, void* stream);

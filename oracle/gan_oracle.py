@@ -133,6 +133,12 @@ class SeqNet:
                 self.buffers[key + ".num_batches_tracked"] = torch.tensor(0, dtype=torch.long)
         for p in self.params.values():
             p.requires_grad_(True)
+        # test hooks (unset = the plain reference arithmetic): ``mask_feed`` -- per forward call, one
+        # bool tensor per LeakyReLU (x > 0) imposed instead of the sign of this run's own x, so that a
+        # comparison run can follow another implementation's branch decisions at the kink;
+        # ``trace_sink`` -- a list collecting every LeakyReLU input (see ``forward``)
+        self.mask_feed = []
+        self.trace_sink = None
 
     # weights_init of mixed-gan.py:68-77 (Linear W~N(0,.02), b=0; BN g~N(1,.02), b=0),
     # applied in nn.Module.apply's post-order == spec order for a flat Sequential.
@@ -146,15 +152,27 @@ class SeqNet:
                     torch.nn.init.normal_(self.params[ent[1] + ".weight"], 1.0, 0.02, generator=generator)
                     torch.nn.init.constant_(self.params[ent[1] + ".bias"], 0)
 
-    def forward(self, x, train=True, trace=None):
+    def forward(self, x, train=True, trace=None, masks=None):
         """nn.Sequential forward of the spec (train-mode BatchNorm updates running stats).
 
-        ``trace`` (a list) collects the input of every LeakyReLU (conditioning checks in tests)."""
+        ``trace`` (a list) collects the input of every LeakyReLU (conditioning checks in tests).
+        ``masks``: one bool tensor per LeakyReLU, the branch taken (x > 0); by default the next entry
+        of ``mask_feed`` if any, else the sign of x itself (= F.leaky_relu, the reference)."""
         h = x.reshape(x.shape[0], -1)
+        if masks is None and self.mask_feed:
+            masks = self.mask_feed.pop(0)
+        if trace is None:
+            trace = self.trace_sink
+        li = 0
         for ent in self.spec:
             if trace is not None and ent[0] == "leaky":
                 trace.append(h.detach())
             kind = ent[0]
+            if kind == "leaky" and masks is not None:
+                m = masks[li].to(h.device).reshape(h.shape)
+                h = torch.where(m, h, h * SLOPE)
+                li += 1
+                continue
             if kind == "linear":
                 h = F.linear(h, self.params[ent[1] + ".weight"], self.params[ent[1] + ".bias"])
             elif kind == "bn":
@@ -487,6 +505,32 @@ def fedavg(state_dicts, data_lens, segema=0.0, self_sd=None):
         for key in p:
             p[key] = segema * self_sd[key] + (1 - segema) * p[key]
     return p
+
+
+@torch.no_grad()
+def eshare_mean(workers):
+    """E-share of D: every worker's D <- the mean of the N discriminators,
+    summed in worker order.  The only reference code for it is commented out and broken
+    (ACGAN/MNIST/acgan.py:240-263), so this is the build's definition: parity unpinned."""
+    n = len(workers)
+    for k in workers[0].D.params:
+        tot = workers[0].D.params[k].detach().clone()
+        for w in workers[1:]:
+            tot += w.D.params[k]
+        tot /= n
+        for w in workers:
+            w.D.params[k].copy_(tot)
+
+
+@torch.no_grad()
+def dswap(workers, perm):
+    """MD-GAN D-swap (MDGAN/MNIST/mdgan.py:158-164 with copy_parameters :233-238, commented out in
+    the reference: parity unpinned): worker i continues with D_{perm[i]}'s parameters and keeps its
+    own optimiser state."""
+    old = [{k: v.detach().clone() for k, v in w.D.params.items()} for w in workers]
+    for i, w in enumerate(workers):
+        for k, v in w.D.params.items():
+            v.copy_(old[perm[i]][k])
 
 
 def capgan_alpha(lam, losses, beta):

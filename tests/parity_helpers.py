@@ -231,3 +231,83 @@ def check_single_round(kind, B, Br=None, epoch=1, seed0=7):
             if int(gsd[k]) != int(sd32[k]):
                 fail.append(("num_batches_tracked", k))
     return fail, st
+
+
+def gpu_kink_margin(step, slope=0.2):
+    """min over every LeakyReLU input of the round the HIP step just ran of |x| / std(x), read from
+    the step's own activations (cgl_gan_tensor: G layers' LeakyReLU outputs, the D-step and G-loss
+    hidden layers through the D actually used -- the updated D for the G loss).  LeakyReLU keeps the
+    sign, so x = y (y > 0) or y / slope.  A LeakyReLU' mask can differ from the fp64 oracle's only
+    where |x| is within rounding distance of 0 (fp32 pre-activation errors are ~3e-7 std, up to a
+    few 1e-6 std), so rounds whose margin is >= KINK_MARGIN are comparable at the 1e-5 bound."""
+    gm, dm = step.gm, step.dm
+    codes = [(48 + l) if gm.bn[l] else (64 + l) for l in range(gm.n_layers - 1)]
+    codes += [112 + j for j in range(dm.n_layers - 1)] + [128 + j for j in range(dm.n_layers - 1)]
+    m = float("inf")
+    for c in codes:
+        y = step.internal(c)
+        x = torch.where(y > 0, y, y / slope)
+        m = min(m, float(x.abs().min() / (x.std() + 1e-30)))
+    return m
+
+
+def gpu_masks(step):
+    """The LeakyReLU branch decisions (x > 0) the HIP round just took, per oracle forward call:
+    ``g`` -- [G(z1) call, G(z2) call], one mask per hidden G layer; ``d`` -- [D(real), D(fake) of the
+    (last) local D step, D(Xg) of the G loss], one mask per hidden D layer (cgl_gan_tensor 48+/64+,
+    112+, 128+; LeakyReLU keeps the sign, so y > 0 <=> x > 0)."""
+    gm, dm, B, Br = step.gm, step.dm, step.B, step.Br
+    gt = [step.internal((48 + l) if gm.bn[l] else (64 + l)).view(2 * B, -1) > 0 for l in range(gm.n_layers - 1)]
+    P = [step.internal(112 + j).view(Br + B, -1) > 0 for j in range(dm.n_layers - 1)]
+    S = [step.internal(128 + j).view(B, -1) > 0 for j in range(dm.n_layers - 1)]
+    return {"g": [[t[:B].cpu() for t in gt], [t[B:].cpu() for t in gt]],
+            "d": [[p[:Br].cpu() for p in P], [p[Br:].cpu() for p in P], [s.cpu() for s in S]]}
+
+
+class MaskedRun:
+    """Make oracle runs follow the HIP round's branch decisions at the LeakyReLU kinks.
+
+    A mask can only differ from the fp64 oracle's own sign where |x| is at rounding level (fp32
+    pre-activation errors are ~3e-7 std, at most a few 1e-6 std), and such a flip -- a legitimate fp32
+    outcome -- moves the gradients by O(1/sqrt(rows x features)), far above the 1e-5 bound.  So the
+    oracle runs are fed the GPU's masks (SeqNet.mask_feed), which makes the 1e-5 comparison a test of
+    everything but those decisions, and the decisions themselves are checked by ``check_signs``: every
+    fed mask agrees with the sign of the fp64 run's own LeakyReLU input wherever |x| > SIGN_TOL std."""
+
+    SIGN_TOL = 2e-5
+
+    def __init__(self, G, workers, masks, head_layer=None):
+        """``masks``: gpu_masks() of each worker (the replicated G's from worker 0, or, with a Mix-G
+        ``head_layer``, the trunk's from worker 0 and head h's from worker h)."""
+        self.fed = []
+        if head_layer is None:
+            self._feed(G, masks[0]["g"])
+        else:
+            self._feed(G.trunk, [c[:head_layer] for c in masks[0]["g"]])
+            for h, hd in enumerate(G.heads):
+                self._feed(hd, [c[head_layer:] for c in masks[h]["g"]])
+        for w, m in zip(workers, masks):
+            self._feed(w.D, m["d"])
+
+    def _feed(self, net, calls):
+        net.mask_feed = [list(c) for c in calls]
+        net.trace_sink = []
+        self.fed.append((net, [m for c in calls for m in c]))
+
+    def check_signs(self):
+        worst = 0.0
+        for net, fed in self.fed:
+            assert not net.mask_feed, "oracle made fewer forward calls than the HIP round"
+            assert len(net.trace_sink) == len(fed)
+            for x, m in zip(net.trace_sink, fed):
+                x = x.reshape(m.shape)
+                bad = (x > 0) != m
+                if bool(bad.any()):
+                    worst = max(worst, float(x[bad].abs().max() / x.std()))
+        assert worst <= self.SIGN_TOL, f"GPU LeakyReLU branch differs from fp64 at |x| = {worst:.2e} std"
+        return worst
+
+
+def masked_pair(G32, workers32, G64, workers64, masks, head_layer=None):
+    """Feed the same GPU masks to the fp32 and the fp64 oracle (see MaskedRun)."""
+    return MaskedRun(G32, workers32, masks, head_layer), MaskedRun(G64, workers64, masks, head_layer)

@@ -49,3 +49,17 @@ def test_kl_score_strided_subsample():
     kl = kl_score(torch.from_numpy(real).cuda(), torch.from_numpy(gen).cuda(), num_sample=1000, num_servers=1)
     _, _, ref = _ref(real[::8000 // 1000], gen[::3000 // 1000])
     assert abs(kl - ref) <= 1e-12 * max(1.0, abs(ref))
+
+
+def test_kl_score_two_servers_per_server_stride():
+    """num_servers = 2 (CGLGAN/2DMG/main.py:75-80): each server's X is strided by
+    len(X_s) // (num_sample // S) on its own, then the two samples are concatenated."""
+    from cglgan.evaluation import kl_score
+    g = np.random.default_rng(2)
+    real = _ring(10000, g)
+    x0, x1 = _ring(500, g, std=0.03), _ring(1500, g, std=0.06)
+    kl = kl_score(torch.from_numpy(real).cuda(), [torch.from_numpy(x0).cuda(), torch.from_numpy(x1).cuda()],
+                  num_sample=1000)
+    d = np.concatenate([x0[::500 // 500], x1[::1500 // 500]], 0)
+    _, _, ref = _ref(real[::10000 // 1000], d)
+    assert abs(kl - ref) <= 1e-12 * max(1.0, abs(ref)), (kl, ref)
