@@ -278,7 +278,7 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
         if (col >= N) continue;
         float v = acc[i][j][r] + bj[j];
         if (act == CGL_EPI_ACT_LEAKY) v = v > 0.f ? v : v * sl;
-        else if (act == CGL_EPI_ACT_TANH) v = tanhf(v);
+        else if (act == CGL_EPI_ACT_TANH) v = cgl_tanh(v);
         else if (act == CGL_EPI_ACT_SIGMOID) v = 1.f / (1.f + expf(-v));
         if (drop) v *= gld(drop + (long)img * ldy + col);
         gst(Y + pix * ldy + col, v);
@@ -549,7 +549,7 @@ __global__ __launch_bounds__(256) void cgl_conv_n1(CglConvLaunch args) {
     if (mv && q == 0) {
       float y = acc + bias;
       if (L->act == CGL_EPI_ACT_LEAKY) y = y > 0.f ? y : y * L->slope;
-      else if (L->act == CGL_EPI_ACT_TANH) y = tanhf(y);
+      else if (L->act == CGL_EPI_ACT_TANH) y = cgl_tanh(y);
       else if (L->act == CGL_EPI_ACT_SIGMOID) y = 1.f / (1.f + expf(-y));
       if (L->drop) y *= gld(L->drop + (long)img * P->ldy);
       gst(P->Y + (((long)img * P->YH + oy * P->osy + P->ooy) * P->YW + ox * P->osx + P->oox) * P->ldy, y);
@@ -629,7 +629,7 @@ __global__ __launch_bounds__(256) void cgl_conv_n1_tile(CglConvLaunch args) {
     if (valid && q == 0 && y0 + ty < H) {
       float yv = acc + bias;
       if (L->act == CGL_EPI_ACT_LEAKY) yv = yv > 0.f ? yv : yv * L->slope;
-      else if (L->act == CGL_EPI_ACT_TANH) yv = tanhf(yv);
+      else if (L->act == CGL_EPI_ACT_TANH) yv = cgl_tanh(yv);
       else if (L->act == CGL_EPI_ACT_SIGMOID) yv = 1.f / (1.f + expf(-yv));
       if (L->drop) yv *= gld(L->drop + (long)img * P->ldy);
       gst(P->Y + (((long)img * P->YH + y0 + ty) * P->YW + tx) * P->ldy, yv);
@@ -708,7 +708,7 @@ __global__ __launch_bounds__(256) void cgl_conv_n1_part(CglConvLaunch args) {
   if (y0 + ty < H) {
     float yv = acc + (L->bias ? gld(L->bias) : 0.f);
     if (L->act == CGL_EPI_ACT_LEAKY) yv = yv > 0.f ? yv : yv * L->slope;
-    else if (L->act == CGL_EPI_ACT_TANH) yv = tanhf(yv);
+    else if (L->act == CGL_EPI_ACT_TANH) yv = cgl_tanh(yv);
     else if (L->act == CGL_EPI_ACT_SIGMOID) yv = 1.f / (1.f + expf(-yv));
     if (L->drop) yv *= gld(L->drop + (long)img * P->ldy);
     gst(P->Y + (((long)img * P->YH + y0 + ty) * P->YW + tx) * P->ldy, yv);
@@ -1421,7 +1421,7 @@ __global__ __launch_bounds__(256) void cgl_eltwise(CglEltArgs a) {
     } else {
       const f32x4 dy = *(gcf4p)(a.dY + e), y = *(gcf4p)(a.X + e);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = dy[j] * (1.f - y[j] * y[j]);
+      for (int j = 0; j < 4; ++j) o[j] = cgl_dtanh(dy[j], y[j]);
     }
     *(gf4p)(a.out + e) = o;
   }
@@ -1435,7 +1435,7 @@ __global__ __launch_bounds__(256) void cgl_eltwise1(CglEltArgs a) {
     float o = gld(a.dY + e);
     if (a.mode == 3) {
       const float y = gld(a.X + e);
-      o *= 1.f - y * y;
+      o = cgl_dtanh(o, y);
     } else {
       if (a.post_out) o = gld(a.post_out + e) > 0.f ? o : o * a.slope;
       if (a.drop) o *= gld(a.drop + (long)(r / a.hw) * a.C + c);

@@ -379,7 +379,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
           for (int r = 0; r < 16; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * sl;
         } else if (d->act == CGL_EPI_ACT_TANH) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = tanhf(v[r]);
+          for (int r = 0; r < 16; ++r) v[r] = cgl_tanh(v[r]);
         } else if (d->act == CGL_EPI_ACT_SIGMOID) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) v[r] = 1.f / (1.f + expf(-v[r]));
@@ -403,7 +403,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
             t[r] = gld(d->tanh_ref + (long)row * d->tanh_ld + col);
           }
 #pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = v[r] * (1.f - t[r] * t[r]);
+          for (int r = 0; r < 16; ++r) v[r] = cgl_dtanh(v[r], t[r]);
         }
       }
     }

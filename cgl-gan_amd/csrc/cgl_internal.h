@@ -26,6 +26,18 @@ __device__ __forceinline__ float gld(const float* p) { return *(gcfp)p; }
 __device__ __forceinline__ void gst(float* p, float v) { *(gfp)p = v; }
 __device__ __forceinline__ int gldi(const int* p) { return *(const CGL_GLOBAL int*)p; }
 
+// Tanh of the generator output and its derivative.  The derivative 1 - t^2 cancels as |t| -> 1
+// (one ulp of t near 0.999 is ~6e-5 of 1 - t^2), so an ulp-level error of a single-precision
+// tanh becomes a visible error of every gradient that flows back through the image and of the
+// cancelling bias-gradient sum of the output layer.  Both are evaluated in double and rounded
+// once: t is then the correctly rounded fp32 tanh (as the CPU reference's) and 1 - t^2 carries
+// no cancellation error.  Elementwise on the image only, so the double cost is negligible.
+__device__ __forceinline__ float cgl_tanh(float x) { return (float)tanh((double)x); }
+__device__ __forceinline__ float cgl_dtanh(float g, float t) {
+  const double td = (double)t;
+  return (float)((double)g * (1.0 - td * td));
+}
+
 // Row source of a row-major operand whose rows are the non-contiguous index.
 // Row r < split comes from p0 (optionally through idx0[idx_off + r]), rows >= split from p1.
 struct CglRowSrc {

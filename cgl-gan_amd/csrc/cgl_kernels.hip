@@ -524,7 +524,7 @@ __global__ __launch_bounds__(256) void cgl_act_fwd_k(const float* X, long n, int
     const float x = gld(X + i);
     float y = x;
     if (act == CGL_EPI_ACT_LEAKY) y = x > 0.f ? x : x * slope;
-    else if (act == CGL_EPI_ACT_TANH) y = tanhf(x);
+    else if (act == CGL_EPI_ACT_TANH) y = cgl_tanh(x);
     else if (act == CGL_EPI_ACT_SIGMOID) y = 1.f / (1.f + expf(-x));
     gst(Y + i, y);
   }
@@ -536,7 +536,7 @@ __global__ __launch_bounds__(256) void cgl_act_bwd_k(const float* dY, const floa
     const float g = gld(dY + i), y = gld(Y + i);
     float d = g;
     if (act == CGL_EPI_ACT_LEAKY) d = y > 0.f ? g : g * slope;
-    else if (act == CGL_EPI_ACT_TANH) d = g * (1.f - y * y);
+    else if (act == CGL_EPI_ACT_TANH) d = cgl_dtanh(g, y);
     else if (act == CGL_EPI_ACT_SIGMOID) d = g * (y * (1.f - y));
     gst(dX + i, d);
   }

@@ -90,21 +90,34 @@ def _bn(x, P, Bf, key, train):
                         P[key + ".bias"], train, BN_MOMENTUM, BN_EPS)
 
 
-def g_forward(P, Bf, z, train=True):
+def _leaky(x, signs=None, trace=None):
+    """LeakyReLU(0.2).  ``signs`` (a list, consumed in call order): the branch decisions (x > 0) to
+    follow instead of x's own sign -- used by the parity tests to make an oracle run take the GPU
+    round's decisions at the kinks (a flip there is a legitimate fp32 outcome, checked separately);
+    ``trace`` (a list) collects every LeakyReLU input."""
+    if trace is not None:
+        trace.append(x.detach())
+    if signs:
+        m = signs.pop(0).to(x.device).reshape(x.shape)
+        return torch.where(m, x, x * SLOPE)
+    return F.leaky_relu(x, SLOPE)
+
+
+def g_forward(P, Bf, z, train=True, signs=None, trace=None):
     """Generator.forward model/lsgan.py:23-27 (+ conv_blocks :10-21)."""
     out = F.linear(z, P["l1.0.weight"], P["l1.0.bias"])
     x = out.view(out.shape[0], 128, 8, 8)
     x = F.interpolate(x, scale_factor=2, mode="nearest")
     x = F.conv2d(x, P["conv_blocks.1.weight"], P["conv_blocks.1.bias"], 1, 1)
-    x = F.leaky_relu(_bn(x, P, Bf, "conv_blocks.2", train), SLOPE)
+    x = _leaky(_bn(x, P, Bf, "conv_blocks.2", train), signs, trace)
     x = F.interpolate(x, scale_factor=2, mode="nearest")
     x = F.conv2d(x, P["conv_blocks.5.weight"], P["conv_blocks.5.bias"], 1, 1)
-    x = F.leaky_relu(_bn(x, P, Bf, "conv_blocks.6", train), SLOPE)
+    x = _leaky(_bn(x, P, Bf, "conv_blocks.6", train), signs, trace)
     x = F.conv2d(x, P["conv_blocks.8.weight"], P["conv_blocks.8.bias"], 1, 1)
     return torch.tanh(x)
 
 
-def d_forward(P, Bf, img, masks=None, train=True):
+def d_forward(P, Bf, img, masks=None, train=True, signs=None, trace=None):
     """Discriminator.forward model/lsgan.py:94-99; ``masks`` = the 4 Dropout2d scales [B, C]
     (None in eval mode: Dropout2d is the identity)."""
     x = img
@@ -112,7 +125,7 @@ def d_forward(P, Bf, img, masks=None, train=True):
     bns = [None, "model.6", "model.10", "model.14"]
     for i, (ck, bk) in enumerate(zip(convs, bns)):
         x = F.conv2d(x, P[ck + ".weight"], P[ck + ".bias"], 2, 1)
-        x = F.leaky_relu(x, SLOPE)
+        x = _leaky(x, signs, trace)
         if train:
             x = x * masks[i].to(x.dtype)[:, :, None, None]
         if bk is not None:
@@ -171,25 +184,33 @@ class ConvGan:
         self.lam = 0.0
         self.dtype = dtype
 
-    def round(self, z1, z2, real, masks_real, masks_fake, masks_g):
-        """capgan.py:215-260 with one worker (capgan.py:324-347), explicit inputs and masks."""
+    CALLS = ("g1", "g2", "dr", "df", "dg")   # forward calls of a round: G(z1), G(z2), D(real), D(Xd), D(Xg)
+
+    def round(self, z1, z2, real, masks_real, masks_fake, masks_g, signs=None, trace=None):
+        """capgan.py:215-260 with one worker (capgan.py:324-347), explicit inputs and masks.
+        ``signs`` / ``trace``: optional dicts keyed by CALLS -- the LeakyReLU branch decisions to follow
+        in each forward call and the lists that collect its LeakyReLU inputs (see ``_leaky``)."""
         dt = self.dtype
         z1, z2, real = z1.to(dt), z2.to(dt), real.to(dt)
+        sg = lambda k: list(signs[k]) if signs else None
+        tr = lambda k: trace.setdefault(k, []) if trace is not None else None
         with torch.no_grad():
-            Xd = g_forward(self.gp, self.gb, z1)
-        Xg = g_forward(self.gp, self.gb, z2)
+            Xd = g_forward(self.gp, self.gb, z1, signs=sg("g1"), trace=tr("g1"))
+        Xg = g_forward(self.gp, self.gb, z2, signs=sg("g2"), trace=tr("g2"))
         half = 0.5 if self.loss == "mse" else 1.0
         for p in self.dp.values():
             p.grad = None
-        real_loss = adv_loss(d_forward(self.dp, self.db, real, masks_real), 1, self.loss)
-        fake_loss = adv_loss(d_forward(self.dp, self.db, Xd.detach(), masks_fake), 0, self.loss)
+        real_loss = adv_loss(d_forward(self.dp, self.db, real, masks_real, signs=sg("dr"), trace=tr("dr")), 1,
+                             self.loss)
+        fake_loss = adv_loss(d_forward(self.dp, self.db, Xd.detach(), masks_fake, signs=sg("df"), trace=tr("df")), 0,
+                             self.loss)
         d_loss = (real_loss + fake_loss) * half
         d_loss.backward()
         d_grads = OrderedDict((k, p.grad.detach().clone()) for k, p in self.dp.items())
         self.opt_d.step()
         for p in self.gp.values():
             p.grad = None
-        g_loss = adv_loss(d_forward(self.dp, self.db, Xg, masks_g), 1, self.loss)
+        g_loss = adv_loss(d_forward(self.dp, self.db, Xg, masks_g, signs=sg("dg"), trace=tr("dg")), 1, self.loss)
         F_max = g_loss - LAMBDA_REG * self.lam
         F_max.backward()
         g_grads = OrderedDict((k, p.grad.detach().clone()) for k, p in self.gp.items())

@@ -32,7 +32,50 @@ def _check(name, hip, o64, o32, fails, tol=STEP_TOL):
         fails.append(f"{name}: err {e:.3e} > bound {bound:.3e} (fp32 oracle err {_err(o32, o64):.3e})")
 
 
-def _run(B, loss, seed=3, rounds=1):
+SIGN_TOL = 2e-5   # |x| / std below which a GPU LeakyReLU branch may differ from fp64's (parity_helpers)
+
+
+def _gpu_signs(st, d_calls):
+    """The LeakyReLU branch decisions (x > 0, NCHW) the HIP round took, per oracle forward call, and
+    where they matter (D: Dropout2d-zeroed channels carry no value and no gradient).  LeakyReLU keeps
+    the sign, so y > 0 <=> x > 0 on the stored outputs (G: a1, a2; D: q_k = Dropout2d(LeakyReLU))."""
+    B = st.B
+    nchw = lambda t: t.permute(0, 3, 1, 2).cpu()
+    a1, a2 = nchw(st.a1 > 0), nchw(st.a2 > 0)
+    signs = {"g1": [a1[:B], a2[:B]], "g2": [a1[B:], a2[B:]]}
+    valid = {"g1": [None, None], "g2": [None, None]}
+    (dstep, dgl) = d_calls
+    signs["dr"] = [nchw(q[:B] > 0) for q in dstep]
+    signs["df"] = [nchw(q[B:2 * B] > 0) for q in dstep]
+    signs["dg"] = [nchw(q[:B] > 0) for q in dgl]
+    valid["dr"] = [nchw(q[:B] != 0) for q in dstep]
+    valid["df"] = [nchw(q[B:2 * B] != 0) for q in dstep]
+    valid["dg"] = [nchw(q[:B] != 0) for q in dgl]
+    return signs, valid
+
+
+def _check_signs(signs, valid, trace):
+    """Every followed branch agrees with the fp64 run's own sign wherever |x| > SIGN_TOL std."""
+    worst = 0.0
+    for k, ms in signs.items():
+        xs = trace[k]
+        assert len(xs) == len(ms), k
+        for x, m, v in zip(xs, ms, valid[k]):
+            bad = (x > 0) != m
+            if v is not None:
+                bad &= v
+            if bool(bad.any()):
+                worst = max(worst, float(x[bad].abs().max() / x.std()))
+    assert worst <= SIGN_TOL, f"GPU LeakyReLU branch differs from fp64 at |x| = {worst:.2e} std"
+    return worst
+
+
+def _run(B, loss, seed=3, rounds=1, follow_gpu=True):
+    """``follow_gpu``: the oracles take the HIP round's LeakyReLU branch decisions (checked against
+    the fp64 run's own signs); at B = 256 the G's BatchNorm2d outputs alone hold 2.5e7 LeakyReLU
+    inputs, so a few sit within fp32 rounding of 0 and a legitimate flip there moves the conv weight /
+    BatchNorm beta gradients far past 1e-5 -- the same treatment as the MLP configs
+    (tests/parity_helpers.py MaskedRun)."""
     from cglgan.conv_step import ConvGanStep
     torch.set_num_threads(4)
     st = ConvGanStep(B, loss=loss, seed=seed)
@@ -45,24 +88,40 @@ def _run(B, loss, seed=3, rounds=1):
     o64 = CO.ConvGan(gp, gb, dp, db, loss=loss, dtype=torch.float64)
     o32 = CO.ConvGan(gp, gb, dp, db, loss=loss, dtype=torch.float32)
     g = torch.Generator().manual_seed(seed)
+    d_calls = []
+    fwd = st._d_forward
+
+    def rec(x, n, groups, masks):      # keep each D forward call's LeakyReLU outputs (the G-loss pass
+        fwd(x, n, groups, masks)       # reuses the D-step buffers)
+        d_calls.append([q[:n].clone() for q in st.q])
+    st._d_forward = rec
     outs = []
     for r in range(rounds):
         real = torch.rand(B, 1, 32, 32, generator=g) * 2 - 1
+        d_calls.clear()
         st.run(real=real.cuda())
         torch.cuda.synchronize()
         z = st.z.cpu()
         mr = [m[:B].cpu() for m in st.mask_d]
         mf = [m[B:].cpu() for m in st.mask_d]
         mg = [m.cpu() for m in st.mask_g]
-        r64 = o64.round(z[:B], z[B:], real, mr, mf, mg)
-        r32 = o32.round(z[:B], z[B:], real, mr, mf, mg)
+        signs, valid, trace = None, None, None
+        if follow_gpu:
+            signs, valid = _gpu_signs(st, d_calls)
+            trace = {}
+        r64 = o64.round(z[:B], z[B:], real, mr, mf, mg, signs=signs, trace=trace)
+        r32 = o32.round(z[:B], z[B:], real, mr, mf, mg, signs=signs)
+        if follow_gpu:
+            r64["sign_margin"] = _check_signs(signs, valid, trace)
         outs.append((st.stats(), r64, r32, st.G.grads, st.D.grads))
     return st, o64, o32, outs
 
 
-@pytest.mark.parametrize("loss", ["mse", "bce"])
-def test_conv_round_parity(loss):
-    B = 8
+@pytest.mark.parametrize("B,loss", [(8, "mse"), (8, "bce"), (256, "mse"), (256, "bce")])
+def test_conv_round_parity(B, loss):
+    """One round at B = 8 and at the benchmarked B = 256 (bench.py --model lsgan: the same
+    geometry, so the same kernel instantiations, tile / split choices and specialised
+    Conv2d(64, 1) kernels as the timed round)."""
     st, o64, o32, outs = _run(B, loss)
     s, r64, r32, gg, dg = outs[0]
     fails = []
@@ -73,12 +132,7 @@ def test_conv_round_parity(loss):
     for k, v in r64["g_grads"].items():
         if k in PRE_BN_BIAS:
             continue
-        # the output conv's bias gradient is a cancelling sum over every pixel (BCE: norm 4.2e-4):
-        # its error (~4e-9) comes from the whole D backward and sat at 0.95x of the 1e-5 bound with
-        # either Conv2d(64, 1) forward kernel -- the tap-partial kernel's forward is the MORE accurate
-        # (9.6e-8 vs 1.3e-7 relative, torch fp32 CPU 3.2e-7; profiles/r01_n1_accuracy.txt)
-        _check("G grad " + k, gg[k], v, r32["g_grads"][k], fails,
-               tol=2 * STEP_TOL if k == "conv_blocks.8.bias" else STEP_TOL)
+        _check("G grad " + k, gg[k], v, r32["g_grads"][k], fails)
     for k, v in r64["d_grads"].items():
         _check("D grad " + k, dg[k], v, r32["d_grads"][k], fails)
     p0g = {k: v.detach() for k, v in o64.gp.items()}
@@ -101,7 +155,7 @@ def test_conv_round_parity(loss):
 def test_conv_trajectory_5_rounds():
     """Free-running 5 rounds: losses within 1e-4 relative of the fp64 oracle."""
     B = 8
-    st, o64, o32, outs = _run(B, "mse", seed=5, rounds=5)
+    st, o64, o32, outs = _run(B, "mse", seed=5, rounds=5, follow_gpu=False)
     for s, r64, r32, _, _ in outs:
         for k in ("d_real", "d_fake", "g_loss"):
             ref = r64[k]
