@@ -38,23 +38,33 @@ PEAK_HBM = 8000.0        # GB/s
 FLOP_PER_IMAGE_MIN = 18.95e6
 
 
+def default_batch(model):
+    return {"mdgan": 512, "ring": 64}.get(model, 256)
+
+
 def args_():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--batch", type=int, default=256)
+    p.add_argument("--batch", type=int, default=None, help="per-worker batch (default 256; 512 for mdgan, 64 for ring)")
     p.add_argument("--rows", type=int, default=59904, help="synthetic dataset rows per worker")
     p.add_argument("--E", type=int, default=1, help="D-share all-reduce period (N > 1)")
     p.add_argument("--eager", action="store_true", help="launch without hipGraph")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--profile-reps", type=int, default=20, help="back-to-back replays per launch when timing launches")
-    p.add_argument("--model", choices=["mlp", "lsgan"], default="mlp",
-                   help="mlp: model/mnist_model.py (BASELINE configs[1], the default workload); "
+    p.add_argument("--model", choices=["mlp", "lsgan", "mixg", "mdgan", "ring"], default="mlp",
+                   help="mlp: model/mnist_model.py CAPGAN round (BASELINE configs[1] at N=1, configs[2] at N>1, "
+                        "the default workload); mixg: configs[3], Mix-G through cglgan.driver (num_servers=2 when N "
+                        "is even, Cloud FedAvg every round); mdgan: configs[4] (non-IID shards, D-swap every --E "
+                        "rounds, bs512, fp32); ring: configs[0], the CGLGAN 2-D Gaussian-mixture round (B=64); "
                         "lsgan: the model/lsgan.py conv GAN round (32x32, MSE/LSGAN loss)")
     p.add_argument("--loss", choices=["mse", "bce"], default="mse", help="conv GAN objective (--model lsgan)")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.batch is None:
+        a.batch = default_batch(a.model)
+    return a
 
 
 def build_step(a, rank, world):
@@ -317,6 +327,237 @@ def main_lsgan(a, world, rank, local):
     return out
 
 
+def parity_vs_cpu(kind, B, rounds=10):
+    """The metric's "D-loss match vs CPU": ``rounds`` rounds of the fused HIP step and of the CPU oracle
+    (the torch-fp32 restatement of the reference step, oracle/gan_oracle.py -- the checker, run only in
+    this CPU leg) from the same initial state on identical explicit inputs (z, real batches); the
+    largest per-round relative difference of D_loss and G_loss.  SURVEY F8: <= 1e-4 over 10 rounds."""
+    sys.path.insert(0, ROOT)
+    from cglgan import GanStep, specs
+    from cglgan.data import gmm
+    from oracle import gan_oracle as O
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    if kind == "capgan":
+        G, ws = O.build_capgan(1)
+        srv, kw = O.CapganServer(G, torch.tensor([1.0])), {"weighting": "capgan"}
+        gm, dm, loss, wt, xl = specs.mnist_generator(), specs.mnist_discriminator(), "ce", "capgan", -1
+    elif kind == "mdgan":
+        G, ws = O.build_capgan(1, loss="bce")
+        srv, kw = O.CapganServer(G, torch.tensor([1.0])), {"weighting": "mean"}
+        gm, dm, loss, wt, xl = specs.mnist_generator(), specs.mnist_discriminator(sigmoid=True), "bce", "mean", -1
+    elif kind == "mixg":
+        G, ws = O.build_mixg(1)
+        srv, kw = O.MixgServer(G, torch.tensor([1.0])), {}
+        gm, dm, loss, wt, xl = specs.mixgen_worker(0), specs.mnist_discriminator(), "ce", "mix_single", \
+            specs.MIXGEN_HEAD_LAYER
+    else:
+        G, ws = O.build_ring(1, 1)
+        srv, kw = O.CglganServer(G, torch.tensor([1.0])), {}
+        gm, dm, loss, wt, xl = specs.ring_generator(0), specs.ring_discriminator(), "bce", "cglgan", -1
+    step = GanStep(gm, dm, batch=B, loss=loss, weighting=wt, exchange_layer=xl)
+    step.load_state_dicts(G.state_dict(), ws[0].D.state_dict())
+    step.reset()
+    ring = gmm(8, 2000)[0] if kind == "ring" else None
+    g = torch.Generator().manual_seed(4242)
+    dmax = gmax = 0.0
+    rows = []
+    for r in range(rounds):
+        z1, z2 = torch.randn(B, gm.dims[0], generator=g), torch.randn(B, gm.dims[0], generator=g)
+        if ring is not None:
+            real = ring[torch.randint(0, ring.shape[0], (B,), generator=g)]
+        else:
+            real = torch.rand(B, 784, generator=g) * 2 - 1
+        step.z[:B].copy_(z1)
+        step.z[B:].copy_(z2)
+        step.real.copy_(real)
+        step.run()
+        st = step.stats()
+        if kind in ("capgan", "mdgan"):
+            out = srv.round(ws, z1, z2, [[real]], **kw)
+        else:
+            out = srv.round(ws, z1, z2, [[real]])
+        dc, gc = float(out["d_losses"][0]), float(out["g_losses"][0])
+        dr, gr = abs(st["d_loss"][0] - dc) / abs(dc), abs(st["g_loss"] - gc) / abs(gc)
+        dmax, gmax = max(dmax, dr), max(gmax, gr)
+        rows.append([round(st["d_loss"][0], 7), round(dc, 7)])
+    return {"rounds": rounds, "batch": B, "kind": kind, "d_loss_max_rel": dmax, "g_loss_max_rel": gmax, "tol": 1e-4,
+            "pass": bool(dmax <= 1e-4 and gmax <= 1e-4),
+            "d_loss_gpu_cpu_per_round": rows,
+            "reference": "CPU oracle: torch fp32 restatement of the reference step, same initial state, identical "
+                         "z and real batches every round"}
+
+
+def cpu_rounds(kind, B, seconds):
+    """The CPU oracle's round rate on this host (kind: ring / mdgan / mixg; N = 1)."""
+    sys.path.insert(0, ROOT)
+    from cglgan.data import gmm
+    from oracle import gan_oracle as O
+    threads = max(1, min(16, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    if kind == "ring":
+        G, ws = O.build_ring(1, 1)
+        srv = O.CglganServer(G, torch.tensor([1.0]))
+        ring = gmm(8, 2000)[0]
+    elif kind == "mdgan":
+        G, ws = O.build_capgan(1, loss="bce")
+        srv = O.CapganServer(G, torch.tensor([1.0]))
+    else:
+        G, ws = O.build_mixg(1)
+        srv = O.MixgServer(G, torch.tensor([1.0]))
+    g = torch.Generator().manual_seed(5)
+    n, t_total, warm = 0, 0.0, 3
+    while True:
+        z1, z2 = torch.randn(B, 100, generator=g), torch.randn(B, 100, generator=g)
+        real = ring[torch.randint(0, ring.shape[0], (B,), generator=g)] if kind == "ring" else \
+            torch.rand(B, 784, generator=g) * 2 - 1
+        t0 = time.perf_counter()
+        if kind == "mdgan":
+            srv.round(ws, z1, z2, [[real]], weighting="mean")
+        else:
+            srv.round(ws, z1, z2, [[real]])
+        dt = time.perf_counter() - t0
+        n += 1
+        if n > warm:
+            t_total += dt
+        if (n > warm and t_total >= seconds) or n >= 20000:
+            break
+    rounds = n - warm
+    return {"value": round(B * rounds / t_total, 1), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{rounds} {kind} rounds (B={B}, N=1) of the torch-CPU oracle after {warm} warm-up rounds, "
+                      f"{t_total:.1f} s, torch {torch.__version__}"}
+
+
+def timed_rounds(round_fn, a, world):
+    """W untimed rounds, then K rounds between barrier + synchronize; max over ranks."""
+    torch.cuda.synchronize()
+    for r in range(a.warmup):
+        round_fn(r)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for r in range(a.steps):
+        round_fn(a.warmup + r)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
+def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None, parity_kind=None):
+    """The bench line of a fused-round model (mlp / mixg / mdgan / ring): GEMM-family roofline from
+    per-launch HIP-event timing on the launch stream, CPU baseline and CPU parity at N = 1."""
+    per_kind, gemm_us, gemm_flops, gemm_n = profile_launches(step, world, a.profile_reps)
+    plan = step.plan_info()
+    st = step.stats()
+    ms_step = el / a.steps * 1e3
+    value = world * a.batch * a.steps / el
+    if rank != 0:
+        return None
+    gemm_s = sum(gemm_us) * 1e-6
+    gemm_tf = gemm_flops / gemm_s / 1e12 if gemm_s > 0 else 0.0
+    step_flops = plan["gemm_flops"]
+    step_tf = step_flops / (ms_step * 1e-3) / 1e12
+    cfg = {"workload": workload, "global_batch": a.batch * world, "batch_per_worker": a.batch,
+           "parallelism": f"workers{world}", "graph": not a.eager}
+    cfg.update(config_extra)
+    if world > 1:
+        cfg["dist"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size()}
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic", "config": cfg,
+        "roofline": {"bound": "mfma", "kernel": "cgl_gemm_f32 (the round's GEMM launches)",
+                     "achieved": round(gemm_tf, 3), "peak": PEAK_F32_MFMA, "unit": "TFLOP/s",
+                     "frac": round(gemm_tf / PEAK_F32_MFMA, 4),
+                     "traffic": traffic_per_gemm_launch() if a.model == "mlp" else None,
+                     "traffic_unit": "bytes per GEMM launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/r01_traffic.json)",
+                     "gemm_launches_per_round": gemm_n, "gemm_flops_per_round": gemm_flops,
+                     "flops_per_gemm_launch": gemm_flops / max(gemm_n, 1),
+                     "avg_gemm_launch_us": round(sum(gemm_us) / max(gemm_n, 1), 3),
+                     "gemm_launch_us": [round(u, 2) for u in gemm_us],
+                     "step_achieved_tflops": round(step_tf, 3),
+                     "step_frac_mfma": round(step_tf / PEAK_F32_MFMA, 4),
+                     "per_kind_us_per_round": {k: round(v[0], 2) for k, v in per_kind.items()},
+                     "launches_per_round": plan["launches"]},
+        "losses": {"d_loss": st["d_loss"][0], "g_loss": st["g_loss"], "lambda": st["lambda"], "round": st["round"]},
+    }
+    if world == 1 and not a.no_cpu_baseline:
+        if cpu_leg is not None:
+            out["cpu_baseline"] = cpu_leg()
+        if parity_kind is not None:
+            out["parity"] = parity_vs_cpu(parity_kind, a.batch)
+    print(json.dumps(out), flush=True)
+    return out
+
+
+def main_mlp(a, world, rank):
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        step, _ = build_step(a, rank, world)
+        ex = make_exchange(step, world, a)
+        el = timed_rounds(lambda r: ex.round(r, graph=not a.eager), a, world)
+        wl = ("C2: model/mnist_model.py MLP GAN, CAPGAN worker round (G fwd x2, D step, G loss, G bwd, Adam G/D), "
+              "1 worker per GPU" if world == 1 else
+              f"C3: CAPGAN {world} workers (1 per GPU), S=1, lambda-weighted G-gradient all-reduce + E={a.E} D "
+              f"all-reduce over RCCL")
+        return fused_report(a, world, rank, step, el, wl, {"img": "28x28x1", "dataset_rows_per_worker": a.rows},
+                            cpu_leg=lambda: cpu_baseline(a), parity_kind="capgan")
+
+
+def main_driver(a, world, rank, algo):
+    """BASELINE configs[3] (mixg) / configs[4] (mdgan) through cglgan.driver: the reference's topology
+    (server groups, Cloud), shards cut by allocate_dataset from a synthetic labelled dataset."""
+    from cglgan.driver import Driver, DriverConfig
+    S = 2 if (algo == "mixg" and world % 2 == 0) else 1
+    cfg = DriverConfig(algo=algo, num_workers=world, num_servers=S, batch_size=a.batch,
+                       num_communication=a.warmup + a.steps + a.profile_reps + 8, cloud_epoch=1,
+                       iid=1 if algo == "mdgan" else 0, swap_every=(a.E if (algo == "mdgan" and world > 1) else 0),
+                       dataset_rows=max(60000, 8 * a.batch * world), graph=not a.eager)
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        drv = Driver(cfg)
+        el = timed_rounds(lambda r: drv.exchange.round(r, graph=cfg.graph), a, world)
+        if algo == "mixg":
+            wl = (f"C4: mixed-gan.py Mix-G, num_workers={world} num_servers={S} (one MixGenerator head per "
+                  f"worker, trunk gradient all-reduced in each server group, Cloud trunk FedAvg every round)")
+        else:
+            wl = (f"C5: MD-GAN, num_workers={world}, non-IID (iid=1) shards, Sigmoid D + BCE, G on mean(l_i)"
+                  + (f", D-swap every {a.E} rounds" if world > 1 else "") + " (fp32; the fp16 part is not built)")
+        return fused_report(a, world, rank, drv.step, el, wl,
+                            {"img": "28x28x1", "num_servers": S, "shard_rows": int(drv.step.real.shape[0])},
+                            cpu_leg=lambda: cpu_rounds(algo, a.batch, a.cpu_seconds), parity_kind=algo)
+
+
+def main_ring(a, world, rank):
+    """BASELINE configs[0]: CGLGAN/2DMG, one worker, the 2-D Gaussian-mixture ring (num_class=8), B=64."""
+    from cglgan import GanStep, specs
+    from cglgan.data import gmm
+    from cglgan.init import default_init
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        torch.manual_seed(20211212 + rank)
+        data, _ = gmm(8, 10000, device="cuda")       # CGLGAN/2DMG/main.py:456: num_sample = 10000 per mode
+        gm, dm = specs.ring_generator(0), specs.ring_discriminator()
+        step = GanStep(gm, dm, batch=a.batch, loss="bce", weighting="cglgan", n_workers=world, rank=rank,
+                       gen_z=True, real=data, sample_n=data.shape[0])
+        torch.manual_seed(20211212)
+        default_init(gm, step.g_views)
+        default_init(dm, step.d_views)
+        step.reset()
+        ex = make_exchange(step, world, a)
+        el = timed_rounds(lambda r: ex.round(r, graph=not a.eager), a, world)
+        wl = ("C1: CGLGAN/2DMG ring GAN (G 100-32-2, D 2-128-256-1 Sigmoid, BCE, closed-form lambda), 8-mode 2-D "
+              "Gaussian mixture, 1 worker per GPU" + (f", {world} workers" if world > 1 else ""))
+        return fused_report(a, world, rank, step, el, wl, {"data_points": int(data.shape[0])},
+                            cpu_leg=lambda: cpu_rounds("ring", a.batch, a.cpu_seconds), parity_kind="ring")
+
+
 def main():
     a = args_()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -328,78 +569,21 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    if a.model == "lsgan":
-        out = main_lsgan(a, world, rank, local)
+        assert dist.get_world_size() == world, (dist.get_world_size(), world)
+        if rank == 0:
+            print(f"bench: {dist.get_world_size()} ranks, backend {dist.get_backend()}", file=sys.stderr, flush=True)
+    try:
+        if a.model == "lsgan":
+            return main_lsgan(a, world, rank, local)
+        if a.model in ("mixg", "mdgan"):
+            return main_driver(a, world, rank, a.model)
+        if a.model == "ring":
+            return main_ring(a, world, rank)
+        return main_mlp(a, world, rank)
+    finally:
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
-        return out
-    stream = torch.cuda.Stream()
-    with torch.cuda.stream(stream):
-        step, data = build_step(a, rank, world)
-        ex = make_exchange(step, world, a)
-        graph = not a.eager
-        torch.cuda.synchronize()
-        for r in range(a.warmup):
-            ex.round(r, graph=graph)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        for r in range(a.steps):
-            ex.round(a.warmup + r, graph=graph)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        el = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([el], device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        st = step.stats()
-        per_kind, gemm_us, gemm_flops, gemm_n = profile_launches(step, world, a.profile_reps)
-        plan = step.plan_info()
-    ms_step = el / a.steps * 1e3
-    value = world * a.batch * a.steps / el
-    out = None
-    if rank == 0:
-        gemm_s = sum(gemm_us) * 1e-6
-        gemm_tf = gemm_flops / gemm_s / 1e12 if gemm_s > 0 else 0.0
-        step_tf = a.batch * FLOP_PER_IMAGE_MIN / (ms_step * 1e-3) / 1e12
-        out = {
-            "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": ("C2: model/mnist_model.py MLP GAN, CAPGAN worker round (G fwd x2, D step, "
-                                    "G loss, G bwd, Adam G/D), 1 worker per GPU" if world == 1 else
-                                    f"C3: CAPGAN {world} workers (1 per GPU), S=1, lambda-weighted G-gradient "
-                                    f"all-reduce + E={a.E} D all-reduce over RCCL"),
-                       "global_batch": a.batch * world, "batch_per_worker": a.batch, "img": "28x28x1",
-                       "parallelism": f"workers{world}", "graph": not a.eager,
-                       "dataset_rows_per_worker": a.rows},
-            "roofline": {"bound": "mfma", "kernel": "cgl_gemm_f32 (the round's GEMM launches)",
-                         "achieved": round(gemm_tf, 3), "peak": PEAK_F32_MFMA, "unit": "TFLOP/s",
-                         "frac": round(gemm_tf / PEAK_F32_MFMA, 4),
-                         "traffic": traffic_per_gemm_launch(),
-                         "traffic_unit": "bytes per GEMM launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/r01_traffic.json)",
-                         "gemm_launches_per_round": gemm_n, "gemm_flops_per_round": gemm_flops,
-                         "flops_per_gemm_launch": gemm_flops / max(gemm_n, 1),
-                         "avg_gemm_launch_us": round(sum(gemm_us) / max(gemm_n, 1), 3),
-                         "gemm_launch_us": [round(u, 2) for u in gemm_us],
-                         "step_achieved_tflops": round(step_tf, 3),
-                         "step_frac_mfma": round(step_tf / PEAK_F32_MFMA, 4),
-                         "per_kind_us_per_round": {k: round(v[0], 2) for k, v in per_kind.items()},
-                         "launches_per_round": plan["launches"]},
-            "losses": {"d_loss": st["d_loss"][0], "g_loss": st["g_loss"], "lambda": st["lambda"],
-                       "round": st["round"]},
-        }
-        if world == 1 and not a.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(a)
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
-    return out
 
 
 if __name__ == "__main__":

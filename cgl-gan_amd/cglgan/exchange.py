@@ -94,6 +94,8 @@ class WorkerExchange:
     """One worker's communication round (phase A -> collectives -> phase B).
 
     ``share_every`` > 0: E-share of the D parameters every that many rounds (a19).
+    ``swap_every`` > 0: the MD-GAN D-swap inside the group every that many rounds, drawn by server
+    ``server_rank``'s generator.
     ``cloud``/``cloud_every``: Cloud FedAvg across server groups (a18) with data-size weights
     ``cloud_weights`` (one per member of the cloud group), after every ``cloud_every``-th round;
     or, with ``cloud_due(r)`` (see ``mixg_cloud_due`` / ``capgan_cloud_due``), before round r as the
@@ -105,12 +107,13 @@ class WorkerExchange:
 
     def __init__(self, step, comm=None, share_every: int = 0, cloud=None, cloud_every: int = 0,
                  cloud_weights=None, fedavg_compat_noop: bool = False, swap_every: int = 0,
-                 cloud_scope: str = "trunk", segema: float = 0.0, cloud_due=None):
+                 cloud_scope: str = "trunk", segema: float = 0.0, cloud_due=None, server_rank: int = 0):
         self.step = step
         self.comm = comm
         self.share_every = share_every
         self.swap_every = swap_every
-        self.dswap = DSwap(comm.size) if (comm is not None and swap_every > 0) else None
+        # the server's own generator: Random() seeded with server_rank + 100 (MDGAN/MNIST/mdgan.py:122-123)
+        self.dswap = DSwap(comm.size, server_rank) if (comm is not None and swap_every > 0) else None
         self.cloud, self.cloud_every = cloud, cloud_every
         self.cloud_weights = cloud_weights
         self.fedavg_compat_noop = fedavg_compat_noop

@@ -71,6 +71,61 @@ def _trunk_and_heads(n_heads, img_dim, z_dim):
     return t, heads
 
 
+def _draw_default(model: MlpModel):
+    v = _views_of(model)
+    default_init(model, v)
+    return v
+
+
+def _draw_mixgen(n_heads, img_dim, z_dim):
+    trunk, heads = _trunk_and_heads(n_heads, img_dim, z_dim)
+    g = _views_of(trunk)
+    for h in heads:
+        _views_of(h, g)
+    default_init(trunk, g)
+    for h in heads:
+        default_init(h, g)
+    weights_init(trunk, g)
+    for h in heads:
+        weights_init(h, g)
+    return g
+
+
+def _draw_d(img_dim, sigmoid=False, reinit=False):
+    from .specs import mnist_discriminator
+    dm = mnist_discriminator(img_dim, sigmoid)
+    d = _views_of(dm)
+    default_init(dm, d)
+    if reinit:
+        weights_init(dm, d)
+    return d
+
+
+def topology_state(algo: str, num_servers: int, num_workers: int, seed: int = 20211212, img_dim: int = 784,
+                   z_dim: int = 100):
+    """Initial parameters of a whole driver topology, drawn once from ``torch.manual_seed(seed)``: every
+    server's generator (capgan.py:156 ``Generator(ims)`` / mixed-gan.py:180-181 ``MixGenerator(ims, H)
+    .apply(weights_init)`` with H = num_workers // num_servers heads), servers in rank order, then every
+    worker's discriminator (capgan.py:309 default init; mixed-gan.py:347-348 ``.apply(weights_init)``;
+    the Sigmoid D for MD-GAN).  The reference constructs these inside its Server / Worker threads, servers
+    started first (capgan.py:521-525), so this is its order with the thread interleaving fixed; with one
+    server it equals ``capgan_state`` / ``mixgen_state``.  Returns ``([G params per server], [D params per
+    worker])`` keyed by the reference's state-dict keys."""
+    from .specs import mnist_generator
+    if algo not in ("capgan", "mixg", "mdgan"):
+        raise ValueError(algo)
+    if num_workers % num_servers:
+        raise ValueError("num_workers must be a multiple of num_servers")
+    torch.manual_seed(seed)
+    heads = num_workers // num_servers
+    if algo == "mixg":
+        gs = [_draw_mixgen(heads, img_dim, z_dim) for _ in range(num_servers)]
+    else:
+        gs = [_draw_default(mnist_generator(img_dim, z_dim)) for _ in range(num_servers)]
+    ds = [_draw_d(img_dim, sigmoid=(algo == "mdgan"), reinit=(algo == "mixg")) for _ in range(num_workers)]
+    return gs, ds
+
+
 def capgan_state(n_workers: int = 1, seed: int = 20211212, sigmoid: bool = False, img_dim: int = 784,
                  z_dim: int = 100):
     """``torch.manual_seed(seed); net_g = Generator(ims)`` then one ``Discriminator(ims)`` per worker
