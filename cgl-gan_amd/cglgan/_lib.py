@@ -10,7 +10,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libcglgan_hip.so")
+LIB_PATH = os.environ.get("CGL_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "lib", "libcglgan_hip.so")
 
 MAX_LAYERS = 8
 LOSS_CE2, LOSS_BCE = 0, 1

@@ -70,6 +70,54 @@ __device__ __forceinline__ void cgl_mask(float v[8], bool ok, int k, int K) {
   for (int j = 0; j < 8; ++j) v[j] = (ok && k + j < K) ? v[j] : 0.f;
 }
 
+
+// ------------------------------------------------------------------------------------------
+// In-launch rendezvous of the tiles_m workgroups of one column tile (fused BatchNorm).
+// Published words are written with agent-scope atomic (sc1, write-through) stores and drained
+// before the ticket; the ticket counter is monotonic (zero at workspace creation, every launch
+// adds exactly n per column tile), so target = the next multiple of n above this workgroup's
+// ticket and no per-call reset is needed; one lane polls relaxed with s_sleep, then ONE
+// every reader loads the published words with agent-scope atomic (sc1) loads, so the poll needs
+// no agent acquire (cdna_hip_programming.md Guideline 16, the all-sc1 form).  Requires the launch's workgroups co-resident (the
+// planner checks the grid against the occupancy); the spin is bounded and a timeout sets *err.
+typedef CGL_GLOBAL unsigned int cgl_gu32;
+typedef CGL_GLOBAL unsigned long long cgl_gu64;
+__device__ __forceinline__ void cgl_rendezvous(unsigned int* cnt, unsigned int n, unsigned int* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // every wave's publish stores have landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned int old = __hip_atomic_fetch_add((cgl_gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned int target = old - old % n + n;
+    unsigned int spins = 0;
+    while ((int)(__hip_atomic_load((cgl_gu32*)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 21)) {
+        __hip_atomic_store((cgl_gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    // every handed-off word is read with an sc1 (agent-scope atomic) load, so no agent acquire
+    // (buffer_inv) is needed -- only the compiler must not hoist those loads above the poll
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ void cgl_pub2f(float* p, float a, float b) {
+  const unsigned long long v = (unsigned long long)__float_as_uint(a) | ((unsigned long long)__float_as_uint(b) << 32);
+  __hip_atomic_store((cgl_gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void cgl_pubd(double* p, double a) {
+  __hip_atomic_store((cgl_gu64*)p, (unsigned long long)__double_as_longlong(a), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long cgl_ld64(const void* p) {
+  return __hip_atomic_load((cgl_gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#define CGL_BN_MAXT 32     // row tiles per column tile a fused BatchNorm combines (tiles_m <= 32)
+#define CGL_BN_STG 4       // staged partial items per thread: tiles_m x tile columns <= 1024
+// dynamic LDS a fused-BatchNorm problem needs for its staged partials (bytes)
+inline int cgl_bn_stage_bytes(int tiles_m, int ncw) { return tiles_m * ncw * 16; }
+
 // ------------------------------------------------------------------------------------------
 // Main body.  One wave owns TM x TN 32x32 accumulator blocks ((32 TM) x (32 TN) outputs); the
 // workgroup tile is (32 TM WM) x (32 TN WN), K split WK ways.  Operand fragments of S chunks
@@ -84,9 +132,13 @@ struct CglPipe {
   static constexpr int S = CGL_GEMM_STAGES;
 };
 
-template <int LAYOUT, int VEC, int TM, int TN, bool SK>
+typedef __attribute__((address_space(3))) void cgl_lds_void;
+#define CGL_GL_NS 2        // LDS ring depth of the staged main loop (measured: 2 beats 3 at 64 KB per workgroup)
+
+template <int LAYOUT, int VEC, int TM, int TN, bool SK, bool GL>
 __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d, int bid, float* __restrict__ s_red,
-                                              float* __restrict__ s_col, int* __restrict__ s_flag) {
+                                              float* __restrict__ s_col, int* __restrict__ s_flag,
+                                              float* __restrict__ s_bn, double* __restrict__ s_bnd) {
   constexpr int S = CglPipe<TM, TN>::S;
   const int M = d->M, N = d->N, K = d->K;
   const int WN = d->WN, WK = d->WK, WM = d->WM;
@@ -125,7 +177,143 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+#ifndef CGL_GEMM_NACC
+#define CGL_GEMM_NACC 2
+#endif
+  // 1x1 blocks: NACC independent accumulation chains over alternating k-steps of a chunk (summed in
+  // a fixed order after the k-loop), so consecutive MFMAs do not wait on each other's result
+  constexpr int NX = (TM * TN == 1) ? CGL_GEMM_NACC : 1;
+  f32x16 accx[NX > 1 ? NX - 1 : 1];
+#pragma unroll
+  for (int x = 0; x < (NX > 1 ? NX - 1 : 1); ++x)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accx[x][r] = 0.f;
 
+  if constexpr (GL && LAYOUT != 2 && TM == 1 && TN == 1 && VEC) {
+    // ---------------- LDS-staged main loop (glds): the waves of one K-slice share a ring of
+    // CGL_GL_NS stages of 32 k, filled by global_load_lds_dwordx4 in whole 128-byte row segments
+    // (8 rows per wave-instruction) instead of fragment-shaped loads that touch 32 rows per
+    // instruction (those saturate the vector L1's tag lookups: TA_ADDR_STALLED_BY_TC, r02 PMC).
+    //   A (k-contiguous): image [32 WM rows][32 k], row r's 16-byte piece p at p ^ ((r >> 1) & 7)
+    //     (conflict-free ds_read_b128 of 8 consecutive k per lane half: the k-permuted fragment);
+    //   B, NT (k-contiguous): the same image of 32 WN rows; NN (n-contiguous): k-major image
+    //     [32 k][32 WN], fragments by ds_read_b32 (32 consecutive columns per lane half).
+    // Rows / columns past M / N read clamped (valid) addresses and feed unstored outputs; k past
+    // K (last stage only) reads clamped addresses and A's values there are zeroed.
+    const int gw = WM * WN;
+    const int na = 4 * WM, nb = 4 * WN, ninst = na + nb, per = ninst / gw;
+    const int stg = ninst * 256;                          // floats per stage of one slice
+    float* ring = s_red + wk * CGL_GL_NS * stg;
+    const int nst = (K + 31) / 32;
+    const int nsl = KS * WK, sl = kslice * WK + wk;
+    const int sb = (sl * nst) / nsl, se = ((sl + 1) * nst) / nsl;
+    const int cmax = (nst + nsl - 1) / nsl;
+    const int arow0 = tm * BM, bcol0 = tn * WN * 32;     // first A row / B row (NT) or column (NN) of the tile
+    const int ldb = d->b.ld;
+    float* __restrict__ a_copy = d->a_copy;
+    const bool do_copy = a_copy && tn == 0 && wn == 0 && (m0 + li) < M && (m0 + li) >= d->a_copy_row0;
+    // this lane's global source of each of its fill instructions (instruction q = wmn + u gw)
+    const float* src[8];
+    int src_k[8];            // NT / A: offset of the piece in k; NN's B: k-row within the stage
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int q = min(wmn + u * gw, ninst - 1);
+      if (q < na || LAYOUT == 0) {
+        const bool isA = q < na;
+        const int row = (isA ? q : q - na) * 8 + (lane >> 3);
+        const int p = (lane & 7) ^ ((row >> 1) & 7);
+        src[u] = isA ? cgl_row(d->a, min(arow0 + row, M - 1)) : cgl_row(d->b, min(bcol0 + row, N - 1));
+        src_k[u] = 4 * p;
+      } else {                                            // NN's B: k-major image
+        const int e = (q - na) * 256 + 4 * (lane & 63);   // float index in the [32][32 WN] image
+        const int kr = e / (32 * WN), col = e % (32 * WN);
+        src[u] = d->b.p0 + min(bcol0 + col, nmem - 4);
+        src_k[u] = kr;
+      }
+    }
+    auto issue = [&](int s, int buf) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (u < per) {
+          const int q = wmn + u * gw;
+          const float* g;
+          if (q < na || LAYOUT == 0)
+            g = src[u] + min(s * 32 + src_k[u], K - 4);
+          else
+            g = src[u] + (long)min(s * 32 + src_k[u], K - 1) * ldb;
+          __builtin_amdgcn_global_load_lds((const void*)g, (cgl_lds_void*)(ring + buf * stg + q * 256), 16, 0, 0);
+        }
+      }
+    };
+    const int arow = wm * 32 + li, asw = (arow >> 1) & 7;
+    const int brow = wn * 32 + li, bsw = (brow >> 1) & 7;
+    for (int j = 0; j < CGL_GL_NS - 1; ++j)
+      if (sb + j < se) issue(sb + j, j);
+    for (int it = 0; it < cmax; ++it) {
+      const int s = sb + it;
+      if (CGL_GL_NS > 2 && s + CGL_GL_NS - 2 < se) {
+        // (CGL_GL_NS == 3: the next stage's `per` fills may stay in flight)
+        switch (per) {
+          case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+          case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+          case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+          default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        }
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      // (a full __syncthreads: it also orders the compiler's LDS reads after the barrier; with
+      // CGL_GL_NS == 2 no fill is in flight here, so its vmcnt(0) costs nothing)
+      __syncthreads();
+      if (s + CGL_GL_NS - 1 < se) issue(s + CGL_GL_NS - 1, (it + CGL_GL_NS - 1) % CGL_GL_NS);
+      if (s < se) {
+        const float* la = ring + (it % CGL_GL_NS) * stg;
+        const float* lb = la + na * 256;
+        const int kleft = K - s * 32;                     // < 32 on a K-tail stage
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int p0 = 4 * c + 2 * lh;
+          const f32x4 a0 = *(const f32x4*)(la + arow * 32 + 4 * (p0 ^ asw));
+          const f32x4 a1 = *(const f32x4*)(la + arow * 32 + 4 * ((p0 + 1) ^ asw));
+          float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+          float bv[8];
+          if (LAYOUT == 0) {
+            const f32x4 b0 = *(const f32x4*)(lb + brow * 32 + 4 * (p0 ^ bsw));
+            const f32x4 b1 = *(const f32x4*)(lb + brow * 32 + 4 * ((p0 + 1) ^ bsw));
+            bv[0] = b0[0]; bv[1] = b0[1]; bv[2] = b0[2]; bv[3] = b0[3];
+            bv[4] = b1[0]; bv[5] = b1[1]; bv[6] = b1[2]; bv[7] = b1[3];
+          } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) bv[q] = lb[(16 * c + 8 * lh + q) * (32 * WN) + brow];
+          }
+          if (kleft < 32) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+              if (16 * c + 8 * lh + q >= kleft) av[q] = 0.f;
+          }
+          if (do_copy) {
+            float* dst = a_copy + (long)(m0 + li) * d->a_copy_ld + s * 32 + 16 * c + 8 * lh;
+            if (kleft >= 16 * c + 8 * lh + 8) {
+              *(gf4p)dst = f32x4{av[0], av[1], av[2], av[3]};
+              *(gf4p)(dst + 4) = f32x4{av[4], av[5], av[6], av[7]};
+            } else {
+#pragma unroll
+              for (int q = 0; q < 8; ++q)
+                if (16 * c + 8 * lh + q < kleft) gst(dst + q, av[q]);
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            if (q % NX == 0)
+              acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], bv[q], acc[0][0], 0, 0, 0);
+            else
+              accx[q % NX - 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], bv[q], accx[q % NX - 1], 0, 0, 0);
+          }
+        }
+      }
+    }
+    __syncthreads();                        // the ring is reused by the split-K reduction below
+  } else {
   const int nch = (K + CGL_GEMM_KCHUNK - 1) / CGL_GEMM_KCHUNK;
   // chunk range of this wave: slice kslice * WK + wk of KS * WK equal slices of the K chunks
   const int nsl = KS * WK, sl = kslice * WK + wk;
@@ -230,13 +418,23 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
           if (b_is_ones[j]) B_[j][q] = (!T || k + q < K) ? 1.f : 0.f;
       }
     }
+    if constexpr (NX > 1) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
+      for (int q = 0; q < 8; ++q) {
+        if (q % NX == 0)
+          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A_[0][q], B_[0][q], acc[0][0], 0, 0, 0);
+        else
+          accx[q % NX - 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A_[0][q], B_[0][q], accx[q % NX - 1], 0, 0, 0);
+      }
+    } else {
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int q = 0; q < 8; ++q)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(A_[i][q], B_[j][q], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(A_[i][q], B_[j][q], acc[i][j], 0, 0, 0);
+    }
   };
 
   // S register sets in rotation: set s holds chunk c + s; after its MFMAs are issued it is
@@ -266,6 +464,14 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     float xa[TM][8], xb[TN][8];
     load_chunk(tailc, cfull, xa, xb);
     compute_chunk(tailc, cfull, xa, xb);
+  }
+  }   // (register-pipelined main loop)
+
+  if constexpr (NX > 1) {
+#pragma unroll
+    for (int x = 0; x < NX - 1; ++x)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[0][0][r] += accx[x][r];
   }
 
   // ---------------- split-K reduction (fixed order: wk = 1, 2, 3)
@@ -379,7 +585,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
           for (int r = 0; r < 16; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * sl;
         } else if (d->act == CGL_EPI_ACT_TANH) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = cgl_tanh(v[r]);
+          for (int r = 0; r < 16; ++r) v[r] = tanhf(v[r]);   // (double tanh here costs ~4 us on G L4)
         } else if (d->act == CGL_EPI_ACT_SIGMOID) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) v[r] = 1.f / (1.f + expf(-v[r]));
@@ -407,6 +613,140 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
         }
       }
     }
+  }
+
+  // ---------------- fused BatchNorm1d backward (bn_fuse 2): C = dZ of the BatchNorm below
+  // (torch's batch_norm_backward, train mode, as cgl_bn_bwd):
+  //   dy = leaky'(post) * acc,  S = sum dy,  D = sum (y - mean) dy   (per column, over all M rows)
+  //   dZ = (dy - S / M - (y - mean) D invstd^2 / M) invstd gamma,  dgamma = D invstd,  dbeta = S
+  if (d->bn_fuse == 2) {
+    const float sl = d->slope;
+    float dy[TM][TN][16], yc[TM][TN][16];
+    const int ldp = d->bn_ld_post;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int colc = min(n0 + 32 * j + li, N - 1);
+      const float mu = gld(d->bn_mean + colc);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        float po[16], yv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = min(rbase + 32 * i + (r & 3) + 8 * (r >> 2), M - 1);
+          po[r] = gld(d->bn_post + (long)row * ldp + colc);
+          yv[r] = gld(d->bn_y + (long)row * ldp + colc);
+        }
+        const float* v = (const float*)&acc[i][j];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          dy[i][j][r] = po[r] > 0.f ? v[r] : v[r] * sl;
+          yc[i][j][r] = yv[r] - mu;
+        }
+      }
+    }
+    // tile partials per column: lane rows (16 per block) -> lane halves -> waves of the column
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const bool colok = n0 + 32 * j + li < N;
+      double S = 0.0, D = 0.0;
+      if (owner && colok) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
+            if (row < M) {
+              S += (double)dy[i][j][r];
+              D += (double)(yc[i][j][r] * dy[i][j][r]);
+            }
+          }
+      }
+      S += __shfl_xor(S, 32);
+      D += __shfl_xor(D, 32);
+      if (owner && lh == 0) {
+        s_bnd[(((wm * WN + wn) * TN + j) * 32 + li) * 2] = S;
+        s_bnd[(((wm * WN + wn) * TN + j) * 32 + li) * 2 + 1] = D;
+      }
+    }
+    __syncthreads();
+    if (owner && wm == 0 && lh == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + 32 * j + li;
+        double S = 0.0, D = 0.0;
+        for (int q = 0; q < WM; ++q) {
+          S += s_bnd[(((q * WN + wn) * TN + j) * 32 + li) * 2];
+          D += s_bnd[(((q * WN + wn) * TN + j) * 32 + li) * 2 + 1];
+        }
+        if (col < N) {
+          cgl_pubd(d->bn_dpart + ((long)tm * N + col) * 2, S);
+          cgl_pubd(d->bn_dpart + ((long)tm * N + col) * 2 + 1, D);
+        }
+      }
+    }
+    cgl_rendezvous(d->rv_count + tn, (unsigned int)d->tiles_m, d->err);
+    // every column of the workgroup tile: the tiles_m partials staged through LDS (one round trip,
+    // few registers), then summed in tile order
+    const int ncw = WN * TN * 32, c0 = tn * WN * TN * 32;
+    float* s_gm = s_bn;          // [ncw]: S / M
+    float* s_k = s_bn + 128;     // [ncw]: D invstd^2 / M
+    {
+      const int nt = d->tiles_m, items = nt * ncw;
+      unsigned long long* stg = (unsigned long long*)s_red;    // [nt][ncw][2]
+      unsigned long long v0[CGL_BN_STG], v1[CGL_BN_STG];
+#pragma unroll
+      for (int u = 0; u < CGL_BN_STG; ++u) {
+        const int q = min(tid + 256 * u, items - 1);
+        const int t = q / ncw, col = min(c0 + q % ncw, N - 1);
+        v0[u] = cgl_ld64(d->bn_dpart + ((long)t * N + col) * 2);
+        v1[u] = cgl_ld64(d->bn_dpart + ((long)t * N + col) * 2 + 1);
+      }
+#pragma unroll
+      for (int u = 0; u < CGL_BN_STG; ++u) {
+        const int q = tid + 256 * u;
+        if (q < items) {
+          stg[2 * q] = v0[u];
+          stg[2 * q + 1] = v1[u];
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < ncw) {
+      const int col = min(c0 + tid, N - 1);
+      const int nt = d->tiles_m;
+      const unsigned long long* stg = (const unsigned long long*)s_red;
+      double S = 0.0, D = 0.0;
+      for (int t = 0; t < nt; ++t) {
+        S += __longlong_as_double((long long)stg[2 * (t * ncw + tid)]);
+        D += __longlong_as_double((long long)stg[2 * (t * ncw + tid) + 1]);
+      }
+      const float invstd = gld(d->bn_invstd + col);
+      s_k[tid] = (float)D * invstd * invstd / M;
+      s_gm[tid] = (float)(S / M);
+      if (tm == 0 && c0 + tid < N) {
+        gst(d->bn_g_gamma + col, (float)(D * (double)invstd));
+        gst(d->bn_g_beta + col, (float)S);
+      }
+    }
+    __syncthreads();
+    if (owner) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + 32 * j + li;
+        if (col >= N) continue;
+        const int cl = col - c0;
+        const float invstd = gld(d->bn_invstd + col), w = gld(d->bn_gamma + col);
+        const float gm = s_gm[cl], k = s_k[cl];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
+            if (row < M) gst(d->C + (long)row * d->ldc + col, (dy[i][j][r] - gm - yc[i][j][r] * k) * invstd * w);
+          }
+      }
+    }
+    return;
   }
 
   // forward BatchNorm partials of the stored output: per column, per group slot {sum, M2}
@@ -486,12 +826,124 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
         if (col < N) {
           for (int s = 0; s < 2; ++s) {
             float* p = d->stat_part + ((long)(tm * 2 + s) * N + col) * 2;
-            gst(p, part[j][s][0]);
-            gst(p + 1, part[j][s][1]);
+            if (d->bn_fuse == 1) {
+              cgl_pub2f(p, part[j][s][0], part[j][s][1]);
+            } else {
+              gst(p, part[j][s][0]);
+              gst(p + 1, part[j][s][1]);
+            }
           }
         }
       }
     }
+  }
+
+  // ---------------- fused BatchNorm1d forward (bn_fuse 1): C = Y (the Linear output, kept for
+  // the backward), act = LeakyReLU(BN(Y)) with the statistics of the Y rows' forward call (group
+  // of stat_gr rows), combined from every row tile's published {sum, M2} partials exactly as
+  // cgl_bn_apply does (tile order, double, Chan); row tile 0 writes save_mean / save_invstd and
+  // updates the running statistics group by group (the reference's forward-call order)
+  if (d->bn_fuse == 1) {
+    cgl_rendezvous(d->rv_count + tn, (unsigned int)d->tiles_m, d->err);
+    const int gr = d->stat_gr;
+    const int ng = (M + gr - 1) / gr;          // <= 2 (planner)
+    const int ncw = WN * TN * 32, c0 = tn * WN * TN * 32;
+    float* s_sc = s_bn;            // [2][128]
+    float* s_sh = s_bn + 256;      // [2][128]
+    double* s_mu = s_bnd;          // [2][128]
+    double* s_m2 = s_bnd + 256;    // [2][128]
+    {
+      // stage every row tile's {sum, M2} pair of both group slots for the tile's columns (one round
+      // trip): stg[slot][t][c]
+      const int nt = d->tiles_m, items = 2 * nt * ncw;
+      unsigned long long* stg = (unsigned long long*)s_red;
+      unsigned long long v[2 * CGL_BN_STG];
+#pragma unroll
+      for (int u = 0; u < 2 * CGL_BN_STG; ++u) {
+        const int q = min(tid + 256 * u, items - 1);
+        const int sl2 = q / (nt * ncw), t = (q / ncw) % nt, col = min(c0 + q % ncw, N - 1);
+        v[u] = cgl_ld64(d->stat_part + ((long)(t * 2 + sl2) * N + col) * 2);
+      }
+#pragma unroll
+      for (int u = 0; u < 2 * CGL_BN_STG; ++u) {
+        const int q = tid + 256 * u;
+        if (q < items) stg[q] = v[u];
+      }
+    }
+    __syncthreads();
+    int n_g = 0;
+    if (tid < ncw * ng) {
+      const int cl = tid % ncw, g = tid / ncw;
+      const int col = min(c0 + cl, N - 1);
+      const int r0 = g * gr, r1 = min(r0 + gr, M);
+      n_g = r1 - r0;
+      const int t0 = r0 / BM, t1 = (r1 - 1) / BM;
+      const int nt = t1 - t0 + 1;
+      const unsigned long long* stg = (const unsigned long long*)s_red;
+      auto pr = [&](int j) {
+        const int t = t0 + j;
+        const int slot = (t * BM < r0) ? 1 : 0;   // tile starts in the previous group
+        return stg[(slot * d->tiles_m + t) * ncw + cl];
+      };
+      double sm = 0.0;
+      for (int j = 0; j < nt; ++j) sm += (double)__uint_as_float((unsigned int)pr(j));
+      const double mu = sm / n_g;
+      double m2 = 0.0;
+      for (int j = 0; j < nt; ++j) {
+        const int t = t0 + j;
+        const int c = min((t + 1) * BM, r1) - max(t * BM, r0);
+        const unsigned long long p = pr(j);
+        const double dd = (double)__uint_as_float((unsigned int)p) / c - mu;
+        m2 += (double)__uint_as_float((unsigned int)(p >> 32)) + c * dd * dd;
+      }
+      const double invstd = 1.0 / sqrt(m2 / n_g + d->bn_eps);
+      const float sc = (float)invstd * gld(d->bn_gamma + col);
+      s_sc[g * 128 + cl] = sc;
+      s_sh[g * 128 + cl] = gld(d->bn_beta + col) - (float)mu * sc;
+      s_mu[g * 128 + cl] = mu;
+      s_m2[g * 128 + cl] = m2;
+      if (tm == 0 && c0 + cl < N && d->bn_save_mean) {
+        gst(d->bn_save_mean + (long)g * N + col, (float)mu);
+        gst(d->bn_save_invstd + (long)g * N + col, (float)invstd);
+      }
+    }
+    __syncthreads();
+    if (tm == 0 && tid < ncw && c0 + tid < N && d->bn_run_mean) {
+      const int col = c0 + tid;
+      const double mom = d->bn_momentum;
+      float rm = gld(d->bn_run_mean + col), rv = gld(d->bn_run_var + col);
+      for (int g = 0; g < ng; ++g) {
+        const int n = min((g + 1) * gr, M) - g * gr;
+        rm = (float)(mom * s_mu[g * 128 + tid] + (1.0 - mom) * (double)rm);
+        rv = (float)(mom * (s_m2[g * 128 + tid] / (n - 1)) + (1.0 - mom) * (double)rv);
+      }
+      gst(d->bn_run_mean + col, rm);
+      gst(d->bn_run_var + col, rv);
+    }
+    if (owner) {
+      const float sl = d->slope;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + 32 * j + li;
+        if (col >= N) continue;
+        const int cl = col - c0;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const float* v = (const float*)&acc[i][j];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
+            if (row < M) {
+              const int g = row >= gr ? 1 : 0;
+              const float x = fmaf(v[r], s_sc[g * 128 + cl], s_sh[g * 128 + cl]);
+              gst(d->C + (long)row * d->ldc + col, v[r]);
+              gst(d->bn_act + (long)row * d->bn_ld_act + col, x > 0.f ? x : x * sl);
+            }
+          }
+        }
+      }
+    }
+    return;
   }
 
   if (owner) {
@@ -530,11 +982,13 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 // layer side by side).  Separate symbols keep the 1x1 variant's register budget (and so its
 // occupancy) independent of the 2x2 variant's.
 // Dynamic LDS: split-K partials of the waves with wk > 0.
-template <int TM, int TN, bool SK = false>
+template <int TM, int TN, bool SK = false, bool GL = false>
 __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDesc* __restrict__ descs, int ndesc) {
   extern __shared__ float cgl_dyn_lds[];
   __shared__ float s_col[4 * TN * 32];          // per-column reductions across waves (WM WN <= 4)
   __shared__ int s_flag[1];                     // split-K: this workgroup reduces its tile
+  __shared__ float s_bn[512];                   // fused BatchNorm: per-column tables
+  __shared__ double s_bnd[4 * TN * 32 * 2 > 512 ? 4 * TN * 32 * 2 : 512];
   float* s_red = cgl_dyn_lds;
   const int bid = blockIdx.x;
   int di = 0;
@@ -547,9 +1001,9 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
 #define CGL_BODY(L)                                               \
   do {                                                            \
     if (vec)                                                      \
-      cgl_gemm_body<L, 1, TM, TN, SK>(d, bid, s_red, s_col, s_flag);    \
+      cgl_gemm_body<L, 1, TM, TN, SK, GL>(d, bid, s_red, s_col, s_flag, s_bn, s_bnd);    \
     else                                                          \
-      cgl_gemm_body<L, 0, TM, TN, SK>(d, bid, s_red, s_col, s_flag);    \
+      cgl_gemm_body<L, 0, TM, TN, SK, GL>(d, bid, s_red, s_col, s_flag, s_bn, s_bnd);    \
   } while (0)
   if (layout == 0)
     CGL_BODY(0);
@@ -561,8 +1015,20 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
 }
 
 // Host helper: dynamic LDS bytes of one problem's split-K partials.
-inline int cgl_gemm_stage_bytes(const CglGemmDesc& d) {
-  return (d.WK > 1) ? d.WM * d.WN * (d.WK - 1) * d.TM * d.TN * 16 * 64 * 4 : 0;
+// LDS ring of the staged main loop (GL launches, 1x1 blocks, layouts 0 / 1 with 16-byte operands)
+inline bool cgl_gemm_gl_ok(const CglGemmDesc& d) {
+  return d.layout != 2 && d.TM == 1 && d.TN == 1 && d.a_vec && d.b_vec && d.ksplit <= 1 && !d.b_ones_col &&
+         d.WM * d.WN * d.WK == 4;
+}
+inline int cgl_gemm_gl_bytes(const CglGemmDesc& d) {
+  return cgl_gemm_gl_ok(d) ? d.WK * CGL_GL_NS * (4 * d.WM + 4 * d.WN) * 1024 : 0;
+}
+inline int cgl_gemm_stage_bytes(const CglGemmDesc& d, bool gl = false) {
+  const int sk0 = (d.WK > 1) ? d.WM * d.WN * (d.WK - 1) * d.TM * d.TN * 16 * 64 * 4 : 0;
+  const int glb = gl ? cgl_gemm_gl_bytes(d) : 0;
+  const int sk = sk0 > glb ? sk0 : glb;
+  const int bn = d.bn_fuse ? cgl_bn_stage_bytes(d.tiles_m, d.WN * d.TN * 32) : 0;
+  return sk > bn ? sk : bn;
 }
 
 // Host helpers: workgroups of one problem, and the split-K partial floats it needs.

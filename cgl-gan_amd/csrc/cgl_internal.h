@@ -97,6 +97,25 @@ struct CglGemmDesc {
   int ksplit;
   float* kpart;                        // [ksplit][tiles][WM*WN][TM*TN][16][64] floats
   unsigned int* kcount;                // [tiles], zero at rest
+  // BatchNorm1d fused into the epilogue through an in-launch rendezvous of the column tile's
+  // tiles_m workgroups (cgl_gemm.hip, "fused BatchNorm"):
+  //   bn_fuse 1 (forward, train): C = the Linear output Y, act = LeakyReLU(BN(Y)) per group of
+  //            stat_gr rows; statistics from the published per-tile {sum, M2} partials (stat_part);
+  //            save_mean / save_invstd and the running statistics written by row tile 0
+  //   bn_fuse 2 (backward, train): C = dZ = BN-backward(LeakyReLU'(post) * (A B)) with the
+  //            saved mean / invstd of one forward call; per-tile {sum dy, sum dy (y - mean)}
+  //            partials (bn_dpart, double); g_gamma / g_beta written by row tile 0
+  int bn_fuse;
+  unsigned int* rv_count;              // [tiles_n] monotonic rendezvous tickets (zero at creation)
+  unsigned int* err;                   // set on a rendezvous timeout (never expected)
+  const float* bn_gamma; const float* bn_beta;
+  float* bn_act; int bn_ld_act;        // forward: post-LeakyReLU output
+  double bn_eps, bn_momentum;
+  float* bn_run_mean; float* bn_run_var; float* bn_save_mean; float* bn_save_invstd;
+  const float* bn_post; const float* bn_y; int bn_ld_post;   // backward: LeakyReLU output, BN input
+  const float* bn_mean; const float* bn_invstd;              // backward: saved statistics
+  float* bn_g_gamma; float* bn_g_beta;
+  double* bn_dpart;                    // backward partials [tiles_m][N][2]
 };
 
 // BatchNorm1d(train) + LeakyReLU over the whole [mtot][F] output of one G layer.
@@ -173,6 +192,7 @@ struct CglStepState {
   float losses[CGL_MAX_WORKERS];    // gathered G losses (N > 1)
   float alphas[CGL_MAX_WORKERS];
   long long bn_batches;             // num_batches_tracked of every G BatchNorm layer
+  unsigned int err;                 // sticky: an in-launch rendezvous timed out (never expected)
 };
 
 enum { CGL_W_CAPGAN = 0, CGL_W_MEAN = 1, CGL_W_MIX_SINGLE = 2, CGL_W_MIX_DOUBLE = 3, CGL_W_CGLGAN = 4 };

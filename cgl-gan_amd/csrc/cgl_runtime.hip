@@ -114,6 +114,7 @@ constexpr int kMaxHeadDescs = 2 * CGL_MAX_EPOCH + 4;
 constexpr int kMaxBnDescs = 2 * CGL_MAX_LAYERS;
 constexpr int kSplitKCounters = 8192;           // split-K tickets (one per tile of a launch)
 constexpr int kCounters = 64;                    // head-loss tickets
+constexpr int kRvCounters = 4096;                // fused-BatchNorm rendezvous tickets (monotonic)
 constexpr int64_t kSplitKFloats = 4 << 20;       // split-K partials of one launch (16 MiB)
 
 struct WS {
@@ -141,6 +142,8 @@ struct WS {
   unsigned int* counters;   // [kCounters]: head-loss tickets
   float* kpart;             // [kSplitKFloats]: split-K partials (reused by every launch)
   unsigned int* kcount;     // [kSplitKCounters]: split-K tickets (zero at rest)
+  unsigned int* rvcount;    // [kRvCounters]: fused-BatchNorm rendezvous tickets (monotonic)
+  double* gdpart[CGL_MAX_LAYERS];   // fused BatchNorm backward partials [B/32][f][2]
   CglStepState* st;
   int* idx;       // sampler output when sample_n > 0
   CglGemmDesc* gemm;
@@ -192,6 +195,9 @@ WS carve_ws(const cgl_gan_config& c, void* base) {
   // split-K scratch last, so that the layout of everything the default plan touches is unchanged
   w.kpart = cv.take<float>(kSplitKFloats);
   w.kcount = cv.take<unsigned int>(kSplitKCounters);
+  w.rvcount = cv.take<unsigned int>(kRvCounters);
+  for (int l = 0; l + 1 < L; ++l)
+    if (g.bn[l]) w.gdpart[l] = cv.take<double>((int64_t)((B + 31) / 32) * g.dims[l + 1] * 2);
   w.total = cv.off;
   return w;
 }
@@ -218,6 +224,7 @@ struct Launch {
   int shmem = 0;        // dynamic LDS bytes (GEMM)
   int blk = 1;          // GEMM per-wave block shape (TM = TN = blk)
   bool sk = false;      // GEMM launch holds a split-K problem
+  bool gl = false;      // GEMM launch uses the LDS-staged (glds) main loop instantiation
 };
 
 // Split-K partials of 2x2-block waves need up to 48 KB of dynamic LDS (+16 KB BN table).
@@ -226,6 +233,7 @@ hipError_t gemm_lds_attr() {
   if (!done) {
     // advisory on this platform (launches up to the per-CU LDS succeed); never fail on it
     for (const void* fn : {(const void*)cgl_gemm_f32<1, 1>, (const void*)cgl_gemm_f32<2, 2>,
+                           (const void*)cgl_gemm_f32<1, 1, false, true>,
                            (const void*)cgl_gemm_f32<1, 1, true>, (const void*)cgl_gemm_f32<2, 2, true>}) {
       for (int kb : {150, 128, 96, 64}) {
         const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kb * 1024);
@@ -238,8 +246,11 @@ hipError_t gemm_lds_attr() {
   return hipSuccess;
 }
 
-void launch_gemm(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, int n, bool sk = false) {
-  if (sk) {   // a launch with a split-K problem: the instantiation carrying the combine
+void launch_gemm(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, int n, bool sk = false,
+                 bool gl = false) {
+  if (gl) {
+    cgl_gemm_f32<1, 1, false, true><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+  } else if (sk) {   // a launch with a split-K problem: the instantiation carrying the combine
     if (blk == 2)
       cgl_gemm_f32<2, 2, true><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
     else
@@ -393,6 +404,8 @@ struct cgl_gan {
   bool two_streams = false;
   float* xchg = nullptr;
   int64_t xchg_n = 0;
+  int rv_used = 0;             // rendezvous counters handed out
+  int gemm_cap[3] = {0, 0, 0}; // co-resident workgroups of cgl_gemm_f32<1,1> / <2,2> (0: unknown)
   // parameter tensor pointers
   std::vector<TensorRec> gl, dl;
   int64_t run_mean_off[CGL_MAX_LAYERS], run_var_off[CGL_MAX_LAYERS];
@@ -429,8 +442,51 @@ float* dgrad(const cgl_gan* c, int layer, int kind) {
   return nullptr;
 }
 
-// Add a grouped GEMM launch built from `descs` (workgroup offsets assigned here).
-void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> descs) {
+// Workgroups of cgl_gemm_f32<blk, blk> guaranteed co-resident on the device at `shmem` dynamic LDS:
+// one workgroup per CU less than the occupancy query reports (MI355X_MICROARCH.md: the query can be one
+// high), times the CU count.
+int gemm_resident(int blk, int shmem) {
+  int dev = 0, cus = 0, nb = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  const void* fn = blk == 2 ? (const void*)cgl_gemm_f32<2, 2> : (const void*)cgl_gemm_f32<1, 1>;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, CGL_GEMM_THREADS, shmem) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return std::max(nb - 1, 0) * cus;
+}
+
+// Fused BatchNorm (in-launch rendezvous instead of the cgl_bn_apply / cgl_bn_bwd launches) is
+// correct but measured no faster on MI355X at B = 256 (profiles/r02_bn_fuse_ab.txt: the rendezvous
+// -- ticket, poll, the staged partials' sc1 round trip -- costs what the launch boundary it removes
+// costs, and G L3's 512-workgroup launch loses to load imbalance), so it is opt-in: CGL_BN_FUSE=1.
+// LDS-staged (glds) GEMM main loop: correct on every shape, faster in isolation on the large NT
+// shapes (tools/gemm_lds_bench.hip: G L4 fwd 20.6 -> 14.2 us, L2-hot operands) but slower inside
+// the round (profiles/r02_gemm_gl_ab.txt: 0.272 vs 0.255 ms; its one-stage prefetch exposes the
+// operands' first-touch latency every 32 k), so opt-in: CGL_GEMM_GL=1.
+bool gemm_gl_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CGL_GEMM_GL");
+    v = (e && atoi(e) != 0) ? 1 : 0;
+  }
+  return v == 1;
+}
+
+bool bn_fuse_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CGL_BN_FUSE");
+    v = (e && atoi(e) != 0) ? 1 : 0;
+  }
+  return v == 1;
+}
+
+// Add a grouped GEMM launch built from `descs` (workgroup offsets assigned here).  Returns false --
+// and pushes nothing -- when a fused-BatchNorm problem is in the group but the launch's grid is not
+// guaranteed co-resident (its in-launch rendezvous could then wait on an unscheduled workgroup).
+bool push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> descs) {
   Launch L;
   L.kind = K_GEMM;
   L.first = (int)c->gemm.size();
@@ -448,14 +504,35 @@ void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
   }
   for (auto& d : descs)
     if (d.TM != blk) choose_tiles(d, 0, blk);
+  // LDS-staged main loop: every problem of the launch must qualify (a TN problem beside it would
+  // pay the ring's LDS in occupancy); its tiling is 32x32 per workgroup with the four waves on K
+  // slices (microbenchmarked best for the staged loop: tools/gemm_lds_bench.hip)
+  bool gl = blk == 1 && gemm_gl_enabled();
+  for (auto& d : descs) {
+    set_vec(d);
+    CglGemmDesc t = d;
+    t.WM = t.WN = 1;
+    t.WK = 4;
+    t.ksplit = 1;
+    gl = gl && !d.bn_fuse && cgl_gemm_gl_ok(t);
+  }
+  if (gl)
+    for (auto& d : descs) {
+      d.WM = d.WN = 1;
+      d.WK = 4;
+      d.tiles_m = (d.M + 31) / 32;
+      d.tiles_n = (d.N + 31) / 32;
+    }
   L.blk = blk;
   long kp = 0;
   unsigned int kc = 0;
+  bool fused = false;
+  for (auto& d : descs) fused = fused || d.bn_fuse != 0;
   for (auto& d : descs) {
     set_vec(d);
     // split-K: only on the single-stream plan (the partial / ticket regions are per launch)
     d.ksplit = 1;
-    if (!c->two_streams) {
+    if (!c->two_streams && !fused && !gl) {
       choose_ks(d);
       if (d.ksplit > 1 && (kp + cgl_gemm_kpart_floats(d) > kSplitKFloats ||
                            kc + d.tiles_m * d.tiles_n > (unsigned)kSplitKCounters))
@@ -477,7 +554,48 @@ void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
   }
   L.grid = wg;
   L.shmem = stage;
+  if (gl) {
+    L.gl = true;
+    int st2 = 0;
+    for (int q = L.first; q < L.first + L.count; ++q) st2 = std::max(st2, cgl_gemm_stage_bytes(c->gemm[q], true));
+    L.shmem = st2;
+  }
+  if (getenv("CGL_PLAN_DEBUG")) {
+    for (int q = L.first; q < L.first + L.count; ++q) {
+      const CglGemmDesc& d = c->gemm[q];
+      fprintf(stderr, "gemm launch %zu: desc %d layout %d M %d N %d K %d WM %d WN %d WK %d TM %d TN %d tiles %dx%d "
+              "ks %d grid %d shmem %d gl %d blk %d vec %d/%d\n", ph.size(), q, d.layout, d.M, d.N, d.K, d.WM, d.WN,
+              d.WK, d.TM, d.TN, d.tiles_m, d.tiles_n, d.ksplit, L.grid, L.shmem, (int)L.gl, L.blk, d.a_vec, d.b_vec);
+    }
+  }
+  if (fused) {
+    int rv = c->rv_used;
+    for (auto& d : descs) {
+      if (!d.bn_fuse) continue;
+      const bool ok = d.tiles_m <= CGL_BN_MAXT && d.tiles_m * d.WN * d.TN * 32 <= 256 * CGL_BN_STG &&
+                      rv + d.tiles_n <= kRvCounters &&
+                      (d.bn_fuse != 1 || (d.M + d.stat_gr - 1) / d.stat_gr <= 2);
+      if (!ok) {
+        c->gemm.resize(L.first);
+        return false;
+      }
+    }
+    const int cap = gemm_resident(blk, stage);
+    if (cap <= 0 || L.grid > cap) {
+      c->gemm.resize(L.first);
+      return false;
+    }
+    for (int q = L.first; q < L.first + L.count; ++q) {
+      CglGemmDesc& d = c->gemm[q];
+      if (!d.bn_fuse) continue;
+      d.rv_count = c->ws.rvcount + rv;
+      d.err = &c->ws.st->err;
+      rv += d.tiles_n;
+    }
+    c->rv_used = rv;
+  }
   ph.push_back(L);
+  return true;
 }
 
 void push_head(cgl_gan* c, std::vector<Launch>& ph, const CglHeadDesc& h) {
@@ -596,6 +714,23 @@ int build_plan(cgl_gan* c) {
     e.slope = sl;
     e.C = w.gout[l];
     e.ldc = fo;
+    if (l + 1 < L && g.bn[l] && bn_fuse_enabled()) {
+      // BatchNorm1d(train) + LeakyReLU in this GEMM's epilogue (in-launch rendezvous of each
+      // column tile's row tiles) instead of a cgl_bn_apply launch
+      CglGemmDesc f = e;
+      f.bn_fuse = 1;
+      f.bn_gamma = gparam(c, l, 2);
+      f.bn_beta = gparam(c, l, 3);
+      f.bn_act = w.gact[l];
+      f.bn_ld_act = fo;
+      f.bn_eps = cf.bn_eps;
+      f.bn_momentum = cf.bn_momentum;
+      f.bn_run_mean = c->bufs.g_running + c->run_mean_off[l];
+      f.bn_run_var = c->bufs.g_running + c->run_var_off[l];
+      f.bn_save_mean = w.gmean[l];
+      f.bn_save_invstd = w.ginvstd[l];
+      if (push_gemm(c, A, {f})) continue;
+    }
     push_gemm(c, A, {e});
     if (l + 1 < L && g.bn[l]) {
       CglBnApplyDesc ap;
@@ -607,7 +742,8 @@ int build_plan(cgl_gan* c) {
       ap.ld_act = fo;
       CglBnFwd& bn = ap.bn;
       bn.part = w.gpart[l];
-      bn.part_bm = 32 * e.TM * e.WM;
+      // the producer's row-tile height as pushed (push_gemm may re-tile the launch)
+      bn.part_bm = 32 * c->gemm.back().TM * c->gemm.back().WM;
       bn.gr = B;
       bn.mtot = 2 * B;
       bn.gamma = gparam(c, l, 2);
@@ -865,6 +1001,7 @@ int build_plan(cgl_gan* c) {
       t.bias_out = ggrad(c, l, 1);
       grp.push_back(t);
     }
+    bool bn_fused = false;
     if (l >= 1) {
       CglGemmDesc n = make_gemm(1, B, fi, fo);
       n.a = rows(gbuf(l), fo);
@@ -879,15 +1016,34 @@ int build_plan(cgl_gan* c) {
         n.mask_ld = fi;
         n.C = w.gG[l - 1];
       }
+      // BatchNorm1d backward in the input-gradient GEMM's epilogue (not at the Mix-G exchange
+      // point: there the all-reduce of dA sits between the GEMM and the BatchNorm backward)
+      if (g.bn[l - 1] && cf.exchange_layer != l && bn_fuse_enabled()) {
+        CglGemmDesc f = n;
+        f.bn_fuse = 2;
+        f.C = w.gG[l - 1];
+        f.bn_post = w.gact[l - 1] + (int64_t)B * fi;
+        f.bn_y = w.gout[l - 1] + (int64_t)B * fi;
+        f.bn_ld_post = fi;
+        f.bn_mean = w.gmean[l - 1] + fi;        // group 1 = the Xg forward call
+        f.bn_invstd = w.ginvstd[l - 1] + fi;
+        f.bn_gamma = gparam(c, l - 1, 2);
+        f.bn_g_gamma = ggrad(c, l - 1, 2);
+        f.bn_g_beta = ggrad(c, l - 1, 3);
+        f.bn_dpart = w.gdpart[l - 1];
+        std::vector<CglGemmDesc> g2 = grp;
+        g2.push_back(f);
+        bn_fused = push_gemm(c, *ph, g2);
+      }
       grp.push_back(n);
     }
-    push_gemm(c, *ph, grp);
+    if (!bn_fused) push_gemm(c, *ph, grp);
     if (l >= 1 && cf.exchange_layer == l) {
       c->xchg = g.bn[l - 1] ? w.gdA[l - 1] : w.gG[l - 1];
       c->xchg_n = (int64_t)B * fi;
       ph = &Bp;
     }
-    if (l >= 1 && g.bn[l - 1]) {
+    if (l >= 1 && g.bn[l - 1] && !bn_fused) {
       CglBnBwdDesc b;
       std::memset(&b, 0, sizeof(b));
       b.M = B;
@@ -982,7 +1138,7 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
   }
   switch (L.kind) {
     case K_GEMM:
-      launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, L.count, L.sk);
+      launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, L.count, L.sk, L.gl);
       break;
     case K_HEAD:
       hipLaunchKernelGGL(cgl_head_loss, dim3(L.grid), dim3(256), 0, s, c->ws.head + L.first);
@@ -1125,6 +1281,7 @@ int cgl_gan_create(const cgl_gan_config* cfg, const cgl_gan_buffers* bufs, cgl_g
     he = hipMemcpy(c->ws.bnb, c->bnb.data(), c->bnb.size() * sizeof(CglBnBwdDesc), hipMemcpyHostToDevice);
   if (he == hipSuccess) he = hipMemset(c->ws.counters, 0, kCounters * sizeof(unsigned int));
   if (he == hipSuccess) he = hipMemset(c->ws.kcount, 0, kSplitKCounters * sizeof(unsigned int));
+  if (he == hipSuccess) he = hipMemset(c->ws.rvcount, 0, kRvCounters * sizeof(unsigned int));
   if (he == hipSuccess) he = hipMemset(c->ws.st, 0, sizeof(CglStepState));
   if (he == hipSuccess) he = hipDeviceSynchronize();
   if (he != hipSuccess) {
@@ -1154,6 +1311,7 @@ int cgl_gan_reset(cgl_gan* c, const float* beta_host, void* stream) {
   HIPCHK(hipMemcpyAsync(c->ws.st, &h, sizeof(h), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemsetAsync(c->ws.counters, 0, kCounters * sizeof(unsigned int), s));
   HIPCHK(hipMemsetAsync(c->ws.kcount, 0, kSplitKCounters * sizeof(unsigned int), s));
+  HIPCHK(hipMemsetAsync(c->ws.rvcount, 0, kRvCounters * sizeof(unsigned int), s));
   HIPCHK(hipStreamSynchronize(s));
   return CGL_OK;
 }
@@ -1270,7 +1428,7 @@ int cgl_gan_read_stats(cgl_gan* c, cgl_gan_stats* out, void* stream) {
   out->F = h.F;
   out->lambda_ = h.lambda;
   out->bn_batches = h.bn_batches;
-  return CGL_OK;
+  return h.err ? CGL_E_STATE : CGL_OK;   // a fused-BatchNorm rendezvous timed out
 }
 
 int cgl_gan_plan_info(cgl_gan* c, int phase, int* n_launches, int* n_gemm, double* flops) {
