@@ -28,9 +28,11 @@ EXPORTS = [
     "cgl_bn1d_bwd",
     # conv GAN path (model/lsgan.py)
     "cgl_conv3x3_workspace_bytes", "cgl_conv3x3_fwd", "cgl_conv3x3_bwd_data", "cgl_conv3x3_bwd_weight",
-    "cgl_bn2d_workspace_bytes", "cgl_bn2d_fwd", "cgl_bn2d_bwd", "cgl_act_drop_bwd", "cgl_dropout2d_mask",
+    "cgl_bn2d_workspace_bytes", "cgl_bn2d_fwd", "cgl_bn2d_bwd", "cgl_act_drop_bwd", "cgl_dropout2d_mask", "cgl_dropout2d_masks",
     "cgl_nchw_to_nhwc", "cgl_nhwc_to_nchw", "cgl_adv_loss", "cgl_adam_multi", "cgl_dense_workspace_bytes",
     "cgl_dense_fwd", "cgl_dense_bwd_data", "cgl_dense_bwd_weight", "cgl_gather_rows", "cgl_weights_scale",
+    "cgl_conv_packed_floats", "cgl_conv_pack_multi", "cgl_conv3x3_fwd_packed", "cgl_conv3x3_bwd_data_packed",
+    "cgl_dense_fwd_packed", "cgl_dense_bwd_data_packed",
     # evaluation (CGLGAN/2DMG/main.py plot_2d KL score)
     "cgl_kl_score",
 ]
@@ -60,6 +62,12 @@ class GanBuffers(ctypes.Structure):
                 ("z", ctypes.c_void_p), ("real", ctypes.c_void_p), ("real_idx", ctypes.c_void_p),
                 ("losses_all", ctypes.c_void_p), ("workspace", ctypes.c_void_p),
                 ("workspace_bytes", ctypes.c_int64)]
+
+
+class ConvPackJob(ctypes.Structure):
+    _fields_ = [("W", ctypes.c_void_p), ("Wp", ctypes.c_void_p), ("h", ctypes.c_int), ("w", ctypes.c_int),
+                ("cin", ctypes.c_int), ("cout", ctypes.c_int), ("stride", ctypes.c_int), ("up", ctypes.c_int),
+                ("ks", ctypes.c_int), ("dir", ctypes.c_int)]
 
 
 class GanStats(ctypes.Structure):
@@ -112,6 +120,7 @@ def _load():
         "cgl_bn2d_bwd": (ci, [vp, vp, vp, ci, ci, ci, ci, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, i64, vp]),
         "cgl_act_drop_bwd": (ci, [vp, vp, vp, ci, ci, ci, cf, ci, vp, vp]),
         "cgl_dropout2d_mask": (ci, [vp, ci, ci, cd, ctypes.c_ulonglong, ctypes.c_ulonglong, vp]),
+        "cgl_dropout2d_masks": (ci, [ci, P(vp), P(ci), P(ci), cd, ctypes.c_ulonglong, P(ctypes.c_ulonglong), vp]),
         "cgl_nchw_to_nhwc": (ci, [vp, vp, ci, ci, ci, vp]),
         "cgl_nhwc_to_nchw": (ci, [vp, vp, ci, ci, ci, vp]),
         "cgl_adv_loss": (ci, [vp, ci, ci, ci, ci, cd, vp, vp, vp]),
@@ -119,6 +128,12 @@ def _load():
         "cgl_dense_fwd": (ci, [vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, i64, vp]),
         "cgl_dense_bwd_data": (ci, [vp, vp, vp, ci, ci, ci, vp, i64, vp]),
         "cgl_dense_bwd_weight": (ci, [vp, vp, vp, vp, ci, ci, ci, vp, i64, vp]),
+        "cgl_conv_packed_floats": (i64, [ci] * 8),
+        "cgl_conv_pack_multi": (ci, [ci, P(ConvPackJob), vp]),
+        "cgl_conv3x3_fwd_packed": (ci, [vp, vp, vp, vp] + [ci] * 8 + [cf, vp, vp, i64, vp]),
+        "cgl_conv3x3_bwd_data_packed": (ci, [vp, vp, vp, vp] + [ci] * 7 + [vp, i64, vp]),
+        "cgl_dense_fwd_packed": (ci, [vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, i64, vp]),
+        "cgl_dense_bwd_data_packed": (ci, [vp, vp, vp, ci, ci, ci, vp, i64, vp]),
         "cgl_gather_rows": (ci, [vp, vp, i64, ci, ci, vp, vp]),
         "cgl_weights_scale": (ci, [ci, ci, ci, cf, P(cf), vp, vp, i64, vp, vp]),
         "cgl_kl_score": (ci, [vp, i64, i64, vp, i64, i64, ci, cd, cd, cd, cd, vp, vp, vp]),

@@ -58,17 +58,26 @@ def conv_ws_bytes(n, h, w, cin, cout, stride, up):
     return b
 
 
-def conv3x3_fwd(x, w, b, y, n, h, wd, cin, cout, stride=1, up=0, act=ACT_NONE, slope=0.2, drop=None):
-    _chk(x, w, b, y, drop)
+def conv3x3_fwd(x, w, b, y, n, h, wd, cin, cout, stride=1, up=0, act=ACT_NONE, slope=0.2, drop=None, wp=None):
+    """``wp``: the weights pre-packed by a PackSet (no per-call pack launch); ``w`` is then unused."""
+    _chk(x, w, b, y, drop, wp)
     ws = workspace(conv_ws_bytes(n, h, wd, cin, cout, stride, up), x.device)
+    if wp is not None:
+        C.check(C.lib.cgl_conv3x3_fwd_packed(_p(x), _p(wp), _p(b), _p(y), n, h, wd, cin, cout, stride, up, act,
+                                             float(slope), _p(drop), _p(ws), ws.numel(), _s()), "cgl_conv3x3_fwd_packed")
+        return y
     C.check(C.lib.cgl_conv3x3_fwd(_p(x), _p(w), _p(b), _p(y), n, h, wd, cin, cout, stride, up, act, float(slope),
                                   _p(drop), _p(ws), ws.numel(), _s()), "cgl_conv3x3_fwd")
     return y
 
 
-def conv3x3_bwd_data(dy, w, dx, n, h, wd, cin, cout, stride=1, up=0):
-    _chk(dy, w, dx)
+def conv3x3_bwd_data(dy, w, dx, n, h, wd, cin, cout, stride=1, up=0, wp=None):
+    _chk(dy, w, dx, wp)
     ws = workspace(conv_ws_bytes(n, h, wd, cin, cout, stride, up), dy.device)
+    if wp is not None:
+        C.check(C.lib.cgl_conv3x3_bwd_data_packed(_p(dy), _p(w), _p(wp), _p(dx), n, h, wd, cin, cout, stride, up,
+                                                  _p(ws), ws.numel(), _s()), "cgl_conv3x3_bwd_data_packed")
+        return dx
     C.check(C.lib.cgl_conv3x3_bwd_data(_p(dy), _p(w), _p(dx), n, h, wd, cin, cout, stride, up, _p(ws), ws.numel(),
                                        _s()), "cgl_conv3x3_bwd_data")
     return dx
@@ -89,17 +98,25 @@ def dense_ws_bytes(M, K, N):
     return b
 
 
-def dense_fwd(x, w, b, y, M, K, N, act=ACT_NONE, slope=0.2):
-    _chk(x, w, b, y)
+def dense_fwd(x, w, b, y, M, K, N, act=ACT_NONE, slope=0.2, wp=None):
+    _chk(x, w, b, y, wp)
     ws = workspace(dense_ws_bytes(M, K, N), x.device)
+    if wp is not None:
+        C.check(C.lib.cgl_dense_fwd_packed(_p(x), _p(wp), _p(b), _p(y), M, K, N, act, float(slope), _p(ws), ws.numel(),
+                                           _s()), "cgl_dense_fwd_packed")
+        return y
     C.check(C.lib.cgl_dense_fwd(_p(x), _p(w), _p(b), _p(y), M, K, N, act, float(slope), _p(ws), ws.numel(), _s()),
             "cgl_dense_fwd")
     return y
 
 
-def dense_bwd_data(dy, w, dx, M, K, N):
-    _chk(dy, w, dx)
+def dense_bwd_data(dy, w, dx, M, K, N, wp=None):
+    _chk(dy, w, dx, wp)
     ws = workspace(dense_ws_bytes(M, K, N), dy.device)
+    if wp is not None:
+        C.check(C.lib.cgl_dense_bwd_data_packed(_p(dy), _p(wp), _p(dx), M, K, N, _p(ws), ws.numel(), _s()),
+                "cgl_dense_bwd_data_packed")
+        return dx
     C.check(C.lib.cgl_dense_bwd_data(_p(dy), _p(w), _p(dx), M, K, N, _p(ws), ws.numel(), _s()), "cgl_dense_bwd_data")
     return dx
 
@@ -110,6 +127,45 @@ def dense_bwd_weight(dy, x, dw, db, M, K, N):
     C.check(C.lib.cgl_dense_bwd_weight(_p(dy), _p(x), _p(dw), _p(db), M, K, N, _p(ws), ws.numel(), _s()),
             "cgl_dense_bwd_weight")
     return dw
+
+
+class PackSet:
+    """The packed MFMA weight operands of several layers, refreshed by ONE cgl_conv_pack_multi launch.
+
+    ``add(group, key, w, h, w_, cin, cout, stride, up, ks, dir)`` registers a (layer, direction)
+    pair; ``finalize(device)`` allocates one flat buffer (views ``self[key]``); ``run(group)`` packs
+    every operand of that group (None: all groups) from the current weights (stream-ordered,
+    capturable)."""
+
+    def __init__(self):
+        self._jobs, self._views, self._arrs = [], {}, {}
+
+    def add(self, group, key, w, h, wd, cin, cout, stride=1, up=0, ks=3, dir=0):
+        n = C.lib.cgl_conv_packed_floats(h, wd, cin, cout, stride, up, ks, dir)
+        if n < 0:
+            raise RuntimeError(f"PackSet: bad geometry for {key} (rc={n})")
+        self._jobs.append((group, key, w, int(n), (h, wd, cin, cout, stride, up, ks, dir)))
+
+    def finalize(self, device):
+        tot = sum((n + 63) // 64 * 64 for _, _, _, n, _ in self._jobs)
+        self.buf = torch.zeros(max(tot, 64), dtype=torch.float32, device=device)
+        recs, off = [], 0
+        for group, key, w, n, geo in self._jobs:
+            _chk(w)
+            self._views[key] = self.buf[off:off + n]
+            recs.append((group, C.ConvPackJob(w.data_ptr(), self.buf[off:].data_ptr(), *geo)))
+            off += (n + 63) // 64 * 64
+        for g in [None] + sorted({r[0] for r in recs}):
+            sel = [j for grp, j in recs if g is None or grp == g]
+            self._arrs[g] = (len(sel), (C.ConvPackJob * len(sel))(*sel))
+        return self
+
+    def __getitem__(self, key):
+        return self._views[key]
+
+    def run(self, group=None):
+        n, arr = self._arrs[group]
+        C.check(C.lib.cgl_conv_pack_multi(n, arr, _s()), "cgl_conv_pack_multi")
 
 
 def gather_rows(src, idx, row0, nrows, row_floats, dst):
@@ -159,6 +215,17 @@ def dropout2d_mask(mask, n, c, p, seed, counter):
     C.check(C.lib.cgl_dropout2d_mask(_p(mask), n, c, float(p), int(seed) & (2 ** 64 - 1), int(counter) & (2 ** 64 - 1),
                                      _s()), "cgl_dropout2d_mask")
     return mask
+
+
+def dropout2d_masks(masks, ns, cs, p, seed, counters):
+    """Several dropout2d_mask calls in one launch (same p and seed)."""
+    _chk(*masks)
+    k = len(masks)
+    C.check(C.lib.cgl_dropout2d_masks(k, (ctypes.c_void_p * k)(*[m.data_ptr() for m in masks]),
+                                      (ctypes.c_int * k)(*ns), (ctypes.c_int * k)(*cs), float(p),
+                                      int(seed) & (2 ** 64 - 1),
+                                      (ctypes.c_ulonglong * k)(*[int(c) & (2 ** 64 - 1) for c in counters]), _s()),
+            "cgl_dropout2d_masks")
 
 
 def nchw_to_nhwc(x, y, n, c, hw):

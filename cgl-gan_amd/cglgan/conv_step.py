@@ -181,6 +181,23 @@ class ConvGanStep:
         self.beta = None
         self.set_beta(beta)
         self.round = 0
+        # packed MFMA weight operands of every layer (cglgan.conv_ops.PackSet): G and D are packed
+        # together at the start of a round (the exchanges between rounds may rewrite either), D again
+        # after its Adam step -- two pack launches per round instead of one per conv call
+        PG, PD = self.G.params, self.D.params
+        pk = O.PackSet()
+        pk.add("G", "l1", PG["l1.0.weight"], 1, 1, 100, 8192, ks=1)
+        pk.add("G", "c1f", PG["conv_blocks.1.weight"], 8, 8, 128, 128, 1, 1)
+        pk.add("G", "c1b", PG["conv_blocks.1.weight"], 8, 8, 128, 128, 1, 1, dir=1)
+        pk.add("G", "c5f", PG["conv_blocks.5.weight"], 16, 16, 128, 64, 1, 1)
+        pk.add("G", "c5b", PG["conv_blocks.5.weight"], 16, 16, 128, 64, 1, 1, dir=1)
+        pk.add("G", "c8f", PG["conv_blocks.8.weight"], 32, 32, 64, 1, 1, 0)
+        for ck, _, ci, co, hw in D_CONVS:
+            pk.add("D", ck + "f", PD[ck + ".weight"], hw, hw, ci, co, 2, 0)
+            pk.add("D", ck + "b", PD[ck + ".weight"], hw, hw, ci, co, 2, 0, dir=1)
+        pk.add("D", "advf", PD["adv_layer.weight"], 1, 1, 512, 1, ks=1)
+        pk.add("D", "advb", PD["adv_layer.weight"], 1, 1, 512, 1, ks=1, dir=1)
+        self.pk = pk.finalize(dev)
         # sampler over a device-resident real shard [n, 1024] (DataLoader(shuffle=True), capgan.py:282)
         self.data = data
         self._perm, self._pos = None, 0
@@ -220,14 +237,16 @@ class ConvGanStep:
 
     def _g_forward(self):
         P, B2 = self.G.params, 2 * self.B
-        O.dense_fwd(self.z, P["l1.0.weight"], P["l1.0.bias"], self.h, B2, 100, 8192)
+        O.dense_fwd(self.z, P["l1.0.weight"], P["l1.0.bias"], self.h, B2, 100, 8192, wp=self.pk["l1"])
         O.nchw_to_nhwc(self.h, self.h0, B2, 128, 64)      # out.view(B, 128, 8, 8), model/lsgan.py:25
-        O.conv3x3_fwd(self.h0, P["conv_blocks.1.weight"], P["conv_blocks.1.bias"], self.y1, B2, 8, 8, 128, 128, 1, 1)
+        O.conv3x3_fwd(self.h0, P["conv_blocks.1.weight"], P["conv_blocks.1.bias"], self.y1, B2, 8, 8, 128, 128, 1, 1,
+                      wp=self.pk["c1f"])
         self._g_bn("conv_blocks.2", self.y1, self.a1, 256, 128)
-        O.conv3x3_fwd(self.a1, P["conv_blocks.5.weight"], P["conv_blocks.5.bias"], self.y2, B2, 16, 16, 128, 64, 1, 1)
+        O.conv3x3_fwd(self.a1, P["conv_blocks.5.weight"], P["conv_blocks.5.bias"], self.y2, B2, 16, 16, 128, 64, 1, 1,
+                      wp=self.pk["c5f"])
         self._g_bn("conv_blocks.6", self.y2, self.a2, 1024, 64)
         O.conv3x3_fwd(self.a2, P["conv_blocks.8.weight"], P["conv_blocks.8.bias"], self.x3[self.B:], B2, 32, 32, 64, 1,
-                      1, 0, act=O.ACT_TANH)
+                      1, 0, act=O.ACT_TANH, wp=self.pk["c8f"])
 
     def _g_bn(self, key, x, y, hw, c):
         P, R = self.G.params, self.G.running
@@ -237,16 +256,20 @@ class ConvGanStep:
                    train=True, act=O.ACT_LEAKY, slope=SLOPE, save_mean=sm, save_invstd=si)
         self.G.batches[key] += 2
 
-    def _masks(self, masks, n, call):
-        for k, (_, _, _, co, _) in enumerate(D_CONVS):
-            O.dropout2d_mask(masks[k], n, co, DROP_P, self.seed * 7919 + self.rank, (self.round * 2 + call) * 4 + k)
+    def _masks(self):
+        """Every Dropout2d mask of the round in one launch: the D step's (call 0, 2B images) and the
+        G-loss pass's (call 1, B images); counter (round * 2 + call) * 4 + layer."""
+        B, cs = self.B, [co for _, _, _, co, _ in D_CONVS]
+        O.dropout2d_masks(self.mask_d + self.mask_g, [2 * B] * 4 + [B] * 4, cs + cs, DROP_P,
+                          self.seed * 7919 + self.rank,
+                          [(self.round * 2 + call) * 4 + k for call in (0, 1) for k in range(4)])
 
     def _d_forward(self, x, n, groups, masks):
         P, R = self.D.params, self.D.running
         inp = x
         for k, (ck, bk, ci, co, hw) in enumerate(D_CONVS):
             O.conv3x3_fwd(inp, P[ck + ".weight"], P[ck + ".bias"], self.q[k], n, hw, hw, ci, co, 2, 0, act=O.ACT_LEAKY,
-                          slope=SLOPE, drop=masks[k])
+                          slope=SLOPE, drop=masks[k], wp=self.pk[ck + "f"])
             inp = self.q[k]
             if bk:
                 sm, si = self.d_save[bk]
@@ -256,11 +279,11 @@ class ConvGanStep:
                 self.D.batches[bk] += groups
                 inp = self.r[k]
         O.nhwc_to_nchw(self.r[3], self.flat, n, 128, 4)    # out.view(B, -1), model/lsgan.py:96
-        O.dense_fwd(self.flat, P["adv_layer.weight"], P["adv_layer.bias"], self.v, n, 512, 1)
+        O.dense_fwd(self.flat, P["adv_layer.weight"], P["adv_layer.bias"], self.v, n, 512, 1, wp=self.pk["advf"])
 
     def _d_backward(self, x, n, groups, masks, wgrad, dx):
         P, G = self.D.params, self.D.grads
-        O.dense_bwd_data(self.dv, P["adv_layer.weight"], self.dflat, n, 512, 1)
+        O.dense_bwd_data(self.dv, P["adv_layer.weight"], self.dflat, n, 512, 1, wp=self.pk["advb"])
         if wgrad:
             O.dense_bwd_weight(self.dv, self.flat, G["adv_layer.weight"], G["adv_layer.bias"], n, 512, 1)
         O.nchw_to_nhwc(self.dflat, self.dr[3], n, 128, 4)
@@ -279,9 +302,9 @@ class ConvGanStep:
                 O.conv3x3_bwd_weight(self.dc[k], inp, G[ck + ".weight"], G[ck + ".bias"], n, hw, hw, ci, co, 2, 0)
             if k > 0:
                 O.conv3x3_bwd_data(self.dc[k], P[ck + ".weight"], self.dr[k - 1] if k > 1 else self.dq1, n, hw, hw, ci, co,
-                                   2, 0)
+                                   2, 0, wp=self.pk[ck + "b"])
             elif dx is not None:
-                O.conv3x3_bwd_data(self.dc[0], P[ck + ".weight"], dx, n, hw, hw, ci, co, 2, 0)
+                O.conv3x3_bwd_data(self.dc[0], P[ck + ".weight"], dx, n, hw, hw, ci, co, 2, 0, wp=self.pk[ck + "b"])
 
     def _g_backward(self):
         P, G, B = self.G.params, self.G.grads, self.B
@@ -294,13 +317,13 @@ class ConvGanStep:
                    post=self.a2[B:], dgamma=G["conv_blocks.6.weight"], dbeta=G["conv_blocks.6.bias"], slope=SLOPE)
         O.conv3x3_bwd_weight(self.dy2, self.a1[B:], G["conv_blocks.5.weight"], G["conv_blocks.5.bias"], B, 16, 16, 128,
                              64, 1, 1)
-        O.conv3x3_bwd_data(self.dy2, P["conv_blocks.5.weight"], self.da1, B, 16, 16, 128, 64, 1, 1)
+        O.conv3x3_bwd_data(self.dy2, P["conv_blocks.5.weight"], self.da1, B, 16, 16, 128, 64, 1, 1, wp=self.pk["c5b"])
         sm, si = self.g_save["conv_blocks.2"]
         O.bn2d_bwd(self.da1, self.y1[B:], B, 256, 128, sm[1], si[1], P["conv_blocks.2.weight"], self.dy1,
                    post=self.a1[B:], dgamma=G["conv_blocks.2.weight"], dbeta=G["conv_blocks.2.bias"], slope=SLOPE)
         O.conv3x3_bwd_weight(self.dy1, self.h0[B:], G["conv_blocks.1.weight"], G["conv_blocks.1.bias"], B, 8, 8, 128,
                              128, 1, 1)
-        O.conv3x3_bwd_data(self.dy1, P["conv_blocks.1.weight"], self.dh0, B, 8, 8, 128, 128, 1, 1)
+        O.conv3x3_bwd_data(self.dy1, P["conv_blocks.1.weight"], self.dh0, B, 8, 8, 128, 128, 1, 1, wp=self.pk["c1b"])
         O.nhwc_to_nchw(self.dh0, self.dh, B, 128, 64)
         O.dense_bwd_weight(self.dh, self.z[B:], G["l1.0.weight"], G["l1.0.bias"], B, 100, 8192)
 
@@ -316,17 +339,18 @@ class ConvGanStep:
             O.gather_rows(real.reshape(-1, 1024), None, 0, B, 1024, self.x3)
         elif self.data is not None:
             self._sample_real()
+        self.pk.run()
+        self._masks()
         self._g_forward()
         # local D step on [real; Xd]: two forward calls (statistics, masks per call), one backward
         half = 0.5 if self.loss == "mse" else 1.0
-        self._masks(self.mask_d, 2 * B, 0)
         self._d_forward(self.x3, 2 * B, 2, self.mask_d)
         O.adv_loss(self.v[:B], B, 1, self.loss, 1, half, self.lbuf[0:1], self.dv[:B])
         O.adv_loss(self.v[B:2 * B], B, 1, self.loss, 0, half, self.lbuf[1:2], self.dv[B:2 * B])
         self._d_backward(self.x3, 2 * B, 2, self.mask_d, wgrad=True, dx=None)
         self.D.adam(self.lr, self.betas, self.eps)
+        self.pk.run("D")
         # G loss through the updated D (its D weight gradient is discarded by the reference: skipped)
-        self._masks(self.mask_g, B, 1)
         self._d_forward(self.x3[2 * B:], B, 1, self.mask_g)
         O.adv_loss(self.v[:B], B, 1, self.loss, 1, 1.0, self.lbuf[2:3], self.dv[:B])
         self._d_backward(self.x3[2 * B:], B, 1, self.mask_g, wgrad=False, dx=self.dimg)

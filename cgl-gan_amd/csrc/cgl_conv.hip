@@ -931,6 +931,52 @@ __global__ __launch_bounds__(256) void cgl_conv_pack(CglPackArgs a) {
   gst(a.dst[p] + local, v);
 }
 
+// Multi-op weight pack: every packed problem of several (layer, direction) pairs -- a whole model's
+// forward and input-gradient operands -- in ONE launch, so that a training round re-packs each
+// model once per parameter update instead of once per convolution call.  Each job starts on a
+// block boundary, so the job lookup is uniform (scalar) per block.
+#define CGL_PACKM_MAXJ 48
+struct CglPackJobK {
+  const float* W;            // [cout][cin][ks][ks]
+  float* dst;                // packed [N][Kp]
+  int cout, cin, transpose, ks, N, Kp, Cg, Tx, T;
+  int tapm;                  // ym[ty] in bits 4 ty .. 4 ty + 3, xm[tx] in bits 16 + 4 tx ..
+  int blk_begin;
+};
+struct CglPackMultiArgs {
+  int nj, pad;
+  CglPackJobK j[CGL_PACKM_MAXJ];
+};
+
+__global__ __launch_bounds__(256) void cgl_conv_pack_multi(CglPackMultiArgs) {
+  typedef const CGL_AS4 CglPackMultiArgs* KA;
+  const KA A = (KA)__builtin_amdgcn_kernarg_segment_ptr();
+  const int b = blockIdx.x;
+  int q = 0;
+  for (int i = 1; i < A->nj; ++i)
+    if (b >= A->j[i].blk_begin) q = i;
+  const CGL_AS4 CglPackJobK* J = &A->j[q];
+  const int Kp = J->Kp, Cg = J->Cg;
+  const int local = (b - J->blk_begin) * 256 + (int)threadIdx.x;
+  if (local >= J->N * Kp) return;
+  const int n = local / Kp, k = local - n * Kp;
+  float v = 0.f;
+  if (k < J->T * Cg) {
+    const int t = k / Cg, c = k - t * Cg;
+    const int ty = t / J->Tx, tx = t - ty * J->Tx;
+    const int co = J->transpose ? c : n, ci = J->transpose ? n : c;
+    const int ks = J->ks;
+    const float* w = J->W + ((long)co * J->cin + ci) * ks * ks;
+    const int ymk = (J->tapm >> (4 * ty)) & 15, xmk = (J->tapm >> (16 + 4 * tx)) & 15;
+    for (int kh = 0; kh < ks; ++kh) {
+      if (!((ymk >> kh) & 1)) continue;
+      for (int kw = 0; kw < ks; ++kw)
+        if ((xmk >> kw) & 1) v += gld(w + kh * ks + kw);
+    }
+  }
+  gst(J->dst + local, v);
+}
+
 // Weight-gradient reduction: dW[co][ci][kh][kw] = sum over problems, taps containing (kh, kw) and
 // splits of the partial tiles.  A block covers EB consecutive elements
 // e = ((co * ks + kh) * ks + kw) * cin + ci (consecutive ci: coalesced partial reads) x SG
@@ -1456,6 +1502,35 @@ __global__ __launch_bounds__(256) void cgl_dropout_mask_k(float* mask, long n, f
   gst(mask + i, u < keep ? scale : 0.f);
 }
 
+// Several Dropout2d masks (every mask of a round: one launch instead of one per layer and call);
+// mask j is exactly cgl_dropout_mask_k(mask[j], n[j], keep, scale, seed, ctr[j]).
+#define CGL_MASKS_MAX 16
+struct CglMasksArgs {
+  int nm;
+  float keep, scale;
+  unsigned long long seed;
+  float* mask[CGL_MASKS_MAX];
+  long n[CGL_MASKS_MAX];
+  unsigned long long ctr[CGL_MASKS_MAX];
+  int blk_begin[CGL_MASKS_MAX];
+};
+
+__global__ __launch_bounds__(256) void cgl_dropout_masks_k(CglMasksArgs) {
+  typedef const CGL_AS4 CglMasksArgs* KA;
+  const KA A = (KA)__builtin_amdgcn_kernarg_segment_ptr();
+  const int b = blockIdx.x;
+  int q = 0;
+  for (int j = 1; j < A->nm; ++j)
+    if (b >= A->blk_begin[j]) q = j;
+  const long i = (long)(b - A->blk_begin[q]) * 256 + threadIdx.x;
+  if (i >= A->n[q]) return;
+  const unsigned long long ctr = A->ctr[q], seed = A->seed;
+  uint32_t c[4] = {(uint32_t)i, (uint32_t)(i >> 32), (uint32_t)ctr, (uint32_t)(ctr >> 32) ^ 0x5bd1e995u};
+  cgl_philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const float u = (float)(c[0] >> 8) * (1.0f / 16777216.0f);
+  gst(A->mask[q] + i, u < A->keep ? A->scale : 0.f);
+}
+
 // NCHW <-> NHWC for one batch: X [n][c][hw] -> Y [n][hw][c] (to_nhwc) or back.  32x32 tiles in LDS.
 __global__ __launch_bounds__(256) void cgl_transpose_k(const float* X, float* Y, int rows, int cols) {
   // per image: X [rows][cols] -> Y [cols][rows]
@@ -1827,6 +1902,17 @@ int64_t conv_ws_bytes(const ConvGeom& g) {
   return 4 * (std::max(a, b) + w.part_floats + 2 * bias_part) + 4096;
 }
 
+// Packed-operand layout of one op (the problems of fwd_probs / bwd_probs): problem i's [N][Kp]
+// block at base + (256-byte aligned running offset).  Returns the total floats.
+int64_t pack_layout(CglConvProb* P, int np, const float* base) {
+  int64_t off = 0;
+  for (int i = 0; i < np; ++i) {
+    P[i].Wp = base ? base + off : nullptr;
+    off += al256((int64_t)P[i].N * P[i].Kp * 4) / 4;
+  }
+  return off;
+}
+
 int launch_pack(const float* W, const ConvGeom& g, int transpose, CglConvProb* P, int np, float* dst,
                 hipStream_t s) {
   CglPackArgs a;
@@ -1975,8 +2061,8 @@ int col_sum(const float* X, int64_t rows, int C, double* part, float* out, hipSt
 namespace {
 
 int conv_fwd_impl(const ConvGeom& g, const float* X, const float* W, const float* bias, float* Y, int act, float slope,
-                  const float* drop, void* ws, int64_t wsb, hipStream_t s) {
-  if (!X || !W || !Y || !ws || act < 0 || act > 3 || !al16(ws)) return CGL_E_ARG;
+                  const float* drop, void* ws, int64_t wsb, hipStream_t s, const float* Wp = nullptr) {
+  if (!X || !(W || Wp) || !Y || !ws || act < 0 || act > 3 || !al16(ws) || (Wp && !al16(Wp))) return CGL_E_ARG;
   if (wsb < conv_ws_bytes(g)) return CGL_E_SIZE;
   if ((g.cin % 4 == 0) && !al16(X)) return CGL_E_ARG;
   CglConvProb P[CGL_CONV_MAXP];
@@ -1986,16 +2072,17 @@ int conv_fwd_impl(const ConvGeom& g, const float* X, const float* W, const float
     P[i].Y = Y;
   }
   int rc;
-  if ((rc = launch_pack(W, g, 0, P, np, (float*)ws, s))) return rc;
+  if (Wp) pack_layout(P, np, Wp);
+  else if ((rc = launch_pack(W, g, 0, P, np, (float*)ws, s))) return rc;
   return launch_conv_mma(P, np, bias, act, slope, drop, s);
 }
 
 int conv_bwd_data_impl(const ConvGeom& g, const float* dY, const float* W, float* dX, void* ws, int64_t wsb,
-                       hipStream_t s) {
-  if (!dY || !W || !dX || !ws || !al16(ws)) return CGL_E_ARG;
+                       hipStream_t s, const float* Wp = nullptr) {
+  if (!dY || !(W || Wp) || !dX || !ws || !al16(ws) || (Wp && !al16(Wp))) return CGL_E_ARG;
   if (wsb < conv_ws_bytes(g)) return CGL_E_SIZE;
   if ((g.cout % 4 == 0) && !al16(dY)) return CGL_E_ARG;
-  if (g.cout == 1 && g.cin == 64 && g.ks == 3 && g.stride == 1 && !g.up && al16(dX) &&
+  if (W && g.cout == 1 && g.cin == 64 && g.ks == 3 && g.stride == 1 && !g.up && al16(dX) &&
       (int64_t)g.n * g.h * g.w < (int64_t)1 << 30) {
     const int npix = g.n * g.h * g.w;
     hipLaunchKernelGGL((cgl_conv_bwd_n1<16>), dim3((npix + 16 * CGL_BN1_PPT - 1) / (16 * CGL_BN1_PPT)), dim3(256), 0, s, dY, W, dX, npix, g.h, g.w);
@@ -2008,7 +2095,8 @@ int conv_bwd_data_impl(const ConvGeom& g, const float* dY, const float* W, float
     P[i].Y = dX;
   }
   int rc;
-  if ((rc = launch_pack(W, g, 1, P, np, (float*)ws, s))) return rc;
+  if (Wp) pack_layout(P, np, Wp);
+  else if ((rc = launch_pack(W, g, 1, P, np, (float*)ws, s))) return rc;
   return launch_conv_mma(P, np, nullptr, CGL_EPI_ACT_NONE, 0.f, nullptr, s);
 }
 
@@ -2171,6 +2259,85 @@ int cgl_dense_bwd_weight(const float* dY, const float* X, float* dW, float* db, 
   return conv_bwd_weight_impl(g, dY, X, dW, db, ws, wsb, (hipStream_t)stream);
 }
 
+int64_t cgl_conv_packed_floats(int h, int w, int cin, int cout, int stride, int up, int ks, int dir) {
+  ConvGeom g;
+  const int rc = conv_geom(1, h, w, cin, cout, stride, up, g, ks);
+  if (rc) return rc;
+  if (dir != 0 && dir != 1) return CGL_E_ARG;
+  CglConvProb P[CGL_CONV_MAXP];
+  const int np = dir ? bwd_probs(g, P) : fwd_probs(g, P);
+  return pack_layout(P, np, nullptr);
+}
+
+int cgl_conv_pack_multi(int njobs, const CglConvPackJob* jobs, void* stream) {
+  if (njobs < 1 || !jobs) return CGL_E_ARG;
+  CglPackMultiArgs a;
+  std::memset(&a, 0, sizeof(a));
+  int nj = 0, blk = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const CglConvPackJob& J = jobs[i];
+    ConvGeom g;
+    int rc = conv_geom(1, J.h, J.w, J.cin, J.cout, J.stride, J.up, g, J.ks);
+    if (rc) return rc;
+    if (!J.W || !J.Wp || !al16(J.Wp) || (J.dir != 0 && J.dir != 1)) return CGL_E_ARG;
+    CglConvProb P[CGL_CONV_MAXP];
+    const int np = J.dir ? bwd_probs(g, P) : fwd_probs(g, P);
+    pack_layout(P, np, J.Wp);
+    for (int p = 0; p < np; ++p) {
+      if (nj == CGL_PACKM_MAXJ) return CGL_E_SIZE;
+      CglPackJobK& k = a.j[nj++];
+      k.W = J.W;
+      k.dst = const_cast<float*>(P[p].Wp);
+      k.cout = g.cout; k.cin = g.cin; k.transpose = J.dir; k.ks = g.ks;
+      k.N = P[p].N; k.Kp = P[p].Kp; k.Cg = P[p].Cin; k.Tx = P[p].Tx; k.T = P[p].Ty * P[p].Tx;
+      k.tapm = 0;
+      for (int t = 0; t < 4; ++t) k.tapm |= (P[p].ym[t] & 15) << (4 * t) | (P[p].xm[t] & 15) << (16 + 4 * t);
+      k.blk_begin = blk;
+      blk += (int)(((int64_t)P[p].N * P[p].Kp + 255) / 256);
+    }
+  }
+  a.nj = nj;
+  hipLaunchKernelGGL(cgl_conv_pack_multi, dim3(blk), dim3(256), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+int cgl_conv3x3_fwd_packed(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w, int cin,
+                           int cout, int stride, int up, int act, float slope, const float* drop, void* ws,
+                           int64_t wsb, void* stream) {
+  ConvGeom g;
+  const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
+  if (rc) return rc;
+  if (!Wp) return CGL_E_ARG;
+  return conv_fwd_impl(g, X, nullptr, bias, Y, act, slope, drop, ws, wsb, (hipStream_t)stream, Wp);
+}
+
+int cgl_conv3x3_bwd_data_packed(const float* dY, const float* W, const float* Wp, float* dX, int n, int h, int w,
+                                int cin, int cout, int stride, int up, void* ws, int64_t wsb, void* stream) {
+  ConvGeom g;
+  const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
+  if (rc) return rc;
+  if (!Wp) return CGL_E_ARG;
+  return conv_bwd_data_impl(g, dY, W, dX, ws, wsb, (hipStream_t)stream, Wp);
+}
+
+int cgl_dense_fwd_packed(const float* X, const float* Wp, const float* b, float* Y, int M, int K, int N, int act,
+                         float slope, void* ws, int64_t wsb, void* stream) {
+  ConvGeom g;
+  const int rc = conv_geom(M, 1, 1, K, N, 1, 0, g, 1);
+  if (rc) return rc;
+  if (!Wp) return CGL_E_ARG;
+  return conv_fwd_impl(g, X, nullptr, b, Y, act, slope, nullptr, ws, wsb, (hipStream_t)stream, Wp);
+}
+
+int cgl_dense_bwd_data_packed(const float* dY, const float* Wp, float* dX, int M, int K, int N, void* ws, int64_t wsb,
+                              void* stream) {
+  ConvGeom g;
+  const int rc = conv_geom(M, 1, 1, K, N, 1, 0, g, 1);
+  if (rc) return rc;
+  if (!Wp) return CGL_E_ARG;
+  return conv_bwd_data_impl(g, dY, nullptr, dX, ws, wsb, (hipStream_t)stream, Wp);
+}
+
 int64_t cgl_bn2d_workspace_bytes(int n, int hw, int C, int groups) {
   if (n < 1 || hw < 1 || C < 1 || groups < 1 || n % groups) return CGL_E_ARG;
   const int64_t gr = (int64_t)(n / groups) * hw;
@@ -2290,6 +2457,28 @@ int cgl_dropout2d_mask(float* mask, int n, int C, double p, unsigned long long s
   const float scale = 1.0f / keep;
   hipLaunchKernelGGL(cgl_dropout_mask_k, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream, mask,
                      tot, keep, scale, seed, counter);
+  return (int)hipGetLastError();
+}
+
+int cgl_dropout2d_masks(int nm, float* const* masks, const int* n, const int* C, double p, unsigned long long seed,
+                        const unsigned long long* counters, void* stream) {
+  if (nm < 1 || nm > CGL_MASKS_MAX || !masks || !n || !C || !counters || !(p >= 0.0 && p < 1.0)) return CGL_E_ARG;
+  CglMasksArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.nm = nm;
+  a.keep = (float)(1.0 - p);
+  a.scale = 1.0f / a.keep;
+  a.seed = seed;
+  int blk = 0;
+  for (int j = 0; j < nm; ++j) {
+    if (!masks[j] || n[j] < 1 || C[j] < 1) return CGL_E_ARG;
+    a.mask[j] = masks[j];
+    a.n[j] = (long)n[j] * C[j];
+    a.ctr[j] = counters[j];
+    a.blk_begin[j] = blk;
+    blk += (int)((a.n[j] + 255) / 256);
+  }
+  hipLaunchKernelGGL(cgl_dropout_masks_k, dim3(blk), dim3(256), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 

@@ -217,6 +217,34 @@ int cgl_dense_bwd_data(const float* dY, const float* W, float* dX, int M, int K,
 int cgl_dense_bwd_weight(const float* dY, const float* X, float* dW, float* db, int M, int K, int N, void* workspace,
                          int64_t ws_bytes, void* stream);
 
+/* Pre-packed weight operands.  The ops above re-pack W into the MFMA operand layout on every call
+ * (one extra launch each); a training round instead packs every layer of a model, forward (dir 0)
+ * and input-gradient (dir 1) operands, in one launch after each parameter update (the reference
+ * has no equivalent: autograd reads W directly, model/lsgan.py:12-99) and passes the packed
+ * operand Wp to the *_packed ops.  ks = 3 (conv3x3 geometry) or 1 (dense: h = w = 1, stride 1,
+ * up 0, cin = K, cout = N).  Packed layout depends only on (h, w, cin, cout, stride, up, ks, dir). */
+typedef struct CglConvPackJob {
+  const float* W;            /* [cout][cin][ks][ks], the reference's layout */
+  float* Wp;                 /* cgl_conv_packed_floats(...) floats, 16-byte aligned */
+  int h, w, cin, cout, stride, up, ks, dir;
+} CglConvPackJob;
+int64_t cgl_conv_packed_floats(int h, int w, int cin, int cout, int stride, int up, int ks, int dir);
+/* all jobs in one launch (at most 48 packed problems: a forward up-conv is 4, a stride-2
+ * input gradient 4, everything else 1) */
+int cgl_conv_pack_multi(int njobs, const CglConvPackJob* jobs, void* stream);
+int cgl_conv3x3_fwd_packed(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w, int cin,
+                           int cout, int stride, int up, int act, float slope, const float* drop, void* workspace,
+                           int64_t ws_bytes, void* stream);
+/* W (may be null) is read only by the one-output-channel stride-1 input gradient, which uses the
+ * unpacked weights */
+int cgl_conv3x3_bwd_data_packed(const float* dY, const float* W, const float* Wp, float* dX, int n, int h, int w,
+                                int cin, int cout, int stride, int up, void* workspace, int64_t ws_bytes,
+                                void* stream);
+int cgl_dense_fwd_packed(const float* X, const float* Wp, const float* b, float* Y, int M, int K, int N, int act,
+                         float slope, void* workspace, int64_t ws_bytes, void* stream);
+int cgl_dense_bwd_data_packed(const float* dY, const float* Wp, float* dX, int M, int K, int N, void* workspace,
+                              int64_t ws_bytes, void* stream);
+
 /* nn.BatchNorm2d(C, eps, momentum) [+ LeakyReLU(slope) when act == 1] on NHWC X[n][hw][C]
  * (model/lsgan.py:13,17,80).  `groups` independent forward calls are stacked along n (statistics
  * per group, running stats updated group by group in call order); save_mean / save_invstd are
@@ -241,6 +269,9 @@ int cgl_act_drop_bwd(const float* dY, const float* post, const float* drop, int 
  * (Philox4x32-10, counter-based: (seed, counter) selects the stream). */
 int cgl_dropout2d_mask(float* mask, int n, int C, double p, unsigned long long seed, unsigned long long counter,
                        void* stream);
+/* nm (<= 16) masks in one launch: mask j = cgl_dropout2d_mask(masks[j], n[j], C[j], p, seed, counters[j]) */
+int cgl_dropout2d_masks(int nm, float* const* masks, const int* n, const int* C, double p, unsigned long long seed,
+                        const unsigned long long* counters, void* stream);
 /* Layout changes of model/lsgan.py:25 (view(B,128,8,8) of the Linear output) and :96 (view(B,-1)). */
 int cgl_nchw_to_nhwc(const float* X, float* Y, int n, int c, int hw, void* stream);
 int cgl_nhwc_to_nchw(const float* X, float* Y, int n, int c, int hw, void* stream);
