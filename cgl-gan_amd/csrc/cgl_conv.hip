@@ -87,6 +87,16 @@ __device__ __forceinline__ void cgl_conv_pix(CglKP P, int m, int& img, int& oy, 
   ox = r - oy * P->OW;
 }
 
+// q = a / d, r = a % d for 0 <= a < 2^31, d >= 1 (inv = 1.0 / d): the double product is within
+// one of the quotient, fixed by one branch-free correction step (no integer division sequence)
+__device__ __forceinline__ void cgl_divmod(int a, int d, double inv, int& q, int& r) {
+  q = (int)((double)a * inv);
+  r = a - q * d;
+  const bool hi = r >= d, lo = r < 0;
+  q += hi ? 1 : (lo ? -1 : 0);
+  r += hi ? -d : (lo ? d : 0);
+}
+
 __device__ __forceinline__ int cgl_xcd_tile(int local, int nwg) {
   if (nwg < 16) return local;
   const int xcd = local & 7, pos = local >> 3, q = nwg >> 3, r = nwg & 7;
@@ -142,18 +152,22 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
     const int k0 = c * 16;
     okm = 0;
     if (FAST) {
-      const int t = k0 / Cin;   // uniform: the chunk lies inside one tap
+      // the chunk lies inside one tap (Cin % 16 == 0), or the problem has a single tap and
+      // Cin % 4 == 0: then the K tail is masked per float4 (bits 4 / 5 of okm)
+      const int t = k0 / Cin;
       const int ci = k0 - t * Cin + 8 * lh;
       const int ty = t / Tx, tx = t - ty * Tx;
       const int dyv = P->dy[ty], dxv = P->dx[tx];
+      okm = (ci < Cin ? 16 : 0) | (ci + 4 < Cin ? 32 : 0);
+      const int c0 = min(ci, Cin - 4), c1 = min(ci + 4, Cin - 4);
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int iy = ay[i] + dyv, ix = ax[i] + dxv;
         const bool ok = (unsigned)iy < (unsigned)IH && (unsigned)ix < (unsigned)IW;
         okm |= ok ? (1 << i) : 0;
         const int cy = min(max(iy, 0), IH - 1) >> ish, cx = min(max(ix, 0), IW - 1) >> ish;
-        gcfp p = (gcfp)(X + aoff[i] + ((long)cy * XW + cx) * Cin + ci);
-        const f32x4 u = *(gcf4p)p, w = *(gcf4p)(p + 4);
+        gcfp p = (gcfp)(X + aoff[i] + ((long)cy * XW + cx) * Cin);
+        const f32x4 u = *(gcf4p)(p + c0), w = *(gcf4p)(p + c1);
         A[i][0] = u[0]; A[i][1] = u[1]; A[i][2] = u[2]; A[i][3] = u[3];
         A[i][4] = w[0]; A[i][5] = w[1]; A[i][6] = w[2]; A[i][7] = w[3];
       }
@@ -186,9 +200,9 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       if (FAST) {
-        const bool ok = (okm >> i) & 1;
+        const bool ok0 = ((okm >> i) & 1) && (okm & 16), ok1 = ((okm >> i) & 1) && (okm & 32);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) A[i][q] = ok ? A[i][q] : 0.f;
+        for (int q = 0; q < 8; ++q) A[i][q] = (q < 4 ? ok0 : ok1) ? A[i][q] : 0.f;
       } else {
 #pragma unroll
         for (int q = 0; q < 8; ++q) A[i][q] = ((okm >> (i * 8 + q)) & 1) ? A[i][q] : 0.f;
@@ -249,8 +263,13 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
     }
   }
 
-  // epilogue: bias, activation, Dropout2d scale, NHWC store at the mapped position
-  const int ldy = P->ldy, YH = P->YH, YW = P->YW;
+  // epilogue: bias, activation, Dropout2d scale, NHWC store at the mapped position.  The activation
+  // is a uniform branch around the element loops; the output pixel of each row is decoded once per
+  // 32-row block and stepped from row to row (no per-element divisions); the Dropout2d multipliers of
+  // a block are all loaded before its stores (a load after a store may alias it, which would
+  // serialise one global round trip per element).
+  const int ldy = P->ldy, YH = P->YH, YW = P->YW, OW = P->OW, hw = P->OH * P->OW;
+  const double inv_hw = 1.0 / hw, inv_ow = 1.0 / OW;
   const int osy = P->osy, osx = P->osx, ooy = P->ooy, oox = P->oox;
   const float* __restrict__ bias = L->bias;
   const float* __restrict__ drop = L->drop;
@@ -263,25 +282,67 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
     const int col = min(n0 + 32 * j + li, N - 1);
     bj[j] = bias ? gld(bias + col) : 0.f;
   }
+#define CGL_EPI_LOOP(EXPR)                                  \
+  _Pragma("unroll") for (int i = 0; i < TM; ++i)            \
+  _Pragma("unroll") for (int j = 0; j < TN; ++j)            \
+  _Pragma("unroll") for (int r = 0; r < 16; ++r) {          \
+    float v = acc[i][j][r] + bj[j];                         \
+    EXPR;                                                   \
+    acc[i][j][r] = v;                                       \
+  }
+  if (act == CGL_EPI_ACT_LEAKY) { CGL_EPI_LOOP(v = v > 0.f ? v : v * sl) }
+  else if (act == CGL_EPI_ACT_TANH) { CGL_EPI_LOOP(v = cgl_tanh(v)) }
+  else if (act == CGL_EPI_ACT_SIGMOID) { CGL_EPI_LOOP(v = 1.f / (1.f + expf(-v))) }
+  else { CGL_EPI_LOOP((void)0) }
+#undef CGL_EPI_LOOP
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
+    const int rowb = m0 + 32 * i;               // wave-uniform first row of the block
+    if (rowb >= M) break;
+    const int row0 = rowb + 4 * lh;
+    int pix[16];
+    auto decode = [&](int r, int& img) {
+      const int row = row0 + (r & 3) + 8 * (r >> 2);
+      int rem, oy, ox;
+      cgl_divmod(row, hw, inv_hw, img, rem);
+      cgl_divmod(rem, OW, inv_ow, oy, ox);
+      pix[r] = (img * YH + oy * osy + ooy) * YW + ox * osx + oox;
+      return row;
+    };
+    if (drop) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int img;
+        const int row = decode(r, img);
+        const long dro = (long)(row < M ? img : 0) * ldy;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j][r] *= gld(drop + dro + min(n0 + 32 * j + li, N - 1));
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int img;
+        decode(r, img);
+      }
+    }
+    // stores through a buffer resource based at the block's first output pixel (output pixels grow
+    // with the row, so every offset is >= 0): rows past M / columns past N get an out-of-range
+    // offset and are dropped by the hardware -- no per-element branches
+    int imb, remb, oyb, oxb;
+    cgl_divmod(rowb, hw, inv_hw, imb, remb);
+    cgl_divmod(remb, OW, inv_ow, oyb, oxb);
+    const int pixb = __builtin_amdgcn_readfirstlane((imb * YH + oyb * osy + ooy) * YW + oxb * osx + oox);
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(Y + (long)pixb * ldy, (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int row = m0 + 32 * i + 4 * lh + (r & 3) + 8 * (r >> 2);
-      if (row >= M) continue;
-      int img, oy, ox;
-      cgl_conv_pix(P, row, img, oy, ox);
-      const long pix = ((long)img * YH + oy * osy + ooy) * YW + ox * osx + oox;
+      const bool rok = row0 + (r & 3) + 8 * (r >> 2) < M;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = n0 + 32 * j + li;
-        if (col >= N) continue;
-        float v = acc[i][j][r] + bj[j];
-        if (act == CGL_EPI_ACT_LEAKY) v = v > 0.f ? v : v * sl;
-        else if (act == CGL_EPI_ACT_TANH) v = cgl_tanh(v);
-        else if (act == CGL_EPI_ACT_SIGMOID) v = 1.f / (1.f + expf(-v));
-        if (drop) v *= gld(drop + (long)img * ldy + col);
-        gst(Y + pix * ldy + col, v);
+        const int off = (rok && col < N) ? ((pix[r] - pixb) * ldy + col) * 4 : (int)0x80000000;
+        // (through a scalar copy: a bit_cast of the vector element itself was lowered to element 0)
+        const float v = acc[i][j][r];
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(v), rs, off, 0, 0);
       }
     }
   }
@@ -2008,7 +2069,7 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
     P[i].tiles_n = (P[i].N + 32 * t.TN * t.WN - 1) / (32 * t.TN * t.WN);
     P[i].wg_begin = wg;
     wg += P[i].tiles_m * P[i].tiles_n;
-    fast = fast && (P[i].Cin % 16 == 0);
+    fast = fast && (P[i].Cin % 16 == 0 || (P[i].Ty * P[i].Tx == 1 && P[i].Cin % 4 == 0));
     L.p[i] = P[i];
   }
   if (t.TM == 2 && t.TN == 2) {
