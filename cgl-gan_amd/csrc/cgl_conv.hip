@@ -62,6 +62,7 @@ struct CglConvLaunch {
   int act;                   // CGL_EPI_ACT_*
   float slope;
   const float* drop;         // Dropout2d scale per (image, channel) [img][ldy], or null
+  int wbias;                 // weight gradient: im2col column K is the constant 1 (bias gradient)
 };
 
 typedef const CGL_AS4 CglConvLaunch* CglKL;
@@ -404,11 +405,13 @@ __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local)
 #pragma unroll
   for (int i = 0; i < TM; ++i) rch[i] = min(n0 + 32 * i + li, N - 1);
   int cdy[TN], cdx[TN], cci[TN];
-  bool cok[TN];
+  bool cok[TN], cone[TN];
+  const int wbias = L->wbias;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int kc = k0c + 32 * j + li;
     cok[j] = kc < K;
+    cone[j] = wbias && kc == K;   // the bias column: B = 1 for every valid pixel
     const int kk = min(kc, K - 1);
     const int t = kk / Cin;
     cci[j] = kk - t * Cin;
@@ -452,6 +455,10 @@ __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local)
           B[j][q] = *(gcfp)bb;
         }
       }
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) B[j][q] = cone[j] ? 1.f : B[j][q];
       return;
     }
     // decode the first pixel of this lane half once, then step along the row (wrapping)
@@ -483,6 +490,7 @@ __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local)
         const bool ok = mv && cok[j] && (unsigned)iy < (unsigned)IH && (unsigned)ix < (unsigned)IW;
         const float* bb = ok ? X + xo + ((long)(iy >> ish) * XW + (ix >> ish)) * Cin : zp;
         B[j][q] = ((gcfp)bb)[cci[j]];
+        B[j][q] = cone[j] ? (mv ? 1.f : 0.f) : B[j][q];
       }
     }
   };
@@ -522,7 +530,7 @@ __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local)
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int kc = k0c + 32 * j + li;
-    if (kc >= K) continue;
+    if (kc >= K + wbias) continue;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1045,7 +1053,10 @@ __global__ __launch_bounds__(256) void cgl_conv_pack_multi(CglPackMultiArgs) {
 // partial sums are combined through LDS in a fixed order (deterministic).
 struct CglWgradReduceArgs {
   float* dW;
+  float* db;                 // bias gradient from the partials' column K (or null)
   int cout, cin, np, ks, EB, SG;
+  int wblocks;               // blocks of the dW elements; the db blocks follow
+  int K[CGL_CONV_MAXP];
   const float* part[CGL_CONV_MAXP];
   int Kp[CGL_CONV_MAXP], splits[CGL_CONV_MAXP], Tx[CGL_CONV_MAXP], Ty[CGL_CONV_MAXP];
   int ym[CGL_CONV_MAXP][4], xm[CGL_CONV_MAXP][4];
@@ -1058,6 +1069,33 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad_reduce(CglWgradReduceArgs 
   const int e = blockIdx.x * EB + el;
   const int cin = a.cin, ks = a.ks;
   const int E = a.cout * ks * ks * cin;
+  if (a.db && (int)blockIdx.x >= a.wblocks) {   // uniform per block
+    // bias gradient: db[co] = sum over problems and splits of part[s][co][K]
+    const int eb = ((int)blockIdx.x - a.wblocks) * EB + el;
+    const int co = min(eb, a.cout - 1);
+    double acc = 0.0;
+    for (int p = 0; p < a.np; ++p) {
+      const int S = a.splits[p];
+      const long sstride = (long)a.cout * a.Kp[p];
+      const float* src = a.part[p] + (long)co * a.Kp[p] + a.K[p];
+      for (int s0 = sg; s0 < S; s0 += 8 * SG) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = gld(src + (long)min(s0 + i * SG, S - 1) * sstride);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (s0 + i * SG < S) acc += (double)v[i];
+      }
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (sg == 0 && eb < a.cout) {
+      double t = 0.0;
+      for (int g = 0; g < SG; ++g) t += red[g * EB + el];
+      gst(a.db + eb, (float)t);
+    }
+    return;
+  }
   const int ee = min(e, E - 1);
   const int ci = ee % cin;
   const int rest = ee / cin;
@@ -1927,16 +1965,34 @@ bool wgrad_n1t_ok(const ConvGeom& g, const CglConvProb& P0) {
          P0.Ty * P0.Tx <= 16 && (256 / c4) * P0.Ty * P0.Tx * P0.Cin <= 16384;
 }
 
-WgradPlan wgrad_plan(const ConvGeom& g) {
+// the MFMA weight gradient also produces the bias gradient, from an im2col column of ones (column K)
+// when the column is free (K is not a multiple of the tile width, so it lands in padding) or the
+// layer is small (latency-bound: the extra tile costs less than the two column-sum launches); the
+// vector one-output-channel kernels keep the column sum
+bool wgrad_bias_col(const ConvGeom& g, const CglConvProb* P, int np) {
+  if (g.cout == 1 && np == 1) return false;
+  const int tw = P[0].K > 32 ? 64 : 32;
+  int64_t macs = 0;
+  bool free_col = true;
+  for (int i = 0; i < np; ++i) {
+    macs += (int64_t)P[i].M * P[i].N * P[i].K;
+    free_col = free_col && (P[i].K % tw != 0);
+  }
+  return free_col || macs < ((int64_t)1 << 28);
+}
+
+WgradPlan wgrad_plan(const ConvGeom& g, bool bias = true) {
   WgradPlan w;
   w.np = fwd_probs(g, w.P);
-  w.t = ConvTiling{g.cout > 32 ? 2 : 1, w.P[0].K > 32 ? 2 : 1, 1, 1, 1};
+  const int wb = bias && wgrad_bias_col(g, w.P, w.np) ? 1 : 0;
+  w.t = ConvTiling{g.cout > 32 ? 2 : 1, w.P[0].K + wb > 32 ? 2 : 1, 1, 1, 1};
   int tiles_total = 0;
   int64_t nk_total = 0;
   for (int i = 0; i < w.np; ++i) {
     CglConvProb& P = w.P[i];
+    P.Kp = (P.K + wb + 15) & ~15;   // partial row length (room for the bias column)
     P.tiles_m = (P.N + 32 * w.t.TM - 1) / (32 * w.t.TM);
-    P.tiles_n = (P.K + 32 * w.t.TN - 1) / (32 * w.t.TN);
+    P.tiles_n = (P.K + wb + 32 * w.t.TN - 1) / (32 * w.t.TN);
     tiles_total += P.tiles_m * P.tiles_n;
     nk_total += (int64_t)P.N * P.Kp;
   }
@@ -2173,10 +2229,12 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
   if (!dY || !X || !dW || !ws || !al16(ws)) return CGL_E_ARG;
   if (wsb < conv_ws_bytes(g)) return CGL_E_SIZE;
   if (g.cout > CGL_ZERO_PAGE || g.cin > CGL_ZERO_PAGE) return CGL_E_ARG;   // cgl_zero_page bound
-  WgradPlan pl = wgrad_plan(g);
+  WgradPlan pl = wgrad_plan(g, db != nullptr);
+  const bool bias_col = db && wgrad_bias_col(g, pl.P, pl.np);
   CglConvLaunch L;
   std::memset(&L, 0, sizeof(L));
   L.np = pl.np;
+  L.wbias = bias_col ? 1 : 0;
   L.WM = 1;
   L.WN = 1;
   L.WK = 1;
@@ -2202,6 +2260,7 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
     L.p[i] = P;
     r.part[i] = P.part;
     r.Kp[i] = P.Kp;
+    r.K[i] = P.K;
     r.splits[i] = P.splits;
     r.Tx[i] = P.Tx;
     r.Ty[i] = P.Ty;
@@ -2243,9 +2302,12 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
   while (EB > 4 && (nred + EB - 1) / EB < 512) EB >>= 1;
   r.EB = EB;
   r.SG = 256 / EB;
-  hipLaunchKernelGGL(cgl_conv_wgrad_reduce, dim3((unsigned)((nred + EB - 1) / EB)), dim3(256), 0, s, r);
+  r.wblocks = (int)((nred + EB - 1) / EB);
+  r.db = bias_col ? db : nullptr;
+  const int bblocks = bias_col ? (g.cout + EB - 1) / EB : 0;
+  hipLaunchKernelGGL(cgl_conv_wgrad_reduce, dim3((unsigned)(r.wblocks + bblocks)), dim3(256), 0, s, r);
   if ((rc = (int)hipGetLastError())) return rc;
-  if (db) {
+  if (db && !bias_col) {
     double* bp = (double*)(((uintptr_t)part + 255) & ~(uintptr_t)255);
     if ((rc = col_sum(dY, (int64_t)g.n * g.ho * g.wo, g.cout, bp, db, s))) return rc;
   }
