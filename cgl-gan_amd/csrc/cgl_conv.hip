@@ -2002,7 +2002,7 @@ WgradPlan wgrad_plan(const ConvGeom& g, bool bias = true) {
   for (int i = 0; i < w.np; ++i) {
     CglConvProb& P = w.P[i];
     const int nchk = (P.M + 15) / 16;
-    P.splits = std::max(1, std::min(std::min(s, nchk / 8), 1024));
+    P.splits = std::max(1, std::min(std::min(s, nchk / 4), 1024));
     if (g.cout == 1 && w.np == 1)   // vector kernels: >= 256 (input-stationary) / 32 pixels per split
       P.splits = std::max(1, std::min(1024, P.M / (wgrad_n1t_ok(g, P) ? 256 : 32)));
     w.part_floats += al256((int64_t)P.splits * P.N * P.Kp * 4) / 4;
