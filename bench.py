@@ -61,6 +61,9 @@ def args_():
                         "rounds, bs512, fp32); ring: configs[0], the CGLGAN 2-D Gaussian-mixture round (B=64); "
                         "lsgan: the model/lsgan.py conv GAN round (32x32, MSE/LSGAN loss)")
     p.add_argument("--loss", choices=["mse", "bce"], default="mse", help="conv GAN objective (--model lsgan)")
+    p.add_argument("--lowp", choices=["none", "f16", "bf16"], default="bf16",
+                   help="--model mdgan: also time the same round with 16-bit GEMM operands (BASELINE configs[4]'s "
+                        "fp16) and report it beside the fp32 line as 'lowp_variant' (parity unpinned)")
     a = p.parse_args()
     if a.batch is None:
         a.batch = default_batch(a.model)
@@ -449,7 +452,7 @@ def timed_rounds(round_fn, a, world):
     return el
 
 
-def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None, parity_kind=None):
+def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None, parity_kind=None, extra=None):
     """The bench line of a fused-round model (mlp / mixg / mdgan / ring): GEMM-family roofline from
     per-launch HIP-event timing on the launch stream, CPU baseline and CPU parity at N = 1."""
     per_kind, gemm_us, gemm_flops, gemm_n = profile_launches(step, world, a.profile_reps)
@@ -487,6 +490,8 @@ def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None,
                      "launches_per_round": plan["launches"]},
         "losses": {"d_loss": st["d_loss"][0], "g_loss": st["g_loss"], "lambda": st["lambda"], "round": st["round"]},
     }
+    if extra:
+        out.update(extra)
     if world == 1 and not a.no_cpu_baseline:
         if cpu_leg is not None:
             out["cpu_baseline"] = cpu_leg()
@@ -528,10 +533,26 @@ def main_driver(a, world, rank, algo):
                   f"worker, trunk gradient all-reduced in each server group, Cloud trunk FedAvg every round)")
         else:
             wl = (f"C5: MD-GAN, num_workers={world}, non-IID (iid=1) shards, Sigmoid D + BCE, G on mean(l_i)"
-                  + (f", D-swap every {a.E} rounds" if world > 1 else "") + " (fp32; the fp16 part is not built)")
+                  + (f", D-swap every {a.E} rounds" if world > 1 else "") + " (fp32 GEMMs; the 16-bit GEMM "
+                  "variant is 'lowp_variant')")
+        lowp = None
+        if algo == "mdgan" and a.lowp != "none":
+            # the same workload with 16-bit GEMM operands (fp32 accumulation, fp32 master weights /
+            # BatchNorm / losses / Adam): reported BESIDE the fp32 line, never as its value
+            cfg16 = DriverConfig(**{**cfg.__dict__, "gemm_dtype": a.lowp})
+            drv16 = Driver(cfg16)
+            el16 = timed_rounds(lambda r: drv16.exchange.round(r, graph=cfg16.graph), a, world)
+            st16 = drv16.step.stats()
+            lowp = {"gemm_dtype": a.lowp, "value": round(world * a.batch * a.steps / el16, 1), "unit": "images/s",
+                    "ms_per_step": round(el16 / a.steps * 1e3, 4),
+                    "losses": {"d_loss": st16["d_loss"][0], "g_loss": st16["g_loss"]},
+                    "parity": "unpinned (the reference has no 16-bit path); tests/test_gpu_lowp.py checks it "
+                              "against an fp64 oracle restating the operand rounding (losses <= 1e-4; tensors "
+                              "<= 0.1-0.35 of their distance to the exact fp64 round)"}
         return fused_report(a, world, rank, drv.step, el, wl,
                             {"img": "28x28x1", "num_servers": S, "shard_rows": int(drv.step.real.shape[0])},
-                            cpu_leg=lambda: cpu_rounds(algo, a.batch, a.cpu_seconds), parity_kind=algo)
+                            cpu_leg=lambda: cpu_rounds(algo, a.batch, a.cpu_seconds), parity_kind=algo,
+                            extra={"lowp_variant": lowp} if lowp else None)
 
 
 def main_ring(a, world, rank):

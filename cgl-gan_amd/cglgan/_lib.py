@@ -16,6 +16,7 @@ MAX_LAYERS = 8
 LOSS_CE2, LOSS_BCE = 0, 1
 WEIGHT_CAPGAN, WEIGHT_MEAN, WEIGHT_MIX_SINGLE, WEIGHT_MIX_DOUBLE, WEIGHT_CGLGAN = 0, 1, 2, 3, 4
 PHASE_ALL, PHASE_A, PHASE_B = 0, 1, 2
+DTYPE_F32, DTYPE_F16, DTYPE_BF16 = 0, 1, 2
 MODEL_G, MODEL_D = 0, 1
 
 # every symbol include/cglgan.h declares (checked by tests/test_lib_exports.py)
@@ -52,7 +53,7 @@ class GanConfig(ctypes.Structure):
                 ("lr_g", ctypes.c_double), ("lr_d", ctypes.c_double), ("beta1", ctypes.c_double),
                 ("beta2", ctypes.c_double), ("adam_eps", ctypes.c_double), ("bn_eps", ctypes.c_double),
                 ("bn_momentum", ctypes.c_double), ("slope", ctypes.c_float), ("seed", ctypes.c_ulonglong),
-                ("gen_z", ctypes.c_int), ("sample_n", ctypes.c_int)]
+                ("gen_z", ctypes.c_int), ("sample_n", ctypes.c_int), ("gemm_dtype", ctypes.c_int)]
 
 
 class GanBuffers(ctypes.Structure):

@@ -99,6 +99,7 @@ class DriverConfig:
     log_every: int = 0
     checkpoint_dir: str = ""
     graph: bool = True
+    gemm_dtype: str = "f32"          # "f16" / "bf16": 16-bit GEMM operands (BASELINE config 5's fp16)
 
     @classmethod
     def from_module(cls, **overrides):
@@ -192,7 +193,7 @@ def gpu_step(cfg: DriverConfig, topo: Topology, shard: torch.Tensor, beta, g_sd,
     step = GanStep(gm, dm, batch=cfg.batch_size, epoch=cfg.epoch, loss=loss, weighting=cfg.weighting_,
                    n_workers=topo.heads, rank=topo.local, exchange_layer=xl, lr_g=cfg.lr_g, lr_d=cfg.lr_d,
                    betas=(cfg.b1, cfg.b2), seed=cfg.seed + 7919 * topo.server, gen_z=True, real=real,
-                   sample_n=real.shape[0], device=device)
+                   sample_n=real.shape[0], device=device, gemm_dtype=cfg.gemm_dtype)
     step.load_state_dicts(g_sd, d_sd)
     step.reset(beta=beta)
     return step

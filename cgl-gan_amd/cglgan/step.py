@@ -39,6 +39,9 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+_DTYPE = {"f32": C.DTYPE_F32, "f16": C.DTYPE_F16, "bf16": C.DTYPE_BF16}
+
+
 class GanStep:
     """Fused worker round.  ``run()`` = one communication round of one worker.
 
@@ -51,7 +54,10 @@ class GanStep:
                  exchange_layer: int = -1, lr_g: float = 2e-4, lr_d: float = 2e-4, betas=(0.5, 0.999),
                  adam_eps: float = 1e-8, bn_eps: float = 0.8, bn_momentum: float = 0.1, slope: float = 0.2,
                  seed: int = 20211212, gen_z: bool = False, real: torch.Tensor = None, sample_n: int = 0,
-                 real_idx: torch.Tensor = None, device="cuda"):
+                 real_idx: torch.Tensor = None, device="cuda", gemm_dtype: str = "f32"):
+        """``gemm_dtype``: "f32" (the reference arithmetic), or "f16" / "bf16": every GEMM operand
+        rounded to 16 bits at the matrix core with fp32 accumulation (BASELINE config 5's fp16;
+        fp32 master weights, BatchNorm, losses and Adam; outside the fp32 parity band)."""
         self.gm, self.dm = g, d
         self.B = batch
         self.Br = batch_real or batch
@@ -67,6 +73,10 @@ class GanStep:
         cfg.beta1, cfg.beta2, cfg.adam_eps = betas[0], betas[1], adam_eps
         cfg.bn_eps, cfg.bn_momentum, cfg.slope = bn_eps, bn_momentum, slope
         cfg.seed, cfg.gen_z, cfg.sample_n = seed, int(gen_z), sample_n
+        if gemm_dtype not in _DTYPE:
+            raise ValueError(f"gemm_dtype must be one of {sorted(_DTYPE)}")
+        cfg.gemm_dtype = _DTYPE[gemm_dtype]
+        self.gemm_dtype = gemm_dtype
         self.cfg = cfg
         self.n_workers, self.rank = n_workers, rank
         self.exchange_layer = exchange_layer

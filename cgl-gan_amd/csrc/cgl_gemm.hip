@@ -24,6 +24,28 @@
 #include <type_traits>
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// 16-bit operand GEMMs (cgl_gan_config.gemm_dtype, BASELINE config 5): the fp32 operands are
+// rounded to fp16 / bf16 (round-to-nearest-even) as they enter the MFMA; products are exact and
+// accumulate in fp32.  The k-permuted fragment of a 16-k chunk (lane half h holds k = 8h .. 8h + 7)
+// is exactly the operand of v_mfma_f32_32x32x16_{f16,bf16}, so one MFMA replaces the eight
+// 32x32x2 f32 MFMAs of the chunk.
+template <int DT>
+__device__ __forceinline__ void cgl_mfma16(f32x16& acc, const float (&a)[8], const float (&b)[8]) {
+  if constexpr (DT == CGL_DTYPE_F16) {
+    f16x8 x, y;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { x[q] = (_Float16)a[q]; y[q] = (_Float16)b[q]; }
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x, y, acc, 0, 0, 0);
+  } else {
+    bf16x8 x, y;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { x[q] = (__bf16)a[q]; y[q] = (__bf16)b[q]; }
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, acc, 0, 0, 0);
+  }
+}
 
 __device__ __forceinline__ const float* cgl_row(const CglRowSrc& s, int r) {
   if (r < s.split) {
@@ -135,7 +157,7 @@ struct CglPipe {
 typedef __attribute__((address_space(3))) void cgl_lds_void;
 #define CGL_GL_NS 2        // LDS ring depth of the staged main loop (measured: 2 beats 3 at 64 KB per workgroup)
 
-template <int LAYOUT, int VEC, int TM, int TN, bool SK, bool GL>
+template <int LAYOUT, int VEC, int TM, int TN, bool SK, bool GL, int DT = 0>
 __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d, int bid, float* __restrict__ s_red,
                                               float* __restrict__ s_col, int* __restrict__ s_flag,
                                               float* __restrict__ s_bn, double* __restrict__ s_bnd) {
@@ -182,14 +204,14 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 #endif
   // 1x1 blocks: NACC independent accumulation chains over alternating k-steps of a chunk (summed in
   // a fixed order after the k-loop), so consecutive MFMAs do not wait on each other's result
-  constexpr int NX = (TM * TN == 1) ? CGL_GEMM_NACC : 1;
+  constexpr int NX = (TM * TN == 1 && DT == CGL_DTYPE_F32) ? CGL_GEMM_NACC : 1;
   f32x16 accx[NX > 1 ? NX - 1 : 1];
 #pragma unroll
   for (int x = 0; x < (NX > 1 ? NX - 1 : 1); ++x)
 #pragma unroll
     for (int r = 0; r < 16; ++r) accx[x][r] = 0.f;
 
-  if constexpr (GL && LAYOUT != 2 && TM == 1 && TN == 1 && VEC) {
+  if constexpr (GL && LAYOUT != 2 && TM == 1 && TN == 1 && VEC && DT == CGL_DTYPE_F32) {
     // ---------------- LDS-staged main loop (glds): the waves of one K-slice share a ring of
     // CGL_GL_NS stages of 32 k, filled by global_load_lds_dwordx4 in whole 128-byte row segments
     // (8 rows per wave-instruction) instead of fragment-shaped loads that touch 32 rows per
@@ -418,7 +440,12 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
           if (b_is_ones[j]) B_[j][q] = (!T || k + q < K) ? 1.f : 0.f;
       }
     }
-    if constexpr (NX > 1) {
+    if constexpr (DT != CGL_DTYPE_F32) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) cgl_mfma16<DT>(acc[i][j], A_[i], B_[j]);
+    } else if constexpr (NX > 1) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         if (q % NX == 0)
@@ -982,7 +1009,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 // layer side by side).  Separate symbols keep the 1x1 variant's register budget (and so its
 // occupancy) independent of the 2x2 variant's.
 // Dynamic LDS: split-K partials of the waves with wk > 0.
-template <int TM, int TN, bool SK = false, bool GL = false>
+template <int TM, int TN, bool SK = false, bool GL = false, int DT = CGL_DTYPE_F32>
 __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDesc* __restrict__ descs, int ndesc) {
   extern __shared__ float cgl_dyn_lds[];
   __shared__ float s_col[4 * TN * 32];          // per-column reductions across waves (WM WN <= 4)
@@ -1001,9 +1028,9 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
 #define CGL_BODY(L)                                               \
   do {                                                            \
     if (vec)                                                      \
-      cgl_gemm_body<L, 1, TM, TN, SK, GL>(d, bid, s_red, s_col, s_flag, s_bn, s_bnd);    \
+      cgl_gemm_body<L, 1, TM, TN, SK, GL, DT>(d, bid, s_red, s_col, s_flag, s_bn, s_bnd);    \
     else                                                          \
-      cgl_gemm_body<L, 0, TM, TN, SK, GL>(d, bid, s_red, s_col, s_flag, s_bn, s_bnd);    \
+      cgl_gemm_body<L, 0, TM, TN, SK, GL, DT>(d, bid, s_red, s_col, s_flag, s_bn, s_bnd);    \
   } while (0)
   if (layout == 0)
     CGL_BODY(0);

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/cglgan.h"
+
 #define CGL_WAVE 64
 #define CGL_GEMM_THREADS 256
 #define CGL_GEMM_KCHUNK 16           // k per MFMA chunk: 8 per lane half (k-permuted)

@@ -91,6 +91,7 @@ int validate(const cgl_gan_config* c) {
   if (c->weighting < 0 || c->weighting > 4) return CGL_E_ARG;
   if (c->exchange_layer != -1 && (c->exchange_layer < 1 || c->exchange_layer >= g.n_layers)) return CGL_E_ARG;
   if (c->sample_n < 0 || (c->sample_n > 0 && c->sample_n % c->batch_real != 0)) return CGL_E_ARG;
+  if (c->gemm_dtype < CGL_DTYPE_F32 || c->gemm_dtype > CGL_DTYPE_BF16) return CGL_E_ARG;
   return CGL_OK;
 }
 
@@ -225,6 +226,7 @@ struct Launch {
   int blk = 1;          // GEMM per-wave block shape (TM = TN = blk)
   bool sk = false;      // GEMM launch holds a split-K problem
   bool gl = false;      // GEMM launch uses the LDS-staged (glds) main loop instantiation
+  int dt = CGL_DTYPE_F32;   // GEMM operand type (cgl_gan_config.gemm_dtype)
 };
 
 // Split-K partials of 2x2-block waves need up to 48 KB of dynamic LDS (+16 KB BN table).
@@ -246,9 +248,27 @@ hipError_t gemm_lds_attr() {
   return hipSuccess;
 }
 
+template <int DT>
+void launch_gemm16(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, int n, bool sk) {
+  if (sk) {
+    if (blk == 2)
+      cgl_gemm_f32<2, 2, true, false, DT><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+    else
+      cgl_gemm_f32<1, 1, true, false, DT><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+  } else if (blk == 2) {
+    cgl_gemm_f32<2, 2, false, false, DT><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+  } else {
+    cgl_gemm_f32<1, 1, false, false, DT><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+  }
+}
+
 void launch_gemm(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, int n, bool sk = false,
-                 bool gl = false) {
-  if (gl) {
+                 bool gl = false, int dt = CGL_DTYPE_F32) {
+  if (dt == CGL_DTYPE_F16) {
+    launch_gemm16<CGL_DTYPE_F16>(blk, grid, shmem, s, d, n, sk);
+  } else if (dt == CGL_DTYPE_BF16) {
+    launch_gemm16<CGL_DTYPE_BF16>(blk, grid, shmem, s, d, n, sk);
+  } else if (gl) {
     cgl_gemm_f32<1, 1, false, true><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
   } else if (sk) {   // a launch with a split-K problem: the instantiation carrying the combine
     if (blk == 2)
@@ -507,7 +527,8 @@ bool push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
   // LDS-staged main loop: every problem of the launch must qualify (a TN problem beside it would
   // pay the ring's LDS in occupancy); its tiling is 32x32 per workgroup with the four waves on K
   // slices (microbenchmarked best for the staged loop: tools/gemm_lds_bench.hip)
-  bool gl = blk == 1 && gemm_gl_enabled();
+  bool gl = blk == 1 && gemm_gl_enabled() && c->cfg.gemm_dtype == CGL_DTYPE_F32;
+  L.dt = c->cfg.gemm_dtype;
   for (auto& d : descs) {
     set_vec(d);
     CglGemmDesc t = d;
@@ -1138,7 +1159,7 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
   }
   switch (L.kind) {
     case K_GEMM:
-      launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, L.count, L.sk, L.gl);
+      launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, L.count, L.sk, L.gl, L.dt);
       break;
     case K_HEAD:
       hipLaunchKernelGGL(cgl_head_loss, dim3(L.grid), dim3(256), 0, s, c->ws.head + L.first);

@@ -39,6 +39,12 @@ enum {
   CGL_WEIGHT_CGLGAN = 4       /* alpha = (beta + softmax(lambda * l)) / 2      CGLGAN/2DMG/main.py:261-264 */
 };
 enum { CGL_PHASE_ALL = 0, CGL_PHASE_A = 1, CGL_PHASE_B = 2 };
+/* Operand type of the step's GEMMs (cgl_gan_config.gemm_dtype).  F32 is the reference arithmetic;
+ * F16 / BF16 round each GEMM operand (activations, weights, gradients) to 16 bits as it enters
+ * the matrix core and accumulate in fp32 -- autocast-style mixed precision with fp32 master
+ * weights, BatchNorm, losses and Adam (BASELINE config 5, "bs512 fp16").  The reference has no
+ * 16-bit path, so F16 / BF16 results are outside the fp32 parity band (parity unpinned). */
+enum { CGL_DTYPE_F32 = 0, CGL_DTYPE_F16 = 1, CGL_DTYPE_BF16 = 2 };
 enum { CGL_MODEL_G = 0, CGL_MODEL_D = 1 };
 
 /* One MLP: n_layers Linear layers, dims[0] -> ... -> dims[n_layers].
@@ -72,6 +78,7 @@ typedef struct cgl_gan_config {
   int sample_n;         /* >0: in-graph shuffle sampler over sample_n real rows (per-epoch keyed
                            permutation, DataLoader(shuffle=True) capgan.py:282,326-330); 0: the
                            caller provides the round's real rows / indices                      */
+  int gemm_dtype;       /* CGL_DTYPE_*: GEMM operand type (0 = fp32, the reference arithmetic)   */
 } cgl_gan_config;
 
 typedef struct cgl_gan_buffers {

@@ -104,6 +104,32 @@ def ring_discriminator_spec():
 
 
 # --------------------------------------------------------------------------
+# 16-bit GEMM operand emulation (test infrastructure for cgl_gan_config.gemm_dtype).  The
+# reference computes in fp32 only, so this has no reference counterpart: the 16-bit path's parity
+# is unpinned, and this restates what the HIP path computes (every GEMM operand rounded to 16
+# bits, exact products, wide accumulation) so that tests can check it at fp32-level tolerance.
+# --------------------------------------------------------------------------
+class _LowpLinear(torch.autograd.Function):
+    """y = r(x) r(W)^T + b; dx = r(dy) r(W); dW = r(dy)^T r(x); db = sum r(dy), r = round to
+    ``dt`` (round-to-nearest-even) and back.  ``full`` False: forward and input gradient in full
+    precision (the HIP loss head computes the D output layer outside the GEMMs)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, dt, full):
+        ctx.save_for_backward(x, w)
+        ctx.dt, ctx.full = dt, full
+        r = (lambda t: t.to(dt).to(x.dtype)) if full else (lambda t: t)
+        return r(x) @ r(w).t() + b
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        rr = lambda t: t.to(ctx.dt).to(gy.dtype)
+        r = rr if ctx.full else (lambda t: t)
+        return r(gy) @ r(w), rr(gy).t() @ rr(x), rr(gy).sum(0), None, None
+
+
+# --------------------------------------------------------------------------
 # Functional network
 # --------------------------------------------------------------------------
 class SeqNet:
@@ -139,6 +165,9 @@ class SeqNet:
         # ``trace_sink`` -- a list collecting every LeakyReLU input (see ``forward``)
         self.mask_feed = []
         self.trace_sink = None
+        # ``lowp`` = (dtype, head_key): emulate 16-bit GEMM operands (_LowpLinear); the Linear
+        # ``head_key`` (the D output layer) keeps a full-precision forward / input gradient
+        self.lowp = None
 
     # weights_init of mixed-gan.py:68-77 (Linear W~N(0,.02), b=0; BN g~N(1,.02), b=0),
     # applied in nn.Module.apply's post-order == spec order for a flat Sequential.
@@ -173,7 +202,10 @@ class SeqNet:
                 h = torch.where(m, h, h * SLOPE)
                 li += 1
                 continue
-            if kind == "linear":
+            if kind == "linear" and self.lowp is not None:
+                h = _LowpLinear.apply(h, self.params[ent[1] + ".weight"], self.params[ent[1] + ".bias"],
+                                      self.lowp[0], ent[1] != self.lowp[1])
+            elif kind == "linear":
                 h = F.linear(h, self.params[ent[1] + ".weight"], self.params[ent[1] + ".bias"])
             elif kind == "bn":
                 k = ent[1]

@@ -40,7 +40,7 @@ def rel_scalar(a, b):
     return abs(float(a) - float(b)) / max(abs(float(b)), 1e-30)
 
 
-def make_pair(kind, B, Br=None, epoch=1, seed=20211212, gen_z=False):
+def make_pair(kind, B, Br=None, epoch=1, seed=20211212, gen_z=False, gemm_dtype="f32"):
     """(oracle server, oracle workers, HIP step) with identical initial parameters."""
     if kind == "capgan":
         G, workers = O.build_capgan(1)
@@ -65,10 +65,21 @@ def make_pair(kind, B, Br=None, epoch=1, seed=20211212, gen_z=False):
     else:
         raise ValueError(kind)
     step = GanStep(gm, dm, batch=B, batch_real=Br or B, epoch=epoch, loss=loss, weighting=weighting,
-                   exchange_layer=xl, seed=seed, gen_z=gen_z)
+                   exchange_layer=xl, seed=seed, gen_z=gen_z, gemm_dtype=gemm_dtype)
     step.load_state_dicts(G.state_dict(), workers[0].D.state_dict())
     step.reset()
     return srv, workers, step
+
+
+def make_pair_oracle_only(kind, B=64):
+    """The oracle server + workers of make_pair (no GPU)."""
+    if kind == "capgan":
+        G, workers = O.build_capgan(1)
+        return O.CapganServer(G, torch.tensor([1.0])), workers
+    if kind == "mdgan":
+        G, workers = O.build_capgan(1, loss="bce")
+        return O.CapganServer(G, torch.tensor([1.0])), workers
+    raise ValueError(kind)
 
 
 def feed(step, z1, z2, reals):
