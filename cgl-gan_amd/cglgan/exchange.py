@@ -128,6 +128,8 @@ class WorkerExchange:
         s = self.step
         if self.cloud is not None and self.cloud_due is not None and self.cloud_due(r):
             self.cloud_average()
+        share = self.comm is not None and self.share_every > 0 and (r + 1) % self.share_every == 0
+        swap = self.dswap is not None and (r + 1) % self.swap_every == 0
         if self.comm is None or self.comm.size == 1:
             s.run(C.PHASE_ALL, graph=graph)
         else:
@@ -135,14 +137,38 @@ class WorkerExchange:
             self.comm.all_gather(s.losses_all, s.own_loss())
             s.alpha_scale()
             self.comm.all_reduce_sum(s.exchange_buffer())
-            s.run(C.PHASE_B, graph=graph)
-        if self.comm is not None and self.share_every > 0 and (r + 1) % self.share_every == 0:
-            self.comm.all_reduce_mean(s.d_params)
-        if self.dswap is not None and (r + 1) % self.swap_every == 0:
-            self.comm.swap([s.d_params], self.dswap.next_perm())
+            side = self._side_stream() if (share or swap) else None
+            if side is not None:
+                # phase B (G backward + Adam G) never touches D: the E-share all-reduce / D-swap of
+                # this round's updated D run on a side stream concurrently with it (issued in the
+                # same order on every rank), joined before the next round's D step
+                main = torch.cuda.current_stream()
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    self._d_exchange(r, share, swap)
+                s.run(C.PHASE_B, graph=graph)
+                main.wait_stream(side)
+                share = swap = False
+            else:
+                s.run(C.PHASE_B, graph=graph)
+        self._d_exchange(r, share, swap)
         if (self.cloud is not None and self.cloud_due is None and self.cloud_every > 0 and
                 (r + 1) % self.cloud_every == 0):
             self.cloud_average()
+
+    def _d_exchange(self, r, share, swap):
+        s = self.step
+        if share:
+            self.comm.all_reduce_mean(s.d_params)
+        if swap:
+            self.comm.swap([s.d_params], self.dswap.next_perm())
+
+    def _side_stream(self):
+        if not self.step.d_params.is_cuda:
+            return None
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.step.d_params.device)
+        return self._side
 
     def cloud_average(self):
         """Data-size-weighted average of the shared trunk (+ its BatchNorm running stats) across
