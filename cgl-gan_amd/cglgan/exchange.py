@@ -302,6 +302,8 @@ class ConvWorkerExchange:
     def round(self, r: int, real=None):
         from . import conv_ops as O
         s = self.step
+        share = self.comm is not None and self.share_every > 0 and (r + 1) % self.share_every == 0
+        swap = self.dswap is not None and (r + 1) % self.swap_every == 0
         if self.comm is None or self.comm.size == 1:
             s.run(real)
         else:
@@ -309,11 +311,27 @@ class ConvWorkerExchange:
             self.comm.all_gather(s.losses_all, s.lbuf[2:3])
             O.weights_scale(s.weighting, s.lam, s.beta, s.losses_all, s.rank, s.dimg)
             self.comm.all_reduce_sum(s.dimg)
-            s.phase_b()
-        if self.comm is not None and self.share_every > 0 and (r + 1) % self.share_every == 0:
+            if (share or swap) and s.D.p.is_cuda:
+                # as WorkerExchange.round: phase B (G backward + Adam G) never touches D, so the D
+                # exchange of this round runs on a side stream beside it, joined before the next round
+                if getattr(self, "_side", None) is None:
+                    self._side = torch.cuda.Stream(device=s.D.p.device)
+                main = torch.cuda.current_stream()
+                self._side.wait_stream(main)
+                with torch.cuda.stream(self._side):
+                    self._d_exchange(share, swap)
+                s.phase_b()
+                main.wait_stream(self._side)
+                share = swap = False
+            else:
+                s.phase_b()
+        self._d_exchange(share, swap)
+
+    def _d_exchange(self, share, swap):
+        if share:
             for t in self._d_state():
                 self.comm.all_reduce_mean(t)
-        if self.dswap is not None and (r + 1) % self.swap_every == 0:
+        if swap:
             self.comm.swap(self._d_state(), self.dswap.next_perm())
 
 
