@@ -286,6 +286,8 @@ def parse_args(argv=None):
     p.add_argument("--fedavg_compat_noop", action="store_true")
     p.add_argument("--checkpoint_dir", default="")
     p.add_argument("--eager", action="store_true", help="launch the round without hipGraph replay")
+    p.add_argument("--gemm_dtype", default="f32", choices=["f32", "f16", "bf16"],
+                   help="GEMM operand type (f16 / bf16: 16-bit operands, fp32 accumulation; BASELINE config 5)")
     return p.parse_args(argv)
 
 
