@@ -33,7 +33,8 @@ EXPORTS = [
     "cgl_nchw_to_nhwc", "cgl_nhwc_to_nchw", "cgl_adv_loss", "cgl_adam_multi", "cgl_dense_workspace_bytes",
     "cgl_dense_fwd", "cgl_dense_bwd_data", "cgl_dense_bwd_weight", "cgl_gather_rows", "cgl_weights_scale",
     "cgl_conv_packed_floats", "cgl_conv_pack_multi", "cgl_conv3x3_fwd_packed", "cgl_conv3x3_bwd_data_packed",
-    "cgl_dense_fwd_packed", "cgl_dense_bwd_data_packed",
+    "cgl_dense_fwd_packed", "cgl_dense_bwd_data_packed", "cgl_conv3x3_stat_chunks", "cgl_conv3x3_fwd_packed_stats",
+    "cgl_bn2d_fwd_stats", "cgl_bn2d_stats_scratch_bytes",
     # evaluation (CGLGAN/2DMG/main.py plot_2d KL score)
     "cgl_kl_score",
 ]
@@ -133,6 +134,10 @@ def _load():
         "cgl_conv_pack_multi": (ci, [ci, P(ConvPackJob), vp]),
         "cgl_conv3x3_fwd_packed": (ci, [vp, vp, vp, vp] + [ci] * 8 + [cf, vp, vp, i64, vp]),
         "cgl_conv3x3_bwd_data_packed": (ci, [vp, vp, vp, vp] + [ci] * 7 + [vp, i64, vp]),
+        "cgl_conv3x3_stat_chunks": (i64, [ci] * 8),
+        "cgl_conv3x3_fwd_packed_stats": (ci, [vp, vp, vp, vp] + [ci] * 8 + [cf, vp, ci, vp, vp, i64, vp]),
+        "cgl_bn2d_fwd_stats": (ci, [vp, ci, vp, ci, ci, ci, ci, vp, vp, cd, cd, vp, vp, ci, cf, vp, vp, vp, vp, vp, i64, vp]),
+        "cgl_bn2d_stats_scratch_bytes": (i64, [ci, ci]),
         "cgl_dense_fwd_packed": (ci, [vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, i64, vp]),
         "cgl_dense_bwd_data_packed": (ci, [vp, vp, vp, ci, ci, ci, vp, i64, vp]),
         "cgl_gather_rows": (ci, [vp, vp, i64, ci, ci, vp, vp]),

@@ -58,10 +58,26 @@ def conv_ws_bytes(n, h, w, cin, cout, stride, up):
     return b
 
 
-def conv3x3_fwd(x, w, b, y, n, h, wd, cin, cout, stride=1, up=0, act=ACT_NONE, slope=0.2, drop=None, wp=None):
-    """``wp``: the weights pre-packed by a PackSet (no per-call pack launch); ``w`` is then unused."""
+def stat_chunks(n, h, wd, cin, cout, stride=1, up=0, groups=1):
+    """32-row statistic chunks of a forward's output (0: epilogue statistics unsupported)."""
+    return int(C.lib.cgl_conv3x3_stat_chunks(n, h, wd, cin, cout, stride, up, groups))
+
+
+def conv3x3_fwd(x, w, b, y, n, h, wd, cin, cout, stride=1, up=0, act=ACT_NONE, slope=0.2, drop=None, wp=None,
+                stats=None):
+    """``wp``: the weights pre-packed by a PackSet (no per-call pack launch); ``w`` is then unused.
+    ``stats`` = (part, groups): also write the next BatchNorm2d's {sum, M2} partials per 32-row chunk
+    (float64 tensor of stat_chunks(...) * cout * 2) -- consumed by bn2d_fwd_stats."""
     _chk(x, w, b, y, drop, wp)
     ws = workspace(conv_ws_bytes(n, h, wd, cin, cout, stride, up), x.device)
+    if stats is not None:
+        part, groups = stats
+        if wp is None or not part.is_cuda or part.dtype != torch.float64:
+            raise RuntimeError("conv3x3_fwd(stats=...): needs packed weights and a float64 CUDA partial buffer")
+        C.check(C.lib.cgl_conv3x3_fwd_packed_stats(_p(x), _p(wp), _p(b), _p(y), n, h, wd, cin, cout, stride, up, act,
+                                                   float(slope), _p(drop), int(groups), _p(part), _p(ws), ws.numel(),
+                                                   _s()), "cgl_conv3x3_fwd_packed_stats")
+        return y
     if wp is not None:
         C.check(C.lib.cgl_conv3x3_fwd_packed(_p(x), _p(wp), _p(b), _p(y), n, h, wd, cin, cout, stride, up, act,
                                              float(slope), _p(drop), _p(ws), ws.numel(), _s()), "cgl_conv3x3_fwd_packed")
@@ -190,6 +206,27 @@ def bn2d_fwd(x, n, hw, c, gamma, beta, y, groups=1, eps=0.8, momentum=0.1, runni
     C.check(C.lib.cgl_bn2d_fwd(_p(x), n, hw, c, groups, _p(gamma), _p(beta), float(eps), float(momentum),
                                _p(running_mean), _p(running_var), int(train), act, float(slope), _p(y), _p(save_mean),
                                _p(save_invstd), _p(ws), ws.numel(), _s()), "cgl_bn2d_fwd")
+    return y
+
+
+def bn2d_stats_scratch(c, groups, device):
+    """The zeroed per-BatchNorm scratch of bn2d_fwd_stats (sliced finalize tickets + slice results)."""
+    n = C.lib.cgl_bn2d_stats_scratch_bytes(c, groups)
+    if n < 0:
+        raise RuntimeError(f"bn2d_stats_scratch: bad shape (rc={n})")
+    return torch.zeros(int(n), dtype=torch.uint8, device=device)
+
+
+def bn2d_fwd_stats(part, x, n, hw, c, gamma, beta, y, groups=1, eps=0.8, momentum=0.1, running_mean=None,
+                   running_var=None, act=ACT_NONE, slope=0.2, save_mean=None, save_invstd=None, R=32, scratch=None):
+    """bn2d_fwd (train) from the partials a conv3x3_fwd(stats=...) wrote: finalize + apply.
+    ``scratch``: bn2d_stats_scratch(c, max groups) kept with the layer (parallel finalize)."""
+    _chk(x, gamma, beta, y, running_mean, running_var, save_mean, save_invstd)
+    ws = workspace(bn2d_ws_bytes(n, hw, c, groups), x.device)
+    C.check(C.lib.cgl_bn2d_fwd_stats(_p(part), int(R), _p(x), n, hw, c, groups, _p(gamma), _p(beta), float(eps),
+                                     float(momentum), _p(running_mean), _p(running_var), act, float(slope), _p(y),
+                                     _p(save_mean), _p(save_invstd), _p(scratch), _p(ws), ws.numel(), _s()),
+            "cgl_bn2d_fwd_stats")
     return y
 
 

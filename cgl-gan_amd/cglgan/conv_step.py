@@ -198,6 +198,19 @@ class ConvGanStep:
         pk.add("D", "advf", PD["adv_layer.weight"], 1, 1, 512, 1, ks=1)
         pk.add("D", "advb", PD["adv_layer.weight"], 1, 1, 512, 1, ks=1, dir=1)
         self.pk = pk.finalize(dev)
+        # BatchNorm2d statistics written by the producing conv's epilogue (cgl_conv3x3_fwd_packed_stats):
+        # one float64 partial buffer per BatchNorm, sized for its largest call (the D step's 2B rows)
+        sc = lambda n, h, ci, co, st, up, grp: O.stat_chunks(n, h, h, ci, co, st, up, grp)
+        self.st_geo = {"conv_blocks.2": (B2, 8, 128, 128, 1, 1, 2), "conv_blocks.6": (B2, 16, 128, 64, 1, 1, 2)}
+        for ck, bk, ci, co, hw in D_CONVS:
+            if bk:
+                self.st_geo[bk] = (B2, hw, ci, co, 2, 0, 2)
+        self.st_part, self.st_scratch = {}, {}
+        for k, geo in self.st_geo.items():
+            n = sc(*geo)
+            if n > 0:
+                self.st_part[k] = torch.zeros(n * geo[3] * 2, dtype=torch.float64, device=dev)
+                self.st_scratch[k] = O.bn2d_stats_scratch(geo[3], geo[6], dev)
         # sampler over a device-resident real shard [n, 1024] (DataLoader(shuffle=True), capgan.py:282)
         self.data = data
         self._perm, self._pos = None, 0
@@ -240,21 +253,33 @@ class ConvGanStep:
         O.dense_fwd(self.z, P["l1.0.weight"], P["l1.0.bias"], self.h, B2, 100, 8192, wp=self.pk["l1"])
         O.nchw_to_nhwc(self.h, self.h0, B2, 128, 64)      # out.view(B, 128, 8, 8), model/lsgan.py:25
         O.conv3x3_fwd(self.h0, P["conv_blocks.1.weight"], P["conv_blocks.1.bias"], self.y1, B2, 8, 8, 128, 128, 1, 1,
-                      wp=self.pk["c1f"])
+                      wp=self.pk["c1f"], stats=self._stats("conv_blocks.2", 2))
         self._g_bn("conv_blocks.2", self.y1, self.a1, 256, 128)
         O.conv3x3_fwd(self.a1, P["conv_blocks.5.weight"], P["conv_blocks.5.bias"], self.y2, B2, 16, 16, 128, 64, 1, 1,
-                      wp=self.pk["c5f"])
+                      wp=self.pk["c5f"], stats=self._stats("conv_blocks.6", 2))
         self._g_bn("conv_blocks.6", self.y2, self.a2, 1024, 64)
         O.conv3x3_fwd(self.a2, P["conv_blocks.8.weight"], P["conv_blocks.8.bias"], self.x3[self.B:], B2, 32, 32, 64, 1,
                       1, 0, act=O.ACT_TANH, wp=self.pk["c8f"])
 
+    def _stats(self, key, groups):
+        part = self.st_part.get(key)
+        return (part, groups) if part is not None else None
+
+    def _bn_fwd(self, key, fm, x, y, n, hw, c, groups, act):
+        """BatchNorm2d (train) from the partials the producing conv wrote, else with its own pass."""
+        P, R = fm.params, fm.running
+        sm, si = (self.g_save if fm is self.G else self.d_save)[key]
+        kw = dict(groups=groups, eps=BN_EPS, momentum=BN_MOM, running_mean=R[key + ".running_mean"],
+                  running_var=R[key + ".running_var"], act=act, slope=SLOPE, save_mean=sm, save_invstd=si)
+        if key in self.st_part:
+            O.bn2d_fwd_stats(self.st_part[key], x, n, hw, c, P[key + ".weight"], P[key + ".bias"], y,
+                             scratch=self.st_scratch[key], **kw)
+        else:
+            O.bn2d_fwd(x, n, hw, c, P[key + ".weight"], P[key + ".bias"], y, train=True, **kw)
+        fm.batches[key] += groups
+
     def _g_bn(self, key, x, y, hw, c):
-        P, R = self.G.params, self.G.running
-        sm, si = self.g_save[key]
-        O.bn2d_fwd(x, 2 * self.B, hw, c, P[key + ".weight"], P[key + ".bias"], y, groups=2, eps=BN_EPS,
-                   momentum=BN_MOM, running_mean=R[key + ".running_mean"], running_var=R[key + ".running_var"],
-                   train=True, act=O.ACT_LEAKY, slope=SLOPE, save_mean=sm, save_invstd=si)
-        self.G.batches[key] += 2
+        self._bn_fwd(key, self.G, x, y, 2 * self.B, hw, c, 2, O.ACT_LEAKY)
 
     def _masks(self):
         """Every Dropout2d mask of the round in one launch: the D step's (call 0, 2B images) and the
@@ -269,14 +294,10 @@ class ConvGanStep:
         inp = x
         for k, (ck, bk, ci, co, hw) in enumerate(D_CONVS):
             O.conv3x3_fwd(inp, P[ck + ".weight"], P[ck + ".bias"], self.q[k], n, hw, hw, ci, co, 2, 0, act=O.ACT_LEAKY,
-                          slope=SLOPE, drop=masks[k], wp=self.pk[ck + "f"])
+                          slope=SLOPE, drop=masks[k], wp=self.pk[ck + "f"], stats=self._stats(bk, groups) if bk else None)
             inp = self.q[k]
             if bk:
-                sm, si = self.d_save[bk]
-                O.bn2d_fwd(self.q[k], n, (hw // 2) ** 2, co, P[bk + ".weight"], P[bk + ".bias"], self.r[k], groups=groups,
-                           eps=BN_EPS, momentum=BN_MOM, running_mean=R[bk + ".running_mean"],
-                           running_var=R[bk + ".running_var"], train=True, act=O.ACT_NONE, save_mean=sm, save_invstd=si)
-                self.D.batches[bk] += groups
+                self._bn_fwd(bk, self.D, self.q[k], self.r[k], n, (hw // 2) ** 2, co, groups, O.ACT_NONE)
                 inp = self.r[k]
         O.nhwc_to_nchw(self.r[3], self.flat, n, 128, 4)    # out.view(B, -1), model/lsgan.py:96
         O.dense_fwd(self.flat, P["adv_layer.weight"], P["adv_layer.bias"], self.v, n, 512, 1, wp=self.pk["advf"])

@@ -53,6 +53,8 @@ struct CglConvProb {
   const float* Wp;           // packed weights [N][Kp]
   float* Y;                  // output (fwd), or the output gradient dY (wgrad, read only)
   float* part;               // wgrad partials [splits][N][Kp]
+  int st_gr, st_off;         // BatchNorm statistics in the epilogue: rows per forward call (group),
+                             // first 32-row chunk of this problem within a group's chunks
 };
 
 struct CglConvLaunch {
@@ -63,6 +65,8 @@ struct CglConvLaunch {
   float slope;
   const float* drop;         // Dropout2d scale per (image, channel) [img][ldy], or null
   int wbias;                 // weight gradient: im2col column K is the constant 1 (bias gradient)
+  double* st_part;           // forward: per-(32-row chunk, channel) {sum, M2} of the stored output
+  int st_cpg;                // 32-row chunks per group (all problems)
 };
 
 typedef const CGL_AS4 CglConvLaunch* CglKL;
@@ -324,6 +328,34 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
       for (int r = 0; r < 16; ++r) {
         int img;
         decode(r, img);
+      }
+    }
+    // BatchNorm2d statistics of the stored values (the next op's BatchNorm, cgl_bn2d_fwd_stats): per
+    // 32-row chunk and channel {sum, M2 about the chunk mean} in double, the two lane halves
+    // combined by one xor-32 exchange (fixed order); the chunks of a forward call are contiguous
+    if (L->st_part) {
+      const int g = rowb / P->st_gr;
+      const long chunk = (long)g * L->st_cpg + P->st_off + (rowb - g * P->st_gr) / 32;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        double sm = 0.0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sm += (double)acc[i][j][r];
+        sm += __shfl_xor(sm, 32);
+        const double mu = sm * (1.0 / 32.0);
+        double m2 = 0.0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const double dd = (double)acc[i][j][r] - mu;
+          m2 += dd * dd;
+        }
+        m2 += __shfl_xor(m2, 32);
+        const int col = n0 + 32 * j + li;
+        if (lh == 0 && col < N) {
+          double* dst = L->st_part + (chunk * N + col) * 2;
+          dst[0] = sm;
+          dst[1] = m2;
+        }
       }
     }
     // stores through a buffer resource based at the block's first output pixel (output pixels grow
@@ -1395,6 +1427,24 @@ __device__ __forceinline__ double cgl_block_sum_d(double x, double* red) {
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// sum over chunks q = lane, lane + 256, ... < cnt of f(part pair at chunk q0 + q) -- 8 independent
+// 16-byte loads in flight per thread, accumulated in chunk order (the per-thread order is fixed)
+template <class Fn>
+__device__ __forceinline__ double cgl_fin_sum(const double* part, long q0, int cnt, int C, int c, int lane, Fn fn) {
+  typedef double f64x2 __attribute__((ext_vector_type(2)));
+  typedef const CGL_GLOBAL f64x2* gcd2p;
+  double t = 0.0;
+  for (int qb = lane; qb < cnt; qb += 8 * 256) {
+    f64x2 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = *(gcd2p)(part + ((q0 + min(qb + 256 * i, cnt - 1)) * C + c) * 2);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (qb + 256 * i < cnt) t += fn(v[i]);
+  }
+  return t;
+}
+
 __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
   __shared__ double red[4];
   const int lane = threadIdx.x;          // thread index within the channel's workgroup
@@ -1402,9 +1452,8 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
   const int C = a.C;
   const double* part = a.part;
   if (a.mode == 2) {
-    double t = 0.0;
     const int nch = a.groups * a.chunks_per_group;
-    for (int q = lane; q < nch; q += 256) t += part[((long)q * C + c) * 2];
+    double t = cgl_fin_sum(part, 0, nch, C, c, lane, [](auto v) { return (double)v[0]; });
     t = cgl_block_sum_d(t, red);
     if (lane == 0) gst(a.dgamma + c, (float)t);
     return;
@@ -1414,12 +1463,8 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
   if (a.mode == 1) {
     double dg = 0.0, db = 0.0;
     for (int g = 0; g < a.groups; ++g) {
-      double S = 0.0, D = 0.0;
-      for (int q = lane; q < cpg; q += 256) {
-        const long o = ((long)(g * cpg + q) * C + c) * 2;
-        S += part[o];
-        D += part[o + 1];
-      }
+      double S = cgl_fin_sum(part, (long)g * cpg, cpg, C, c, lane, [](auto v) { return (double)v[0]; });
+      double D = cgl_fin_sum(part, (long)g * cpg, cpg, C, c, lane, [](auto v) { return (double)v[1]; });
       S = cgl_block_sum_d(S, red);
       D = cgl_block_sum_d(D, red);
       const float invstd = gld(a.save_invstd + (long)g * C + c);
@@ -1449,18 +1494,16 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
   }
   float rm = a.run_mean ? gld(a.run_mean + c) : 0.f, rv = a.run_var ? gld(a.run_var + c) : 0.f;
   for (int g = 0; g < a.groups; ++g) {
-    double s = 0.0;
-    for (int q = lane; q < cpg; q += 256) s += part[((long)(g * cpg + q) * C + c) * 2];
+    const long q0 = (long)g * cpg;
+    double s = cgl_fin_sum(part, q0, cpg, C, c, lane, [](auto v) { return (double)v[0]; });
     s = cgl_block_sum_d(s, red);
     const double n = a.gr;
     const double mu = s / n;
-    double m2 = 0.0;
-    for (int q = lane; q < cpg; q += 256) {
-      const long o = ((long)(g * cpg + q) * C + c) * 2;
-      const double cnt = a.R;
-      const double dd = part[o] / cnt - mu;
-      m2 += part[o + 1] + cnt * dd * dd;
-    }
+    const double cnt = a.R;
+    double m2 = cgl_fin_sum(part, q0, cpg, C, c, lane, [&](auto v) {
+      const double dd = v[0] / cnt - mu;
+      return (double)v[1] + cnt * dd * dd;
+    });
     m2 = cgl_block_sum_d(m2, red);
     const double invstd = 1.0 / sqrt(m2 / n + a.eps);
     const float sc = (float)invstd * w;
@@ -1481,6 +1524,94 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
   if (a.run_mean && lane == 0) {
     gst(a.run_mean + c, rm);
     gst(a.run_var + c, rv);
+  }
+}
+
+// Sliced training-mode BatchNorm2d finalize for statistics with many chunks (the 32-row chunks a
+// conv epilogue writes: 8192 per forward call of the generator's last BatchNorm at B=256): block
+// (s, c) merges slice s of channel c's chunks of every call into {mean_s, M2_s} (two passes, fixed
+// order), publishes them with agent-scope atomic stores and takes a ticket; the last block of
+// channel c merges the S slices in slice order (Chan) and finishes exactly as cgl_bn_finalize mode
+// 0.  Tickets are monotonic (the caller zeroes them once; every launch adds S per channel).
+#define CGL_FIN_MAXS 64
+struct CglBnFinSliced {
+  CglBnFinArgs f;
+  int S, L;                  // slices per channel, chunks per slice
+  double* sl;                // [C][groups][S][2] slice {mean, M2}
+  unsigned int* ctr;         // [C] tickets
+};
+
+__global__ __launch_bounds__(256) void cgl_bn_finalize_sliced(CglBnFinSliced a) {
+  __shared__ double red[4];
+  __shared__ double smu[CGL_FIN_MAXS], sm2[CGL_FIN_MAXS];
+  __shared__ int last;
+  const int s = blockIdx.x, c = blockIdx.y, lane = threadIdx.x;
+  const int C = a.f.C, cpg = a.f.chunks_per_group, G = a.f.groups, S = a.S;
+  const int q_lo = s * a.L, cnt = min(q_lo + a.L, cpg) - q_lo;
+  const double R = a.f.R;
+  for (int g = 0; g < G; ++g) {
+    const long q0 = (long)g * cpg + q_lo;
+    double sm = cgl_fin_sum(a.f.part, q0, cnt, C, c, lane, [](auto v) { return (double)v[0]; });
+    sm = cgl_block_sum_d(sm, red);
+    const double mu = sm / (cnt * R);
+    double m2 = cgl_fin_sum(a.f.part, q0, cnt, C, c, lane, [&](auto v) {
+      const double dd = v[0] / R - mu;
+      return (double)v[1] + R * dd * dd;
+    });
+    m2 = cgl_block_sum_d(m2, red);
+    if (lane == 0) {
+      double* dst = a.sl + (((long)c * G + g) * S + s) * 2;
+      cgl_pubd(dst, mu);
+      cgl_pubd(dst + 1, m2);
+    }
+  }
+  if (lane == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the published words have landed
+    const unsigned int old = __hip_atomic_fetch_add((cgl_gu32*)(a.ctr + c), 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+    last = (old % (unsigned)S) == (unsigned)(S - 1);
+  }
+  __syncthreads();
+  if (!last) return;
+  const float w = a.f.gamma ? gld(a.f.gamma + c) : 1.f;
+  const float b = a.f.beta ? gld(a.f.beta + c) : 0.f;
+  float rm = a.f.run_mean ? gld(a.f.run_mean + c) : 0.f, rv = a.f.run_var ? gld(a.f.run_var + c) : 0.f;
+  for (int g = 0; g < G; ++g) {
+    if (lane < S) {
+      const double* src = a.sl + (((long)c * G + g) * S + lane) * 2;
+      smu[lane] = __longlong_as_double((long long)cgl_ld64(src));
+      sm2[lane] = __longlong_as_double((long long)cgl_ld64(src + 1));
+    }
+    __syncthreads();
+    if (lane == 0) {
+      const double n = a.f.gr;
+      double tot = 0.0;
+      for (int q = 0; q < S; ++q) tot += smu[q] * (min((q + 1) * a.L, cpg) - q * a.L) * R;
+      const double mu = tot / n;
+      double m2 = 0.0;
+      for (int q = 0; q < S; ++q) {
+        const double dd = smu[q] - mu;
+        m2 += sm2[q] + (min((q + 1) * a.L, cpg) - q * a.L) * R * dd * dd;
+      }
+      const double invstd = 1.0 / sqrt(m2 / n + a.f.eps);
+      const float sc = (float)invstd * w;
+      gst(a.f.coef0 + (long)g * C + c, sc);
+      gst(a.f.coef1 + (long)g * C + c, b - (float)mu * sc);
+      if (a.f.save_mean) {
+        gst(a.f.save_mean + (long)g * C + c, (float)mu);
+        gst(a.f.save_invstd + (long)g * C + c, (float)invstd);
+      }
+      if (a.f.run_mean) {
+        const double mom = a.f.momentum;
+        rm = (float)(mom * mu + (1.0 - mom) * (double)rm);
+        rv = (float)(mom * (n > 1 ? m2 / (n - 1) : m2 / n) + (1.0 - mom) * (double)rv);
+      }
+    }
+    __syncthreads();
+  }
+  if (a.f.run_mean && lane == 0) {
+    gst(a.f.run_mean + c, rm);
+    gst(a.f.run_var + c, rv);
   }
 }
 
@@ -2074,7 +2205,7 @@ bool n1_ok(const CglConvProb* P, int np) {
 }
 
 int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float slope, const float* drop,
-                    hipStream_t s) {
+                    hipStream_t s, double* st_part = nullptr, int st_cpg = 0) {
   const int N = P[0].N;
   CglConvLaunch L;
   std::memset(&L, 0, sizeof(L));
@@ -2083,6 +2214,9 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
   L.act = act;
   L.slope = slope;
   L.drop = drop;
+  L.st_part = st_part;
+  L.st_cpg = st_cpg;
+  if (st_part && N == 1) return CGL_E_ARG;   // statistics only from the MFMA kernel
   if (N == 1 && np == 1 && P[0].Ty == 3 && P[0].Tx == 3 && P[0].isy == 1 && P[0].isx == 1 && P[0].ish == 0 &&
       P[0].osy == 1 && P[0].osx == 1 && P[0].dy[0] == -1 && P[0].dx[0] == -1 && P[0].Cin % 4 == 0 &&
       P[0].Cin <= 256 && ((P[0].Cin / 4) & (P[0].Cin / 4 - 1)) == 0 && P[0].XH == P[0].OH && P[0].XW == P[0].OW &&
@@ -2177,13 +2311,40 @@ int col_sum(const float* X, int64_t rows, int C, double* part, float* out, hipSt
 
 namespace {
 
+// BatchNorm statistics in the forward epilogue: supported when every problem's rows per forward
+// call are whole 32-row chunks and the launch takes the MFMA kernel; returns the chunks per call
+// (0: unsupported)
+int stat_chunks_per_group(const ConvGeom& g, int groups) {
+  if (groups < 1 || g.n % groups || g.cout < 32) return 0;
+  CglConvProb P[CGL_CONV_MAXP];
+  const int np = fwd_probs(g, P);
+  int cpg = 0;
+  for (int i = 0; i < np; ++i) {
+    const long gr = (long)(g.n / groups) * P[i].OH * P[i].OW;
+    if (gr % 32) return 0;
+    cpg += (int)(gr / 32);
+  }
+  return cpg;
+}
+
 int conv_fwd_impl(const ConvGeom& g, const float* X, const float* W, const float* bias, float* Y, int act, float slope,
-                  const float* drop, void* ws, int64_t wsb, hipStream_t s, const float* Wp = nullptr) {
+                  const float* drop, void* ws, int64_t wsb, hipStream_t s, const float* Wp = nullptr,
+                  double* st_part = nullptr, int st_groups = 1) {
   if (!X || !(W || Wp) || !Y || !ws || act < 0 || act > 3 || !al16(ws) || (Wp && !al16(Wp))) return CGL_E_ARG;
   if (wsb < conv_ws_bytes(g)) return CGL_E_SIZE;
   if ((g.cin % 4 == 0) && !al16(X)) return CGL_E_ARG;
   CglConvProb P[CGL_CONV_MAXP];
   const int np = fwd_probs(g, P);
+  int cpg = 0;
+  if (st_part) {
+    if (!(cpg = stat_chunks_per_group(g, st_groups)) || ((uintptr_t)st_part & 15)) return CGL_E_ARG;
+    int off = 0;
+    for (int i = 0; i < np; ++i) {
+      P[i].st_gr = (g.n / st_groups) * P[i].OH * P[i].OW;
+      P[i].st_off = off;
+      off += P[i].st_gr / 32;
+    }
+  }
   for (int i = 0; i < np; ++i) {
     P[i].X = X;
     P[i].Y = Y;
@@ -2191,7 +2352,7 @@ int conv_fwd_impl(const ConvGeom& g, const float* X, const float* W, const float
   int rc;
   if (Wp) pack_layout(P, np, Wp);
   else if ((rc = launch_pack(W, g, 0, P, np, (float*)ws, s))) return rc;
-  return launch_conv_mma(P, np, bias, act, slope, drop, s);
+  return launch_conv_mma(P, np, bias, act, slope, drop, s, st_part, cpg);
 }
 
 int conv_bwd_data_impl(const ConvGeom& g, const float* dY, const float* W, float* dX, void* ws, int64_t wsb,
@@ -2434,6 +2595,23 @@ int cgl_conv3x3_fwd_packed(const float* X, const float* Wp, const float* bias, f
   return conv_fwd_impl(g, X, nullptr, bias, Y, act, slope, drop, ws, wsb, (hipStream_t)stream, Wp);
 }
 
+int64_t cgl_conv3x3_stat_chunks(int n, int h, int w, int cin, int cout, int stride, int up, int groups) {
+  ConvGeom g;
+  const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
+  if (rc) return rc;
+  return (int64_t)stat_chunks_per_group(g, groups) * groups;
+}
+
+int cgl_conv3x3_fwd_packed_stats(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w,
+                                 int cin, int cout, int stride, int up, int act, float slope, const float* drop,
+                                 int groups, double* part, void* ws, int64_t wsb, void* stream) {
+  ConvGeom g;
+  const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
+  if (rc) return rc;
+  if (!Wp || !part) return CGL_E_ARG;
+  return conv_fwd_impl(g, X, nullptr, bias, Y, act, slope, drop, ws, wsb, (hipStream_t)stream, Wp, part, groups);
+}
+
 int cgl_conv3x3_bwd_data_packed(const float* dY, const float* W, const float* Wp, float* dX, int n, int h, int w,
                                 int cin, int cout, int stride, int up, void* ws, int64_t wsb, void* stream) {
   ConvGeom g;
@@ -2502,6 +2680,59 @@ int cgl_bn2d_fwd(const float* X, int n, int hw, int C, int groups, const float* 
   f.run_mean = running_mean; f.run_var = running_var; f.save_mean = save_mean; f.save_invstd = save_invstd;
   f.coef0 = c0; f.coef1 = c1;
   hipLaunchKernelGGL(cgl_bn_finalize, dim3(C), dim3(256), 0, s, f);
+  CglEltArgs e;
+  std::memset(&e, 0, sizeof(e));
+  e.mode = 0; e.rows = (int)rows; e.C = C; e.gr = (int)gr; e.hw = hw; e.act = act; e.slope = slope;
+  e.X = X; e.coef0 = c0; e.coef1 = c1; e.out = Y;
+  const long n4 = rows * C / 4;
+  hipLaunchKernelGGL(cgl_eltwise, dim3((unsigned)std::min<long>((n4 + 255) / 256, 8192)), dim3(256), 0, s, e);
+  return (int)hipGetLastError();
+}
+
+int64_t cgl_bn2d_stats_scratch_bytes(int C, int groups) {
+  if (C < 1 || groups < 1) return CGL_E_ARG;
+  return al256((int64_t)C * 4) + (int64_t)C * groups * CGL_FIN_MAXS * 16;
+}
+
+int cgl_bn2d_fwd_stats(const double* part, int R, const float* X, int n, int hw, int C, int groups, const float* gamma,
+                       const float* beta, double eps, double momentum, float* running_mean, float* running_var,
+                       int act, float slope, float* Y, float* save_mean, float* save_invstd, void* scratch,
+                       void* ws, int64_t wsb, void* stream) {
+  if (!part || !X || !Y || !gamma || !beta || !ws || !al16(ws) || !al16(X) || !al16(Y)) return CGL_E_ARG;
+  if (n < 1 || hw < 1 || C % 4 != 0 || !pow2_le256(C) || groups < 1 || n % groups || (act != 0 && act != 1))
+    return CGL_E_ARG;
+  if ((running_mean == nullptr) != (running_var == nullptr)) return CGL_E_ARG;
+  if ((save_mean == nullptr) != (save_invstd == nullptr)) return CGL_E_ARG;
+  const int64_t gr = (int64_t)(n / groups) * hw;
+  if (R < 1 || gr % R || gr < 2) return CGL_E_ARG;
+  if (wsb < cgl_bn2d_workspace_bytes(n, hw, C, groups)) return CGL_E_SIZE;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t rows = (int64_t)n * hw;
+  const int R0 = chan_chunk(gr);
+  float* coef = (float*)((char*)ws + al256((rows / R0) * C * 16));
+  float* c0 = coef;
+  float* c1 = coef + al256((int64_t)groups * C * 4) / 4;
+  CglBnFinArgs f;
+  std::memset(&f, 0, sizeof(f));
+  f.part = part; f.C = C; f.groups = groups; f.chunks_per_group = (int)(gr / R); f.R = R; f.gr = (int)gr;
+  f.mode = 0; f.train = 1; f.gamma = gamma; f.beta = beta; f.eps = eps; f.momentum = momentum;
+  f.run_mean = running_mean; f.run_var = running_var; f.save_mean = save_mean; f.save_invstd = save_invstd;
+  f.coef0 = c0; f.coef1 = c1;
+  const int cpg = (int)(gr / R);
+  if (scratch && cpg > 1024) {   // many chunks: slices of <= 512 per block, merged by the last block
+    if ((uintptr_t)scratch & 255) return CGL_E_ARG;
+    CglBnFinSliced a;
+    std::memset(&a, 0, sizeof(a));
+    a.f = f;
+    a.L = 512;
+    a.S = (cpg + a.L - 1) / a.L;
+    if (a.S > CGL_FIN_MAXS) a.L = (cpg + CGL_FIN_MAXS - 1) / CGL_FIN_MAXS, a.S = (cpg + a.L - 1) / a.L;
+    a.ctr = (unsigned int*)scratch;
+    a.sl = (double*)((char*)scratch + al256((int64_t)C * 4));
+    hipLaunchKernelGGL(cgl_bn_finalize_sliced, dim3(a.S, C), dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(cgl_bn_finalize, dim3(C), dim3(256), 0, s, f);
+  }
   CglEltArgs e;
   std::memset(&e, 0, sizeof(e));
   e.mode = 0; e.rows = (int)rows; e.C = C; e.gr = (int)gr; e.hw = hw; e.act = act; e.slope = slope;

@@ -247,6 +247,15 @@ int cgl_conv3x3_fwd_packed(const float* X, const float* Wp, const float* bias, f
 int cgl_conv3x3_bwd_data_packed(const float* dY, const float* W, const float* Wp, float* dX, int n, int h, int w,
                                 int cin, int cout, int stride, int up, void* workspace, int64_t ws_bytes,
                                 void* stream);
+/* The forward with the next BatchNorm2d's statistics computed in its epilogue (no separate pass
+ * over Y): part [groups * chunks][cout][2] doubles = {sum, M2 about the chunk mean} of every 32-row
+ * chunk of the stored output (after act / drop), the chunks of forward call g contiguous.
+ * cgl_conv3x3_stat_chunks gives the chunk count (groups * chunks; 0 when unsupported: cout < 32 or a
+ * call's rows not whole 32-row chunks).  Consumed by cgl_bn2d_fwd_stats (R = 32). */
+int64_t cgl_conv3x3_stat_chunks(int n, int h, int w, int cin, int cout, int stride, int up, int groups);
+int cgl_conv3x3_fwd_packed_stats(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w,
+                                 int cin, int cout, int stride, int up, int act, float slope, const float* drop,
+                                 int groups, double* part, void* workspace, int64_t ws_bytes, void* stream);
 int cgl_dense_fwd_packed(const float* X, const float* Wp, const float* b, float* Y, int M, int K, int N, int act,
                          float slope, void* workspace, int64_t ws_bytes, void* stream);
 int cgl_dense_bwd_data_packed(const float* dY, const float* Wp, float* dX, int M, int K, int N, void* workspace,
@@ -264,6 +273,15 @@ int cgl_bn2d_fwd(const float* X, int n, int hw, int C, int groups, const float* 
  * `post` (that activation's output) is given.  The result is optionally multiplied by
  * LeakyReLU'(post_out) and the Dropout2d scale drop[n][C] (the Conv -> LeakyReLU -> Dropout2d ->
  * BatchNorm2d block of model/lsgan.py:78-80, backward in one pass).  dgamma / dbeta may be null. */
+/* cgl_bn2d_fwd (train) from statistics partials already computed (R rows per chunk, the layout of
+ * cgl_conv3x3_fwd_packed_stats): finalize + apply only.  scratch (may be null; 256-byte aligned,
+ * cgl_bn2d_stats_scratch_bytes, ZEROED ONCE by the caller and kept per BatchNorm layer): lets a call
+ * with more than 1024 chunks per forward call finalize in parallel slices (monotonic tickets). */
+int64_t cgl_bn2d_stats_scratch_bytes(int C, int groups);
+int cgl_bn2d_fwd_stats(const double* part, int R, const float* X, int n, int hw, int C, int groups, const float* gamma,
+                       const float* beta, double eps, double momentum, float* running_mean, float* running_var,
+                       int act, float slope, float* Y, float* save_mean, float* save_invstd, void* scratch,
+                       void* workspace, int64_t ws_bytes, void* stream);
 int cgl_bn2d_bwd(const float* dY, const float* post, const float* X, int n, int hw, int C, int groups,
                  const float* save_mean, const float* save_invstd, const float* gamma, float slope,
                  const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta, void* workspace,
