@@ -34,7 +34,8 @@ EXPORTS = [
     "cgl_dense_fwd", "cgl_dense_bwd_data", "cgl_dense_bwd_weight", "cgl_gather_rows", "cgl_weights_scale",
     "cgl_conv_packed_floats", "cgl_conv_pack_multi", "cgl_conv3x3_fwd_packed", "cgl_conv3x3_bwd_data_packed",
     "cgl_dense_fwd_packed", "cgl_dense_bwd_data_packed", "cgl_conv3x3_stat_chunks", "cgl_conv3x3_fwd_packed_stats",
-    "cgl_bn2d_fwd_stats", "cgl_bn2d_stats_scratch_bytes",
+    "cgl_bn2d_fwd_stats", "cgl_bn2d_stats_scratch_bytes", "cgl_linear_desc_bytes", "cgl_linear_prepare",
+    "cgl_linear_launch",
     # evaluation (CGLGAN/2DMG/main.py plot_2d KL score)
     "cgl_kl_score",
 ]
@@ -70,6 +71,10 @@ class ConvPackJob(ctypes.Structure):
     _fields_ = [("W", ctypes.c_void_p), ("Wp", ctypes.c_void_p), ("h", ctypes.c_int), ("w", ctypes.c_int),
                 ("cin", ctypes.c_int), ("cout", ctypes.c_int), ("stride", ctypes.c_int), ("up", ctypes.c_int),
                 ("ks", ctypes.c_int), ("dir", ctypes.c_int)]
+
+
+class LinearLaunch(ctypes.Structure):
+    _fields_ = [("tm", ctypes.c_int), ("grid", ctypes.c_int), ("shmem", ctypes.c_int), ("flags", ctypes.c_int)]
 
 
 class GanStats(ctypes.Structure):
@@ -138,6 +143,9 @@ def _load():
         "cgl_conv3x3_fwd_packed_stats": (ci, [vp, vp, vp, vp] + [ci] * 8 + [cf, vp, ci, vp, vp, i64, vp]),
         "cgl_bn2d_fwd_stats": (ci, [vp, ci, vp, ci, ci, ci, ci, vp, vp, cd, cd, vp, vp, ci, cf, vp, vp, vp, vp, vp, i64, vp]),
         "cgl_bn2d_stats_scratch_bytes": (i64, [ci, ci]),
+        "cgl_linear_desc_bytes": (i64, []),
+        "cgl_linear_prepare": (ci, [ci, vp, vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, P(LinearLaunch)]),
+        "cgl_linear_launch": (ci, [vp, P(LinearLaunch), vp]),
         "cgl_dense_fwd_packed": (ci, [vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, i64, vp]),
         "cgl_dense_bwd_data_packed": (ci, [vp, vp, vp, ci, ci, ci, vp, i64, vp]),
         "cgl_gather_rows": (ci, [vp, vp, i64, ci, ci, vp, vp]),

@@ -145,6 +145,23 @@ def dense_bwd_weight(dy, x, dw, db, M, K, N):
     return dw
 
 
+class PreparedLinear:
+    """A Linear GEMM (op 0 forward, 1 input gradient, 2 weight + bias gradient) prepared once on the
+    fused-MLP GEMM kernel (cgl_linear_prepare) and launched stream-ordered, capturable, without a
+    descriptor upload: the operand tensors given here are the ones every launch reads."""
+
+    def __init__(self, op, a, b, bias, c, db, M, N, K, act=ACT_NONE, slope=0.2):
+        _chk(a, b, bias, c, db)
+        self._keep = (a, b, bias, c, db)
+        self.desc = torch.zeros(int(C.lib.cgl_linear_desc_bytes()), dtype=torch.uint8, device=a.device)
+        self.launch = C.LinearLaunch()
+        C.check(C.lib.cgl_linear_prepare(int(op), _p(a), _p(b), _p(bias), _p(c), _p(db), M, N, K, act, float(slope),
+                                         _p(self.desc), ctypes.byref(self.launch)), "cgl_linear_prepare")
+
+    def __call__(self):
+        C.check(C.lib.cgl_linear_launch(_p(self.desc), ctypes.byref(self.launch), _s()), "cgl_linear_launch")
+
+
 class PackSet:
     """The packed MFMA weight operands of several layers, refreshed by ONE cgl_conv_pack_multi launch.
 

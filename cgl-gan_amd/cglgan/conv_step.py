@@ -186,7 +186,6 @@ class ConvGanStep:
         # after its Adam step -- two pack launches per round instead of one per conv call
         PG, PD = self.G.params, self.D.params
         pk = O.PackSet()
-        pk.add("G", "l1", PG["l1.0.weight"], 1, 1, 100, 8192, ks=1)
         pk.add("G", "c1f", PG["conv_blocks.1.weight"], 8, 8, 128, 128, 1, 1)
         pk.add("G", "c1b", PG["conv_blocks.1.weight"], 8, 8, 128, 128, 1, 1, dir=1)
         pk.add("G", "c5f", PG["conv_blocks.5.weight"], 16, 16, 128, 64, 1, 1)
@@ -198,6 +197,11 @@ class ConvGanStep:
         pk.add("D", "advf", PD["adv_layer.weight"], 1, 1, 512, 1, ks=1)
         pk.add("D", "advb", PD["adv_layer.weight"], 1, 1, 512, 1, ks=1, dir=1)
         self.pk = pk.finalize(dev)
+        # G's nn.Linear(100, 8192) (model/lsgan.py:8) on the fused-MLP GEMM kernel, prepared once:
+        # forward on [z1; z2] and its weight + bias gradient on the z2 rows
+        GG = self.G.grads
+        self.l1_fwd = O.PreparedLinear(0, self.z, PG["l1.0.weight"], PG["l1.0.bias"], self.h, None, B2, 8192, 100)
+        self.l1_wgrad = O.PreparedLinear(2, self.dh, self.z[B:], None, GG["l1.0.weight"], GG["l1.0.bias"], B, 8192, 100)
         # BatchNorm2d statistics written by the producing conv's epilogue (cgl_conv3x3_fwd_packed_stats):
         # one float64 partial buffer per BatchNorm, sized for its largest call (the D step's 2B rows)
         sc = lambda n, h, ci, co, st, up, grp: O.stat_chunks(n, h, h, ci, co, st, up, grp)
@@ -250,7 +254,7 @@ class ConvGanStep:
 
     def _g_forward(self):
         P, B2 = self.G.params, 2 * self.B
-        O.dense_fwd(self.z, P["l1.0.weight"], P["l1.0.bias"], self.h, B2, 100, 8192, wp=self.pk["l1"])
+        self.l1_fwd()
         O.nchw_to_nhwc(self.h, self.h0, B2, 128, 64)      # out.view(B, 128, 8, 8), model/lsgan.py:25
         O.conv3x3_fwd(self.h0, P["conv_blocks.1.weight"], P["conv_blocks.1.bias"], self.y1, B2, 8, 8, 128, 128, 1, 1,
                       wp=self.pk["c1f"], stats=self._stats("conv_blocks.2", 2))
@@ -346,7 +350,7 @@ class ConvGanStep:
                              128, 1, 1)
         O.conv3x3_bwd_data(self.dy1, P["conv_blocks.1.weight"], self.dh0, B, 8, 8, 128, 128, 1, 1, wp=self.pk["c1b"])
         O.nhwc_to_nchw(self.dh0, self.dh, B, 128, 64)
-        O.dense_bwd_weight(self.dh, self.z[B:], G["l1.0.weight"], G["l1.0.bias"], B, 100, 8192)
+        self.l1_wgrad()
 
     # ------------------------------------------------------------------ round
     def phase_a(self, real=None):

@@ -1567,6 +1567,63 @@ int cgl_linear_bwd_weight(const float* dY, const float* X, float* dW, float* db,
   return single_gemm(d, ws, wsb, (hipStream_t)stream);
 }
 
+// Prepared (graph-capturable) Linear GEMMs: the descriptor is written once into caller-owned device
+// memory (a synchronous copy at preparation), the launch then only reads it -- no per-call upload
+// and no stream synchronisation, unlike the cgl_linear_* ops above.
+int64_t cgl_linear_desc_bytes(void) { return (int64_t)((sizeof(CglGemmDesc) + 255) & ~size_t(255)); }
+
+int cgl_linear_prepare(int op, const float* A, const float* B, const float* bias, float* C, float* db, int M, int N,
+                       int K, int act, float slope, void* desc, CglLinearLaunch* launch) {
+  if (!A || !B || !C || !desc || !launch || M < 1 || N < 1 || K < 1 || act < 0 || act > 3 || !al16(desc))
+    return CGL_E_ARG;
+  CglGemmDesc d;
+  if (op == 0) {            // Y[M][N] = act(X[M][K] W[N][K]^T + b)
+    d = make_gemm(0, M, N, K);
+    d.a = rows(A, K);
+    d.a_vec = (K % 4 == 0) && al16(A);
+    d.b = rows(B, K);
+    d.b_vec = (K % 4 == 0) && al16(B);
+    d.bias = bias;
+    d.act = act;
+    d.slope = slope;
+    d.C = C;
+    d.ldc = N;
+  } else if (op == 1) {     // dX[M][K] = dY[M][N] W[N][K]
+    d = make_gemm(1, M, K, N);
+    d.a = rows(A, N);
+    d.a_vec = (N % 4 == 0) && al16(A);
+    d.b = rows(B, K);
+    d.C = C;
+    d.ldc = K;
+  } else if (op == 2) {     // dW[N][K] = dY[M][N]^T X[M][K], db[N] = column sums of dY
+    d = make_gemm(2, N, K + (db ? 1 : 0), M);
+    d.a = rows(A, N);
+    d.b = rows(B, K);
+    d.b_ones_col = db ? 1 : 0;
+    d.C = C;
+    d.ldc = K;
+    d.bias_out = db;
+  } else {
+    return CGL_E_ARG;
+  }
+  d.wg_begin = 0;
+  set_vec(d);
+  d.ksplit = 1;
+  HIPCHK(hipMemcpy(desc, &d, sizeof(d), hipMemcpyHostToDevice));
+  launch->tm = d.TM;
+  launch->grid = cgl_gemm_wgs(d);
+  launch->shmem = cgl_gemm_stage_bytes(d);
+  launch->flags = 0;
+  return 0;
+}
+
+int cgl_linear_launch(const void* desc, const CglLinearLaunch* launch, void* stream) {
+  if (!desc || !launch || launch->grid < 1 || (launch->tm != 1 && launch->tm != 2)) return CGL_E_ARG;
+  HIPCHK(gemm_lds_attr());
+  launch_gemm(launch->tm, launch->grid, launch->shmem, (hipStream_t)stream, (const CglGemmDesc*)desc, 1);
+  return (int)hipGetLastError();
+}
+
 int cgl_act_fwd(const float* X, int64_t n, int act, float slope, float* Y, void* stream) {
   if (!X || !Y || n < 0 || act < 0 || act > 3) return CGL_E_ARG;
   if (n == 0) return 0;

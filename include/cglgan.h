@@ -189,6 +189,18 @@ int cgl_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int s
 int cgl_normal_fill(float* out, int64_t n, unsigned long long seed, int round, int stream_id, void* stream);
 int64_t cgl_op_workspace_bytes(void);
 
+/* Prepared Linear GEMMs (graph-capturable; the fused conv round's nn.Linear layers,
+ * model/lsgan.py:8,92): cgl_linear_prepare writes the GEMM descriptor once into caller-owned
+ * device memory `desc` (cgl_linear_desc_bytes, 256-byte aligned; synchronous) and fills `launch`;
+ * cgl_linear_launch then runs it stream-ordered without any upload or synchronisation, reading the
+ * operand pointers given at preparation.  op 0: C[M][N] = act(A[M][K] B[N][K]^T + bias);
+ * op 1: C[M][K] = A[M][N] B[N][K]; op 2: C[N][K] = A[M][N]^T B[M][K] and db[N] = column sums of A. */
+typedef struct CglLinearLaunch { int tm, grid, shmem, flags; } CglLinearLaunch;
+int64_t cgl_linear_desc_bytes(void);
+int cgl_linear_prepare(int op, const float* A, const float* B, const float* bias, float* C, float* db, int M, int N,
+                       int K, int act, float slope, void* desc, CglLinearLaunch* launch);
+int cgl_linear_launch(const void* desc, const CglLinearLaunch* launch, void* stream);
+
 /* ---------------- conv GAN ops (model/lsgan.py) ----------------
  * Activations are NHWC (torch channels_last memory of the reference's NCHW tensors); weights are
  * the reference's nn.Conv2d layout [cout][cin][3][3].  No op allocates or synchronises: every
