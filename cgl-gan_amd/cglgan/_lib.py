@@ -35,7 +35,7 @@ EXPORTS = [
     "cgl_conv_packed_floats", "cgl_conv_pack_multi", "cgl_conv3x3_fwd_packed", "cgl_conv3x3_bwd_data_packed",
     "cgl_dense_fwd_packed", "cgl_dense_bwd_data_packed", "cgl_conv3x3_stat_chunks", "cgl_conv3x3_fwd_packed_stats",
     "cgl_bn2d_fwd_stats", "cgl_bn2d_stats_scratch_bytes", "cgl_linear_desc_bytes", "cgl_linear_prepare",
-    "cgl_linear_launch",
+    "cgl_linear_launch", "cgl_conv3x3_bwd_stat_chunks", "cgl_conv3x3_bwd_data_packed_stats", "cgl_bn2d_bwd_stats",
     # evaluation (CGLGAN/2DMG/main.py plot_2d KL score)
     "cgl_kl_score",
 ]
@@ -144,6 +144,9 @@ def _load():
         "cgl_bn2d_fwd_stats": (ci, [vp, ci, vp, ci, ci, ci, ci, vp, vp, cd, cd, vp, vp, ci, cf, vp, vp, vp, vp, vp, i64, vp]),
         "cgl_bn2d_stats_scratch_bytes": (i64, [ci, ci]),
         "cgl_linear_desc_bytes": (i64, []),
+        "cgl_conv3x3_bwd_stat_chunks": (i64, [ci] * 8),
+        "cgl_conv3x3_bwd_data_packed_stats": (ci, [vp, vp, vp] + [ci] * 8 + [vp, vp, vp, vp, cf, vp, i64, vp]),
+        "cgl_bn2d_bwd_stats": (ci, [vp, ci, vp, vp, vp, ci, ci, ci, ci, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, i64, vp]),
         "cgl_linear_prepare": (ci, [ci, vp, vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, P(LinearLaunch)]),
         "cgl_linear_launch": (ci, [vp, P(LinearLaunch), vp]),
         "cgl_dense_fwd_packed": (ci, [vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, i64, vp]),

@@ -58,9 +58,11 @@ def conv_ws_bytes(n, h, w, cin, cout, stride, up):
     return b
 
 
-def stat_chunks(n, h, wd, cin, cout, stride=1, up=0, groups=1):
-    """32-row statistic chunks of a forward's output (0: epilogue statistics unsupported)."""
-    return int(C.lib.cgl_conv3x3_stat_chunks(n, h, wd, cin, cout, stride, up, groups))
+def stat_chunks(n, h, wd, cin, cout, stride=1, up=0, groups=1, bwd=False):
+    """32-row statistic chunks of a forward's output, or (bwd) of an input gradient's output
+    (0: epilogue statistics unsupported)."""
+    fn = C.lib.cgl_conv3x3_bwd_stat_chunks if bwd else C.lib.cgl_conv3x3_stat_chunks
+    return int(fn(n, h, wd, cin, cout, stride, up, groups))
 
 
 def conv3x3_fwd(x, w, b, y, n, h, wd, cin, cout, stride=1, up=0, act=ACT_NONE, slope=0.2, drop=None, wp=None,
@@ -87,9 +89,21 @@ def conv3x3_fwd(x, w, b, y, n, h, wd, cin, cout, stride=1, up=0, act=ACT_NONE, s
     return y
 
 
-def conv3x3_bwd_data(dy, w, dx, n, h, wd, cin, cout, stride=1, up=0, wp=None):
+def conv3x3_bwd_data(dy, w, dx, n, h, wd, cin, cout, stride=1, up=0, wp=None, stats=None):
+    """``stats`` = (part, groups, x, post, mean, slope): also write the previous BatchNorm2d's backward
+    partials {sum g, sum g (x - mean)} per 32-row chunk of dx (g = dx * leaky'(post) if post) --
+    consumed by bn2d_bwd_stats; needs ``wp``."""
     _chk(dy, w, dx, wp)
     ws = workspace(conv_ws_bytes(n, h, wd, cin, cout, stride, up), dy.device)
+    if stats is not None:
+        part, groups, x, post, mean, slope = stats
+        _chk(x, post, mean)
+        if wp is None or not part.is_cuda or part.dtype != torch.float64:
+            raise RuntimeError("conv3x3_bwd_data(stats=...): needs packed weights and a float64 CUDA partial buffer")
+        C.check(C.lib.cgl_conv3x3_bwd_data_packed_stats(_p(dy), _p(wp), _p(dx), n, h, wd, cin, cout, stride, up,
+                                                        int(groups), _p(part), _p(x), _p(post), _p(mean), float(slope),
+                                                        _p(ws), ws.numel(), _s()), "cgl_conv3x3_bwd_data_packed_stats")
+        return dx
     if wp is not None:
         C.check(C.lib.cgl_conv3x3_bwd_data_packed(_p(dy), _p(w), _p(wp), _p(dx), n, h, wd, cin, cout, stride, up,
                                                   _p(ws), ws.numel(), _s()), "cgl_conv3x3_bwd_data_packed")
@@ -254,6 +268,17 @@ def bn2d_bwd(dy, x, n, hw, c, save_mean, save_invstd, gamma, dx, groups=1, post=
     C.check(C.lib.cgl_bn2d_bwd(_p(dy), _p(post), _p(x), n, hw, c, groups, _p(save_mean), _p(save_invstd), _p(gamma),
                                float(slope), _p(post_out), _p(drop), _p(dx), _p(dgamma), _p(dbeta), _p(ws), ws.numel(),
                                _s()), "cgl_bn2d_bwd")
+    return dx
+
+
+def bn2d_bwd_stats(part, dy, x, n, hw, c, save_mean, save_invstd, gamma, dx, groups=1, post=None, post_out=None,
+                   drop=None, dgamma=None, dbeta=None, slope=0.2, R=32):
+    """bn2d_bwd from the partials a conv3x3_bwd_data(stats=...) wrote: finalize + apply."""
+    _chk(dy, x, save_mean, save_invstd, gamma, dx, post, post_out, drop, dgamma, dbeta)
+    ws = workspace(bn2d_ws_bytes(n, hw, c, groups), dy.device)
+    C.check(C.lib.cgl_bn2d_bwd_stats(_p(part), int(R), _p(dy), _p(post), _p(x), n, hw, c, groups, _p(save_mean),
+                                     _p(save_invstd), _p(gamma), float(slope), _p(post_out), _p(drop), _p(dx),
+                                     _p(dgamma), _p(dbeta), _p(ws), ws.numel(), _s()), "cgl_bn2d_bwd_stats")
     return dx
 
 

@@ -215,6 +215,16 @@ class ConvGanStep:
             if n > 0:
                 self.st_part[k] = torch.zeros(n * geo[3] * 2, dtype=torch.float64, device=dev)
                 self.st_scratch[k] = O.bn2d_stats_scratch(geo[3], geo[6], dev)
+        # backward statistics: the same buffers (the forward's partials are consumed by then), written
+        # by the input-gradient conv that produces the BatchNorm's output gradient
+        self.bst_ok = {}
+        bgeo = {"conv_blocks.2": (B, 16, 128, 64, 1, 1, 1)}     # conv_blocks.5 input gradient -> da1
+        for k in range(2, 4):
+            ck, _, ci, co, hw = D_CONVS[k]
+            bgeo[D_CONVS[k - 1][1]] = (B2, hw, ci, co, 2, 0, 2)   # conv k input gradient -> dr[k - 1]
+        for key, (n, h, ci, co, st, up, grp) in bgeo.items():
+            nb = O.stat_chunks(n, h, h, ci, co, st, up, grp, bwd=True)
+            self.bst_ok[key] = key in self.st_part and 0 < nb * ci * 2 <= self.st_part[key].numel()
         # sampler over a device-resident real shard [n, 1024] (DataLoader(shuffle=True), capgan.py:282)
         self.data = data
         self._perm, self._pos = None, 0
@@ -308,6 +318,7 @@ class ConvGanStep:
 
     def _d_backward(self, x, n, groups, masks, wgrad, dx):
         P, G = self.D.params, self.D.grads
+        bst = set()     # BatchNorms whose backward partials the previous input-gradient conv wrote
         O.dense_bwd_data(self.dv, P["adv_layer.weight"], self.dflat, n, 512, 1, wp=self.pk["advb"])
         if wgrad:
             O.dense_bwd_weight(self.dv, self.flat, G["adv_layer.weight"], G["adv_layer.bias"], n, 512, 1)
@@ -317,17 +328,26 @@ class ConvGanStep:
             ho = hw // 2
             if bk:
                 sm, si = self.d_save[bk]
-                O.bn2d_bwd(self.dr[k], self.q[k], n, ho * ho, co, sm, si, P[bk + ".weight"], self.dc[k], groups=groups,
-                           post_out=self.q[k], drop=masks[k], dgamma=G[bk + ".weight"] if wgrad else None,
-                           dbeta=G[bk + ".bias"] if wgrad else None, slope=SLOPE)
+                kw = dict(groups=groups, post_out=self.q[k], drop=masks[k], dgamma=G[bk + ".weight"] if wgrad else None,
+                          dbeta=G[bk + ".bias"] if wgrad else None, slope=SLOPE)
+                if bk in bst:
+                    O.bn2d_bwd_stats(self.st_part[bk], self.dr[k], self.q[k], n, ho * ho, co, sm, si, P[bk + ".weight"],
+                                     self.dc[k], **kw)
+                else:
+                    O.bn2d_bwd(self.dr[k], self.q[k], n, ho * ho, co, sm, si, P[bk + ".weight"], self.dc[k], **kw)
             else:
                 O.act_drop_bwd(self.dq1, self.q[0], masks[0], n, ho * ho, co, self.dc[0], slope=SLOPE)
             inp = x if k == 0 else (self.q[0] if k == 1 else self.r[k - 1])
             if wgrad:
                 O.conv3x3_bwd_weight(self.dc[k], inp, G[ck + ".weight"], G[ck + ".bias"], n, hw, hw, ci, co, 2, 0)
             if k > 0:
+                pbk = D_CONVS[k - 1][1]
+                st = None
+                if k > 1 and self.bst_ok.get(pbk):
+                    st = (self.st_part[pbk], groups, self.q[k - 1], None, self.d_save[pbk][0], SLOPE)
+                    bst.add(pbk)
                 O.conv3x3_bwd_data(self.dc[k], P[ck + ".weight"], self.dr[k - 1] if k > 1 else self.dq1, n, hw, hw, ci, co,
-                                   2, 0, wp=self.pk[ck + "b"])
+                                   2, 0, wp=self.pk[ck + "b"], stats=st)
             elif dx is not None:
                 O.conv3x3_bwd_data(self.dc[0], P[ck + ".weight"], dx, n, hw, hw, ci, co, 2, 0, wp=self.pk[ck + "b"])
 
@@ -342,10 +362,18 @@ class ConvGanStep:
                    post=self.a2[B:], dgamma=G["conv_blocks.6.weight"], dbeta=G["conv_blocks.6.bias"], slope=SLOPE)
         O.conv3x3_bwd_weight(self.dy2, self.a1[B:], G["conv_blocks.5.weight"], G["conv_blocks.5.bias"], B, 16, 16, 128,
                              64, 1, 1)
-        O.conv3x3_bwd_data(self.dy2, P["conv_blocks.5.weight"], self.da1, B, 16, 16, 128, 64, 1, 1, wp=self.pk["c5b"])
         sm, si = self.g_save["conv_blocks.2"]
-        O.bn2d_bwd(self.da1, self.y1[B:], B, 256, 128, sm[1], si[1], P["conv_blocks.2.weight"], self.dy1,
-                   post=self.a1[B:], dgamma=G["conv_blocks.2.weight"], dbeta=G["conv_blocks.2.bias"], slope=SLOPE)
+        st = None
+        if self.bst_ok.get("conv_blocks.2"):
+            st = (self.st_part["conv_blocks.2"], 1, self.y1[B:], self.a1[B:], sm[1], SLOPE)
+        O.conv3x3_bwd_data(self.dy2, P["conv_blocks.5.weight"], self.da1, B, 16, 16, 128, 64, 1, 1, wp=self.pk["c5b"],
+                           stats=st)
+        kw = dict(post=self.a1[B:], dgamma=G["conv_blocks.2.weight"], dbeta=G["conv_blocks.2.bias"], slope=SLOPE)
+        if st is not None:
+            O.bn2d_bwd_stats(self.st_part["conv_blocks.2"], self.da1, self.y1[B:], B, 256, 128, sm[1], si[1],
+                             P["conv_blocks.2.weight"], self.dy1, **kw)
+        else:
+            O.bn2d_bwd(self.da1, self.y1[B:], B, 256, 128, sm[1], si[1], P["conv_blocks.2.weight"], self.dy1, **kw)
         O.conv3x3_bwd_weight(self.dy1, self.h0[B:], G["conv_blocks.1.weight"], G["conv_blocks.1.bias"], B, 8, 8, 128,
                              128, 1, 1)
         O.conv3x3_bwd_data(self.dy1, P["conv_blocks.1.weight"], self.dh0, B, 8, 8, 128, 128, 1, 1, wp=self.pk["c1b"])

@@ -65,8 +65,13 @@ struct CglConvLaunch {
   float slope;
   const float* drop;         // Dropout2d scale per (image, channel) [img][ldy], or null
   int wbias;                 // weight gradient: im2col column K is the constant 1 (bias gradient)
-  double* st_part;           // forward: per-(32-row chunk, channel) {sum, M2} of the stored output
+  double* st_part;           // per-(32-row chunk, channel) BatchNorm2d partials of the stored output:
   int st_cpg;                // 32-row chunks per group (all problems)
+  int st_mode;               //   0 {sum, M2} (forward statistics), 1 {sum g, sum g (x - mean)} with
+  float st_slope;            //   g = the stored dY (* leaky'(post)) (backward statistics)
+  const float* st_x;         // mode 1: the BatchNorm input x, the post-activation (or null) and the
+  const float* st_post;      // saved per-call mean [groups][N], all at the stored tensor's positions
+  const float* st_mean;
 };
 
 typedef const CGL_AS4 CglConvLaunch* CglKL;
@@ -333,7 +338,50 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
     // BatchNorm2d statistics of the stored values (the next op's BatchNorm, cgl_bn2d_fwd_stats): per
     // 32-row chunk and channel {sum, M2 about the chunk mean} in double, the two lane halves
     // combined by one xor-32 exchange (fixed order); the chunks of a forward call are contiguous
-    if (L->st_part) {
+    int imb, remb, oyb, oxb;
+    cgl_divmod(rowb, hw, inv_hw, imb, remb);
+    cgl_divmod(remb, OW, inv_ow, oyb, oxb);
+    const int pixb = __builtin_amdgcn_readfirstlane((imb * YH + oyb * osy + ooy) * YW + oxb * osx + oox);
+    if (L->st_part && L->st_mode == 1) {
+      // backward statistics (cgl_bn2d_bwd_stats): x and post loaded at the stored positions through
+      // buffer resources of the same base (every row of a statistics launch is valid)
+      const int g = rowb / P->st_gr;
+      const long chunk = (long)g * L->st_cpg + P->st_off + (rowb - g * P->st_gr) / 32;
+      const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(L->st_x) + (long)pixb * ldy, (short)0,
+                                                        0x7fffffff, 0x00020000);
+      const float* pp = L->st_post ? L->st_post : L->st_x;
+      const auto rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(pp) + (long)pixb * ldy, (short)0,
+                                                        0x7fffffff, 0x00020000);
+      const float psl = L->st_slope;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + 32 * j + li;
+        const int colc = min(col, N - 1);
+        const float mu = gld(L->st_mean + (long)g * N + colc);
+        float xv[16], pv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int off = ((pix[r] - pixb) * ldy + colc) * 4;
+          xv[r] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, off, 0, 0));
+          pv[r] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rp, off, 0, 0));
+        }
+        double S = 0.0, D = 0.0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float y = acc[i][j][r];
+          const float gg = L->st_post ? (pv[r] > 0.f ? y : y * psl) : y;
+          S += (double)gg;
+          D += (double)(gg * (xv[r] - mu));
+        }
+        S += __shfl_xor(S, 32);
+        D += __shfl_xor(D, 32);
+        if (lh == 0 && col < N) {
+          double* dst = L->st_part + (chunk * N + col) * 2;
+          dst[0] = S;
+          dst[1] = D;
+        }
+      }
+    } else if (L->st_part) {
       const int g = rowb / P->st_gr;
       const long chunk = (long)g * L->st_cpg + P->st_off + (rowb - g * P->st_gr) / 32;
 #pragma unroll
@@ -361,10 +409,6 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
     // stores through a buffer resource based at the block's first output pixel (output pixels grow
     // with the row, so every offset is >= 0): rows past M / columns past N get an out-of-range
     // offset and are dropped by the hardware -- no per-element branches
-    int imb, remb, oyb, oxb;
-    cgl_divmod(rowb, hw, inv_hw, imb, remb);
-    cgl_divmod(remb, OW, inv_ow, oyb, oxb);
-    const int pixb = __builtin_amdgcn_readfirstlane((imb * YH + oyb * osy + ooy) * YW + oxb * osx + oox);
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(Y + (long)pixb * ldy, (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -990,6 +1034,124 @@ __global__ __launch_bounds__(256) void cgl_conv_bwd_n1(const float* __restrict__
     acc[3] = fmaf(dv[t], w[t][3], acc[3]);
   }
   if (p < npix) *(gf4p)(dX + (long)p * (4 * C4) + 4 * q) = acc;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// One-input-channel 3x3 convolutions on the vector ALUs (the discriminator's Conv2d(1, 16, 3, 2, 1),
+// model/lsgan.py:78 on the 32x32 image): 9 MACs per output element are far too few for an MFMA
+// tile (the implicit GEMM decoded its k index per element and ran 4-6x slower than this).
+//   forward: one thread per output pixel, the 9 input taps in registers, the weights in LDS
+//   (broadcast reads), bias + activation + Dropout2d scale fused, cout floats stored contiguously;
+//   weight gradient: thread (channel, pixel lane) accumulates its channel's 9 taps + bias over a
+//   pixel slice, the block's lanes are summed through LDS in a fixed order into per-block partials,
+//   and cgl_conv_c1_wgrad_fin sums the blocks in order (double) into dW [cout][1][3][3] and db.
+struct CglC1Args {
+  const float* X; const float* W; int wst;   // weights: row co at W + co * wst, 9 taps
+  const float* bias; float* Y; const float* drop;
+  const float* dY; float* part; float* dW; float* db;
+  int n, h, w, ho, wo, cout, stride, act, nblk, chunk;
+  float slope;
+};
+
+__global__ __launch_bounds__(256) void cgl_conv_c1_fwd(CglC1Args a) {
+  __shared__ float sw[64 * 9], sb[64];
+  const int tid = threadIdx.x, cout = a.cout;
+  for (int e = tid; e < cout * 9; e += 256) sw[e] = gld(a.W + (e / 9) * a.wst + e % 9);
+  if (tid < cout) sb[tid] = a.bias ? gld(a.bias + tid) : 0.f;
+  __syncthreads();
+  const int hw = a.ho * a.wo;
+  const long p = (long)blockIdx.x * 256 + tid;
+  if (p >= (long)a.n * hw) return;
+  const int img = (int)(p / hw), r = (int)(p - (long)img * hw), oy = r / a.wo, ox = r - oy * a.wo;
+  float xv[9];
+  const float* xi = a.X + (long)img * a.h * a.w;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int iy = oy * a.stride + t / 3 - 1, ix = ox * a.stride + t % 3 - 1;
+    const bool ok = (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+    const float v = gld(xi + min(max(iy, 0), a.h - 1) * a.w + min(max(ix, 0), a.w - 1));
+    xv[t] = ok ? v : 0.f;
+  }
+  for (int c4 = 0; c4 < cout; c4 += 4) {
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = sb[c4 + j];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) v = fmaf(xv[t], sw[(c4 + j) * 9 + t], v);
+      if (a.act == CGL_EPI_ACT_LEAKY) v = v > 0.f ? v : v * a.slope;
+      o[j] = v;
+    }
+    if (a.drop) {
+      const f32x4 dm = *(gcf4p)(a.drop + (long)img * cout + c4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] *= dm[j];
+    }
+    *(gf4p)(a.Y + p * cout + c4) = o;
+  }
+}
+
+#define CGL_C1_PPT 8
+__global__ __launch_bounds__(256) void cgl_conv_c1_wgrad(CglC1Args a) {
+  __shared__ float red[256 * 10];
+  const int tid = threadIdx.x, cout = a.cout, lanes = 256 / cout;
+  const int co = tid % cout, lj = tid / cout;
+  const int hw = a.ho * a.wo;
+  const long npix = (long)a.n * hw;
+  const long p0 = (long)blockIdx.x * a.chunk, p1 = min(p0 + a.chunk, npix);
+  float acc[10];
+#pragma unroll
+  for (int t = 0; t < 10; ++t) acc[t] = 0.f;
+  // CGL_C1_PPT pixels per thread per pass, every load of the pass issued before the first use
+  for (long pb = p0 + lj; pb < p1; pb += (long)CGL_C1_PPT * lanes) {
+    float dy[CGL_C1_PPT], xv[CGL_C1_PPT][9];
+#pragma unroll
+    for (int u = 0; u < CGL_C1_PPT; ++u) {
+      const long p = min(pb + (long)u * lanes, p1 - 1);
+      const int img = (int)(p / hw), r = (int)(p - (long)img * hw), oy = r / a.wo, ox = r - oy * a.wo;
+      dy[u] = pb + (long)u * lanes < p1 ? gld(a.dY + p * cout + co) : 0.f;
+      const float* xi = a.X + (long)img * a.h * a.w;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int iy = oy * a.stride + t / 3 - 1, ix = ox * a.stride + t % 3 - 1;
+        const bool ok = (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+        const float v = gld(xi + min(max(iy, 0), a.h - 1) * a.w + min(max(ix, 0), a.w - 1));
+        xv[u][t] = ok ? v : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < CGL_C1_PPT; ++u) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) acc[t] = fmaf(dy[u], xv[u][t], acc[t]);
+      acc[9] += dy[u];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 10; ++t) red[t * 256 + tid] = acc[t];
+  __syncthreads();
+  if (tid < cout * 10) {        // (channel, tap) = (tid % cout, tid / cout): lanes summed in order
+    const int c = tid % cout, t = tid / cout;
+    float v = 0.f;
+    for (int l = 0; l < lanes; ++l) v += red[t * 256 + l * cout + c];
+    a.part[(long)blockIdx.x * cout * 10 + t * cout + c] = v;
+  }
+}
+
+__device__ __forceinline__ double cgl_block_sum_d(double x, double* red);
+
+// one workgroup per (tap, channel) output: blocks b = thread, thread + 256, ... summed in order,
+// then the fixed-order block sum
+__global__ __launch_bounds__(256) void cgl_conv_c1_wgrad_fin(CglC1Args a) {
+  __shared__ double red[4];
+  const int o = blockIdx.x, cout = a.cout, tid = threadIdx.x;
+  double v = 0.0;
+  for (int b = tid; b < a.nblk; b += 256) v += (double)gld(a.part + (long)b * cout * 10 + o);
+  v = cgl_block_sum_d(v, red);
+  if (tid == 0) {
+    const int c = o % cout, t = o / cout;
+    if (t < 9) gst(a.dW + c * 9 + t, (float)v);
+    else if (a.db) gst(a.db + c, (float)v);
   }
 }
 
@@ -2127,7 +2289,8 @@ WgradPlan wgrad_plan(const ConvGeom& g, bool bias = true) {
     tiles_total += P.tiles_m * P.tiles_n;
     nk_total += (int64_t)P.N * P.Kp;
   }
-  int s = std::max(1, 2048 / std::max(1, tiles_total));
+  static const int wg_units = getenv("CGL_WG_UNITS") ? atoi(getenv("CGL_WG_UNITS")) : 2048;
+  int s = std::max(1, wg_units / std::max(1, tiles_total));
   s = (int)std::min<int64_t>(s, std::max<int64_t>(1, (8 << 20) / std::max<int64_t>(1, nk_total)));
   w.part_floats = 0;
   for (int i = 0; i < w.np; ++i) {
@@ -2204,8 +2367,10 @@ bool n1_ok(const CglConvProb* P, int np) {
   return true;
 }
 
+struct StatBwd { const float* x = nullptr; const float* post = nullptr; const float* mean = nullptr; float slope = 0.f; };
+
 int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float slope, const float* drop,
-                    hipStream_t s, double* st_part = nullptr, int st_cpg = 0) {
+                    hipStream_t s, double* st_part = nullptr, int st_cpg = 0, const StatBwd* sb = nullptr) {
   const int N = P[0].N;
   CglConvLaunch L;
   std::memset(&L, 0, sizeof(L));
@@ -2216,6 +2381,13 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
   L.drop = drop;
   L.st_part = st_part;
   L.st_cpg = st_cpg;
+  if (sb) {
+    L.st_mode = 1;
+    L.st_x = sb->x;
+    L.st_post = sb->post;
+    L.st_mean = sb->mean;
+    L.st_slope = sb->slope;
+  }
   if (st_part && N == 1) return CGL_E_ARG;   // statistics only from the MFMA kernel
   if (N == 1 && np == 1 && P[0].Ty == 3 && P[0].Tx == 3 && P[0].isy == 1 && P[0].isx == 1 && P[0].ish == 0 &&
       P[0].osy == 1 && P[0].osx == 1 && P[0].dy[0] == -1 && P[0].dx[0] == -1 && P[0].Cin % 4 == 0 &&
@@ -2314,10 +2486,11 @@ namespace {
 // BatchNorm statistics in the forward epilogue: supported when every problem's rows per forward
 // call are whole 32-row chunks and the launch takes the MFMA kernel; returns the chunks per call
 // (0: unsupported)
-int stat_chunks_per_group(const ConvGeom& g, int groups) {
-  if (groups < 1 || g.n % groups || g.cout < 32) return 0;
+int stat_chunks_per_group(const ConvGeom& g, int groups, int bwd = 0) {
+  if (groups < 1 || g.n % groups || (bwd ? g.cin : g.cout) < 32) return 0;
+  if (bwd && g.cout == 1) return 0;   // the vector one-output-channel input gradient has no epilogue
   CglConvProb P[CGL_CONV_MAXP];
-  const int np = fwd_probs(g, P);
+  const int np = bwd ? bwd_probs(g, P) : fwd_probs(g, P);
   int cpg = 0;
   for (int i = 0; i < np; ++i) {
     const long gr = (long)(g.n / groups) * P[i].OH * P[i].OW;
@@ -2325,6 +2498,11 @@ int stat_chunks_per_group(const ConvGeom& g, int groups) {
     cpg += (int)(gr / 32);
   }
   return cpg;
+}
+
+// the vector one-input-channel kernels (cgl_conv_c1_*) apply
+bool c1_ok(const ConvGeom& g) {
+  return g.cin == 1 && g.ks == 3 && !g.up && g.cout % 4 == 0 && g.cout <= 16 && 256 % g.cout == 0;
 }
 
 int conv_fwd_impl(const ConvGeom& g, const float* X, const float* W, const float* bias, float* Y, int act, float slope,
@@ -2349,6 +2527,18 @@ int conv_fwd_impl(const ConvGeom& g, const float* X, const float* W, const float
     P[i].X = X;
     P[i].Y = Y;
   }
+  if (c1_ok(g) && !st_part && act != CGL_EPI_ACT_TANH && act != CGL_EPI_ACT_SIGMOID && al16(Y) &&
+      (!drop || al16(drop))) {
+    // the packed forward operand of a Cin = 1 conv is [cout][16] (9 taps, zero padded)
+    CglC1Args a;
+    std::memset(&a, 0, sizeof(a));
+    a.X = X; a.W = Wp ? Wp : W; a.wst = Wp ? 16 : 9; a.bias = bias; a.Y = Y; a.drop = drop;
+    a.n = g.n; a.h = g.h; a.w = g.w; a.ho = g.ho; a.wo = g.wo; a.cout = g.cout; a.stride = g.stride;
+    a.act = act; a.slope = slope;
+    const long npix = (long)g.n * g.ho * g.wo;
+    hipLaunchKernelGGL(cgl_conv_c1_fwd, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, a);
+    return (int)hipGetLastError();
+  }
   int rc;
   if (Wp) pack_layout(P, np, Wp);
   else if ((rc = launch_pack(W, g, 0, P, np, (float*)ws, s))) return rc;
@@ -2356,11 +2546,17 @@ int conv_fwd_impl(const ConvGeom& g, const float* X, const float* W, const float
 }
 
 int conv_bwd_data_impl(const ConvGeom& g, const float* dY, const float* W, float* dX, void* ws, int64_t wsb,
-                       hipStream_t s, const float* Wp = nullptr) {
+                       hipStream_t s, const float* Wp = nullptr, double* st_part = nullptr, int st_groups = 1,
+                       const StatBwd* sb = nullptr) {
   if (!dY || !(W || Wp) || !dX || !ws || !al16(ws) || (Wp && !al16(Wp))) return CGL_E_ARG;
   if (wsb < conv_ws_bytes(g)) return CGL_E_SIZE;
   if ((g.cout % 4 == 0) && !al16(dY)) return CGL_E_ARG;
-  if (W && g.cout == 1 && g.cin == 64 && g.ks == 3 && g.stride == 1 && !g.up && al16(dX) &&
+  int cpg = 0;
+  if (st_part) {
+    if (!sb || !sb->x || !sb->mean || !(cpg = stat_chunks_per_group(g, st_groups, 1)) || ((uintptr_t)st_part & 15))
+      return CGL_E_ARG;
+  }
+  if (!st_part && W && g.cout == 1 && g.cin == 64 && g.ks == 3 && g.stride == 1 && !g.up && al16(dX) &&
       (int64_t)g.n * g.h * g.w < (int64_t)1 << 30) {
     const int npix = g.n * g.h * g.w;
     hipLaunchKernelGGL((cgl_conv_bwd_n1<16>), dim3((npix + 16 * CGL_BN1_PPT - 1) / (16 * CGL_BN1_PPT)), dim3(256), 0, s, dY, W, dX, npix, g.h, g.w);
@@ -2368,14 +2564,20 @@ int conv_bwd_data_impl(const ConvGeom& g, const float* dY, const float* W, float
   }
   CglConvProb P[CGL_CONV_MAXP];
   const int np = bwd_probs(g, P);
+  int off = 0;
   for (int i = 0; i < np; ++i) {
     P[i].X = dY;
     P[i].Y = dX;
+    if (st_part) {
+      P[i].st_gr = (g.n / st_groups) * P[i].OH * P[i].OW;
+      P[i].st_off = off;
+      off += P[i].st_gr / 32;
+    }
   }
   int rc;
   if (Wp) pack_layout(P, np, Wp);
   else if ((rc = launch_pack(W, g, 1, P, np, (float*)ws, s))) return rc;
-  return launch_conv_mma(P, np, nullptr, CGL_EPI_ACT_NONE, 0.f, nullptr, s);
+  return launch_conv_mma(P, np, nullptr, CGL_EPI_ACT_NONE, 0.f, nullptr, s, st_part, cpg, st_part ? sb : nullptr);
 }
 
 // the ROW fast path of cgl_conv_wgrad_body: whole 8-pixel row segments in every problem
@@ -2390,6 +2592,20 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
   if (!dY || !X || !dW || !ws || !al16(ws)) return CGL_E_ARG;
   if (wsb < conv_ws_bytes(g)) return CGL_E_SIZE;
   if (g.cout > CGL_ZERO_PAGE || g.cin > CGL_ZERO_PAGE) return CGL_E_ARG;   // cgl_zero_page bound
+  if (c1_ok(g)) {
+    const long npix = (long)g.n * g.ho * g.wo;
+    CglC1Args a;
+    std::memset(&a, 0, sizeof(a));
+    a.X = X; a.dY = dY; a.dW = dW; a.db = db;
+    a.n = g.n; a.h = g.h; a.w = g.w; a.ho = g.ho; a.wo = g.wo; a.cout = g.cout; a.stride = g.stride;
+    a.chunk = 128;
+    a.nblk = (int)((npix + a.chunk - 1) / a.chunk);
+    if ((int64_t)a.nblk * g.cout * 10 * 4 > wsb) return CGL_E_SIZE;
+    a.part = (float*)ws;
+    hipLaunchKernelGGL(cgl_conv_c1_wgrad, dim3(a.nblk), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(cgl_conv_c1_wgrad_fin, dim3(g.cout * 10), dim3(256), 0, s, a);
+    return (int)hipGetLastError();
+  }
   WgradPlan pl = wgrad_plan(g, db != nullptr);
   const bool bias_col = db && wgrad_bias_col(g, pl.P, pl.np);
   CglConvLaunch L;
@@ -2612,6 +2828,26 @@ int cgl_conv3x3_fwd_packed_stats(const float* X, const float* Wp, const float* b
   return conv_fwd_impl(g, X, nullptr, bias, Y, act, slope, drop, ws, wsb, (hipStream_t)stream, Wp, part, groups);
 }
 
+int64_t cgl_conv3x3_bwd_stat_chunks(int n, int h, int w, int cin, int cout, int stride, int up, int groups) {
+  ConvGeom g;
+  const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
+  if (rc) return rc;
+  return (int64_t)stat_chunks_per_group(g, groups, 1) * groups;
+}
+
+int cgl_conv3x3_bwd_data_packed_stats(const float* dY, const float* Wp, float* dX, int n, int h, int w, int cin,
+                                      int cout, int stride, int up, int groups, double* part, const float* bn_x,
+                                      const float* bn_post, const float* bn_mean, float slope, void* ws, int64_t wsb,
+                                      void* stream) {
+  ConvGeom g;
+  const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
+  if (rc) return rc;
+  if (!Wp || !part) return CGL_E_ARG;
+  StatBwd sb;
+  sb.x = bn_x; sb.post = bn_post; sb.mean = bn_mean; sb.slope = slope;
+  return conv_bwd_data_impl(g, dY, nullptr, dX, ws, wsb, (hipStream_t)stream, Wp, part, groups, &sb);
+}
+
 int cgl_conv3x3_bwd_data_packed(const float* dY, const float* W, const float* Wp, float* dX, int n, int h, int w,
                                 int cin, int cout, int stride, int up, void* ws, int64_t wsb, void* stream) {
   ConvGeom g;
@@ -2737,6 +2973,39 @@ int cgl_bn2d_fwd_stats(const double* part, int R, const float* X, int n, int hw,
   std::memset(&e, 0, sizeof(e));
   e.mode = 0; e.rows = (int)rows; e.C = C; e.gr = (int)gr; e.hw = hw; e.act = act; e.slope = slope;
   e.X = X; e.coef0 = c0; e.coef1 = c1; e.out = Y;
+  const long n4 = rows * C / 4;
+  hipLaunchKernelGGL(cgl_eltwise, dim3((unsigned)std::min<long>((n4 + 255) / 256, 8192)), dim3(256), 0, s, e);
+  return (int)hipGetLastError();
+}
+
+int cgl_bn2d_bwd_stats(const double* part, int R, const float* dY, const float* post, const float* X, int n, int hw,
+                       int C, int groups, const float* save_mean, const float* save_invstd, const float* gamma,
+                       float slope, const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta,
+                       void* ws, int64_t wsb, void* stream) {
+  if (!part || !dY || !X || !save_mean || !save_invstd || !gamma || !dX || !ws || !al16(ws)) return CGL_E_ARG;
+  if (!al16(dY) || !al16(X) || !al16(dX) || (post && !al16(post)) || (post_out && !al16(post_out))) return CGL_E_ARG;
+  if (!al16(save_mean) || !al16(save_invstd) || !al16(gamma) || (drop && !al16(drop))) return CGL_E_ARG;
+  if (n < 1 || hw < 1 || C % 4 != 0 || !pow2_le256(C) || groups < 1 || n % groups) return CGL_E_ARG;
+  const int64_t gr = (int64_t)(n / groups) * hw;
+  if (R < 1 || gr % R) return CGL_E_ARG;
+  if (wsb < cgl_bn2d_workspace_bytes(n, hw, C, groups)) return CGL_E_SIZE;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t rows = (int64_t)n * hw;
+  const int R0 = chan_chunk(gr);
+  float* coef = (float*)((char*)ws + al256((rows / R0) * C * 16));
+  float* c0 = coef;
+  float* c1 = coef + al256((int64_t)groups * C * 4) / 4;
+  CglBnFinArgs f;
+  std::memset(&f, 0, sizeof(f));
+  f.part = part; f.C = C; f.groups = groups; f.chunks_per_group = (int)(gr / R); f.R = R; f.gr = (int)gr;
+  f.mode = 1; f.gamma = gamma; f.save_invstd = const_cast<float*>(save_invstd); f.coef0 = c0; f.coef1 = c1;
+  f.dgamma = dgamma; f.dbeta = dbeta;
+  hipLaunchKernelGGL(cgl_bn_finalize, dim3(C), dim3(256), 0, s, f);
+  CglEltArgs e;
+  std::memset(&e, 0, sizeof(e));
+  e.mode = 1; e.rows = (int)rows; e.C = C; e.gr = (int)gr; e.hw = hw; e.slope = slope;
+  e.X = X; e.dY = dY; e.post = post; e.coef0 = c0; e.coef1 = c1; e.mean = save_mean; e.invstd = save_invstd;
+  e.gamma = gamma; e.post_out = post_out; e.drop = drop; e.out = dX;
   const long n4 = rows * C / 4;
   hipLaunchKernelGGL(cgl_eltwise, dim3((unsigned)std::min<long>((n4 + 255) / 256, 8192)), dim3(256), 0, s, e);
   return (int)hipGetLastError();

@@ -268,6 +268,16 @@ int64_t cgl_conv3x3_stat_chunks(int n, int h, int w, int cin, int cout, int stri
 int cgl_conv3x3_fwd_packed_stats(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w,
                                  int cin, int cout, int stride, int up, int act, float slope, const float* drop,
                                  int groups, double* part, void* workspace, int64_t ws_bytes, void* stream);
+/* The input gradient with the previous BatchNorm2d's backward statistics computed in its epilogue:
+ * part [groups * chunks][cin][2] = {sum g, sum g (x - mean)} per 32-row chunk of dX, g = dX (*
+ * leaky'(bn_post) when bn_post is given), x = bn_x (the BatchNorm input) and mean = bn_mean
+ * [groups][cin] (the saved per-call mean), all at dX's positions.  Consumed by cgl_bn2d_bwd_stats.
+ * cgl_conv3x3_bwd_stat_chunks: chunk count (0: unsupported). */
+int64_t cgl_conv3x3_bwd_stat_chunks(int n, int h, int w, int cin, int cout, int stride, int up, int groups);
+int cgl_conv3x3_bwd_data_packed_stats(const float* dY, const float* Wp, float* dX, int n, int h, int w, int cin,
+                                      int cout, int stride, int up, int groups, double* part, const float* bn_x,
+                                      const float* bn_post, const float* bn_mean, float slope, void* workspace,
+                                      int64_t ws_bytes, void* stream);
 int cgl_dense_fwd_packed(const float* X, const float* Wp, const float* b, float* Y, int M, int K, int N, int act,
                          float slope, void* workspace, int64_t ws_bytes, void* stream);
 int cgl_dense_bwd_data_packed(const float* dY, const float* Wp, float* dX, int M, int K, int N, void* workspace,
@@ -293,6 +303,11 @@ int64_t cgl_bn2d_stats_scratch_bytes(int C, int groups);
 int cgl_bn2d_fwd_stats(const double* part, int R, const float* X, int n, int hw, int C, int groups, const float* gamma,
                        const float* beta, double eps, double momentum, float* running_mean, float* running_var,
                        int act, float slope, float* Y, float* save_mean, float* save_invstd, void* scratch,
+                       void* workspace, int64_t ws_bytes, void* stream);
+/* cgl_bn2d_bwd from backward partials already computed (cgl_conv3x3_bwd_data_packed_stats, R = 32). */
+int cgl_bn2d_bwd_stats(const double* part, int R, const float* dY, const float* post, const float* X, int n, int hw,
+                       int C, int groups, const float* save_mean, const float* save_invstd, const float* gamma,
+                       float slope, const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta,
                        void* workspace, int64_t ws_bytes, void* stream);
 int cgl_bn2d_bwd(const float* dY, const float* post, const float* X, int n, int hw, int C, int groups,
                  const float* save_mean, const float* save_invstd, const float* gamma, float slope,
