@@ -1572,6 +1572,7 @@ struct CglBnFinArgs {
   float* save_mean; float* save_invstd;     // [groups][C]
   float* coef0; float* coef1;               // [groups][C]: fwd scale, shift; bwd gm, k
   float* dgamma; float* dbeta;              // bwd, or bias out (mode 2: dgamma)
+  int nocache;                              // A/B switch: stream the partials twice (CGL_FIN_NOCACHE)
 };
 
 __device__ __forceinline__ double cgl_wave_sum_d(double x) {
@@ -1607,12 +1608,52 @@ __device__ __forceinline__ double cgl_fin_sum(const double* part, long q0, int c
   return t;
 }
 
+// This thread's chunk pairs of up to 2 groups x NI chunks (chunk q0_g + lane + 256 i), all loaded
+// up front: the second pass over the partials (and every group) then costs no memory round trip.
+// sum(g, fn) accumulates in the same chunk order as cgl_fin_sum.
+template <int NI>
+struct CglFinCache {
+  typedef double f64x2 __attribute__((ext_vector_type(2)));
+  f64x2 v[2][NI];
+  int cnt, lane;
+  __device__ __forceinline__ void load(const double* part, long gstride, int groups, int cnt_, int C, int c,
+                                       int lane_, long q0 = 0) {
+    typedef const CGL_GLOBAL f64x2* gcd2p;
+    cnt = cnt_;
+    lane = lane_;
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int q = min(lane + 256 * i, cnt - 1);
+        const int gg = min(g, groups - 1);
+        v[g][i] = *(gcd2p)(part + ((q0 + gg * gstride + q) * C + c) * 2);
+      }
+  }
+  template <class Fn>
+  __device__ __forceinline__ double sum(int g, Fn fn) const {
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      if (lane + 256 * i < cnt) t += fn(v[g][i]);
+    return t;
+  }
+};
+
 __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
   __shared__ double red[4];
   const int lane = threadIdx.x;          // thread index within the channel's workgroup
   const int c = blockIdx.x;
   const int C = a.C;
   const double* part = a.part;
+  // <= 1024 chunks per call and <= 2 calls: every partial this thread needs is loaded once, up front
+  CglFinCache<4> fc;
+  const bool cached = a.chunks_per_group <= 1024 && a.groups <= 2 && a.mode != 2 && (a.mode == 1 || a.train) &&
+                      !a.nocache;
+  if (cached) fc.load(part, a.chunks_per_group, a.groups, a.chunks_per_group, C, c, lane);
+  auto gsum = [&](int g, auto fn) -> double {
+    return cached ? fc.sum(g, fn) : cgl_fin_sum(part, (long)g * a.chunks_per_group, a.chunks_per_group, C, c, lane, fn);
+  };
   if (a.mode == 2) {
     const int nch = a.groups * a.chunks_per_group;
     double t = cgl_fin_sum(part, 0, nch, C, c, lane, [](auto v) { return (double)v[0]; });
@@ -1621,12 +1662,11 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
     return;
   }
   const float w = a.gamma ? gld(a.gamma + c) : 1.f;
-  const int cpg = a.chunks_per_group;
   if (a.mode == 1) {
     double dg = 0.0, db = 0.0;
     for (int g = 0; g < a.groups; ++g) {
-      double S = cgl_fin_sum(part, (long)g * cpg, cpg, C, c, lane, [](auto v) { return (double)v[0]; });
-      double D = cgl_fin_sum(part, (long)g * cpg, cpg, C, c, lane, [](auto v) { return (double)v[1]; });
+      double S = gsum(g, [](auto v) { return (double)v[0]; });
+      double D = gsum(g, [](auto v) { return (double)v[1]; });
       S = cgl_block_sum_d(S, red);
       D = cgl_block_sum_d(D, red);
       const float invstd = gld(a.save_invstd + (long)g * C + c);
@@ -1656,13 +1696,12 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
   }
   float rm = a.run_mean ? gld(a.run_mean + c) : 0.f, rv = a.run_var ? gld(a.run_var + c) : 0.f;
   for (int g = 0; g < a.groups; ++g) {
-    const long q0 = (long)g * cpg;
-    double s = cgl_fin_sum(part, q0, cpg, C, c, lane, [](auto v) { return (double)v[0]; });
+    double s = gsum(g, [](auto v) { return (double)v[0]; });
     s = cgl_block_sum_d(s, red);
     const double n = a.gr;
     const double mu = s / n;
     const double cnt = a.R;
-    double m2 = cgl_fin_sum(part, q0, cpg, C, c, lane, [&](auto v) {
+    double m2 = gsum(g, [&](auto v) {
       const double dd = v[0] / cnt - mu;
       return (double)v[1] + cnt * dd * dd;
     });
@@ -1711,12 +1750,17 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize_sliced(CglBnFinSliced a) 
   const int C = a.f.C, cpg = a.f.chunks_per_group, G = a.f.groups, S = a.S;
   const int q_lo = s * a.L, cnt = min(q_lo + a.L, cpg) - q_lo;
   const double R = a.f.R;
+  CglFinCache<2> fc;                     // a slice is <= 512 chunks: <= 2 per thread and call
+  if (G <= 2 && a.L <= 512) fc.load(a.f.part, cpg, G, cnt, C, c, lane, q_lo);
   for (int g = 0; g < G; ++g) {
     const long q0 = (long)g * cpg + q_lo;
-    double sm = cgl_fin_sum(a.f.part, q0, cnt, C, c, lane, [](auto v) { return (double)v[0]; });
+    auto gsum = [&](auto fn) -> double {
+      return (G <= 2 && a.L <= 512) ? fc.sum(g, fn) : cgl_fin_sum(a.f.part, q0, cnt, C, c, lane, fn);
+    };
+    double sm = gsum([](auto v) { return (double)v[0]; });
     sm = cgl_block_sum_d(sm, red);
     const double mu = sm / (cnt * R);
-    double m2 = cgl_fin_sum(a.f.part, q0, cnt, C, c, lane, [&](auto v) {
+    double m2 = gsum([&](auto v) {
       const double dd = v[0] / R - mu;
       return (double)v[1] + R * dd * dd;
     });
@@ -2448,6 +2492,11 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
 }
 
 
+int fin_nocache() {
+  static const int v = getenv("CGL_FIN_NOCACHE") ? atoi(getenv("CGL_FIN_NOCACHE")) : 0;
+  return v;
+}
+
 int chan_chunk(int64_t gr) {
   int R = 128;
   while (R > 1 && gr % R != 0) R >>= 1;
@@ -2475,6 +2524,7 @@ int col_sum(const float* X, int64_t rows, int C, double* part, float* out, hipSt
   CglBnFinArgs f;
   std::memset(&f, 0, sizeof(f));
   f.part = part; f.C = C; f.groups = 1; f.chunks_per_group = nch; f.mode = 2; f.dgamma = out;
+  f.nocache = fin_nocache();
   hipLaunchKernelGGL(cgl_bn_finalize, dim3(C), dim3(256), 0, s, f);
   return (int)hipGetLastError();
 }
@@ -2915,6 +2965,7 @@ int cgl_bn2d_fwd(const float* X, int n, int hw, int C, int groups, const float* 
   f.mode = 0; f.train = train; f.gamma = gamma; f.beta = beta; f.eps = eps; f.momentum = momentum;
   f.run_mean = running_mean; f.run_var = running_var; f.save_mean = save_mean; f.save_invstd = save_invstd;
   f.coef0 = c0; f.coef1 = c1;
+  f.nocache = fin_nocache();
   hipLaunchKernelGGL(cgl_bn_finalize, dim3(C), dim3(256), 0, s, f);
   CglEltArgs e;
   std::memset(&e, 0, sizeof(e));
@@ -2967,7 +3018,8 @@ int cgl_bn2d_fwd_stats(const double* part, int R, const float* X, int n, int hw,
     a.sl = (double*)((char*)scratch + al256((int64_t)C * 4));
     hipLaunchKernelGGL(cgl_bn_finalize_sliced, dim3(a.S, C), dim3(256), 0, s, a);
   } else {
-    hipLaunchKernelGGL(cgl_bn_finalize, dim3(C), dim3(256), 0, s, f);
+    f.nocache = fin_nocache();
+  hipLaunchKernelGGL(cgl_bn_finalize, dim3(C), dim3(256), 0, s, f);
   }
   CglEltArgs e;
   std::memset(&e, 0, sizeof(e));
@@ -3000,6 +3052,7 @@ int cgl_bn2d_bwd_stats(const double* part, int R, const float* dY, const float* 
   f.part = part; f.C = C; f.groups = groups; f.chunks_per_group = (int)(gr / R); f.R = R; f.gr = (int)gr;
   f.mode = 1; f.gamma = gamma; f.save_invstd = const_cast<float*>(save_invstd); f.coef0 = c0; f.coef1 = c1;
   f.dgamma = dgamma; f.dbeta = dbeta;
+  f.nocache = fin_nocache();
   hipLaunchKernelGGL(cgl_bn_finalize, dim3(C), dim3(256), 0, s, f);
   CglEltArgs e;
   std::memset(&e, 0, sizeof(e));
@@ -3039,6 +3092,7 @@ int cgl_bn2d_bwd(const float* dY, const float* post, const float* X, int n, int 
   f.part = part; f.C = C; f.groups = groups; f.chunks_per_group = (int)(gr / R); f.R = R; f.gr = (int)gr;
   f.mode = 1; f.gamma = gamma; f.save_invstd = const_cast<float*>(save_invstd); f.coef0 = c0; f.coef1 = c1;
   f.dgamma = dgamma; f.dbeta = dbeta;
+  f.nocache = fin_nocache();
   hipLaunchKernelGGL(cgl_bn_finalize, dim3(C), dim3(256), 0, s, f);
   CglEltArgs e;
   std::memset(&e, 0, sizeof(e));
