@@ -1,0 +1,74 @@
+// Device / host helpers shared by the two translation units of libcglgan_hip (the MLP step:
+// cgl_runtime.hip with cgl_gemm.hip + cgl_kernels.hip; the conv path: cgl_conv_tu.hip with
+// cgl_conv.hip + cgl_eval.hip).  Included by cgl_internal.h.
+#pragma once
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef CGL_GLOBAL unsigned int cgl_gu32;
+typedef CGL_GLOBAL unsigned long long cgl_gu64;
+__device__ __forceinline__ void cgl_pub2f(float* p, float a, float b) {
+  const unsigned long long v = (unsigned long long)__float_as_uint(a) | ((unsigned long long)__float_as_uint(b) << 32);
+  __hip_atomic_store((cgl_gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void cgl_pubd(double* p, double a) {
+  __hip_atomic_store((cgl_gu64*)p, (unsigned long long)__double_as_longlong(a), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ unsigned long long cgl_ld64(const void* p) {
+  return __hip_atomic_load((cgl_gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ float cgl_lerp(float self, float end, float w) {
+  // at::lerp: |w| < 0.5 ? self + w * (end - self) : end - (end - self) * (1 - w)
+  return fabsf(w) < 0.5f ? self + w * (end - self) : end - (end - self) * (1.f - w);
+}
+
+__device__ __forceinline__ float cgl_softmax_at(const float* x, int n, int i) {
+  float mx = x[0];
+  for (int q = 1; q < n; ++q) mx = fmaxf(mx, x[q]);
+  float s = 0.f;
+  for (int q = 0; q < n; ++q) s += expf(x[q] - mx);
+  return expf(x[i] - mx) / s;
+}
+
+__device__ inline void cgl_weights(int mode, int N, float lam, const float* beta, const float* loss, float* alpha) {
+  float tmp[CGL_MAX_WORKERS], tmp2[CGL_MAX_WORKERS];
+  if (mode == CGL_W_MEAN) {
+    for (int i = 0; i < N; ++i) alpha[i] = 1.f / N;
+    return;
+  }
+  if (mode == CGL_W_MIX_SINGLE) {
+    for (int i = 0; i < N; ++i) tmp[i] = beta[i] * lam * loss[i];
+    for (int i = 0; i < N; ++i) alpha[i] = cgl_softmax_at(tmp, N, i);
+    return;
+  }
+  for (int i = 0; i < N; ++i) tmp[i] = lam * loss[i];
+  for (int i = 0; i < N; ++i) tmp2[i] = cgl_softmax_at(tmp, N, i);   // softmax(lambda * l)
+  if (mode == CGL_W_CGLGAN) {
+    for (int i = 0; i < N; ++i) alpha[i] = (beta[i] + tmp2[i]) * 0.5f;
+    return;
+  }
+  if (mode == CGL_W_CAPGAN) {
+    for (int i = 0; i < N; ++i) tmp[i] = tmp2[i] * beta[i];          // softmax(a * beta)
+  } else {  // CGL_W_MIX_DOUBLE
+    for (int i = 0; i < N; ++i) tmp[i] = beta[i] * tmp2[i];
+  }
+  for (int i = 0; i < N; ++i) alpha[i] = cgl_softmax_at(tmp, N, i);
+}
+
+__device__ __forceinline__ void cgl_philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)M0 * c[0], p1 = (uint64_t)M1 * c[2];
+    const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0;
+    const uint32_t h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+    const uint32_t n0 = h1 ^ c[1] ^ k0, n2 = h0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = l1; c[2] = n2; c[3] = l0;
+    k0 += W0; k1 += W1;
+  }
+}
+
+inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }

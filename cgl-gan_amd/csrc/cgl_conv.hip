@@ -32,7 +32,7 @@
 //  * Every launch takes its descriptor by value (kernel arguments): no uploads, no host syncs, so
 //    the ops are stream-ordered and capturable in a hipGraph.
 //
-// Unity build: included by cgl_runtime.hip (shares cgl_internal.h, cgl_philox, cgl_lerp, HIPCHK).
+// Compiled in cgl_conv_tu.hip (shares cgl_internal.h / cgl_common.h: cgl_philox, cgl_lerp, ...).
 
 #define CGL_CONV_MAXP 4
 #define CGL_AS4 __attribute__((address_space(4)))

@@ -23,7 +23,6 @@
 
 #include <type_traits>
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
@@ -102,8 +101,6 @@ __device__ __forceinline__ void cgl_mask(float v[8], bool ok, int k, int K) {
 // every reader loads the published words with agent-scope atomic (sc1) loads, so the poll needs
 // no agent acquire (cdna_hip_programming.md Guideline 16, the all-sc1 form).  Requires the launch's workgroups co-resident (the
 // planner checks the grid against the occupancy); the spin is bounded and a timeout sets *err.
-typedef CGL_GLOBAL unsigned int cgl_gu32;
-typedef CGL_GLOBAL unsigned long long cgl_gu64;
 __device__ __forceinline__ void cgl_rendezvous(unsigned int* cnt, unsigned int n, unsigned int* err) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // every wave's publish stores have landed
   __syncthreads();
@@ -123,17 +120,6 @@ __device__ __forceinline__ void cgl_rendezvous(unsigned int* cnt, unsigned int n
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   __syncthreads();
-}
-__device__ __forceinline__ void cgl_pub2f(float* p, float a, float b) {
-  const unsigned long long v = (unsigned long long)__float_as_uint(a) | ((unsigned long long)__float_as_uint(b) << 32);
-  __hip_atomic_store((cgl_gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void cgl_pubd(double* p, double a) {
-  __hip_atomic_store((cgl_gu64*)p, (unsigned long long)__double_as_longlong(a), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long cgl_ld64(const void* p) {
-  return __hip_atomic_load((cgl_gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 #define CGL_BN_MAXT 32     // row tiles per column tile a fused BatchNorm combines (tiles_m <= 32)
 #define CGL_BN_STG 4       // staged partial items per thread: tiles_m x tile columns <= 1024

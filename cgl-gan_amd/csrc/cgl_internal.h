@@ -198,3 +198,5 @@ struct CglStepState {
 };
 
 enum { CGL_W_CAPGAN = 0, CGL_W_MEAN = 1, CGL_W_MIX_SINGLE = 2, CGL_W_MIX_DOUBLE = 3, CGL_W_CGLGAN = 4 };
+
+#include "cgl_common.h"

@@ -551,44 +551,9 @@ struct CglAdamArgs {
   float b2, w1, w2, eps;   // w1 = (float)(1 - beta1), w2 = (float)(1 - beta2) computed in double
 };
 
-__device__ __forceinline__ float cgl_lerp(float self, float end, float w) {
-  // at::lerp: |w| < 0.5 ? self + w * (end - self) : end - (end - self) * (1 - w)
-  return fabsf(w) < 0.5f ? self + w * (end - self) : end - (end - self) * (1.f - w);
-}
 
-__device__ __forceinline__ float cgl_softmax_at(const float* x, int n, int i) {
-  float mx = x[0];
-  for (int q = 1; q < n; ++q) mx = fmaxf(mx, x[q]);
-  float s = 0.f;
-  for (int q = 0; q < n; ++q) s += expf(x[q] - mx);
-  return expf(x[i] - mx) / s;
-}
 
 // alpha_i for every worker from the gathered losses (the reference's Server.train weighting).
-__device__ void cgl_weights(int mode, int N, float lam, const float* beta, const float* loss, float* alpha) {
-  float tmp[CGL_MAX_WORKERS], tmp2[CGL_MAX_WORKERS];
-  if (mode == CGL_W_MEAN) {
-    for (int i = 0; i < N; ++i) alpha[i] = 1.f / N;
-    return;
-  }
-  if (mode == CGL_W_MIX_SINGLE) {
-    for (int i = 0; i < N; ++i) tmp[i] = beta[i] * lam * loss[i];
-    for (int i = 0; i < N; ++i) alpha[i] = cgl_softmax_at(tmp, N, i);
-    return;
-  }
-  for (int i = 0; i < N; ++i) tmp[i] = lam * loss[i];
-  for (int i = 0; i < N; ++i) tmp2[i] = cgl_softmax_at(tmp, N, i);   // softmax(lambda * l)
-  if (mode == CGL_W_CGLGAN) {
-    for (int i = 0; i < N; ++i) alpha[i] = (beta[i] + tmp2[i]) * 0.5f;
-    return;
-  }
-  if (mode == CGL_W_CAPGAN) {
-    for (int i = 0; i < N; ++i) tmp[i] = tmp2[i] * beta[i];          // softmax(a * beta)
-  } else {  // CGL_W_MIX_DOUBLE
-    for (int i = 0; i < N; ++i) tmp[i] = beta[i] * tmp2[i];
-  }
-  for (int i = 0; i < N; ++i) alpha[i] = cgl_softmax_at(tmp, N, i);
-}
 
 __global__ __launch_bounds__(256) void cgl_adam(CglAdamArgs a, CglStepState* st, int tail) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -681,18 +646,6 @@ __device__ void cgl_begin_at(const CglBeginArgs& a, int r) {
 
 // ------------------------------------------------------------------------------------------
 // Philox4x32-10 counter-based RNG + Box-Muller: out[i] ~ N(0,1), fresh per round.
-__device__ __forceinline__ void cgl_philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
-  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    const uint64_t p0 = (uint64_t)M0 * c[0], p1 = (uint64_t)M1 * c[2];
-    const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0;
-    const uint32_t h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
-    const uint32_t n0 = h1 ^ c[1] ^ k0, n2 = h0 ^ c[3] ^ k1;
-    c[0] = n0; c[1] = l1; c[2] = n2; c[3] = l0;
-    k0 += W0; k1 += W1;
-  }
-}
 
 // outputs 4q .. 4q+3 of the N(0,1) stream (seed, round, stream_id)
 __device__ __forceinline__ void cgl_normal_at(long q, float* out, long n, unsigned long long seed, uint32_t round,

@@ -403,7 +403,6 @@ CglRowSrc rows(const float* p, int ld) {
   return r;
 }
 
-inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
 
@@ -1735,6 +1734,5 @@ int cgl_normal_fill(float* out, int64_t n, unsigned long long seed, int round, i
 
 }  // extern "C"
 
-// conv GAN path (model/lsgan.py): implicit-GEMM convolutions, BatchNorm2d, losses, Adam
-#include "cgl_conv.hip"
-#include "cgl_eval.hip"
+// the conv GAN path (model/lsgan.py) and the evaluation kernels are the second translation unit
+// (cgl_conv_tu.hip)
