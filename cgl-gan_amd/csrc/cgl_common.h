@@ -72,3 +72,15 @@ __device__ __forceinline__ void cgl_philox(uint32_t c[4], uint32_t k0, uint32_t 
 }
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// One Adam element update in torch 2.10 _single_tensor_adam's operation order (foreach=False,
+// capgan.py:158,312): m = lerp(m, g, 1 - beta1), v = v beta2 + (1 - beta2) g g,
+// p += -step_size m / (sqrt(v) / sqrt(bias_correction2) + eps).  Shared by cgl_adam and the Adam
+// folded into the GEMM launches (cgl_gemm.hip) so that both round identically.
+__device__ __forceinline__ void cgl_adam_update(float& p, float g, float& m, float& v, float ss, float bc, float b2,
+                                                float w1, float w2, float eps) {
+  m = cgl_lerp(m, g, w1);
+  v = __fadd_rn(__fmul_rn(v, b2), __fmul_rn(__fmul_rn(w2, g), g));
+  const float denom = sqrtf(v) / bc + eps;
+  p = p + (-ss) * m / denom;
+}

@@ -72,6 +72,8 @@ struct CglConvLaunch {
   const float* st_x;         // mode 1: the BatchNorm input x, the post-activation (or null) and the
   const float* st_post;      // saved per-call mean [groups][N], all at the stored tensor's positions
   const float* st_mean;
+  int ilv;                   // forward: the np problems share X and their tile grid -- tiles interleaved
+                             // problem-minor (tile t of every problem back to back on one XCD)
 };
 
 typedef const CGL_AS4 CglConvLaunch* CglKL;
@@ -119,7 +121,7 @@ __device__ __forceinline__ int cgl_xcd_tile(int local, int nwg) {
 // FAST: Cin % 16 == 0, so a 16-k chunk lies inside one tap (uniform tap, 2 x 16-byte loads per
 // lane and block).  Otherwise each k is decoded per element (tiny-K layers: Cin = 1).
 template <int TM, int TN, bool FAST>
-__device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, float* s_red) {
+__device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, float* s_red, bool direct = false) {
   constexpr int S = 3;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -128,7 +130,7 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
   const int wk = wave % WK, wmn = wave / WK;
   const int wm = wmn / WN, wn = wmn - wm * WN;
   const int tiles_n = P->tiles_n;
-  const int tile = cgl_xcd_tile(local, P->tiles_m * tiles_n);
+  const int tile = direct ? local : cgl_xcd_tile(local, P->tiles_m * tiles_n);
   const int tn = tile % tiles_n, tm = tile / tiles_n;
   const int M = P->M, N = P->N, K = P->K, Kp = P->Kp, Cin = P->Cin;
   const int IH = P->IH, IW = P->IW, ish = P->ish, XW = P->XW, Tx = P->Tx;
@@ -431,6 +433,15 @@ __global__ __launch_bounds__(256) void cgl_conv_fwd(CglConvLaunch args) {
   extern __shared__ float cgl_conv_lds[];
   CglKL L = cgl_conv_args();
   const int bid = blockIdx.x;
+  if (L->ilv) {
+    // problems sharing one input (the 4 output parities of an upsampling conv in phase form, the
+    // input-parity problems of a stride-2 input gradient): unit u = (tile u / np of problem u % np),
+    // units XCD-contiguous, so the np tiles reading one input window run back to back in one L2
+    const int np = L->np;
+    const int unit = cgl_xcd_tile(bid, L->p[0].tiles_m * L->p[0].tiles_n * np);
+    cgl_conv_fwd_body<TM, TN, FAST>(L, &L->p[unit % np], unit / np, cgl_conv_lds, true);
+    return;
+  }
   const int pi = cgl_conv_prob(L, bid);
   CglKP P = &L->p[pi];
   cgl_conv_fwd_body<TM, TN, FAST>(L, P, bid - P->wg_begin, cgl_conv_lds);
@@ -2478,6 +2489,12 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
     fast = fast && (P[i].Cin % 16 == 0 || (P[i].Ty * P[i].Tx == 1 && P[i].Cin % 4 == 0));
     L.p[i] = P[i];
   }
+  // interleaved tile order for problems that read one input through the same tile grid
+  // (CGL_CONV_ILV=0: problem-major order)
+  static const int ilv_env = getenv("CGL_CONV_ILV") ? atoi(getenv("CGL_CONV_ILV")) : 1;
+  L.ilv = ilv_env != 0 && np > 1;
+  for (int i = 1; i < np; ++i)
+    L.ilv = L.ilv && P[i].X == P[0].X && P[i].tiles_m == P[0].tiles_m && P[i].tiles_n == P[0].tiles_n;
   if (t.TM == 2 && t.TN == 2) {
     if (fast) hipLaunchKernelGGL((cgl_conv_fwd<2, 2, true>), dim3(wg), dim3(256), lds, s, L);
     else hipLaunchKernelGGL((cgl_conv_fwd<2, 2, false>), dim3(wg), dim3(256), lds, s, L);

@@ -555,60 +555,80 @@ struct CglAdamArgs {
 
 // alpha_i for every worker from the gathered losses (the reference's Server.train weighting).
 
+// Scalar tail of Server.train: F_max and the lambda update (after every parameter read of this
+// round, before the next round's prologue).  Written without per-worker local arrays (alpha_i is
+// recomputed per worker, O(N^2) for N <= 64 in one thread) so that the kernels it is inlined into
+// (cgl_adam, the GEMM launch carrying the folded Adam) need no scratch memory; the arithmetic and
+// its order are those of cgl_weights / cgl_softmax_at.
+__device__ __forceinline__ float cgl_tail_loss(const CglStepState* st, int q) {
+  return st->n_workers == 1 ? st->g_loss_parts[0] : st->losses[q];
+}
+// softmax(lam * l)_i
+__device__ float cgl_tail_sm1(const CglStepState* st, float lam, int i) {
+  const int N = st->n_workers;
+  float mx = lam * cgl_tail_loss(st, 0);
+  for (int q = 1; q < N; ++q) mx = fmaxf(mx, lam * cgl_tail_loss(st, q));
+  float s = 0.f;
+  for (int q = 0; q < N; ++q) s += expf(lam * cgl_tail_loss(st, q) - mx);
+  return expf(lam * cgl_tail_loss(st, i) - mx) / s;
+}
+// the pre-softmax argument of alpha's outer softmax for worker i (modes CAPGAN / MIX_*)
+__device__ float cgl_tail_arg(const CglStepState* st, int mode, float lam, int i) {
+  if (mode == CGL_W_MIX_SINGLE) return st->beta[i] * lam * cgl_tail_loss(st, i);
+  if (mode == CGL_W_CAPGAN) return cgl_tail_sm1(st, lam, i) * st->beta[i];
+  return st->beta[i] * cgl_tail_sm1(st, lam, i);   // CGL_W_MIX_DOUBLE
+}
+__device__ float cgl_tail_alpha(const CglStepState* st, int mode, float lam, int i) {
+  const int N = st->n_workers;
+  float mx = cgl_tail_arg(st, mode, lam, 0);
+  for (int q = 1; q < N; ++q) mx = fmaxf(mx, cgl_tail_arg(st, mode, lam, q));
+  float s = 0.f;
+  for (int q = 0; q < N; ++q) s += expf(cgl_tail_arg(st, mode, lam, q) - mx);
+  return expf(cgl_tail_arg(st, mode, lam, i) - mx) / s;
+}
+__device__ void cgl_round_tail(CglStepState* st) {
+  const int N = st->n_workers;
+  const float lam = st->lambda;
+  const int mode = st->weighting;
+  if (mode == CGL_W_MEAN) {
+    float s = 0.f;
+    for (int q = 0; q < N; ++q) s += cgl_tail_loss(st, q);
+    st->F = s / N;
+  } else if (mode == CGL_W_CGLGAN) {
+    float fb = 0.f, fg = 0.f, g1 = 0.f, g2 = 0.f;
+    for (int q = 0; q < N; ++q) {
+      const float lq = cgl_tail_loss(st, q);
+      fb += st->beta[q] * lq;
+      fg += cgl_tail_sm1(st, lam, q) * lq;
+    }
+    st->F = (fb + fg) / 2.f;
+    for (int q = 0; q < N; ++q) {
+      const float lq = cgl_tail_loss(st, q), gm = cgl_tail_sm1(st, lam, q);
+      g1 += lq * lq * gm;
+      g2 += lq * gm * fg;
+    }
+    st->lambda = lam + 10.f * (g1 - g2);
+  } else {
+    float s = 0.f;
+    for (int q = 0; q < N; ++q) s += cgl_tail_alpha(st, mode, lam, q) * cgl_tail_loss(st, q);
+    st->F = s - 0.001f * lam;
+    // optim.SGD([Lambda], lr=0.1): dF/dLambda = -0.001
+    st->lambda = lam + (-0.1f) * (-0.001f);
+  }
+  st->round = st->round + 1;   // round complete (read by the next round's prologue)
+}
+
 __global__ __launch_bounds__(256) void cgl_adam(CglAdamArgs a, CglStepState* st, int tail) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const float ss = gld(a.step_size), bc = gld(a.bc2sqrt);
-  const float w1 = a.w1, w2 = a.w2;
   if (i < a.n) {
-    const float g = gld(a.g + i);
-    const float m = cgl_lerp(gld(a.m + i), g, w1);
-    const float v = __fadd_rn(__fmul_rn(gld(a.v + i), a.b2), __fmul_rn(__fmul_rn(w2, g), g));
+    float p = gld(a.p + i), m = gld(a.m + i), v = gld(a.v + i);
+    cgl_adam_update(p, gld(a.g + i), m, v, ss, bc, a.b2, a.w1, a.w2, a.eps);
     gst(a.m + i, m);
     gst(a.v + i, v);
-    const float denom = sqrtf(v) / bc + a.eps;
-    gst(a.p + i, gld(a.p + i) + (-ss) * m / denom);
+    gst(a.p + i, p);
   }
-  if (tail && i == 0) {
-    // scalar tail of Server.train: F_max and the lambda update (after every parameter read
-    // of this round, before the next round's prologue).
-    const int N = st->n_workers;
-    const float lam = st->lambda;
-    float l[CGL_MAX_WORKERS];
-    if (N == 1) {
-      l[0] = st->g_loss_parts[0];
-    } else {
-      for (int q = 0; q < N; ++q) l[q] = st->losses[q];
-    }
-    float al[CGL_MAX_WORKERS];
-    cgl_weights(st->weighting, N, lam, st->beta, l, al);
-    if (st->weighting == CGL_W_MEAN) {
-      float s = 0.f;
-      for (int q = 0; q < N; ++q) s += l[q];
-      st->F = s / N;
-    } else if (st->weighting == CGL_W_CGLGAN) {
-      float fb = 0.f, fg = 0.f, g1 = 0.f, g2 = 0.f;
-      float gm[CGL_MAX_WORKERS], tmp[CGL_MAX_WORKERS];
-      for (int q = 0; q < N; ++q) tmp[q] = lam * l[q];
-      for (int q = 0; q < N; ++q) gm[q] = cgl_softmax_at(tmp, N, q);
-      for (int q = 0; q < N; ++q) {
-        fb += st->beta[q] * l[q];
-        fg += gm[q] * l[q];
-      }
-      st->F = (fb + fg) / 2.f;
-      for (int q = 0; q < N; ++q) {
-        g1 += l[q] * l[q] * gm[q];
-        g2 += l[q] * gm[q] * fg;
-      }
-      st->lambda = lam + 10.f * (g1 - g2);
-    } else {
-      float s = 0.f;
-      for (int q = 0; q < N; ++q) s += al[q] * l[q];
-      st->F = s - 0.001f * lam;
-      // optim.SGD([Lambda], lr=0.1): dF/dLambda = -0.001
-      st->lambda = lam + (-0.1f) * (-0.001f);
-    }
-    st->round = st->round + 1;   // round complete (read by the next round's prologue)
-  }
+  if (tail && i == 0) cgl_round_tail(st);
 }
 
 // ------------------------------------------------------------------------------------------
