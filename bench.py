@@ -256,6 +256,18 @@ def conv_cpu_baseline(a):
                       f"oracle after {warm} warm-up round, {t_total:.1f} s, torch {torch.__version__}"}
 
 
+def conv_traffic():
+    """HBM-side traffic of the dominant conv op per dispatch from the rocprofv3 PMC passes
+    (profiles/r02_conv_dominant_traffic.json, FETCH_SIZE x2 + WRITE_SIZE; None when absent)."""
+    path = os.path.join(ROOT, "profiles", "r02_conv_dominant_traffic.json")
+    if not os.path.exists(path):
+        return {"traffic": None}
+    p = json.load(open(path))
+    return {"traffic": round(p["bytes"]), "traffic_unit": f"bytes per {p['kernel']} dispatch of the dominant op "
+            f"{p['geom']} (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/r02_conv_dominant_traffic.json)",
+            "traffic_algorithmic": p["algorithmic_bytes"], "traffic_ratio": round(p["ratio"], 2)}
+
+
 def main_lsgan(a, world, rank, local):
     from cglgan.conv_step import ConvGanStep
     from cglgan.exchange import ConvWorkerExchange, DistComm
@@ -312,7 +324,7 @@ def main_lsgan(a, world, rank, local):
                    "parallelism": f"workers{world}", "dataset_rows_per_worker": rows},
         "roofline": {"bound": "mfma", "kernel": "cgl_conv_fwd + cgl_conv_wgrad (+ pack / reduce), every conv op of "
                                                 "one round", "achieved": round(tf, 3), "peak": PEAK_F32_MFMA,
-                     "unit": "TFLOP/s", "frac": round(tf / PEAK_F32_MFMA, 4), "traffic": None,
+                     "unit": "TFLOP/s", "frac": round(tf / PEAK_F32_MFMA, 4), **conv_traffic(),
                      "conv_exec_gflop_per_round": round(exe / 1e9, 3),
                      "conv_ref_gflop_per_round": round(ref / 1e9, 3),
                      "conv_us_per_round": round(mma_us, 1),

@@ -7,7 +7,10 @@ stream (no host synchronisation) and raises on a non-zero return code; there is 
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import functools
+import os
 
 import torch
 
@@ -17,6 +20,8 @@ ACT_NONE, ACT_LEAKY, ACT_TANH, ACT_SIGMOID = 0, 1, 2, 3
 LOSS = {"ce": C.LOSS_OP_CE2, "bce_prob": C.LOSS_OP_BCE, "mse": C.LOSS_OP_MSE, "bce": C.LOSS_OP_BCE_LOGIT}
 
 _WS = {}
+_CUR = None     # (device index, stream handle, ctypes handle) inside a stream_cache() block
+_NO_CACHE = os.environ.get("CGL_STREAM_CACHE", "1") == "0"
 
 
 def _p(t):
@@ -24,13 +29,39 @@ def _p(t):
 
 
 def _s():
+    if _CUR is not None:
+        return _CUR[2]
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+@contextlib.contextmanager
+def stream_cache():
+    """Resolve the current torch stream once for a block of ops that all run on it (the fused conv
+    round issues ~100 ops per round; looking the stream up per op was a visible share of the host
+    time that leaves the GPU idle between the small discriminator kernels).  The block must not
+    switch streams."""
+    global _CUR
+    if _NO_CACHE:
+        yield
+        return
+    prev = _CUR
+    s = torch.cuda.current_stream()
+    _CUR = (s.device.index, s.cuda_stream, ctypes.c_void_p(s.cuda_stream))
+    try:
+        yield
+    finally:
+        _CUR = prev
 
 
 def workspace(nbytes: int, device) -> torch.Tensor:
     """Scratch owned by the caching allocator, one buffer per (device, stream): ops issued on one
     stream are ordered, so they share it; ops on another stream (a side-stream round beside the
     drop-in modules, two-stream overlap) get their own and never race on it.  Grown on demand."""
+    if _CUR is not None and (getattr(device, "index", None) in (None, _CUR[0])):
+        key = (_CUR[0], _CUR[1])
+        w = _WS.get(key)
+        if w is not None and w.numel() >= nbytes:
+            return w
     dev = torch.device(device)
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     key = (idx, torch.cuda.current_stream(idx).cuda_stream)
@@ -51,6 +82,7 @@ def conv_out_hw(h, w, stride, up):
     return ((h << up) - 1) // stride + 1, ((w << up) - 1) // stride + 1
 
 
+@functools.lru_cache(maxsize=512)
 def conv_ws_bytes(n, h, w, cin, cout, stride, up):
     b = C.lib.cgl_conv3x3_workspace_bytes(n, h, w, cin, cout, stride, up)
     if b < 0:

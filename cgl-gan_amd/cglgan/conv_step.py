@@ -384,6 +384,10 @@ class ConvGanStep:
     def phase_a(self, real=None):
         """G forward (Xd, Xg), the local D step, the G loss through the updated D and its gradient
         w.r.t. Xg (capgan.py:215-225, 322-347).  Ends with ``dimg`` = d l_rank / d Xg."""
+        with O.stream_cache():     # every op of the phase runs on the current stream
+            self._phase_a(real)
+
+    def _phase_a(self, real=None):
         B = self.B
         if self.gen_z:
             C.check(C.lib.cgl_normal_fill(ctypes_ptr(self.z), self.z.numel(), self.seed, self.round, 0,
@@ -410,8 +414,9 @@ class ConvGanStep:
 
     def phase_b(self):
         """Replicated G backward from the (exchanged) image gradient, lambda SGD, Adam G (capgan.py:258-260)."""
-        self._g_backward()
-        self.G.adam(self.lr, self.betas, self.eps)
+        with O.stream_cache():
+            self._g_backward()
+            self.G.adam(self.lr, self.betas, self.eps)
         # optim.SGD([Lambda], lr=0.1) with dF/dLambda = -0.001 (capgan.py:249,259), in the fp32
         # arithmetic of the reference's 0-d tensor (the MLP path's cgl_adam tail does the same)
         if self.weighting != "mean":     # MD-GAN's server has no lambda (MDGAN/MNIST/mdgan.py:203-205)
