@@ -277,7 +277,9 @@ def main_lsgan(a, world, rank, local):
         rows = (a.rows // a.batch) * a.batch
         data = torch.rand(rows, 1024, device="cuda", generator=g) * 2 - 1
         # one worker per GPU: G replicated (same init and z stream), D and real shard per rank
-        step = ConvGanStep(a.batch, loss=a.loss, data=data, seed=20211212, n_workers=world, rank=rank)
+        # N = 1: the round replays as one hipGraph (device-side round state, cglgan.conv_step graph mode)
+        step = ConvGanStep(a.batch, loss=a.loss, data=data, seed=20211212, n_workers=world, rank=rank,
+                           graph=world == 1 and not a.eager)
         step.init_default(20211212, 20211212 + 1 + rank)
         ex = ConvWorkerExchange(step, DistComm() if world > 1 else None, share_every=a.E if world > 1 else 0)
         torch.cuda.synchronize()
@@ -301,7 +303,8 @@ def main_lsgan(a, world, rank, local):
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
         st = step.stats()
-        ops = profile_conv_round(lambda: ex.round(r))
+        # per-op timing needs the ops issued one by one: an eager round (same device round state)
+        ops = profile_conv_round(lambda: step.run(eager=True) if world == 1 else ex.round(r))
     ms_step = el / a.steps * 1e3
     value = world * a.batch * a.steps / el
     if rank != 0:
@@ -321,7 +324,8 @@ def main_lsgan(a, world, rank, local):
                                + (f", {world} workers: loss all-gather, alpha-weighted image-gradient "
                                   f"all-reduce, E={a.E} D all-reduce over RCCL" if world > 1 else ""),
                    "global_batch": a.batch * world, "batch_per_worker": a.batch, "img": "32x32x1",
-                   "parallelism": f"workers{world}", "dataset_rows_per_worker": rows},
+                   "parallelism": f"workers{world}", "dataset_rows_per_worker": rows,
+                   "graph": world == 1 and not a.eager},
         "roofline": {"bound": "mfma", "kernel": "cgl_conv_fwd + cgl_conv_wgrad (+ pack / reduce), every conv op of "
                                                 "one round", "achieved": round(tf, 3), "peak": PEAK_F32_MFMA,
                      "unit": "TFLOP/s", "frac": round(tf / PEAK_F32_MFMA, 4), **conv_traffic(),

@@ -36,6 +36,7 @@ EXPORTS = [
     "cgl_dense_fwd_packed", "cgl_dense_bwd_data_packed", "cgl_conv3x3_stat_chunks", "cgl_conv3x3_fwd_packed_stats",
     "cgl_bn2d_fwd_stats", "cgl_bn2d_stats_scratch_bytes", "cgl_linear_desc_bytes", "cgl_linear_prepare",
     "cgl_linear_launch", "cgl_conv3x3_bwd_stat_chunks", "cgl_conv3x3_bwd_data_packed_stats", "cgl_bn2d_bwd_stats",
+    "cgl_normal_fill_dev", "cgl_dropout2d_masks_dev", "cgl_adam_multi_dev", "cgl_sample_rows_dev", "cgl_counters_add",
     # evaluation (CGLGAN/2DMG/main.py plot_2d KL score)
     "cgl_kl_score",
 ]
@@ -155,6 +156,12 @@ def _load():
         "cgl_weights_scale": (ci, [ci, ci, ci, cf, P(cf), vp, vp, i64, vp, vp]),
         "cgl_kl_score": (ci, [vp, i64, i64, vp, i64, i64, ci, cd, cd, cd, cd, vp, vp, vp]),
         "cgl_adam_multi": (ci, [ci, P(vp), P(vp), P(vp), P(vp), P(i64), ci, cd, cd, cd, cd, vp]),
+        "cgl_adam_multi_dev": (ci, [ci, P(vp), P(vp), P(vp), P(vp), P(i64), vp, cd, cd, cd, cd, vp]),
+        "cgl_normal_fill_dev": (ci, [vp, i64, ctypes.c_ulonglong, vp, ci, vp]),
+        "cgl_dropout2d_masks_dev": (ci, [ci, P(vp), P(ci), P(ci), cd, ctypes.c_ulonglong, P(ctypes.c_ulonglong), vp,
+                                         ctypes.c_ulonglong, vp]),
+        "cgl_sample_rows_dev": (ci, [vp, ci, ci, ci, ctypes.c_ulonglong, vp, vp, vp]),
+        "cgl_counters_add": (ci, [vp, ci, ci, vp]),
         "cgl_version": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():

@@ -339,6 +339,37 @@ def dropout2d_masks(masks, ns, cs, p, seed, counters):
             "cgl_dropout2d_masks")
 
 
+def dropout2d_masks_dev(masks, ns, cs, p, seed, counters, round_dev, round_stride):
+    """dropout2d_masks with counter j = counters[j] + round_stride * round_dev[0] (device int32)."""
+    _chk(*masks)
+    k = len(masks)
+    C.check(C.lib.cgl_dropout2d_masks_dev(k, (ctypes.c_void_p * k)(*[m.data_ptr() for m in masks]),
+                                          (ctypes.c_int * k)(*ns), (ctypes.c_int * k)(*cs), float(p),
+                                          int(seed) & (2 ** 64 - 1),
+                                          (ctypes.c_ulonglong * k)(*[int(c) & (2 ** 64 - 1) for c in counters]),
+                                          _p(round_dev), int(round_stride), _s()), "cgl_dropout2d_masks_dev")
+
+
+def normal_fill_dev(out, seed, round_dev, stream_id=0):
+    """N(0,1) fill of the z stream with round = round_dev[0] (device int32)."""
+    _chk(out)
+    C.check(C.lib.cgl_normal_fill_dev(_p(out), out.numel(), int(seed) & (2 ** 64 - 1), _p(round_dev), stream_id, _s()),
+            "cgl_normal_fill_dev")
+
+
+def sample_rows_dev(src, nrows, seed, round_dev, dst):
+    """Real batch of round round_dev[0] from a device-resident [n, f] shard (keyed per-epoch permutation)."""
+    _chk(src, dst)
+    C.check(C.lib.cgl_sample_rows_dev(_p(src), src.shape[0], nrows, src.shape[1], int(seed) & (2 ** 64 - 1),
+                                      _p(round_dev), _p(dst), _s()), "cgl_sample_rows_dev")
+    return dst
+
+
+def counters_add(counters, v=1):
+    """counters (device int32) += v, stream-ordered."""
+    C.check(C.lib.cgl_counters_add(_p(counters), counters.numel(), int(v), _s()), "cgl_counters_add")
+
+
 def nchw_to_nhwc(x, y, n, c, hw):
     _chk(x, y)
     C.check(C.lib.cgl_nchw_to_nhwc(_p(x), _p(y), n, c, hw, _s()), "cgl_nchw_to_nhwc")
@@ -357,14 +388,19 @@ def adv_loss(x, M, Cc, kind, target, weight, loss_out=None, grad=None):
             "cgl_adv_loss")
 
 
-def adam_multi(params, grads, ms, vs, step, lr=2e-4, betas=(0.5, 0.999), eps=1e-8):
-    """One optim.Adam step over up to 32 tensors per launch (chunks larger lists)."""
+def adam_multi(params, grads, ms, vs, step, lr=2e-4, betas=(0.5, 0.999), eps=1e-8, step_dev=None):
+    """One optim.Adam step over up to 32 tensors per launch (chunks larger lists).  ``step_dev``
+    (device int32, completed steps): the step is step_dev[0] + 1, read on the device (graph replay)."""
     for i in range(0, len(params), 32):
         ps, gs, mm, vv = params[i:i + 32], grads[i:i + 32], ms[i:i + 32], vs[i:i + 32]
         _chk(*ps, *gs, *mm, *vv)
         nt = len(ps)
         arr = lambda ts: (ctypes.c_void_p * nt)(*[t.data_ptr() for t in ts])
         ns = (ctypes.c_int64 * nt)(*[t.numel() for t in ps])
+        if step_dev is not None:
+            C.check(C.lib.cgl_adam_multi_dev(nt, arr(ps), arr(gs), arr(mm), arr(vv), ns, _p(step_dev), float(lr),
+                                             float(betas[0]), float(betas[1]), float(eps), _s()), "cgl_adam_multi_dev")
+            continue
         C.check(C.lib.cgl_adam_multi(nt, arr(ps), arr(gs), arr(mm), arr(vv), ns, int(step), float(lr), float(betas[0]),
                                      float(betas[1]), float(eps), _s()), "cgl_adam_multi")
 

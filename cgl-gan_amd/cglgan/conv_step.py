@@ -84,11 +84,13 @@ class FlatModel:
                 self.batches[key] = 0
         self.step = 0
 
-    def adam(self, lr, betas, eps):
+    def adam(self, lr, betas, eps, step_dev=None):
+        """step_dev: device int32 holding the completed steps (the graph-replayable round reads the
+        step there); the host count advances either way."""
         self.step += 1
         ps = [self.params[k].view(-1) for k, _, _, _ in self.layout]
         gs = [self.grads[k].view(-1) for k, _, _, _ in self.layout]
-        O.adam_multi(ps, gs, self._m, self._v, self.step, lr, betas, eps)
+        O.adam_multi(ps, gs, self._m, self._v, self.step, lr, betas, eps, step_dev=step_dev)
 
     def state_dict(self):
         sd = OrderedDict()
@@ -140,7 +142,7 @@ class ConvGanStep:
     """Fused CAPGAN worker round of the model/lsgan.py GAN (see module docstring)."""
 
     def __init__(self, batch, loss="mse", data=None, seed=20211212, n_workers=1, rank=0, weighting="capgan",
-                 lr=2e-4, betas=(0.5, 0.999), adam_eps=1e-8, gen_z=True, beta=None, device="cuda"):
+                 lr=2e-4, betas=(0.5, 0.999), adam_eps=1e-8, gen_z=True, beta=None, device="cuda", graph=False):
         if loss not in ("mse", "bce"):
             raise ValueError("loss must be 'mse' (LSGAN) or 'bce' (Sigmoid + BCELoss)")
         if batch < 2:
@@ -181,6 +183,15 @@ class ConvGanStep:
         self.beta = None
         self.set_beta(beta)
         self.round = 0
+        # graph=True: every per-round value comes from the device counter block `dstate` (round, G
+        # Adam steps, D Adam steps) -- z stream, Dropout2d counters, Adam bias corrections, and the
+        # real batch through the device sampler (cgl_sample_rows_dev) -- and run() replays one
+        # captured round as a hipGraph (N = 1; phases stay eager for the multi-worker exchange)
+        self.graph = bool(graph)
+        self.dstate = torch.zeros(4, dtype=torch.int32, device=dev)
+        self._dstate_host = (0, 0, 0)         # host mirror of dstate after the last issued round
+        self._cuda_graph = None
+        self._graph_delta = None
         # packed MFMA weight operands of every layer (cglgan.conv_ops.PackSet): G and D are packed
         # together at the start of a round (the exchanges between rounds may rewrite either), D again
         # after its Adam step -- two pack launches per round instead of one per conv call
@@ -299,6 +310,11 @@ class ConvGanStep:
         """Every Dropout2d mask of the round in one launch: the D step's (call 0, 2B images) and the
         G-loss pass's (call 1, B images); counter (round * 2 + call) * 4 + layer."""
         B, cs = self.B, [co for _, _, _, co, _ in D_CONVS]
+        if self.graph:      # counter = (round * 2 + call) * 4 + k with the round read on the device
+            O.dropout2d_masks_dev(self.mask_d + self.mask_g, [2 * B] * 4 + [B] * 4, cs + cs, DROP_P,
+                                  self.seed * 7919 + self.rank, [call * 4 + k for call in (0, 1) for k in range(4)],
+                                  self.dstate[0:1], 8)
+            return
         O.dropout2d_masks(self.mask_d + self.mask_g, [2 * B] * 4 + [B] * 4, cs + cs, DROP_P,
                           self.seed * 7919 + self.rank,
                           [(self.round * 2 + call) * 4 + k for call in (0, 1) for k in range(4)])
@@ -389,13 +405,21 @@ class ConvGanStep:
 
     def _phase_a(self, real=None):
         B = self.B
+        if self.graph:
+            self._sync_dstate()
         if self.gen_z:
-            C.check(C.lib.cgl_normal_fill(ctypes_ptr(self.z), self.z.numel(), self.seed, self.round, 0,
-                                          O._s()), "cgl_normal_fill")
+            if self.graph:
+                O.normal_fill_dev(self.z, self.seed, self.dstate[0:1])
+            else:
+                C.check(C.lib.cgl_normal_fill(ctypes_ptr(self.z), self.z.numel(), self.seed, self.round, 0,
+                                              O._s()), "cgl_normal_fill")
         if real is not None:
             O.gather_rows(real.reshape(-1, 1024), None, 0, B, 1024, self.x3)
         elif self.data is not None:
-            self._sample_real()
+            if self.graph:
+                O.sample_rows_dev(self.data, B, self.seed + 1 + self.rank, self.dstate[0:1], self.x3)
+            else:
+                self._sample_real()
         self.pk.run()
         self._masks()
         self._g_forward()
@@ -405,7 +429,7 @@ class ConvGanStep:
         O.adv_loss(self.v[:B], B, 1, self.loss, 1, half, self.lbuf[0:1], self.dv[:B])
         O.adv_loss(self.v[B:2 * B], B, 1, self.loss, 0, half, self.lbuf[1:2], self.dv[B:2 * B])
         self._d_backward(self.x3, 2 * B, 2, self.mask_d, wgrad=True, dx=None)
-        self.D.adam(self.lr, self.betas, self.eps)
+        self.D.adam(self.lr, self.betas, self.eps, step_dev=self.dstate[2:3] if self.graph else None)
         self.pk.run("D")
         # G loss through the updated D (its D weight gradient is discarded by the reference: skipped)
         self._d_forward(self.x3[2 * B:], B, 1, self.mask_g)
@@ -416,19 +440,77 @@ class ConvGanStep:
         """Replicated G backward from the (exchanged) image gradient, lambda SGD, Adam G (capgan.py:258-260)."""
         with O.stream_cache():
             self._g_backward()
-            self.G.adam(self.lr, self.betas, self.eps)
+            self.G.adam(self.lr, self.betas, self.eps, step_dev=self.dstate[1:2] if self.graph else None)
+            if self.graph:
+                O.counters_add(self.dstate[0:3], 1)     # round, G steps, D steps (epoch = 1)
+                self._dstate_host = (self.round + 1, self.G.step, self.D.step)
+        self._lam_step()
+        self.round += 1
+
+    def _lam_step(self):
         # optim.SGD([Lambda], lr=0.1) with dF/dLambda = -0.001 (capgan.py:249,259), in the fp32
         # arithmetic of the reference's 0-d tensor (the MLP path's cgl_adam tail does the same)
         if self.weighting != "mean":     # MD-GAN's server has no lambda (MDGAN/MNIST/mdgan.py:203-205)
             self.lam = float(np.float32(self.lam) + np.float32(-0.1) * np.float32(-0.001))
-        self.round += 1
 
-    def run(self, real=None):
-        """One round with N = 1 (alpha = 1 exactly, capgan.py:247-248)."""
+    def run(self, real=None, eager=False):
+        """One round with N = 1 (alpha = 1 exactly, capgan.py:247-248).  With graph=True (and the
+        round drawing its own real batch) the first round runs eagerly, the second is captured into a
+        hipGraph and every round from then on is one replay."""
         if self.n_workers != 1:
             raise RuntimeError("n_workers > 1: use cglgan.exchange.ConvWorkerExchange")
-        self.phase_a(real)
-        self.phase_b()
+        if not self.graph or eager or real is not None or self.data is None or self.round == 0:
+            self.phase_a(real)
+            self.phase_b()
+            return
+        if self._cuda_graph is None:
+            self._capture()
+        self._sync_dstate()
+        self._cuda_graph.replay()
+        self._apply_host_delta()
+
+    # ------------------------------------------------------------------ graph replay
+    def _host_state(self):
+        return (self.round, self.G.step, self.D.step, dict(self.G.batches), dict(self.D.batches), self.lam)
+
+    def _sync_dstate(self):
+        """dstate must hold (round, G steps, D steps) of the host: rewritten only when the host state
+        moved without it (a load_state_dict, a round of another path)."""
+        want = (self.round, self.G.step, self.D.step)
+        if want != self._dstate_host:
+            self.dstate[:3].copy_(torch.tensor(want, dtype=torch.int32))
+            self._dstate_host = want
+
+    def _capture(self):
+        before = self._host_state()
+        self._sync_dstate()
+        torch.cuda.current_stream().synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.phase_a(None)
+            self.phase_b()
+        after = self._host_state()
+        # capturing issued nothing: restore the host bookkeeping, remember what one round adds
+        self.round, self.G.step, self.D.step = before[0], before[1], before[2]
+        self.G.batches.update(before[3])
+        self.D.batches.update(before[4])
+        self.lam = before[5]
+        self._dstate_host = (self.round, self.G.step, self.D.step)
+        self._graph_delta = ({k: after[3][k] - before[3][k] for k in before[3]},
+                             {k: after[4][k] - before[4][k] for k in before[4]})
+        self._cuda_graph = g
+
+    def _apply_host_delta(self):
+        gb, db = self._graph_delta
+        for k, v in gb.items():
+            self.G.batches[k] += v
+        for k, v in db.items():
+            self.D.batches[k] += v
+        self.G.step += 1
+        self.D.step += 1
+        self._lam_step()
+        self.round += 1
+        self._dstate_host = (self.round, self.G.step, self.D.step)
 
     def stats(self):
         l = self.lbuf.cpu()

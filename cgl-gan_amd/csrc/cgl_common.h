@@ -84,3 +84,54 @@ __device__ __forceinline__ void cgl_adam_update(float& p, float g, float& m, flo
   const float denom = sqrtf(v) / bc + eps;
   p = p + (-ss) * m / denom;
 }
+
+// outputs 4q .. 4q+3 of the N(0,1) stream (seed, round, stream_id)
+__device__ __forceinline__ void cgl_normal_at(long q, float* out, long n, unsigned long long seed, uint32_t round,
+                                              int stream_id) {
+  if (q * 4 >= n) return;
+  uint32_t c[4] = {(uint32_t)q, (uint32_t)(q >> 32), round, (uint32_t)stream_id};
+  cgl_philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const float inv = 2.3283064365386963e-10f;   // 2^-32
+  float z[4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float u1 = ((float)c[2 * j] + 1.0f) * inv;   // (0, 1]
+    const float u2 = (float)c[2 * j + 1] * inv;
+    const float rr = sqrtf(-2.0f * logf(u1));
+    float s, co;
+    sincosf(6.283185307179586f * u2, &s, &co);
+    z[2 * j] = rr * co;
+    z[2 * j + 1] = rr * s;
+  }
+  for (int j = 0; j < 4; ++j)
+    if (q * 4 + j < n) out[q * 4 + j] = z[j];
+}
+
+// Shuffle sampler: keyed Feistel permutation of [0, n) per data epoch (cycle walking).
+__device__ __forceinline__ uint32_t cgl_hash(uint32_t x, uint32_t k) {
+  x ^= k;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ inline uint32_t cgl_permute(uint32_t i, uint32_t n, uint32_t key) {
+  int bits = 2;
+  while ((1u << bits) < n) ++bits;
+  if (bits & 1) ++bits;
+  const int hb = bits / 2;
+  const uint32_t mask = (1u << hb) - 1;
+  uint32_t x = i;
+  do {
+    uint32_t l = x >> hb, r = x & mask;
+    for (int round = 0; round < 4; ++round) {
+      const uint32_t t = l ^ (cgl_hash(r, key + 0x9e3779b9u * (round + 1)) & mask);
+      l = r;
+      r = t;
+    }
+    x = (l << hb) | r;
+  } while (x >= n);
+  return x;
+}

@@ -1960,6 +1960,8 @@ struct CglMasksArgs {
   long n[CGL_MASKS_MAX];
   unsigned long long ctr[CGL_MASKS_MAX];
   int blk_begin[CGL_MASKS_MAX];
+  const int* rdev;                  // optional device round: counter j = ctr[j] + rstride * (*rdev)
+  unsigned long long rstride;
 };
 
 __global__ __launch_bounds__(256) void cgl_dropout_masks_k(CglMasksArgs) {
@@ -1971,7 +1973,8 @@ __global__ __launch_bounds__(256) void cgl_dropout_masks_k(CglMasksArgs) {
     if (b >= A->blk_begin[j]) q = j;
   const long i = (long)(b - A->blk_begin[q]) * 256 + threadIdx.x;
   if (i >= A->n[q]) return;
-  const unsigned long long ctr = A->ctr[q], seed = A->seed;
+  const unsigned long long ctr = A->ctr[q] + (A->rdev ? A->rstride * (unsigned long long)gldi(A->rdev) : 0ull),
+                           seed = A->seed;
   uint32_t c[4] = {(uint32_t)i, (uint32_t)(i >> 32), (uint32_t)ctr, (uint32_t)(ctr >> 32) ^ 0x5bd1e995u};
   cgl_philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
   const float u = (float)(c[0] >> 8) * (1.0f / 16777216.0f);
@@ -2064,9 +2067,23 @@ struct CglAdamMulti {
   long n[CGL_ADAM_MAXT];
   int blk[CGL_ADAM_MAXT + 1];
   float step_size, bc2sqrt, b2, w1, w2, eps;
+  const int* step_dev;      // optional: completed steps on the device; this update is step *step_dev + 1
+  double lr, beta1, beta2;  //   (its bias corrections computed here as cgl_adam_multi does on the host)
 };
 
 __global__ __launch_bounds__(256) void cgl_adam_multi_k(CglAdamMulti a) {
+  __shared__ float s_sc[2];
+  float step_size = a.step_size, bc2sqrt = a.bc2sqrt;
+  if (a.step_dev) {
+    if (threadIdx.x == 0) {
+      const double st = (double)(gldi(a.step_dev) + 1);
+      s_sc[0] = (float)(a.lr / (1.0 - pow(a.beta1, st)));
+      s_sc[1] = (float)pow(1.0 - pow(a.beta2, st), 0.5);
+    }
+    __syncthreads();
+    step_size = s_sc[0];
+    bc2sqrt = s_sc[1];
+  }
   const int b = blockIdx.x;
   int t = 0;
   for (int q = 1; q < a.nt; ++q)
@@ -2081,8 +2098,37 @@ __global__ __launch_bounds__(256) void cgl_adam_multi_k(CglAdamMulti a) {
   const float vv = __fadd_rn(__fmul_rn(gld(v + i), a.b2), __fmul_rn(__fmul_rn(a.w2, g), g));
   gst(m + i, mm);
   gst(v + i, vv);
-  const float denom = sqrtf(vv) / a.bc2sqrt + a.eps;
-  gst(p + i, gld(p + i) + (-a.step_size) * mm / denom);
+  const float denom = sqrtf(vv) / bc2sqrt + a.eps;
+  gst(p + i, gld(p + i) + (-step_size) * mm / denom);
+}
+
+// ------------------------------------------------------------------------------------------
+// Device-side round state of the fused conv round (ConvGanStep(graph=True)): every per-round value
+// the eager round passes from the host -- the z stream's round, the Dropout2d counters, the Adam
+// steps, the sampler position -- is read from a small device counter block instead, so one captured
+// round replays as a hipGraph; the round's last launch advances the counters.
+__global__ __launch_bounds__(256) void cgl_normal_dev_k(float* out, long n, unsigned long long seed, const int* round,
+                                                        int stream_id) {
+  cgl_normal_at((long)blockIdx.x * 256 + threadIdx.x, out, n, seed, (uint32_t)gldi(round), stream_id);
+}
+
+// real batch of round R: rows R*nrows .. R*nrows + nrows - 1 of the sample stream, data epoch e =
+// pos / per (per = whole batches per pass: drop_last), row = keyed Feistel permutation of [0, n_src)
+// per data epoch (the MLP prologue's sampler); one workgroup per row, float4 copies
+__global__ __launch_bounds__(256) void cgl_sample_rows_k(const float* src, int n_src, int nrows, int rowf,
+                                                         unsigned long long seed, const int* round, float* dst) {
+  const int r = blockIdx.x;
+  const long per = (long)(n_src / nrows) * nrows;
+  const long pos = (long)gldi(round) * nrows + r;
+  const uint32_t ep = (uint32_t)(pos / per), j = (uint32_t)(pos % per);
+  const uint32_t idx = cgl_permute(j, (uint32_t)n_src, (uint32_t)seed ^ (ep * 0x85ebca6bu + 0x1234567u));
+  const f32x4* s4 = (const f32x4*)(src + (long)idx * rowf);
+  f32x4* d4 = (f32x4*)(dst + (long)r * rowf);
+  for (int c = threadIdx.x; c < rowf / 4; c += 256) *(gf4p)(d4 + c) = *(gcf4p)(s4 + c);
+}
+
+__global__ __launch_bounds__(64) void cgl_counters_add_k(int* p, int n, int v) {
+  if ((int)threadIdx.x < n) p[threadIdx.x] += v;
 }
 
 // Real-batch gather of the worker's sampler: dst[r] = src[idx ? idx[r] : row0 + r] (rows of
@@ -3154,8 +3200,9 @@ int cgl_dropout2d_mask(float* mask, int n, int C, double p, unsigned long long s
   return (int)hipGetLastError();
 }
 
-int cgl_dropout2d_masks(int nm, float* const* masks, const int* n, const int* C, double p, unsigned long long seed,
-                        const unsigned long long* counters, void* stream) {
+static int dropout2d_masks_impl(int nm, float* const* masks, const int* n, const int* C, double p,
+                                unsigned long long seed, const unsigned long long* counters, const int* round_dev,
+                                unsigned long long round_stride, void* stream) {
   if (nm < 1 || nm > CGL_MASKS_MAX || !masks || !n || !C || !counters || !(p >= 0.0 && p < 1.0)) return CGL_E_ARG;
   CglMasksArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -3172,8 +3219,15 @@ int cgl_dropout2d_masks(int nm, float* const* masks, const int* n, const int* C,
     a.blk_begin[j] = blk;
     blk += (int)((a.n[j] + 255) / 256);
   }
+  a.rdev = round_dev;
+  a.rstride = round_stride;
   hipLaunchKernelGGL(cgl_dropout_masks_k, dim3(blk), dim3(256), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
+}
+
+int cgl_dropout2d_masks(int nm, float* const* masks, const int* n, const int* C, double p, unsigned long long seed,
+                        const unsigned long long* counters, void* stream) {
+  return dropout2d_masks_impl(nm, masks, n, C, p, seed, counters, nullptr, 0, stream);
 }
 
 int cgl_nchw_to_nhwc(const float* X, float* Y, int n, int c, int hw, void* stream) {
@@ -3224,9 +3278,10 @@ int cgl_gather_rows(const float* src, const int* idx, int64_t row0, int nrows, i
   return (int)hipGetLastError();
 }
 
-int cgl_adam_multi(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
-                   const int64_t* n, int step, double lr, double beta1, double beta2, double eps, void* stream) {
-  if (nt < 1 || nt > CGL_ADAM_MAXT || !p || !g || !m || !v || !n || step < 1) return CGL_E_ARG;
+static int adam_multi_impl(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
+                           const int64_t* n, int step, const int* step_dev, double lr, double beta1, double beta2,
+                           double eps, void* stream) {
+  if (nt < 1 || nt > CGL_ADAM_MAXT || !p || !g || !m || !v || !n) return CGL_E_ARG;
   CglAdamMulti a;
   std::memset(&a, 0, sizeof(a));
   a.nt = nt;
@@ -3246,8 +3301,57 @@ int cgl_adam_multi(int nt, float* const* p, const float* const* g, float* const*
   a.w1 = (float)(1.0 - beta1);
   a.w2 = (float)(1.0 - beta2);
   a.eps = (float)eps;
+  a.step_dev = step_dev;
+  a.lr = lr;
+  a.beta1 = beta1;
+  a.beta2 = beta2;
   if (blk == 0) return 0;
   hipLaunchKernelGGL(cgl_adam_multi_k, dim3(blk), dim3(256), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+int cgl_adam_multi(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
+                   const int64_t* n, int step, double lr, double beta1, double beta2, double eps, void* stream) {
+  if (step < 1) return CGL_E_ARG;
+  return adam_multi_impl(nt, p, g, m, v, n, step, nullptr, lr, beta1, beta2, eps, stream);
+}
+
+int cgl_adam_multi_dev(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
+                       const int64_t* n, const int* step_dev, double lr, double beta1, double beta2, double eps,
+                       void* stream) {
+  if (!step_dev) return CGL_E_ARG;
+  return adam_multi_impl(nt, p, g, m, v, n, 1, step_dev, lr, beta1, beta2, eps, stream);
+}
+
+int cgl_normal_fill_dev(float* out, int64_t n, unsigned long long seed, const int* round_dev, int stream_id,
+                        void* stream) {
+  if (!out || n < 0 || !round_dev) return CGL_E_ARG;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(cgl_normal_dev_k, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, out,
+                     (long)n, seed, round_dev, stream_id);
+  return (int)hipGetLastError();
+}
+
+int cgl_dropout2d_masks_dev(int nm, float* const* masks, const int* n, const int* C, double p,
+                            unsigned long long seed, const unsigned long long* counters, const int* round_dev,
+                            unsigned long long round_stride, void* stream) {
+  if (!round_dev) return CGL_E_ARG;
+  return dropout2d_masks_impl(nm, masks, n, C, p, seed, counters, round_dev, round_stride, stream);
+}
+
+int cgl_sample_rows_dev(const float* src, int n_src, int nrows, int row_floats, unsigned long long seed,
+                        const int* round_dev, float* dst, void* stream) {
+  if (!src || !dst || !round_dev || nrows < 1 || n_src < nrows || row_floats < 4 || row_floats % 4 ||
+      ((uintptr_t)src & 15) || ((uintptr_t)dst & 15))
+    return CGL_E_ARG;
+  hipLaunchKernelGGL(cgl_sample_rows_k, dim3(nrows), dim3(256), 0, (hipStream_t)stream, src, n_src, nrows, row_floats,
+                     seed, round_dev, dst);
+  return (int)hipGetLastError();
+}
+
+int cgl_counters_add(int* p, int n, int v, void* stream) {
+  if (!p || n < 1 || n > 64) return CGL_E_ARG;
+  hipLaunchKernelGGL(cgl_counters_add_k, dim3(1), dim3(64), 0, (hipStream_t)stream, p, n, v);
   return (int)hipGetLastError();
 }
 

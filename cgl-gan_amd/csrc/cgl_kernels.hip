@@ -667,28 +667,6 @@ __device__ void cgl_begin_at(const CglBeginArgs& a, int r) {
 // ------------------------------------------------------------------------------------------
 // Philox4x32-10 counter-based RNG + Box-Muller: out[i] ~ N(0,1), fresh per round.
 
-// outputs 4q .. 4q+3 of the N(0,1) stream (seed, round, stream_id)
-__device__ __forceinline__ void cgl_normal_at(long q, float* out, long n, unsigned long long seed, uint32_t round,
-                                              int stream_id) {
-  if (q * 4 >= n) return;
-  uint32_t c[4] = {(uint32_t)q, (uint32_t)(q >> 32), round, (uint32_t)stream_id};
-  cgl_philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-  const float inv = 2.3283064365386963e-10f;   // 2^-32
-  float z[4];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const float u1 = ((float)c[2 * j] + 1.0f) * inv;   // (0, 1]
-    const float u2 = (float)c[2 * j + 1] * inv;
-    const float rr = sqrtf(-2.0f * logf(u1));
-    float s, co;
-    sincosf(6.283185307179586f * u2, &s, &co);
-    z[2 * j] = rr * co;
-    z[2 * j + 1] = rr * s;
-  }
-  for (int j = 0; j < 4; ++j)
-    if (q * 4 + j < n) out[q * 4 + j] = z[j];
-}
-
 __global__ __launch_bounds__(256) void cgl_normal(float* out, long n, unsigned long long seed, int round,
                                                   int stream_id) {
   cgl_normal_at((long)blockIdx.x * blockDim.x + threadIdx.x, out, n, seed, (uint32_t)round, stream_id);

@@ -1095,35 +1095,6 @@ int build_plan(cgl_gan* c) {
   return CGL_OK;
 }
 
-// Shuffle sampler: keyed Feistel permutation of [0, n) per data epoch (cycle walking).
-__device__ __forceinline__ uint32_t cgl_hash(uint32_t x, uint32_t k) {
-  x ^= k;
-  x *= 0x7feb352dU;
-  x ^= x >> 15;
-  x *= 0x846ca68bU;
-  x ^= x >> 16;
-  return x;
-}
-
-__device__ uint32_t cgl_permute(uint32_t i, uint32_t n, uint32_t key) {
-  int bits = 2;
-  while ((1u << bits) < n) ++bits;
-  if (bits & 1) ++bits;
-  const int hb = bits / 2;
-  const uint32_t mask = (1u << hb) - 1;
-  uint32_t x = i;
-  do {
-    uint32_t l = x >> hb, r = x & mask;
-    for (int round = 0; round < 4; ++round) {
-      const uint32_t t = l ^ (cgl_hash(r, key + 0x9e3779b9u * (round + 1)) & mask);
-      l = r;
-      r = t;
-    }
-    x = (l << hb) | r;
-  } while (x >= n);
-  return x;
-}
-
 // Round prologue: block 0 writes the round's scalars, the next nb_norm blocks draw z, the
 // last blocks draw the real-row indices of this round's local D steps.  Every block reads the
 // completed-round counter, which only the G-Adam tail (a later launch) advances.

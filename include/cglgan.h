@@ -348,6 +348,30 @@ int cgl_gather_rows(const float* src, const int* idx, int64_t row0, int nrows, i
 int cgl_adam_multi(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
                    const int64_t* n, int step, double lr, double beta1, double beta2, double eps, void* stream);
 
+/* ---- device-side round state (graph-replayable fused conv round) ----------------------------
+ * The per-round values the ops above take from the host -- the z stream's round (capgan.py:216,219),
+ * the Dropout2d counters (model/lsgan.py:78), the Adam step (capgan.py:158,312), the sampler position
+ * (capgan.py:282,326-332) -- read from device int32 counters instead, so that one captured round
+ * replays as a hipGraph; cgl_counters_add advances them at the end of the round. */
+/* cgl_normal_fill with round = *round_dev */
+int cgl_normal_fill_dev(float* out, int64_t n, unsigned long long seed, const int* round_dev, int stream_id,
+                        void* stream);
+/* cgl_dropout2d_masks with counter j = counters[j] + round_stride * (*round_dev) */
+int cgl_dropout2d_masks_dev(int nm, float* const* masks, const int* n, const int* C, double p,
+                            unsigned long long seed, const unsigned long long* counters, const int* round_dev,
+                            unsigned long long round_stride, void* stream);
+/* cgl_adam_multi with step = *step_dev + 1 (bias corrections computed on the device) */
+int cgl_adam_multi_dev(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
+                       const int64_t* n, const int* step_dev, double lr, double beta1, double beta2, double eps,
+                       void* stream);
+/* dst[r] = src[perm_e(pos % per)] for r < nrows, pos = (*round_dev) * nrows + r, data epoch e = pos / per
+ * (per = whole batches per pass), perm_e a keyed Feistel permutation of [0, n_src) per data epoch
+ * (DataLoader(shuffle=True) with drop_last semantics); rows of row_floats (% 4 == 0) floats, 16-byte aligned */
+int cgl_sample_rows_dev(const float* src, int n_src, int nrows, int row_floats, unsigned long long seed,
+                        const int* round_dev, float* dst, void* stream);
+/* p[i] += v for i < n (<= 64): advances the device round state */
+int cgl_counters_add(int* p, int n, int v, void* stream);
+
 /* ---- evaluation ------------------------------------------------------------------------------
  * KL score of generated 2-D samples (CGLGAN/2DMG/main.py:63-101 plot_2d): np.histogram2d of the
  * real points (rows r * real_stride of real [., 2]) and of the generated points over

@@ -174,3 +174,34 @@ def test_conv_round_deterministic():
         a.run(real=real)
         b.run(real=real)
     assert torch.equal(a.G.p, b.G.p) and torch.equal(a.D.p, b.D.p)
+
+
+@pytest.mark.parametrize("B", [8, 256])
+def test_conv_round_graph_replay(B):
+    """graph=True: rounds replayed as one captured hipGraph (device-side round state: z round, Dropout2d
+    counters, Adam steps, device sampler) equal the same rounds issued op by op, bitwise -- at the
+    benchmarked B=256 too (the kernel selection bench.py times)."""
+    from cglgan.conv_step import ConvGanStep
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        data = torch.rand(4 * B + 3, 1024, device="cuda", generator=torch.Generator("cuda").manual_seed(3)) * 2 - 1
+        a = ConvGanStep(B, seed=21, data=data, graph=True)
+        b = ConvGanStep(B, seed=21, data=data, graph=True)
+        a.init_default(5, 6)
+        b.init_default(5, 6)
+        for r in range(4):
+            a.run(eager=True)
+            b.run()              # round 0 eager, round 1 captured + replayed, rounds 2-3 replays
+            assert a.round == b.round == r + 1 and a.G.step == b.G.step and a.D.step == b.D.step
+        torch.cuda.synchronize()
+    assert b._cuda_graph is not None
+    assert torch.equal(a.G.p, b.G.p) and torch.equal(a.D.p, b.D.p)
+    assert torch.equal(a.G.m, b.G.m) and torch.equal(a.D.v, b.D.v)
+    assert torch.equal(a.lbuf, b.lbuf) and torch.equal(a.x3, b.x3)
+    assert torch.equal(a.dstate, b.dstate) and a.dstate[:3].tolist() == [4, 4, 4]
+    assert a.G.batches == b.G.batches and a.lam == b.lam
+    for k in a.G.running:
+        assert torch.equal(a.G.running[k], b.G.running[k]), k
+    # the sampler drew real rows of the shard: every image of the last real batch is a row of `data`
+    x = b.x3[:B].reshape(B, 1024)
+    assert all(bool((data == x[i]).all(dim=1).any()) for i in range(B))
