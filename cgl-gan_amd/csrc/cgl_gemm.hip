@@ -143,7 +143,7 @@ struct CglPipe {
 typedef __attribute__((address_space(3))) void cgl_lds_void;
 #define CGL_GL_NS 2        // LDS ring depth of the staged main loop (measured: 2 beats 3 at 64 KB per workgroup)
 
-template <int LAYOUT, int VEC, int TM, int TN, bool SK, bool GL, int DT = 0>
+template <int LAYOUT, int VEC, int TM, int TN, bool SK, bool GL, int DT = 0, bool BNF = false>
 __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d, int bid, float* __restrict__ s_red,
                                               float* __restrict__ s_col, int* __restrict__ s_flag,
                                               float* __restrict__ s_bn, double* __restrict__ s_bnd) {
@@ -632,7 +632,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   // (torch's batch_norm_backward, train mode, as cgl_bn_bwd):
   //   dy = leaky'(post) * acc,  S = sum dy,  D = sum (y - mean) dy   (per column, over all M rows)
   //   dZ = (dy - S / M - (y - mean) D invstd^2 / M) invstd gamma,  dgamma = D invstd,  dbeta = S
-  if (d->bn_fuse == 2) {
+  if (BNF && d->bn_fuse == 2) {   // (BNF: only the fused-BatchNorm instantiation carries these paths)
     const float sl = d->slope;
     float dy[TM][TN][16], yc[TM][TN][16];
     const int ldp = d->bn_ld_post;
@@ -856,7 +856,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   // of stat_gr rows), combined from every row tile's published {sum, M2} partials exactly as
   // cgl_bn_apply does (tile order, double, Chan); row tile 0 writes save_mean / save_invstd and
   // updates the running statistics group by group (the reference's forward-call order)
-  if (d->bn_fuse == 1) {
+  if (BNF && d->bn_fuse == 1) {
     cgl_rendezvous(d->rv_count + tn, (unsigned int)d->tiles_m, d->err);
     const int gr = d->stat_gr;
     const int ng = (M + gr - 1) / gr;          // <= 2 (planner)
@@ -995,7 +995,9 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 // layer side by side).  Separate symbols keep the 1x1 variant's register budget (and so its
 // occupancy) independent of the 2x2 variant's.
 // Dynamic LDS: split-K partials of the waves with wk > 0.
-template <int TM, int TN, bool SK = false, bool GL = false, int DT = CGL_DTYPE_F32>
+// BNF: the instantiation that carries the (opt-in) fused-BatchNorm epilogues (bn_fuse 1 / 2); the
+// default instantiations compile them out, so their register budget is the plain GEMM's.
+template <int TM, int TN, bool SK = false, bool GL = false, int DT = CGL_DTYPE_F32, bool BNF = false>
 __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDesc* __restrict__ descs, int ndesc) {
   extern __shared__ float cgl_dyn_lds[];
   __shared__ float s_col[4 * TN * 32];          // per-column reductions across waves (WM WN <= 4)
@@ -1014,9 +1016,9 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
 #define CGL_BODY(L)                                               \
   do {                                                            \
     if (vec)                                                      \
-      cgl_gemm_body<L, 1, TM, TN, SK, GL, DT>(d, bid, s_red, s_col, s_flag, s_bn, s_bnd);    \
+      cgl_gemm_body<L, 1, TM, TN, SK, GL, DT, BNF>(d, bid, s_red, s_col, s_flag, s_bn, s_bnd);    \
     else                                                          \
-      cgl_gemm_body<L, 0, TM, TN, SK, GL, DT>(d, bid, s_red, s_col, s_flag, s_bn, s_bnd);    \
+      cgl_gemm_body<L, 0, TM, TN, SK, GL, DT, BNF>(d, bid, s_red, s_col, s_flag, s_bn, s_bnd);    \
   } while (0)
   if (layout == 0)
     CGL_BODY(0);

@@ -226,6 +226,7 @@ struct Launch {
   int blk = 1;          // GEMM per-wave block shape (TM = TN = blk)
   bool sk = false;      // GEMM launch holds a split-K problem
   bool gl = false;      // GEMM launch uses the LDS-staged (glds) main loop instantiation
+  bool bnf = false;     // GEMM launch holds a fused-BatchNorm problem (the BNF instantiation)
   int dt = CGL_DTYPE_F32;   // GEMM operand type (cgl_gan_config.gemm_dtype)
 };
 
@@ -235,6 +236,7 @@ hipError_t gemm_lds_attr() {
   if (!done) {
     // advisory on this platform (launches up to the per-CU LDS succeed); never fail on it
     for (const void* fn : {(const void*)cgl_gemm_f32<1, 1>, (const void*)cgl_gemm_f32<2, 2>,
+                           (const void*)cgl_gemm_f32<1, 1, false, false, CGL_DTYPE_F32, true>,
                            (const void*)cgl_gemm_f32<1, 1, false, true>,
                            (const void*)cgl_gemm_f32<1, 1, true>, (const void*)cgl_gemm_f32<2, 2, true>}) {
       for (int kb : {150, 128, 96, 64}) {
@@ -263,8 +265,10 @@ void launch_gemm16(int blk, int grid, int shmem, hipStream_t s, const CglGemmDes
 }
 
 void launch_gemm(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, int n, bool sk = false,
-                 bool gl = false, int dt = CGL_DTYPE_F32) {
-  if (dt == CGL_DTYPE_F16) {
+                 bool gl = false, int dt = CGL_DTYPE_F32, bool bnf = false) {
+  if (bnf) {    // fused BatchNorm: 1x1 blocks, fp32, no split-K (planner)
+    cgl_gemm_f32<1, 1, false, false, CGL_DTYPE_F32, true><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+  } else if (dt == CGL_DTYPE_F16) {
     launch_gemm16<CGL_DTYPE_F16>(blk, grid, shmem, s, d, n, sk);
   } else if (dt == CGL_DTYPE_BF16) {
     launch_gemm16<CGL_DTYPE_BF16>(blk, grid, shmem, s, d, n, sk);
@@ -337,9 +341,35 @@ void choose_ks(CglGemmDesc& d) {
 }
 
 // force_wm: rows per wave-row group fixed (32 * TM * WM == 32 * force_wm); force_t: TM = TN fixed
+// CGL_GEMM_TILE="WM,WN,WK,T" forces one wave arrangement and block shape on every problem the
+// planner tiles freely (tile-search experiments, profiles/r02_gemm_tile_search*.txt; unset = the
+// cost model)
+bool gemm_tile_env(int* o) {
+  static int v[5] = {-1, 0, 0, 0, 0};
+  if (v[0] < 0) {
+    v[0] = 0;
+    const char* e = getenv("CGL_GEMM_TILE");
+    if (e && sscanf(e, "%d,%d,%d,%d", &v[1], &v[2], &v[3], &v[4]) == 4 && v[1] * v[2] * v[3] == 4 &&
+        (v[4] == 1 || v[4] == 2))
+      v[0] = 1;
+  }
+  for (int i = 0; i < 4; ++i) o[i] = v[i + 1];
+  return v[0] == 1;
+}
+
 void choose_tiles(CglGemmDesc& d, int force_wm = 0, int force_t = 0) {
   static const int opts[4][3] = {{2, 2, 1}, {2, 1, 2}, {1, 2, 2}, {1, 1, 4}};
   double best = 1e300;
+  int fe[4];
+  if (!force_wm && !force_t && gemm_tile_env(fe)) {
+    d.WM = fe[0];
+    d.WN = fe[1];
+    d.WK = fe[2];
+    d.TM = d.TN = fe[3];
+    d.tiles_m = (d.M + 32 * fe[3] * fe[0] - 1) / (32 * fe[3] * fe[0]);
+    d.tiles_n = (d.N + 32 * fe[3] * fe[1] - 1) / (32 * fe[3] * fe[1]);
+    return;
+  }
   for (int t = 1; t <= 2; ++t) {
     if (force_t && t != force_t) continue;
     for (auto& o : opts) {
@@ -468,7 +498,8 @@ int gemm_resident(int blk, int shmem) {
   int dev = 0, cus = 0, nb = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
-  const void* fn = blk == 2 ? (const void*)cgl_gemm_f32<2, 2> : (const void*)cgl_gemm_f32<1, 1>;
+  (void)blk;   // fused-BatchNorm launches run the 1x1 BNF instantiation
+  const void* fn = (const void*)cgl_gemm_f32<1, 1, false, false, CGL_DTYPE_F32, true>;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, CGL_GEMM_THREADS, shmem) != hipSuccess) {
     (void)hipGetLastError();
     return 0;
@@ -521,6 +552,9 @@ bool push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
       blk = d.TM;
     }
   }
+  bool fused0 = false;
+  for (auto& d : descs) fused0 = fused0 || d.bn_fuse != 0;
+  if (fused0) blk = 1;   // the BNF instantiation is 1x1
   for (auto& d : descs)
     if (d.TM != blk) choose_tiles(d, 0, blk);
   // LDS-staged main loop: every problem of the launch must qualify (a TN problem beside it would
@@ -574,6 +608,7 @@ bool push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
   }
   L.grid = wg;
   L.shmem = stage;
+  L.bnf = fused;
   if (gl) {
     L.gl = true;
     int st2 = 0;
@@ -734,7 +769,7 @@ int build_plan(cgl_gan* c) {
     e.slope = sl;
     e.C = w.gout[l];
     e.ldc = fo;
-    if (l + 1 < L && g.bn[l] && bn_fuse_enabled()) {
+    if (l + 1 < L && g.bn[l] && bn_fuse_enabled() && cf.gemm_dtype == CGL_DTYPE_F32) {
       // BatchNorm1d(train) + LeakyReLU in this GEMM's epilogue (in-launch rendezvous of each
       // column tile's row tiles) instead of a cgl_bn_apply launch
       CglGemmDesc f = e;
@@ -1038,7 +1073,7 @@ int build_plan(cgl_gan* c) {
       }
       // BatchNorm1d backward in the input-gradient GEMM's epilogue (not at the Mix-G exchange
       // point: there the all-reduce of dA sits between the GEMM and the BatchNorm backward)
-      if (g.bn[l - 1] && cf.exchange_layer != l && bn_fuse_enabled()) {
+      if (g.bn[l - 1] && cf.exchange_layer != l && bn_fuse_enabled() && cf.gemm_dtype == CGL_DTYPE_F32) {
         CglGemmDesc f = n;
         f.bn_fuse = 2;
         f.C = w.gG[l - 1];
@@ -1129,7 +1164,7 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
   }
   switch (L.kind) {
     case K_GEMM:
-      launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, L.count, L.sk, L.gl, L.dt);
+      launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, L.count, L.sk, L.gl, L.dt, L.bnf);
       break;
     case K_HEAD:
       hipLaunchKernelGGL(cgl_head_loss, dim3(L.grid), dim3(256), 0, s, c->ws.head + L.first);
