@@ -125,8 +125,8 @@ def profile_launches(step, world, reps):
 
 def traffic_per_gemm_launch():
     """HBM-side bytes per GEMM dispatch from the committed PMC passes of this build
-    (profiles/r01_traffic.json, made by tools/pmc_traffic.py; None when absent)."""
-    path = os.path.join(ROOT, "profiles", "r01_traffic.json")
+    (profiles/r02_traffic.json, made by tools/pmc_traffic.py; None when absent)."""
+    path = os.path.join(ROOT, "profiles", "r02_traffic.json")
     if not os.path.exists(path):
         return None
     d = json.load(open(path))
@@ -495,7 +495,7 @@ def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None,
                      "achieved": round(gemm_tf, 3), "peak": PEAK_F32_MFMA, "unit": "TFLOP/s",
                      "frac": round(gemm_tf / PEAK_F32_MFMA, 4),
                      "traffic": traffic_per_gemm_launch() if a.model == "mlp" else None,
-                     "traffic_unit": "bytes per GEMM launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/r01_traffic.json)",
+                     "traffic_unit": "bytes per GEMM launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/r02_traffic.json)",
                      "gemm_launches_per_round": gemm_n, "gemm_flops_per_round": gemm_flops,
                      "flops_per_gemm_launch": gemm_flops / max(gemm_n, 1),
                      "avg_gemm_launch_us": round(sum(gemm_us) / max(gemm_n, 1), 3),
