@@ -136,6 +136,20 @@ def traffic_per_gemm_launch():
     return None
 
 
+def mlp_traffic_algorithmic(B, gemm_n):
+    """Compulsory bytes per GEMM launch of the MLP round (SURVEY §8d byte model without its Adam
+    term 28·(P_G+P_D): weight reads, gradient writes, inputs, images and saved activations), spread
+    over the round's GEMM launches.  An upper bound on what the GEMMs must move (it includes the
+    BatchNorm / head passes' share), so traffic / this is a lower bound on the over-fetch."""
+    pg, pd = 1510032, 533762
+    nbytes = (4 * (2 * pg + 4 * pd) + 4 * (pg + pd) + 4 * B * (784 + 2 * 100) + 8 * B * 784
+              + 8 * B * (2 * 1920 + 3 * 768))
+    per = nbytes / max(gemm_n, 1)
+    t = traffic_per_gemm_launch()
+    return {"traffic_algorithmic": round(per), "traffic_ratio": round(t / per, 2) if t else None,
+            "traffic_algorithmic_note": "SURVEY 8d compulsory bytes/round minus the Adam term, / GEMM launches"}
+
+
 def cpu_baseline(a):
     """The CPU oracle (torch-CPU restatement of the reference step) on this host's cores."""
     sys.path.insert(0, ROOT)
@@ -496,6 +510,7 @@ def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None,
                      "frac": round(gemm_tf / PEAK_F32_MFMA, 4),
                      "traffic": traffic_per_gemm_launch() if a.model == "mlp" else None,
                      "traffic_unit": "bytes per GEMM launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/r02_traffic.json)",
+                     **(mlp_traffic_algorithmic(a.batch, gemm_n) if a.model == "mlp" else {}),
                      "gemm_launches_per_round": gemm_n, "gemm_flops_per_round": gemm_flops,
                      "flops_per_gemm_launch": gemm_flops / max(gemm_n, 1),
                      "avg_gemm_launch_us": round(sum(gemm_us) / max(gemm_n, 1), 3),

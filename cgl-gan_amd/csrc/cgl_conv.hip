@@ -1643,10 +1643,11 @@ struct CglFinCache {
   }
   template <class Fn>
   __device__ __forceinline__ double sum(int g, Fn fn) const {
+    // the group is selected, not indexed: a runtime index into v[][] puts the cache in scratch
     double t = 0.0;
 #pragma unroll
     for (int i = 0; i < NI; ++i)
-      if (lane + 256 * i < cnt) t += fn(v[g][i]);
+      if (lane + 256 * i < cnt) t += fn(g ? v[1][i] : v[0][i]);
     return t;
   }
 };
