@@ -376,6 +376,16 @@ def nchw_to_nhwc(x, y, n, c, hw):
     return y
 
 
+def dense1_bwd_data_nhwc(dy, w, dx, n, c, hw):
+    """d/dx of Linear(c*hw, 1) over an NCHW-flattened [n, hw, c] NHWC map, stored NHWC
+    (model/lsgan.py:96-97; replaces dense_bwd_data(K=1) + nchw_to_nhwc)."""
+    _chk(dy, w, dx)
+    if dy.numel() < n or w.numel() < c * hw or dx.numel() < n * c * hw:
+        raise ValueError("dense1_bwd_data_nhwc: tensor too small for the geometry")
+    C.check(C.lib.cgl_dense1_bwd_data_nhwc(_p(dy), _p(w), _p(dx), n, c, hw, _s()), "cgl_dense1_bwd_data_nhwc")
+    return dx
+
+
 def nhwc_to_nchw(x, y, n, c, hw):
     _chk(x, y)
     C.check(C.lib.cgl_nhwc_to_nchw(_p(x), _p(y), n, c, hw, _s()), "cgl_nhwc_to_nchw")

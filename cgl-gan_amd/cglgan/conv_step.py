@@ -169,7 +169,7 @@ class ConvGanStep:
         self.mask_d = [e(B2, co) for _, _, _, co, _ in D_CONVS]    # D step masks (real rows, then fake rows)
         self.mask_g = [e(B, co) for _, _, _, co, _ in D_CONVS]     # G-loss pass masks
         # gradients
-        self.dv, self.dflat = e(B2, 1), e(B2, 512)
+        self.dv = e(B2, 1)
         self.dr = [None] + [e(B2, hw // 2, hw // 2, co) for _, _, _, co, hw in D_CONVS[1:]]
         self.dc = [e(B2, hw // 2, hw // 2, co) for _, _, _, co, hw in D_CONVS]
         self.dq1 = e(B2, 16, 16, 16)
@@ -206,7 +206,6 @@ class ConvGanStep:
             pk.add("D", ck + "f", PD[ck + ".weight"], hw, hw, ci, co, 2, 0)
             pk.add("D", ck + "b", PD[ck + ".weight"], hw, hw, ci, co, 2, 0, dir=1)
         pk.add("D", "advf", PD["adv_layer.weight"], 1, 1, 512, 1, ks=1)
-        pk.add("D", "advb", PD["adv_layer.weight"], 1, 1, 512, 1, ks=1, dir=1)
         self.pk = pk.finalize(dev)
         # G's nn.Linear(100, 8192) (model/lsgan.py:8) on the fused-MLP GEMM kernel, prepared once:
         # forward on [z1; z2] and its weight + bias gradient on the z2 rows
@@ -335,10 +334,9 @@ class ConvGanStep:
     def _d_backward(self, x, n, groups, masks, wgrad, dx):
         P, G = self.D.params, self.D.grads
         bst = set()     # BatchNorms whose backward partials the previous input-gradient conv wrote
-        O.dense_bwd_data(self.dv, P["adv_layer.weight"], self.dflat, n, 512, 1, wp=self.pk["advb"])
+        O.dense1_bwd_data_nhwc(self.dv, P["adv_layer.weight"], self.dr[3], n, 128, 4)
         if wgrad:
             O.dense_bwd_weight(self.dv, self.flat, G["adv_layer.weight"], G["adv_layer.bias"], n, 512, 1)
-        O.nchw_to_nhwc(self.dflat, self.dr[3], n, 128, 4)
         for k in (3, 2, 1, 0):
             ck, bk, ci, co, hw = D_CONVS[k]
             ho = hw // 2

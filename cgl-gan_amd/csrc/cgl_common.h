@@ -33,8 +33,10 @@ __device__ __forceinline__ float cgl_softmax_at(const float* x, int n, int i) {
   return expf(x[i] - mx) / s;
 }
 
-__device__ inline void cgl_weights(int mode, int N, float lam, const float* beta, const float* loss, float* alpha) {
-  float tmp[CGL_MAX_WORKERS], tmp2[CGL_MAX_WORKERS];
+// tmp / tmp2: 2 x CGL_MAX_WORKERS floats of caller scratch -- LDS in every kernel that calls this (per-lane
+// arrays indexed by a runtime N would put the whole kernel on a private scratch segment)
+__device__ inline void cgl_weights(int mode, int N, float lam, const float* beta, const float* loss, float* alpha,
+                                   float* tmp, float* tmp2) {
   if (mode == CGL_W_MEAN) {
     for (int i = 0; i < N; ++i) alpha[i] = 1.f / N;
     return;

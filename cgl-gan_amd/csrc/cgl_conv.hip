@@ -1921,6 +1921,26 @@ __global__ __launch_bounds__(256) void cgl_eltwise(CglEltArgs a) {
   }
 }
 
+// Input gradient of a one-output Linear over a flattened NCHW feature map (the discriminator head,
+// model/lsgan.py:96-97: out.view(B, -1) -> adv_layer), written straight into the NHWC layout of the
+// map: dX[m][s][c] = dY[m] * W[c * hw + s].  One product per element (what the K = 1 GEMM computes),
+// with the view's transpose folded into the store -- one launch instead of a GEMM and a transpose.
+__global__ __launch_bounds__(256) void cgl_dense1_bwd_nhwc_k(const float* __restrict__ dY,
+                                                             const float* __restrict__ W, float* __restrict__ dX,
+                                                             int n, int C, int hw) {
+  const int per = C * hw, q4 = per >> 2;      // C % 4 == 0: a float4 never crosses a pixel
+  const int total = n * q4;
+  for (int q = blockIdx.x * 256 + threadIdx.x; q < total; q += gridDim.x * 256) {
+    const int m = q / q4, e = (q - m * q4) * 4;
+    const int s = e / C, c = e - s * C;
+    const float d = gld(dY + m);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = d * gld(W + (long)(c + j) * hw + s);
+    *(gf4p)(dX + (long)m * per + e) = o;
+  }
+}
+
 // Scalar fallback of mode 2 / 3 for C % 4 != 0 (single-channel tensors: the generator image).
 __global__ __launch_bounds__(256) void cgl_eltwise1(CglEltArgs a) {
   const long n = (long)a.rows * a.C;
@@ -2159,13 +2179,13 @@ struct CglWeightsArgs {
 
 __global__ __launch_bounds__(256) void cgl_weights_scale_k(CglWeightsArgs a) {
   __shared__ float s_alpha;
+  __shared__ float s_l[CGL_MAX_WORKERS], s_al[CGL_MAX_WORKERS], s_t[2][CGL_MAX_WORKERS];
   if (threadIdx.x == 0) {
-    float l[CGL_MAX_WORKERS], al[CGL_MAX_WORKERS];
-    for (int q = 0; q < a.n; ++q) l[q] = gld(a.losses + q);
-    cgl_weights(a.mode, a.n, a.lam, a.beta, l, al);
-    s_alpha = al[a.rank];
+    for (int q = 0; q < a.n; ++q) s_l[q] = gld(a.losses + q);
+    cgl_weights(a.mode, a.n, a.lam, a.beta, s_l, s_al, s_t[0], s_t[1]);
+    s_alpha = s_al[a.rank];
     if (blockIdx.x == 0 && a.alpha_out)
-      for (int q = 0; q < a.n; ++q) gst(a.alpha_out + q, al[q]);
+      for (int q = 0; q < a.n; ++q) gst(a.alpha_out + q, s_al[q]);
   }
   __syncthreads();
   const float al = s_alpha;
@@ -3235,6 +3255,14 @@ int cgl_nchw_to_nhwc(const float* X, float* Y, int n, int c, int hw, void* strea
   if (!X || !Y || n < 1 || c < 1 || hw < 1) return CGL_E_ARG;
   hipLaunchKernelGGL(cgl_transpose_k, dim3((hw + 31) / 32, (c + 31) / 32, n), dim3(256), 0, (hipStream_t)stream, X, Y,
                      c, hw);
+  return (int)hipGetLastError();
+}
+
+int cgl_dense1_bwd_data_nhwc(const float* dY, const float* W, float* dX, int n, int c, int hw, void* stream) {
+  if (!dY || !W || !dX || n < 1 || c < 4 || (c & 3) || hw < 1 || (long)n * c * hw >= (1L << 31)) return CGL_E_ARG;
+  const long q = (long)n * c * hw / 4;
+  const int grid = (int)std::min<long>((q + 255) / 256, 8192);
+  hipLaunchKernelGGL(cgl_dense1_bwd_nhwc_k, dim3(grid), dim3(256), 0, (hipStream_t)stream, dY, W, dX, n, c, hw);
   return (int)hipGetLastError();
 }
 

@@ -677,10 +677,10 @@ __global__ __launch_bounds__(256) void cgl_normal(float* out, long n, unsigned l
 __global__ __launch_bounds__(256) void cgl_alpha_scale(CglStepState* st, const float* losses, float* x,
                                                        long n) {
   __shared__ float s_alpha;
+  __shared__ float al[CGL_MAX_WORKERS], s_t[2][CGL_MAX_WORKERS];
   if (threadIdx.x == 0) {
     const int N = st->n_workers;
-    float al[CGL_MAX_WORKERS];
-    cgl_weights(st->weighting, N, st->lambda, st->beta, losses, al);
+    cgl_weights(st->weighting, N, st->lambda, st->beta, losses, al, s_t[0], s_t[1]);
     s_alpha = al[st->rank];
     if (blockIdx.x == 0) {
       for (int q = 0; q < N; ++q) {

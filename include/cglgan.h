@@ -327,6 +327,10 @@ int cgl_dropout2d_masks(int nm, float* const* masks, const int* n, const int* C,
 /* Layout changes of model/lsgan.py:25 (view(B,128,8,8) of the Linear output) and :96 (view(B,-1)). */
 int cgl_nchw_to_nhwc(const float* X, float* Y, int n, int c, int hw, void* stream);
 int cgl_nhwc_to_nchw(const float* X, float* Y, int n, int c, int hw, void* stream);
+/* Input gradient of the discriminator head Linear(c * hw, 1) (model/lsgan.py:96-97, adv_layer over
+ * out.view(B, -1)) written in the NHWC layout of the [n, hw, c] map: dX[m][s][c] = dY[m] * W[c * hw + s]
+ * (replaces cgl_dense_bwd_data(K = 1) + cgl_nchw_to_nhwc). c % 4 == 0. */
+int cgl_dense1_bwd_data_nhwc(const float* dY, const float* W, float* dX, int n, int c, int hw, void* stream);
 /* Mean adversarial loss of one forward call and weight * its gradient (grad may be null):
  * loss 0 CrossEntropy on 2 logits (capgan.py:311), 1 BCELoss on probabilities
  * (CGLGAN/2DMG/main.py:336), 2 MSELoss (LSGAN objective of model/lsgan.py's D), 3 Sigmoid + BCELoss
