@@ -30,7 +30,7 @@ EXPORTS = [
     # conv GAN path (model/lsgan.py)
     "cgl_conv3x3_workspace_bytes", "cgl_conv3x3_fwd", "cgl_conv3x3_bwd_data", "cgl_conv3x3_bwd_weight",
     "cgl_bn2d_workspace_bytes", "cgl_bn2d_fwd", "cgl_bn2d_bwd", "cgl_act_drop_bwd", "cgl_dropout2d_mask", "cgl_dropout2d_masks",
-    "cgl_nchw_to_nhwc", "cgl_nhwc_to_nchw", "cgl_dense1_bwd_data_nhwc", "cgl_adv_loss", "cgl_adam_multi", "cgl_dense_workspace_bytes",
+    "cgl_nchw_to_nhwc", "cgl_nhwc_to_nchw", "cgl_dense1_bwd_data_nhwc", "cgl_dense1_fwd_nhwc", "cgl_adv_loss", "cgl_adam_multi", "cgl_dense_workspace_bytes",
     "cgl_dense_fwd", "cgl_dense_bwd_data", "cgl_dense_bwd_weight", "cgl_gather_rows", "cgl_weights_scale",
     "cgl_conv_packed_floats", "cgl_conv_pack_multi", "cgl_conv3x3_fwd_packed", "cgl_conv3x3_bwd_data_packed",
     "cgl_dense_fwd_packed", "cgl_dense_bwd_data_packed", "cgl_conv3x3_stat_chunks", "cgl_conv3x3_fwd_packed_stats",
@@ -131,6 +131,7 @@ def _load():
         "cgl_dropout2d_masks": (ci, [ci, P(vp), P(ci), P(ci), cd, ctypes.c_ulonglong, P(ctypes.c_ulonglong), vp]),
         "cgl_nchw_to_nhwc": (ci, [vp, vp, ci, ci, ci, vp]),
         "cgl_dense1_bwd_data_nhwc": (ci, [vp, vp, vp, ci, ci, ci, vp]),
+        "cgl_dense1_fwd_nhwc": (ci, [vp, vp, vp, vp, vp, ci, ci, ci, vp]),
         "cgl_nhwc_to_nchw": (ci, [vp, vp, ci, ci, ci, vp]),
         "cgl_adv_loss": (ci, [vp, ci, ci, ci, ci, cd, vp, vp, vp]),
         "cgl_dense_workspace_bytes": (i64, [ci] * 3),

@@ -376,6 +376,16 @@ def nchw_to_nhwc(x, y, n, c, hw):
     return y
 
 
+def dense1_fwd_nhwc(x, w, b, y, n, c, hw, flat=None):
+    """Linear(c*hw, 1) over the NCHW flattening of an [n, hw, c] NHWC map (model/lsgan.py:96-97), read
+    from the NHWC map -- bitwise nhwc_to_nchw + dense_fwd(N=1); ``flat`` (optional) receives the NCHW view."""
+    _chk(x, w, b, y, flat)
+    if x.numel() < n * c * hw or w.numel() < c * hw or y.numel() < n or (flat is not None and flat.numel() < n * c * hw):
+        raise ValueError("dense1_fwd_nhwc: tensor too small for the geometry")
+    C.check(C.lib.cgl_dense1_fwd_nhwc(_p(x), _p(w), _p(b), _p(y), _p(flat), n, c, hw, _s()), "cgl_dense1_fwd_nhwc")
+    return y
+
+
 def dense1_bwd_data_nhwc(dy, w, dx, n, c, hw):
     """d/dx of Linear(c*hw, 1) over an NCHW-flattened [n, hw, c] NHWC map, stored NHWC
     (model/lsgan.py:96-97; replaces dense_bwd_data(K=1) + nchw_to_nhwc)."""

@@ -205,7 +205,6 @@ class ConvGanStep:
         for ck, _, ci, co, hw in D_CONVS:
             pk.add("D", ck + "f", PD[ck + ".weight"], hw, hw, ci, co, 2, 0)
             pk.add("D", ck + "b", PD[ck + ".weight"], hw, hw, ci, co, 2, 0, dir=1)
-        pk.add("D", "advf", PD["adv_layer.weight"], 1, 1, 512, 1, ks=1)
         self.pk = pk.finalize(dev)
         # G's nn.Linear(100, 8192) (model/lsgan.py:8) on the fused-MLP GEMM kernel, prepared once:
         # forward on [z1; z2] and its weight + bias gradient on the z2 rows
@@ -328,8 +327,10 @@ class ConvGanStep:
             if bk:
                 self._bn_fwd(bk, self.D, self.q[k], self.r[k], n, (hw // 2) ** 2, co, groups, O.ACT_NONE)
                 inp = self.r[k]
-        O.nhwc_to_nchw(self.r[3], self.flat, n, 128, 4)    # out.view(B, -1), model/lsgan.py:96
-        O.dense_fwd(self.flat, P["adv_layer.weight"], P["adv_layer.bias"], self.v, n, 512, 1, wp=self.pk["advf"])
+        # out.view(B, -1) -> adv_layer (model/lsgan.py:96-97) from the NHWC map; the D step's call keeps the
+        # NCHW view for adv_layer's weight gradient, the G-loss pass (no D weight gradient) does not
+        O.dense1_fwd_nhwc(self.r[3], P["adv_layer.weight"], P["adv_layer.bias"], self.v, n, 128, 4,
+                          flat=self.flat if masks is self.mask_d else None)
 
     def _d_backward(self, x, n, groups, masks, wgrad, dx):
         P, G = self.D.params, self.D.grads

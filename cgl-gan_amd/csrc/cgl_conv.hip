@@ -1833,6 +1833,50 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize_sliced(CglBnFinSliced a) 
   }
 }
 
+// The discriminator head forward (model/lsgan.py:96-97: out.view(B, -1) -> adv_layer = Linear(C*hw, 1))
+// read straight from the NHWC map, with the NCHW view's transpose folded into the loads.  The
+// arithmetic is cgl_conv_n1's for this single-tap problem, in its order: lane q owns flat elements
+// 4 (q + 64 b) + j, fma-chained over b then j from 0, lanes combined by the same xor tree, then + bias --
+// so Y is bitwise what nhwc_to_nchw + dense_fwd(N = 1) produced.  `flat` (may be null) receives the
+// NCHW view for adv_layer's weight gradient.
+__global__ __launch_bounds__(256) void cgl_dense1_fwd_nhwc_k(const float* __restrict__ X, const float* __restrict__ W,
+                                                             const float* __restrict__ b, float* __restrict__ Y,
+                                                             float* __restrict__ flat, int n, int C, int hw) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), q = threadIdx.x & 63;
+  if (row >= n) return;                      // wave-uniform
+  const int per = C * hw, nb = per >> 8;     // per % 256 == 0, nb <= 4
+  const float* __restrict__ x = X + (long)row * per;
+  f32x4 v[4], w[4];
+#pragma unroll
+  for (int bb = 0; bb < 4; ++bb) {
+    if (bb < nb) {
+      const int k0 = 4 * (q + 64 * bb);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = (k0 + j) / hw, s = k0 + j - c * hw;
+        v[bb][j] = gld(x + s * C + c);
+      }
+      w[bb] = *(gcf4p)(W + k0);
+    }
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int bb = 0; bb < 4; ++bb)
+    if (bb < nb) {
+      acc = fmaf(v[bb][0], w[bb][0], acc);
+      acc = fmaf(v[bb][1], w[bb][1], acc);
+      acc = fmaf(v[bb][2], w[bb][2], acc);
+      acc = fmaf(v[bb][3], w[bb][3], acc);
+    }
+  for (int o = 1; o < 64; o <<= 1) acc += __shfl_xor(acc, o);
+  if (flat) {
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb)
+      if (bb < nb) *(gf4p)(flat + (long)row * per + 4 * (q + 64 * bb)) = v[bb];
+  }
+  if (q == 0) gst(Y + row, acc + (b ? gld(b) : 0.f));
+}
+
 // Elementwise NHWC passes (float4 over channels; C % 4 == 0):
 //   mode 0  Y = act(X * coef0[g][c] + coef1[g][c])                               (BatchNorm2d apply)
 //   mode 1  dX = (g - coef0[g][c] - (X - mean[g][c]) coef1[g][c]) invstd[g][c] gamma[c],
@@ -3255,6 +3299,17 @@ int cgl_nchw_to_nhwc(const float* X, float* Y, int n, int c, int hw, void* strea
   if (!X || !Y || n < 1 || c < 1 || hw < 1) return CGL_E_ARG;
   hipLaunchKernelGGL(cgl_transpose_k, dim3((hw + 31) / 32, (c + 31) / 32, n), dim3(256), 0, (hipStream_t)stream, X, Y,
                      c, hw);
+  return (int)hipGetLastError();
+}
+
+int cgl_dense1_fwd_nhwc(const float* X, const float* W, const float* b, float* Y, float* flat, int n, int c, int hw,
+                        void* stream) {
+  const long per = (long)c * hw;
+  if (!X || !W || !Y || n < 1 || c < 1 || hw < 1 || per % 256 || per > 1024 || (long)n * per >= (1L << 31) || !al16(W) ||
+      (flat && !al16(flat)))
+    return CGL_E_ARG;
+  hipLaunchKernelGGL(cgl_dense1_fwd_nhwc_k, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, X, W, b, Y, flat, n, c,
+                     hw);
   return (int)hipGetLastError();
 }
 

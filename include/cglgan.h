@@ -331,6 +331,11 @@ int cgl_nhwc_to_nchw(const float* X, float* Y, int n, int c, int hw, void* strea
  * out.view(B, -1)) written in the NHWC layout of the [n, hw, c] map: dX[m][s][c] = dY[m] * W[c * hw + s]
  * (replaces cgl_dense_bwd_data(K = 1) + cgl_nchw_to_nhwc). c % 4 == 0. */
 int cgl_dense1_bwd_data_nhwc(const float* dY, const float* W, float* dX, int n, int c, int hw, void* stream);
+/* Forward of the same head from the NHWC map: Y[m] = b + sum_k flat[m][k] W[k], flat[m][c * hw + s] =
+ * X[m][s][c], bitwise what cgl_nhwc_to_nchw + cgl_dense_fwd(N = 1) give; flat (may be null) receives the
+ * NCHW view (model/lsgan.py:96 out.view(B, -1)). b may be null. c * hw % 256 == 0, <= 1024. */
+int cgl_dense1_fwd_nhwc(const float* X, const float* W, const float* b, float* Y, float* flat, int n, int c, int hw,
+                        void* stream);
 /* Mean adversarial loss of one forward call and weight * its gradient (grad may be null):
  * loss 0 CrossEntropy on 2 logits (capgan.py:311), 1 BCELoss on probabilities
  * (CGLGAN/2DMG/main.py:336), 2 MSELoss (LSGAN objective of model/lsgan.py's D), 3 Sigmoid + BCELoss

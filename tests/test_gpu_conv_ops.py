@@ -309,3 +309,36 @@ def test_adam_multi_matches_torch_single_tensor():
         close(a, b, rel=1e-6, what="param")
         close(m, mr, rel=1e-6, what="exp_avg")
         close(v, vr, rel=1e-6, what="exp_avg_sq")
+
+
+@pytest.mark.parametrize("n", [1, 8, 512])
+def test_dense1_head_nhwc_bitwise(n):
+    """D head of model/lsgan.py:96-97 (out.view(B, -1) -> Linear(512, 1)) from the NHWC 2x2x128 map:
+    cgl_dense1_fwd_nhwc equals nhwc_to_nchw + dense_fwd(N=1) bit for bit (and writes the same view),
+    cgl_dense1_bwd_data_nhwc equals dense_bwd_data(K=1) + nchw_to_nhwc bit for bit, both close to fp64."""
+    O = ops()
+    g = torch.Generator(device="cpu").manual_seed(n)
+    x = torch.randn(n, 2, 2, 128, generator=g).to(DEV)
+    w = (torch.randn(1, 512, generator=g) * 0.05).to(DEV)
+    b = torch.randn(1, generator=g).to(DEV)
+    dy = torch.randn(n, 1, generator=g).to(DEV)
+    flat = torch.empty(n, 512, device=DEV)
+    y_old = torch.empty(n, 1, device=DEV)
+    O.nhwc_to_nchw(x, flat, n, 128, 4)
+    O.dense_fwd(flat, w, b, y_old, n, 512, 1)
+    y_new, flat_new = torch.empty(n, 1, device=DEV), torch.full((n, 512), float("nan"), device=DEV)
+    O.dense1_fwd_nhwc(x, w, b, y_new, n, 128, 4, flat=flat_new)
+    y_noflat = torch.empty(n, 1, device=DEV)
+    O.dense1_fwd_nhwc(x, w, b, y_noflat, n, 128, 4)
+    dflat, dx_old = torch.empty(n, 512, device=DEV), torch.empty(n, 2, 2, 128, device=DEV)
+    O.dense_bwd_data(dy, w, dflat, n, 512, 1)
+    O.nchw_to_nhwc(dflat, dx_old, n, 128, 4)
+    dx_new = torch.empty(n, 2, 2, 128, device=DEV)
+    O.dense1_bwd_data_nhwc(dy, w, dx_new, n, 128, 4)
+    torch.cuda.synchronize()
+    assert torch.equal(y_new, y_old) and torch.equal(y_noflat, y_old)
+    assert torch.equal(flat_new, flat)
+    assert torch.equal(dx_new, dx_old)
+    xr = nchw(x.cpu().double()).reshape(n, 512)
+    close(y_new, xr @ w.cpu().double().t() + b.cpu().double(), what="head fwd")
+    close(dx_new, nhwc((dy.cpu().double() @ w.cpu().double()).reshape(n, 128, 2, 2)), what="head bwd")
