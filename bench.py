@@ -150,11 +150,40 @@ def mlp_traffic_algorithmic(B, gemm_n):
             "traffic_algorithmic_note": "SURVEY 8d compulsory bytes/round minus the Adam term, / GEMM launches"}
 
 
+def host_info(threads):
+    """the host the CPU baseline ran on -- CPU model, logical CPUs of the machine and of
+    this process's affinity mask, the torch threads actually used, torch version."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return {"cpu_model": model, "host_logical_cpus": os.cpu_count(), "affinity_cpus": affinity,
+            "threads": threads, "torch": torch.__version__}
+
+
+def cpu_threads():
+    """Torch threads of the CPU leg: the process's CPU share, at most 16 (the GPU box's per-GPU share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def cpu_baseline(a):
     """The CPU oracle (torch-CPU restatement of the reference step) on this host's cores."""
     sys.path.insert(0, ROOT)
     from oracle import gan_oracle as O
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     G, workers = O.build_capgan(1)
     srv = O.CapganServer(G, torch.tensor([1.0]))
@@ -172,7 +201,7 @@ def cpu_baseline(a):
         if (n > warm and t_total >= a.cpu_seconds) or n >= 2000:
             break
     rounds = n - warm
-    return {"value": round(B * rounds / t_total, 1), "unit": "images/s", "cores": threads, "kind": "port",
+    return {"value": round(B * rounds / t_total, 1), "unit": "images/s", "cores": threads, "kind": "port", "host": host_info(threads),
             "sample": f"{rounds} CAPGAN rounds (B={B}, N=1) of the torch-CPU oracle after {warm} warm-up "
                       f"rounds, {t_total:.1f} s, torch {torch.__version__}"}
 
@@ -243,7 +272,7 @@ def conv_cpu_baseline(a):
     """The conv oracle (torch-CPU restatement of the model/lsgan.py round) on this host's cores."""
     sys.path.insert(0, ROOT)
     from oracle import conv_oracle as CV
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     torch.manual_seed(20211212)
     gp, gb = CV.init_params(CV.G_SPEC)
@@ -265,7 +294,7 @@ def conv_cpu_baseline(a):
         if (n > warm and t_total >= a.cpu_seconds) or n >= 200:
             break
     rounds = n - warm
-    return {"value": round(B * rounds / t_total, 2), "unit": "images/s", "cores": threads, "kind": "port",
+    return {"value": round(B * rounds / t_total, 2), "unit": "images/s", "cores": threads, "kind": "port", "host": host_info(threads),
             "sample": f"{rounds} conv-GAN CAPGAN rounds (model/lsgan.py, B={B}, N=1, {a.loss}) of the torch-CPU "
                       f"oracle after {warm} warm-up round, {t_total:.1f} s, torch {torch.__version__}"}
 
@@ -425,7 +454,7 @@ def cpu_rounds(kind, B, seconds):
     sys.path.insert(0, ROOT)
     from cglgan.data import gmm
     from oracle import gan_oracle as O
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     if kind == "ring":
         G, ws = O.build_ring(1, 1)
@@ -455,7 +484,7 @@ def cpu_rounds(kind, B, seconds):
         if (n > warm and t_total >= seconds) or n >= 20000:
             break
     rounds = n - warm
-    return {"value": round(B * rounds / t_total, 1), "unit": "images/s", "cores": threads, "kind": "port",
+    return {"value": round(B * rounds / t_total, 1), "unit": "images/s", "cores": threads, "kind": "port", "host": host_info(threads),
             "sample": f"{rounds} {kind} rounds (B={B}, N=1) of the torch-CPU oracle after {warm} warm-up rounds, "
                       f"{t_total:.1f} s, torch {torch.__version__}"}
 

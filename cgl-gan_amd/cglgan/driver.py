@@ -199,12 +199,35 @@ def gpu_step(cfg: DriverConfig, topo: Topology, shard: torch.Tensor, beta, g_sd,
     return step
 
 
+def capgan_cloud_schedule(cfg: DriverConfig, srv_lens, server: int):
+    """The Cloud schedule of a multi-server CAPGAN run (capgan.py:169, Cloud.run :99-117).
+
+    Each reference server syncs before rounds with t % (data_len * cloud_epoch / batch_size) == 0,
+    data_len = ITS OWN shard total, and the Cloud averages whichever ``num_servers`` puts arrive
+    next.  Servers with different shard totals therefore sync on different rounds and a different
+    number of times: the Cloud pairs one server's puts with each other (``p[idx]`` overwritten) and a
+    server blocks forever on its cache -- the reference hangs.  Here every Cloud step is a world
+    all-reduce, so all servers must fire on the same rounds: the schedule is used when every
+    server's period gives the same set of rounds over the run, and such a run is refused otherwise
+    (equal-size servers -- iid 0 -- or ``cloud_epoch = 0`` keep it well defined)."""
+    from .exchange import capgan_cloud_due
+    dues = [capgan_cloud_due(cfg.num_communication, float(n), cfg.cloud_epoch, cfg.batch_size) for n in srv_lens]
+    if len(set(srv_lens)) > 1:
+        fire = [[r for r in range(cfg.num_communication) if d(r)] for d in dues]
+        if any(f != fire[0] for f in fire[1:]):
+            raise ValueError(
+                "capgan with num_servers > 1: the servers' Cloud periods t % (data_len * cloud_epoch / batch_size) "
+                f"differ (server shard totals {list(srv_lens)}); the reference Cloud deadlocks on such a run "
+                "(capgan.py:108-117, :169-175). Use equal-size servers (iid 0), cloud_epoch 0, or algo mixg.")
+    return dues[server]
+
+
 class Driver:
     """One worker process of a CAPGAN / Mix-G / MD-GAN run (see module docstring)."""
 
     def __init__(self, cfg: DriverConfig, rank: int = None, world: int = None, step_factory=None, device=None):
         from .data import beta_weights, cloud_weights
-        from .exchange import DistComm, WorkerExchange, capgan_cloud_due, mixg_cloud_due
+        from .exchange import DistComm, WorkerExchange, mixg_cloud_due
         from .init import topology_state
         self.cfg = cfg.validate()
         dist_on = dist.is_available() and dist.is_initialized()
@@ -233,7 +256,7 @@ class Driver:
             if cfg.algo == "mixg":
                 due = mixg_cloud_due(cfg.num_communication, cfg.cloud_epoch)
             else:
-                due = capgan_cloud_due(cfg.num_communication, data_len, cfg.cloud_epoch, cfg.batch_size)
+                due = capgan_cloud_schedule(cfg, srv_lens, topo.server)
                 scope = "all"
         # one weight per member of the cloud group (the world): A_s / H on each replica of server s
         cw = [A[r // topo.heads] / topo.heads for r in range(self.world)]

@@ -26,6 +26,7 @@ tests).  Both expose the same three collectives, so ``WorkerExchange`` is writte
 """
 from __future__ import annotations
 
+import os
 import random
 
 import torch
@@ -137,7 +138,9 @@ class WorkerExchange:
             self.comm.all_gather(s.losses_all, s.own_loss())
             s.alpha_scale()
             self.comm.all_reduce_sum(s.exchange_buffer())
-            side = self._side_stream() if (share or swap) else None
+            # (not beside the opt-in fused-BatchNorm GEMMs: their in-launch rendezvous needs every
+            # workgroup of the launch co-resident, which side-stream kernels holding CUs can break)
+            side = self._side_stream() if (share or swap) and not _bn_fuse_on() else None
             if side is not None:
                 # phase B (G backward + Adam G) never touches D: the E-share all-reduce / D-swap of
                 # this round's updated D run on a side stream concurrently with it (issued in the
@@ -189,6 +192,10 @@ class WorkerExchange:
             self.cloud.all_reduce_mean(t, self.cloud_weights)
             if own is not None:     # segema * self_p + (1 - segema) * recv_p, in that order
                 torch.add(own * self.segema, t * (1.0 - self.segema), out=t)
+
+
+def _bn_fuse_on():
+    return os.environ.get("CGL_BN_FUSE", "0") not in ("", "0")
 
 
 def mixg_cloud_due(num_communication: int, cloud_epoch: int):
@@ -288,13 +295,14 @@ class ConvWorkerExchange:
     BatchNorm running statistics; D-swap moves both (the reference's copy_parameters keeps every
     non-scalar state-dict entry, MDGAN/MNIST/mdgan.py:233-238)."""
 
-    def __init__(self, step, comm=None, share_every: int = 0, swap_every: int = 0):
+    def __init__(self, step, comm=None, share_every: int = 0, swap_every: int = 0, server_rank: int = 0):
         self.step, self.comm = step, comm
         self.share_every, self.swap_every = share_every, swap_every
         n = comm.size if comm is not None else 1
         if n != step.n_workers:
             raise ValueError(f"step planned for {step.n_workers} workers, group has {n}")
-        self.dswap = DSwap(n) if (comm is not None and swap_every > 0) else None
+        # the server's own generator, Random(server_rank + 100) (MDGAN/MNIST/mdgan.py:122-123), as WorkerExchange
+        self.dswap = DSwap(n, server_rank) if (comm is not None and swap_every > 0) else None
 
     def _d_state(self):
         return [self.step.D.p] + list(self.step.D.running.values())

@@ -3314,7 +3314,8 @@ int cgl_dense1_fwd_nhwc(const float* X, const float* W, const float* b, float* Y
 }
 
 int cgl_dense1_bwd_data_nhwc(const float* dY, const float* W, float* dX, int n, int c, int hw, void* stream) {
-  if (!dY || !W || !dX || n < 1 || c < 4 || (c & 3) || hw < 1 || (long)n * c * hw >= (1L << 31)) return CGL_E_ARG;
+  if (!dY || !W || !dX || n < 1 || c < 4 || (c & 3) || hw < 1 || (long)n * c * hw >= (1L << 31) || !al16(dX))
+    return CGL_E_ARG;   // (the kernel stores float4 into dX)
   const long q = (long)n * c * hw / 4;
   const int grid = (int)std::min<long>((q + 255) / 256, 8192);
   hipLaunchKernelGGL(cgl_dense1_bwd_nhwc_k, dim3(grid), dim3(256), 0, (hipStream_t)stream, dY, W, dX, n, c, hw);

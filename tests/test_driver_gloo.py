@@ -190,3 +190,19 @@ def test_driver_config_knobs_and_cli():
     import pytest
     with pytest.raises(ValueError):
         D.DriverConfig(num_workers=10, num_servers=3).validate()
+
+
+def test_capgan_multi_server_cloud_schedule():
+    """ADVICE r2: capgan servers with different shard totals sync on different rounds (capgan.py:169);
+    the world all-reduce Cloud refuses such a run instead of pairing mismatched rounds (or hanging)."""
+    import pytest
+
+    from cglgan.driver import capgan_cloud_schedule
+    cfg = _cfg(algo="capgan", num_workers=4, num_servers=2, num_communication=40, batch_size=10, cloud_epoch=1)
+    due = capgan_cloud_schedule(cfg, [100.0, 100.0], 1)        # period 10: rounds with t % 10 == 0
+    assert [r for r in range(40) if due(r)] == [0, 10, 20, 30]
+    with pytest.raises(ValueError, match="periods"):
+        capgan_cloud_schedule(cfg, [100.0, 150.0], 0)
+    # different totals whose schedules coincide over the run are accepted (both never fire)
+    due = capgan_cloud_schedule(cfg, [1001.0, 1003.0], 0)
+    assert not any(due(r) for r in range(40))
