@@ -10,7 +10,15 @@ inputs: z (drawn on device, read back), the real batch, and the Dropout2d scales
 i.e. it is within 1e-5 relative of exact, or at least as close to exact as (4x) the reference's
 fp32 computation -- the yardstick for quantities that fp32 itself cannot resolve (LeakyReLU
 kinks hit by rounding, the analytically-zero gradient of a conv bias that feeds BatchNorm2d).
+
+A bias gradient that is one long cancelling sum (``conv_blocks.8.bias``: the sum of the Tanh-input
+gradient over all B x 32 x 32 output pixels) is judged against fp64 by the error bound of the sum
+itself, 2 log2(n) eps32 sum|terms| (a tree-ordered fp32 sum of n terms), as a third admissible
+bound: the fp32 oracle's own error on such a sum is a matter of luck in its summation order, so a
+MORE accurate kernel could fail "4x the fp32 oracle's error" (VERDICT r2, weak #8).
 """
+import math
+
 import pytest
 import torch
 
@@ -30,6 +38,23 @@ def _check(name, hip, o64, o32, fails, tol=STEP_TOL):
     bound = max(tol * float(o64.detach().double().norm()), 4 * _err(o32, o64), 1e-12)
     if e > bound:
         fails.append(f"{name}: err {e:.3e} > bound {bound:.3e} (fp32 oracle err {_err(o32, o64):.3e})")
+
+
+EPS32 = 2.0 ** -24
+SUM_BIASES = {"conv_blocks.8.bias"}   # bias gradient = one sum over every output pixel
+
+
+def sum_bound(terms):
+    """fp32 error bound of a tree-ordered sum of ``terms`` (float tensor): 2 log2(n) eps sum|t|."""
+    n = terms.numel()
+    return 2 * math.log2(max(n, 2)) * EPS32 * float(terms.detach().double().abs().sum())
+
+
+def _check_sum(name, hip, o64, o32, terms, fails):
+    e = _err(hip, o64)
+    bound = max(STEP_TOL * float(o64.detach().double().norm()), 4 * _err(o32, o64), sum_bound(terms), 1e-12)
+    if e > bound:
+        fails.append(f"{name}: err {e:.3e} > bound {bound:.3e} (sum bound {sum_bound(terms):.3e})")
 
 
 SIGN_TOL = 2e-5   # |x| / std below which a GPU LeakyReLU branch may differ from fp64's (parity_helpers)
@@ -131,6 +156,9 @@ def test_conv_round_parity(B, loss):
     _check("Xg", st.xg().permute(0, 3, 1, 2), r64["Xg"], r32["Xg"], fails)
     for k, v in r64["g_grads"].items():
         if k in PRE_BN_BIAS:
+            continue
+        if k in SUM_BIASES:
+            _check_sum("G grad " + k, gg[k], v, r32["g_grads"][k], st.dc3g, fails)
             continue
         _check("G grad " + k, gg[k], v, r32["g_grads"][k], fails)
     for k, v in r64["d_grads"].items():
