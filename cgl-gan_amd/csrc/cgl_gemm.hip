@@ -1,7 +1,8 @@
 // fp32 MFMA GEMM for the MLP GAN step (gfx950, v_mfma_f32_32x32x2_f32).
 //
 // Replaces the reference's implicit cuBLAS addmm / mm calls of nn.Linear forward and
-// autograd backward (model/mnist_model.py:11,22,77,79,81).
+// autograd backward (model/mnist_model.py:11,22,77,79,81), with the
+// BatchNorm1d(train) + LeakyReLU of model/mnist_model.py:13-14 folded into the operand loads.
 //
 // Design (MI355X-first, not a CUDA tiling):
 //  * one wave owns TM x TN 32x32 f32 MFMA accumulators (1x1 for small problems, 2x2 for the
@@ -13,12 +14,22 @@
 //  * operands are loaded straight into the MFMA fragment registers.  The k index of the
 //    32x32x2 fragment is permuted so that lane half h owns 8 CONSECUTIVE k of every 16-k
 //    chunk: a k-contiguous operand is then two float4 loads per lane per 8 MFMAs;
+//  * A-operand transforms applied between the load and the MFMA (no separate launch):
+//      a_bn 1  BatchNorm1d(train) + LeakyReLU of a k-contiguous A (the previous layer's Linear
+//              output): the workgroup prologue combines the producer GEMM's per-tile {sum, M2}
+//              partials of the forward call its rows belong to into scale / shift per k (LDS);
+//              workgroup 0 also writes the saved mean / invstd and the running statistics;
+//      a_bn 2  BatchNorm1d backward of A = dy (the LeakyReLU'-masked gradient the previous GEMM
+//              stored with its {sum dy, sum (y - mean) dy} partials): dZ = (dy - S/M - (y - mean)
+//              D invstd^2 / M) invstd gamma per k (k-contiguous A) or per m (m-contiguous A),
+//              the BatchNorm input y streamed beside A; workgroup 0 writes dgamma / dbeta;
 //  * prologue fusion: the A operand rows can be gathered through an index list (the sampled
-//    real batch) from two sources (real rows, then generated rows) and written out once;
+//    real batch) from two sources (real rows, then generated rows) and written out once
+//    (the copy-out of each 16-k chunk is spread over the workgroups that load it);
 //  * epilogue fusion: bias, LeakyReLU / Tanh, LeakyReLU' mask, Tanh' (1 - t^2), the
-//    bias-gradient column (B's extra all-ones column), and per-column {sum, M2} partials of
-//    the stored output for the next layer's BatchNorm, grouped per forward call (combined by
-//    cgl_bn_apply, cgl_kernels.hip).
+//    bias-gradient column (B's extra all-ones column), per-column {sum, M2} partials of the
+//    stored output for the next layer's forward BatchNorm, and per-column {sum dy,
+//    sum (y - mean) dy} partials of the stored gradient for its backward BatchNorm.
 #include "cgl_internal.h"
 
 #include <type_traits>
@@ -91,40 +102,179 @@ __device__ __forceinline__ void cgl_mask(float v[8], bool ok, int k, int K) {
   for (int j = 0; j < 8; ++j) v[j] = (ok && k + j < K) ? v[j] : 0.f;
 }
 
-
 // ------------------------------------------------------------------------------------------
-// In-launch rendezvous of the tiles_m workgroups of one column tile (fused BatchNorm).
-// Published words are written with agent-scope atomic (sc1, write-through) stores and drained
-// before the ticket; the ticket counter is monotonic (zero at workspace creation, every launch
-// adds exactly n per column tile), so target = the next multiple of n above this workgroup's
-// ticket and no per-call reset is needed; one lane polls relaxed with s_sleep, then ONE
-// every reader loads the published words with agent-scope atomic (sc1) loads, so the poll needs
-// no agent acquire (cdna_hip_programming.md Guideline 16, the all-sc1 form).  Requires the launch's workgroups co-resident (the
-// planner checks the grid against the occupancy); the spin is bounded and a timeout sets *err.
-__device__ __forceinline__ void cgl_rendezvous(unsigned int* cnt, unsigned int n, unsigned int* err) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // every wave's publish stores have landed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned int old = __hip_atomic_fetch_add((cgl_gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned int target = old - old % n + n;
-    unsigned int spins = 0;
-    while ((int)(__hip_atomic_load((cgl_gu32*)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 21)) {
-        __hip_atomic_store((cgl_gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
+// BatchNorm statistics of group g for Q features k[q] (k[q] < 0: unused) from the producer
+// partials: the exact parallel combination of per-tile {S_t, M2_t} over c_t rows, in double
+// like torch's CPU kernel and in a fixed tile order,
+//   mean = sum_t S_t / n,   M2 = sum_t (M2_t + c_t (S_t / c_t - mean)^2).
+// Fast path (<= 8 tiles per group): every {S_t, M2_t} pair of the Q features is loaded up front
+// as one 8-byte load, so the whole computation costs a single memory round trip.
+template <int Q>
+__device__ __forceinline__ void cgl_bn_stats(const CglBnFwd& bn, int K, const int (&k)[Q], int g, double (&mean)[Q],
+                                             double (&m2)[Q], int& n) {
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  const int r0 = g * bn.gr, r1 = min(r0 + bn.gr, bn.mtot);
+  n = r1 - r0;
+  const int t0 = r0 / bn.part_bm, t1 = (r1 - 1) / bn.part_bm;
+  const int nt = t1 - t0 + 1;
+  if (nt <= 8) {
+    f32x2 pr[Q][8];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int kk = max(k[q], 0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int t = t0 + min(j, nt - 1);
+        const int slot = (t * bn.part_bm < r0) ? 1 : 0;   // tile starts in the previous group
+        pr[q][j] = *(const CGL_GLOBAL f32x2*)(bn.part + ((long)(t * 2 + slot) * K + kk) * 2);
       }
     }
-    // every handed-off word is read with an sc1 (agent-scope atomic) load, so no agent acquire
-    // (buffer_inv) is needed -- only the compiler must not hoist those loads above the poll
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      double s = 0.0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j < nt) s += (double)pr[q][j][0];
+      const double mu = s / n;
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (j < nt) {
+          const int t = t0 + j;
+          const int c = min((t + 1) * bn.part_bm, r1) - max(t * bn.part_bm, r0);
+          const double dd = (double)pr[q][j][0] / c - mu;
+          acc += (double)pr[q][j][1] + c * dd * dd;
+        }
+      }
+      mean[q] = mu;
+      m2[q] = acc;
+    }
+    return;
   }
-  __syncthreads();
+  for (int q = 0; q < Q; ++q) {
+    const int kk = max(k[q], 0);
+    double s = 0.0;
+    for (int t = t0; t <= t1; ++t) {
+      const int slot = (t * bn.part_bm < r0) ? 1 : 0;
+      s += (double)gld(bn.part + ((long)(t * 2 + slot) * K + kk) * 2);
+    }
+    const double mu = s / n;
+    double acc = 0.0;
+    for (int t = t0; t <= t1; ++t) {
+      const int slot = (t * bn.part_bm < r0) ? 1 : 0;
+      const float* pp = bn.part + ((long)(t * 2 + slot) * K + kk) * 2;
+      const int c = min((t + 1) * bn.part_bm, r1) - max(t * bn.part_bm, r0);
+      const double dd = (double)gld(pp) / c - mu;
+      acc += (double)gld(pp + 1) + c * dd * dd;
+    }
+    mean[q] = mu;
+    m2[q] = acc;
+  }
 }
-#define CGL_BN_MAXT 32     // row tiles per column tile a fused BatchNorm combines (tiles_m <= 32)
-#define CGL_BN_STG 4       // staged partial items per thread: tiles_m x tile columns <= 1024
-// dynamic LDS a fused-BatchNorm problem needs for its staged partials (bytes)
-inline int cgl_bn_stage_bytes(int tiles_m, int ncw) { return tiles_m * ncw * 16; }
+
+// a_bn 1 prologue: scale / shift of every k of this workgroup's forward call g into the LDS
+// tables t_sc / t_sh (torch's arithmetic: invstd = 1 / sqrt(var_biased + eps), scale = invstd
+// gamma, shift = beta - mean scale); workgroup 0 (lead) combines every call -- in the reference's
+// call order (Xd then Xg) -- to write the saved mean / invstd and update the running statistics.
+__device__ __forceinline__ void cgl_abn_fwd_prologue(const CglBnFwd& bn, int K, int g, bool lead, float* t_sc,
+                                                     float* t_sh) {
+  // every {sum, M2} pair this thread needs (Q features x <= 8 tiles) is loaded at once: one memory
+  // round trip per forward call (the register peak is here, not in the main loop)
+  const int tid = threadIdx.x;
+  const int ng = (bn.mtot + bn.gr - 1) / bn.gr;     // <= 2 (planner)
+  constexpr int Q = CGL_BN_MAXF / 256;
+  int k[Q];
+  float rm[Q], rv[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    k[q] = tid + 256 * q < K ? tid + 256 * q : -1;
+    rm[q] = rv[q] = 0.f;
+  }
+  if (lead && bn.run_mean) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+      if (k[q] >= 0) {
+        rm[q] = gld(bn.run_mean + k[q]);
+        rv[q] = gld(bn.run_var + k[q]);
+      }
+  }
+  for (int gg = 0; gg < ng; ++gg) {
+    if (!lead && gg != g) continue;
+    double mean[Q], m2[Q];
+    int n;
+    cgl_bn_stats<Q>(bn, K, k, gg, mean, m2, n);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      if (k[q] < 0) continue;
+      const double invstd = 1.0 / sqrt(m2[q] / n + bn.eps);
+      if (gg == g) {
+        const float sc = (float)invstd * gld(bn.gamma + k[q]);
+        t_sc[k[q]] = sc;
+        t_sh[k[q]] = gld(bn.beta + k[q]) - (float)mean[q] * sc;
+      }
+      if (lead) {
+        if (bn.save_mean) {
+          gst(bn.save_mean + (long)gg * K + k[q], (float)mean[q]);
+          gst(bn.save_invstd + (long)gg * K + k[q], (float)invstd);
+        }
+        if (bn.run_mean) {
+          const double mom = bn.momentum;
+          rm[q] = (float)(mom * mean[q] + (1.0 - mom) * (double)rm[q]);
+          rv[q] = (float)(mom * (m2[q] / (n - 1)) + (1.0 - mom) * (double)rv[q]);
+        }
+      }
+    }
+  }
+  if (lead && bn.run_mean) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+      if (k[q] >= 0) {
+        gst(bn.run_mean + k[q], rm[q]);
+        gst(bn.run_var + k[q], rv[q]);
+      }
+  }
+}
+
+// a_bn 2 prologue: per feature f in [f0, f1) the backward coefficients of torch's
+// batch_norm_backward (train) from the producer's per-row-tile {sum dy, sum (y - mean) dy}
+// partials (tile order, double): mean, invstd, gamma, S / M, D invstd^2 / M (as cgl_bn_bwd
+// computes them, in float); lead: dgamma = D invstd, dbeta = S.
+__device__ __forceinline__ void cgl_abn_bwd_prologue(const CglBnBwdFold& b, int f0, int f1, bool lead, float* t) {
+  typedef double f64x2 __attribute__((ext_vector_type(2)));
+  const int tid = threadIdx.x;
+  for (int f = f0 + tid; f < f1; f += 256) {
+    // the tiles' partials in groups of 8 loads in flight, summed in tile order
+    double S = 0.0, D = 0.0;
+    for (int t0 = 0; t0 < b.tiles; t0 += 8) {
+      f64x2 pr[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        pr[j] = *(const CGL_GLOBAL f64x2*)(b.part + ((long)min(t0 + j, b.tiles - 1) * b.F + f) * 2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (t0 + j < b.tiles) {
+          S += pr[j][0];
+          D += pr[j][1];
+        }
+    }
+    const float invstd = gld(b.invstd + f);
+    const int i = f - f0;
+    t[0 * CGL_BNB_TAB + i] = gld(b.mean + f);
+    t[1 * CGL_BNB_TAB + i] = invstd;
+    t[2 * CGL_BNB_TAB + i] = gld(b.gamma + f);
+    t[3 * CGL_BNB_TAB + i] = (float)(S / b.M);
+    t[4 * CGL_BNB_TAB + i] = (float)D * invstd * invstd / b.M;
+    if (lead) {
+      gst(b.g_gamma + f, (float)(D * (double)invstd));
+      gst(b.g_beta + f, (float)S);
+    }
+  }
+}
+
+// dZ of one element: torch's (dy - S/M - (y - mean) D invstd^2 / M) invstd gamma, as cgl_bn_bwd
+__device__ __forceinline__ float cgl_bnb_apply(float dy, float y, float mean, float invstd, float w, float gm, float kk) {
+  return (dy - gm - (y - mean) * kk) * invstd * w;
+}
 
 // ------------------------------------------------------------------------------------------
 // Main body.  One wave owns TM x TN 32x32 accumulator blocks ((32 TM) x (32 TN) outputs); the
@@ -140,13 +290,11 @@ struct CglPipe {
   static constexpr int S = CGL_GEMM_STAGES;
 };
 
-typedef __attribute__((address_space(3))) void cgl_lds_void;
-#define CGL_GL_NS 2        // LDS ring depth of the staged main loop (measured: 2 beats 3 at 64 KB per workgroup)
-
-template <int LAYOUT, int VEC, int TM, int TN, bool SK, bool GL, int DT = 0, bool BNF = false>
-__device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d, int bid, float* __restrict__ s_red,
+// Dynamic LDS layout: [operand-transform tables (cgl_gemm_tab_floats)] [split-K partials]
+template <int LAYOUT, int VEC, int TM, int TN, bool SK, int DT = 0, int ABN = 0>
+__device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d, int bid, float* __restrict__ s_dyn,
                                               float* __restrict__ s_col, int* __restrict__ s_flag,
-                                              float* __restrict__ s_bn, double* __restrict__ s_bnd) {
+                                              double* __restrict__ s_bnd) {
   constexpr int S = CglPipe<TM, TN>::S;
   const int M = d->M, N = d->N, K = d->K;
   const int WN = d->WN, WK = d->WK, WM = d->WM;
@@ -174,6 +322,36 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   const int BM = 32 * TM * WM;
   const int m0 = tm * BM + wm * 32 * TM;            // first row of this wave's tile
   const int n0 = (tn * WN + wn) * 32 * TN;          // first column of this wave's tile
+  float* __restrict__ s_tab = s_dyn;                // operand-transform tables
+  float* __restrict__ s_red = s_dyn + d->tab_floats;   // split-K partials
+
+  // ---------------- operand-transform prologue (before any operand load is consumed)
+  // ABN: the instantiation carrying the operand transforms (0: none compiled in; 1 / 2: the mode
+  // of the launch's problems, a problem with a_bn 0 beside them runs untransformed)
+  const int abn = ABN ? d->a_bn : 0;
+  if (ABN == 1 && abn == 1) {                 // forward BatchNorm of A (k-contiguous, every k)
+    cgl_abn_fwd_prologue(d->a_bnf, K, (tm * BM) / d->a_bnf.gr, local == 0 && kslice == 0, s_tab,
+                         s_tab + CGL_BN_MAXF + 16);
+    __syncthreads();
+  } else if (ABN == 2 && abn == 2) {   // backward BatchNorm of A: every k (kc) or this tile's m range (mn)
+    const int f0 = LAYOUT == 2 ? tm * BM : 0, f1 = LAYOUT == 2 ? min(tm * BM + BM, M) : K;
+    cgl_abn_bwd_prologue(d->a_bnb, f0, f1, LAYOUT != 2 && local == 0 && kslice == 0, s_tab);
+    __syncthreads();
+  }
+  // per-lane coefficients of an m-contiguous A under a_bn 2 (its lane's row m is fixed)
+  float bm_mean[TM], bm_inv[TM], bm_w[TM], bm_gm[TM], bm_k[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    bm_mean[i] = bm_inv[i] = bm_w[i] = bm_gm[i] = bm_k[i] = 0.f;
+    if (ABN == 2 && LAYOUT == 2 && abn == 2) {
+      const int r = min(m0 + 32 * i + li, M - 1) - tm * BM;
+      bm_mean[i] = s_tab[0 * CGL_BNB_TAB + r];
+      bm_inv[i] = s_tab[1 * CGL_BNB_TAB + r];
+      bm_w[i] = s_tab[2 * CGL_BNB_TAB + r];
+      bm_gm[i] = s_tab[3 * CGL_BNB_TAB + r];
+      bm_k[i] = s_tab[4 * CGL_BNB_TAB + r];
+    }
+  }
 
   // ---------------- main loop
   const int b_ones = (LAYOUT != 0) ? d->b_ones_col : 0;
@@ -197,147 +375,31 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 #pragma unroll
     for (int r = 0; r < 16; ++r) accx[x][r] = 0.f;
 
-  if constexpr (GL && LAYOUT != 2 && TM == 1 && TN == 1 && VEC && DT == CGL_DTYPE_F32) {
-    // ---------------- LDS-staged main loop (glds): the waves of one K-slice share a ring of
-    // CGL_GL_NS stages of 32 k, filled by global_load_lds_dwordx4 in whole 128-byte row segments
-    // (8 rows per wave-instruction) instead of fragment-shaped loads that touch 32 rows per
-    // instruction (those saturate the vector L1's tag lookups: TA_ADDR_STALLED_BY_TC, r02 PMC).
-    //   A (k-contiguous): image [32 WM rows][32 k], row r's 16-byte piece p at p ^ ((r >> 1) & 7)
-    //     (conflict-free ds_read_b128 of 8 consecutive k per lane half: the k-permuted fragment);
-    //   B, NT (k-contiguous): the same image of 32 WN rows; NN (n-contiguous): k-major image
-    //     [32 k][32 WN], fragments by ds_read_b32 (32 consecutive columns per lane half).
-    // Rows / columns past M / N read clamped (valid) addresses and feed unstored outputs; k past
-    // K (last stage only) reads clamped addresses and A's values there are zeroed.
-    const int gw = WM * WN;
-    const int na = 4 * WM, nb = 4 * WN, ninst = na + nb, per = ninst / gw;
-    const int stg = ninst * 256;                          // floats per stage of one slice
-    float* ring = s_red + wk * CGL_GL_NS * stg;
-    const int nst = (K + 31) / 32;
-    const int nsl = KS * WK, sl = kslice * WK + wk;
-    const int sb = (sl * nst) / nsl, se = ((sl + 1) * nst) / nsl;
-    const int cmax = (nst + nsl - 1) / nsl;
-    const int arow0 = tm * BM, bcol0 = tn * WN * 32;     // first A row / B row (NT) or column (NN) of the tile
-    const int ldb = d->b.ld;
-    float* __restrict__ a_copy = d->a_copy;
-    const bool do_copy = a_copy && tn == 0 && wn == 0 && (m0 + li) < M && (m0 + li) >= d->a_copy_row0;
-    // this lane's global source of each of its fill instructions (instruction q = wmn + u gw)
-    const float* src[8];
-    int src_k[8];            // NT / A: offset of the piece in k; NN's B: k-row within the stage
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int q = min(wmn + u * gw, ninst - 1);
-      if (q < na || LAYOUT == 0) {
-        const bool isA = q < na;
-        const int row = (isA ? q : q - na) * 8 + (lane >> 3);
-        const int p = (lane & 7) ^ ((row >> 1) & 7);
-        src[u] = isA ? cgl_row(d->a, min(arow0 + row, M - 1)) : cgl_row(d->b, min(bcol0 + row, N - 1));
-        src_k[u] = 4 * p;
-      } else {                                            // NN's B: k-major image
-        const int e = (q - na) * 256 + 4 * (lane & 63);   // float index in the [32][32 WN] image
-        const int kr = e / (32 * WN), col = e % (32 * WN);
-        src[u] = d->b.p0 + min(bcol0 + col, nmem - 4);
-        src_k[u] = kr;
-      }
-    }
-    auto issue = [&](int s, int buf) {
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (u < per) {
-          const int q = wmn + u * gw;
-          const float* g;
-          if (q < na || LAYOUT == 0)
-            g = src[u] + min(s * 32 + src_k[u], K - 4);
-          else
-            g = src[u] + (long)min(s * 32 + src_k[u], K - 1) * ldb;
-          __builtin_amdgcn_global_load_lds((const void*)g, (cgl_lds_void*)(ring + buf * stg + q * 256), 16, 0, 0);
-        }
-      }
-    };
-    const int arow = wm * 32 + li, asw = (arow >> 1) & 7;
-    const int brow = wn * 32 + li, bsw = (brow >> 1) & 7;
-    for (int j = 0; j < CGL_GL_NS - 1; ++j)
-      if (sb + j < se) issue(sb + j, j);
-    for (int it = 0; it < cmax; ++it) {
-      const int s = sb + it;
-      if (CGL_GL_NS > 2 && s + CGL_GL_NS - 2 < se) {
-        // (CGL_GL_NS == 3: the next stage's `per` fills may stay in flight)
-        switch (per) {
-          case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-          case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-          case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-          default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-        }
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      // (a full __syncthreads: it also orders the compiler's LDS reads after the barrier; with
-      // CGL_GL_NS == 2 no fill is in flight here, so its vmcnt(0) costs nothing)
-      __syncthreads();
-      if (s + CGL_GL_NS - 1 < se) issue(s + CGL_GL_NS - 1, (it + CGL_GL_NS - 1) % CGL_GL_NS);
-      if (s < se) {
-        const float* la = ring + (it % CGL_GL_NS) * stg;
-        const float* lb = la + na * 256;
-        const int kleft = K - s * 32;                     // < 32 on a K-tail stage
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const int p0 = 4 * c + 2 * lh;
-          const f32x4 a0 = *(const f32x4*)(la + arow * 32 + 4 * (p0 ^ asw));
-          const f32x4 a1 = *(const f32x4*)(la + arow * 32 + 4 * ((p0 + 1) ^ asw));
-          float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-          float bv[8];
-          if (LAYOUT == 0) {
-            const f32x4 b0 = *(const f32x4*)(lb + brow * 32 + 4 * (p0 ^ bsw));
-            const f32x4 b1 = *(const f32x4*)(lb + brow * 32 + 4 * ((p0 + 1) ^ bsw));
-            bv[0] = b0[0]; bv[1] = b0[1]; bv[2] = b0[2]; bv[3] = b0[3];
-            bv[4] = b1[0]; bv[5] = b1[1]; bv[6] = b1[2]; bv[7] = b1[3];
-          } else {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) bv[q] = lb[(16 * c + 8 * lh + q) * (32 * WN) + brow];
-          }
-          if (kleft < 32) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-              if (16 * c + 8 * lh + q >= kleft) av[q] = 0.f;
-          }
-          if (do_copy) {
-            float* dst = a_copy + (long)(m0 + li) * d->a_copy_ld + s * 32 + 16 * c + 8 * lh;
-            if (kleft >= 16 * c + 8 * lh + 8) {
-              *(gf4p)dst = f32x4{av[0], av[1], av[2], av[3]};
-              *(gf4p)(dst + 4) = f32x4{av[4], av[5], av[6], av[7]};
-            } else {
-#pragma unroll
-              for (int q = 0; q < 8; ++q)
-                if (16 * c + 8 * lh + q < kleft) gst(dst + q, av[q]);
-            }
-          }
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            if (q % NX == 0)
-              acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], bv[q], acc[0][0], 0, 0, 0);
-            else
-              accx[q % NX - 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], bv[q], accx[q % NX - 1], 0, 0, 0);
-          }
-        }
-      }
-    }
-    __syncthreads();                        // the ring is reused by the split-K reduction below
-  } else {
+  {
   const int nch = (K + CGL_GEMM_KCHUNK - 1) / CGL_GEMM_KCHUNK;
   // chunk range of this wave: slice kslice * WK + wk of KS * WK equal slices of the K chunks
   const int nsl = KS * WK, sl = kslice * WK + wk;
   const int cb = (sl * nch) / nsl, ce = ((sl + 1) * nch) / nsl;
   const int lda = d->a.ld, ldb = d->b.ld;
   float* __restrict__ a_copy = d->a_copy;
+  // copy-out: chunk c of a row block is written by the one wave of the (tiles_n x WN) that load
+  // it whose column index equals c modulo their count (the copy work spread over every workgroup)
+  const int copy_n = d->tiles_n * WN, copy_me = tn * WN + wn;
+  const bool ybn = ABN == 2 && abn == 2;        // A under a_bn 2 streams the BatchNorm input y
+  const float* __restrict__ ybase = d->a_bnb.y;
+  const int ldy = d->a_bnb.ldy;
 
   // per-lane operand rows / columns of each block, clamped (always dereferenceable) bases
   const float* a_base[TM];
+  const float* y_base[TM];
   const float* b_base[TN];
-  bool b_is_ones[TN], do_copy[TM];
+  bool b_is_ones[TN], copy_row[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int am = m0 + 32 * i + li;      // A row (kc) or A column (mn)
     a_base[i] = (LAYOUT != 2) ? cgl_row(d->a, min(am, M - 1)) : d->a.p0 + min(am, M - 1);
-    do_copy[i] = (LAYOUT != 2) && a_copy && tn == 0 && wn == 0 && am < M && am >= d->a_copy_row0;
+    y_base[i] = ybn ? ((LAYOUT != 2) ? ybase + (long)min(am, M - 1) * ldy : ybase + min(am, M - 1)) : a_base[i];
+    copy_row[i] = (LAYOUT != 2) && a_copy && am < M && am >= d->a_copy_row0;
   }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -349,32 +411,39 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   // Full chunks (k + 16 <= K) load without clamps and multiply without masks: rows / columns
   // past M / N come from clamped (valid) addresses and only feed accumulator rows / columns
   // that are never stored.  Only the K-tail chunk clamps its k and zeroes k >= K.
-  auto load_chunk = [&](auto tail, int c, float (&A_)[TM][8], float (&B_)[TN][8]) {
+  auto load_a = [&](auto tail, int c, const float* const (&base)[TM], int ld, float (&A_)[TM][8]) {
     constexpr bool T = decltype(tail)::value;
     const int k = c * CGL_GEMM_KCHUNK + 8 * lh;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       if (LAYOUT == 2) {
         if (T) {
-          cgl_ld_mn(a_base[i], lda, k, K, A_[i]);
+          cgl_ld_mn(base[i], ld, k, K, A_[i]);
         } else {
-          gcfp q = (gcfp)a_base[i] + (long)k * lda;
+          gcfp q = (gcfp)base[i] + (long)k * ld;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) A_[i][j] = q[(long)j * lda];
+          for (int j = 0; j < 8; ++j) A_[i][j] = q[(long)j * ld];
         }
       } else {
         if (T) {
-          cgl_ld_kc<VEC>(a_base[i], k, K, A_[i]);
+          cgl_ld_kc<VEC>(base[i], k, K, A_[i]);
         } else if (VEC) {
-          const f32x4 x = *(gcf4p)(a_base[i] + k), y = *(gcf4p)(a_base[i] + k + 4);
+          const f32x4 x = *(gcf4p)(base[i] + k), y = *(gcf4p)(base[i] + k + 4);
           A_[i][0] = x[0]; A_[i][1] = x[1]; A_[i][2] = x[2]; A_[i][3] = x[3];
           A_[i][4] = y[0]; A_[i][5] = y[1]; A_[i][6] = y[2]; A_[i][7] = y[3];
         } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) A_[i][j] = ((gcfp)a_base[i])[k + j];
+          for (int j = 0; j < 8; ++j) A_[i][j] = ((gcfp)base[i])[k + j];
         }
       }
     }
+  };
+  auto load_chunk = [&](auto tail, int c, float (&A_)[TM][8], auto& Y_, float (&B_)[TN][8]) {
+    constexpr bool T = decltype(tail)::value;
+    const int k = c * CGL_GEMM_KCHUNK + 8 * lh;
+    load_a(tail, c, a_base, lda, A_);
+    if constexpr (ABN == 2)
+      if (ybn) load_a(tail, c, y_base, ldy, Y_);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       if (LAYOUT == 0) {
@@ -399,13 +468,55 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
       }
     }
   };
-  auto compute_chunk = [&](auto tail, int c, float (&A_)[TM][8], float (&B_)[TN][8]) {
+  auto compute_chunk = [&](auto tail, int c, float (&A_)[TM][8], auto& Y_, float (&B_)[TN][8]) {
     constexpr bool T = decltype(tail)::value;
     const int k = c * CGL_GEMM_KCHUNK + 8 * lh;
+    if (ABN == 1 && abn == 1 && LAYOUT == 0) {
+      // BatchNorm1d(train) + LeakyReLU of the Linear output, scale / shift of k from LDS
+      // (the 8 k of a lane half are contiguous: two 16-byte LDS reads per table)
+      const f32x4 sc0 = *(const f32x4*)(s_tab + k), sc1 = *(const f32x4*)(s_tab + k + 4);
+      const f32x4 sh0 = *(const f32x4*)(s_tab + CGL_BN_MAXF + 16 + k);
+      const f32x4 sh1 = *(const f32x4*)(s_tab + CGL_BN_MAXF + 16 + k + 4);
+      const float sc[8] = {sc0[0], sc0[1], sc0[2], sc0[3], sc1[0], sc1[1], sc1[2], sc1[3]};
+      const float sh[8] = {sh0[0], sh0[1], sh0[2], sh0[3], sh1[0], sh1[1], sh1[2], sh1[3]};
+      const float sl = d->a_bnf.slope;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float x = fmaf(A_[i][q], sc[q], sh[q]);
+          A_[i][q] = x > 0.f ? x : x * sl;
+        }
+    } else if constexpr (ABN == 2) {
+     if (abn == 2) {
+      if (LAYOUT == 2) {       // m-contiguous A: the lane's feature is fixed
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            A_[i][q] = cgl_bnb_apply(A_[i][q], Y_[i][q], bm_mean[i], bm_inv[i], bm_w[i], bm_gm[i], bm_k[i]);
+      } else {                 // k-contiguous A: the 8 k of the lane half (two 16-byte LDS reads
+        float cf[5][8];        // per table; past K in the tail chunk: padding, masked below)
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+          const f32x4 u0 = *(const f32x4*)(s_tab + t * CGL_BNB_TAB + k);
+          const f32x4 u1 = *(const f32x4*)(s_tab + t * CGL_BNB_TAB + k + 4);
+          cf[t][0] = u0[0]; cf[t][1] = u0[1]; cf[t][2] = u0[2]; cf[t][3] = u0[3];
+          cf[t][4] = u1[0]; cf[t][5] = u1[1]; cf[t][6] = u1[2]; cf[t][7] = u1[3];
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            A_[i][q] = cgl_bnb_apply(A_[i][q], Y_[i][q], cf[0][q], cf[1][q], cf[2][q], cf[3][q], cf[4][q]);
+      }
+     }
+    }
+    const bool own = (c % copy_n) == copy_me;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       if (T) cgl_mask(A_[i], true, k, K);
-      if (do_copy[i]) {
+      if (copy_row[i] && own) {
         float* dst = a_copy + (long)(m0 + 32 * i + li) * d->a_copy_ld;
         if (VEC && (!T || k + 7 < K)) {
           *(gf4p)(dst + k) = f32x4{A_[i][0], A_[i][1], A_[i][2], A_[i][3]};
@@ -458,25 +569,25 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   std::integral_constant<bool, false> full;
   std::integral_constant<bool, true> tailc;
   if (cb < cfull) {
-    float xa[S][TM][8], xb[S][TN][8];
+    float xa[S][TM][8], xy[S][ABN == 2 ? TM : 1][8], xb[S][TN][8];
 #pragma unroll
-    for (int s = 0; s < S; ++s) load_chunk(full, min(cb + s, cfull - 1), xa[s], xb[s]);
+    for (int s = 0; s < S; ++s) load_chunk(full, min(cb + s, cfull - 1), xa[s], xy[s], xb[s]);
     int c = cb;
     for (; c + S <= cfull; c += S) {
 #pragma unroll
       for (int s = 0; s < S; ++s) {
-        compute_chunk(full, c + s, xa[s], xb[s]);
-        load_chunk(full, min(c + s + S, cfull - 1), xa[s], xb[s]);
+        compute_chunk(full, c + s, xa[s], xy[s], xb[s]);
+        load_chunk(full, min(c + s + S, cfull - 1), xa[s], xy[s], xb[s]);
       }
     }
 #pragma unroll
     for (int s = 0; s < S - 1; ++s)
-      if (c + s < cfull) compute_chunk(full, c + s, xa[s], xb[s]);
+      if (c + s < cfull) compute_chunk(full, c + s, xa[s], xy[s], xb[s]);
   }
   if (cfull < ce) {   // the K tail (at most one chunk, owned by the last k-group)
-    float xa[TM][8], xb[TN][8];
-    load_chunk(tailc, cfull, xa, xb);
-    compute_chunk(tailc, cfull, xa, xb);
+    float xa[TM][8], xy[ABN == 2 ? TM : 1][8], xb[TN][8];
+    load_chunk(tailc, cfull, xa, xy, xb);
+    compute_chunk(tailc, cfull, xa, xy, xb);
   }
   }   // (register-pipelined main loop)
 
@@ -628,57 +739,42 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     }
   }
 
-  // ---------------- fused BatchNorm1d backward (bn_fuse 2): C = dZ of the BatchNorm below
-  // (torch's batch_norm_backward, train mode, as cgl_bn_bwd):
-  //   dy = leaky'(post) * acc,  S = sum dy,  D = sum (y - mean) dy   (per column, over all M rows)
-  //   dZ = (dy - S / M - (y - mean) D invstd^2 / M) invstd gamma,  dgamma = D invstd,  dbeta = S
-  if (BNF && d->bn_fuse == 2) {   // (BNF: only the fused-BatchNorm instantiation carries these paths)
-    const float sl = d->slope;
-    float dy[TM][TN][16], yc[TM][TN][16];
-    const int ldp = d->bn_ld_post;
+  // backward BatchNorm partials of the stored gradient dy (the next GEMM's a_bn 2): per
+  // (row tile, column) {sum dy, sum (y - mean) dy} in double over the workgroup's rows (lane
+  // rows, then the two lane halves, then the WM waves of the column, fixed order)
+  if (d->bnb_part) {
+    const int ldy = d->bnb_ld;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int colc = min(n0 + 32 * j + li, N - 1);
-      const float mu = gld(d->bn_mean + colc);
+      const int col = n0 + 32 * j + li;
+      const int colc = min(col, N - 1);
+      const float mu = gld(d->bnb_mean + colc);
+      double Sd = 0.0, Dd = 0.0;
+      if (owner && col < N) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        float po[16], yv[16];
+        for (int i = 0; i < TM; ++i) {
+          float yv[16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = min(rbase + 32 * i + (r & 3) + 8 * (r >> 2), M - 1);
-          po[r] = gld(d->bn_post + (long)row * ldp + colc);
-          yv[r] = gld(d->bn_y + (long)row * ldp + colc);
-        }
-        const float* v = (const float*)&acc[i][j];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          dy[i][j][r] = po[r] > 0.f ? v[r] : v[r] * sl;
-          yc[i][j][r] = yv[r] - mu;
-        }
-      }
-    }
-    // tile partials per column: lane rows (16 per block) -> lane halves -> waves of the column
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const bool colok = n0 + 32 * j + li < N;
-      double S = 0.0, D = 0.0;
-      if (owner && colok) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
+          for (int r = 0; r < 16; ++r) {
+            const int row = min(rbase + 32 * i + (r & 3) + 8 * (r >> 2), M - 1);
+            yv[r] = gld(d->bnb_y + (long)row * ldy + colc);
+          }
+          const float* v = (const float*)&acc[i][j];
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
             if (row < M) {
-              S += (double)dy[i][j][r];
-              D += (double)(yc[i][j][r] * dy[i][j][r]);
+              Sd += (double)v[r];
+              Dd += (double)((yv[r] - mu) * v[r]);
             }
           }
+        }
       }
-      S += __shfl_xor(S, 32);
-      D += __shfl_xor(D, 32);
+      Sd += __shfl_xor(Sd, 32);
+      Dd += __shfl_xor(Dd, 32);
       if (owner && lh == 0) {
-        s_bnd[(((wm * WN + wn) * TN + j) * 32 + li) * 2] = S;
-        s_bnd[(((wm * WN + wn) * TN + j) * 32 + li) * 2 + 1] = D;
+        s_bnd[(((wm * WN + wn) * TN + j) * 32 + li) * 2] = Sd;
+        s_bnd[(((wm * WN + wn) * TN + j) * 32 + li) * 2 + 1] = Dd;
       }
     }
     __syncthreads();
@@ -686,80 +782,18 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = n0 + 32 * j + li;
-        double S = 0.0, D = 0.0;
+        double Sd = 0.0, Dd = 0.0;
         for (int q = 0; q < WM; ++q) {
-          S += s_bnd[(((q * WN + wn) * TN + j) * 32 + li) * 2];
-          D += s_bnd[(((q * WN + wn) * TN + j) * 32 + li) * 2 + 1];
+          Sd += s_bnd[(((q * WN + wn) * TN + j) * 32 + li) * 2];
+          Dd += s_bnd[(((q * WN + wn) * TN + j) * 32 + li) * 2 + 1];
         }
         if (col < N) {
-          cgl_pubd(d->bn_dpart + ((long)tm * N + col) * 2, S);
-          cgl_pubd(d->bn_dpart + ((long)tm * N + col) * 2 + 1, D);
+          double* p = d->bnb_part + ((long)tm * N + col) * 2;
+          *(CGL_GLOBAL double*)p = Sd;
+          *(CGL_GLOBAL double*)(p + 1) = Dd;
         }
       }
     }
-    cgl_rendezvous(d->rv_count + tn, (unsigned int)d->tiles_m, d->err);
-    // every column of the workgroup tile: the tiles_m partials staged through LDS (one round trip,
-    // few registers), then summed in tile order
-    const int ncw = WN * TN * 32, c0 = tn * WN * TN * 32;
-    float* s_gm = s_bn;          // [ncw]: S / M
-    float* s_k = s_bn + 128;     // [ncw]: D invstd^2 / M
-    {
-      const int nt = d->tiles_m, items = nt * ncw;
-      unsigned long long* stg = (unsigned long long*)s_red;    // [nt][ncw][2]
-      unsigned long long v0[CGL_BN_STG], v1[CGL_BN_STG];
-#pragma unroll
-      for (int u = 0; u < CGL_BN_STG; ++u) {
-        const int q = min(tid + 256 * u, items - 1);
-        const int t = q / ncw, col = min(c0 + q % ncw, N - 1);
-        v0[u] = cgl_ld64(d->bn_dpart + ((long)t * N + col) * 2);
-        v1[u] = cgl_ld64(d->bn_dpart + ((long)t * N + col) * 2 + 1);
-      }
-#pragma unroll
-      for (int u = 0; u < CGL_BN_STG; ++u) {
-        const int q = tid + 256 * u;
-        if (q < items) {
-          stg[2 * q] = v0[u];
-          stg[2 * q + 1] = v1[u];
-        }
-      }
-    }
-    __syncthreads();
-    if (tid < ncw) {
-      const int col = min(c0 + tid, N - 1);
-      const int nt = d->tiles_m;
-      const unsigned long long* stg = (const unsigned long long*)s_red;
-      double S = 0.0, D = 0.0;
-      for (int t = 0; t < nt; ++t) {
-        S += __longlong_as_double((long long)stg[2 * (t * ncw + tid)]);
-        D += __longlong_as_double((long long)stg[2 * (t * ncw + tid) + 1]);
-      }
-      const float invstd = gld(d->bn_invstd + col);
-      s_k[tid] = (float)D * invstd * invstd / M;
-      s_gm[tid] = (float)(S / M);
-      if (tm == 0 && c0 + tid < N) {
-        gst(d->bn_g_gamma + col, (float)(D * (double)invstd));
-        gst(d->bn_g_beta + col, (float)S);
-      }
-    }
-    __syncthreads();
-    if (owner) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = n0 + 32 * j + li;
-        if (col >= N) continue;
-        const int cl = col - c0;
-        const float invstd = gld(d->bn_invstd + col), w = gld(d->bn_gamma + col);
-        const float gm = s_gm[cl], k = s_k[cl];
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
-            if (row < M) gst(d->C + (long)row * d->ldc + col, (dy[i][j][r] - gm - yc[i][j][r] * k) * invstd * w);
-          }
-      }
-    }
-    return;
   }
 
   // forward BatchNorm partials of the stored output: per column, per group slot {sum, M2}
@@ -839,124 +873,12 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
         if (col < N) {
           for (int s = 0; s < 2; ++s) {
             float* p = d->stat_part + ((long)(tm * 2 + s) * N + col) * 2;
-            if (d->bn_fuse == 1) {
-              cgl_pub2f(p, part[j][s][0], part[j][s][1]);
-            } else {
-              gst(p, part[j][s][0]);
-              gst(p + 1, part[j][s][1]);
-            }
+            gst(p, part[j][s][0]);
+            gst(p + 1, part[j][s][1]);
           }
         }
       }
     }
-  }
-
-  // ---------------- fused BatchNorm1d forward (bn_fuse 1): C = Y (the Linear output, kept for
-  // the backward), act = LeakyReLU(BN(Y)) with the statistics of the Y rows' forward call (group
-  // of stat_gr rows), combined from every row tile's published {sum, M2} partials exactly as
-  // cgl_bn_apply does (tile order, double, Chan); row tile 0 writes save_mean / save_invstd and
-  // updates the running statistics group by group (the reference's forward-call order)
-  if (BNF && d->bn_fuse == 1) {
-    cgl_rendezvous(d->rv_count + tn, (unsigned int)d->tiles_m, d->err);
-    const int gr = d->stat_gr;
-    const int ng = (M + gr - 1) / gr;          // <= 2 (planner)
-    const int ncw = WN * TN * 32, c0 = tn * WN * TN * 32;
-    float* s_sc = s_bn;            // [2][128]
-    float* s_sh = s_bn + 256;      // [2][128]
-    double* s_mu = s_bnd;          // [2][128]
-    double* s_m2 = s_bnd + 256;    // [2][128]
-    {
-      // stage every row tile's {sum, M2} pair of both group slots for the tile's columns (one round
-      // trip): stg[slot][t][c]
-      const int nt = d->tiles_m, items = 2 * nt * ncw;
-      unsigned long long* stg = (unsigned long long*)s_red;
-      unsigned long long v[2 * CGL_BN_STG];
-#pragma unroll
-      for (int u = 0; u < 2 * CGL_BN_STG; ++u) {
-        const int q = min(tid + 256 * u, items - 1);
-        const int sl2 = q / (nt * ncw), t = (q / ncw) % nt, col = min(c0 + q % ncw, N - 1);
-        v[u] = cgl_ld64(d->stat_part + ((long)(t * 2 + sl2) * N + col) * 2);
-      }
-#pragma unroll
-      for (int u = 0; u < 2 * CGL_BN_STG; ++u) {
-        const int q = tid + 256 * u;
-        if (q < items) stg[q] = v[u];
-      }
-    }
-    __syncthreads();
-    int n_g = 0;
-    if (tid < ncw * ng) {
-      const int cl = tid % ncw, g = tid / ncw;
-      const int col = min(c0 + cl, N - 1);
-      const int r0 = g * gr, r1 = min(r0 + gr, M);
-      n_g = r1 - r0;
-      const int t0 = r0 / BM, t1 = (r1 - 1) / BM;
-      const int nt = t1 - t0 + 1;
-      const unsigned long long* stg = (const unsigned long long*)s_red;
-      auto pr = [&](int j) {
-        const int t = t0 + j;
-        const int slot = (t * BM < r0) ? 1 : 0;   // tile starts in the previous group
-        return stg[(slot * d->tiles_m + t) * ncw + cl];
-      };
-      double sm = 0.0;
-      for (int j = 0; j < nt; ++j) sm += (double)__uint_as_float((unsigned int)pr(j));
-      const double mu = sm / n_g;
-      double m2 = 0.0;
-      for (int j = 0; j < nt; ++j) {
-        const int t = t0 + j;
-        const int c = min((t + 1) * BM, r1) - max(t * BM, r0);
-        const unsigned long long p = pr(j);
-        const double dd = (double)__uint_as_float((unsigned int)p) / c - mu;
-        m2 += (double)__uint_as_float((unsigned int)(p >> 32)) + c * dd * dd;
-      }
-      const double invstd = 1.0 / sqrt(m2 / n_g + d->bn_eps);
-      const float sc = (float)invstd * gld(d->bn_gamma + col);
-      s_sc[g * 128 + cl] = sc;
-      s_sh[g * 128 + cl] = gld(d->bn_beta + col) - (float)mu * sc;
-      s_mu[g * 128 + cl] = mu;
-      s_m2[g * 128 + cl] = m2;
-      if (tm == 0 && c0 + cl < N && d->bn_save_mean) {
-        gst(d->bn_save_mean + (long)g * N + col, (float)mu);
-        gst(d->bn_save_invstd + (long)g * N + col, (float)invstd);
-      }
-    }
-    __syncthreads();
-    if (tm == 0 && tid < ncw && c0 + tid < N && d->bn_run_mean) {
-      const int col = c0 + tid;
-      const double mom = d->bn_momentum;
-      float rm = gld(d->bn_run_mean + col), rv = gld(d->bn_run_var + col);
-      for (int g = 0; g < ng; ++g) {
-        const int n = min((g + 1) * gr, M) - g * gr;
-        rm = (float)(mom * s_mu[g * 128 + tid] + (1.0 - mom) * (double)rm);
-        rv = (float)(mom * (s_m2[g * 128 + tid] / (n - 1)) + (1.0 - mom) * (double)rv);
-      }
-      gst(d->bn_run_mean + col, rm);
-      gst(d->bn_run_var + col, rv);
-    }
-    if (owner) {
-      const float sl = d->slope;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = n0 + 32 * j + li;
-        if (col >= N) continue;
-        const int cl = col - c0;
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const float* v = (const float*)&acc[i][j];
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
-            if (row < M) {
-              const int g = row >= gr ? 1 : 0;
-              const float x = fmaf(v[r], s_sc[g * 128 + cl], s_sh[g * 128 + cl]);
-              gst(d->C + (long)row * d->ldc + col, v[r]);
-              gst(d->bn_act + (long)row * d->bn_ld_act + col, x > 0.f ? x : x * sl);
-            }
-          }
-        }
-      }
-    }
-    return;
   }
 
   if (owner) {
@@ -994,17 +916,13 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 // launch may mix layouts (e.g. the weight gradient (TN) and the input gradient (NN) of one
 // layer side by side).  Separate symbols keep the 1x1 variant's register budget (and so its
 // occupancy) independent of the 2x2 variant's.
-// Dynamic LDS: split-K partials of the waves with wk > 0.
-// BNF: the instantiation that carries the (opt-in) fused-BatchNorm epilogues (bn_fuse 1 / 2); the
-// default instantiations compile them out, so their register budget is the plain GEMM's.
-template <int TM, int TN, bool SK = false, bool GL = false, int DT = CGL_DTYPE_F32, bool BNF = false>
+// Dynamic LDS: the operand-transform tables, then the split-K partials of the waves with wk > 0.
+template <int TM, int TN, bool SK = false, int DT = CGL_DTYPE_F32, int ABN = 0>
 __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDesc* __restrict__ descs, int ndesc) {
   extern __shared__ float cgl_dyn_lds[];
   __shared__ float s_col[4 * TN * 32];          // per-column reductions across waves (WM WN <= 4)
   __shared__ int s_flag[1];                     // split-K: this workgroup reduces its tile
-  __shared__ float s_bn[512];                   // fused BatchNorm: per-column tables
-  __shared__ double s_bnd[4 * TN * 32 * 2 > 512 ? 4 * TN * 32 * 2 : 512];
-  float* s_red = cgl_dyn_lds;
+  __shared__ double s_bnd[4 * TN * 32 * 2];     // backward BatchNorm partials across waves
   const int bid = blockIdx.x;
   int di = 0;
   for (int q = 1; q < ndesc; ++q)
@@ -1016,9 +934,9 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
 #define CGL_BODY(L)                                               \
   do {                                                            \
     if (vec)                                                      \
-      cgl_gemm_body<L, 1, TM, TN, SK, GL, DT, BNF>(d, bid, s_red, s_col, s_flag, s_bn, s_bnd);    \
+      cgl_gemm_body<L, 1, TM, TN, SK, DT, ABN>(d, bid, cgl_dyn_lds, s_col, s_flag, s_bnd);    \
     else                                                          \
-      cgl_gemm_body<L, 0, TM, TN, SK, GL, DT, BNF>(d, bid, s_red, s_col, s_flag, s_bn, s_bnd);    \
+      cgl_gemm_body<L, 0, TM, TN, SK, DT, ABN>(d, bid, cgl_dyn_lds, s_col, s_flag, s_bnd);    \
   } while (0)
   if (layout == 0)
     CGL_BODY(0);
@@ -1029,24 +947,17 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
 #undef CGL_BODY
 }
 
-// Host helper: dynamic LDS bytes of one problem's split-K partials.
-// LDS ring of the staged main loop (GL launches, 1x1 blocks, layouts 0 / 1 with 16-byte operands)
-inline bool cgl_gemm_gl_ok(const CglGemmDesc& d) {
-  return d.layout != 2 && d.TM == 1 && d.TN == 1 && d.a_vec && d.b_vec && d.ksplit <= 1 && !d.b_ones_col &&
-         d.WM * d.WN * d.WK == 4;
+// Host helpers: the LDS tables of a problem's operand transform, its dynamic LDS bytes, its
+// workgroups, and the split-K partial floats it needs.
+inline int cgl_gemm_tab_floats(const CglGemmDesc& d) {
+  if (d.a_bn == 1) return 2 * (CGL_BN_MAXF + 16);
+  if (d.a_bn == 2) return 5 * CGL_BNB_TAB;
+  return 0;
 }
-inline int cgl_gemm_gl_bytes(const CglGemmDesc& d) {
-  return cgl_gemm_gl_ok(d) ? d.WK * CGL_GL_NS * (4 * d.WM + 4 * d.WN) * 1024 : 0;
+inline int cgl_gemm_stage_bytes(const CglGemmDesc& d) {
+  const int sk = (d.WK > 1) ? d.WM * d.WN * (d.WK - 1) * d.TM * d.TN * 16 * 64 * 4 : 0;
+  return sk + 4 * cgl_gemm_tab_floats(d);
 }
-inline int cgl_gemm_stage_bytes(const CglGemmDesc& d, bool gl = false) {
-  const int sk0 = (d.WK > 1) ? d.WM * d.WN * (d.WK - 1) * d.TM * d.TN * 16 * 64 * 4 : 0;
-  const int glb = gl ? cgl_gemm_gl_bytes(d) : 0;
-  const int sk = sk0 > glb ? sk0 : glb;
-  const int bn = d.bn_fuse ? cgl_bn_stage_bytes(d.tiles_m, d.WN * d.TN * 32) : 0;
-  return sk > bn ? sk : bn;
-}
-
-// Host helpers: workgroups of one problem, and the split-K partial floats it needs.
 inline int cgl_gemm_wgs(const CglGemmDesc& d) { return d.tiles_m * d.tiles_n * (d.ksplit > 1 ? d.ksplit : 1); }
 inline long cgl_gemm_kpart_floats(const CglGemmDesc& d) {
   return d.ksplit > 1 ? (long)d.ksplit * d.tiles_m * d.tiles_n * d.WM * d.WN * d.TM * d.TN * 16 * 64 : 0;

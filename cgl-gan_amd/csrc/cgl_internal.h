@@ -70,6 +70,18 @@ struct CglBnFwd {
   float* save_invstd;
 };
 
+// Backward BatchNorm1d of a GEMM's A operand (a_bn 2): the A values are dy (LeakyReLU'-masked
+// gradient w.r.t. the BatchNorm output) stored by the previous GEMM together with per-row-tile
+// partials {sum dy, sum (y - mean) dy}; dZ = (dy - S/M - (y - mean) D invstd^2 / M) invstd gamma.
+#define CGL_BNB_TAB (CGL_BN_MAXF + 16)   // LDS table stride (floats; padding for the K-tail chunk)
+struct CglBnBwdFold {
+  const double* part;     // [tiles][F][2]
+  int tiles, F, M;        // producer row tiles, features, rows of the BatchNorm call
+  const float* mean; const float* invstd; const float* gamma;   // [F] (the call's saved statistics)
+  float* g_gamma; float* g_beta;       // written by workgroup 0 of the k-contiguous problem
+  const float* y; int ldy;             // BatchNorm input rows (same row / column positions as A)
+};
+
 struct CglGemmDesc {
   int M, N, K;
   int WM, WN, WK;         // wave arrangement, WM*WN*WK == 4
@@ -99,25 +111,16 @@ struct CglGemmDesc {
   int ksplit;
   float* kpart;                        // [ksplit][tiles][WM*WN][TM*TN][16][64] floats
   unsigned int* kcount;                // [tiles], zero at rest
-  // BatchNorm1d fused into the epilogue through an in-launch rendezvous of the column tile's
-  // tiles_m workgroups (cgl_gemm.hip, "fused BatchNorm"):
-  //   bn_fuse 1 (forward, train): C = the Linear output Y, act = LeakyReLU(BN(Y)) per group of
-  //            stat_gr rows; statistics from the published per-tile {sum, M2} partials (stat_part);
-  //            save_mean / save_invstd and the running statistics written by row tile 0
-  //   bn_fuse 2 (backward, train): C = dZ = BN-backward(LeakyReLU'(post) * (A B)) with the
-  //            saved mean / invstd of one forward call; per-tile {sum dy, sum dy (y - mean)}
-  //            partials (bn_dpart, double); g_gamma / g_beta written by row tile 0
-  int bn_fuse;
-  unsigned int* rv_count;              // [tiles_n] monotonic rendezvous tickets (zero at creation)
-  unsigned int* err;                   // set on a rendezvous timeout (never expected)
-  const float* bn_gamma; const float* bn_beta;
-  float* bn_act; int bn_ld_act;        // forward: post-LeakyReLU output
-  double bn_eps, bn_momentum;
-  float* bn_run_mean; float* bn_run_var; float* bn_save_mean; float* bn_save_invstd;
-  const float* bn_post; const float* bn_y; int bn_ld_post;   // backward: LeakyReLU output, BN input
-  const float* bn_mean; const float* bn_invstd;              // backward: saved statistics
-  float* bn_g_gamma; float* bn_g_beta;
-  double* bn_dpart;                    // backward partials [tiles_m][N][2]
+  // A-operand transform (cgl_gemm.hip): 0 none, 1 forward BatchNorm1d + LeakyReLU (a_bnf),
+  // 2 backward BatchNorm1d (a_bnb); its LDS tables take the first tab_floats of the dynamic LDS
+  int a_bn;
+  int tab_floats;
+  CglBnFwd a_bnf;
+  CglBnBwdFold a_bnb;
+  // backward BatchNorm partials of the stored output dy: [tiles_m][N][2] {sum dy, sum (y - mean) dy}
+  double* bnb_part;
+  const float* bnb_y; int bnb_ld;      // the BatchNorm input at the stored positions
+  const float* bnb_mean;               // its saved batch mean [N]
 };
 
 // BatchNorm1d(train) + LeakyReLU over the whole [mtot][F] output of one G layer.

@@ -163,74 +163,7 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
   }
 }
 
-// BatchNorm statistics of group g for Q features k[q] (k[q] < 0: unused) from the producer
-// partials: the exact parallel combination of per-tile {S_t, M2_t} over c_t rows, in double
-// like torch's CPU kernel and in a fixed tile order,
-//   mean = sum_t S_t / n,   M2 = sum_t (M2_t + c_t (S_t / c_t - mean)^2).
-// Fast path (<= 8 tiles per group): every {S_t, M2_t} pair of the Q features is loaded up front
-// as one 8-byte load, so the whole computation costs a single memory round trip.
-template <int Q>
-__device__ __forceinline__ void cgl_bn_stats(const CglBnFwd& bn, int K, const int (&k)[Q], int g, double (&mean)[Q],
-                                             double (&m2)[Q], int& n) {
-  typedef float f32x2 __attribute__((ext_vector_type(2)));
-  const int r0 = g * bn.gr, r1 = min(r0 + bn.gr, bn.mtot);
-  n = r1 - r0;
-  const int t0 = r0 / bn.part_bm, t1 = (r1 - 1) / bn.part_bm;
-  const int nt = t1 - t0 + 1;
-  if (nt <= 8) {
-    f32x2 pr[Q][8];
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int kk = max(k[q], 0);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int t = t0 + min(j, nt - 1);
-        const int slot = (t * bn.part_bm < r0) ? 1 : 0;   // tile starts in the previous group
-        pr[q][j] = *(const CGL_GLOBAL f32x2*)(bn.part + ((long)(t * 2 + slot) * K + kk) * 2);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      double s = 0.0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j < nt) s += (double)pr[q][j][0];
-      const double mu = s / n;
-      double acc = 0.0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (j < nt) {
-          const int t = t0 + j;
-          const int c = min((t + 1) * bn.part_bm, r1) - max(t * bn.part_bm, r0);
-          const double dd = (double)pr[q][j][0] / c - mu;
-          acc += (double)pr[q][j][1] + c * dd * dd;
-        }
-      }
-      mean[q] = mu;
-      m2[q] = acc;
-    }
-    return;
-  }
-  for (int q = 0; q < Q; ++q) {
-    const int kk = max(k[q], 0);
-    double s = 0.0;
-    for (int t = t0; t <= t1; ++t) {
-      const int slot = (t * bn.part_bm < r0) ? 1 : 0;
-      s += (double)gld(bn.part + ((long)(t * 2 + slot) * K + kk) * 2);
-    }
-    const double mu = s / n;
-    double acc = 0.0;
-    for (int t = t0; t <= t1; ++t) {
-      const int slot = (t * bn.part_bm < r0) ? 1 : 0;
-      const float* pp = bn.part + ((long)(t * 2 + slot) * K + kk) * 2;
-      const int c = min((t + 1) * bn.part_bm, r1) - max(t * bn.part_bm, r0);
-      const double dd = (double)gld(pp) / c - mu;
-      acc += (double)gld(pp + 1) + c * dd * dd;
-    }
-    mean[q] = mu;
-    m2[q] = acc;
-  }
-}
+// (cgl_bn_stats: cgl_gemm.hip, shared with the GEMMs that fold the BatchNorm into their loads)
 
 // BatchNorm1d(train) + LeakyReLU of one G layer's [mtot][F] output, torch's arithmetic:
 //   invstd = 1 / sqrt(var_biased + eps),  scale = invstd * gamma,  shift = beta - mean * scale,

@@ -115,7 +115,6 @@ constexpr int kMaxHeadDescs = 2 * CGL_MAX_EPOCH + 4;
 constexpr int kMaxBnDescs = 2 * CGL_MAX_LAYERS;
 constexpr int kSplitKCounters = 8192;           // split-K tickets (one per tile of a launch)
 constexpr int kCounters = 64;                    // head-loss tickets
-constexpr int kRvCounters = 4096;                // fused-BatchNorm rendezvous tickets (monotonic)
 constexpr int64_t kSplitKFloats = 4 << 20;       // split-K partials of one launch (16 MiB)
 
 struct WS {
@@ -143,8 +142,7 @@ struct WS {
   unsigned int* counters;   // [kCounters]: head-loss tickets
   float* kpart;             // [kSplitKFloats]: split-K partials (reused by every launch)
   unsigned int* kcount;     // [kSplitKCounters]: split-K tickets (zero at rest)
-  unsigned int* rvcount;    // [kRvCounters]: fused-BatchNorm rendezvous tickets (monotonic)
-  double* gdpart[CGL_MAX_LAYERS];   // fused BatchNorm backward partials [B/32][f][2]
+  double* gdpart[CGL_MAX_LAYERS];   // backward BatchNorm partials of dy [B/32][f][2] (a_bn 2)
   CglStepState* st;
   int* idx;       // sampler output when sample_n > 0
   CglGemmDesc* gemm;
@@ -196,7 +194,6 @@ WS carve_ws(const cgl_gan_config& c, void* base) {
   // split-K scratch last, so that the layout of everything the default plan touches is unchanged
   w.kpart = cv.take<float>(kSplitKFloats);
   w.kcount = cv.take<unsigned int>(kSplitKCounters);
-  w.rvcount = cv.take<unsigned int>(kRvCounters);
   for (int l = 0; l + 1 < L; ++l)
     if (g.bn[l]) w.gdpart[l] = cv.take<double>((int64_t)((B + 31) / 32) * g.dims[l + 1] * 2);
   w.total = cv.off;
@@ -225,20 +222,21 @@ struct Launch {
   int shmem = 0;        // dynamic LDS bytes (GEMM)
   int blk = 1;          // GEMM per-wave block shape (TM = TN = blk)
   bool sk = false;      // GEMM launch holds a split-K problem
-  bool gl = false;      // GEMM launch uses the LDS-staged (glds) main loop instantiation
-  bool bnf = false;     // GEMM launch holds a fused-BatchNorm problem (the BNF instantiation)
   int dt = CGL_DTYPE_F32;   // GEMM operand type (cgl_gan_config.gemm_dtype)
+  int abn = 0;              // GEMM operand-transform instantiation (the launch's a_bn)
 };
 
-// Split-K partials of 2x2-block waves need up to 48 KB of dynamic LDS (+16 KB BN table).
+// Split-K partials of 2x2-block waves need up to 48 KB of dynamic LDS (+ the 20 KB operand tables).
 hipError_t gemm_lds_attr() {
   static bool done = false;
   if (!done) {
     // advisory on this platform (launches up to the per-CU LDS succeed); never fail on it
     for (const void* fn : {(const void*)cgl_gemm_f32<1, 1>, (const void*)cgl_gemm_f32<2, 2>,
-                           (const void*)cgl_gemm_f32<1, 1, false, false, CGL_DTYPE_F32, true>,
-                           (const void*)cgl_gemm_f32<1, 1, false, true>,
-                           (const void*)cgl_gemm_f32<1, 1, true>, (const void*)cgl_gemm_f32<2, 2, true>}) {
+                           (const void*)cgl_gemm_f32<1, 1, true>, (const void*)cgl_gemm_f32<2, 2, true>,
+                           (const void*)cgl_gemm_f32<1, 1, false, CGL_DTYPE_F32, 1>,
+                           (const void*)cgl_gemm_f32<2, 2, false, CGL_DTYPE_F32, 1>,
+                           (const void*)cgl_gemm_f32<1, 1, false, CGL_DTYPE_F32, 2>,
+                           (const void*)cgl_gemm_f32<2, 2, false, CGL_DTYPE_F32, 2>}) {
       for (int kb : {150, 128, 96, 64}) {
         const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kb * 1024);
         (void)hipGetLastError();
@@ -254,26 +252,32 @@ template <int DT>
 void launch_gemm16(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, int n, bool sk) {
   if (sk) {
     if (blk == 2)
-      cgl_gemm_f32<2, 2, true, false, DT><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+      cgl_gemm_f32<2, 2, true, DT><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
     else
-      cgl_gemm_f32<1, 1, true, false, DT><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+      cgl_gemm_f32<1, 1, true, DT><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
   } else if (blk == 2) {
-    cgl_gemm_f32<2, 2, false, false, DT><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+    cgl_gemm_f32<2, 2, false, DT><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
   } else {
-    cgl_gemm_f32<1, 1, false, false, DT><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+    cgl_gemm_f32<1, 1, false, DT><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
   }
 }
 
 void launch_gemm(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, int n, bool sk = false,
-                 bool gl = false, int dt = CGL_DTYPE_F32, bool bnf = false) {
-  if (bnf) {    // fused BatchNorm: 1x1 blocks, fp32, no split-K (planner)
-    cgl_gemm_f32<1, 1, false, false, CGL_DTYPE_F32, true><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+                 int dt = CGL_DTYPE_F32, int abn = 0) {
+  if (abn == 1) {          // fp32, no split-K (planner)
+    if (blk == 2)
+      cgl_gemm_f32<2, 2, false, CGL_DTYPE_F32, 1><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+    else
+      cgl_gemm_f32<1, 1, false, CGL_DTYPE_F32, 1><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+  } else if (abn == 2) {
+    if (blk == 2)
+      cgl_gemm_f32<2, 2, false, CGL_DTYPE_F32, 2><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+    else
+      cgl_gemm_f32<1, 1, false, CGL_DTYPE_F32, 2><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
   } else if (dt == CGL_DTYPE_F16) {
     launch_gemm16<CGL_DTYPE_F16>(blk, grid, shmem, s, d, n, sk);
   } else if (dt == CGL_DTYPE_BF16) {
     launch_gemm16<CGL_DTYPE_BF16>(blk, grid, shmem, s, d, n, sk);
-  } else if (gl) {
-    cgl_gemm_f32<1, 1, false, true><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
   } else if (sk) {   // a launch with a split-K problem: the instantiation carrying the combine
     if (blk == 2)
       cgl_gemm_f32<2, 2, true><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
@@ -453,8 +457,6 @@ struct cgl_gan {
   bool two_streams = false;
   float* xchg = nullptr;
   int64_t xchg_n = 0;
-  int rv_used = 0;             // rendezvous counters handed out
-  int gemm_cap[3] = {0, 0, 0}; // co-resident workgroups of cgl_gemm_f32<1,1> / <2,2> (0: unknown)
   // parameter tensor pointers
   std::vector<TensorRec> gl, dl;
   int64_t run_mean_off[CGL_MAX_LAYERS], run_var_off[CGL_MAX_LAYERS];
@@ -491,52 +493,23 @@ float* dgrad(const cgl_gan* c, int layer, int kind) {
   return nullptr;
 }
 
-// Workgroups of cgl_gemm_f32<blk, blk> guaranteed co-resident on the device at `shmem` dynamic LDS:
-// one workgroup per CU less than the occupancy query reports (MI355X_MICROARCH.md: the query can be one
-// high), times the CU count.
-int gemm_resident(int blk, int shmem) {
-  int dev = 0, cus = 0, nb = 0;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    return 0;
-  (void)blk;   // fused-BatchNorm launches run the 1x1 BNF instantiation
-  const void* fn = (const void*)cgl_gemm_f32<1, 1, false, false, CGL_DTYPE_F32, true>;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, CGL_GEMM_THREADS, shmem) != hipSuccess) {
-    (void)hipGetLastError();
-    return 0;
-  }
-  return std::max(nb - 1, 0) * cus;
-}
-
-// Fused BatchNorm (in-launch rendezvous instead of the cgl_bn_apply / cgl_bn_bwd launches) is
-// correct but measured no faster on MI355X at B = 256 (profiles/r02_bn_fuse_ab.txt: the rendezvous
-// -- ticket, poll, the staged partials' sc1 round trip -- costs what the launch boundary it removes
-// costs, and G L3's 512-workgroup launch loses to load imbalance), so it is opt-in: CGL_BN_FUSE=1.
-// LDS-staged (glds) GEMM main loop: correct on every shape, faster in isolation on the large NT
-// shapes (tools/gemm_lds_bench.hip: G L4 fwd 20.6 -> 14.2 us, L2-hot operands) but slower inside
-// the round (profiles/r02_gemm_gl_ab.txt: 0.272 vs 0.255 ms; its one-stage prefetch exposes the
-// operands' first-touch latency every 32 k), so opt-in: CGL_GEMM_GL=1.
-bool gemm_gl_enabled() {
+// BatchNorm1d folded into the neighbouring GEMMs' operand loads instead of the cgl_bn_apply (bit 1:
+// forward, a_bn 1) / cgl_bn_bwd (bit 2: backward, a_bn 2) launches.  CGL_BN_FOLD = mask, default 0:
+// correct (the MLP GPU suite passes with either bit) but measured slower in the B = 256 round
+// (profiles/r03_bn_fold_ab.txt: 0.259 ms separate, 0.270 / 0.269 / 0.281 ms with bit 1 / 2 / both --
+// the consumer GEMMs grow by more than the launches they remove: the forward fold's prologue and
+// the backward fold's second operand stream, re-read by every column tile)
+int bn_fold_mask() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("CGL_GEMM_GL");
-    v = (e && atoi(e) != 0) ? 1 : 0;
+    const char* e = getenv("CGL_BN_FOLD");
+    v = e ? atoi(e) : 0;
   }
-  return v == 1;
+  return v;
 }
 
-bool bn_fuse_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("CGL_BN_FUSE");
-    v = (e && atoi(e) != 0) ? 1 : 0;
-  }
-  return v == 1;
-}
-
-// Add a grouped GEMM launch built from `descs` (workgroup offsets assigned here).  Returns false --
-// and pushes nothing -- when a fused-BatchNorm problem is in the group but the launch's grid is not
-// guaranteed co-resident (its in-launch rendezvous could then wait on an unscheduled workgroup).
-bool push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> descs) {
+// Add a grouped GEMM launch built from `descs` (workgroup offsets assigned here).
+void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> descs) {
   Launch L;
   L.kind = K_GEMM;
   L.first = (int)c->gemm.size();
@@ -552,41 +525,18 @@ bool push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
       blk = d.TM;
     }
   }
-  bool fused0 = false;
-  for (auto& d : descs) fused0 = fused0 || d.bn_fuse != 0;
-  if (fused0) blk = 1;   // the BNF instantiation is 1x1
   for (auto& d : descs)
     if (d.TM != blk) choose_tiles(d, 0, blk);
-  // LDS-staged main loop: every problem of the launch must qualify (a TN problem beside it would
-  // pay the ring's LDS in occupancy); its tiling is 32x32 per workgroup with the four waves on K
-  // slices (microbenchmarked best for the staged loop: tools/gemm_lds_bench.hip)
-  bool gl = blk == 1 && gemm_gl_enabled() && c->cfg.gemm_dtype == CGL_DTYPE_F32;
   L.dt = c->cfg.gemm_dtype;
-  for (auto& d : descs) {
-    set_vec(d);
-    CglGemmDesc t = d;
-    t.WM = t.WN = 1;
-    t.WK = 4;
-    t.ksplit = 1;
-    gl = gl && !d.bn_fuse && cgl_gemm_gl_ok(t);
-  }
-  if (gl)
-    for (auto& d : descs) {
-      d.WM = d.WN = 1;
-      d.WK = 4;
-      d.tiles_m = (d.M + 31) / 32;
-      d.tiles_n = (d.N + 31) / 32;
-    }
   L.blk = blk;
   long kp = 0;
   unsigned int kc = 0;
-  bool fused = false;
-  for (auto& d : descs) fused = fused || d.bn_fuse != 0;
   for (auto& d : descs) {
     set_vec(d);
-    // split-K: only on the single-stream plan (the partial / ticket regions are per launch)
+    // split-K: only on the single-stream plan (the partial / ticket regions are per launch), never
+    // under an operand transform (its prologue tables are per workgroup)
     d.ksplit = 1;
-    if (!c->two_streams && !fused && !gl) {
+    if (!c->two_streams && !d.a_bn) {
       choose_ks(d);
       if (d.ksplit > 1 && (kp + cgl_gemm_kpart_floats(d) > kSplitKFloats ||
                            kc + d.tiles_m * d.tiles_n > (unsigned)kSplitKCounters))
@@ -598,6 +548,8 @@ bool push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
         kc += d.tiles_m * d.tiles_n;
       }
     }
+    d.tab_floats = cgl_gemm_tab_floats(d);
+    L.abn = std::max(L.abn, d.a_bn);
     d.wg_begin = wg;
     wg += cgl_gemm_wgs(d);
     L.sk = L.sk || d.ksplit > 1;
@@ -608,49 +560,15 @@ bool push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
   }
   L.grid = wg;
   L.shmem = stage;
-  L.bnf = fused;
-  if (gl) {
-    L.gl = true;
-    int st2 = 0;
-    for (int q = L.first; q < L.first + L.count; ++q) st2 = std::max(st2, cgl_gemm_stage_bytes(c->gemm[q], true));
-    L.shmem = st2;
-  }
   if (getenv("CGL_PLAN_DEBUG")) {
     for (int q = L.first; q < L.first + L.count; ++q) {
       const CglGemmDesc& d = c->gemm[q];
       fprintf(stderr, "gemm launch %zu: desc %d layout %d M %d N %d K %d WM %d WN %d WK %d TM %d TN %d tiles %dx%d "
-              "ks %d grid %d shmem %d gl %d blk %d vec %d/%d\n", ph.size(), q, d.layout, d.M, d.N, d.K, d.WM, d.WN,
-              d.WK, d.TM, d.TN, d.tiles_m, d.tiles_n, d.ksplit, L.grid, L.shmem, (int)L.gl, L.blk, d.a_vec, d.b_vec);
+              "ks %d grid %d shmem %d blk %d vec %d/%d a_bn %d\n", ph.size(), q, d.layout, d.M, d.N, d.K, d.WM, d.WN,
+              d.WK, d.TM, d.TN, d.tiles_m, d.tiles_n, d.ksplit, L.grid, L.shmem, L.blk, d.a_vec, d.b_vec, d.a_bn);
     }
-  }
-  if (fused) {
-    int rv = c->rv_used;
-    for (auto& d : descs) {
-      if (!d.bn_fuse) continue;
-      const bool ok = d.tiles_m <= CGL_BN_MAXT && d.tiles_m * d.WN * d.TN * 32 <= 256 * CGL_BN_STG &&
-                      rv + d.tiles_n <= kRvCounters &&
-                      (d.bn_fuse != 1 || (d.M + d.stat_gr - 1) / d.stat_gr <= 2);
-      if (!ok) {
-        c->gemm.resize(L.first);
-        return false;
-      }
-    }
-    const int cap = gemm_resident(blk, stage);
-    if (cap <= 0 || L.grid > cap) {
-      c->gemm.resize(L.first);
-      return false;
-    }
-    for (int q = L.first; q < L.first + L.count; ++q) {
-      CglGemmDesc& d = c->gemm[q];
-      if (!d.bn_fuse) continue;
-      d.rv_count = c->ws.rvcount + rv;
-      d.err = &c->ws.st->err;
-      rv += d.tiles_n;
-    }
-    c->rv_used = rv;
   }
   ph.push_back(L);
-  return true;
 }
 
 void push_head(cgl_gan* c, std::vector<Launch>& ph, const CglHeadDesc& h) {
@@ -742,7 +660,14 @@ int build_plan(cgl_gan* c) {
     A.push_back(Lp);
   }
 
-  // ---- G forward on [z1; z2] (2B rows; BatchNorm statistics per B-row forward call)
+  // ---- G forward on [z1; z2] (2B rows; BatchNorm statistics per B-row forward call).  The
+  // BatchNorm1d(train) + LeakyReLU of a layer's output is applied by the next layer's GEMM as it
+  // loads its A operand (a_bn 1: statistics from this GEMM's per-tile partials, combined in the
+  // consumer's prologue), which also writes the activation out for the backward pass; a
+  // cgl_bn_apply launch remains for shapes the fold does not cover (and with CGL_BN_FOLD=0).
+  CglBnFwd pend;
+  std::memset(&pend, 0, sizeof(pend));
+  bool pend_on = false;
   for (int l = 0; l < L; ++l) {
     const int fi = g.dims[l], fo = g.dims[l + 1];
     CglGemmDesc e = make_gemm(0, 2 * B, fo, fi);
@@ -751,7 +676,28 @@ int build_plan(cgl_gan* c) {
       e.a = rows(c->bufs.z, fi);
     } else {
       e.a = rows(w.gout[l - 1], fi);
-      if (g.bn[l - 1]) e.a = rows(w.gact[l - 1], fi);   // BatchNorm + LeakyReLU applied by cgl_bn_apply
+    }
+    if (pend_on) {
+      const int bm = 32 * e.TM * e.WM;
+      if ((bn_fold_mask() & 1) && cf.gemm_dtype == CGL_DTYPE_F32 && fi <= CGL_BN_MAXF && B % bm == 0) {
+        e.a_bn = 1;
+        e.a_bnf = pend;
+        e.a_copy = w.gact[l - 1];        // the activation, for the backward pass (both calls' rows)
+        e.a_copy_ld = fi;
+        e.a_copy_row0 = 0;
+      } else {
+        CglBnApplyDesc ap;
+        std::memset(&ap, 0, sizeof(ap));
+        ap.F = fi;
+        ap.Y = w.gout[l - 1];
+        ap.ld_y = fi;
+        ap.act = w.gact[l - 1];
+        ap.ld_act = fi;
+        ap.bn = pend;
+        push_bna(c, A, ap);
+        e.a = rows(w.gact[l - 1], fi);
+      }
+      pend_on = false;
     }
     e.a_vec = (fi % 4 == 0) && al16(e.a.p0);
     e.b = rows(gparam(c, l, 0), fi);
@@ -769,35 +715,12 @@ int build_plan(cgl_gan* c) {
     e.slope = sl;
     e.C = w.gout[l];
     e.ldc = fo;
-    if (l + 1 < L && g.bn[l] && bn_fuse_enabled() && cf.gemm_dtype == CGL_DTYPE_F32) {
-      // BatchNorm1d(train) + LeakyReLU in this GEMM's epilogue (in-launch rendezvous of each
-      // column tile's row tiles) instead of a cgl_bn_apply launch
-      CglGemmDesc f = e;
-      f.bn_fuse = 1;
-      f.bn_gamma = gparam(c, l, 2);
-      f.bn_beta = gparam(c, l, 3);
-      f.bn_act = w.gact[l];
-      f.bn_ld_act = fo;
-      f.bn_eps = cf.bn_eps;
-      f.bn_momentum = cf.bn_momentum;
-      f.bn_run_mean = c->bufs.g_running + c->run_mean_off[l];
-      f.bn_run_var = c->bufs.g_running + c->run_var_off[l];
-      f.bn_save_mean = w.gmean[l];
-      f.bn_save_invstd = w.ginvstd[l];
-      if (push_gemm(c, A, {f})) continue;
-    }
     push_gemm(c, A, {e});
     if (l + 1 < L && g.bn[l]) {
-      CglBnApplyDesc ap;
-      std::memset(&ap, 0, sizeof(ap));
-      ap.F = fo;
-      ap.Y = w.gout[l];
-      ap.ld_y = fo;
-      ap.act = w.gact[l];
-      ap.ld_act = fo;
-      CglBnFwd& bn = ap.bn;
+      CglBnFwd& bn = pend;
+      std::memset(&bn, 0, sizeof(bn));
       bn.part = w.gpart[l];
-      // the producer's row-tile height as pushed (push_gemm may re-tile the launch)
+      // the producer's row-tile height as pushed
       bn.part_bm = 32 * c->gemm.back().TM * c->gemm.back().WM;
       bn.gr = B;
       bn.mtot = 2 * B;
@@ -810,7 +733,7 @@ int build_plan(cgl_gan* c) {
       bn.run_var = c->bufs.g_running + c->run_var_off[l];
       bn.save_mean = w.gmean[l];
       bn.save_invstd = w.ginvstd[l];
-      push_bna(c, A, ap);
+      pend_on = true;
     }
   }
   const float* Xd = w.gout[L - 1];
@@ -1035,10 +958,41 @@ int build_plan(cgl_gan* c) {
     c->xchg_n = (int64_t)B * img;
     ph = &Bp;
   }
+  // The BatchNorm1d backward of layer l - 1 is folded into the GEMMs around it (a_bn 2): the
+  // input-gradient GEMM of layer l stores dy = dA * LeakyReLU'(post) with per-tile {sum dy,
+  // sum (y - mean) dy} partials, and layer l - 1's weight- and input-gradient GEMMs apply the
+  // BatchNorm backward as they load dy (their k-contiguous problem also writes dgamma / dbeta).
+  // Not at the Mix-G exchange point (the all-reduce of dA sits between the two), and a cgl_bn_bwd
+  // launch where no input-gradient problem follows (and with CGL_BN_FOLD=0).
   auto gbuf = [&](int l) -> float* { return l == L - 1 ? w.dYL : w.gG[l]; };
+  CglBnBwdFold gfold;
+  std::memset(&gfold, 0, sizeof(gfold));
+  bool gfold_on = false;          // layer l's output gradient is dy in gdA[l] + partials
   for (int l = L - 1; l >= 0; --l) {
     std::vector<CglGemmDesc> grp;
     const int fi = g.dims[l], fo = g.dims[l + 1];
+    const float* gA = gfold_on ? w.gdA[l] : gbuf(l);
+    if (gfold_on && l == 0) {     // no input-gradient problem to carry the fold: the launch
+      CglBnBwdDesc b;             // (dy already masked: no post)
+      std::memset(&b, 0, sizeof(b));
+      b.M = B;
+      b.F = fo;
+      b.dA = w.gdA[l];
+      b.ld_da = fo;
+      b.Y = gfold.y;
+      b.ld_y = fo;
+      b.mean = gfold.mean;
+      b.invstd = gfold.invstd;
+      b.gamma = gfold.gamma;
+      b.dZ = w.gG[l];
+      b.ld_dz = fo;
+      b.g_gamma = gfold.g_gamma;
+      b.g_beta = gfold.g_beta;
+      b.slope = sl;
+      push_bnb(c, *ph, b);
+      gfold_on = false;
+      gA = gbuf(l);
+    }
     {
       const float* prev;
       if (l == 0)
@@ -1048,57 +1002,71 @@ int build_plan(cgl_gan* c) {
       else
         prev = w.gout[l - 1] + (int64_t)B * fi;
       CglGemmDesc t = make_gemm(2, fo, fi + 1, B);
-      t.a = rows(gbuf(l), fo);
+      t.a = rows(gA, fo);
       t.b = rows(prev, fi);
       t.b_ones_col = 1;
       t.C = ggrad(c, l, 0);
       t.ldc = fi;
       t.bias_out = ggrad(c, l, 1);
+      if (gfold_on) {
+        t.a_bn = 2;
+        t.a_bnb = gfold;
+      }
       grp.push_back(t);
     }
-    bool bn_fused = false;
+    bool fold_next = false;
     if (l >= 1) {
       CglGemmDesc n = make_gemm(1, B, fi, fo);
-      n.a = rows(gbuf(l), fo);
+      n.a = rows(gA, fo);
       n.a_vec = (fo % 4 == 0);
       n.b = rows(gparam(c, l, 0), fi);
       n.slope = sl;
       n.ldc = fi;
+      if (gfold_on) {
+        n.a_bn = 2;
+        n.a_bnb = gfold;
+      }
       if (g.bn[l - 1]) {
         n.C = w.gdA[l - 1];
+        fold_next = (bn_fold_mask() & 2) && cf.gemm_dtype == CGL_DTYPE_F32 && cf.exchange_layer != l &&
+                    fi <= CGL_BN_MAXF;
+        if (fold_next) {
+          n.mask_ref = w.gact[l - 1] + (int64_t)B * fi;    // LeakyReLU' of the BatchNorm output
+          n.mask_ld = fi;
+          n.bnb_part = w.gdpart[l - 1];
+          n.bnb_y = w.gout[l - 1] + (int64_t)B * fi;       // the Xg call's BatchNorm input
+          n.bnb_ld = fi;
+          n.bnb_mean = w.gmean[l - 1] + fi;                // group 1 = the Xg forward call
+        }
       } else {
         n.mask_ref = w.gout[l - 1] + (int64_t)B * fi;
         n.mask_ld = fi;
         n.C = w.gG[l - 1];
       }
-      // BatchNorm1d backward in the input-gradient GEMM's epilogue (not at the Mix-G exchange
-      // point: there the all-reduce of dA sits between the GEMM and the BatchNorm backward)
-      if (g.bn[l - 1] && cf.exchange_layer != l && bn_fuse_enabled() && cf.gemm_dtype == CGL_DTYPE_F32) {
-        CglGemmDesc f = n;
-        f.bn_fuse = 2;
-        f.C = w.gG[l - 1];
-        f.bn_post = w.gact[l - 1] + (int64_t)B * fi;
-        f.bn_y = w.gout[l - 1] + (int64_t)B * fi;
-        f.bn_ld_post = fi;
-        f.bn_mean = w.gmean[l - 1] + fi;        // group 1 = the Xg forward call
-        f.bn_invstd = w.ginvstd[l - 1] + fi;
-        f.bn_gamma = gparam(c, l - 1, 2);
-        f.bn_g_gamma = ggrad(c, l - 1, 2);
-        f.bn_g_beta = ggrad(c, l - 1, 3);
-        f.bn_dpart = w.gdpart[l - 1];
-        std::vector<CglGemmDesc> g2 = grp;
-        g2.push_back(f);
-        bn_fused = push_gemm(c, *ph, g2);
-      }
       grp.push_back(n);
     }
-    if (!bn_fused) push_gemm(c, *ph, grp);
+    push_gemm(c, *ph, grp);
+    gfold_on = false;
+    if (fold_next) {
+      gfold.part = w.gdpart[l - 1];
+      gfold.tiles = c->gemm.back().tiles_m;
+      gfold.F = fi;
+      gfold.M = B;
+      gfold.mean = w.gmean[l - 1] + fi;
+      gfold.invstd = w.ginvstd[l - 1] + fi;
+      gfold.gamma = gparam(c, l - 1, 2);
+      gfold.g_gamma = ggrad(c, l - 1, 2);
+      gfold.g_beta = ggrad(c, l - 1, 3);
+      gfold.y = w.gout[l - 1] + (int64_t)B * fi;
+      gfold.ldy = fi;
+      gfold_on = true;
+    }
     if (l >= 1 && cf.exchange_layer == l) {
       c->xchg = g.bn[l - 1] ? w.gdA[l - 1] : w.gG[l - 1];
       c->xchg_n = (int64_t)B * fi;
       ph = &Bp;
     }
-    if (l >= 1 && g.bn[l - 1] && !bn_fused) {
+    if (l >= 1 && g.bn[l - 1] && !fold_next) {
       CglBnBwdDesc b;
       std::memset(&b, 0, sizeof(b));
       b.M = B;
@@ -1164,7 +1132,7 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
   }
   switch (L.kind) {
     case K_GEMM:
-      launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, L.count, L.sk, L.gl, L.dt, L.bnf);
+      launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, L.count, L.sk, L.dt, L.abn);
       break;
     case K_HEAD:
       hipLaunchKernelGGL(cgl_head_loss, dim3(L.grid), dim3(256), 0, s, c->ws.head + L.first);
@@ -1307,7 +1275,6 @@ int cgl_gan_create(const cgl_gan_config* cfg, const cgl_gan_buffers* bufs, cgl_g
     he = hipMemcpy(c->ws.bnb, c->bnb.data(), c->bnb.size() * sizeof(CglBnBwdDesc), hipMemcpyHostToDevice);
   if (he == hipSuccess) he = hipMemset(c->ws.counters, 0, kCounters * sizeof(unsigned int));
   if (he == hipSuccess) he = hipMemset(c->ws.kcount, 0, kSplitKCounters * sizeof(unsigned int));
-  if (he == hipSuccess) he = hipMemset(c->ws.rvcount, 0, kRvCounters * sizeof(unsigned int));
   if (he == hipSuccess) he = hipMemset(c->ws.st, 0, sizeof(CglStepState));
   if (he == hipSuccess) he = hipDeviceSynchronize();
   if (he != hipSuccess) {
@@ -1337,7 +1304,6 @@ int cgl_gan_reset(cgl_gan* c, const float* beta_host, void* stream) {
   HIPCHK(hipMemcpyAsync(c->ws.st, &h, sizeof(h), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemsetAsync(c->ws.counters, 0, kCounters * sizeof(unsigned int), s));
   HIPCHK(hipMemsetAsync(c->ws.kcount, 0, kSplitKCounters * sizeof(unsigned int), s));
-  HIPCHK(hipMemsetAsync(c->ws.rvcount, 0, kRvCounters * sizeof(unsigned int), s));
   HIPCHK(hipStreamSynchronize(s));
   return CGL_OK;
 }
