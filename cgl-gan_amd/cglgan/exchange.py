@@ -26,7 +26,6 @@ tests).  Both expose the same three collectives, so ``WorkerExchange`` is writte
 """
 from __future__ import annotations
 
-import os
 import random
 
 import torch
@@ -138,9 +137,7 @@ class WorkerExchange:
             self.comm.all_gather(s.losses_all, s.own_loss())
             s.alpha_scale()
             self.comm.all_reduce_sum(s.exchange_buffer())
-            # (not beside the opt-in fused-BatchNorm GEMMs: their in-launch rendezvous needs every
-            # workgroup of the launch co-resident, which side-stream kernels holding CUs can break)
-            side = self._side_stream() if (share or swap) and not _bn_fuse_on() else None
+            side = self._side_stream() if (share or swap) else None
             if side is not None:
                 # phase B (G backward + Adam G) never touches D: the E-share all-reduce / D-swap of
                 # this round's updated D run on a side stream concurrently with it (issued in the
@@ -192,10 +189,6 @@ class WorkerExchange:
             self.cloud.all_reduce_mean(t, self.cloud_weights)
             if own is not None:     # segema * self_p + (1 - segema) * recv_p, in that order
                 torch.add(own * self.segema, t * (1.0 - self.segema), out=t)
-
-
-def _bn_fuse_on():
-    return os.environ.get("CGL_BN_FUSE", "0") not in ("", "0")
 
 
 def mixg_cloud_due(num_communication: int, cloud_epoch: int):
