@@ -394,10 +394,14 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   const float* y_base[TM];
   const float* b_base[TN];
   bool b_is_ones[TN], copy_row[TM];
+  const int kcn = (K + CGL_GEMM_KCHUNK - 1) / CGL_GEMM_KCHUNK;   // k chunks (packed block stride)
+  const bool apk = LAYOUT == 0 && d->a_pk, bpk = LAYOUT == 0 && d->b_pk;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int am = m0 + 32 * i + li;      // A row (kc) or A column (mn)
     a_base[i] = (LAYOUT != 2) ? cgl_row(d->a, min(am, M - 1)) : d->a.p0 + min(am, M - 1);
+    // packed A: the lane's float4 of chunk 0 of its (clamped) 32-row block
+    if (apk) a_base[i] = d->a.p0 + (long)(min(m0 + 32 * i, (M - 1) & ~31) >> 5) * kcn * 512 + lane * 4;
     y_base[i] = ybn ? ((LAYOUT != 2) ? ybase + (long)min(am, M - 1) * ldy : ybase + min(am, M - 1)) : a_base[i];
     copy_row[i] = (LAYOUT != 2) && a_copy && am < M && am >= d->a_copy_row0;
   }
@@ -406,17 +410,22 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     const int bc = n0 + 32 * j + li;      // B row (NT) or B column (NN/TN)
     b_is_ones[j] = b_ones && (bc == N - 1);
     b_base[j] = (LAYOUT == 0) ? cgl_row(d->b, min(bc, N - 1)) : d->b.p0 + max(0, min(bc, nmem - 1));
+    if (bpk) b_base[j] = d->b.p0 + (long)(min(n0 + 32 * j, (N - 1) & ~31) >> 5) * kcn * 512 + lane * 4;
   }
 
   // Full chunks (k + 16 <= K) load without clamps and multiply without masks: rows / columns
   // past M / N come from clamped (valid) addresses and only feed accumulator rows / columns
   // that are never stored.  Only the K-tail chunk clamps its k and zeroes k >= K.
-  auto load_a = [&](auto tail, int c, const float* const (&base)[TM], int ld, float (&A_)[TM][8]) {
+  auto load_a = [&](auto tail, int c, const float* const (&base)[TM], int ld, float (&A_)[TM][8], bool pk) {
     constexpr bool T = decltype(tail)::value;
     const int k = c * CGL_GEMM_KCHUNK + 8 * lh;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      if (LAYOUT == 2) {
+      if (LAYOUT == 0 && pk) {          // packed: two contiguous 1 KB wave loads (padding past K)
+        const f32x4 x = *(gcf4p)(base[i] + c * 512), y = *(gcf4p)(base[i] + c * 512 + 256);
+        A_[i][0] = x[0]; A_[i][1] = x[1]; A_[i][2] = x[2]; A_[i][3] = x[3];
+        A_[i][4] = y[0]; A_[i][5] = y[1]; A_[i][6] = y[2]; A_[i][7] = y[3];
+      } else if (LAYOUT == 2) {
         if (T) {
           cgl_ld_mn(base[i], ld, k, K, A_[i]);
         } else {
@@ -441,12 +450,16 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   auto load_chunk = [&](auto tail, int c, float (&A_)[TM][8], auto& Y_, float (&B_)[TN][8]) {
     constexpr bool T = decltype(tail)::value;
     const int k = c * CGL_GEMM_KCHUNK + 8 * lh;
-    load_a(tail, c, a_base, lda, A_);
+    load_a(tail, c, a_base, lda, A_, apk);
     if constexpr (ABN == 2)
-      if (ybn) load_a(tail, c, y_base, ldy, Y_);
+      if (ybn) load_a(tail, c, y_base, ldy, Y_, false);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      if (LAYOUT == 0) {
+      if (LAYOUT == 0 && bpk) {
+        const f32x4 x = *(gcf4p)(b_base[j] + c * 512), y = *(gcf4p)(b_base[j] + c * 512 + 256);
+        B_[j][0] = x[0]; B_[j][1] = x[1]; B_[j][2] = x[2]; B_[j][3] = x[3];
+        B_[j][4] = y[0]; B_[j][5] = y[1]; B_[j][6] = y[2]; B_[j][7] = y[3];
+      } else if (LAYOUT == 0) {
         if (T) {
           cgl_ld_kc<VEC>(b_base[j], k, K, B_[j]);
         } else if (VEC) {

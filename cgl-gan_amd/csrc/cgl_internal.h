@@ -40,6 +40,30 @@ __device__ __forceinline__ float cgl_dtanh(float g, float t) {
   return (float)((double)g * (1.0 - td * td));
 }
 
+// Fragment-packed operand layout P(X; R, K) of the MFMA GEMMs (cgl_gemm.hip): 32-row blocks x 16-k
+// chunks x 2 halves x 64 lanes x 4 floats.  Lane l = (r % 32) + 32 lh of a row block holds, for
+// chunk c and half h, X[r][16 c + 8 lh + 4 h + e] (e = 0..3) -- the k-permuted 32x32x2 fragment --
+// at float ((rb Kc + c) 2 + h) 256 + 4 l + e, so each 16-byte fragment load of a wave reads one
+// contiguous 1 KB (8 whole 128-byte lines) instead of 64 pieces of 32 rows.  Padding rows / k
+// (past R / K) are never consumed unmasked.
+__host__ __device__ inline long cgl_pk_off(int r, int k, int Kc) {
+  return ((long)((r >> 5) * Kc + (k >> 4)) * 2 + ((k >> 2) & 1)) * 256 + ((r & 31) + 32 * ((k >> 3) & 1)) * 4 + (k & 3);
+}
+inline long cgl_pk_floats(int R, int K) { return (long)((R + 31) / 32) * ((K + 15) / 16) * 512; }
+
+// Packing job of the round prologue: dst = P(X; R, K) with X[r][k] = trans ? src[k ld + r] : src[r ld + k]
+#define CGL_PACK_MAXJ 12
+struct CglOpPackJob {
+  const float* src;
+  float* dst;
+  int R, K, ld, trans;
+  int blk_begin;          // first prologue block of this job (one packed float4 per thread)
+};
+struct CglOpPack {
+  int nj, blocks;
+  CglOpPackJob j[CGL_PACK_MAXJ];
+};
+
 // Row source of a row-major operand whose rows are the non-contiguous index.
 // Row r < split comes from p0 (optionally through idx0[idx_off + r]), rows >= split from p1.
 struct CglRowSrc {
@@ -91,6 +115,7 @@ struct CglGemmDesc {
   int a_vec, b_vec;       // 16-byte vector loads allowed along each operand's contiguous dim
   int TM, TN;             // 32x32 accumulator blocks per wave (1x1 or 2x2)
   CglRowSrc a, b;
+  int a_pk, b_pk;         // NT operand in the fragment-packed layout P (a.p0 / b.p0 = its base)
   // A copy-out (kc A only)
   float* a_copy;         // optional copy-out of the (transformed) A rows; rows >= a_copy_row0
   int a_copy_ld, a_copy_row0;
@@ -128,6 +153,7 @@ struct CglBnApplyDesc {
   int F;
   const float* Y; int ld_y;       // pre-BN (Linear output)
   float* act; int ld_act;         // post-LeakyReLU
+  float* act_pk;                  // the same in the fragment-packed layout P(act; mtot, F), or null
   CglBnFwd bn;
 };
 
@@ -172,6 +198,7 @@ struct CglBnBwdDesc {
   const float* Y; int ld_y;       // BatchNorm input (pre-BN)
   const float* mean; const float* invstd; const float* gamma;
   float* dZ; int ld_dz;           // gradient w.r.t. the BatchNorm input
+  float* dZ_pk;                   // the same in the fragment-packed layout P(dZ; M, F), or null
   float* g_gamma; float* g_beta;
   float slope;
 };

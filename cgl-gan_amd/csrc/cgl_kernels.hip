@@ -220,13 +220,16 @@ __global__ __launch_bounds__(256) void cgl_bn_apply(const CglBnApplyDesc* __rest
   }
   if (f >= F) return;
   const float sl = bn.slope;
+  const int kc = (F + 15) >> 4;
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
     const int r = r0 + rl + 4 * i;
     if (r < mtot) {
       const int g = r >= bn.gr ? 1 : 0;
       const float x = fmaf(y[i], s_sc[g][fl], s_sh[g][fl]);
-      gst(ad->act + (long)r * ad->ld_act + f, x > 0.f ? x : x * sl);
+      const float a = x > 0.f ? x : x * sl;
+      gst(ad->act + (long)r * ad->ld_act + f, a);
+      if (ad->act_pk) gst(ad->act_pk + cgl_pk_off(r, f, kc), a);   // the next GEMM's packed A operand
     }
   }
 }
@@ -258,6 +261,7 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
   const long lda = bd->ld_da, ldp = bd->ld_post, ldy = bd->ld_y;
   float* dZ = bd->dZ + fc;
   const long ldz = bd->ld_dz;
+  const int kcz = (F + 15) >> 4;
   double sum = 0.0, dotp = 0.0;
   if (M <= 8 * CGL_BNB_RPT) {
     float dy[CGL_BNB_RPT], yc[CGL_BNB_RPT];
@@ -292,7 +296,11 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
 #pragma unroll
       for (int j = 0; j < CGL_BNB_RPT; ++j) {
         const int r = rg + 8 * j;
-        if (r < M) gst(dZ + r * ldz, (dy[j] - gmean - yc[j] * k) * invstd * w);
+        if (r < M) {
+          const float z = (dy[j] - gmean - yc[j] * k) * invstd * w;
+          gst(dZ + r * ldz, z);
+          if (bd->dZ_pk) gst(bd->dZ_pk + cgl_pk_off(r, f, kcz), z);   // the input-gradient GEMM's packed A
+        }
       }
       if (rg == 0) {
         gst(bd->g_gamma + f, (float)(D * (double)invstd));
@@ -345,7 +353,9 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
       if (r < M) {
         const float dy = (!post_on || po[j] > 0.f) ? da[j] : da[j] * sl;
         const float gi = (y[j] - mean) * k;
-        gst(dZ + r * ldz, (dy - gmean - gi) * invstd * w);
+        const float z = (dy - gmean - gi) * invstd * w;
+        gst(dZ + r * ldz, z);
+        if (bd->dZ_pk) gst(bd->dZ_pk + cgl_pk_off(r, f, kcz), z);
       }
     }
   }

@@ -143,6 +143,10 @@ struct WS {
   float* kpart;             // [kSplitKFloats]: split-K partials (reused by every launch)
   unsigned int* kcount;     // [kSplitKCounters]: split-K tickets (zero at rest)
   double* gdpart[CGL_MAX_LAYERS];   // backward BatchNorm partials of dy [B/32][f][2] (a_bn 2)
+  float* gpk[CGL_MAX_LAYERS];       // packed BatchNorm + LeakyReLU output P(act_l; 2B, f) (next GEMM's A)
+  float* wpk[CGL_MAX_LAYERS];       // packed G weights P(W_l; fo, fi) (the forward GEMM's B)
+  float* wtpk[CGL_MAX_LAYERS];      // packed transposed G weights P(W_l^T; fi, fo) (input-gradient B)
+  float* gGpk[CGL_MAX_LAYERS];      // packed cgl_bn_bwd output P(dZ_l; B, f) (input-gradient A)
   CglStepState* st;
   int* idx;       // sampler output when sample_n > 0
   CglGemmDesc* gemm;
@@ -196,6 +200,12 @@ WS carve_ws(const cgl_gan_config& c, void* base) {
   w.kcount = cv.take<unsigned int>(kSplitKCounters);
   for (int l = 0; l + 1 < L; ++l)
     if (g.bn[l]) w.gdpart[l] = cv.take<double>((int64_t)((B + 31) / 32) * g.dims[l + 1] * 2);
+  for (int l = 0; l < L; ++l) {
+    if (l + 1 < L && g.bn[l]) w.gpk[l] = cv.take<float>(cgl_pk_floats(2 * B, g.dims[l + 1]));
+    w.wpk[l] = cv.take<float>(cgl_pk_floats(g.dims[l + 1], g.dims[l]));
+    if (l >= 1) w.wtpk[l] = cv.take<float>(cgl_pk_floats(g.dims[l], g.dims[l + 1]));
+    if (l + 1 < L && g.bn[l]) w.gGpk[l] = cv.take<float>(cgl_pk_floats(B, g.dims[l + 1]));
+  }
   w.total = cv.off;
   return w;
 }
@@ -297,7 +307,8 @@ void launch_gemm(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc*
 //   (a fragment load touches 32 cache lines), plus the split-K reduction.
 //   KS > 1: cross-workgroup split-K -- KS times the workgroups, 1 / KS of the chunks each, plus
 //   the combine (publish, ticket, the reducer's read of KS partials).
-double gemm_cost(int M, int N, int K, int WM, int WN, int WK, int TM, int TN, int KS = 1) {
+double gemm_cost(int M, int N, int K, int WM, int WN, int WK, int TM, int TN, int KS = 1, double ta_a = 1.0,
+                 double ta_b = 1.0) {
   const double lat = 2000.0;
   const int S = 3;
   const long tiles = (long)((M + 32 * TM * WM - 1) / (32 * TM * WM)) * ((N + 32 * TN * WN - 1) / (32 * TN * WN));
@@ -307,7 +318,8 @@ double gemm_cost(int M, int N, int K, int WM, int WN, int WK, int TM, int TN, in
   const double blk = 512.0 * TM * TN;
   const double mfma = wg_per_cu * per * blk;
   const double chain = per * std::max(blk, lat / (S - 1));
-  const double ta = wg_per_cu * 4 * per * (TM + TN) * 64.0;
+  // a fragment load of a row-major k-contiguous operand touches 32 lines, a packed one 8 (ta_x = 1 / 0.25)
+  const double ta = wg_per_cu * 4 * per * (TM * ta_a + TN * ta_b) * 64.0;
   return std::max(mfma, std::max(chain, ta)) + (WK > 1 ? 400.0 * TM * TN : 0.0) +
          (KS > 1 ? 2400.0 + 300.0 * KS * TM * TN : 0.0);
 }
@@ -378,7 +390,7 @@ void choose_tiles(CglGemmDesc& d, int force_wm = 0, int force_t = 0) {
     if (force_t && t != force_t) continue;
     for (auto& o : opts) {
       if (force_wm && o[0] * t != force_wm) continue;
-      const double c = gemm_cost(d.M, d.N, d.K, o[0], o[1], o[2], t, t);
+      const double c = gemm_cost(d.M, d.N, d.K, o[0], o[1], o[2], t, t, 1, d.a_pk ? 0.25 : 1.0, d.b_pk ? 0.25 : 1.0);
       if (c < best * (1.0 - 1e-9)) {
         best = c;
         d.WM = o[0];
@@ -417,8 +429,8 @@ void set_vec(CglGemmDesc& d) {
   };
   const int nmem = d.N - (d.layout != 0 ? d.b_ones_col : 0);
   if (d.layout == 0) {
-    d.a_vec = (d.K % 4 == 0) && src_ok(d.a);
-    d.b_vec = (d.K % 4 == 0) && src_ok(d.b);
+    d.a_vec = d.a_pk || ((d.K % 4 == 0) && src_ok(d.a));
+    d.b_vec = d.b_pk || ((d.K % 4 == 0) && src_ok(d.b));
   } else if (d.layout == 1) {
     d.a_vec = (d.K % 4 == 0) && src_ok(d.a);
     d.b_vec = (nmem % 4 == 0) && src_ok(d.b);
@@ -453,6 +465,7 @@ struct cgl_gan {
   hipGraphExec_t gexec[3] = {nullptr, nullptr, nullptr};
   hipStream_t cap = nullptr;   // private capture stream (the legacy default stream cannot capture)
   hipStream_t side = nullptr;  // second stream: the real-row D chain of the first local D step
+  CglOpPack pack{};          // the round prologue's operand-packing jobs
   hipEvent_t ev[2] = {nullptr, nullptr};   // fork (after the prologue), join (before the D-step head)
   bool two_streams = false;
   float* xchg = nullptr;
@@ -506,6 +519,16 @@ int bn_fold_mask() {
     v = e ? atoi(e) : 0;
   }
   return v;
+}
+
+// Fragment-packed GEMM operands (cgl_pk_off): on by default, CGL_PACK=0 keeps every operand row-major.
+bool pack_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CGL_PACK");
+    v = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return v == 1;
 }
 
 // Add a grouped GEMM launch built from `descs` (workgroup offsets assigned here).
@@ -677,6 +700,19 @@ int build_plan(cgl_gan* c) {
     } else {
       e.a = rows(w.gout[l - 1], fi);
     }
+    // fragment-packed operands (cgl_pk_off): the weights, packed by the round prologue, and the
+    // BatchNorm + LeakyReLU output cgl_bn_apply writes packed beside its row-major copy
+    const bool pk_on = pack_enabled();
+    if (pk_on && fi >= 256 && c->pack.nj < CGL_PACK_MAXJ) {   // (short-K layers: no gain measured)
+      CglOpPackJob& J = c->pack.j[c->pack.nj++];
+      J.src = gparam(c, l, 0);
+      J.dst = w.wpk[l];
+      J.R = fo;
+      J.K = fi;
+      J.ld = fi;
+      J.trans = 0;
+      e.b_pk = 1;
+    }
     if (pend_on) {
       const int bm = 32 * e.TM * e.WM;
       if ((bn_fold_mask() & 1) && cf.gemm_dtype == CGL_DTYPE_F32 && fi <= CGL_BN_MAXF && B % bm == 0) {
@@ -694,13 +730,18 @@ int build_plan(cgl_gan* c) {
         ap.act = w.gact[l - 1];
         ap.ld_act = fi;
         ap.bn = pend;
+        if (pk_on) {
+          ap.act_pk = w.gpk[l - 1];
+          e.a_pk = 1;
+        }
         push_bna(c, A, ap);
-        e.a = rows(w.gact[l - 1], fi);
+        e.a = rows(e.a_pk ? w.gpk[l - 1] : w.gact[l - 1], fi);
       }
       pend_on = false;
     }
+    if ((e.a_pk || e.b_pk) && !(l + 1 < L && g.bn[l] && B < 64) && !e.a_bn) choose_tiles(e);
     e.a_vec = (fi % 4 == 0) && al16(e.a.p0);
-    e.b = rows(gparam(c, l, 0), fi);
+    e.b = rows(e.b_pk ? w.wpk[l] : gparam(c, l, 0), fi);
     e.b_vec = (fi % 4 == 0);
     e.bias = gparam(c, l, 1);
     if (l == L - 1) {
@@ -965,6 +1006,7 @@ int build_plan(cgl_gan* c) {
   // Not at the Mix-G exchange point (the all-reduce of dA sits between the two), and a cgl_bn_bwd
   // launch where no input-gradient problem follows (and with CGL_BN_FOLD=0).
   auto gbuf = [&](int l) -> float* { return l == L - 1 ? w.dYL : w.gG[l]; };
+  bool gG_packed[CGL_MAX_LAYERS] = {};   // gG[l] has a packed copy (written by cgl_bn_bwd)
   CglBnBwdFold gfold;
   std::memset(&gfold, 0, sizeof(gfold));
   bool gfold_on = false;          // layer l's output gradient is dy in gdA[l] + partials
@@ -1016,10 +1058,29 @@ int build_plan(cgl_gan* c) {
     }
     bool fold_next = false;
     if (l >= 1) {
-      CglGemmDesc n = make_gemm(1, B, fi, fo);
+      // dA = dZ W_l: NN on the row-major W, or NT on its packed transpose P(W_l^T) (round prologue)
+      // with dZ packed too when cgl_bn_bwd wrote it
+      const bool pk = pack_enabled() && !gfold_on && c->pack.nj < CGL_PACK_MAXJ;
+      CglGemmDesc n = make_gemm(pk ? 0 : 1, B, fi, fo);
       n.a = rows(gA, fo);
       n.a_vec = (fo % 4 == 0);
       n.b = rows(gparam(c, l, 0), fi);
+      if (pk) {
+        CglOpPackJob& J = c->pack.j[c->pack.nj++];
+        J.src = gparam(c, l, 0);
+        J.dst = w.wtpk[l];
+        J.R = fi;
+        J.K = fo;
+        J.ld = fi;
+        J.trans = 1;
+        n.b = rows(w.wtpk[l], fo);
+        n.b_pk = 1;
+        if (l < L - 1 && gG_packed[l]) {
+          n.a = rows(w.gGpk[l], fo);
+          n.a_pk = 1;
+        }
+        choose_tiles(n);
+      }
       n.slope = sl;
       n.ldc = fi;
       if (gfold_on) {
@@ -1085,6 +1146,10 @@ int build_plan(cgl_gan* c) {
       b.g_gamma = ggrad(c, l - 1, 2);
       b.g_beta = ggrad(c, l - 1, 3);
       b.slope = sl;
+      if (pack_enabled() && l - 1 >= 1) {     // the next input-gradient GEMM reads it packed
+        b.dZ_pk = w.gGpk[l - 1];
+        gG_packed[l - 1] = true;
+      }
       push_bnb(c, *ph, b);
     }
   }
@@ -1092,6 +1157,18 @@ int build_plan(cgl_gan* c) {
   param_layout(g, &ng);
   push_adam(c, *ph, c->bufs.g_params, c->bufs.g_grads, c->bufs.g_m, c->bufs.g_v, (long)ng, &st->g_step_size,
             &st->g_bc2sqrt, 1);
+  // the packing jobs run as the round prologue's last blocks
+  {
+    int blk = 0;
+    for (int q = 0; q < c->pack.nj; ++q) {
+      CglOpPackJob& J = c->pack.j[q];
+      J.blk_begin = blk;
+      blk += (int)((cgl_pk_floats(J.R, J.K) / 4 + 255) / 256);
+    }
+    c->pack.blocks = blk;
+    for (auto& Lq : A)
+      if (Lq.kind == K_PROLOGUE) Lq.grid += blk;
+  }
   if ((int)c->gemm.size() > kMaxGemmDescs || (int)c->head.size() > kMaxHeadDescs ||
       (int)c->bnb.size() > kMaxBnDescs || (int)c->bna.size() > kMaxBnDescs)
     return CGL_E_SIZE;
@@ -1101,11 +1178,48 @@ int build_plan(cgl_gan* c) {
 // Round prologue: block 0 writes the round's scalars, the next nb_norm blocks draw z, the
 // last blocks draw the real-row indices of this round's local D steps.  Every block reads the
 // completed-round counter, which only the G-Adam tail (a later launch) advances.
+// The round prologue's last blocks pack operands into the GEMMs' fragment layout (CglOpPackJob): thread
+// t of a job writes packed float4 t, i.e. (row block, chunk, half, lane) of P(X; R, K); a transposed
+// source is read along its contiguous rows (the lanes of a block span 32 consecutive r).
+__device__ __forceinline__ void cgl_pack_job(const CglOpPackJob& J, long t) {
+  const int Kc = (J.K + 15) >> 4;
+  const long n4 = (long)((J.R + 31) >> 5) * Kc * 128;
+  if (t >= n4) return;
+  const int l = (int)(t & 63), h = (int)((t >> 6) & 1);
+  const long q = t >> 7;
+  const int c = (int)(q % Kc), rb = (int)(q / Kc);
+  const int r = rb * 32 + (l & 31), k0 = c * 16 + 8 * (l >> 5) + 4 * h;
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (r < J.R) {
+    if (J.trans) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (k0 + e < J.K) v[e] = gld(J.src + (long)(k0 + e) * J.ld + r);
+    } else if (k0 + 3 < J.K && ((J.ld | J.K) & 3) == 0) {
+      v = *(gcf4p)(J.src + (long)r * J.ld + k0);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (k0 + e < J.K) v[e] = gld(J.src + (long)r * J.ld + k0 + e);
+    }
+  }
+  *(gf4p)(J.dst + t * 4) = v;
+}
+
 __global__ __launch_bounds__(256) void cgl_round_prologue(CglBeginArgs a, float* z, long nz, unsigned long long zseed,
                                                           int nb_norm, int* idx, int epoch, int br, int n,
-                                                          unsigned long long sseed) {
+                                                          unsigned long long sseed, CglOpPack pk) {
   const int done = a.st->round;
   const int bid = blockIdx.x;
+  const int pk0 = (int)gridDim.x - pk.blocks;     // the packing blocks come last
+  if (bid >= pk0) {
+    const int b = bid - pk0;
+    int j = 0;
+    for (int q = 1; q < pk.nj; ++q)
+      if (b >= pk.j[q].blk_begin) j = q;
+    cgl_pack_job(pk.j[j], (long)(b - pk.j[j].blk_begin) * 256 + threadIdx.x);
+    return;
+  }
   if (bid == 0) {
     if (threadIdx.x == 0) cgl_begin_at(a, done + 1);
     return;
@@ -1149,7 +1263,7 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
     case K_PROLOGUE:
       hipLaunchKernelGGL(cgl_round_prologue, dim3(L.grid), dim3(256), 0, s, L.begin, L.nptr, L.nn, c->cfg.seed,
                          L.nb_norm, c->ws.idx, c->cfg.epoch, c->cfg.batch_real, c->cfg.sample_n,
-                         c->cfg.seed ^ 0x5bd1e995ULL);
+                         c->cfg.seed ^ 0x5bd1e995ULL, c->pack);
       break;
     default:
       return CGL_E_STATE;

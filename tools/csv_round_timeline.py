@@ -7,7 +7,7 @@ import sys
 path = sys.argv[1]
 marker = sys.argv[2] if len(sys.argv) > 2 else "cgl_normal"
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(marker)]
+idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
 a, b = idx[-3], idx[-2]          # the last full round before the bench's per-op profiling round
 tot = collections.defaultdict(lambda: [0, 0.0])
 for r in rows[a:b]:
