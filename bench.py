@@ -10,8 +10,8 @@ Workload (BASELINE.json configs[1] at N=1, configs[2] at N>1):
     real batch (CE, Adam), the G loss through the updated D, G backward, lambda SGD and Adam G
     (capgan.py:211-262 + :316-349), captured as hipGraph(s) and replayed.
   * inputs: z drawn on device each round (Philox); the real batch gathered each round from a
-    synthetic 28x28 dataset resident in HBM (59,904 rows = 234 full batches, uniform(-1,1)) through
-    the in-graph per-epoch shuffle sampler.
+    synthetic 28x28 dataset resident in HBM (60,000 rows, uniform(-1,1)) through the in-graph
+    per-pass shuffle sampler (234 full batches, then the pass's short batch of 96 real rows).
   * N > 1: one worker per GPU (CAPGAN N workers, S=1, G replicated with a shared z stream): per
     round all_gather(G losses) -> lambda-weighting -> all_reduce(sum) of the weighted G-output
     gradient -> replicated G update, plus the E-share all_reduce(avg) of D every --E rounds (RCCL).
@@ -48,7 +48,8 @@ def args_():
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--batch", type=int, default=None, help="per-worker batch (default 256; 512 for mdgan, 64 for ring)")
-    p.add_argument("--rows", type=int, default=59904, help="synthetic dataset rows per worker")
+    p.add_argument("--rows", type=int, default=60000,
+                   help="synthetic dataset rows per worker (MNIST train size: 234 full batches + one of 96)")
     p.add_argument("--E", type=int, default=1, help="D-share all-reduce period (N > 1)")
     p.add_argument("--eager", action="store_true", help="launch without hipGraph")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -123,17 +124,31 @@ def profile_launches(step, world, reps):
     return per_kind, gemm_us, gemm_flops, gemm_n
 
 
+def _latest_profile(names):
+    for n in names:
+        path = os.path.join(ROOT, "profiles", n)
+        if os.path.exists(path):
+            return n, json.load(open(path))
+    return None, None
+
+
 def traffic_per_gemm_launch():
-    """HBM-side bytes per GEMM dispatch from the committed PMC passes of this build
-    (profiles/r02_traffic.json, made by tools/pmc_traffic.py; None when absent)."""
-    path = os.path.join(ROOT, "profiles", "r02_traffic.json")
-    if not os.path.exists(path):
-        return None
-    d = json.load(open(path))
+    """HBM-side bytes per GEMM dispatch (every cgl_gemm_f32 instantiation, dispatch-weighted) from the
+    newest committed FETCH_SIZE / WRITE_SIZE passes (tools/run_r03_traffic.sh -> tools/pmc_traffic.py).
+    A static, labelled measurement: PMC passes cannot run inside the timed bench, so roofline.traffic
+    names the profile file and the commit it was measured at (traffic_source).  None when absent."""
+    name, d = _latest_profile(["r03_traffic.json", "r02_traffic.json"])
+    if d is None:
+        return None, None
+    src = {"file": f"profiles/{name}", "commit": (d.get("_meta") or {}).get("commit"),
+           "kind": "static PMC measurement (not measured in this run)"}
+    fam = d.get("cgl_gemm_f32 (all instantiations)")
+    if fam:
+        return round(fam["bytes_per_dispatch"]), src
     for k, v in d.items():
         if "cgl_gemm_f32" in k:
-            return round(v["bytes_per_dispatch"])
-    return None
+            return round(v["bytes_per_dispatch"]), src
+    return None, None
 
 
 def mlp_traffic_algorithmic(B, gemm_n):
@@ -145,7 +160,7 @@ def mlp_traffic_algorithmic(B, gemm_n):
     nbytes = (4 * (2 * pg + 4 * pd) + 4 * (pg + pd) + 4 * B * (784 + 2 * 100) + 8 * B * 784
               + 8 * B * (2 * 1920 + 3 * 768))
     per = nbytes / max(gemm_n, 1)
-    t = traffic_per_gemm_launch()
+    t, _ = traffic_per_gemm_launch()
     return {"traffic_algorithmic": round(per), "traffic_ratio": round(t / per, 2) if t else None,
             "traffic_algorithmic_note": "SURVEY 8d compulsory bytes/round minus the Adam term, / GEMM launches"}
 
@@ -300,14 +315,15 @@ def conv_cpu_baseline(a):
 
 
 def conv_traffic():
-    """HBM-side traffic of the dominant conv op per dispatch from the rocprofv3 PMC passes
-    (profiles/r02_conv_dominant_traffic.json, FETCH_SIZE x2 + WRITE_SIZE; None when absent)."""
-    path = os.path.join(ROOT, "profiles", "r02_conv_dominant_traffic.json")
-    if not os.path.exists(path):
+    """HBM-side traffic of the dominant conv op per dispatch from the newest committed PMC passes
+    (tools/conv_traffic.py: FETCH_SIZE x2 + WRITE_SIZE; None when absent), labelled with its source."""
+    name, p = _latest_profile(["r03_conv_dominant_traffic.json", "r02_conv_dominant_traffic.json"])
+    if p is None:
         return {"traffic": None}
-    p = json.load(open(path))
     return {"traffic": round(p["bytes"]), "traffic_unit": f"bytes per {p['kernel']} dispatch of the dominant op "
-            f"{p['geom']} (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/r02_conv_dominant_traffic.json)",
+            f"{p['geom']} (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+            "traffic_source": {"file": f"profiles/{name}", "commit": p.get("commit"),
+                               "kind": "static PMC measurement (not measured in this run)"},
             "traffic_algorithmic": p["algorithmic_bytes"], "traffic_ratio": round(p["ratio"], 2)}
 
 
@@ -537,8 +553,9 @@ def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None,
         "roofline": {"bound": "mfma", "kernel": "cgl_gemm_f32 (the round's GEMM launches)",
                      "achieved": round(gemm_tf, 3), "peak": PEAK_F32_MFMA, "unit": "TFLOP/s",
                      "frac": round(gemm_tf / PEAK_F32_MFMA, 4),
-                     "traffic": traffic_per_gemm_launch() if a.model == "mlp" else None,
-                     "traffic_unit": "bytes per GEMM launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/r02_traffic.json)",
+                     "traffic": traffic_per_gemm_launch()[0] if a.model == "mlp" else None,
+                     "traffic_unit": "bytes per GEMM launch, all cgl_gemm_f32 instantiations (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                     "traffic_source": traffic_per_gemm_launch()[1] if a.model == "mlp" else None,
                      **(mlp_traffic_algorithmic(a.batch, gemm_n) if a.model == "mlp" else {}),
                      "gemm_launches_per_round": gemm_n, "gemm_flops_per_round": gemm_flops,
                      "flops_per_gemm_launch": gemm_flops / max(gemm_n, 1),

@@ -176,11 +176,26 @@ def _load():
 lib = _load()
 
 
+# CGL_SYNC_CHECK=1: synchronise the device after every C-ABI call that returns through check() and
+# name the call on a device fault (a fault otherwise surfaces at some later call, whenever the runtime
+# next polls the queue).  Diagnostics only: it serialises the host with the GPU.
+_SYNC_CHECK = os.environ.get("CGL_SYNC_CHECK", "0") == "1"
+_SYNC_N = [0]
+
+
 def check(rc, what="libcglgan_hip"):
     """Turn a non-zero C-ABI return code into RuntimeError (include/cglgan.h conventions)."""
     if rc != 0:
         kinds = {-1: "invalid argument", -2: "bad call order", -3: "buffer too small"}
         raise RuntimeError(f"{what} failed: rc={rc} ({kinds.get(rc, 'hipError')})")
+    if _SYNC_CHECK:
+        import torch
+        if not torch.cuda.is_current_stream_capturing():
+            _SYNC_N[0] += 1
+            try:
+                torch.cuda.synchronize()
+            except Exception as e:
+                raise RuntimeError(f"CGL_SYNC_CHECK: device fault in or before call #{_SYNC_N[0]} ({what})") from e
     return rc
 
 

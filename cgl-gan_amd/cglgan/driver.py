@@ -183,13 +183,11 @@ def gpu_step(cfg: DriverConfig, topo: Topology, shard: torch.Tensor, beta, g_sd,
         gm, xl = specs.mixgen_worker(topo.local, img), specs.MIXGEN_HEAD_LAYER
     if cfg.algo == "mdgan":
         loss = "bce"
-    # whole batches only: the in-graph sampler keeps every batch inside one pass over the shard
-    # (DataLoader(shuffle=True) without its short last batch); the allocate_dataset shard order is
-    # already random, so the <= batch_size - 1 rows dropped are a random subset
-    n = (shard.shape[0] // cfg.batch_size) * cfg.batch_size
-    if n == 0:
-        raise ValueError(f"worker {topo.rank}: shard of {shard.shape[0]} rows < batch_size {cfg.batch_size}")
-    real = shard[:n].to(device=device, dtype=torch.float32).contiguous()
+    # the whole shard: the in-graph sampler is DataLoader(shuffle=True) over it, each pass ending
+    # with the short batch of len(shard) mod batch_size rows (capgan.py:282, 326-331)
+    if shard.shape[0] == 0:
+        raise ValueError(f"worker {topo.rank}: empty shard")
+    real = shard.to(device=device, dtype=torch.float32).contiguous()
     step = GanStep(gm, dm, batch=cfg.batch_size, epoch=cfg.epoch, loss=loss, weighting=cfg.weighting_,
                    n_workers=topo.heads, rank=topo.local, exchange_layer=xl, lr_g=cfg.lr_g, lr_d=cfg.lr_d,
                    betas=(cfg.b1, cfg.b2), seed=cfg.seed + 7919 * topo.server, gen_z=True, real=real,

@@ -169,6 +169,8 @@ struct CglHeadDesc {
   float* dlogits;         // [M][C] (optional)
   float* dP; int lddp;    // (dlogits . W) * leaky'(P)
   float slope;
+  const int* n0_dev;      // when set: segment 0 has only *n0_dev valid rows (the rest carry no loss and
+                          // no gradient) and its mean / dlogit weight use that count (w0 = combine / n0)
   float* part;            // [nwg][2] per-workgroup loss sums per segment
   unsigned int* counter;  // last-arriver ticket (zero at rest)
   float* loss_out0;       // mean loss of segment 0 / 1 (written by the last workgroup), may be null
@@ -224,6 +226,8 @@ struct CglStepState {
   float losses[CGL_MAX_WORKERS];    // gathered G losses (N > 1)
   float alphas[CGL_MAX_WORKERS];
   long long bn_batches;             // num_batches_tracked of every G BatchNorm layer
+  int real_rows[CGL_MAX_EPOCH];     // real rows of each local D step's batch (device sampler: the
+                                    // pass's short last batch has fewer, capgan.py:326-331)
   unsigned int err;                 // sticky: an in-launch rendezvous timed out (never expected)
 };
 

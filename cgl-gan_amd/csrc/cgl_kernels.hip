@@ -35,6 +35,8 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
   __shared__ float s_part[2 * 1024];
   const int M = hd->M, F = hd->F, C = hd->C;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n0 = hd->n0_dev ? gldi(hd->n0_dev) : hd->split;
+  const float wr0 = hd->n0_dev ? hd->combine / (float)n0 : hd->w0;   // real-segment dlogit weight
   const int lane = threadIdx.x & 63;
   const int r0 = blockIdx.x * hd->rows_per_wg;
   const int r1 = min(r0 + hd->rows_per_wg, M);
@@ -72,7 +74,9 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
     z[1] = C == 2 ? cgl_wave_sum(s1) + b1 : 0.f;
     const int seg = r < hd->split ? 0 : 1;
     const int t = seg ? hd->t1 : hd->t0;
-    const float wgt = seg ? hd->w1 : hd->w0;
+    // a device-sized real segment (the sampler's short batch): rows past n0 carry nothing
+    const bool dead = seg == 0 && r >= n0;
+    const float wgt = dead ? 0.f : seg ? hd->w1 : wr0;
     float dl[2];
     float lossv;
     if (hd->loss == 0) {
@@ -95,7 +99,7 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
       dl[0] = gp * (1.f - pr) * pr;
       dl[1] = 0.f;
     }
-    lsum[seg] += lossv;
+    if (!dead) lsum[seg] += lossv;
     if (hd->dlogits && lane < C) gst(hd->dlogits + (long)r * C + lane, dl[lane]);
     if (hd->dP) {
       float* dp = hd->dP + (long)r * hd->lddp;
@@ -153,7 +157,8 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
       s0 += (double)s_part[2 * q];
       s1 += (double)s_part[2 * q + 1];
     }
-    const int n0 = min(hd->split, M), n1 = M - n0;
+    const int n0s = min(hd->split, M), n1 = M - n0s;
+    const int n0 = hd->n0_dev ? min(gldi(hd->n0_dev), n0s) : n0s;
     const float l0 = n0 > 0 ? (float)(s0 / n0) : (hd->combine_in0 ? gld(hd->combine_in0) : 0.f);
     const float l1 = n1 > 0 ? (float)(s1 / n1) : 0.f;
     if (hd->loss_out0 && n0 > 0) gst(hd->loss_out0, l0);

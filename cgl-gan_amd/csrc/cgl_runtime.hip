@@ -90,7 +90,7 @@ int validate(const cgl_gan_config* c) {
     return CGL_E_ARG;
   if (c->weighting < 0 || c->weighting > 4) return CGL_E_ARG;
   if (c->exchange_layer != -1 && (c->exchange_layer < 1 || c->exchange_layer >= g.n_layers)) return CGL_E_ARG;
-  if (c->sample_n < 0 || (c->sample_n > 0 && c->sample_n % c->batch_real != 0)) return CGL_E_ARG;
+  if (c->sample_n < 0) return CGL_E_ARG;
   if (c->gemm_dtype < CGL_DTYPE_F32 || c->gemm_dtype > CGL_DTYPE_BF16) return CGL_E_ARG;
   return CGL_OK;
 }
@@ -858,6 +858,7 @@ int build_plan(cgl_gan* c) {
     h.slope = sl;
     h.part = part == 0 ? w.hpart2 : w.hpart;
     h.counter = w.counters + (part == 0 ? 16 : ep);
+    if (cf.sample_n > 0 && part != 1) h.n0_dev = &st->real_rows[ep];   // the sampler's short batch
     h.loss_out0 = &st->d_loss_parts[ep][0];
     h.loss_out1 = &st->d_loss_parts[ep][1];
     h.combine = combine;
@@ -1228,11 +1229,21 @@ __global__ __launch_bounds__(256) void cgl_round_prologue(CglBeginArgs a, float*
     cgl_normal_at((long)(bid - 1) * 256 + threadIdx.x, z, nz, zseed, (uint32_t)(done + 1), 0);
     return;
   }
+  // DataLoader(shuffle=True) over the n resident rows (capgan.py:282, 326-331): each pass is a fresh
+  // keyed permutation cut into ceil(n / br) batches, the last one short (n mod br rows); local D step
+  // e of round `done` takes batch done * epoch + e.  Rows past a short batch index a valid dummy row
+  // (no loss, no gradient: the head's n0_dev)
   const int t = (bid - 1 - nb_norm) * 256 + threadIdx.x;
   if (t >= epoch * br) return;
-  const long pos = ((long)done * epoch) * br + t;
-  const uint32_t ep = (uint32_t)(pos / n), j = (uint32_t)(pos % n);
-  idx[t] = (int)cgl_permute(j, (uint32_t)n, (uint32_t)sseed ^ (ep * 0x85ebca6bu + 0x1234567u));
+  const int e = t / br, row = t - e * br;
+  const long nb = (n + br - 1) / br;
+  const long bpos = (long)done * epoch + e;
+  const uint32_t pass = (uint32_t)(bpos / nb);
+  const long b = bpos % nb;
+  const long j = b * br + row;
+  idx[t] = (int)cgl_permute((uint32_t)(j < n ? j : n - 1), (uint32_t)n,
+                            (uint32_t)sseed ^ (pass * 0x85ebca6bu + 0x1234567u));
+  if (row == 0) a.st->real_rows[e] = (int)(n - b * br < br ? n - b * br : br);
 }
 
 int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = true) {
@@ -1379,8 +1390,13 @@ int cgl_gan_create(const cgl_gan_config* cfg, const cgl_gan_buffers* bufs, cgl_g
     delete c;
     return e;
   }
-  // upload descriptors, zero counters / state
-  hipError_t he = hipMemcpy(c->ws.gemm, c->gemm.data(), c->gemm.size() * sizeof(CglGemmDesc), hipMemcpyHostToDevice);
+  // upload descriptors, zero counters / state.  The caller's workspace may still have work pending on
+  // a non-blocking stream (torch.zeros on a side stream: such streams do not order against the
+  // legacy null stream these synchronous copies use), and a fill that lands after the upload zeroes
+  // the descriptors: the kernels then dereference null operand pointers.  Drain the device first.
+  hipError_t he = hipDeviceSynchronize();
+  if (he == hipSuccess)
+    he = hipMemcpy(c->ws.gemm, c->gemm.data(), c->gemm.size() * sizeof(CglGemmDesc), hipMemcpyHostToDevice);
   if (he == hipSuccess && !c->head.empty())
     he = hipMemcpy(c->ws.head, c->head.data(), c->head.size() * sizeof(CglHeadDesc), hipMemcpyHostToDevice);
   if (he == hipSuccess && !c->bna.empty())
@@ -1483,6 +1499,15 @@ int cgl_gan_tensor(cgl_gan* c, int which, float** ptr, int64_t* n) {
   } else if (which == 2) {
     *ptr = c->ws.dYL;
     *n = (int64_t)B * g.dims[L];
+  } else if (which == 3) {                          // device sampler: real-row indices [epoch][Br] (int32)
+    *ptr = (float*)c->ws.idx;
+    *n = (int64_t)c->cfg.epoch * c->cfg.batch_real;
+  } else if (which == 4) {                          // device sampler: real rows per local D step (int32)
+    *ptr = (float*)&c->ws.st->real_rows[0];
+    *n = c->cfg.epoch;
+  } else if (which == 5) {                          // the uploaded GEMM descriptor table (raw words)
+    *ptr = (float*)c->ws.gemm;
+    *n = (int64_t)(c->gemm.size() * sizeof(CglGemmDesc) / 4);
   } else if (which >= 16 && which < 16 + L) {       // gdA[l]: grad w.r.t. BN+LeakyReLU output (Xg rows)
     *ptr = c->ws.gdA[which - 16];
     *n = (int64_t)B * g.dims[which - 16 + 1];
@@ -1694,6 +1719,9 @@ int cgl_linear_prepare(int op, const float* A, const float* B, const float* bias
   d.wg_begin = 0;
   set_vec(d);
   d.ksplit = 1;
+  // the descriptor buffer may have been allocated / zeroed on a non-blocking stream that the null
+  // stream's copy does not wait for: drain the device so that no pending fill overwrites it
+  HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(desc, &d, sizeof(d), hipMemcpyHostToDevice));
   launch->tm = d.TM;
   launch->grid = cgl_gemm_wgs(d);

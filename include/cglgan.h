@@ -137,6 +137,9 @@ int cgl_gan_alpha_scale(cgl_gan* ctx, void* stream);
 int cgl_gan_exchange_buffer(cgl_gan* ctx, float** ptr, int64_t* n);
 /* Device pointer of an internal tensor: 0 = G output [2B][img] (Xd rows then Xg rows),
  * 1 = own G-loss scalar, 2 = gradient at the G output [B][img] (after Tanh'),
+ * 3 / 4 = device sampler (sample_n > 0): the round's real-row indices [epoch][batch_real] / real rows
+ * of each local D step [epoch] (int32; a pass ends with a short batch of sample_n mod batch_real rows),
+ * 5 = the round's GEMM descriptor table as uploaded by cgl_gan_create (raw 32-bit words),
  * 16+l / 32+l = gradient w.r.t. layer l's activation / Linear output [B][dims[l+1]] (Xg rows),
  * 48+l / 64+l = layer l's BN+LeakyReLU output / Linear output [2B][dims[l+1]],
  * 80+l / 96+l = saved BN batch mean / invstd [2][dims[l+1]],
