@@ -10,6 +10,12 @@ MDGAN/MNIST/mdgan.py:168-170 with its own 3-tuple):
 ``save_server`` writes both from a fused step (cglgan.GanStep / ConvGanStep, whose state dicts carry
 the reference's keys) or any module; ``load_generator`` reads a .pt back with torch.load(weights_only=
 True), so reference checkpoints load into cglgan.model modules and vice versa.
+
+Resume (new; the reference cannot resume): ``save_resume`` / ``load_resume`` write and read one file
+per worker with the step's whole training state (``resume_state()``: both models, both Adams, the
+round counter that drives z, the sampler and the Dropout counters, lambda) plus caller metadata --
+tensors, ints, floats and strings only, so it loads with ``weights_only=True``.  A run resumed from
+round r continues bitwise as the uninterrupted run would (tests/test_gpu_resume.py).
 """
 from __future__ import annotations
 
@@ -45,6 +51,24 @@ def save_server(obj, directory: str, name: str, client_list, beta, lambda_list=(
     with open(cfg, "wb") as f:
         pickle.dump(tup, f)
     return pt, cfg
+
+
+def save_resume(obj, path: str, **meta):
+    """One worker's resume file: ``obj.resume_state()`` under "state" + ``meta`` (round, config ...)."""
+    d = os.path.dirname(path)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    tmp = path + ".tmp"
+    torch.save({"state": dict(obj.resume_state()), "meta": dict(meta)}, tmp)
+    os.replace(tmp, path)            # a crash mid-write never leaves a truncated resume file
+    return path
+
+
+def load_resume(obj, path: str):
+    """Restore ``obj`` from a save_resume file; returns its metadata."""
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    obj.load_resume_state(ck["state"])
+    return ck["meta"]
 
 
 def load_generator(path: str):

@@ -261,6 +261,46 @@ class ConvGanStep:
             torch.manual_seed(seed_d)
         default_init(self.D)
 
+    # ------------------------------------------------------------------ resume
+    def resume_state(self):
+        """Everything the next round reads: G / D parameters and Adam moments, BatchNorm running
+        statistics and batch counts, Adam steps, the round counter (z stream, Dropout2d counters),
+        lambda and the real-batch sampler (permutation, position, its generator) as CPU tensors."""
+        torch.cuda.current_stream().synchronize()
+        out = OrderedDict()
+        for tag, fm in (("G", self.G), ("D", self.D)):
+            for k in ("p", "m", "v"):
+                out[f"{tag}.{k}"] = getattr(fm, k).detach().cpu().clone()
+            for k, v in fm.running.items():
+                out[f"{tag}.running.{k}"] = v.detach().cpu().clone()
+            out[f"{tag}.batches"] = torch.tensor([fm.batches[k] for k in fm.batches], dtype=torch.long)
+            out[f"{tag}.step"] = torch.tensor(fm.step, dtype=torch.long)
+        out["round"] = torch.tensor(self.round, dtype=torch.long)
+        out["lam"] = torch.tensor(self.lam, dtype=torch.float64)
+        out["sampler.pos"] = torch.tensor(self._pos, dtype=torch.long)
+        out["sampler.perm"] = (self._perm.cpu().clone() if self._perm is not None else torch.zeros(0, dtype=torch.int32))
+        out["sampler.gen"] = self._gen.get_state()
+        return out
+
+    @torch.no_grad()
+    def load_resume_state(self, sd):
+        for tag, fm in (("G", self.G), ("D", self.D)):
+            for k in ("p", "m", "v"):
+                getattr(fm, k).copy_(sd[f"{tag}.{k}"])
+            for k, v in fm.running.items():
+                v.copy_(sd[f"{tag}.running.{k}"])
+            for k, b in zip(list(fm.batches), sd[f"{tag}.batches"].tolist()):
+                fm.batches[k] = int(b)
+            fm.step = int(sd[f"{tag}.step"])
+        self.round = int(sd["round"])
+        self.lam = float(sd["lam"])
+        self._pos = int(sd["sampler.pos"])
+        perm = sd["sampler.perm"]
+        self._perm = perm.to(self.device) if perm.numel() else None
+        self._gen.set_state(sd["sampler.gen"])
+        self._dstate_host = None            # rewritten from the host state by the next round
+        torch.cuda.current_stream().synchronize()
+
     # ------------------------------------------------------------------ pieces
     def _sample_real(self):
         B = self.B

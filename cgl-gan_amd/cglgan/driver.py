@@ -98,6 +98,8 @@ class DriverConfig:
     data_seed: int = 11
     log_every: int = 0
     checkpoint_dir: str = ""
+    resume_dir: str = ""             # per-worker resume files (new): written every resume_every rounds
+    resume_every: int = 0            #   and at the end; a run started with an existing file resumes
     graph: bool = True
     gemm_dtype: str = "f32"          # "f16" / "bf16": 16-bit GEMM operands (BASELINE config 5's fp16)
 
@@ -263,16 +265,22 @@ class Driver:
                                        cloud_scope=scope, segema=cfg.segema, cloud_due=due, server_rank=topo.server)
         self.lambda_list = []
         self.round = 0
+        if cfg.resume_dir and os.path.exists(self.resume_path()):
+            self.load_resume()
 
     def run(self, rounds: int = None, log=print):
         """``rounds`` communication rounds (default: num_communication), as Server.run's
         ``while t > 0`` loop (capgan.py:164-196)."""
         cfg = self.cfg
         n = cfg.num_communication if rounds is None else rounds
+        if rounds is None:
+            n = max(0, n - self.round)          # a resumed run finishes the schedule it started
         t0 = time.perf_counter()
         for _ in range(n):
             self.exchange.round(self.round, graph=cfg.graph)
             self.round += 1
+            if cfg.resume_dir and cfg.resume_every and self.round % cfg.resume_every == 0:
+                self.save_resume()
             if cfg.log_every and self.round % cfg.log_every == 0:
                 st = self.step.stats()
                 self.lambda_list.append(st.get("lambda"))
@@ -282,7 +290,31 @@ class Driver:
                                     "s": round(time.perf_counter() - t0, 3)}))
         if cfg.checkpoint_dir and self.topo.local == 0:
             self.save(cfg.checkpoint_dir)
+        if cfg.resume_dir:
+            self.save_resume()
         return self.step.stats()
+
+    # ---------------------------------------------------------------- resume (new)
+    def resume_path(self):
+        return os.path.join(self.cfg.resume_dir, f"resume-{self.cfg.algo}-rank{self.rank}.pt")
+
+    def _resume_key(self):
+        c = self.cfg
+        return json.dumps({k: getattr(c, k) for k in ("algo", "num_workers", "num_servers", "epoch", "batch_size",
+                                                      "iid", "seed", "img_size", "gemm_dtype")}, sort_keys=True)
+
+    def save_resume(self):
+        from .checkpoint import save_resume
+        return save_resume(self.step, self.resume_path(), round=self.round, rank=self.rank,
+                           config=self._resume_key(), lambda_list=[float(x) for x in self.lambda_list if x is not None])
+
+    def load_resume(self):
+        from .checkpoint import load_resume
+        meta = load_resume(self.step, self.resume_path())
+        if meta.get("config") != self._resume_key() or meta.get("rank") != self.rank:
+            raise ValueError(f"{self.resume_path()}: saved by a different configuration or rank")
+        self.round = int(meta["round"])
+        self.lambda_list = list(meta.get("lambda_list", []))
 
     def save(self, directory):
         """capgan.py:185-200: the server's generator state dict + its config pickle."""
@@ -306,6 +338,8 @@ def parse_args(argv=None):
     p.add_argument("--weighting", default="", choices=["", "capgan", "mean", "mix_single", "mix_double"])
     p.add_argument("--fedavg_compat_noop", action="store_true")
     p.add_argument("--checkpoint_dir", default="")
+    p.add_argument("--resume_dir", default="", help="per-worker resume files (written; resumed from if present)")
+    p.add_argument("--resume_every", type=int, default=0)
     p.add_argument("--eager", action="store_true", help="launch the round without hipGraph replay")
     p.add_argument("--gemm_dtype", default="f32", choices=["f32", "f16", "bf16"],
                    help="GEMM operand type (f16 / bf16: 16-bit operands, fp32 accumulation; BASELINE config 5)")

@@ -215,6 +215,32 @@ class GanStep:
     def d_state_dict(self):
         return OrderedDict((k, v.detach().clone()) for k, v in self.d_views.items())
 
+    # ------------------------------------------------------------------ resume
+    _RESUME_BUFS = ("g_params", "g_m", "g_v", "g_running", "d_params", "d_m", "d_v")
+
+    def resume_state(self):
+        """Everything the next round reads (SURVEY 5 "resume"): G / D parameters, both Adams' moments,
+        the BatchNorm running statistics and the device round state (round counter -- which also
+        drives the z stream, the sampler position and the Adam step counts --, lambda, beta),
+        as CPU tensors.  The reference only saves the generator (capgan.py:185-200)."""
+        torch.cuda.current_stream().synchronize()
+        out = OrderedDict((k, getattr(self, k).detach().cpu().clone()) for k in self._RESUME_BUFS)
+        out["device_state"] = self.internal(6).view(torch.int32).cpu().clone()
+        return out
+
+    @torch.no_grad()
+    def load_resume_state(self, sd):
+        for k in self._RESUME_BUFS:
+            dst = getattr(self, k)
+            if sd[k].shape != dst.shape:
+                raise ValueError(f"resume state {k}: shape {tuple(sd[k].shape)} != {tuple(dst.shape)}")
+            dst.copy_(sd[k])
+        st = self.internal(6).view(torch.int32)
+        if sd["device_state"].shape != st.shape:
+            raise ValueError("resume state: device round state of another build / configuration")
+        st.copy_(sd["device_state"])
+        torch.cuda.current_stream().synchronize()
+
     # ------------------------------------------------------------------ execution
     def run(self, phase=C.PHASE_ALL, graph=False):
         fn = C.lib.cgl_gan_run_graph if graph else C.lib.cgl_gan_run

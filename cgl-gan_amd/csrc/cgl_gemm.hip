@@ -293,7 +293,7 @@ struct CglPipe {
 // Dynamic LDS layout: [operand-transform tables (cgl_gemm_tab_floats)] [split-K partials]
 template <int LAYOUT, int VEC, int TM, int TN, bool SK, int DT = 0, int ABN = 0>
 __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d, int bid, float* __restrict__ s_dyn,
-                                              float* __restrict__ s_col, int* __restrict__ s_flag,
+                                              int* __restrict__ s_flag,
                                               double* __restrict__ s_bnd) {
   constexpr int S = CglPipe<TM, TN>::S;
   const int M = d->M, N = d->N, K = d->K;
@@ -809,22 +809,37 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     }
   }
 
-  // forward BatchNorm partials of the stored output: per column, per group slot {sum, M2}
-  // over the workgroup's BM rows (two-pass: tile-slot sum, then M2 about the tile-slot mean)
+  // forward BatchNorm partials of the stored output: per column, per group slot {sum, M2 about the
+  // tile-slot mean} over the workgroup's BM rows.  Each lane reduces its own rows two-pass (count, sum,
+  // M2 about its own mean), the two lane halves and then the WM waves of the column are merged by
+  // Chan's pairwise update in a fixed order: one workgroup barrier per slot, and a slot holding none
+  // of the tile's rows (a tile spans <= 2 forward calls; usually one) costs nothing.
   if (d->stat_part) {
     const int gr = d->stat_gr;
     const int trow0 = tm * BM;
     const int gfirst = trow0 / gr;
-    const int gsplit = (gfirst + 1) * gr;   // first row of slot 1 (a tile spans <= 2 groups)
-    float part[TN][2][2];
+    const int gsplit = (gfirst + 1) * gr;   // first row of slot 1
+    float* s_st = (float*)s_bnd;            // [WM WN TN 32][3] {n, sum, M2} (s_bnd is free here)
+    if (d->bnb_part) __syncthreads();
     for (int s = 0; s < 2; ++s) {
       const int ra = max(trow0, (gfirst + s) * gr), rb = min(min(trow0 + BM, M), (gfirst + s + 1) * gr);
-      const int cnt = rb - ra;
-      float tot[TN], mean[TN];
+      if (rb - ra <= 0) {                   // workgroup-uniform
+        if (owner && wm == 0 && lh == 0)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int col = n0 + 32 * j + li;
+            if (col < N) {
+              float* p = d->stat_part + ((long)(tm * 2 + s) * N + col) * 2;
+              gst(p, 0.f);
+              gst(p + 1, 0.f);
+            }
+          }
+        continue;
+      }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const bool colok = n0 + 32 * j + li < N;
-        float sum = 0.f;
+        float cn = 0.f, sum = 0.f, m2 = 0.f;
         if (owner && colok) {
 #pragma unroll
           for (int i = 0; i < TM; ++i) {
@@ -832,65 +847,64 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
-              if (row < M && (row >= gsplit) == (s == 1)) sum += v[r];
+              const bool in = row < M && (row >= gsplit) == (s == 1);
+              sum += in ? v[r] : 0.f;
+              cn += in ? 1.f : 0.f;
             }
           }
-        }
-        sum += __shfl_xor(sum, 32);
-        if (owner && lh == 0) s_col[((wm * WN + wn) * TN + j) * 32 + li] = sum;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        float t = 0.f;
-        for (int q = 0; q < WM; ++q) t += s_col[((q * WN + wn) * TN + j) * 32 + li];
-        tot[j] = t;
-        mean[j] = cnt > 0 ? t / cnt : 0.f;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const bool colok = n0 + 32 * j + li < N;
-        float q2 = 0.f;
-        if (owner && colok) {
+          const float mu = cn > 0.f ? sum / cn : 0.f;
 #pragma unroll
           for (int i = 0; i < TM; ++i) {
             const float* v = (const float*)&acc[i][j];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
-              if (row < M && (row >= gsplit) == (s == 1)) {
-                const float dd = v[r] - mean[j];
-                q2 += dd * dd;
-              }
+              const bool in = row < M && (row >= gsplit) == (s == 1);
+              const float dd = v[r] - mu;
+              m2 += in ? dd * dd : 0.f;
             }
           }
         }
-        q2 += __shfl_xor(q2, 32);
-        if (owner && lh == 0) s_col[((wm * WN + wn) * TN + j) * 32 + li] = q2;
+        {   // lane half 0 (a) with lane half 1 (b)
+          const float cb = __shfl_xor(cn, 32), sb = __shfl_xor(sum, 32), mb = __shfl_xor(m2, 32);
+          const float ca = lh ? cb : cn, sa = lh ? sb : sum, ma = lh ? mb : m2;
+          const float c2 = lh ? cn : cb, s2 = lh ? sum : sb, m22 = lh ? m2 : mb;
+          const float nt = ca + c2;
+          const float dl = (ca > 0.f && c2 > 0.f) ? s2 / c2 - sa / ca : 0.f;
+          cn = nt;
+          sum = sa + s2;
+          m2 = ma + m22 + (nt > 0.f ? dl * dl * (ca * c2 / nt) : 0.f);
+        }
+        if (owner && lh == 0) {
+          float* e = s_st + (((wm * WN + wn) * TN + j) * 32 + li) * 3;
+          e[0] = cn;
+          e[1] = sum;
+          e[2] = m2;
+        }
       }
       __syncthreads();
+      if (owner && wm == 0 && lh == 0) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        float qt = 0.f;
-        for (int q = 0; q < WM; ++q) qt += s_col[((q * WN + wn) * TN + j) * 32 + li];
-        part[j][s][0] = cnt > 0 ? tot[j] : 0.f;
-        part[j][s][1] = cnt > 0 ? qt : 0.f;
-      }
-      __syncthreads();
-    }
-    if (owner && wm == 0 && lh == 0) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = n0 + 32 * j + li;
-        if (col < N) {
-          for (int s = 0; s < 2; ++s) {
+        for (int j = 0; j < TN; ++j) {
+          const int col = n0 + 32 * j + li;
+          float cn = 0.f, sum = 0.f, m2 = 0.f;
+          for (int q = 0; q < WM; ++q) {
+            const float* e = s_st + (((q * WN + wn) * TN + j) * 32 + li) * 3;
+            const float c2 = e[0], s2 = e[1];
+            const float nt = cn + c2;
+            const float dl = (cn > 0.f && c2 > 0.f) ? s2 / c2 - sum / cn : 0.f;
+            m2 += e[2] + (nt > 0.f ? dl * dl * (cn * c2 / nt) : 0.f);
+            sum += s2;
+            cn = nt;
+          }
+          if (col < N) {
             float* p = d->stat_part + ((long)(tm * 2 + s) * N + col) * 2;
-            gst(p, part[j][s][0]);
-            gst(p + 1, part[j][s][1]);
+            gst(p, sum);
+            gst(p + 1, m2);
           }
         }
       }
+      __syncthreads();
     }
   }
 
@@ -933,9 +947,8 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 template <int TM, int TN, bool SK = false, int DT = CGL_DTYPE_F32, int ABN = 0>
 __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDesc* __restrict__ descs, int ndesc) {
   extern __shared__ float cgl_dyn_lds[];
-  __shared__ float s_col[4 * TN * 32];          // per-column reductions across waves (WM WN <= 4)
   __shared__ int s_flag[1];                     // split-K: this workgroup reduces its tile
-  __shared__ double s_bnd[4 * TN * 32 * 2];     // backward BatchNorm partials across waves
+  __shared__ double s_bnd[4 * TN * 32 * 2];     // per-column BatchNorm partials across waves (WM WN <= 4)
   const int bid = blockIdx.x;
   int di = 0;
   for (int q = 1; q < ndesc; ++q)
@@ -947,9 +960,9 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
 #define CGL_BODY(L)                                               \
   do {                                                            \
     if (vec)                                                      \
-      cgl_gemm_body<L, 1, TM, TN, SK, DT, ABN>(d, bid, cgl_dyn_lds, s_col, s_flag, s_bnd);    \
+      cgl_gemm_body<L, 1, TM, TN, SK, DT, ABN>(d, bid, cgl_dyn_lds, s_flag, s_bnd);    \
     else                                                          \
-      cgl_gemm_body<L, 0, TM, TN, SK, DT, ABN>(d, bid, cgl_dyn_lds, s_col, s_flag, s_bnd);    \
+      cgl_gemm_body<L, 0, TM, TN, SK, DT, ABN>(d, bid, cgl_dyn_lds, s_flag, s_bnd);    \
   } while (0)
   if (layout == 0)
     CGL_BODY(0);

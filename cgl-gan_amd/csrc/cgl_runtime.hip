@@ -1505,6 +1505,9 @@ int cgl_gan_tensor(cgl_gan* c, int which, float** ptr, int64_t* n) {
   } else if (which == 4) {                          // device sampler: real rows per local D step (int32)
     *ptr = (float*)&c->ws.st->real_rows[0];
     *n = c->cfg.epoch;
+  } else if (which == 6) {                          // the device round state (CglStepState, raw words)
+    *ptr = (float*)c->ws.st;
+    *n = (int64_t)(sizeof(CglStepState) / 4);
   } else if (which == 5) {                          // the uploaded GEMM descriptor table (raw words)
     *ptr = (float*)c->ws.gemm;
     *n = (int64_t)(c->gemm.size() * sizeof(CglGemmDesc) / 4);

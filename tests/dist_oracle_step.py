@@ -207,6 +207,30 @@ class OracleDriverStep:
     def exchange_buffer(self):
         return self._x
 
+    def resume_state(self):
+        """The stand-in's training state (GanStep.resume_state's role): flat G / running / D buffers,
+        both Adams, lambda and the round counter that drives its inputs."""
+        out = {"g_params": self.g_params.clone(), "g_running": self.g_running.clone(),
+               "d_params": self.d_params.clone(), "round": torch.tensor(self.round),
+               "lam": self.lsgd.lam.detach().clone()}
+        for tag, opt in (("g", self.opt_g), ("d", self.w.opt)):
+            for i, (m, v, st) in enumerate(zip(opt.m, opt.v, opt.step_t)):
+                out[f"{tag}_m{i}"], out[f"{tag}_v{i}"], out[f"{tag}_t{i}"] = m.clone(), v.clone(), st.clone()
+        return out
+
+    @torch.no_grad()
+    def load_resume_state(self, sd):
+        self.g_params.copy_(sd["g_params"])
+        self.g_running.copy_(sd["g_running"])
+        self.d_params.copy_(sd["d_params"])
+        self.round = int(sd["round"])
+        self.lsgd.lam.copy_(sd["lam"])
+        for tag, opt in (("g", self.opt_g), ("d", self.w.opt)):
+            for i in range(len(opt.m)):
+                opt.m[i].copy_(sd[f"{tag}_m{i}"])
+                opt.v[i].copy_(sd[f"{tag}_v{i}"])
+                opt.step_t[i].copy_(sd[f"{tag}_t{i}"])
+
     def stats(self):
         return {"round": self.round, "d_loss": [float(x) for x in self.d_losses], "g_loss": float(self.loss.detach()),
                 "lambda": float(self.lsgd.lam), "F": self.F}

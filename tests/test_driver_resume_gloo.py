@@ -1,0 +1,74 @@
+"""Resume (new; the reference only saves its generator, capgan.py:185-200): a CAPGAN run of
+two workers over gloo interrupted after 2 rounds and resumed from the per-worker resume files (a NEW
+Driver, as a restarted process would build it) ends bitwise where the uninterrupted 4-round run ends --
+G, G running statistics, D, and lambda -- on the CPU stand-in step (tests/dist_oracle_step.py)."""
+import os
+import tempfile
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from test_driver_gloo import _cfg, _free_port
+
+KW = dict(algo="capgan", num_workers=2, num_servers=1, share_every=1)
+
+
+def _proc(rank, world, port, outdir, mode):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from cglgan.driver import Driver
+        from dist_oracle_step import oracle_step_factory
+        if mode == "straight":
+            drv = Driver(_cfg(**KW), step_factory=oracle_step_factory, device="cpu")
+            drv.run(4, log=None)
+        else:
+            rd = os.path.join(outdir, "resume")
+            first = Driver(_cfg(resume_dir=rd, **KW), step_factory=oracle_step_factory, device="cpu")
+            assert first.round == 0
+            first.run(2, log=None)                      # writes resume-capgan-rank{r}.pt at the end
+            del first
+            drv = Driver(_cfg(resume_dir=rd, **KW), step_factory=oracle_step_factory, device="cpu")
+            assert drv.round == 2 and drv.step.round == 2
+            drv.run(2, log=None)
+        s = drv.step
+        torch.save({"g": s.g_params, "r": s.g_running, "d": s.d_params, "lam": s.lsgd.lam.detach(),
+                    "round": drv.round}, os.path.join(outdir, f"{mode}{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_capgan_resume_bitwise_world2():
+    with tempfile.TemporaryDirectory() as td:
+        for mode in ("straight", "resumed"):
+            mp.spawn(_proc, args=(2, _free_port(), td, mode), nprocs=2, join=True)
+        for r in range(2):
+            a = torch.load(os.path.join(td, f"straight{r}.pt"), weights_only=True)
+            b = torch.load(os.path.join(td, f"resumed{r}.pt"), weights_only=True)
+            assert a["round"] == b["round"] == 4
+            for k in ("g", "r", "d", "lam"):
+                assert torch.equal(a[k], b[k]), (r, k)
+        assert os.path.exists(os.path.join(td, "resume", "resume-capgan-rank1.pt"))
+
+
+def test_resume_file_roundtrip(tmp_path):
+    from cglgan.checkpoint import load_resume, save_resume
+
+    class S:
+        def __init__(self):
+            self.x = torch.arange(4.0)
+
+        def resume_state(self):
+            return {"x": self.x.clone()}
+
+        def load_resume_state(self, sd):
+            self.x.copy_(sd["x"])
+
+    a, b = S(), S()
+    b.x.zero_()
+    p = save_resume(a, str(tmp_path / "r.pt"), round=7, config="k")
+    meta = load_resume(b, p)
+    assert meta == {"round": 7, "config": "k"} and torch.equal(b.x, a.x)
