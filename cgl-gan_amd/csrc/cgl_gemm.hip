@@ -287,7 +287,11 @@ struct CglPipe {
 #ifndef CGL_GEMM_STAGES
 #define CGL_GEMM_STAGES 3
 #endif
-  static constexpr int S = CGL_GEMM_STAGES;
+#ifndef CGL_GEMM_STAGES1
+#define CGL_GEMM_STAGES1 CGL_GEMM_STAGES
+#endif
+  // 1x1-block waves (16 staging floats per chunk) can afford a deeper rotation than 2x2 ones
+  static constexpr int S = (TM * TN == 1) ? CGL_GEMM_STAGES1 : CGL_GEMM_STAGES;
 };
 
 // Dynamic LDS layout: [operand-transform tables (cgl_gemm_tab_floats)] [split-K partials]
