@@ -62,7 +62,7 @@ def args_():
                         "rounds, bs512, fp32); ring: configs[0], the CGLGAN 2-D Gaussian-mixture round (B=64); "
                         "lsgan: the model/lsgan.py conv GAN round (32x32, MSE/LSGAN loss)")
     p.add_argument("--loss", choices=["mse", "bce"], default="mse", help="conv GAN objective (--model lsgan)")
-    p.add_argument("--lowp", choices=["none", "f16", "bf16"], default="bf16",
+    p.add_argument("--lowp", choices=["none", "f16", "bf16"], default="f16",
                    help="--model mdgan: also time the same round with 16-bit GEMM operands (BASELINE configs[4]'s "
                         "fp16) and report it beside the fp32 line as 'lowp_variant' (parity unpinned)")
     a = p.parse_args()
@@ -616,13 +616,17 @@ def main_driver(a, world, rank, algo):
         if algo == "mdgan" and a.lowp != "none":
             # the same workload with 16-bit GEMM operands (fp32 accumulation, fp32 master weights /
             # BatchNorm / losses / Adam): reported BESIDE the fp32 line, never as its value
-            cfg16 = DriverConfig(**{**cfg.__dict__, "gemm_dtype": a.lowp})
+            # f16 runs with dynamic loss scaling from torch's default initial scale (GradScaler semantics)
+            scale16 = 65536.0 if a.lowp == "f16" else 0.0
+            cfg16 = DriverConfig(**{**cfg.__dict__, "gemm_dtype": a.lowp, "loss_scale": scale16})
             drv16 = Driver(cfg16)
             el16 = timed_rounds(lambda r: drv16.exchange.round(r, graph=cfg16.graph), a, world)
             st16 = drv16.step.stats()
             lowp = {"gemm_dtype": a.lowp, "value": round(world * a.batch * a.steps / el16, 1), "unit": "images/s",
                     "ms_per_step": round(el16 / a.steps * 1e3, 4),
                     "losses": {"d_loss": st16["d_loss"][0], "g_loss": st16["g_loss"]},
+                    "loss_scaling": ({"init": scale16, "scale_now": st16["loss_scale"], "skipped_steps": st16["skipped"]}
+                                     if scale16 else None),
                     "parity": "unpinned (the reference has no 16-bit path); tests/test_gpu_lowp.py checks it "
                               "against an fp64 oracle restating the operand rounding (losses <= 1e-4; tensors "
                               "<= 0.1-0.35 of their distance to the exact fp64 round)"}

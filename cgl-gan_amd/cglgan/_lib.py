@@ -56,7 +56,8 @@ class GanConfig(ctypes.Structure):
                 ("lr_g", ctypes.c_double), ("lr_d", ctypes.c_double), ("beta1", ctypes.c_double),
                 ("beta2", ctypes.c_double), ("adam_eps", ctypes.c_double), ("bn_eps", ctypes.c_double),
                 ("bn_momentum", ctypes.c_double), ("slope", ctypes.c_float), ("seed", ctypes.c_ulonglong),
-                ("gen_z", ctypes.c_int), ("sample_n", ctypes.c_int), ("gemm_dtype", ctypes.c_int)]
+                ("gen_z", ctypes.c_int), ("sample_n", ctypes.c_int), ("gemm_dtype", ctypes.c_int),
+                ("loss_scale", ctypes.c_float), ("scale_growth_interval", ctypes.c_int)]
 
 
 class GanBuffers(ctypes.Structure):
@@ -81,7 +82,8 @@ class LinearLaunch(ctypes.Structure):
 class GanStats(ctypes.Structure):
     _fields_ = [("round", ctypes.c_int), ("d_loss", ctypes.c_float * 8), ("d_real", ctypes.c_float * 8),
                 ("d_fake", ctypes.c_float * 8), ("g_loss", ctypes.c_float), ("alpha", ctypes.c_float),
-                ("F", ctypes.c_float), ("lambda_", ctypes.c_float), ("bn_batches", ctypes.c_longlong)]
+                ("F", ctypes.c_float), ("lambda_", ctypes.c_float), ("bn_batches", ctypes.c_longlong),
+                ("loss_scale", ctypes.c_float * 2), ("last_skipped", ctypes.c_int * 2), ("skipped", ctypes.c_int * 2)]
 
 
 def _load():

@@ -29,8 +29,8 @@ Algorithms (``algo``):
 Data: there is no MNIST on these hosts (and the reference downloads it at import, capgan.py:57), so
 the dataset is ``cglgan.data.synthetic_mnist`` (labelled, MNIST-shaped); the shards are the
 reference's ``allocate_dataset(iid)`` cut of it (cglgan.data, pinned against the reference), resident
-in HBM and sampled on device each round (DataLoader(shuffle=True) order, whole batches: a shard is
-truncated to a multiple of batch_size rows instead of ending each pass with a short batch).
+in HBM and sampled on device each round (DataLoader(shuffle=True) order: each pass over a shard ends
+with its short batch of len(shard) mod batch_size rows, capgan.py:282, 326-331).
 
 Usage (one process per GPU; ``torchrun`` sets RANK / WORLD_SIZE):
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 -m cglgan.driver \\
@@ -102,6 +102,7 @@ class DriverConfig:
     resume_every: int = 0            #   and at the end; a run started with an existing file resumes
     graph: bool = True
     gemm_dtype: str = "f32"          # "f16" / "bf16": 16-bit GEMM operands (BASELINE config 5's fp16)
+    loss_scale: float = 0.0          # dynamic loss scaling of the 16-bit path (initial scale; 0 = off)
 
     @classmethod
     def from_module(cls, **overrides):
@@ -193,7 +194,8 @@ def gpu_step(cfg: DriverConfig, topo: Topology, shard: torch.Tensor, beta, g_sd,
     step = GanStep(gm, dm, batch=cfg.batch_size, epoch=cfg.epoch, loss=loss, weighting=cfg.weighting_,
                    n_workers=topo.heads, rank=topo.local, exchange_layer=xl, lr_g=cfg.lr_g, lr_d=cfg.lr_d,
                    betas=(cfg.b1, cfg.b2), seed=cfg.seed + 7919 * topo.server, gen_z=True, real=real,
-                   sample_n=real.shape[0], device=device, gemm_dtype=cfg.gemm_dtype)
+                   sample_n=real.shape[0], device=device, gemm_dtype=cfg.gemm_dtype,
+                   loss_scale=cfg.loss_scale)
     step.load_state_dicts(g_sd, d_sd)
     step.reset(beta=beta)
     return step
@@ -343,6 +345,8 @@ def parse_args(argv=None):
     p.add_argument("--eager", action="store_true", help="launch the round without hipGraph replay")
     p.add_argument("--gemm_dtype", default="f32", choices=["f32", "f16", "bf16"],
                    help="GEMM operand type (f16 / bf16: 16-bit operands, fp32 accumulation; BASELINE config 5)")
+    p.add_argument("--loss_scale", type=float, default=0.0,
+                   help="16-bit path: dynamic loss scaling from this initial scale (power of two, e.g. 65536)")
     return p.parse_args(argv)
 
 

@@ -54,10 +54,16 @@ class GanStep:
                  exchange_layer: int = -1, lr_g: float = 2e-4, lr_d: float = 2e-4, betas=(0.5, 0.999),
                  adam_eps: float = 1e-8, bn_eps: float = 0.8, bn_momentum: float = 0.1, slope: float = 0.2,
                  seed: int = 20211212, gen_z: bool = False, real: torch.Tensor = None, sample_n: int = 0,
-                 real_idx: torch.Tensor = None, device="cuda", gemm_dtype: str = "f32"):
+                 real_idx: torch.Tensor = None, device="cuda", gemm_dtype: str = "f32", loss_scale: float = 0.0,
+                 scale_growth_interval: int = 2000):
         """``gemm_dtype``: "f32" (the reference arithmetic), or "f16" / "bf16": every GEMM operand
         rounded to 16 bits at the matrix core with fp32 accumulation (BASELINE config 5's fp16;
-        fp32 master weights, BatchNorm, losses and Adam; outside the fp32 parity band)."""
+        fp32 master weights, BatchNorm, losses and Adam; outside the fp32 parity band).
+        ``loss_scale`` > 0 (16-bit only, a power of two; torch's GradScaler default is 65536): dynamic
+        loss scaling with torch.cuda.amp.GradScaler semantics, one scaler per model -- the loss
+        gradient enters the backward pass multiplied by the scale, the weight gradients are unscaled
+        before Adam, a round whose gradients hold an inf / NaN skips that model's Adam step and halves
+        its scale, ``scale_growth_interval`` clean rounds double it (include/cglgan.h)."""
         self.gm, self.dm = g, d
         self.B = batch
         self.Br = batch_real or batch
@@ -77,6 +83,9 @@ class GanStep:
             raise ValueError(f"gemm_dtype must be one of {sorted(_DTYPE)}")
         cfg.gemm_dtype = _DTYPE[gemm_dtype]
         self.gemm_dtype = gemm_dtype
+        if loss_scale and gemm_dtype == "f32":
+            raise ValueError("loss_scale applies to the 16-bit GEMM paths (gemm_dtype f16 / bf16)")
+        cfg.loss_scale, cfg.scale_growth_interval = float(loss_scale), int(scale_growth_interval)
         self.cfg = cfg
         self.n_workers, self.rank = n_workers, rank
         self.exchange_layer = exchange_layer
@@ -284,7 +293,8 @@ class GanStep:
         C.check(C.lib.cgl_gan_read_stats(self._h, ctypes.byref(s), _stream()), "cgl_gan_read_stats")
         return {"round": s.round, "d_loss": list(s.d_loss)[:self.epoch], "d_real": list(s.d_real)[:self.epoch],
                 "d_fake": list(s.d_fake)[:self.epoch], "g_loss": s.g_loss, "alpha": s.alpha, "F": s.F,
-                "lambda": s.lambda_, "bn_batches": s.bn_batches}
+                "lambda": s.lambda_, "bn_batches": s.bn_batches, "loss_scale": list(s.loss_scale),
+                "last_skipped": list(s.last_skipped), "skipped": list(s.skipped)}
 
     def plan_info(self, phase=C.PHASE_ALL):
         nl, ng, fl = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()

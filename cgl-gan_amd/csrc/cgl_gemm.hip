@@ -912,6 +912,28 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     }
   }
 
+  // dynamic loss scaling (16-bit operand instantiations only): a non-finite stored weight gradient
+  // raises the model's found flag (GradScaler's found_inf), read by that model's Adam launch
+  if constexpr (DT != CGL_DTYPE_F32) {
+    if (owner && d->inf_flag) {
+      bool bad = false;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const bool colok = n0 + 32 * j + li < N;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const float* v = (const float*)&acc[i][j];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
+            bad |= colok && row < M && !isfinite(v[r]);
+          }
+        }
+      }
+      if (bad) atomicOr(d->inf_flag, 1u);
+    }
+  }
+
   if (owner) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {

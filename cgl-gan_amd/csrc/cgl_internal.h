@@ -146,6 +146,8 @@ struct CglGemmDesc {
   double* bnb_part;
   const float* bnb_y; int bnb_ld;      // the BatchNorm input at the stored positions
   const float* bnb_mean;               // its saved batch mean [N]
+  // dynamic loss scaling (16-bit instantiations only): a stored non-finite value raises *inf_flag
+  unsigned int* inf_flag;
 };
 
 // BatchNorm1d(train) + LeakyReLU over the whole [mtot][F] output of one G layer.
@@ -175,6 +177,7 @@ struct CglHeadDesc {
   unsigned int* counter;  // last-arriver ticket (zero at rest)
   float* loss_out0;       // mean loss of segment 0 / 1 (written by the last workgroup), may be null
   float* loss_out1;
+  const float* scale_dev; // dynamic loss scaling: the dlogits (and dP) carry this factor, the loss does not
   float combine;          // D_loss = (seg0 + seg1) * combine  (0.5: capgan.py:339, 1: CGLGAN/2DMG/main.py:364)
   float* combine_out;     // optional
   const float* combine_in0;  // segment-0 mean computed by another launch (when this one has no segment 0)
@@ -228,6 +231,18 @@ struct CglStepState {
   long long bn_batches;             // num_batches_tracked of every G BatchNorm layer
   int real_rows[CGL_MAX_EPOCH];     // real rows of each local D step's batch (device sampler: the
                                     // pass's short last batch has fewer, capgan.py:326-331)
+  // dynamic loss scaling (cgl_gan_config.loss_scale > 0), index 0 = D, 1 = G.  The round's GEMM
+  // epilogues raise found[m] when they store a non-finite weight gradient, the Adam launch of model m
+  // skips its step when found[m] is set; the NEXT round's prologue applies GradScaler.update (scale,
+  // growth tracker, torch's Adam step count adam_t) and clears found (scaler_pending, set by the G-Adam
+  // tail, marks that a round has ended since)
+  float scale[2];
+  unsigned int found[2];
+  int growth[2];
+  int adam_t[2];
+  int skipped[2];
+  int last_skipped[2];
+  int scaler_pending;
   unsigned int err;                 // sticky: an in-launch rendezvous timed out (never expected)
 };
 

@@ -37,6 +37,7 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int n0 = hd->n0_dev ? gldi(hd->n0_dev) : hd->split;
   const float wr0 = hd->n0_dev ? hd->combine / (float)n0 : hd->w0;   // real-segment dlogit weight
+  const float lsc = hd->scale_dev ? gld(hd->scale_dev) : 1.f;         // dynamic loss scale (power of 2)
   const int lane = threadIdx.x & 63;
   const int r0 = blockIdx.x * hd->rows_per_wg;
   const int r1 = min(r0 + hd->rows_per_wg, M);
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
     const int t = seg ? hd->t1 : hd->t0;
     // a device-sized real segment (the sampler's short batch): rows past n0 carry nothing
     const bool dead = seg == 0 && r >= n0;
-    const float wgt = dead ? 0.f : seg ? hd->w1 : wr0;
+    const float wgt = (dead ? 0.f : seg ? hd->w1 : wr0) * lsc;
     float dl[2];
     float lossv;
     if (hd->loss == 0) {
@@ -492,11 +493,16 @@ __global__ __launch_bounds__(256) void cgl_act_bwd_k(const float* dY, const floa
 
 // ------------------------------------------------------------------------------------------
 struct CglAdamArgs {
-  float* p; const float* g; float* m; float* v;
+  float* p; float* g; float* m; float* v;
   long n;
   const float* step_size;   // device scalars (CglStepState fields)
   const float* bc2sqrt;
   float b2, w1, w2, eps;   // w1 = (float)(1 - beta1), w2 = (float)(1 - beta2) computed in double
+  // dynamic loss scaling (null: off): the gradients carry *scale; they are unscaled in place (torch's
+  // GradScaler.unscale_: g * fp32(1 / scale), exact for a power of two) and the step is skipped when
+  // *found (a non-finite weight gradient of this model this round) is set
+  const float* scale;
+  const unsigned int* found;
 };
 
 
@@ -569,14 +575,31 @@ __device__ void cgl_round_tail(CglStepState* st) {
 __global__ __launch_bounds__(256) void cgl_adam(CglAdamArgs a, CglStepState* st, int tail) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const float ss = gld(a.step_size), bc = gld(a.bc2sqrt);
-  if (i < a.n) {
+  if (a.scale) {
+    const float inv = (float)(1.0 / (double)gld(a.scale));
+    const bool skip = *(const CGL_GLOBAL unsigned int*)a.found != 0u;
+    if (i < a.n) {
+      const float g = gld(a.g + i) * inv;
+      gst(a.g + i, g);
+      if (!skip) {
+        float p = gld(a.p + i), m = gld(a.m + i), v = gld(a.v + i);
+        cgl_adam_update(p, g, m, v, ss, bc, a.b2, a.w1, a.w2, a.eps);
+        gst(a.m + i, m);
+        gst(a.v + i, v);
+        gst(a.p + i, p);
+      }
+    }
+  } else if (i < a.n) {
     float p = gld(a.p + i), m = gld(a.m + i), v = gld(a.v + i);
     cgl_adam_update(p, gld(a.g + i), m, v, ss, bc, a.b2, a.w1, a.w2, a.eps);
     gst(a.m + i, m);
     gst(a.v + i, v);
     gst(a.p + i, p);
   }
-  if (tail && i == 0) cgl_round_tail(st);
+  if (tail && i == 0) {
+    cgl_round_tail(st);
+    if (a.scale) st->scaler_pending = 1;   // GradScaler.update runs in the next round's prologue
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -585,7 +608,37 @@ struct CglBeginArgs {
   int epoch;
   double lr_g, lr_d, b1, b2;
   int bn_layers;
+  int scaling;           // dynamic loss scaling on (then epoch == 1)
+  int growth_interval;
 };
+
+// GradScaler.update of the previous round (torch's _amp_update_scale: backoff 0.5 after a skipped step,
+// x2 after growth_interval clean ones) and torch's Adam step counts (a skipped step does not count).
+__device__ void cgl_scaler_update(const CglBeginArgs& a) {
+  CglStepState* st = a.st;
+  if (!st->scaler_pending) return;
+  for (int m = 0; m < 2; ++m) {
+    const bool bad = st->found[m] != 0u;
+    st->last_skipped[m] = bad ? 1 : 0;
+    if (bad) {
+      st->scale[m] *= 0.5f;
+      st->growth[m] = 0;
+      st->skipped[m] += 1;
+    } else {
+      st->adam_t[m] += 1;
+      const int g = st->growth[m] + 1;
+      if (g == a.growth_interval) {
+        const float ns = st->scale[m] * 2.f;
+        if (isfinite(ns)) st->scale[m] = ns;
+        st->growth[m] = 0;
+      } else {
+        st->growth[m] = g;
+      }
+    }
+    st->found[m] = 0u;
+  }
+  st->scaler_pending = 0;
+}
 
 // Per-round scalars of round r (1-based): Adam bias corrections of the G update and of every
 // local D step (torch's step counters: G steps once per round, D `epoch` times), alpha reset,
@@ -594,15 +647,17 @@ struct CglBeginArgs {
 // so that no kernel reads a counter another block of the same launch is writing.
 __device__ void cgl_begin_at(const CglBeginArgs& a, int r) {
   CglStepState* st = a.st;
+  if (a.scaling) cgl_scaler_update(a);
   {
-    const double t = (double)r;
+    // with loss scaling torch's step count is the number of steps taken, not the round
+    const double t = a.scaling ? (double)(st->adam_t[1] + 1) : (double)r;
     const double bc1 = 1.0 - pow(a.b1, t);
     const double bc2 = 1.0 - pow(a.b2, t);
     st->g_step_size = (float)(a.lr_g / bc1);
     st->g_bc2sqrt = (float)pow(bc2, 0.5);
   }
   for (int e = 0; e < a.epoch; ++e) {
-    const double t = (double)((r - 1) * a.epoch + e + 1);
+    const double t = a.scaling ? (double)(st->adam_t[0] + 1) : (double)((r - 1) * a.epoch + e + 1);
     const double bc1 = 1.0 - pow(a.b1, t);
     const double bc2 = 1.0 - pow(a.b2, t);
     st->d_step_size[e] = (float)(a.lr_d / bc1);

@@ -92,6 +92,14 @@ int validate(const cgl_gan_config* c) {
   if (c->exchange_layer != -1 && (c->exchange_layer < 1 || c->exchange_layer >= g.n_layers)) return CGL_E_ARG;
   if (c->sample_n < 0) return CGL_E_ARG;
   if (c->gemm_dtype < CGL_DTYPE_F32 || c->gemm_dtype > CGL_DTYPE_BF16) return CGL_E_ARG;
+  // dynamic loss scaling: 16-bit GEMM operands only, one local D step per round, S a power of two (the
+  // unscale 1 / S is then exact), a non-negative growth interval
+  if (c->loss_scale < 0.f || c->scale_growth_interval < 0) return CGL_E_ARG;
+  if (c->loss_scale > 0.f) {
+    int ex = 0;
+    if (!std::isfinite(c->loss_scale) || std::frexp(c->loss_scale, &ex) != 0.5f) return CGL_E_ARG;
+    if (c->gemm_dtype == CGL_DTYPE_F32 || c->epoch != 1) return CGL_E_ARG;
+  }
   return CGL_OK;
 }
 
@@ -625,8 +633,9 @@ void push_bnb(cgl_gan* c, std::vector<Launch>& ph, const CglBnBwdDesc& b) {
   ph.push_back(L);
 }
 
-void push_adam(cgl_gan* c, std::vector<Launch>& ph, float* p, const float* g, float* m, float* v, long n,
-               const float* ss, const float* bc, int tail) {
+void push_adam(cgl_gan* c, std::vector<Launch>& ph, float* p, float* g, float* m, float* v, long n,
+               const float* ss, const float* bc, int tail, const float* scale = nullptr,
+               const unsigned int* found = nullptr) {
   Launch L;
   L.kind = K_ADAM;
   L.adam.p = p;
@@ -640,6 +649,8 @@ void push_adam(cgl_gan* c, std::vector<Launch>& ph, float* p, const float* g, fl
   L.adam.w1 = (float)(1.0 - c->cfg.beta1);
   L.adam.w2 = (float)(1.0 - c->cfg.beta2);
   L.adam.eps = (float)c->cfg.adam_eps;
+  L.adam.scale = scale;
+  L.adam.found = found;
   L.tail = tail;
   L.grid = (int)((n + 255) / 256);
   ph.push_back(L);
@@ -654,6 +665,7 @@ int build_plan(cgl_gan* c) {
   WS& w = c->ws;
   CglStepState* st = w.st;
   const float sl = cf.slope;
+  const bool scaling = cf.loss_scale > 0.f;
 
   std::vector<Launch>& A = c->phA;
   std::vector<Launch>& Bp = c->phB;
@@ -669,6 +681,8 @@ int build_plan(cgl_gan* c) {
     Lp.begin.lr_d = cf.lr_d;
     Lp.begin.b1 = cf.beta1;
     Lp.begin.b2 = cf.beta2;
+    Lp.begin.scaling = cf.loss_scale > 0.f ? 1 : 0;
+    Lp.begin.growth_interval = cf.scale_growth_interval > 0 ? cf.scale_growth_interval : 2000;
     if (cf.gen_z) {
       Lp.nptr = c->bufs.z;
       Lp.nn = (long)2 * B * g.dims[0];
@@ -864,6 +878,7 @@ int build_plan(cgl_gan* c) {
     h.combine = combine;
     h.combine_out = part == 0 ? nullptr : &st->d_loss[ep];
     h.combine_in0 = part == 1 ? &st->d_loss_parts[ep][0] : nullptr;
+    h.scale_dev = scaling ? &st->scale[0] : nullptr;
     h.rows_per_wg = kHeadRows;
     push_head(c, A, h);
     A.back().stream = stream;
@@ -897,6 +912,7 @@ int build_plan(cgl_gan* c) {
         t.C = dgrad(c, J - 1, 0);
         t.ldc = d.dims[J - 1];
         t.bias_out = dgrad(c, J - 1, 1);
+        if (scaling) t.inf_flag = &st->found[0];
         grp.push_back(t);
         --j;  // the layer below is handled in the same launch
       }
@@ -909,6 +925,7 @@ int build_plan(cgl_gan* c) {
         t.C = dgrad(c, j, 0);
         t.ldc = d.dims[j];
         t.bias_out = dgrad(c, j, 1);
+        if (scaling) t.inf_flag = &st->found[0];
         grp.push_back(t);
       }
       if (j >= 1) {
@@ -928,7 +945,8 @@ int build_plan(cgl_gan* c) {
     int64_t nd = 0;
     param_layout(d, &nd);
     push_adam(c, A, c->bufs.d_params, c->bufs.d_grads, c->bufs.d_m, c->bufs.d_v, (long)nd,
-              &st->d_step_size[ep], &st->d_bc2sqrt[ep], 0);
+              &st->d_step_size[ep], &st->d_bc2sqrt[ep], 0, scaling ? &st->scale[0] : nullptr,
+              scaling ? &st->found[0] : nullptr);
   }
 
   // ---- G loss through the updated D (capgan.py:343-347) and its input gradient
@@ -969,6 +987,7 @@ int build_plan(cgl_gan* c) {
     h.counter = w.counters + CGL_MAX_EPOCH;
     h.loss_out0 = &st->g_loss_parts[0];
     h.combine = 1.0f;
+    h.scale_dev = scaling ? &st->scale[1] : nullptr;
     h.rows_per_wg = kHeadRows;
     push_head(c, A, h);
   }
@@ -1051,6 +1070,7 @@ int build_plan(cgl_gan* c) {
       t.C = ggrad(c, l, 0);
       t.ldc = fi;
       t.bias_out = ggrad(c, l, 1);
+      if (scaling) t.inf_flag = &st->found[1];
       if (gfold_on) {
         t.a_bn = 2;
         t.a_bnb = gfold;
@@ -1157,7 +1177,7 @@ int build_plan(cgl_gan* c) {
   int64_t ng = 0;
   param_layout(g, &ng);
   push_adam(c, *ph, c->bufs.g_params, c->bufs.g_grads, c->bufs.g_m, c->bufs.g_v, (long)ng, &st->g_step_size,
-            &st->g_bc2sqrt, 1);
+            &st->g_bc2sqrt, 1, scaling ? &st->scale[1] : nullptr, scaling ? &st->found[1] : nullptr);
   // the packing jobs run as the round prologue's last blocks
   {
     int blk = 0;
@@ -1429,6 +1449,7 @@ int cgl_gan_reset(cgl_gan* c, const float* beta_host, void* stream) {
   h.rank = c->cfg.rank;
   h.weighting = c->cfg.weighting;
   h.alpha = 1.f;
+  h.scale[0] = h.scale[1] = c->cfg.loss_scale > 0.f ? c->cfg.loss_scale : 1.f;
   for (int i = 0; i < c->cfg.n_workers; ++i) h.beta[i] = beta_host ? beta_host[i] : 1.f / c->cfg.n_workers;
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(hipMemcpyAsync(c->ws.st, &h, sizeof(h), hipMemcpyHostToDevice, s));
@@ -1562,6 +1583,13 @@ int cgl_gan_read_stats(cgl_gan* c, cgl_gan_stats* out, void* stream) {
   out->F = h.F;
   out->lambda_ = h.lambda;
   out->bn_batches = h.bn_batches;
+  for (int m = 0; m < 2; ++m) {
+    // after a round and before the next prologue the pending update is not applied yet: report the
+    // scale that round used and its own found flag
+    out->loss_scale[m] = h.scale[m];
+    out->last_skipped[m] = h.scaler_pending ? (h.found[m] != 0u) : h.last_skipped[m];
+    out->skipped[m] = h.skipped[m] + (h.scaler_pending && h.found[m] != 0u ? 1 : 0);
+  }
   return h.err ? CGL_E_STATE : CGL_OK;   // a fused-BatchNorm rendezvous timed out
 }
 
@@ -1821,8 +1849,9 @@ int cgl_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int s
   sc[1] = (float)std::pow(bc2, 0.5);
   HIPCHK(hipMemcpyAsync(ws, sc, sizeof(sc), hipMemcpyHostToDevice, s));
   CglAdamArgs a;
+  std::memset(&a, 0, sizeof(a));
   a.p = p;
-  a.g = g;
+  a.g = const_cast<float*>(g);   // read only: no loss scale on this entry point
   a.m = m;
   a.v = v;
   a.n = (long)n;

@@ -79,6 +79,15 @@ typedef struct cgl_gan_config {
                            permutation, DataLoader(shuffle=True) capgan.py:282,326-330); 0: the
                            caller provides the round's real rows / indices                      */
   int gemm_dtype;       /* CGL_DTYPE_*: GEMM operand type (0 = fp32, the reference arithmetic)   */
+  /* Dynamic loss scaling of the 16-bit GEMM path (torch.cuda.amp.GradScaler semantics, one scaler per
+   * model): each model's loss gradient is multiplied by its scale S before the backward pass, the
+   * weight gradients are checked for inf / NaN as they are stored and unscaled (x 1/S) in the Adam
+   * launch, which skips the step (parameters, moments and torch's step count unchanged) when any was
+   * non-finite; between rounds S halves after a skipped step and doubles after
+   * scale_growth_interval clean ones.  0 = off (required for fp32).  No reference counterpart (the
+   * reference is fp32 only): parity unpinned. */
+  float loss_scale;            /* initial S (torch's default init_scale: 65536), 0 = off             */
+  int scale_growth_interval;   /* clean steps before S doubles (0: torch's default 2000)             */
 } cgl_gan_config;
 
 typedef struct cgl_gan_buffers {
@@ -104,6 +113,11 @@ typedef struct cgl_gan_stats {
   float F;              /* F_max                     (capgan.py:249)                             */
   float lambda_;        /* Lambda after the round    (capgan.py:259)                             */
   long long bn_batches; /* num_batches_tracked of G's BatchNorm layers                          */
+  /* dynamic loss scaling (cgl_gan_config.loss_scale > 0), index 0 = D, 1 = G: the scale the last round
+   * used, whether that round's step was skipped (non-finite gradient), skipped steps so far */
+  float loss_scale[2];
+  int last_skipped[2];
+  int skipped[2];
 } cgl_gan_stats;
 
 /* ---------------- layout / sizing queries (host only, no device access) ---------------- */

@@ -348,6 +348,19 @@ def bce_loss(probs, target_value):
 # --------------------------------------------------------------------------
 # Rounds
 # --------------------------------------------------------------------------
+def _scaled_backward(loss, scale, params, extra=()):
+    """loss.backward(), or (S * loss).backward() with every gradient of ``params`` / ``extra`` then
+    divided by S (GradScaler.scale + unscale_; test hook, see Worker.loss_scale)."""
+    if not scale:
+        loss.backward()
+        return
+    (loss * scale).backward()
+    with torch.no_grad():
+        for p in list(params) + list(extra):
+            if p.grad is not None:
+                p.grad.div_(scale)
+
+
 class Worker:
     """Worker role: holds D, its Adam and its shard (capgan.py:265-349)."""
 
@@ -355,6 +368,11 @@ class Worker:
         self.D = dnet
         self.opt = Adam(self.D.parameters())
         self.loss = loss
+        # test hook (None = the reference arithmetic): a static loss scale S, GradScaler-style -- the
+        # backward runs on S * loss and the gradients are divided by S before the optimiser step; with
+        # ``SeqNet.lowp`` this restates the 16-bit path's dynamic loss scaling on a round without
+        # overflow (cgl_gan_config.loss_scale; no reference counterpart, parity unpinned)
+        self.loss_scale = None
 
     def d_step(self, real, X, half=True):
         """One local D step.  CE/0.5 form: capgan.py:331-341; BCE/no-0.5 form: CGLGAN/2DMG/main.py:357-366."""
@@ -363,7 +381,7 @@ class Worker:
         real_loss = lossf(self.D.forward(real), 1)
         fake_loss = lossf(self.D.forward(X), 0)
         D_loss = (real_loss + fake_loss) * 0.5 if half else (real_loss + fake_loss)
-        D_loss.backward()
+        _scaled_backward(D_loss, self.loss_scale, self.D.parameters())
         self.opt.step()
         return D_loss.detach()
 
@@ -381,6 +399,7 @@ class CapganServer:
         self.opt = Adam(self.G.parameters())
         self.L = LambdaSGD()
         self.beta = beta.clone()
+        self.loss_scale = None   # test hook: see Worker.loss_scale
 
     def round(self, workers, z1, z2, reals, weighting="capgan"):
         """One communication round: Server.train capgan.py:211-262 + every Worker.train capgan.py:316-349.
@@ -410,7 +429,7 @@ class CapganServer:
             F_max = loss.mean()
         else:
             raise ValueError(weighting)
-        F_max.backward()
+        _scaled_backward(F_max, self.loss_scale, self.G.parameters(), [self.L.lam])
         self.L.step()
         self.opt.step()
         return dict(Xd=Xd.detach(), Xg=Xg.detach(), d_losses=torch.stack(d_losses), g_losses=loss.detach(),

@@ -40,7 +40,7 @@ def rel_scalar(a, b):
     return abs(float(a) - float(b)) / max(abs(float(b)), 1e-30)
 
 
-def make_pair(kind, B, Br=None, epoch=1, seed=20211212, gen_z=False, gemm_dtype="f32"):
+def make_pair(kind, B, Br=None, epoch=1, seed=20211212, gen_z=False, gemm_dtype="f32", **step_kw):
     """(oracle server, oracle workers, HIP step) with identical initial parameters."""
     if kind == "capgan":
         G, workers = O.build_capgan(1)
@@ -65,7 +65,7 @@ def make_pair(kind, B, Br=None, epoch=1, seed=20211212, gen_z=False, gemm_dtype=
     else:
         raise ValueError(kind)
     step = GanStep(gm, dm, batch=B, batch_real=Br or B, epoch=epoch, loss=loss, weighting=weighting,
-                   exchange_layer=xl, seed=seed, gen_z=gen_z, gemm_dtype=gemm_dtype)
+                   exchange_layer=xl, seed=seed, gen_z=gen_z, gemm_dtype=gemm_dtype, **step_kw)
     step.load_state_dicts(G.state_dict(), workers[0].D.state_dict())
     step.reset()
     return srv, workers, step

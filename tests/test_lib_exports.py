@@ -122,6 +122,16 @@ def test_config_validation():
     assert C.lib.cgl_gan_workspace_bytes(ctypes.byref(bad)) == C_E_ARG
     okx = _cfg(gm, dm, xl=specs.MIXGEN_HEAD_LAYER, n_workers=4, rank=3)
     assert C.lib.cgl_gan_workspace_bytes(ctypes.byref(okx)) > 0
+    # dynamic loss scaling: 16-bit GEMM operands only, one local D step, a power-of-two scale
+    def scaled(scale, dt=C.DTYPE_F16, epoch=1, interval=0):
+        c = _cfg(gm, dm, epoch=epoch)
+        c.gemm_dtype, c.loss_scale, c.scale_growth_interval = dt, scale, interval
+        return C.lib.cgl_gan_workspace_bytes(ctypes.byref(c))
+    assert scaled(65536.0) > 0 and scaled(1.0, dt=C.DTYPE_BF16) > 0
+    assert scaled(65536.0, dt=C.DTYPE_F32) == C_E_ARG
+    assert scaled(65536.0, epoch=2) == C_E_ARG
+    assert scaled(1000.0) == C_E_ARG and scaled(-2.0) == C_E_ARG and scaled(float("inf")) == C_E_ARG
+    assert scaled(1024.0, interval=-1) == C_E_ARG
     # create() rejects null buffers without touching a device
     h = ctypes.c_void_p()
     bufs = C.GanBuffers()
