@@ -107,9 +107,13 @@ class WorkerExchange:
 
     def __init__(self, step, comm=None, share_every: int = 0, cloud=None, cloud_every: int = 0,
                  cloud_weights=None, fedavg_compat_noop: bool = False, swap_every: int = 0,
-                 cloud_scope: str = "trunk", segema: float = 0.0, cloud_due=None, server_rank: int = 0):
+                 cloud_scope: str = "trunk", segema: float = 0.0, cloud_due=None, server_rank: int = 0,
+                 force_split: bool = False):
         self.step = step
         self.comm = comm
+        # test hook: take the N > 1 path (phase A, collectives, phase B) even in a one-rank group, so a
+        # one-GPU box can run the exchange over real RCCL (two ranks cannot share a GPU under RCCL)
+        self.force_split = force_split
         self.share_every = share_every
         self.swap_every = swap_every
         # the server's own generator: Random() seeded with server_rank + 100 (MDGAN/MNIST/mdgan.py:122-123)
@@ -130,7 +134,7 @@ class WorkerExchange:
             self.cloud_average()
         share = self.comm is not None and self.share_every > 0 and (r + 1) % self.share_every == 0
         swap = self.dswap is not None and (r + 1) % self.swap_every == 0
-        if self.comm is None or self.comm.size == 1:
+        if self.comm is None or (self.comm.size == 1 and not self.force_split):
             s.run(C.PHASE_ALL, graph=graph)
         else:
             s.run(C.PHASE_A, graph=graph)

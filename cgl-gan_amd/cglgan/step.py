@@ -301,7 +301,7 @@ class GanStep:
         C.check(C.lib.cgl_gan_plan_info(self._h, phase, ctypes.byref(nl), ctypes.byref(ng), ctypes.byref(fl)))
         return {"launches": nl.value, "gemm_launches": ng.value, "gemm_flops": fl.value}
 
-    LAUNCH_KINDS = {0: "gemm", 1: "head", 2: "bn_bwd", 3: "adam", 4: "prologue", 5: "bn_apply"}
+    LAUNCH_KINDS = {0: "gemm", 1: "head", 2: "bn_bwd", 3: "adam", 4: "prologue", 5: "bn_apply", 6: "gemm_adam", 7: "gemm_prologue"}
 
     def launches(self, phase=C.PHASE_ALL):
         """[(kind, flops, grid)] of the planned launches of a phase, in stream order."""

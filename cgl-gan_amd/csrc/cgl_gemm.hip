@@ -276,6 +276,33 @@ __device__ __forceinline__ float cgl_bnb_apply(float dy, float y, float mean, fl
   return (dy - gm - (y - mean) * kk) * invstd * w;
 }
 
+// Epilogue Adam of one accumulator block's 16 gradient values (rows rb + (r & 3) + 8 (r >> 2), column col
+// of a row-major [M][ld] tensor): all parameter / moment loads issued first, then cgl_adam_update -- the
+// arithmetic of cgl_adam on the same gradient values, so the result is bitwise cgl_adam's.
+__device__ __forceinline__ void cgl_epi_adam(const CglGemmDesc* __restrict__ d, float* p_, float* m_, float* v_,
+                                             int rb, int M, int col, int ld, const float* g) {
+  const float ss = gld(d->ad_ss), bc = gld(d->ad_bc);
+  float p[16], m[16], v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const long e = (long)min(rb + (r & 3) + 8 * (r >> 2), M - 1) * ld + col;
+    p[r] = gld(p_ + e);
+    m[r] = gld(m_ + e);
+    v[r] = gld(v_ + e);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = rb + (r & 3) + 8 * (r >> 2);
+    cgl_adam_update(p[r], g[r], m[r], v[r], ss, bc, d->ad_b2, d->ad_w1, d->ad_w2, d->ad_eps);
+    if (row < M) {
+      const long e = (long)row * ld + col;
+      gst(m_ + e, m[r]);
+      gst(v_ + e, v[r]);
+      gst(p_ + e, p[r]);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Main body.  One wave owns TM x TN 32x32 accumulator blocks ((32 TM) x (32 TN) outputs); the
 // workgroup tile is (32 TM WM) x (32 TN WN), K split WK ways.  Operand fragments of S chunks
@@ -295,7 +322,7 @@ struct CglPipe {
 };
 
 // Dynamic LDS layout: [operand-transform tables (cgl_gemm_tab_floats)] [split-K partials]
-template <int LAYOUT, int VEC, int TM, int TN, bool SK, int DT = 0, int ABN = 0>
+template <int LAYOUT, int VEC, int TM, int TN, bool SK, int DT = 0, int ABN = 0, bool ADAM = false>
 __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d, int bid, float* __restrict__ s_dyn,
                                               int* __restrict__ s_flag,
                                               double* __restrict__ s_bnd) {
@@ -328,6 +355,16 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   const int n0 = (tn * WN + wn) * 32 * TN;          // first column of this wave's tile
   float* __restrict__ s_tab = s_dyn;                // operand-transform tables
   float* __restrict__ s_red = s_dyn + d->tab_floats;   // split-K partials
+
+  // ---------------- generated A rows (the fused round prologue): this tile's rows of z, drawn here
+  if (d->a_gen) {
+    const int r0 = tm * BM, r1 = min(r0 + BM, M);
+    const long q0 = ((long)r0 * K) >> 2, q1 = ((long)r1 * K + 3) >> 2;
+    const uint32_t rnd = (uint32_t)(gldi(d->gen_round) + 1);
+    for (long q = q0 + tid; q < q1; q += CGL_GEMM_THREADS)
+      cgl_normal_at(q, const_cast<float*>(d->a.p0), d->gen_n, d->gen_seed, rnd, 0);
+    __syncthreads();   // (workgroup release / acquire: the rows are read back below, by every wave)
+  }
 
   // ---------------- operand-transform prologue (before any operand load is consumed)
   // ABN: the instantiation carrying the operand transforms (0: none compiled in; 1 / 2: the mode
@@ -950,6 +987,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
               const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
               if (row < M) gst(d->bias_out + row, v[r]);
             }
+            if constexpr (ADAM) cgl_epi_adam(d, d->ad_pb, d->ad_mb, d->ad_vb, rbase + 32 * i, M, 0, 1, v);
           }
         } else {
           float* __restrict__ C = d->C;
@@ -959,6 +997,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
             const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
             if (row < M) gst(C + (long)row * ldc + col, v[r]);
           }
+          if constexpr (ADAM) cgl_epi_adam(d, d->ad_p, d->ad_m, d->ad_v, rbase + 32 * i, M, col, ldc, v);
         }
       }
     }

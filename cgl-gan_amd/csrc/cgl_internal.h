@@ -148,6 +148,20 @@ struct CglGemmDesc {
   const float* bnb_mean;               // its saved batch mean [N]
   // dynamic loss scaling (16-bit instantiations only): a stored non-finite value raises *inf_flag
   unsigned int* inf_flag;
+  // epilogue Adam (the ADAM instantiation: G's first-layer weight gradient fused with the G Adam launch):
+  // the parameter / moment tensors parallel to C (ad_p ...) and to bias_out (ad_pb ...), updated with
+  // cgl_adam_update from the stored gradient value, as cgl_adam would from memory
+  // A generated in the prologue of the launch (a_gen: the round prologue fused with G's first GEMM): the
+  // workgroup first draws the N(0,1) rows of its tile into a.p0 (cgl_normal_at, round *gen_round + 1,
+  // stream 0, gen_n floats in all) -- the z the separate prologue launch drew
+  int a_gen;
+  const int* gen_round;
+  unsigned long long gen_seed;
+  long gen_n;
+  float* ad_p; float* ad_m; float* ad_v;
+  float* ad_pb; float* ad_mb; float* ad_vb;
+  const float* ad_ss; const float* ad_bc;
+  float ad_b2, ad_w1, ad_w2, ad_eps;
 };
 
 // BatchNorm1d(train) + LeakyReLU over the whole [mtot][F] output of one G layer.

@@ -572,8 +572,7 @@ __device__ void cgl_round_tail(CglStepState* st) {
   st->round = st->round + 1;   // round complete (read by the next round's prologue)
 }
 
-__global__ __launch_bounds__(256) void cgl_adam(CglAdamArgs a, CglStepState* st, int tail) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void cgl_adam_at(const CglAdamArgs& a, CglStepState* st, int tail, long i) {
   const float ss = gld(a.step_size), bc = gld(a.bc2sqrt);
   if (a.scale) {
     const float inv = (float)(1.0 / (double)gld(a.scale));
@@ -600,6 +599,38 @@ __global__ __launch_bounds__(256) void cgl_adam(CglAdamArgs a, CglStepState* st,
     cgl_round_tail(st);
     if (a.scale) st->scaler_pending = 1;   // GradScaler.update runs in the next round's prologue
   }
+}
+
+__global__ __launch_bounds__(256) void cgl_adam(CglAdamArgs a, CglStepState* st, int tail) {
+  cgl_adam_at(a, st, tail, (long)blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// G's first-layer weight gradient fused with the G Adam launch (the round's last two launches as one):
+// workgroups [0, gemm_wgs) run the weight-gradient GEMM (ADAM instantiation: each tile applies Adam to
+// the parameters it owns from the gradient values it stores), the rest run cgl_adam over every other G
+// parameter (`comp`, which does not depend on this GEMM) and the round's scalar tail.  Same arithmetic as
+// the two launches, so bitwise the same round.
+template <int TM, int TN>
+__global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_adam(const CglGemmDesc* __restrict__ descs, int ndesc,
+                                                                 int gemm_wgs, CglAdamArgs comp, CglStepState* st,
+                                                                 int tail) {
+  extern __shared__ float cgl_dyn_lds[];
+  __shared__ int s_flag[1];
+  __shared__ double s_bnd[4 * TN * 32 * 2];
+  const int bid = blockIdx.x;
+  if (bid >= gemm_wgs) {
+    cgl_adam_at(comp, st, tail, (long)(bid - gemm_wgs) * CGL_GEMM_THREADS + threadIdx.x);
+    return;
+  }
+  int di = 0;
+  for (int q = 1; q < ndesc; ++q)
+    if (bid >= descs[q].wg_begin) di = q;
+  const CglGemmDesc* __restrict__ d = descs + di;
+  if (d->layout != 2) return;     // planner: the fused weight gradient is a TN problem
+  if (d->a_vec && d->b_vec)
+    cgl_gemm_body<2, 1, TM, TN, false, CGL_DTYPE_F32, 0, true>(d, bid, cgl_dyn_lds, s_flag, s_bnd);
+  else
+    cgl_gemm_body<2, 0, TM, TN, false, CGL_DTYPE_F32, 0, true>(d, bid, cgl_dyn_lds, s_flag, s_bnd);
 }
 
 // ------------------------------------------------------------------------------------------

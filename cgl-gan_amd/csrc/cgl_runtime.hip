@@ -219,7 +219,7 @@ WS carve_ws(const cgl_gan_config& c, void* base) {
 }
 
 // ----------------------------------------------------------------------------------------
-enum LaunchKind { K_GEMM, K_HEAD, K_BNBWD, K_ADAM, K_PROLOGUE, K_BNAPPLY };
+enum LaunchKind { K_GEMM, K_HEAD, K_BNBWD, K_ADAM, K_PROLOGUE, K_BNAPPLY, K_GEMM_ADAM, K_GEMM_PRO };
 
 struct Launch {
   LaunchKind kind;
@@ -656,6 +656,101 @@ void push_adam(cgl_gan* c, std::vector<Launch>& ph, float* p, float* g, float* m
   ph.push_back(L);
 }
 
+// A model's first-layer weight gradient and its Adam as one launch (K_GEMM_ADAM, cgl_gemm_adam): the GEMM
+// tiles apply Adam to layer 0's W / b in their epilogue, companion workgroups run Adam over every other
+// parameter of the model (which does not depend on this GEMM) and the G Adam's scalar tail.  Applied to
+// the last two launches of `ph` when they are that weight gradient and that Adam: G's (the round's last
+// two launches) and D's (each local D step's last two).  fp32, no loss scaling (the fused Adam would race
+// the GEMM tiles' found flag), layer 0 without BatchNorm.  Correct (bitwise the two launches) but measured
+// slower in the B = 256 round, so opt-in: CGL_FUSE_GADAM=1 / CGL_FUSE_DADAM=1 (profiles/r03_fuse_ab.txt:
+// the companion Adam floods HBM and the weight-gradient tiles, behind it, end the launch later than the
+// two launches did -- G 14.6 -> 15.9 us, D 15.9 -> 19.1 us).
+void fuse_wgrad_adam(cgl_gan* c, std::vector<Launch>& ph, int model) {
+  const char* var = model == CGL_MODEL_G ? "CGL_FUSE_GADAM" : "CGL_FUSE_DADAM";
+  const int env = getenv(var) ? atoi(getenv(var)) : 0;   // read per plan (tests toggle it)
+  const cgl_gan_config& cf = c->cfg;
+  const cgl_mlp_spec& sp = model == CGL_MODEL_G ? cf.g : cf.d;
+  if (!env || cf.loss_scale > 0.f || cf.gemm_dtype != CGL_DTYPE_F32 || sp.bn[0] || ph.size() < 2) return;
+  Launch& G = ph[ph.size() - 2];
+  Launch& A = ph.back();
+  if (G.kind != K_GEMM || G.count != 1 || G.sk || G.abn || A.kind != K_ADAM) return;
+  CglGemmDesc& d = c->gemm[G.first];
+  const bool gm = model == CGL_MODEL_G;
+  float* gw = gm ? ggrad(c, 0, 0) : dgrad(c, 0, 0);
+  float* gb = gm ? ggrad(c, 0, 1) : dgrad(c, 0, 1);
+  if (d.layout != 2 || d.C != gw || d.bias_out != gb || d.ksplit > 1 || d.a_bn) return;
+  float* P = gm ? c->bufs.g_params : c->bufs.d_params;
+  float* M = gm ? c->bufs.g_m : c->bufs.d_m;
+  float* V = gm ? c->bufs.g_v : c->bufs.d_v;
+  if (A.adam.p != P) return;
+  // layer 0's tensors lead the flat buffer; the companions cover [off1, n) (layers >= 1, padding incl.)
+  int64_t off1 = -1, end0 = 0;
+  for (auto& t : gm ? c->gl : c->dl) {
+    if (t.layer >= 1 && (off1 < 0 || t.off < off1)) off1 = t.off;
+    if (t.layer == 0) end0 = std::max<int64_t>(end0, t.off + (int64_t)t.rows * t.cols);
+  }
+  if (off1 < end0 || off1 <= 0 || off1 >= A.adam.n) return;
+  const int64_t w0 = (gm ? gparam(c, 0, 0) : dparam(c, 0, 0)) - P, b0 = (gm ? gparam(c, 0, 1) : dparam(c, 0, 1)) - P;
+  d.ad_p = P + w0;
+  d.ad_m = M + w0;
+  d.ad_v = V + w0;
+  d.ad_pb = P + b0;
+  d.ad_mb = M + b0;
+  d.ad_vb = V + b0;
+  d.ad_ss = A.adam.step_size;
+  d.ad_bc = A.adam.bc2sqrt;
+  d.ad_b2 = A.adam.b2;
+  d.ad_w1 = A.adam.w1;
+  d.ad_w2 = A.adam.w2;
+  d.ad_eps = A.adam.eps;
+  Launch F = G;
+  F.kind = K_GEMM_ADAM;
+  F.adam = A.adam;
+  F.adam.p += off1;
+  F.adam.g += off1;
+  F.adam.m += off1;
+  F.adam.v += off1;
+  F.adam.n = A.adam.n - off1;
+  F.tail = A.tail;
+  F.grid_y = G.grid;                                   // the GEMM's workgroups come first
+  F.grid = G.grid + (int)((F.adam.n + CGL_GEMM_THREADS - 1) / CGL_GEMM_THREADS);
+  ph.pop_back();
+  ph.back() = F;
+}
+
+// The round prologue and G's first GEMM as one launch (K_GEMM_PRO, cgl_gemm_pro): the GEMM's workgroups
+// draw their own rows of z (a_gen; every column tile of a row tile draws the same rows, identical writes),
+// the prologue's other blocks ride along.  fp32 plans on one stream; CGL_FUSE_PRO=0 keeps two launches.
+void fuse_prologue(cgl_gan* c) {
+  const int env = getenv("CGL_FUSE_PRO") ? atoi(getenv("CGL_FUSE_PRO")) : 1;
+  std::vector<Launch>& A = c->phA;
+  if (!env || c->two_streams || c->cfg.gemm_dtype != CGL_DTYPE_F32 || A.size() < 2) return;
+  const Launch& P = A[0];
+  const Launch& G = A[1];
+  if (P.kind != K_PROLOGUE || G.kind != K_GEMM || G.count != 1 || G.sk || G.abn) return;
+  CglGemmDesc& d = c->gemm[G.first];
+  if (d.layout != 0 || d.a.p0 != c->bufs.z || d.a.idx0 || d.a.split != 0x7fffffff || d.a_pk || d.ksplit > 1) return;
+  if (c->cfg.gen_z) {
+    if (d.M != 2 * c->cfg.batch || d.K != c->cfg.g.dims[0] || d.a.ld != d.K) return;   // the tiles cover every z row
+    d.a_gen = 1;
+    d.gen_round = &c->ws.st->round;
+    d.gen_seed = c->cfg.seed;
+    d.gen_n = P.nn;
+  }
+  Launch F = G;
+  F.kind = K_GEMM_PRO;
+  F.begin = P.begin;
+  F.nptr = P.nptr;
+  F.nn = P.nn;
+  F.nb_norm = 0;
+  F.nb_samp = P.nb_samp;
+  F.grid_y = G.grid;
+  F.grid = G.grid + (P.grid - P.nb_norm);      // every prologue block but the z draw
+  F.record_ev = P.record_ev;
+  A.erase(A.begin());
+  A[0] = F;
+}
+
 int build_plan(cgl_gan* c) {
   const cgl_gan_config& cf = c->cfg;
   const cgl_mlp_spec &g = cf.g, &d = cf.d;
@@ -947,6 +1042,7 @@ int build_plan(cgl_gan* c) {
     push_adam(c, A, c->bufs.d_params, c->bufs.d_grads, c->bufs.d_m, c->bufs.d_v, (long)nd,
               &st->d_step_size[ep], &st->d_bc2sqrt[ep], 0, scaling ? &st->scale[0] : nullptr,
               scaling ? &st->found[0] : nullptr);
+    fuse_wgrad_adam(c, A, CGL_MODEL_D);
   }
 
   // ---- G loss through the updated D (capgan.py:343-347) and its input gradient
@@ -1178,6 +1274,7 @@ int build_plan(cgl_gan* c) {
   param_layout(g, &ng);
   push_adam(c, *ph, c->bufs.g_params, c->bufs.g_grads, c->bufs.g_m, c->bufs.g_v, (long)ng, &st->g_step_size,
             &st->g_bc2sqrt, 1, scaling ? &st->scale[1] : nullptr, scaling ? &st->found[1] : nullptr);
+  fuse_wgrad_adam(c, *ph, CGL_MODEL_G);
   // the packing jobs run as the round prologue's last blocks
   {
     int blk = 0;
@@ -1190,6 +1287,7 @@ int build_plan(cgl_gan* c) {
     for (auto& Lq : A)
       if (Lq.kind == K_PROLOGUE) Lq.grid += blk;
   }
+  fuse_prologue(c);
   if ((int)c->gemm.size() > kMaxGemmDescs || (int)c->head.size() > kMaxHeadDescs ||
       (int)c->bnb.size() > kMaxBnDescs || (int)c->bna.size() > kMaxBnDescs)
     return CGL_E_SIZE;
@@ -1227,12 +1325,11 @@ __device__ __forceinline__ void cgl_pack_job(const CglOpPackJob& J, long t) {
   *(gf4p)(J.dst + t * 4) = v;
 }
 
-__global__ __launch_bounds__(256) void cgl_round_prologue(CglBeginArgs a, float* z, long nz, unsigned long long zseed,
-                                                          int nb_norm, int* idx, int epoch, int br, int n,
-                                                          unsigned long long sseed, CglOpPack pk) {
+__device__ __forceinline__ void cgl_round_prologue_at(int bid, int nblk, const CglBeginArgs& a, float* z, long nz,
+                                                      unsigned long long zseed, int nb_norm, int* idx, int epoch,
+                                                      int br, int n, unsigned long long sseed, const CglOpPack& pk) {
   const int done = a.st->round;
-  const int bid = blockIdx.x;
-  const int pk0 = (int)gridDim.x - pk.blocks;     // the packing blocks come last
+  const int pk0 = nblk - pk.blocks;     // the packing blocks come last
   if (bid >= pk0) {
     const int b = bid - pk0;
     int j = 0;
@@ -1266,6 +1363,36 @@ __global__ __launch_bounds__(256) void cgl_round_prologue(CglBeginArgs a, float*
   if (row == 0) a.st->real_rows[e] = (int)(n - b * br < br ? n - b * br : br);
 }
 
+__global__ __launch_bounds__(256) void cgl_round_prologue(CglBeginArgs a, float* z, long nz, unsigned long long zseed,
+                                                          int nb_norm, int* idx, int epoch, int br, int n,
+                                                          unsigned long long sseed, CglOpPack pk) {
+  cgl_round_prologue_at(blockIdx.x, gridDim.x, a, z, nz, zseed, nb_norm, idx, epoch, br, n, sseed, pk);
+}
+
+// The round prologue fused with G's first GEMM (K_GEMM_PRO, fuse_prologue): workgroups [0, gemm_wgs) run
+// the GEMM, each drawing its own rows of z first (a_gen); the rest run the prologue's other blocks
+// (round scalars, real-batch sampler, operand packing), which nothing in this launch reads.
+template <int TM, int TN>
+__global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_pro(const CglGemmDesc* __restrict__ descs, int gemm_wgs,
+                                                                CglBeginArgs a, float* z, long nz,
+                                                                unsigned long long zseed, int* idx, int epoch, int br,
+                                                                int n, unsigned long long sseed, CglOpPack pk) {
+  extern __shared__ float cgl_dyn_lds[];
+  __shared__ int s_flag[1];
+  __shared__ double s_bnd[4 * TN * 32 * 2];
+  const int bid = blockIdx.x;
+  if (bid >= gemm_wgs) {
+    cgl_round_prologue_at(bid - gemm_wgs, (int)gridDim.x - gemm_wgs, a, z, nz, zseed, 0, idx, epoch, br, n, sseed, pk);
+    return;
+  }
+  const CglGemmDesc* __restrict__ d = descs;
+  if (d->layout != 0) return;     // planner: an NT problem (A = z rows)
+  if (d->a_vec && d->b_vec)
+    cgl_gemm_body<0, 1, TM, TN, false, CGL_DTYPE_F32, 0>(d, bid, cgl_dyn_lds, s_flag, s_bnd);
+  else
+    cgl_gemm_body<0, 0, TM, TN, false, CGL_DTYPE_F32, 0>(d, bid, cgl_dyn_lds, s_flag, s_bnd);
+}
+
 int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = true) {
   hipStream_t s = s_main;
   if (events && c->two_streams) {
@@ -1290,6 +1417,26 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
       break;
     case K_ADAM:
       hipLaunchKernelGGL(cgl_adam, dim3(L.grid), dim3(256), 0, s, L.adam, c->ws.st, L.tail);
+      break;
+    case K_GEMM_PRO:       // grid_y = the GEMM's workgroups (fuse_prologue)
+      if (L.blk == 2)
+        cgl_gemm_pro<2, 2><<<L.grid, CGL_GEMM_THREADS, L.shmem, s>>>(c->ws.gemm + L.first, L.grid_y, L.begin, L.nptr,
+                                                                      L.nn, c->cfg.seed, c->ws.idx, c->cfg.epoch,
+                                                                      c->cfg.batch_real, c->cfg.sample_n,
+                                                                      c->cfg.seed ^ 0x5bd1e995ULL, c->pack);
+      else
+        cgl_gemm_pro<1, 1><<<L.grid, CGL_GEMM_THREADS, L.shmem, s>>>(c->ws.gemm + L.first, L.grid_y, L.begin, L.nptr,
+                                                                      L.nn, c->cfg.seed, c->ws.idx, c->cfg.epoch,
+                                                                      c->cfg.batch_real, c->cfg.sample_n,
+                                                                      c->cfg.seed ^ 0x5bd1e995ULL, c->pack);
+      break;
+    case K_GEMM_ADAM:      // grid_y = the GEMM's workgroups (fuse_wgrad_adam)
+      if (L.blk == 2)
+        cgl_gemm_adam<2, 2><<<L.grid, CGL_GEMM_THREADS, L.shmem, s>>>(c->ws.gemm + L.first, L.count, L.grid_y, L.adam,
+                                                                       c->ws.st, L.tail);
+      else
+        cgl_gemm_adam<1, 1><<<L.grid, CGL_GEMM_THREADS, L.shmem, s>>>(c->ws.gemm + L.first, L.count, L.grid_y, L.adam,
+                                                                       c->ws.st, L.tail);
       break;
     case K_PROLOGUE:
       hipLaunchKernelGGL(cgl_round_prologue, dim3(L.grid), dim3(256), 0, s, L.begin, L.nptr, L.nn, c->cfg.seed,
