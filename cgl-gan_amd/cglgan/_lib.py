@@ -34,7 +34,7 @@ EXPORTS = [
     "cgl_dense_fwd", "cgl_dense_bwd_data", "cgl_dense_bwd_weight", "cgl_gather_rows", "cgl_weights_scale",
     "cgl_conv_packed_floats", "cgl_conv_pack_multi", "cgl_conv3x3_fwd_packed", "cgl_conv3x3_bwd_data_packed",
     "cgl_dense_fwd_packed", "cgl_dense_bwd_data_packed", "cgl_conv3x3_stat_chunks", "cgl_conv3x3_fwd_packed_stats",
-    "cgl_bn2d_fwd_stats", "cgl_bn2d_stats_scratch_bytes", "cgl_linear_desc_bytes", "cgl_linear_prepare",
+    "cgl_bn2d_fwd_stats", "cgl_bn2d_fwd_stats_coef", "cgl_conv3x3_fwd_packed_bnin", "cgl_bn2d_stats_scratch_bytes", "cgl_linear_desc_bytes", "cgl_linear_prepare",
     "cgl_linear_launch", "cgl_conv3x3_bwd_stat_chunks", "cgl_conv3x3_bwd_data_packed_stats", "cgl_bn2d_bwd_stats",
     "cgl_normal_fill_dev", "cgl_dropout2d_masks_dev", "cgl_adam_multi_dev", "cgl_sample_rows_dev", "cgl_counters_add",
     # evaluation (CGLGAN/2DMG/main.py plot_2d KL score)
@@ -147,6 +147,9 @@ def _load():
         "cgl_conv3x3_stat_chunks": (i64, [ci] * 8),
         "cgl_conv3x3_fwd_packed_stats": (ci, [vp, vp, vp, vp] + [ci] * 8 + [cf, vp, ci, vp, vp, i64, vp]),
         "cgl_bn2d_fwd_stats": (ci, [vp, ci, vp, ci, ci, ci, ci, vp, vp, cd, cd, vp, vp, ci, cf, vp, vp, vp, vp, vp, i64, vp]),
+        "cgl_bn2d_fwd_stats_coef": (ci, [vp, ci, vp, ci, ci, ci, ci, vp, vp, cd, cd, vp, vp, ci, cf, vp, vp, vp, vp, vp, ci,
+                                         vp, i64, vp]),
+        "cgl_conv3x3_fwd_packed_bnin": (ci, [vp, vp, vp, vp] + [ci] * 8 + [cf, vp, ci, vp, vp, ci, ci, cf, vp, i64, vp]),
         "cgl_bn2d_stats_scratch_bytes": (i64, [ci, ci]),
         "cgl_linear_desc_bytes": (i64, []),
         "cgl_conv3x3_bwd_stat_chunks": (i64, [ci] * 8),

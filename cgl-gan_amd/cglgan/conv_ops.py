@@ -98,12 +98,25 @@ def stat_chunks(n, h, wd, cin, cout, stride=1, up=0, groups=1, bwd=False):
 
 
 def conv3x3_fwd(x, w, b, y, n, h, wd, cin, cout, stride=1, up=0, act=ACT_NONE, slope=0.2, drop=None, wp=None,
-                stats=None):
+                stats=None, bn_in=None):
     """``wp``: the weights pre-packed by a PackSet (no per-call pack launch); ``w`` is then unused.
     ``stats`` = (part, groups): also write the next BatchNorm2d's {sum, M2} partials per 32-row chunk
-    (float64 tensor of stat_chunks(...) * cout * 2) -- consumed by bn2d_fwd_stats."""
+    (float64 tensor of stat_chunks(...) * cout * 2) -- consumed by bn2d_fwd_stats.
+    ``bn_in`` = (coef, groups, act, slope): ``x`` is the PRE-BatchNorm map; the BatchNorm (+ LeakyReLU)
+    whose scale / shift bn2d_fwd_stats(coef=...) wrote is applied as the operands are loaded (needs ``wp``)."""
     _chk(x, w, b, y, drop, wp)
     ws = workspace(conv_ws_bytes(n, h, wd, cin, cout, stride, up), x.device)
+    if bn_in is not None:
+        coef, groups_in, act_in, slope_in = bn_in
+        _chk(coef)
+        part, groups = stats if stats is not None else (None, 1)
+        if wp is None:
+            raise RuntimeError("conv3x3_fwd(bn_in=...): needs packed weights")
+        C.check(C.lib.cgl_conv3x3_fwd_packed_bnin(_p(x), _p(wp), _p(b), _p(y), n, h, wd, cin, cout, stride, up, act,
+                                                  float(slope), _p(drop), int(groups), _p(part), _p(coef),
+                                                  int(groups_in), int(act_in), float(slope_in), _p(ws), ws.numel(),
+                                                  _s()), "cgl_conv3x3_fwd_packed_bnin")
+        return y
     if stats is not None:
         part, groups = stats
         if wp is None or not part.is_cuda or part.dtype != torch.float64:
@@ -281,11 +294,21 @@ def bn2d_stats_scratch(c, groups, device):
 
 
 def bn2d_fwd_stats(part, x, n, hw, c, gamma, beta, y, groups=1, eps=0.8, momentum=0.1, running_mean=None,
-                   running_var=None, act=ACT_NONE, slope=0.2, save_mean=None, save_invstd=None, R=32, scratch=None):
+                   running_var=None, act=ACT_NONE, slope=0.2, save_mean=None, save_invstd=None, R=32, scratch=None,
+                   coef=None, apply_from=0):
     """bn2d_fwd (train) from the partials a conv3x3_fwd(stats=...) wrote: finalize + apply.
-    ``scratch``: bn2d_stats_scratch(c, max groups) kept with the layer (parallel finalize)."""
-    _chk(x, gamma, beta, y, running_mean, running_var, save_mean, save_invstd)
+    ``scratch``: bn2d_stats_scratch(c, max groups) kept with the layer (parallel finalize).
+    ``coef`` ([2 * groups * c] float32): also keep the scale / shift (for a consumer's bn_in);
+    ``apply_from``: apply (write ``y``) to images [apply_from, n) only."""
+    _chk(x, gamma, beta, y, running_mean, running_var, save_mean, save_invstd, coef)
     ws = workspace(bn2d_ws_bytes(n, hw, c, groups), x.device)
+    if coef is not None or apply_from:
+        C.check(C.lib.cgl_bn2d_fwd_stats_coef(_p(part), int(R), _p(x), n, hw, c, groups, _p(gamma), _p(beta),
+                                              float(eps), float(momentum), _p(running_mean), _p(running_var), act,
+                                              float(slope), _p(y), _p(save_mean), _p(save_invstd), _p(scratch),
+                                              _p(coef), int(apply_from), _p(ws), ws.numel(), _s()),
+                "cgl_bn2d_fwd_stats_coef")
+        return y
     C.check(C.lib.cgl_bn2d_fwd_stats(_p(part), int(R), _p(x), n, hw, c, groups, _p(gamma), _p(beta), float(eps),
                                      float(momentum), _p(running_mean), _p(running_var), act, float(slope), _p(y),
                                      _p(save_mean), _p(save_invstd), _p(scratch), _p(ws), ws.numel(), _s()),

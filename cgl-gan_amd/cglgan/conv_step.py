@@ -23,6 +23,7 @@ state-dict order, exposed as views under the reference's keys (``l1.0.weight``,
 from __future__ import annotations
 
 import math
+import os
 from collections import OrderedDict
 
 import numpy as np
@@ -224,6 +225,15 @@ class ConvGanStep:
             if n > 0:
                 self.st_part[k] = torch.zeros(n * geo[3] * 2, dtype=torch.float64, device=dev)
                 self.st_scratch[k] = O.bn2d_stats_scratch(geo[3], geo[6], dev)
+        # G BatchNorm2d + LeakyReLU folded into the next conv's operand load (model/lsgan.py:15-22): the finalize
+        # keeps scale / shift per (forward call, channel) [2][2][C].  CGL_CONV_BNFOLD = bit mask (1: conv_blocks.2
+        # into the up-convolution conv_blocks.5, 2: conv_blocks.6 into conv_blocks.8), default 2: the up-convolution
+        # reads each input 16 times (4 output parities x 4 taps), so its fold re-applies the BatchNorm 16 times per
+        # element and measured slower than the separate pass (profiles/r03_conv_bnfold_ab.txt)
+        fold = int(os.environ.get("CGL_CONV_BNFOLD", "2"))
+        self.bn_fold = fold & 3 if all(k in self.st_part for k in ("conv_blocks.2", "conv_blocks.6")) else 0
+        self.coef = {k: torch.zeros(4 * c, dtype=torch.float32, device=dev)
+                     for k, c in (("conv_blocks.2", 128), ("conv_blocks.6", 64))}
         # backward statistics: the same buffers (the forward's partials are consumed by then), written
         # by the input-gradient conv that produces the BatchNorm's output gradient
         self.bst_ok = {}
@@ -317,23 +327,45 @@ class ConvGanStep:
         O.nchw_to_nhwc(self.h, self.h0, B2, 128, 64)      # out.view(B, 128, 8, 8), model/lsgan.py:25
         O.conv3x3_fwd(self.h0, P["conv_blocks.1.weight"], P["conv_blocks.1.bias"], self.y1, B2, 8, 8, 128, 128, 1, 1,
                       wp=self.pk["c1f"], stats=self._stats("conv_blocks.2", 2))
-        self._g_bn("conv_blocks.2", self.y1, self.a1, 256, 128)
-        O.conv3x3_fwd(self.a1, P["conv_blocks.5.weight"], P["conv_blocks.5.bias"], self.y2, B2, 16, 16, 128, 64, 1, 1,
-                      wp=self.pk["c5f"], stats=self._stats("conv_blocks.6", 2))
-        self._g_bn("conv_blocks.6", self.y2, self.a2, 1024, 64)
-        O.conv3x3_fwd(self.a2, P["conv_blocks.8.weight"], P["conv_blocks.8.bias"], self.x3[self.B:], B2, 32, 32, 64, 1,
-                      1, 0, act=O.ACT_TANH, wp=self.pk["c8f"])
+        # BatchNorm2d + LeakyReLU of y1 (bit 0) / y2 (bit 1) folded into the next conv's operand load (the finalize
+        # keeps the scale / shift); a folded layer's activation is written for the Xg half only (images B .. 2B),
+        # which the G backward reads
+        f1, f2 = bool(self.bn_fold & 1), bool(self.bn_fold & 2)
+        bi = lambda k: (self.coef[k], 2, O.ACT_LEAKY, SLOPE)
+        self._g_bn("conv_blocks.2", self.y1, self.a1, 256, 128, fold=f1)
+        O.conv3x3_fwd(self.y1 if f1 else self.a1, P["conv_blocks.5.weight"], P["conv_blocks.5.bias"], self.y2, B2, 16,
+                      16, 128, 64, 1, 1, wp=self.pk["c5f"], stats=self._stats("conv_blocks.6", 2),
+                      bn_in=bi("conv_blocks.2") if f1 else None)
+        self._g_bn("conv_blocks.6", self.y2, self.a2, 1024, 64, fold=f2)
+        O.conv3x3_fwd(self.y2 if f2 else self.a2, P["conv_blocks.8.weight"], P["conv_blocks.8.bias"], self.x3[self.B:],
+                      B2, 32, 32, 64, 1, 1, 0, act=O.ACT_TANH, wp=self.pk["c8f"],
+                      bn_in=bi("conv_blocks.6") if f2 else None)
+
+    def g_act_xd(self, name):
+        """The Xd half (images 0 .. B) of a1 / a2: written by the unfolded forward; with the BatchNorm fold
+        (the consumer conv applied it in its loads) recomputed here from y and the kept scale / shift, in
+        double -- for inspection (signs, values), not used by the round."""
+        y, a, key = (self.y1, self.a1, "conv_blocks.2") if name == "a1" else (self.y2, self.a2, "conv_blocks.6")
+        if not (self.bn_fold & (1 if name == "a1" else 2)):
+            return a[:self.B]
+        c = y.shape[-1]
+        sc, sh = self.coef[key][:c].double(), self.coef[key][2 * c:3 * c].double()
+        v = y[:self.B].double() * sc + sh
+        return torch.where(v > 0, v, v * SLOPE).float()
 
     def _stats(self, key, groups):
         part = self.st_part.get(key)
         return (part, groups) if part is not None else None
 
-    def _bn_fwd(self, key, fm, x, y, n, hw, c, groups, act):
-        """BatchNorm2d (train) from the partials the producing conv wrote, else with its own pass."""
+    def _bn_fwd(self, key, fm, x, y, n, hw, c, groups, act, fold=False):
+        """BatchNorm2d (train) from the partials the producing conv wrote, else with its own pass.
+        ``fold``: keep the scale / shift in self.coef[key] and apply to the last group (Xg) only."""
         P, R = fm.params, fm.running
         sm, si = (self.g_save if fm is self.G else self.d_save)[key]
         kw = dict(groups=groups, eps=BN_EPS, momentum=BN_MOM, running_mean=R[key + ".running_mean"],
                   running_var=R[key + ".running_var"], act=act, slope=SLOPE, save_mean=sm, save_invstd=si)
+        if fold:
+            kw.update(coef=self.coef[key], apply_from=n - n // groups)
         if key in self.st_part:
             O.bn2d_fwd_stats(self.st_part[key], x, n, hw, c, P[key + ".weight"], P[key + ".bias"], y,
                              scratch=self.st_scratch[key], **kw)
@@ -341,8 +373,8 @@ class ConvGanStep:
             O.bn2d_fwd(x, n, hw, c, P[key + ".weight"], P[key + ".bias"], y, train=True, **kw)
         fm.batches[key] += groups
 
-    def _g_bn(self, key, x, y, hw, c):
-        self._bn_fwd(key, self.G, x, y, 2 * self.B, hw, c, 2, O.ACT_LEAKY)
+    def _g_bn(self, key, x, y, hw, c, fold=False):
+        self._bn_fwd(key, self.G, x, y, 2 * self.B, hw, c, 2, O.ACT_LEAKY, fold=fold)
 
     def _masks(self):
         """Every Dropout2d mask of the round in one launch: the D step's (call 0, 2B images) and the

@@ -74,6 +74,13 @@ struct CglConvLaunch {
   const float* st_mean;
   int ilv;                   // forward: the np problems share X and their tile grid -- tiles interleaved
                              // problem-minor (tile t of every problem back to back on one XCD)
+  // forward with the input's BatchNorm2d folded into the operand load (the producer's bn2d finalize wrote
+  // scale / shift per (group, channel): in_coef = [2][in_groups][Cin]): x -> fmaf(x, scale, shift), then
+  // LeakyReLU when in_act -- cgl_eltwise's arithmetic, so the operand equals the applied activation
+  const float* in_coef;
+  int in_groups, in_gimg;    // BatchNorm groups (forward calls) and input images per group
+  int in_act;
+  float in_slope;
 };
 
 typedef const CGL_AS4 CglConvLaunch* CglKL;
@@ -120,9 +127,10 @@ __device__ __forceinline__ int cgl_xcd_tile(int local, int nwg) {
 // the tap table.  One wave owns TM x TN 32x32 accumulators; WM x WN waves per workgroup.
 // FAST: Cin % 16 == 0, so a 16-k chunk lies inside one tap (uniform tap, 2 x 16-byte loads per
 // lane and block).  Otherwise each k is decoded per element (tiny-K layers: Cin = 1).
-template <int TM, int TN, bool FAST>
+template <int TM, int TN, bool FAST, bool BNIN = false>
 __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, float* s_red, bool direct = false) {
   constexpr int S = 3;
+  static_assert(!BNIN || FAST, "the folded BatchNorm input needs the FAST (uniform-tap chunk) path");
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, li = lane & 31, lh = lane >> 5;
@@ -140,6 +148,14 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
 
   int ay[TM], ax[TM];
   long aoff[TM];
+  int cgo[TM];                 // BNIN: this row's BatchNorm group offset into the coefficient table
+  float* s_coef = s_red;       // BNIN: [2][in_groups][Cin] scale / shift staged in LDS ahead of s_red
+  const int coef_n = BNIN ? 2 * L->in_groups * Cin : 0;
+  if constexpr (BNIN) {
+    for (int q = tid; q < coef_n; q += 256) s_coef[q] = gld(L->in_coef + q);
+    s_red += (coef_n + 63) & ~63;
+    __syncthreads();
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     int img, oy, ox;
@@ -147,6 +163,7 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
     ay[i] = oy * P->isy;
     ax[i] = ox * P->isx;
     aoff[i] = (long)img * P->XH * XW * Cin;
+    cgo[i] = BNIN ? min(img / L->in_gimg, L->in_groups - 1) * Cin : 0;
   }
   const float* brow[TN];
 #pragma unroll
@@ -172,6 +189,7 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
       const int dyv = P->dy[ty], dxv = P->dx[tx];
       okm = (ci < Cin ? 16 : 0) | (ci + 4 < Cin ? 32 : 0);
       const int c0 = min(ci, Cin - 4), c1 = min(ci + 4, Cin - 4);
+      if (BNIN) okm |= (c0 << 8) | (c1 << 20);   // the channels of the two float4, for the folded BatchNorm
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int iy = ay[i] + dyv, ix = ax[i] + dxv;
@@ -209,6 +227,25 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
     }
   };
   auto compute = [&](float (&A)[TM][8], float (&B)[TN][8], int okm) {
+    if constexpr (BNIN) {
+      // BatchNorm2d (+ LeakyReLU) of the loaded input, from the staged scale / shift (before the mask:
+      // padded taps and out-of-range channels stay zero, as in the applied activation)
+      const int c0 = (okm >> 8) & 0xfff, c1 = (okm >> 20) & 0xfff;
+      const int shb = coef_n >> 1;
+      const float sl = L->in_slope;
+      const bool lk = L->in_act == CGL_EPI_ACT_LEAKY;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const f32x4 s0 = *(const f32x4*)(s_coef + cgo[i] + c0), s1 = *(const f32x4*)(s_coef + cgo[i] + c1);
+        const f32x4 h0 = *(const f32x4*)(s_coef + shb + cgo[i] + c0), h1 = *(const f32x4*)(s_coef + shb + cgo[i] + c1);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          float v = fmaf(A[i][q], q < 4 ? s0[q] : s1[q - 4], q < 4 ? h0[q] : h1[q - 4]);
+          if (lk) v = v > 0.f ? v : v * sl;
+          A[i][q] = v;
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       if (FAST) {
@@ -427,7 +464,7 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
   }
 }
 
-template <int TM, int TN, bool FAST>
+template <int TM, int TN, bool FAST, bool BNIN = false>
 __global__ __launch_bounds__(256) void cgl_conv_fwd(CglConvLaunch args) {
   (void)args;
   extern __shared__ float cgl_conv_lds[];
@@ -439,12 +476,12 @@ __global__ __launch_bounds__(256) void cgl_conv_fwd(CglConvLaunch args) {
     // units XCD-contiguous, so the np tiles reading one input window run back to back in one L2
     const int np = L->np;
     const int unit = cgl_xcd_tile(bid, L->p[0].tiles_m * L->p[0].tiles_n * np);
-    cgl_conv_fwd_body<TM, TN, FAST>(L, &L->p[unit % np], unit / np, cgl_conv_lds, true);
+    cgl_conv_fwd_body<TM, TN, FAST, BNIN>(L, &L->p[unit % np], unit / np, cgl_conv_lds, true);
     return;
   }
   const int pi = cgl_conv_prob(L, bid);
   CglKP P = &L->p[pi];
-  cgl_conv_fwd_body<TM, TN, FAST>(L, P, bid - P->wg_begin, cgl_conv_lds);
+  cgl_conv_fwd_body<TM, TN, FAST, BNIN>(L, P, bid - P->wg_begin, cgl_conv_lds);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -824,6 +861,23 @@ __global__ __launch_bounds__(256) void cgl_conv_n1_part(CglConvLaunch args) {
     const int r = threadIdx.x >> 1, col = (threadIdx.x & 1) ? WR - 1 : 0;
 #pragma unroll
     for (int t = 0; t < 9; ++t) part[t][r * WR + col] = 0.f;
+  }
+  if (L->in_coef) {   // the input's BatchNorm2d (+ LeakyReLU) folded into the load (one group per image)
+    const int cg = min(img / L->in_gimg, L->in_groups - 1) * C, shb = L->in_groups * C;
+    const float sl = L->in_slope;
+    const bool lk = L->in_act == CGL_EPI_ACT_LEAKY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f32x4 sc = *(gcf4p)(L->in_coef + cg + 16 * j + 4 * i), sh = *(gcf4p)(L->in_coef + shb + cg + 16 * j + 4 * i);
+#pragma unroll
+      for (int k = 0; k < NP; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = fmaf(x[k][i][e], sc[e], sh[e]);
+          if (lk) v = v > 0.f ? v : v * sl;
+          x[k][i][e] = v;
+        }
+    }
   }
   f32x4 w[9][4];
 #pragma unroll
@@ -1885,6 +1939,7 @@ __global__ __launch_bounds__(256) void cgl_dense1_fwd_nhwc_k(const float* __rest
 //   mode 3  dX = dY * (1 - Y^2)                                                  (Tanh backward)
 struct CglEltArgs {
   int mode, rows, C, gr, hw, act;
+  int row0;                  // the first row of X / out is row row0 of the whole tensor (its BatchNorm group)
   float slope;
   const float* X; const float* dY; const float* post;
   const float* coef0; const float* coef1; const float* mean; const float* invstd; const float* gamma;
@@ -1910,7 +1965,7 @@ __global__ __launch_bounds__(256) void cgl_eltwise(CglEltArgs a) {
       r = (int)(e / C);
       c = (int)(e - (long)r * C);
     }
-    const int g = r / a.gr;
+    const int g = (r + a.row0) / a.gr;
     const long gc = (long)g * C + c;
     f32x4 o;
     if (a.mode == 0) {
@@ -2535,14 +2590,24 @@ bool n1_ok(const CglConvProb* P, int np) {
 
 struct StatBwd { const float* x = nullptr; const float* post = nullptr; const float* mean = nullptr; float slope = 0.f; };
 
+struct BnIn { const float* coef = nullptr; int groups = 1, gimg = 1, act = 0; float slope = 0.f; };
+
 int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float slope, const float* drop,
-                    hipStream_t s, double* st_part = nullptr, int st_cpg = 0, const StatBwd* sb = nullptr) {
+                    hipStream_t s, double* st_part = nullptr, int st_cpg = 0, const StatBwd* sb = nullptr,
+                    const BnIn* bi = nullptr) {
   const int N = P[0].N;
   CglConvLaunch L;
   std::memset(&L, 0, sizeof(L));
   L.np = np;
   L.bias = bias;
   L.act = act;
+  if (bi && bi->coef) {
+    L.in_coef = bi->coef;
+    L.in_groups = bi->groups;
+    L.in_gimg = bi->gimg;
+    L.in_act = bi->act;
+    L.in_slope = bi->slope;
+  }
   L.slope = slope;
   L.drop = drop;
   L.st_part = st_part;
@@ -2567,12 +2632,14 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
       hipLaunchKernelGGL(cgl_conv_n1_part, dim3(nimg * ((P[0].OH + CGL_N1P_TH - 1) / CGL_N1P_TH)), dim3(256), 0, s, L);
       return (int)hipGetLastError();
     }
+    if (L.in_coef) return CGL_E_ARG;     // the folded BatchNorm input: cgl_conv_n1_part and the MFMA kernels only
     if (P[0].Cin == 64 && P[0].OW == 32)
       hipLaunchKernelGGL((cgl_conv_n1_tile<16, 32>), dim3(nimg * tiles_y), dim3(256), lds, s, L);
     else
       hipLaunchKernelGGL((cgl_conv_n1_tile<0, 0>), dim3(nimg * tiles_y), dim3(256), lds, s, L);
     return (int)hipGetLastError();
   }
+  if (L.in_coef && N == 1) return CGL_E_ARG;
   if (N == 1 && n1_ok(P, np)) {
     int wg = 0;
     for (int i = 0; i < np; ++i) {
@@ -2589,7 +2656,8 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
   L.WM = t.WM;
   L.WN = t.WN;
   L.WK = t.WK;
-  const int lds = t.WK > 1 ? (t.WK - 1) * t.WM * t.WN * t.TM * t.TN * 16 * 64 * 4 : 0;
+  int lds = t.WK > 1 ? (t.WK - 1) * t.WM * t.WN * t.TM * t.TN * 16 * 64 * 4 : 0;
+  if (L.in_coef) lds += ((2 * L.in_groups * P[0].Cin + 63) & ~63) * 4;   // the staged scale / shift
   bool fast = true;
   int wg = 0;
   for (int i = 0; i < np; ++i) {
@@ -2606,6 +2674,15 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
   L.ilv = ilv_env != 0 && np > 1;
   for (int i = 1; i < np; ++i)
     L.ilv = L.ilv && P[i].X == P[0].X && P[i].tiles_m == P[0].tiles_m && P[i].tiles_n == P[0].tiles_n;
+  if (L.in_coef) {
+    for (int i = 0; i < np; ++i)
+      if (P[i].Cin != P[0].Cin || P[i].Cin > 512) return CGL_E_ARG;
+    if (!fast) return CGL_E_ARG;
+    if (t.TM == 2 && t.TN == 2) hipLaunchKernelGGL((cgl_conv_fwd<2, 2, true, true>), dim3(wg), dim3(256), lds, s, L);
+    else if (t.TM == 2) hipLaunchKernelGGL((cgl_conv_fwd<2, 1, true, true>), dim3(wg), dim3(256), lds, s, L);
+    else hipLaunchKernelGGL((cgl_conv_fwd<1, 1, true, true>), dim3(wg), dim3(256), lds, s, L);
+    return (int)hipGetLastError();
+  }
   if (t.TM == 2 && t.TN == 2) {
     if (fast) hipLaunchKernelGGL((cgl_conv_fwd<2, 2, true>), dim3(wg), dim3(256), lds, s, L);
     else hipLaunchKernelGGL((cgl_conv_fwd<2, 2, false>), dim3(wg), dim3(256), lds, s, L);
@@ -2685,7 +2762,7 @@ bool c1_ok(const ConvGeom& g) {
 
 int conv_fwd_impl(const ConvGeom& g, const float* X, const float* W, const float* bias, float* Y, int act, float slope,
                   const float* drop, void* ws, int64_t wsb, hipStream_t s, const float* Wp = nullptr,
-                  double* st_part = nullptr, int st_groups = 1) {
+                  double* st_part = nullptr, int st_groups = 1, const BnIn* bi = nullptr) {
   if (!X || !(W || Wp) || !Y || !ws || act < 0 || act > 3 || !al16(ws) || (Wp && !al16(Wp))) return CGL_E_ARG;
   if (wsb < conv_ws_bytes(g)) return CGL_E_SIZE;
   if ((g.cin % 4 == 0) && !al16(X)) return CGL_E_ARG;
@@ -2705,7 +2782,10 @@ int conv_fwd_impl(const ConvGeom& g, const float* X, const float* W, const float
     P[i].X = X;
     P[i].Y = Y;
   }
-  if (c1_ok(g) && !st_part && act != CGL_EPI_ACT_TANH && act != CGL_EPI_ACT_SIGMOID && al16(Y) &&
+  if (bi && bi->coef && (!Wp || bi->groups < 1 || g.n % bi->groups || !al16(bi->coef) || g.cin % 4 ||
+                         (bi->act != CGL_EPI_ACT_NONE && bi->act != CGL_EPI_ACT_LEAKY)))
+    return CGL_E_ARG;
+  if (c1_ok(g) && !st_part && !(bi && bi->coef) && act != CGL_EPI_ACT_TANH && act != CGL_EPI_ACT_SIGMOID && al16(Y) &&
       (!drop || al16(drop))) {
     // the packed forward operand of a Cin = 1 conv is [cout][16] (9 taps, zero padded)
     CglC1Args a;
@@ -2720,7 +2800,7 @@ int conv_fwd_impl(const ConvGeom& g, const float* X, const float* W, const float
   int rc;
   if (Wp) pack_layout(P, np, Wp);
   else if ((rc = launch_pack(W, g, 0, P, np, (float*)ws, s))) return rc;
-  return launch_conv_mma(P, np, bias, act, slope, drop, s, st_part, cpg);
+  return launch_conv_mma(P, np, bias, act, slope, drop, s, st_part, cpg, nullptr, bi);
 }
 
 int conv_bwd_data_impl(const ConvGeom& g, const float* dY, const float* W, float* dX, void* ws, int64_t wsb,
@@ -3006,6 +3086,24 @@ int cgl_conv3x3_fwd_packed_stats(const float* X, const float* Wp, const float* b
   return conv_fwd_impl(g, X, nullptr, bias, Y, act, slope, drop, ws, wsb, (hipStream_t)stream, Wp, part, groups);
 }
 
+int cgl_conv3x3_fwd_packed_bnin(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w,
+                                int cin, int cout, int stride, int up, int act, float slope, const float* drop,
+                                int groups, double* part, const float* in_coef, int in_groups, int in_act,
+                                float in_slope, void* ws, int64_t wsb, void* stream) {
+  ConvGeom g;
+  const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
+  if (rc) return rc;
+  if (!Wp || !in_coef || in_groups < 1 || n % in_groups) return CGL_E_ARG;
+  BnIn bi;
+  bi.coef = in_coef;
+  bi.groups = in_groups;
+  bi.gimg = n / in_groups;
+  bi.act = in_act;
+  bi.slope = in_slope;
+  return conv_fwd_impl(g, X, nullptr, bias, Y, act, slope, drop, ws, wsb, (hipStream_t)stream, Wp, part,
+                       part ? groups : 1, &bi);
+}
+
 int64_t cgl_conv3x3_bwd_stat_chunks(int n, int h, int w, int cin, int cout, int stride, int up, int groups) {
   ConvGeom g;
   const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
@@ -3113,7 +3211,16 @@ int cgl_bn2d_fwd_stats(const double* part, int R, const float* X, int n, int hw,
                        const float* beta, double eps, double momentum, float* running_mean, float* running_var,
                        int act, float slope, float* Y, float* save_mean, float* save_invstd, void* scratch,
                        void* ws, int64_t wsb, void* stream) {
+  return cgl_bn2d_fwd_stats_coef(part, R, X, n, hw, C, groups, gamma, beta, eps, momentum, running_mean, running_var,
+                                 act, slope, Y, save_mean, save_invstd, scratch, nullptr, 0, ws, wsb, stream);
+}
+
+int cgl_bn2d_fwd_stats_coef(const double* part, int R, const float* X, int n, int hw, int C, int groups,
+                            const float* gamma, const float* beta, double eps, double momentum, float* running_mean,
+                            float* running_var, int act, float slope, float* Y, float* save_mean, float* save_invstd,
+                            void* scratch, float* coef, int apply_img0, void* ws, int64_t wsb, void* stream) {
   if (!part || !X || !Y || !gamma || !beta || !ws || !al16(ws) || !al16(X) || !al16(Y)) return CGL_E_ARG;
+  if ((coef && !al16(coef)) || apply_img0 < 0 || apply_img0 > n) return CGL_E_ARG;
   if (n < 1 || hw < 1 || C % 4 != 0 || !pow2_le256(C) || groups < 1 || n % groups || (act != 0 && act != 1))
     return CGL_E_ARG;
   if ((running_mean == nullptr) != (running_var == nullptr)) return CGL_E_ARG;
@@ -3124,9 +3231,9 @@ int cgl_bn2d_fwd_stats(const double* part, int R, const float* X, int n, int hw,
   hipStream_t s = (hipStream_t)stream;
   const int64_t rows = (int64_t)n * hw;
   const int R0 = chan_chunk(gr);
-  float* coef = (float*)((char*)ws + al256((rows / R0) * C * 16));
-  float* c0 = coef;
-  float* c1 = coef + al256((int64_t)groups * C * 4) / 4;
+  float* cbuf = coef ? coef : (float*)((char*)ws + al256((rows / R0) * C * 16));
+  float* c0 = cbuf;
+  float* c1 = coef ? coef + (int64_t)groups * C : cbuf + al256((int64_t)groups * C * 4) / 4;
   CglBnFinArgs f;
   std::memset(&f, 0, sizeof(f));
   f.part = part; f.C = C; f.groups = groups; f.chunks_per_group = (int)(gr / R); f.R = R; f.gr = (int)gr;
@@ -3149,11 +3256,15 @@ int cgl_bn2d_fwd_stats(const double* part, int R, const float* X, int n, int hw,
     f.nocache = fin_nocache();
   hipLaunchKernelGGL(cgl_bn_finalize, dim3(C), dim3(256), 0, s, f);
   }
+  // apply to images [apply_img0, n) only (a consumer folds the rest into its operand load from `coef`)
+  const int64_t row0 = (int64_t)apply_img0 * hw, arows = rows - row0;
+  if (arows <= 0) return (int)hipGetLastError();
   CglEltArgs e;
   std::memset(&e, 0, sizeof(e));
-  e.mode = 0; e.rows = (int)rows; e.C = C; e.gr = (int)gr; e.hw = hw; e.act = act; e.slope = slope;
-  e.X = X; e.coef0 = c0; e.coef1 = c1; e.out = Y;
-  const long n4 = rows * C / 4;
+  e.mode = 0; e.rows = (int)arows; e.C = C; e.gr = (int)gr; e.hw = hw; e.act = act; e.slope = slope;
+  e.row0 = (int)row0;
+  e.X = X + row0 * C; e.coef0 = c0; e.coef1 = c1; e.out = Y + row0 * C;
+  const long n4 = arows * C / 4;
   hipLaunchKernelGGL(cgl_eltwise, dim3((unsigned)std::min<long>((n4 + 255) / 256, 8192)), dim3(256), 0, s, e);
   return (int)hipGetLastError();
 }

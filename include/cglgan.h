@@ -285,6 +285,16 @@ int64_t cgl_conv3x3_stat_chunks(int n, int h, int w, int cin, int cout, int stri
 int cgl_conv3x3_fwd_packed_stats(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w,
                                  int cin, int cout, int stride, int up, int act, float slope, const float* drop,
                                  int groups, double* part, void* workspace, int64_t ws_bytes, void* stream);
+/* cgl_conv3x3_fwd_packed(_stats) whose input X is the PRE-BatchNorm2d map of a bn2d_fwd_stats_coef call: the
+ * BatchNorm (+ LeakyReLU when in_act = CGL_EPI_ACT_LEAKY) is applied to each operand as it is loaded, from
+ * in_coef = [2][in_groups][cin] (scale, then shift, per forward call of n / in_groups images), with
+ * cgl_eltwise's arithmetic -- the convolution of the applied activation, without that map being written
+ * (model/lsgan.py:15-17,20-22: BatchNorm2d -> LeakyReLU -> Upsample -> Conv2d).  part may be null (no
+ * statistics of the output). */
+int cgl_conv3x3_fwd_packed_bnin(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w,
+                                int cin, int cout, int stride, int up, int act, float slope, const float* drop,
+                                int groups, double* part, const float* in_coef, int in_groups, int in_act,
+                                float in_slope, void* ws, int64_t wsb, void* stream);
 /* The input gradient with the previous BatchNorm2d's backward statistics computed in its epilogue:
  * part [groups * chunks][cin][2] = {sum g, sum g (x - mean)} per 32-row chunk of dX, g = dX (*
  * leaky'(bn_post) when bn_post is given), x = bn_x (the BatchNorm input) and mean = bn_mean
@@ -321,6 +331,14 @@ int cgl_bn2d_fwd_stats(const double* part, int R, const float* X, int n, int hw,
                        const float* beta, double eps, double momentum, float* running_mean, float* running_var,
                        int act, float slope, float* Y, float* save_mean, float* save_invstd, void* scratch,
                        void* workspace, int64_t ws_bytes, void* stream);
+/* cgl_bn2d_fwd_stats, also writing the per-(group, channel) scale / shift it applies into coef
+ * ([2][groups][C]: scale, then shift; may be null) and applying them to images [apply_img0, n) only:
+ * the rest is left for a consumer that folds the BatchNorm into its operand load
+ * (cgl_conv3x3_fwd_packed_bnin). */
+int cgl_bn2d_fwd_stats_coef(const double* part, int R, const float* X, int n, int hw, int C, int groups,
+                            const float* gamma, const float* beta, double eps, double momentum, float* running_mean,
+                            float* running_var, int act, float slope, float* Y, float* save_mean, float* save_invstd,
+                            void* scratch, float* coef, int apply_img0, void* ws, int64_t wsb, void* stream);
 /* cgl_bn2d_bwd from backward partials already computed (cgl_conv3x3_bwd_data_packed_stats, R = 32). */
 int cgl_bn2d_bwd_stats(const double* part, int R, const float* dY, const float* post, const float* X, int n, int hw,
                        int C, int groups, const float* save_mean, const float* save_invstd, const float* gamma,
