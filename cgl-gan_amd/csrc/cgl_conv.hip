@@ -127,15 +127,18 @@ __device__ __forceinline__ int cgl_xcd_tile(int local, int nwg) {
 // the tap table.  One wave owns TM x TN 32x32 accumulators; WM x WN waves per workgroup.
 // FAST: Cin % 16 == 0, so a 16-k chunk lies inside one tap (uniform tap, 2 x 16-byte loads per
 // lane and block).  Otherwise each k is decoded per element (tiny-K layers: Cin = 1).
-template <int TM, int TN, bool FAST, bool BNIN = false>
+template <int TM, int TN, bool FAST, bool BNIN = false, bool HALO = false>
 __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, float* s_red, bool direct = false) {
   constexpr int S = 3;
   static_assert(!BNIN || FAST, "the folded BatchNorm input needs the FAST (uniform-tap chunk) path");
+  static_assert(!HALO || (TM == 2 && TN == 2 && FAST), "the halo path is the 2x2-block FAST path");
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, li = lane & 31, lh = lane >> 5;
   const int WN = L->WN, WM = L->WM, WK = L->WK;
-  const int wk = wave % WK, wmn = wave / WK;
+  // HALO: the workgroup's waves each own the same tile of a different problem (the caller picks P per wave)
+  const int wsel = HALO ? 0 : wave;
+  const int wk = wsel % WK, wmn = wsel / WK;
   const int wm = wmn / WN, wn = wmn - wm * WN;
   const int tiles_n = P->tiles_n;
   const int tile = direct ? local : cgl_xcd_tile(local, P->tiles_m * tiles_n);
@@ -151,7 +154,7 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
   int cgo[TM];                 // BNIN: this row's BatchNorm group offset into the coefficient table
   float* s_coef = s_red;       // BNIN: [2][in_groups][Cin] scale / shift staged in LDS ahead of s_red
   const int coef_n = BNIN ? 2 * L->in_groups * Cin : 0;
-  if constexpr (BNIN) {
+  if constexpr (BNIN && !HALO) {
     for (int q = tid; q < coef_n; q += 256) s_coef[q] = gld(L->in_coef + q);
     s_red += (coef_n + 63) & ~63;
     __syncthreads();
@@ -270,7 +273,104 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
   // This wave's k-split: chunks [cb, ce).
   const int nch = Kp >> 4;
   const int cb = (wk * nch) / WK, ce = ((wk + 1) * nch) / WK;
-  if (cb < ce) {
+  if constexpr (HALO) {
+    // LDS-staged input window (the phase-form upsampling conv: 4 output parities x 2x2 taps, all reading one
+    // low-res window).  The workgroup's tile is 64 enumerated rows = R = 64 / OW whole low-res rows of one
+    // image; its window (rows y0 - 1 .. y0 + R, columns -1 .. OW, every channel, zeros outside the image) is
+    // loaded once -- with the folded BatchNorm applied here, once per element -- and the 4 waves (one per
+    // parity) read their A fragments of every tap from it.  The chunk order and MFMA sequence are the
+    // direct path's, so the results are bitwise equal.
+    const int OWp = P->OW, hwp = P->OH * OWp;
+    const int img = m0 / hwp, y0 = (m0 - img * hwp) / OWp;
+    const int WC = OWp + 2, WR = 64 / OWp + 2, CS = Cin + 4;   // pixel stride padded (LDS banks)
+    const int c4 = Cin >> 2;
+    const float* __restrict__ Xi = X + (long)img * P->XH * XW * Cin;
+    const int g = BNIN ? min(img / L->in_gimg, L->in_groups - 1) : 0;
+    for (int e = tid; e < WR * WC * c4; e += 256) {
+      const int q = e % c4, pix = e / c4;
+      const int wr = pix / WC, wc = pix - wr * WC;
+      const int iy = y0 - 1 + wr, ix = wc - 1;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if ((unsigned)iy < (unsigned)IH && (unsigned)ix < (unsigned)IW) {
+        v = *(gcf4p)(Xi + ((long)iy * XW + ix) * Cin + 4 * q);
+        if constexpr (BNIN) {
+          const f32x4 sc = *(gcf4p)(L->in_coef + g * Cin + 4 * q);
+          const f32x4 sh = *(gcf4p)(L->in_coef + (L->in_groups + g) * Cin + 4 * q);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            float w = fmaf(v[u], sc[u], sh[u]);
+            if (L->in_act == CGL_EPI_ACT_LEAKY) w = w > 0.f ? w : w * L->in_slope;
+            v[u] = w;
+          }
+        }
+      }
+      *(f32x4*)(s_red + pix * CS + 4 * q) = v;
+    }
+    __syncthreads();
+    // this lane's window pixel (tap offset 0) per row block
+    int wpix[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rr = 32 * i + li;                   // row within the tile
+      wpix[i] = (rr / OWp + 1) * WC + (rr % OWp) + 1;
+    }
+    auto lda = [&](int c, float (&A)[TM][8]) {
+      const int k0 = c * 16, t = k0 / Cin, ci = k0 - t * Cin + 8 * lh;
+      const int ty = t / Tx, tx = t - ty * Tx;
+      const int toff = P->dy[ty] * WC + P->dx[tx];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const float* w = s_red + (wpix[i] + toff) * CS + ci;
+        const f32x4 u = *(const f32x4*)w, v = *(const f32x4*)(w + 4);
+        A[i][0] = u[0]; A[i][1] = u[1]; A[i][2] = u[2]; A[i][3] = u[3];
+        A[i][4] = v[0]; A[i][5] = v[1]; A[i][6] = v[2]; A[i][7] = v[3];
+      }
+    };
+    auto ldb = [&](int c, float (&B)[TN][8]) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        gcfp p = (gcfp)(brow[j] + c * 16 + 8 * lh);
+        const f32x4 u = *(gcf4p)p, w = *(gcf4p)(p + 4);
+        B[j][0] = u[0]; B[j][1] = u[1]; B[j][2] = u[2]; B[j][3] = u[3];
+        B[j][4] = w[0]; B[j][5] = w[1]; B[j][6] = w[2]; B[j][7] = w[3];
+      }
+    };
+    auto mm = [&](float (&A)[TM][8], float (&B)[TN][8]) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[i][q], B[j][q], acc[i][j], 0, 0, 0);
+    };
+    // B (weights, global) S - 1 chunks ahead in a rotation of S register sets, A (LDS) one chunk ahead
+    float xb[S][TN][8], xa[2][TM][8];
+#pragma unroll
+    for (int s2 = 0; s2 < S; ++s2) ldb(min(s2, nch - 1), xb[s2]);
+    lda(0, xa[0]);
+    int c = 0;
+    for (; c + S <= nch; c += S) {
+#pragma unroll
+      for (int s2 = 0; s2 < S; ++s2) {
+        lda(min(c + s2 + 1, nch - 1), xa[(s2 + 1) & 1]);
+        mm(xa[s2 & 1], xb[s2]);
+        ldb(min(c + s2 + S, nch - 1), xb[s2]);
+      }
+      if (S & 1) {   // keep the A double buffer's parity aligned with s2 = 0 at the next iteration
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int q = 0; q < 8; ++q) xa[0][i][q] = xa[1][i][q];
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < S - 1; ++s2)
+      if (c + s2 < nch) {
+        lda(min(c + s2 + 1, nch - 1), xa[(s2 + 1) & 1]);
+        mm(xa[s2 & 1], xb[s2]);
+      }
+  } else if (cb < ce) {
     float xa[S][TM][8], xb[S][TN][8];
     int okm[S];
 #pragma unroll
@@ -482,6 +582,17 @@ __global__ __launch_bounds__(256) void cgl_conv_fwd(CglConvLaunch args) {
   const int pi = cgl_conv_prob(L, bid);
   CglKP P = &L->p[pi];
   cgl_conv_fwd_body<TM, TN, FAST, BNIN>(L, P, bid - P->wg_begin, cgl_conv_lds);
+}
+
+// The phase-form upsampling conv with its input window staged in LDS (HALO path of cgl_conv_fwd_body): one
+// workgroup per 64-row tile, its 4 waves = the 4 output-parity problems (launch_conv_mma: conv_halo_ok).
+template <bool BNIN>
+__global__ __launch_bounds__(256) void cgl_conv_fwd_halo(CglConvLaunch args) {
+  (void)args;
+  extern __shared__ float cgl_conv_lds[];
+  CglKL L = cgl_conv_args();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  cgl_conv_fwd_body<2, 2, true, BNIN, true>(L, &L->p[wave], blockIdx.x, cgl_conv_lds, true);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2592,6 +2703,25 @@ struct StatBwd { const float* x = nullptr; const float* post = nullptr; const fl
 
 struct BnIn { const float* coef = nullptr; int groups = 1, gimg = 1, act = 0; float slope = 0.f; };
 
+// The halo path: 4 problems over one input through one tile grid -- the output parities of an upsampling
+// conv (2x2 taps, offsets within one pixel), 64 output channels (one 2x2-block wave tile), whole 64-row
+// tiles of whole low-res rows per image, a window that fits 64 KB of LDS.
+bool conv_halo_ok(const CglConvProb* P, int np) {
+  if (np != 4) return false;
+  const CglConvProb& a = P[0];
+  if (a.OW < 1 || 64 % a.OW || (a.OH * a.OW) % 64 || a.M % 64 || a.Cin % 16 || a.N != 64) return false;
+  if ((64 / a.OW + 2) * (a.OW + 2) * (a.Cin + 4) * 4 > 65536) return false;
+  for (int i = 0; i < np; ++i) {
+    const CglConvProb& p = P[i];
+    if (p.X != a.X || p.M != a.M || p.N != a.N || p.Cin != a.Cin || p.OH != a.OH || p.OW != a.OW || p.Ty != 2 ||
+        p.Tx != 2 || p.isy != 1 || p.isx != 1 || p.ish != 0 || p.IH != a.OH || p.IW != a.OW || p.Kp != p.K)
+      return false;
+    for (int t = 0; t < 2; ++t)
+      if (p.dy[t] < -1 || p.dy[t] > 1 || p.dx[t] < -1 || p.dx[t] > 1) return false;
+  }
+  return true;
+}
+
 int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float slope, const float* drop,
                     hipStream_t s, double* st_part = nullptr, int st_cpg = 0, const StatBwd* sb = nullptr,
                     const BnIn* bi = nullptr) {
@@ -2650,6 +2780,21 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
       L.p[i] = P[i];
     }
     hipLaunchKernelGGL(cgl_conv_n1, dim3(wg), dim3(256), 0, s, L);
+    return (int)hipGetLastError();
+  }
+  // the upsampling conv's 4 parity problems from one LDS-staged window per 64-row tile (CGL_CONV_HALO=0: off)
+  const int halo_env = getenv("CGL_CONV_HALO") ? atoi(getenv("CGL_CONV_HALO")) : 1;   // read per launch (tests toggle it)
+  if (halo_env && !L.st_mode && conv_halo_ok(P, np)) {
+    const int lds = (64 / P[0].OW + 2) * (P[0].OW + 2) * (P[0].Cin + 4) * 4;
+    L.WM = L.WN = L.WK = 1;
+    for (int i = 0; i < np; ++i) {
+      P[i].tiles_m = P[i].M / 64;
+      P[i].tiles_n = 1;
+      P[i].wg_begin = 0;
+      L.p[i] = P[i];
+    }
+    if (L.in_coef) hipLaunchKernelGGL((cgl_conv_fwd_halo<true>), dim3(P[0].M / 64), dim3(256), lds, s, L);
+    else hipLaunchKernelGGL((cgl_conv_fwd_halo<false>), dim3(P[0].M / 64), dim3(256), lds, s, L);
     return (int)hipGetLastError();
   }
   const ConvTiling t = conv_tiling_for(P, np);
