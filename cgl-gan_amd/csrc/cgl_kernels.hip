@@ -249,11 +249,15 @@ __global__ __launch_bounds__(256) void cgl_bn_apply(const CglBnApplyDesc* __rest
 // rows in registers: all loads are issued at once (one memory round trip) and the second pass
 // reuses them; larger M streams the rows twice.
 #define CGL_BNB_RPT 32
-__global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict__ bd) {
-  __shared__ double s_a[8][32], s_b[8][32];
+// FPW features per workgroup (32: the original layout; 16 / 8 / 4 give 2x / 4x / 8x the workgroups for the narrow
+// layers, each thread then owning fewer rows): NRG = 256 / FPW row groups, rows of a group in registers.
+template <int FPW>
+__device__ __forceinline__ void cgl_bn_bwd_body(const CglBnBwdDesc* __restrict__ bd) {
+  constexpr int NRG = 256 / FPW, RPT = 256 / NRG;   // register path: M <= NRG * RPT = 256
+  __shared__ double s_a[NRG][FPW], s_b[NRG][FPW];
   const int M = bd->M, F = bd->F;
-  const int fl = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  const int f = blockIdx.x * 32 + fl;
+  const int fl = threadIdx.x % FPW, rg = threadIdx.x / FPW;
+  const int f = blockIdx.x * FPW + fl;
   const bool fok = f < F;
   const int fc = min(f, F - 1);
   const float sl = bd->slope;
@@ -269,11 +273,11 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
   const long ldz = bd->ld_dz;
   const int kcz = (F + 15) >> 4;
   double sum = 0.0, dotp = 0.0;
-  if (M <= 8 * CGL_BNB_RPT) {
-    float dy[CGL_BNB_RPT], yc[CGL_BNB_RPT];
+  if (M <= NRG * RPT) {
+    float dy[RPT], yc[RPT];
 #pragma unroll
-    for (int j = 0; j < CGL_BNB_RPT; ++j) {
-      const int r = min(rg + 8 * j, M - 1);
+    for (int j = 0; j < RPT; ++j) {
+      const int r = min(rg + NRG * j, M - 1);
       // unconditional load (post aliases Y when unused), select after: a predicated load compiles
       // to a branch with a full vmcnt(0) drain per row
       const float da = gld(dA + r * lda), pr = gld(post + r * ldp), y = gld(Y + r * ldy);
@@ -282,8 +286,8 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
       yc[j] = y - mean;
     }
 #pragma unroll
-    for (int j = 0; j < CGL_BNB_RPT; ++j) {
-      if (rg + 8 * j < M) {
+    for (int j = 0; j < RPT; ++j) {
+      if (rg + NRG * j < M) {
         sum += (double)dy[j];
         dotp += (double)(yc[j] * dy[j]);
       }
@@ -292,7 +296,7 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
     s_b[rg][fl] = dotp;
     __syncthreads();
     double S = 0.0, D = 0.0;
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < NRG; ++q) {
       S += s_a[q][fl];
       D += s_b[q][fl];
     }
@@ -300,8 +304,8 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
     const float gmean = (float)(S / M);
     if (fok) {
 #pragma unroll
-      for (int j = 0; j < CGL_BNB_RPT; ++j) {
-        const int r = rg + 8 * j;
+      for (int j = 0; j < RPT; ++j) {
+        const int r = rg + NRG * j;
         if (r < M) {
           const float z = (dy[j] - gmean - yc[j] * k) * invstd * w;
           gst(dZ + r * ldz, z);
@@ -315,18 +319,18 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
     }
     return;
   }
-  for (int r0 = rg; r0 < M; r0 += 64) {
+  for (int r0 = rg; r0 < M; r0 += 8 * NRG) {
     float da[8], po[8], y[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int r = min(r0 + 8 * j, M - 1);
+      const int r = min(r0 + NRG * j, M - 1);
       da[j] = gld(dA + r * lda);
       po[j] = gld(post + r * ldp);
       y[j] = gld(Y + r * ldy);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      if (r0 + 8 * j < M) {
+      if (r0 + NRG * j < M) {
         const float dy = (!post_on || po[j] > 0.f) ? da[j] : da[j] * sl;
         sum += (double)dy;
         dotp += (double)((y[j] - mean) * dy);
@@ -337,25 +341,25 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
   s_b[rg][fl] = dotp;
   __syncthreads();
   double S = 0.0, D = 0.0;
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < NRG; ++q) {
     S += s_a[q][fl];
     D += s_b[q][fl];
   }
   if (!fok) return;
   const float k = (float)D * invstd * invstd / M;
   const float gmean = (float)(S / M);
-  for (int r0 = rg; r0 < M; r0 += 64) {
+  for (int r0 = rg; r0 < M; r0 += 8 * NRG) {
     float da[8], po[8], y[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int r = min(r0 + 8 * j, M - 1);
+      const int r = min(r0 + NRG * j, M - 1);
       da[j] = gld(dA + r * lda);
       po[j] = gld(post + r * ldp);
       y[j] = gld(Y + r * ldy);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int r = r0 + 8 * j;
+      const int r = r0 + NRG * j;
       if (r < M) {
         const float dy = (!post_on || po[j] > 0.f) ? da[j] : da[j] * sl;
         const float gi = (y[j] - mean) * k;
@@ -371,6 +375,10 @@ __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict
   }
 }
 
+__global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict__ bd) { cgl_bn_bwd_body<32>(bd); }
+__global__ __launch_bounds__(256) void cgl_bn_bwd16(const CglBnBwdDesc* __restrict__ bd) { cgl_bn_bwd_body<16>(bd); }
+__global__ __launch_bounds__(256) void cgl_bn_bwd8(const CglBnBwdDesc* __restrict__ bd) { cgl_bn_bwd_body<8>(bd); }
+__global__ __launch_bounds__(256) void cgl_bn_bwd4(const CglBnBwdDesc* __restrict__ bd) { cgl_bn_bwd_body<4>(bd); }
 // ------------------------------------------------------------------------------------------
 // Standalone BatchNorm1d (+ LeakyReLU) forward, train or eval, for the nn.Module path.  One
 // workgroup owns 32 features x all M rows (8 row groups): column sums in double, fixed order;

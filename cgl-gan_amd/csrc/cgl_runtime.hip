@@ -628,7 +628,11 @@ void push_bnb(cgl_gan* c, std::vector<Launch>& ph, const CglBnBwdDesc& b) {
   L.kind = K_BNBWD;
   L.first = (int)c->bnb.size();
   L.count = 1;
-  L.grid = (b.F + 31) / 32;
+  // features per workgroup (CGL_BNB_FPW = 32 / 16 / 8 / 4, default 8): a narrower slice gives the narrow layers
+  // more workgroups (B = 256, F = 256: 8 -> 32 workgroups; 8 measured -6 us/round vs 32, profiles/r03_bnb_ab.txt)
+  const int fe = getenv("CGL_BNB_FPW") ? atoi(getenv("CGL_BNB_FPW")) : 8;
+  L.blk = (fe == 32 || fe == 16 || fe == 4) ? fe : 8;
+  L.grid = (b.F + L.blk - 1) / L.blk;
   c->bnb.push_back(b);
   ph.push_back(L);
 }
@@ -1413,7 +1417,14 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
       hipLaunchKernelGGL(cgl_bn_apply, dim3(L.grid, L.grid_y), dim3(256), 0, s, c->ws.bna + L.first);
       break;
     case K_BNBWD:
-      hipLaunchKernelGGL(cgl_bn_bwd, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
+      if (L.blk == 16)
+        hipLaunchKernelGGL(cgl_bn_bwd16, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
+      else if (L.blk == 8)
+        hipLaunchKernelGGL(cgl_bn_bwd8, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
+      else if (L.blk == 4)
+        hipLaunchKernelGGL(cgl_bn_bwd4, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
+      else
+        hipLaunchKernelGGL(cgl_bn_bwd, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
       break;
     case K_ADAM:
       hipLaunchKernelGGL(cgl_adam, dim3(L.grid), dim3(256), 0, s, L.adam, c->ws.st, L.tail);
