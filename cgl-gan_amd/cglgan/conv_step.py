@@ -192,6 +192,8 @@ class ConvGanStep:
         self.dstate = torch.zeros(4, dtype=torch.int32, device=dev)
         self._dstate_host = (0, 0, 0)         # host mirror of dstate after the last issued round
         self._cuda_graph = None
+        self._phase_graphs = None      # (phase A, phase B) graphs of the split round (N > 1)
+        self._split_graph = False
         self._graph_delta = None
         # packed MFMA weight operands of every layer (cglgan.conv_ops.PackSet): G and D are packed
         # together at the start of a round (the exchanges between rounds may rewrite either), D again
@@ -540,6 +542,31 @@ class ConvGanStep:
         self._cuda_graph.replay()
         self._apply_host_delta()
 
+    # ------------------------------------------------------------------ split round (N > 1)
+    def round_a(self, real=None, eager=False):
+        """Phase A of a round split at the exchange (N > 1: ConvWorkerExchange / ConvLocalComm issue the
+        G-loss all-gather, the lambda weighting and the image-gradient all-reduce between round_a and
+        round_b).  With graph=True (and the round drawing its own real batch) every round after the first
+        replays phase A and phase B as two hipGraphs captured together; the collectives between them stay
+        eager."""
+        self._split_graph = (self.graph and not eager and real is None and self.data is not None and
+                             self.round > 0)
+        if not self._split_graph:
+            self.phase_a(real)
+            return
+        if self._phase_graphs is None:
+            self._capture(split=True)
+        self._sync_dstate()
+        self._phase_graphs[0].replay()
+
+    def round_b(self):
+        """Phase B of the split round (after the exchange)."""
+        if not self._split_graph:
+            self.phase_b()
+            return
+        self._phase_graphs[1].replay()
+        self._apply_host_delta()
+
     # ------------------------------------------------------------------ graph replay
     def _host_state(self):
         return (self.round, self.G.step, self.D.step, dict(self.G.batches), dict(self.D.batches), self.lam)
@@ -552,14 +579,21 @@ class ConvGanStep:
             self.dstate[:3].copy_(torch.tensor(want, dtype=torch.int32))
             self._dstate_host = want
 
-    def _capture(self):
+    def _capture(self, split=False):
         before = self._host_state()
         self._sync_dstate()
         torch.cuda.current_stream().synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self.phase_a(None)
-            self.phase_b()
+        if split:      # phase A and phase B as two graphs (the exchange runs between their replays)
+            ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(ga):
+                self.phase_a(None)
+            with torch.cuda.graph(gb):
+                self.phase_b()
+        else:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.phase_a(None)
+                self.phase_b()
         after = self._host_state()
         # capturing issued nothing: restore the host bookkeeping, remember what one round adds
         self.round, self.G.step, self.D.step = before[0], before[1], before[2]
@@ -569,7 +603,10 @@ class ConvGanStep:
         self._dstate_host = (self.round, self.G.step, self.D.step)
         self._graph_delta = ({k: after[3][k] - before[3][k] for k in before[3]},
                              {k: after[4][k] - before[4][k] for k in before[4]})
-        self._cuda_graph = g
+        if split:
+            self._phase_graphs = (ga, gb)
+        else:
+            self._cuda_graph = g
 
     def _apply_host_delta(self):
         gb, db = self._graph_delta

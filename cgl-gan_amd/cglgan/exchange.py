@@ -304,15 +304,18 @@ class ConvWorkerExchange:
     def _d_state(self):
         return [self.step.D.p] + list(self.step.D.running.values())
 
-    def round(self, r: int, real=None):
+    def round(self, r: int, real=None, eager=False):
+        """One round.  N > 1: phase A, the exchange, phase B -- with a ConvGanStep(graph=True) drawing its
+        own real batches, phase A and phase B replay as hipGraphs from the second round on
+        (ConvGanStep.round_a / round_b); ``eager`` issues them op by op."""
         from . import conv_ops as O
         s = self.step
         share = self.comm is not None and self.share_every > 0 and (r + 1) % self.share_every == 0
         swap = self.dswap is not None and (r + 1) % self.swap_every == 0
         if self.comm is None or self.comm.size == 1:
-            s.run(real)
+            s.run(real, eager=eager)
         else:
-            s.phase_a(real)
+            s.round_a(real, eager=eager)
             self.comm.all_gather(s.losses_all, s.lbuf[2:3])
             O.weights_scale(s.weighting, s.lam, s.beta, s.losses_all, s.rank, s.dimg)
             self.comm.all_reduce_sum(s.dimg)
@@ -325,11 +328,11 @@ class ConvWorkerExchange:
                 self._side.wait_stream(main)
                 with torch.cuda.stream(self._side):
                     self._d_exchange(share, swap)
-                s.phase_b()
+                s.round_b()
                 main.wait_stream(self._side)
                 share = swap = False
             else:
-                s.phase_b()
+                s.round_b()
         self._d_exchange(share, swap)
 
     def _d_exchange(self, share, swap):
@@ -349,15 +352,15 @@ class ConvLocalComm:
         self.steps = steps
         self.size = len(steps)
 
-    def round(self, r: int, reals=None, share_every: int = 0):
+    def round(self, r: int, reals=None, share_every: int = 0, eager=False):
         from . import conv_ops as O
         ss = self.steps
         reals = reals if reals is not None else [None] * self.size
         if self.size == 1:
-            ss[0].run(reals[0])
+            ss[0].run(reals[0], eager=eager)
             return
         for s, x in zip(ss, reals):
-            s.phase_a(x)
+            s.round_a(x, eager=eager)
         losses = torch.cat([s.lbuf[2:3] for s in ss])
         for s in ss:
             s.losses_all.copy_(losses)
@@ -367,7 +370,7 @@ class ConvLocalComm:
             tot += s.dimg
         for s in ss:
             s.dimg.copy_(tot)
-            s.phase_b()
+            s.round_b()
         if share_every > 0 and (r + 1) % share_every == 0:
             for i in range(1 + len(ss[0].D.running)):
                 ts = [s.D.p if i == 0 else list(s.D.running.values())[i - 1] for s in ss]

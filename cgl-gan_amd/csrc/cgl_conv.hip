@@ -585,14 +585,19 @@ __global__ __launch_bounds__(256) void cgl_conv_fwd(CglConvLaunch args) {
 }
 
 // The phase-form upsampling conv with its input window staged in LDS (HALO path of cgl_conv_fwd_body): one
-// workgroup per 64-row tile, its 4 waves = the 4 output-parity problems (launch_conv_mma: conv_halo_ok).
+// workgroup per (64-row tile, 64-output-channel slice), its 4 waves = the 4 output-parity problems
+// (launch_conv_mma: conv_halo_ok).
 template <bool BNIN>
 __global__ __launch_bounds__(256) void cgl_conv_fwd_halo(CglConvLaunch args) {
   (void)args;
   extern __shared__ float cgl_conv_lds[];
   CglKL L = cgl_conv_args();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  cgl_conv_fwd_body<2, 2, true, BNIN, true>(L, &L->p[wave], blockIdx.x, cgl_conv_lds, true);
+  // XCD-contiguous tile order: the N-halves of one row tile and vertically adjacent tiles (which share
+  // window rows) run on one XCD's L2
+  CglKP P = &L->p[wave];
+  cgl_conv_fwd_body<2, 2, true, BNIN, true>(L, P, cgl_xcd_tile(blockIdx.x, P->tiles_m * P->tiles_n), cgl_conv_lds,
+                                             true);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2709,7 +2714,8 @@ struct BnIn { const float* coef = nullptr; int groups = 1, gimg = 1, act = 0; fl
 bool conv_halo_ok(const CglConvProb* P, int np) {
   if (np != 4) return false;
   const CglConvProb& a = P[0];
-  if (a.OW < 1 || 64 % a.OW || (a.OH * a.OW) % 64 || a.M % 64 || a.Cin % 16 || a.N != 64) return false;
+  if (a.OW < 1 || 64 % a.OW || (a.OH * a.OW) % 64 || a.M % 64 || a.Cin % 16 || (a.N != 64 && a.N != 128))
+    return false;
   if ((64 / a.OW + 2) * (a.OW + 2) * (a.Cin + 4) * 4 > 65536) return false;
   for (int i = 0; i < np; ++i) {
     const CglConvProb& p = P[i];
@@ -2789,12 +2795,13 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
     L.WM = L.WN = L.WK = 1;
     for (int i = 0; i < np; ++i) {
       P[i].tiles_m = P[i].M / 64;
-      P[i].tiles_n = 1;
+      P[i].tiles_n = N / 64;   // a workgroup per (64-row tile, 64-channel half); each stages the tile's window
       P[i].wg_begin = 0;
       L.p[i] = P[i];
     }
-    if (L.in_coef) hipLaunchKernelGGL((cgl_conv_fwd_halo<true>), dim3(P[0].M / 64), dim3(256), lds, s, L);
-    else hipLaunchKernelGGL((cgl_conv_fwd_halo<false>), dim3(P[0].M / 64), dim3(256), lds, s, L);
+    const int grid = P[0].M / 64 * (N / 64);
+    if (L.in_coef) hipLaunchKernelGGL((cgl_conv_fwd_halo<true>), dim3(grid), dim3(256), lds, s, L);
+    else hipLaunchKernelGGL((cgl_conv_fwd_halo<false>), dim3(grid), dim3(256), lds, s, L);
     return (int)hipGetLastError();
   }
   const ConvTiling t = conv_tiling_for(P, np);

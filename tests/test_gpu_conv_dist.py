@@ -31,9 +31,17 @@ def _reals(rank, r):
     return torch.rand(B, 1, 32, 32, generator=g) * 2 - 1
 
 
-def _make(rank, world):
+def _data(rank):
+    g = torch.Generator().manual_seed(500 + rank)
+    return (torch.rand(4 * B + 3, 1024, generator=g) * 2 - 1).cuda()
+
+
+def _make(rank, world, graph=False):
+    """graph=True: the worker draws its real batches on the device from its own shard, so rounds after the
+    first replay phase A / phase B as hipGraphs (ConvGanStep.round_a / round_b)."""
     from cglgan.conv_step import ConvGanStep
-    st = ConvGanStep(B, loss="mse", seed=77, n_workers=world, rank=rank)
+    st = ConvGanStep(B, loss="mse", seed=77, n_workers=world, rank=rank, data=_data(rank) if graph else None,
+                     graph=graph)
     st.init_default(20211212, 20211213 + rank)
     return st
 
@@ -69,17 +77,17 @@ class HostComm:
             t.copy_(h.to(t.device))
 
 
-def _proc(rank, world, port, outdir, rounds):
+def _proc(rank, world, port, outdir, rounds, graph=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from cglgan.exchange import ConvWorkerExchange
         torch.cuda.set_device(0)
-        st = _make(rank, world)
+        st = _make(rank, world, graph)
         ex = ConvWorkerExchange(st, HostComm(), share_every=1, swap_every=2)
         for r in range(rounds):
-            ex.round(r, real=_reals(rank, r).cuda())
+            ex.round(r, real=None if graph else _reals(rank, r).cuda())
         torch.cuda.synchronize()
         torch.save({"g": st.G.p.cpu(), "d": st.D.p.cpu(), "run": [v.cpu() for v in st.D.running.values()],
                     "grun": [v.cpu() for v in st.G.running.values()], "lbuf": st.lbuf.cpu()},
@@ -88,16 +96,20 @@ def _proc(rank, world, port, outdir, rounds):
         dist.destroy_process_group()
 
 
-def test_conv_worker_exchange_distcomm_matches_local():
-    world, rounds = 2, 2
+@pytest.mark.parametrize("graph", [False, True])
+def test_conv_worker_exchange_distcomm_matches_local(graph):
+    """graph=True: the two processes replay phase A / phase B as hipGraphs (rounds 1..3) around the eager
+    collectives and the side-stream D exchange; the in-process reference issues every round op by op."""
+    world, rounds = 2, (4 if graph else 2)
     with tempfile.TemporaryDirectory() as td:
-        mp.spawn(_proc, args=(world, _free_port(), td, rounds), nprocs=world, join=True)
+        mp.spawn(_proc, args=(world, _free_port(), td, rounds, graph), nprocs=world, join=True)
         res = [torch.load(os.path.join(td, f"r{r}.pt"), weights_only=True) for r in range(world)]
     from cglgan.exchange import ConvLocalComm, DSwap
-    steps = [_make(r, world) for r in range(world)]
+    steps = [_make(r, world, graph) for r in range(world)]
     comm, dsw = ConvLocalComm(steps), DSwap(world)
     for r in range(rounds):
-        comm.round(r, reals=[_reals(i, r).cuda() for i in range(world)], share_every=1)
+        comm.round(r, reals=None if graph else [_reals(i, r).cuda() for i in range(world)], share_every=1,
+                   eager=True)
         if (r + 1) % 2 == 0:           # ConvWorkerExchange's D-swap: parameters + running statistics
             perm = dsw.next_perm()
             old = [[s.D.p.clone()] + [v.clone() for v in s.D.running.values()] for s in steps]

@@ -1,10 +1,11 @@
-"""The phase-form upsampling conv (model/lsgan.py:17-18: Upsample(2) -> Conv2d(128, 64)) with its input window
-staged in LDS once per 64-row tile and shared by the 4 output-parity waves (cgl_conv.hip HALO path,
-conv_halo_ok): the same chunk order and MFMA sequence as the direct path's one-wave-per-K tiling, so bitwise equal
-to it (CGL_CONV_HALO=0) whenever the direct path picks that tiling (>= 512 workgroups: n >= 128 images, which the
-bench's n = 512 meets) -- as a single op and over whole eager rounds (with and without the folded input BatchNorm).
-Smaller batches make the direct path split K over the waves of a workgroup (conv_tiling_for), a different summation
-order: there the two agree to fp32 accumulation tolerance."""
+"""The phase-form upsampling convs (model/lsgan.py:14-18: Upsample(2) -> Conv2d(128, 128) and Upsample(2) ->
+Conv2d(128, 64)) with the input window staged in LDS once per 64-row tile and shared by the 4 output-parity waves
+(cgl_conv.hip HALO path, conv_halo_ok): the same chunk order and MFMA sequence as the direct path's
+one-wave-per-K tiling, so bitwise equal to it (CGL_CONV_HALO=0) whenever the direct path picks that tiling
+(>= 512 workgroups: n >= 128 images for the 64-channel conv, n >= 512 for the 128-channel one; the bench runs
+n = 512) -- as a single op and over whole eager rounds (with and without the folded input BatchNorm).
+Smaller batches make the direct path split K over the waves of a workgroup (conv_tiling_for), a different
+summation order: there the two agree to fp32 accumulation tolerance."""
 import os
 
 import pytest
@@ -23,28 +24,34 @@ def _with(env, fn):
         os.environ.pop("CGL_CONV_HALO", None)
 
 
-def _upconv_pair(n):
+# (input side, output channels): conv_blocks.5 (Upsample 16 -> 32, Conv2d(128, 64)) and conv_blocks.1
+# (Upsample 8 -> 16, Conv2d(128, 128): two 64-channel workgroups per row tile)
+GEOMS = [(16, 64), (8, 128)]
+
+
+def _upconv_pair(n, hw, cout):
     from cglgan import conv_ops as O
     g = torch.Generator(device="cuda").manual_seed(7)
-    x = torch.randn(n, 16, 16, 128, device="cuda", generator=g)
-    w = torch.randn(64, 128, 3, 3, device="cuda", generator=g) * 0.05
-    b = torch.randn(64, device="cuda", generator=g)
+    x = torch.randn(n, hw, hw, 128, device="cuda", generator=g)
+    w = torch.randn(cout, 128, 3, 3, device="cuda", generator=g) * 0.05
+    b = torch.randn(cout, device="cuda", generator=g)
     outs = []
     for env in ("1", "0"):
-        y = torch.empty(n, 32, 32, 64, device="cuda")
-        outs.append(_with(env, lambda: O.conv3x3_fwd(x, w, b, y, n, 16, 16, 128, 64, 1, 1, O.ACT_LEAKY, 0.2).clone()))
+        y = torch.empty(n, 2 * hw, 2 * hw, cout, device="cuda")
+        outs.append(_with(env, lambda: O.conv3x3_fwd(x, w, b, y, n, hw, hw, 128, cout, 1, 1, O.ACT_LEAKY,
+                                                     0.2).clone()))
     return outs
 
 
-@pytest.mark.parametrize("n", [128, 512])
-def test_upconv_halo_op_bitwise(n):
-    a, b = _upconv_pair(n)
+@pytest.mark.parametrize("n,geom", [(128, GEOMS[0]), (512, GEOMS[0]), (512, GEOMS[1])])
+def test_upconv_halo_op_bitwise(n, geom):
+    a, b = _upconv_pair(n, *geom)
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("n", [2, 64])
-def test_upconv_halo_op_small_batch(n):
-    a, b = _upconv_pair(n)
+@pytest.mark.parametrize("n,geom", [(2, GEOMS[0]), (64, GEOMS[0]), (2, GEOMS[1]), (64, GEOMS[1]), (128, GEOMS[1])])
+def test_upconv_halo_op_small_batch(n, geom):
+    a, b = _upconv_pair(n, *geom)
     # K = 1152 products of |x| ~ 1, |w| ~ 0.05 per output: fp32 reassociation error well below 1e-4
     torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
 
@@ -52,7 +59,7 @@ def test_upconv_halo_op_small_batch(n):
 @pytest.mark.parametrize("fold", [0, 3])
 def test_conv_round_halo_bitwise(fold):
     from cglgan.conv_step import ConvGanStep
-    B = 64   # G's up-conv over n = 2B = 128 images: the direct path's one-wave-per-K tiling
+    B = 256   # G's up-convs over n = 2B = 512 images: the direct path's one-wave-per-K tiling for both
     data = torch.rand(4 * B + 3, 1024, device="cuda", generator=torch.Generator("cuda").manual_seed(3)) * 2 - 1
     steps = []
     for env in ("1", "0"):
