@@ -336,9 +336,10 @@ def main_lsgan(a, world, rank, local):
         rows = (a.rows // a.batch) * a.batch
         data = torch.rand(rows, 1024, device="cuda", generator=g) * 2 - 1
         # one worker per GPU: G replicated (same init and z stream), D and real shard per rank
-        # N = 1: the round replays as one hipGraph (device-side round state, cglgan.conv_step graph mode)
+        # the round replays as one hipGraph at N = 1 (device-side round state, cglgan.conv_step graph mode);
+        # at N > 1 phase A and phase B replay as two graphs around the eager collectives (round_a / round_b)
         step = ConvGanStep(a.batch, loss=a.loss, data=data, seed=20211212, n_workers=world, rank=rank,
-                           graph=world == 1 and not a.eager)
+                           graph=not a.eager)
         step.init_default(20211212, 20211212 + 1 + rank)
         ex = ConvWorkerExchange(step, DistComm() if world > 1 else None, share_every=a.E if world > 1 else 0)
         torch.cuda.synchronize()
