@@ -364,7 +364,7 @@ def main_lsgan(a, world, rank, local):
             el = float(t.item())
         st = step.stats()
         # per-op timing needs the ops issued one by one: an eager round (same device round state)
-        ops = profile_conv_round(lambda: step.run(eager=True) if world == 1 else ex.round(r))
+        ops = profile_conv_round(lambda: step.run(eager=True) if world == 1 else ex.round(r, eager=True))
     ms_step = el / a.steps * 1e3
     value = world * a.batch * a.steps / el
     if rank != 0:
@@ -385,7 +385,7 @@ def main_lsgan(a, world, rank, local):
                                   f"all-reduce, E={a.E} D all-reduce over RCCL" if world > 1 else ""),
                    "global_batch": a.batch * world, "batch_per_worker": a.batch, "img": "32x32x1",
                    "parallelism": f"workers{world}", "dataset_rows_per_worker": rows,
-                   "graph": world == 1 and not a.eager},
+                   "graph": not a.eager},
         "roofline": {"bound": "mfma", "kernel": "cgl_conv_fwd + cgl_conv_wgrad (+ pack / reduce), every conv op of "
                                                 "one round", "achieved": round(tf, 3), "peak": PEAK_F32_MFMA,
                      "unit": "TFLOP/s", "frac": round(tf / PEAK_F32_MFMA, 4), **conv_traffic(),
