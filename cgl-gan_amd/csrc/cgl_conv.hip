@@ -621,7 +621,10 @@ __device__ float cgl_zero_page[CGL_ZERO_PAGE];
 // strides along the row, the tap's row bounds checked once (a fraction of the generic path's VALU).
 template <int TM, int TN, bool ROW>
 __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local) {
-  constexpr int S = 2;
+#ifndef CGL_WGRAD_S
+#define CGL_WGRAD_S 2
+#endif
+  constexpr int S = CGL_WGRAD_S;   // operand register sets in rotation (S - 1 chunks of loads in flight)
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, li = lane & 31, lh = lane >> 5;
