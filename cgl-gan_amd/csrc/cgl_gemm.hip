@@ -394,6 +394,38 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     }
   }
 
+  // ---------------- epilogue operands, issued before the k-loop
+  // The bias and the LeakyReLU' / Tanh' reference of the stored tile are loaded by the owner waves
+  // ahead of the first chunk's operands: they return with that chunk (loads count in order) instead
+  // of costing one more dependent memory round trip after the k-loop.  (A descriptor carries at most
+  // one of mask_ref / tanh_ref.)  Clamped addresses, unconditional per lane.  CGL_GEMM_EPI_PF=0 keeps the
+  // loads in the epilogue.
+#ifndef CGL_GEMM_EPI_PF
+#define CGL_GEMM_EPI_PF 1
+#endif
+  constexpr bool EPF = CGL_GEMM_EPI_PF && !ADAM && TM * TN == 1;   // (2x2 waves: no registers to spare)
+  float pf_bias[TN], pf_ref[EPF ? TM : 1][EPF ? TN : 1][16];
+  if constexpr (EPF) {
+    if (wk == 0) {
+      const float* ref = d->mask_ref ? d->mask_ref : d->tanh_ref;
+      const long ldr = d->mask_ref ? d->mask_ld : d->tanh_ld;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int colc = min(n0 + 32 * j + li, N - 1);
+        pf_bias[j] = d->bias ? gld(d->bias + colc) : 0.f;
+        if (ref) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = min(m0 + 4 * lh + 32 * i + (r & 3) + 8 * (r >> 2), M - 1);
+              pf_ref[i][j][r] = gld(ref + (long)row * ldr + colc);
+            }
+        }
+      }
+    }
+  }
+
   // ---------------- main loop
   const int b_ones = (LAYOUT != 0) ? d->b_ones_col : 0;
   const int nmem = N - b_ones;     // columns of B actually in memory
@@ -749,7 +781,9 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     const bool colok = col < N;
     const bool ones_col = b_ones && col == N - 1;
     if (owner && colok && !ones_col) {
-      const float bb = d->bias ? gld(d->bias + col) : 0.f;
+      float bb;
+      if constexpr (EPF) bb = pf_bias[j];
+      else bb = d->bias ? gld(d->bias + col) : 0.f;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         float* v = (float*)&acc[i][j];
@@ -773,8 +807,12 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
           float ref[16];
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int row = min(rbase + 32 * i + (r & 3) + 8 * (r >> 2), M - 1);
-            ref[r] = gld(d->mask_ref + (long)row * d->mask_ld + col);
+            if constexpr (EPF) {
+              ref[r] = pf_ref[i][j][r];
+            } else {
+              const int row = min(rbase + 32 * i + (r & 3) + 8 * (r >> 2), M - 1);
+              ref[r] = gld(d->mask_ref + (long)row * d->mask_ld + col);
+            }
           }
 #pragma unroll
           for (int r = 0; r < 16; ++r) v[r] = ref[r] > 0.f ? v[r] : v[r] * sl;
@@ -783,8 +821,12 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
           float t[16];
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int row = min(rbase + 32 * i + (r & 3) + 8 * (r >> 2), M - 1);
-            t[r] = gld(d->tanh_ref + (long)row * d->tanh_ld + col);
+            if constexpr (EPF) {
+              t[r] = pf_ref[i][j][r];
+            } else {
+              const int row = min(rbase + 32 * i + (r & 3) + 8 * (r >> 2), M - 1);
+              t[r] = gld(d->tanh_ref + (long)row * d->tanh_ld + col);
+            }
           }
 #pragma unroll
           for (int r = 0; r < 16; ++r) v[r] = cgl_dtanh(v[r], t[r]);

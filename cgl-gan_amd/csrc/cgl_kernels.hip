@@ -195,6 +195,12 @@ __global__ __launch_bounds__(256) void cgl_bn_apply(const CglBnApplyDesc* __rest
   float y[RPT];
 #pragma unroll
   for (int i = 0; i < RPT; ++i) y[i] = gld(ad->Y + (long)min(r0 + rl + 4 * i, mtot - 1) * ad->ld_y + fc);
+  // gamma / beta and the running statistics are issued with the rows, ahead of the partials' combine:
+  // loaded after it they cost one more dependent memory round trip each (unconditional loads from
+  // valid addresses: a predicated load compiles to a branch with a full vmcnt(0) drain)
+  const float gam = gld(bn.gamma + fc), bet = gld(bn.beta + fc);
+  const float rm0 = gld(bn.run_mean ? bn.run_mean + fc : bn.gamma + fc);
+  const float rv0 = gld(bn.run_var ? bn.run_var + fc : bn.gamma + fc);
   if (tid < 64 * ngroups) {
     const int g = tid >> 6;
     const int k[1] = {f < F ? f : -1};
@@ -202,9 +208,9 @@ __global__ __launch_bounds__(256) void cgl_bn_apply(const CglBnApplyDesc* __rest
     int n;
     cgl_bn_stats<1>(bn, F, k, g, mean, m2, n);
     const double invstd = 1.0 / sqrt(m2[0] / n + bn.eps);
-    const float sc = (float)invstd * gld(bn.gamma + fc);
+    const float sc = (float)invstd * gam;
     s_sc[g][fl] = sc;
-    s_sh[g][fl] = gld(bn.beta + fc) - (float)mean[0] * sc;
+    s_sh[g][fl] = bet - (float)mean[0] * sc;
     s_mean[g][fl] = mean[0];
     s_m2[g][fl] = m2[0];
     if (fl == 0) s_n[g] = n;
@@ -216,7 +222,7 @@ __global__ __launch_bounds__(256) void cgl_bn_apply(const CglBnApplyDesc* __rest
   __syncthreads();
   if (blockIdx.y == 0 && bn.run_mean && tid < 64 && f < F) {
     const double mom = bn.momentum;
-    float rm = gld(bn.run_mean + f), rv = gld(bn.run_var + f);
+    float rm = rm0, rv = rv0;
     for (int g = 0; g < ngroups; ++g) {
       rm = (float)(mom * s_mean[g][fl] + (1.0 - mom) * (double)rm);
       rv = (float)(mom * (s_m2[g][fl] / (s_n[g] - 1)) + (1.0 - mom) * (double)rv);
