@@ -1057,6 +1057,11 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
   __shared__ int s_flag[1];                     // split-K: this workgroup reduces its tile
   __shared__ double s_bnd[4 * TN * 32 * 2];     // per-column BatchNorm partials across waves (WM WN <= 4)
   const int bid = blockIdx.x;
+  // the previous head launch's deferred batch-mean loss reduction rides in one extra workgroup (the last)
+  if (descs[0].fin_head && bid == (int)gridDim.x - 1) {
+    cgl_head_finish(descs[0].fin_head, descs[0].fin_head->nwg, cgl_dyn_lds);
+    return;
+  }
   int di = 0;
   for (int q = 1; q < ndesc; ++q)
     if (bid >= descs[q].wg_begin) di = q;

@@ -162,6 +162,8 @@ struct CglGemmDesc {
   float* ad_pb; float* ad_mb; float* ad_vb;
   const float* ad_ss; const float* ad_bc;
   float ad_b2, ad_w1, ad_w2, ad_eps;
+  const struct CglHeadDesc* fin_head;   // desc 0 of a launch: the previous head launch's deferred loss reduction,
+                                         // run by one extra workgroup (the launch's last)
 };
 
 // BatchNorm1d(train) + LeakyReLU over the whole [mtot][F] output of one G layer.
@@ -196,7 +198,12 @@ struct CglHeadDesc {
   float* combine_out;     // optional
   const float* combine_in0;  // segment-0 mean computed by another launch (when this one has no segment 0)
   int rows_per_wg;
+  int deferred;           // the batch-mean reduction is left to the next GEMM launch's finisher workgroup
+  int nwg;                // (deferred) this launch's workgroups = partials to reduce
 };
+// batch-mean loss reduction of a head launch's partials (cgl_kernels.hip; also run by a GEMM finisher workgroup)
+__device__ void cgl_head_finish(const CglHeadDesc* __restrict__ hd, int nwg, float* s_part);
+
 
 // Standalone BatchNorm1d forward (nn.Module path): batch or running statistics, optional LeakyReLU.
 struct CglBn1dDesc {

@@ -24,6 +24,32 @@ __device__ __forceinline__ float cgl_wave_sum(float x) {
   return x;
 }
 
+// The batch-mean losses from the nwg per-workgroup partials (every thread of the calling workgroup loads
+// them at once, one round trip; thread 0 sums them in a fixed order, in double) -- run by the head's last
+// arriving workgroup, or by the finisher workgroup of the next GEMM launch when the head is deferred.
+__device__ void cgl_head_finish(const CglHeadDesc* __restrict__ hd, int nwg, float* s_part) {
+  const int M = hd->M;
+  // every thread loads partials at once (one round trip), thread 0 sums them in a fixed order
+  const int np = 2 * nwg;
+  for (int i = threadIdx.x; i < np; i += 256)
+    s_part[i] = __hip_atomic_load((CGL_GLOBAL float*)(hd->part + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s0 = 0.0, s1 = 0.0;
+    for (int q = 0; q < nwg; ++q) {
+      s0 += (double)s_part[2 * q];
+      s1 += (double)s_part[2 * q + 1];
+    }
+    const int n0s = min(hd->split, M), n1 = M - n0s;
+    const int n0 = hd->n0_dev ? min(gldi(hd->n0_dev), n0s) : n0s;
+    const float l0 = n0 > 0 ? (float)(s0 / n0) : (hd->combine_in0 ? gld(hd->combine_in0) : 0.f);
+    const float l1 = n1 > 0 ? (float)(s1 / n1) : 0.f;
+    if (hd->loss_out0 && n0 > 0) gst(hd->loss_out0, l0);
+    if (hd->loss_out1 && n1 > 0) gst(hd->loss_out1, l1);
+    if (hd->combine_out) gst(hd->combine_out, (l0 + l1) * hd->combine);
+  }
+}
+
 #define CGL_HEAD_MAXQ 4   // float4 per lane kept in registers: F <= 1024
 __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restrict__ hd) {
   // Each wave owns rows r0 + wave + 4 i; a row is a dot product of F features (F % 4 == 0)
@@ -128,6 +154,18 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
     s_loss[wave][1] = lsum[1];
   }
   __syncthreads();
+  if (hd->deferred) {   // the next launch's finisher workgroup reduces the partials (kernel boundary = visibility)
+    if (threadIdx.x == 0) {
+      float a = 0.f, b = 0.f;
+      for (int q = 0; q < 4; ++q) {
+        a += s_loss[q][0];
+        b += s_loss[q][1];
+      }
+      gst(hd->part + blockIdx.x * 2 + 0, a);
+      gst(hd->part + blockIdx.x * 2 + 1, b);
+    }
+    return;
+  }
   if (threadIdx.x == 0) {
     float a = 0.f, b = 0.f;
     for (int q = 0; q < 4; ++q) {
@@ -147,26 +185,8 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
   }
   __syncthreads();
   if (!s_last) return;
-  // every thread loads partials at once (one round trip), thread 0 sums them in a fixed order
-  const int np = 2 * gridDim.x;
-  for (int i = threadIdx.x; i < np; i += 256)
-    s_part[i] = __hip_atomic_load((CGL_GLOBAL float*)(hd->part + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double s0 = 0.0, s1 = 0.0;
-    for (unsigned int q = 0; q < gridDim.x; ++q) {
-      s0 += (double)s_part[2 * q];
-      s1 += (double)s_part[2 * q + 1];
-    }
-    const int n0s = min(hd->split, M), n1 = M - n0s;
-    const int n0 = hd->n0_dev ? min(gldi(hd->n0_dev), n0s) : n0s;
-    const float l0 = n0 > 0 ? (float)(s0 / n0) : (hd->combine_in0 ? gld(hd->combine_in0) : 0.f);
-    const float l1 = n1 > 0 ? (float)(s1 / n1) : 0.f;
-    if (hd->loss_out0 && n0 > 0) gst(hd->loss_out0, l0);
-    if (hd->loss_out1 && n1 > 0) gst(hd->loss_out1, l1);
-    if (hd->combine_out) gst(hd->combine_out, (l0 + l1) * hd->combine);
-    __hip_atomic_store(hd->counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  cgl_head_finish(hd, (int)gridDim.x, s_part);
+  if (threadIdx.x == 0) __hip_atomic_store(hd->counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // (cgl_bn_stats: cgl_gemm.hip, shared with the GEMMs that fold the BatchNorm into their loads)

@@ -722,6 +722,33 @@ void fuse_wgrad_adam(cgl_gan* c, std::vector<Launch>& ph, int model) {
   ph.back() = F;
 }
 
+// A head launch followed (same stream, no event between) by a GEMM launch leaves its batch-mean loss reduction
+// to that launch: the head workgroups only store their partials (no release, no ticket, no last-arriver
+// round trips), and one extra workgroup of the GEMM launch -- its last -- reduces them in the same fixed
+// order (cgl_head_finish), so the losses are bitwise those of the ticket path.  The kernel boundary makes the
+// partials visible; nothing in the GEMM launch reads the losses.  CGL_HEAD_DEFER=0 keeps the ticket path.
+void defer_heads(cgl_gan* c) {
+  const int env = getenv("CGL_HEAD_DEFER") ? atoi(getenv("CGL_HEAD_DEFER")) : 1;   // read per plan
+  if (!env) return;
+  for (std::vector<Launch>* ph : {&c->phA, &c->phB}) {
+    for (size_t i = 0; i + 1 < ph->size(); ++i) {
+      Launch& H = (*ph)[i];
+      Launch& G = (*ph)[i + 1];
+      if (H.kind != K_HEAD || G.kind != K_GEMM || H.stream != 0 || G.stream != 0 || H.record_ev >= 0 ||
+          G.wait_ev >= 0)
+        continue;
+      CglGemmDesc& d0 = c->gemm[G.first];
+      if (d0.fin_head) continue;
+      CglHeadDesc& h = c->head[H.first];
+      h.deferred = 1;
+      h.nwg = H.grid;
+      d0.fin_head = c->ws.head + H.first;
+      G.grid += 1;
+      G.shmem = std::max(G.shmem, 8 * H.grid);   // the finisher's partials in dynamic LDS
+    }
+  }
+}
+
 // The round prologue and G's first GEMM as one launch (K_GEMM_PRO, cgl_gemm_pro): the GEMM's workgroups
 // draw their own rows of z (a_gen; every column tile of a row tile draws the same rows, identical writes),
 // the prologue's other blocks ride along.  fp32 plans on one stream; CGL_FUSE_PRO=0 keeps two launches.
@@ -1292,6 +1319,7 @@ int build_plan(cgl_gan* c) {
       if (Lq.kind == K_PROLOGUE) Lq.grid += blk;
   }
   fuse_prologue(c);
+  defer_heads(c);
   if ((int)c->gemm.size() > kMaxGemmDescs || (int)c->head.size() > kMaxHeadDescs ||
       (int)c->bnb.size() > kMaxBnDescs || (int)c->bna.size() > kMaxBnDescs)
     return CGL_E_SIZE;
