@@ -24,7 +24,7 @@ EXPORTS = [
     "cgl_gan_param_count", "cgl_gan_param_tensor", "cgl_gan_running_count", "cgl_gan_workspace_bytes",
     "cgl_gan_create", "cgl_gan_destroy", "cgl_gan_reset", "cgl_gan_run", "cgl_gan_run_graph",
     "cgl_gan_alpha_scale", "cgl_gan_exchange_buffer", "cgl_gan_tensor", "cgl_gan_read_stats",
-    "cgl_gan_plan_info", "cgl_gan_launch_count", "cgl_gan_launch_info", "cgl_gan_launch_one", "cgl_linear_fwd", "cgl_linear_bwd_data", "cgl_linear_bwd_weight", "cgl_adam_step",
+    "cgl_gan_plan_info", "cgl_gan_launch_count", "cgl_gan_launch_info", "cgl_gan_launch_one", "cgl_gan_profile", "cgl_linear_fwd", "cgl_linear_bwd_data", "cgl_linear_bwd_weight", "cgl_adam_step",
     "cgl_normal_fill", "cgl_op_workspace_bytes", "cgl_version", "cgl_act_fwd", "cgl_act_bwd", "cgl_bn1d_fwd",
     "cgl_bn1d_bwd",
     # conv GAN path (model/lsgan.py)
@@ -111,6 +111,7 @@ def _load():
         "cgl_gan_launch_count": (ci, [vp, ci]),
         "cgl_gan_launch_info": (ci, [vp, ci, ci, P(ci), P(cd), P(ci)]),
         "cgl_gan_launch_one": (ci, [vp, ci, ci, vp]),
+        "cgl_gan_profile": (ci, [vp, ci, vp, P(ctypes.c_float), ci]),
         "cgl_linear_fwd": (ci, [vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, i64, vp]),
         "cgl_linear_bwd_data": (ci, [vp, vp, vp, ci, ci, ci, vp, i64, vp]),
         "cgl_linear_bwd_weight": (ci, [vp, vp, vp, vp, ci, ci, ci, vp, i64, vp]),

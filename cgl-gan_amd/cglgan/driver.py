@@ -267,8 +267,10 @@ class Driver:
                                        cloud_scope=scope, segema=cfg.segema, cloud_due=due, server_rank=topo.server)
         self.lambda_list = []
         self.round = 0
-        if cfg.resume_dir and os.path.exists(self.resume_path()):
-            self.load_resume()
+        if cfg.resume_dir:
+            if os.path.exists(self.resume_path()):
+                self.load_resume()
+            self._check_resumed_round()
 
     def run(self, rounds: int = None, log=print):
         """``rounds`` communication rounds (default: num_communication), as Server.run's
@@ -300,15 +302,31 @@ class Driver:
     def resume_path(self):
         return os.path.join(self.cfg.resume_dir, f"resume-{self.cfg.algo}-rank{self.rank}.pt")
 
+    # every knob that changes the trajectory or the schedule of a run: a file saved under other settings
+    # is refused instead of continuing a different run
+    RESUME_KEYS = ("algo", "num_workers", "num_servers", "epoch", "batch_size", "num_communication", "cloud_epoch",
+                   "segema", "iid", "num_class", "num_sample", "b1", "b2", "lr_g", "lr_d", "seed", "img_size",
+                   "weighting", "share_every", "swap_every", "fedavg_compat_noop", "dataset_rows", "data_seed",
+                   "gemm_dtype", "loss_scale")
+
     def _resume_key(self):
         c = self.cfg
-        return json.dumps({k: getattr(c, k) for k in ("algo", "num_workers", "num_servers", "epoch", "batch_size",
-                                                      "iid", "seed", "img_size", "gemm_dtype")}, sort_keys=True)
+        return json.dumps({k: getattr(c, k) for k in self.RESUME_KEYS}, sort_keys=True)
+
+    def _rng_states(self):
+        """The exchange's host-side generators (the MD-GAN D-swap's Random(server + 100)) as plain lists
+        (weights_only-loadable): a resumed run draws the permutations the uninterrupted run would."""
+        ds = getattr(self.exchange, "dswap", None)
+        if ds is None:
+            return None
+        ver, ints, gauss = ds.rd.getstate()
+        return [int(ver), [int(x) for x in ints], gauss]
 
     def save_resume(self):
         from .checkpoint import save_resume
         return save_resume(self.step, self.resume_path(), round=self.round, rank=self.rank,
-                           config=self._resume_key(), lambda_list=[float(x) for x in self.lambda_list if x is not None])
+                           config=self._resume_key(), lambda_list=[float(x) for x in self.lambda_list if x is not None],
+                           dswap_state=self._rng_states())
 
     def load_resume(self):
         from .checkpoint import load_resume
@@ -317,6 +335,26 @@ class Driver:
             raise ValueError(f"{self.resume_path()}: saved by a different configuration or rank")
         self.round = int(meta["round"])
         self.lambda_list = list(meta.get("lambda_list", []))
+        ds = getattr(self.exchange, "dswap", None)
+        saved = meta.get("dswap_state")
+        if (ds is None) != (saved is None):
+            raise ValueError(f"{self.resume_path()}: D-swap generator state does not match this run")
+        if ds is not None:
+            ds.rd.setstate((int(saved[0]), tuple(int(x) for x in saved[1]), saved[2]))
+
+    def _check_resumed_round(self):
+        """Every rank must continue from the same round (a crash between two ranks' file replacements
+        leaves files of different rounds; the collectives would then pair different rounds or hang):
+        min and max of the resumed round over the world must agree."""
+        if self.world == 1 or not (dist.is_available() and dist.is_initialized()):
+            return
+        dev = self.step.g_params.device if dist.get_backend() == "nccl" else torch.device("cpu")
+        t = torch.tensor([self.round, -self.round], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        hi, lo = int(t[0]), -int(t[1])
+        if hi != lo:
+            raise RuntimeError(f"rank {self.rank}: resume files of different rounds across the world "
+                               f"(min {lo}, max {hi}) in {self.cfg.resume_dir}")
 
     def save(self, directory):
         """capgan.py:185-200: the server's generator state dict + its config pickle."""

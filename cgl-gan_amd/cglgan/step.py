@@ -316,6 +316,16 @@ class GanStep:
     def launch_one(self, idx, phase=C.PHASE_ALL):
         C.check(C.lib.cgl_gan_launch_one(self._h, phase, idx, _stream()), "cgl_gan_launch_one")
 
+    def profile_round(self, phase=C.PHASE_ALL):
+        """One round (or phase) issued launch by launch with a start / stop event pair on every dispatch:
+        [device microseconds of launch i] in plan order, measured in the round's own data state (each
+        launch's inputs were just written by its producer, as in a replayed round).  Advances the training
+        state like ``run``."""
+        n = C.lib.cgl_gan_launch_count(self._h, phase)
+        buf = (ctypes.c_float * max(n, 1))()
+        C.check(C.lib.cgl_gan_profile(self._h, phase, _stream(), buf, n), "cgl_gan_profile")
+        return [float(buf[i]) for i in range(n)]
+
     def close(self):
         if getattr(self, "_h", None):
             C.lib.cgl_gan_destroy(self._h)

@@ -1085,6 +1085,33 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
 #undef CGL_BODY
 }
 
+// One problem whose descriptor travels in the kernel arguments (the single-op entry points cgl_linear_*):
+// nothing is uploaded before the launch, so the ops need no host synchronisation and can be captured into
+// a graph.  fp32, no split-K, no operand transform, no deferred head.
+template <int TM, int TN>
+__global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32_arg(const CglGemmDesc desc) {
+  extern __shared__ float cgl_dyn_lds[];
+  __shared__ int s_flag[1];
+  __shared__ double s_bnd[4 * TN * 32 * 2];
+  const CglGemmDesc* __restrict__ d = &desc;
+  const int bid = blockIdx.x;
+  const int vec = d->a_vec && d->b_vec;
+#define CGL_BODY_ARG(L)                                                                             \
+  do {                                                                                              \
+    if (vec)                                                                                        \
+      cgl_gemm_body<L, 1, TM, TN, false, CGL_DTYPE_F32, 0>(d, bid, cgl_dyn_lds, s_flag, s_bnd);     \
+    else                                                                                            \
+      cgl_gemm_body<L, 0, TM, TN, false, CGL_DTYPE_F32, 0>(d, bid, cgl_dyn_lds, s_flag, s_bnd);     \
+  } while (0)
+  if (d->layout == 0)
+    CGL_BODY_ARG(0);
+  else if (d->layout == 1)
+    CGL_BODY_ARG(1);
+  else
+    CGL_BODY_ARG(2);
+#undef CGL_BODY_ARG
+}
+
 // Host helpers: the LDS tables of a problem's operand transform, its dynamic LDS bytes, its
 // workgroups, and the split-K partial floats it needs.
 inline int cgl_gemm_tab_floats(const CglGemmDesc& d) {

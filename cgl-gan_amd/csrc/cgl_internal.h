@@ -227,6 +227,9 @@ struct CglBnBwdDesc {
   float* dZ_pk;                   // the same in the fragment-packed layout P(dZ; M, F), or null
   float* g_gamma; float* g_beta;
   float slope;
+  // dynamic loss scaling: a non-finite dgamma / dbeta raises *inf_flag (the model's found word, as the
+  // 16-bit GEMM weight-gradient epilogues do for W / b), so GradScaler's check covers every gradient
+  unsigned int* inf_flag;
 };
 
 #define CGL_MAX_EPOCH 8

@@ -51,6 +51,7 @@ __device__ void cgl_head_finish(const CglHeadDesc* __restrict__ hd, int nwg, flo
 }
 
 #define CGL_HEAD_MAXQ 4   // float4 per lane kept in registers: F <= 1024
+#ifndef CGL_GEMM_PART_TU   // (the GEMM-instantiation translation units compile only device functions)
 __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restrict__ hd) {
   // Each wave owns rows r0 + wave + 4 i; a row is a dot product of F features (F % 4 == 0)
   // over 16-byte loads held in registers, a 64-lane reduction, the loss and its gradient, then
@@ -188,6 +189,7 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
   cgl_head_finish(hd, (int)gridDim.x, s_part);
   if (threadIdx.x == 0) __hip_atomic_store(hd->counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+#endif   // CGL_GEMM_PART_TU
 
 // (cgl_bn_stats: cgl_gemm.hip, shared with the GEMMs that fold the BatchNorm into their loads)
 
@@ -200,6 +202,7 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
 // update the running statistics (momentum, unbiased variance) group by group in the order of the
 // reference's forward calls (Xd then Xg, capgan.py:215-220).
 #define CGL_BNA_ROWS 32
+#ifndef CGL_GEMM_PART_TU   // (the GEMM-instantiation translation units compile only device functions)
 __global__ __launch_bounds__(256) void cgl_bn_apply(const CglBnApplyDesc* __restrict__ ad) {
   __shared__ float s_sc[2][64], s_sh[2][64];
   __shared__ double s_mean[2][64], s_m2[2][64];
@@ -265,6 +268,7 @@ __global__ __launch_bounds__(256) void cgl_bn_apply(const CglBnApplyDesc* __rest
     }
   }
 }
+#endif   // CGL_GEMM_PART_TU
 
 // ------------------------------------------------------------------------------------------
 // BatchNorm1d backward (train) + LeakyReLU' mask.  One workgroup owns 32 features and all M
@@ -275,6 +279,12 @@ __global__ __launch_bounds__(256) void cgl_bn_apply(const CglBnApplyDesc* __rest
 // rows in registers: all loads are issued at once (one memory round trip) and the second pass
 // reuses them; larger M streams the rows twice.
 #define CGL_BNB_RPT 32
+// dgamma / dbeta of feature f, plus the loss-scaling overflow check of those two gradients
+__device__ __forceinline__ void cgl_bnb_store_gb(const CglBnBwdDesc* __restrict__ bd, int f, float dg, float db) {
+  gst(bd->g_gamma + f, dg);
+  gst(bd->g_beta + f, db);
+  if (bd->inf_flag && !(isfinite(dg) && isfinite(db))) atomicOr(bd->inf_flag, 1u);
+}
 // FPW features per workgroup (32: the original layout; 16 / 8 / 4 give 2x / 4x / 8x the workgroups for the narrow
 // layers, each thread then owning fewer rows): NRG = 256 / FPW row groups, rows of a group in registers.
 template <int FPW>
@@ -338,10 +348,7 @@ __device__ __forceinline__ void cgl_bn_bwd_body(const CglBnBwdDesc* __restrict__
           if (bd->dZ_pk) gst(bd->dZ_pk + cgl_pk_off(r, f, kcz), z);   // the input-gradient GEMM's packed A
         }
       }
-      if (rg == 0) {
-        gst(bd->g_gamma + f, (float)(D * (double)invstd));
-        gst(bd->g_beta + f, (float)S);
-      }
+      if (rg == 0) cgl_bnb_store_gb(bd, f, (float)(D * (double)invstd), (float)S);
     }
     return;
   }
@@ -395,16 +402,17 @@ __device__ __forceinline__ void cgl_bn_bwd_body(const CglBnBwdDesc* __restrict__
       }
     }
   }
-  if (rg == 0) {
-    gst(bd->g_gamma + f, (float)(D * (double)invstd));
-    gst(bd->g_beta + f, (float)S);
-  }
+  if (rg == 0) cgl_bnb_store_gb(bd, f, (float)(D * (double)invstd), (float)S);
 }
 
+#ifndef CGL_GEMM_PART_TU   // (the GEMM-instantiation translation units compile only device functions)
 __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict__ bd) { cgl_bn_bwd_body<32>(bd); }
 __global__ __launch_bounds__(256) void cgl_bn_bwd16(const CglBnBwdDesc* __restrict__ bd) { cgl_bn_bwd_body<16>(bd); }
 __global__ __launch_bounds__(256) void cgl_bn_bwd8(const CglBnBwdDesc* __restrict__ bd) { cgl_bn_bwd_body<8>(bd); }
 __global__ __launch_bounds__(256) void cgl_bn_bwd4(const CglBnBwdDesc* __restrict__ bd) { cgl_bn_bwd_body<4>(bd); }
+// the single-op entry point (cgl_bn1d_bwd): the descriptor travels in the kernel arguments
+__global__ __launch_bounds__(256) void cgl_bn_bwd_arg(const CglBnBwdDesc d) { cgl_bn_bwd_body<32>(&d); }
+#endif   // CGL_GEMM_PART_TU
 // ------------------------------------------------------------------------------------------
 // Standalone BatchNorm1d (+ LeakyReLU) forward, train or eval, for the nn.Module path.  One
 // workgroup owns 32 features x all M rows (8 row groups): column sums in double, fixed order;
@@ -415,7 +423,9 @@ __device__ __forceinline__ void cgl_bn1d_apply_row(const CglBn1dDesc* bd, int r,
   gst(bd->Y + (long)r * bd->F + f, y);
 }
 
-__global__ __launch_bounds__(256) void cgl_bn1d_fwd_k(const CglBn1dDesc* __restrict__ bd) {
+#ifndef CGL_GEMM_PART_TU   // (the GEMM-instantiation translation units compile only device functions)
+__global__ __launch_bounds__(256) void cgl_bn1d_fwd_k(const CglBn1dDesc d) {   // descriptor in the kernel arguments
+  const CglBn1dDesc* __restrict__ bd = &d;
   __shared__ double s_a[8][32];
   __shared__ float s_sc[32], s_sh[32];
   const int M = bd->M, F = bd->F;
@@ -525,6 +535,7 @@ __global__ __launch_bounds__(256) void cgl_act_bwd_k(const float* dY, const floa
   }
 }
 
+#endif   // CGL_GEMM_PART_TU
 // ------------------------------------------------------------------------------------------
 struct CglAdamArgs {
   float* p; float* g; float* m; float* v;
@@ -537,6 +548,9 @@ struct CglAdamArgs {
   // *found (a non-finite weight gradient of this model this round) is set
   const float* scale;
   const unsigned int* found;
+  // step_size / bc2sqrt == null: the values themselves, passed in the kernel arguments (cgl_adam_step: no
+  // upload, so the single-op Adam needs no host synchronisation and can be captured)
+  float step_size_v, bc2sqrt_v;
 };
 
 
@@ -607,7 +621,8 @@ __device__ void cgl_round_tail(CglStepState* st) {
 }
 
 __device__ __forceinline__ void cgl_adam_at(const CglAdamArgs& a, CglStepState* st, int tail, long i) {
-  const float ss = gld(a.step_size), bc = gld(a.bc2sqrt);
+  const float ss = a.step_size ? gld(a.step_size) : a.step_size_v;
+  const float bc = a.bc2sqrt ? gld(a.bc2sqrt) : a.bc2sqrt_v;
   if (a.scale) {
     const float inv = (float)(1.0 / (double)gld(a.scale));
     const bool skip = *(const CGL_GLOBAL unsigned int*)a.found != 0u;
@@ -635,9 +650,11 @@ __device__ __forceinline__ void cgl_adam_at(const CglAdamArgs& a, CglStepState* 
   }
 }
 
+#ifndef CGL_GEMM_PART_TU   // (the GEMM-instantiation translation units compile only device functions)
 __global__ __launch_bounds__(256) void cgl_adam(CglAdamArgs a, CglStepState* st, int tail) {
   cgl_adam_at(a, st, tail, (long)blockIdx.x * blockDim.x + threadIdx.x);
 }
+#endif   // CGL_GEMM_PART_TU
 
 // G's first-layer weight gradient fused with the G Adam launch (the round's last two launches as one):
 // workgroups [0, gemm_wgs) run the weight-gradient GEMM (ADAM instantiation: each tile applies Adam to
@@ -735,6 +752,7 @@ __device__ void cgl_begin_at(const CglBeginArgs& a, int r) {
 // ------------------------------------------------------------------------------------------
 // Philox4x32-10 counter-based RNG + Box-Muller: out[i] ~ N(0,1), fresh per round.
 
+#ifndef CGL_GEMM_PART_TU   // (the GEMM-instantiation translation units compile only device functions)
 __global__ __launch_bounds__(256) void cgl_normal(float* out, long n, unsigned long long seed, int round,
                                                   int stream_id) {
   cgl_normal_at((long)blockIdx.x * blockDim.x + threadIdx.x, out, n, seed, (uint32_t)round, stream_id);
@@ -770,3 +788,4 @@ __global__ __launch_bounds__(256) void cgl_scale_inplace(float* x, long n, float
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     x[i] *= a;
 }
+#endif   // CGL_GEMM_PART_TU

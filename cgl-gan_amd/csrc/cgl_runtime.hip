@@ -7,10 +7,18 @@
 // CGLGAN/2DMG/main.py:344-375) -- on ONE device per worker, with G replicated per worker and
 // the reference's queue exchange turned into an all-reduce between phase A and phase B.
 //
-// Unity build: the kernels are compiled in this translation unit.
+// The non-GEMM kernels are compiled in this translation unit, the GEMM kernel instances in cgl_gemm_inst.hip.
 #include "cgl_gemm.hip"
 #include "cgl_kernels.hip"
+#include "cgl_round.h"
 #include "../../include/cglgan.h"
+
+// the GEMM kernels are instantiated in the cgl_gemm_inst.hip translation units (compiled in parallel):
+// declared here so that this unit only launches them
+#define CGL_INST_PREFIX extern template
+#include "cgl_gemm_inst.h"
+
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -244,6 +252,20 @@ struct Launch {
   int abn = 0;              // GEMM operand-transform instantiation (the launch's a_bn)
 };
 
+// Every kernel of a plan is launched through klaunch.  Normally a plain launch; while cgl_gan_profile
+// runs a round, each launch carries a start / stop event pair (hipExtLaunchKernelGGL): the events take
+// the dispatch's own begin / end timestamps -- the interval rocprofv3's kernel trace reports -- so the
+// per-launch durations of a round need no extra barrier packets between the launches.
+thread_local hipEvent_t t_prof_ev[2] = {nullptr, nullptr};
+
+template <typename... KArgs, typename... Args>
+void klaunch(void (*k)(KArgs...), dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, Args... args) {
+  if (t_prof_ev[0])
+    hipExtLaunchKernelGGL(k, grid, block, shmem, s, t_prof_ev[0], t_prof_ev[1], 0u, ((KArgs)args)...);
+  else
+    hipLaunchKernelGGL(k, grid, block, shmem, s, ((KArgs)args)...);
+}
+
 // Split-K partials of 2x2-block waves need up to 48 KB of dynamic LDS (+ the 20 KB operand tables).
 hipError_t gemm_lds_attr() {
   static bool done = false;
@@ -270,13 +292,13 @@ template <int DT>
 void launch_gemm16(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, int n, bool sk) {
   if (sk) {
     if (blk == 2)
-      cgl_gemm_f32<2, 2, true, DT><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+      klaunch(cgl_gemm_f32<2, 2, true, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
     else
-      cgl_gemm_f32<1, 1, true, DT><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+      klaunch(cgl_gemm_f32<1, 1, true, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
   } else if (blk == 2) {
-    cgl_gemm_f32<2, 2, false, DT><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+    klaunch(cgl_gemm_f32<2, 2, false, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
   } else {
-    cgl_gemm_f32<1, 1, false, DT><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+    klaunch(cgl_gemm_f32<1, 1, false, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
   }
 }
 
@@ -284,27 +306,27 @@ void launch_gemm(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc*
                  int dt = CGL_DTYPE_F32, int abn = 0) {
   if (abn == 1) {          // fp32, no split-K (planner)
     if (blk == 2)
-      cgl_gemm_f32<2, 2, false, CGL_DTYPE_F32, 1><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+      klaunch(cgl_gemm_f32<2, 2, false, CGL_DTYPE_F32, 1>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
     else
-      cgl_gemm_f32<1, 1, false, CGL_DTYPE_F32, 1><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+      klaunch(cgl_gemm_f32<1, 1, false, CGL_DTYPE_F32, 1>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
   } else if (abn == 2) {
     if (blk == 2)
-      cgl_gemm_f32<2, 2, false, CGL_DTYPE_F32, 2><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+      klaunch(cgl_gemm_f32<2, 2, false, CGL_DTYPE_F32, 2>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
     else
-      cgl_gemm_f32<1, 1, false, CGL_DTYPE_F32, 2><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+      klaunch(cgl_gemm_f32<1, 1, false, CGL_DTYPE_F32, 2>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
   } else if (dt == CGL_DTYPE_F16) {
     launch_gemm16<CGL_DTYPE_F16>(blk, grid, shmem, s, d, n, sk);
   } else if (dt == CGL_DTYPE_BF16) {
     launch_gemm16<CGL_DTYPE_BF16>(blk, grid, shmem, s, d, n, sk);
   } else if (sk) {   // a launch with a split-K problem: the instantiation carrying the combine
     if (blk == 2)
-      cgl_gemm_f32<2, 2, true><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+      klaunch(cgl_gemm_f32<2, 2, true>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
     else
-      cgl_gemm_f32<1, 1, true><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+      klaunch(cgl_gemm_f32<1, 1, true>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
   } else if (blk == 2) {
-    cgl_gemm_f32<2, 2><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+    klaunch(cgl_gemm_f32<2, 2>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
   } else {
-    cgl_gemm_f32<1, 1><<<grid, CGL_GEMM_THREADS, shmem, s>>>(d, n);
+    klaunch(cgl_gemm_f32<1, 1>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
   }
 }
 
@@ -539,6 +561,39 @@ bool pack_enabled() {
   return v == 1;
 }
 
+// Per-descriptor tile arrangement: the plan's measured table (gemm_tile_pick) and the experiment override
+// CGL_GEMM_TILE_AT="i:WM,WN,WK[,T];..." (i = the descriptor's index in the plan, as CGL_PLAN_DEBUG prints it;
+// read per plan).  Returns true when descriptor i was forced.
+bool gemm_tile_at_env(int i, int* o) {
+  const char* e = getenv("CGL_GEMM_TILE_AT");
+  if (!e) return false;
+  const char* q = e;
+  while (*q) {
+    int di = -1, wm = 0, wn = 0, wk = 0, t = 0, used = 0;
+    const int got = sscanf(q, "%d:%d,%d,%d%n,%d%n", &di, &wm, &wn, &wk, &used, &t, &used);
+    if (got < 4) break;
+    if (di == i && wm * wn * wk == 4) {
+      o[0] = wm;
+      o[1] = wn;
+      o[2] = wk;
+      o[3] = (got == 5 && (t == 1 || t == 2)) ? t : 0;
+      return true;
+    }
+    q += used;
+    while (*q == ';' || *q == ' ') ++q;
+  }
+  return false;
+}
+
+void set_tiles(CglGemmDesc& d, int wm, int wn, int wk, int t) {
+  d.WM = wm;
+  d.WN = wn;
+  d.WK = wk;
+  d.TM = d.TN = t;
+  d.tiles_m = (d.M + 32 * t * wm - 1) / (32 * t * wm);
+  d.tiles_n = (d.N + 32 * t * wn - 1) / (32 * t * wn);
+}
+
 // Add a grouped GEMM launch built from `descs` (workgroup offsets assigned here).
 void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> descs) {
   Launch L;
@@ -556,8 +611,19 @@ void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
       blk = d.TM;
     }
   }
-  for (auto& d : descs)
-    if (d.TM != blk) choose_tiles(d, 0, blk);
+  int forced[CGL_MAX_LAYERS * 4][4];
+  bool isf[CGL_MAX_LAYERS * 4] = {};
+  for (int i = 0; i < (int)descs.size() && i < CGL_MAX_LAYERS * 4; ++i) {
+    isf[i] = gemm_tile_at_env(L.first + i, forced[i]);
+    if (isf[i] && forced[i][3] && descs.size() == 1) blk = forced[i][3];
+  }
+  for (int i = 0; i < (int)descs.size(); ++i) {
+    CglGemmDesc& d = descs[i];
+    if (i < CGL_MAX_LAYERS * 4 && isf[i] && !d.a_bn)
+      set_tiles(d, forced[i][0], forced[i][1], forced[i][2], blk);
+    else if (d.TM != blk)
+      choose_tiles(d, 0, blk);
+  }
   L.dt = c->cfg.gemm_dtype;
   L.blk = blk;
   long kp = 0;
@@ -760,7 +826,11 @@ void fuse_prologue(cgl_gan* c) {
   const Launch& G = A[1];
   if (P.kind != K_PROLOGUE || G.kind != K_GEMM || G.count != 1 || G.sk || G.abn) return;
   CglGemmDesc& d = c->gemm[G.first];
-  if (d.layout != 0 || d.a.p0 != c->bufs.z || d.a.idx0 || d.a.split != 0x7fffffff || d.a_pk || d.ksplit > 1) return;
+  // (b_pk: layer 0's packed weights are written by the prologue's pack blocks, which would run in this same
+  // launch with no ordering against the GEMM tiles reading them -- keep two launches then)
+  if (d.layout != 0 || d.a.p0 != c->bufs.z || d.a.idx0 || d.a.split != 0x7fffffff || d.a_pk || d.b_pk ||
+      d.ksplit > 1)
+    return;
   if (c->cfg.gen_z) {
     if (d.M != 2 * c->cfg.batch || d.K != c->cfg.g.dims[0] || d.a.ld != d.K) return;   // the tiles cover every z row
     d.a_gen = 1;
@@ -1178,6 +1248,7 @@ int build_plan(cgl_gan* c) {
       b.g_gamma = gfold.g_gamma;
       b.g_beta = gfold.g_beta;
       b.slope = sl;
+      if (scaling) b.inf_flag = &st->found[1];
       push_bnb(c, *ph, b);
       gfold_on = false;
       gA = gbuf(l);
@@ -1294,6 +1365,7 @@ int build_plan(cgl_gan* c) {
       b.g_gamma = ggrad(c, l - 1, 2);
       b.g_beta = ggrad(c, l - 1, 3);
       b.slope = sl;
+      if (scaling) b.inf_flag = &st->found[1];
       if (pack_enabled() && l - 1 >= 1) {     // the next input-gradient GEMM reads it packed
         b.dZ_pk = w.gGpk[l - 1];
         gG_packed[l - 1] = true;
@@ -1326,104 +1398,6 @@ int build_plan(cgl_gan* c) {
   return CGL_OK;
 }
 
-// Round prologue: block 0 writes the round's scalars, the next nb_norm blocks draw z, the
-// last blocks draw the real-row indices of this round's local D steps.  Every block reads the
-// completed-round counter, which only the G-Adam tail (a later launch) advances.
-// The round prologue's last blocks pack operands into the GEMMs' fragment layout (CglOpPackJob): thread
-// t of a job writes packed float4 t, i.e. (row block, chunk, half, lane) of P(X; R, K); a transposed
-// source is read along its contiguous rows (the lanes of a block span 32 consecutive r).
-__device__ __forceinline__ void cgl_pack_job(const CglOpPackJob& J, long t) {
-  const int Kc = (J.K + 15) >> 4;
-  const long n4 = (long)((J.R + 31) >> 5) * Kc * 128;
-  if (t >= n4) return;
-  const int l = (int)(t & 63), h = (int)((t >> 6) & 1);
-  const long q = t >> 7;
-  const int c = (int)(q % Kc), rb = (int)(q / Kc);
-  const int r = rb * 32 + (l & 31), k0 = c * 16 + 8 * (l >> 5) + 4 * h;
-  f32x4 v = {0.f, 0.f, 0.f, 0.f};
-  if (r < J.R) {
-    if (J.trans) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (k0 + e < J.K) v[e] = gld(J.src + (long)(k0 + e) * J.ld + r);
-    } else if (k0 + 3 < J.K && ((J.ld | J.K) & 3) == 0) {
-      v = *(gcf4p)(J.src + (long)r * J.ld + k0);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (k0 + e < J.K) v[e] = gld(J.src + (long)r * J.ld + k0 + e);
-    }
-  }
-  *(gf4p)(J.dst + t * 4) = v;
-}
-
-__device__ __forceinline__ void cgl_round_prologue_at(int bid, int nblk, const CglBeginArgs& a, float* z, long nz,
-                                                      unsigned long long zseed, int nb_norm, int* idx, int epoch,
-                                                      int br, int n, unsigned long long sseed, const CglOpPack& pk) {
-  const int done = a.st->round;
-  const int pk0 = nblk - pk.blocks;     // the packing blocks come last
-  if (bid >= pk0) {
-    const int b = bid - pk0;
-    int j = 0;
-    for (int q = 1; q < pk.nj; ++q)
-      if (b >= pk.j[q].blk_begin) j = q;
-    cgl_pack_job(pk.j[j], (long)(b - pk.j[j].blk_begin) * 256 + threadIdx.x);
-    return;
-  }
-  if (bid == 0) {
-    if (threadIdx.x == 0) cgl_begin_at(a, done + 1);
-    return;
-  }
-  if (bid <= nb_norm) {
-    cgl_normal_at((long)(bid - 1) * 256 + threadIdx.x, z, nz, zseed, (uint32_t)(done + 1), 0);
-    return;
-  }
-  // DataLoader(shuffle=True) over the n resident rows (capgan.py:282, 326-331): each pass is a fresh
-  // keyed permutation cut into ceil(n / br) batches, the last one short (n mod br rows); local D step
-  // e of round `done` takes batch done * epoch + e.  Rows past a short batch index a valid dummy row
-  // (no loss, no gradient: the head's n0_dev)
-  const int t = (bid - 1 - nb_norm) * 256 + threadIdx.x;
-  if (t >= epoch * br) return;
-  const int e = t / br, row = t - e * br;
-  const long nb = (n + br - 1) / br;
-  const long bpos = (long)done * epoch + e;
-  const uint32_t pass = (uint32_t)(bpos / nb);
-  const long b = bpos % nb;
-  const long j = b * br + row;
-  idx[t] = (int)cgl_permute((uint32_t)(j < n ? j : n - 1), (uint32_t)n,
-                            (uint32_t)sseed ^ (pass * 0x85ebca6bu + 0x1234567u));
-  if (row == 0) a.st->real_rows[e] = (int)(n - b * br < br ? n - b * br : br);
-}
-
-__global__ __launch_bounds__(256) void cgl_round_prologue(CglBeginArgs a, float* z, long nz, unsigned long long zseed,
-                                                          int nb_norm, int* idx, int epoch, int br, int n,
-                                                          unsigned long long sseed, CglOpPack pk) {
-  cgl_round_prologue_at(blockIdx.x, gridDim.x, a, z, nz, zseed, nb_norm, idx, epoch, br, n, sseed, pk);
-}
-
-// The round prologue fused with G's first GEMM (K_GEMM_PRO, fuse_prologue): workgroups [0, gemm_wgs) run
-// the GEMM, each drawing its own rows of z first (a_gen); the rest run the prologue's other blocks
-// (round scalars, real-batch sampler, operand packing), which nothing in this launch reads.
-template <int TM, int TN>
-__global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_pro(const CglGemmDesc* __restrict__ descs, int gemm_wgs,
-                                                                CglBeginArgs a, float* z, long nz,
-                                                                unsigned long long zseed, int* idx, int epoch, int br,
-                                                                int n, unsigned long long sseed, CglOpPack pk) {
-  extern __shared__ float cgl_dyn_lds[];
-  __shared__ int s_flag[1];
-  __shared__ double s_bnd[4 * TN * 32 * 2];
-  const int bid = blockIdx.x;
-  if (bid >= gemm_wgs) {
-    cgl_round_prologue_at(bid - gemm_wgs, (int)gridDim.x - gemm_wgs, a, z, nz, zseed, 0, idx, epoch, br, n, sseed, pk);
-    return;
-  }
-  const CglGemmDesc* __restrict__ d = descs;
-  if (d->layout != 0) return;     // planner: an NT problem (A = z rows)
-  if (d->a_vec && d->b_vec)
-    cgl_gemm_body<0, 1, TM, TN, false, CGL_DTYPE_F32, 0>(d, bid, cgl_dyn_lds, s_flag, s_bnd);
-  else
-    cgl_gemm_body<0, 0, TM, TN, false, CGL_DTYPE_F32, 0>(d, bid, cgl_dyn_lds, s_flag, s_bnd);
-}
 
 int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = true) {
   hipStream_t s = s_main;
@@ -1439,46 +1413,46 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
       launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, L.count, L.sk, L.dt, L.abn);
       break;
     case K_HEAD:
-      hipLaunchKernelGGL(cgl_head_loss, dim3(L.grid), dim3(256), 0, s, c->ws.head + L.first);
+      klaunch(cgl_head_loss, dim3(L.grid), dim3(256), 0, s, c->ws.head + L.first);
       break;
     case K_BNAPPLY:
-      hipLaunchKernelGGL(cgl_bn_apply, dim3(L.grid, L.grid_y), dim3(256), 0, s, c->ws.bna + L.first);
+      klaunch(cgl_bn_apply, dim3(L.grid, L.grid_y), dim3(256), 0, s, c->ws.bna + L.first);
       break;
     case K_BNBWD:
       if (L.blk == 16)
-        hipLaunchKernelGGL(cgl_bn_bwd16, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
+        klaunch(cgl_bn_bwd16, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
       else if (L.blk == 8)
-        hipLaunchKernelGGL(cgl_bn_bwd8, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
+        klaunch(cgl_bn_bwd8, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
       else if (L.blk == 4)
-        hipLaunchKernelGGL(cgl_bn_bwd4, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
+        klaunch(cgl_bn_bwd4, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
       else
-        hipLaunchKernelGGL(cgl_bn_bwd, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
+        klaunch(cgl_bn_bwd, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
       break;
     case K_ADAM:
-      hipLaunchKernelGGL(cgl_adam, dim3(L.grid), dim3(256), 0, s, L.adam, c->ws.st, L.tail);
+      klaunch(cgl_adam, dim3(L.grid), dim3(256), 0, s, L.adam, c->ws.st, L.tail);
       break;
     case K_GEMM_PRO:       // grid_y = the GEMM's workgroups (fuse_prologue)
       if (L.blk == 2)
-        cgl_gemm_pro<2, 2><<<L.grid, CGL_GEMM_THREADS, L.shmem, s>>>(c->ws.gemm + L.first, L.grid_y, L.begin, L.nptr,
+        klaunch(cgl_gemm_pro<2, 2>, dim3(L.grid), dim3(CGL_GEMM_THREADS), L.shmem, s, c->ws.gemm + L.first, L.grid_y, L.begin, L.nptr,
                                                                       L.nn, c->cfg.seed, c->ws.idx, c->cfg.epoch,
                                                                       c->cfg.batch_real, c->cfg.sample_n,
                                                                       c->cfg.seed ^ 0x5bd1e995ULL, c->pack);
       else
-        cgl_gemm_pro<1, 1><<<L.grid, CGL_GEMM_THREADS, L.shmem, s>>>(c->ws.gemm + L.first, L.grid_y, L.begin, L.nptr,
+        klaunch(cgl_gemm_pro<1, 1>, dim3(L.grid), dim3(CGL_GEMM_THREADS), L.shmem, s, c->ws.gemm + L.first, L.grid_y, L.begin, L.nptr,
                                                                       L.nn, c->cfg.seed, c->ws.idx, c->cfg.epoch,
                                                                       c->cfg.batch_real, c->cfg.sample_n,
                                                                       c->cfg.seed ^ 0x5bd1e995ULL, c->pack);
       break;
     case K_GEMM_ADAM:      // grid_y = the GEMM's workgroups (fuse_wgrad_adam)
       if (L.blk == 2)
-        cgl_gemm_adam<2, 2><<<L.grid, CGL_GEMM_THREADS, L.shmem, s>>>(c->ws.gemm + L.first, L.count, L.grid_y, L.adam,
+        klaunch(cgl_gemm_adam<2, 2>, dim3(L.grid), dim3(CGL_GEMM_THREADS), L.shmem, s, c->ws.gemm + L.first, L.count, L.grid_y, L.adam,
                                                                        c->ws.st, L.tail);
       else
-        cgl_gemm_adam<1, 1><<<L.grid, CGL_GEMM_THREADS, L.shmem, s>>>(c->ws.gemm + L.first, L.count, L.grid_y, L.adam,
+        klaunch(cgl_gemm_adam<1, 1>, dim3(L.grid), dim3(CGL_GEMM_THREADS), L.shmem, s, c->ws.gemm + L.first, L.count, L.grid_y, L.adam,
                                                                        c->ws.st, L.tail);
       break;
     case K_PROLOGUE:
-      hipLaunchKernelGGL(cgl_round_prologue, dim3(L.grid), dim3(256), 0, s, L.begin, L.nptr, L.nn, c->cfg.seed,
+      klaunch(cgl_round_prologue, dim3(L.grid), dim3(256), 0, s, L.begin, L.nptr, L.nn, c->cfg.seed,
                          L.nb_norm, c->ws.idx, c->cfg.epoch, c->cfg.batch_real, c->cfg.sample_n,
                          c->cfg.seed ^ 0x5bd1e995ULL, c->pack);
       break;
@@ -1513,6 +1487,8 @@ int run_phase(cgl_gan* c, int phase, hipStream_t s) {
 }  // namespace
 
 // ==========================================================================================
+static const std::vector<Launch>* phase_list(cgl_gan* c, int phase, int idx, int* local);
+
 extern "C" {
 
 const char* cgl_version(void) { return CGL_VERSION_STR; }
@@ -1671,6 +1647,34 @@ int cgl_gan_run_graph(cgl_gan* c, int phase, void* stream) {
   }
   HIPCHK(hipGraphLaunch(c->gexec[phase], s));
   return CGL_OK;
+}
+
+int cgl_gan_profile(cgl_gan* c, int phase, void* stream, float* us, int n) {
+  if (!c || phase < 0 || phase > 2 || !us) return CGL_E_ARG;
+  const int nl = cgl_gan_launch_count(c, phase);
+  if (n < nl) return CGL_E_SIZE;
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<hipEvent_t> ev(2 * nl, nullptr);
+  int rc = 0;
+  for (auto& e : ev)
+    if (!rc) rc = (int)hipEventCreate(&e);
+  for (int i = 0; i < nl && !rc; ++i) {
+    int li;
+    const std::vector<Launch>* v = phase_list(c, phase, i, &li);
+    t_prof_ev[0] = ev[2 * i];
+    t_prof_ev[1] = ev[2 * i + 1];
+    rc = exec_launch(c, (*v)[li], s);
+    t_prof_ev[0] = t_prof_ev[1] = nullptr;
+  }
+  if (!rc) rc = (int)hipStreamSynchronize(s);
+  for (int i = 0; i < nl && !rc; ++i) {
+    float ms = 0.f;
+    rc = (int)hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]);
+    us[i] = ms * 1e3f;
+  }
+  for (auto& e : ev)
+    if (e) (void)hipEventDestroy(e);
+  return rc;
 }
 
 int cgl_gan_alpha_scale(cgl_gan* c, void* stream) {
@@ -1838,19 +1842,20 @@ int cgl_gan_launch_one(cgl_gan* c, int phase, int idx, void* stream) {
 // ---------------- single ops -------------------------------------------------------------
 int64_t cgl_op_workspace_bytes(void) { return 1 << 16; }   // descriptor + BN scratch (F <= 8000)
 
-static int single_gemm(CglGemmDesc& d, void* ws, int64_t wsb, hipStream_t s) {
-  if (!ws || wsb < (int64_t)sizeof(CglGemmDesc) || !al16(ws)) return CGL_E_ARG;
+// One Linear GEMM with its descriptor in the kernel arguments (cgl_gemm_f32_arg): no upload, no host
+// synchronisation -- stream-ordered like any torch op, and capturable into a graph.  (The workspace
+// arguments of the cgl_linear_* entry points are kept for ABI stability and no longer used.)
+static int single_gemm(CglGemmDesc& d, void*, int64_t, hipStream_t s) {
   HIPCHK(gemm_lds_attr());
   d.wg_begin = 0;
   set_vec(d);
-  HIPCHK(hipMemcpyAsync(ws, &d, sizeof(d), hipMemcpyHostToDevice, s));
   d.ksplit = 1;
-  launch_gemm(d.TM, cgl_gemm_wgs(d), cgl_gemm_stage_bytes(d), s, (const CglGemmDesc*)ws, 1);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
-  // the descriptor lives in the caller's workspace: keep it alive until the kernel has read it
-  HIPCHK(hipStreamSynchronize(s));
-  return 0;
+  const int grid = cgl_gemm_wgs(d), shmem = cgl_gemm_stage_bytes(d);
+  if (d.TM == 2)
+    klaunch(cgl_gemm_f32_arg<2, 2>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d);
+  else
+    klaunch(cgl_gemm_f32_arg<1, 1>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d);
+  return (int)hipGetLastError();
 }
 
 int cgl_linear_fwd(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, int act,
@@ -1980,19 +1985,17 @@ int cgl_bn1d_fwd(const float* X, int M, int F, int ldx, const float* gamma, cons
   if (train && M < 2) return CGL_E_ARG;   // torch: "Expected more than 1 value per channel when training"
   if ((running_mean == nullptr) != (running_var == nullptr)) return CGL_E_ARG;
   if ((save_mean == nullptr) != (save_invstd == nullptr)) return CGL_E_ARG;
-  if (!ws || wsb < (int64_t)sizeof(CglBn1dDesc) || !al16(ws)) return CGL_E_ARG;
+  (void)ws;
+  (void)wsb;
   hipStream_t s = (hipStream_t)stream;
   CglBn1dDesc d;
   std::memset(&d, 0, sizeof(d));
   d.M = M; d.F = F; d.ldx = ldx; d.train = train; d.act = act;
   d.X = X; d.Y = Y; d.gamma = gamma; d.beta = beta; d.eps = eps; d.momentum = momentum; d.slope = slope;
   d.run_mean = running_mean; d.run_var = running_var; d.save_mean = save_mean; d.save_invstd = save_invstd;
-  HIPCHK(hipMemcpyAsync(ws, &d, sizeof(d), hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(cgl_bn1d_fwd_k, dim3((F + 31) / 32), dim3(256), 0, s, (const CglBn1dDesc*)ws);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
-  HIPCHK(hipStreamSynchronize(s));   // the descriptor lives in the caller's workspace
-  return 0;
+  // the descriptor travels in the kernel arguments: no upload, no host synchronisation
+  hipLaunchKernelGGL(cgl_bn1d_fwd_k, dim3((F + 31) / 32), dim3(256), 0, s, d);
+  return (int)hipGetLastError();
 }
 
 int cgl_bn1d_bwd(const float* dY, const float* Y, const float* X, int M, int F, const float* save_mean,
@@ -2000,11 +2003,10 @@ int cgl_bn1d_bwd(const float* dY, const float* Y, const float* X, int M, int F, 
                  float* dbeta, void* ws, int64_t wsb, void* stream) {
   if (!dY || !X || !save_mean || !save_invstd || !gamma || !dX || M < 1 || F < 1) return CGL_E_ARG;
   if ((act != 0 && act != 1) || (act == 1 && !Y)) return CGL_E_ARG;
-  if (!ws || wsb < (int64_t)sizeof(CglBnBwdDesc) + 2 * 4 * (int64_t)F || !al16(ws)) return CGL_E_ARG;
-  hipStream_t s = (hipStream_t)stream;
   // gamma / beta grads land in the workspace when the caller does not want them
-  float* scratch = (float*)((char*)ws + ((sizeof(CglBnBwdDesc) + 255) & ~size_t(255)));
-  if (wsb < (int64_t)((sizeof(CglBnBwdDesc) + 255) & ~size_t(255)) + 2 * 4 * (int64_t)F) return CGL_E_ARG;
+  if ((!dgamma || !dbeta) && (!ws || wsb < 2 * 4 * (int64_t)F || !al16(ws))) return CGL_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  float* scratch = (float*)ws;
   CglBnBwdDesc b;
   std::memset(&b, 0, sizeof(b));
   b.M = M; b.F = F;
@@ -2016,24 +2018,19 @@ int cgl_bn1d_bwd(const float* dY, const float* Y, const float* X, int M, int F, 
   b.g_gamma = dgamma ? dgamma : scratch;
   b.g_beta = dbeta ? dbeta : scratch + F;
   b.slope = slope;
-  HIPCHK(hipMemcpyAsync(ws, &b, sizeof(b), hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(cgl_bn_bwd, dim3((F + 31) / 32), dim3(256), 0, s, (const CglBnBwdDesc*)ws);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
-  HIPCHK(hipStreamSynchronize(s));
-  return 0;
+  // the descriptor travels in the kernel arguments: no upload, no host synchronisation
+  hipLaunchKernelGGL(cgl_bn_bwd_arg, dim3((F + 31) / 32), dim3(256), 0, s, b);
+  return (int)hipGetLastError();
 }
 
 int cgl_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int step, double lr, double beta1,
                   double beta2, double eps, void* ws, int64_t wsb, void* stream) {
-  if (!p || !g || !m || !v || n < 0 || step < 1 || !ws || wsb < 8) return CGL_E_ARG;
+  if (!p || !g || !m || !v || n < 0 || step < 1) return CGL_E_ARG;
+  (void)ws;
+  (void)wsb;
   hipStream_t s = (hipStream_t)stream;
-  float sc[2];
   const double bc1 = 1.0 - std::pow(beta1, (double)step);
   const double bc2 = 1.0 - std::pow(beta2, (double)step);
-  sc[0] = (float)(lr / bc1);
-  sc[1] = (float)std::pow(bc2, 0.5);
-  HIPCHK(hipMemcpyAsync(ws, sc, sizeof(sc), hipMemcpyHostToDevice, s));
   CglAdamArgs a;
   std::memset(&a, 0, sizeof(a));
   a.p = p;
@@ -2041,18 +2038,17 @@ int cgl_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int s
   a.m = m;
   a.v = v;
   a.n = (long)n;
-  a.step_size = (const float*)ws;
-  a.bc2sqrt = (const float*)ws + 1;
+  a.step_size = nullptr;            // the step scalars travel in the kernel arguments (no upload)
+  a.bc2sqrt = nullptr;
+  a.step_size_v = (float)(lr / bc1);
+  a.bc2sqrt_v = (float)std::pow(bc2, 0.5);
   a.b2 = (float)beta2;
   a.w1 = (float)(1.0 - beta1);
   a.w2 = (float)(1.0 - beta2);
   a.eps = (float)eps;
   if (n > 0)
     hipLaunchKernelGGL(cgl_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, (CglStepState*)nullptr, 0);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
-  HIPCHK(hipStreamSynchronize(s));
-  return 0;
+  return (int)hipGetLastError();
 }
 
 int cgl_normal_fill(float* out, int64_t n, unsigned long long seed, int round, int stream_id, void* stream) {

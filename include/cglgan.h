@@ -170,8 +170,18 @@ int cgl_gan_plan_info(cgl_gan* ctx, int phase, int* n_launches, int* n_gemm_laun
 int cgl_gan_launch_count(cgl_gan* ctx, int phase);
 int cgl_gan_launch_info(cgl_gan* ctx, int phase, int idx, int* kind, double* flops, int* grid);
 int cgl_gan_launch_one(cgl_gan* ctx, int phase, int idx, void* stream);
+/* One round (or phase) issued launch by launch, each launch carrying its own start / stop event pair
+ * (the dispatch's begin / end timestamps, the interval rocprofv3's kernel trace reports): us[i] = the
+ * device duration of launch i of the phase, in the round's own order and data state (n must be >=
+ * cgl_gan_launch_count).  Returns 0 or a negative / HIP error code.  The round
+ * advances the training state exactly as cgl_gan_run does. */
+int cgl_gan_profile(cgl_gan* ctx, int phase, void* stream, float* us, int n);
 
 /* ---------------- single ops (nn.Module boundary: model/mnist_model.py) ---------------- */
+/* Every single op is stream-ordered and asynchronous: its descriptor travels in the kernel arguments
+ * (nothing is uploaded, the host never waits), so a sequence of them -- a module's forward + backward --
+ * can be captured into a hipGraph / torch.cuda.graph.  The workspace arguments are kept for ABI
+ * stability; only cgl_bn1d_bwd uses its workspace (2 F floats for dgamma / dbeta when those are null). */
 /* Y[M,N] = act(X[M,K] W[N,K]^T + b)   act: 0 none, 1 LeakyReLU(slope), 2 Tanh, 3 Sigmoid
  * (nn.Linear + the activation module that follows it: model/mnist_model.py:11-14,22-23,77-81,
  * MDGAN/MNIST/mnist_model.py:41-42) */

@@ -1,9 +1,14 @@
-"""Resume (new; the reference only saves its generator, capgan.py:185-200): a CAPGAN run of
-two workers over gloo interrupted after 2 rounds and resumed from the per-worker resume files (a NEW
+"""Resume (new; the reference only saves its generator, capgan.py:185-200): a run of two
+workers over gloo interrupted after 2 rounds and resumed from the per-worker resume files (a NEW
 Driver, as a restarted process would build it) ends bitwise where the uninterrupted 4-round run ends --
-G, G running statistics, D, and lambda -- on the CPU stand-in step (tests/dist_oracle_step.py)."""
+G, G running statistics, D, and lambda -- on the CPU stand-in step (tests/dist_oracle_step.py).
+Cases: CAPGAN with the E-share every round, and MD-GAN with the D-swap every round (the swap
+permutations come from the server's Random(server + 100), whose state travels in the resume file).
+Ranks whose resume files hold different rounds refuse to start."""
 import os
 import tempfile
+
+import pytest
 
 import torch
 import torch.distributed as dist
@@ -12,9 +17,10 @@ import torch.multiprocessing as mp
 from test_driver_gloo import _cfg, _free_port
 
 KW = dict(algo="capgan", num_workers=2, num_servers=1, share_every=1)
+KW_SWAP = dict(algo="mdgan", num_workers=2, num_servers=1, swap_every=1)
 
 
-def _proc(rank, world, port, outdir, mode):
+def _proc(rank, world, port, outdir, mode, kw=KW):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(1)
@@ -23,15 +29,18 @@ def _proc(rank, world, port, outdir, mode):
         from cglgan.driver import Driver
         from dist_oracle_step import oracle_step_factory
         if mode == "straight":
-            drv = Driver(_cfg(**KW), step_factory=oracle_step_factory, device="cpu")
+            drv = Driver(_cfg(**kw), step_factory=oracle_step_factory, device="cpu")
             drv.run(4, log=None)
         else:
             rd = os.path.join(outdir, "resume")
-            first = Driver(_cfg(resume_dir=rd, **KW), step_factory=oracle_step_factory, device="cpu")
+            first = Driver(_cfg(resume_dir=rd, **kw), step_factory=oracle_step_factory, device="cpu")
             assert first.round == 0
-            first.run(2, log=None)                      # writes resume-capgan-rank{r}.pt at the end
+            first.run(2, log=None)                      # writes resume-<algo>-rank{r}.pt at the end
             del first
-            drv = Driver(_cfg(resume_dir=rd, **KW), step_factory=oracle_step_factory, device="cpu")
+            if mode == "torn" and rank == 1:            # a crash before rank 1 replaced its file
+                os.remove(os.path.join(rd, f"resume-{kw['algo']}-rank1.pt"))
+            dist.barrier()
+            drv = Driver(_cfg(resume_dir=rd, **kw), step_factory=oracle_step_factory, device="cpu")
             assert drv.round == 2 and drv.step.round == 2
             drv.run(2, log=None)
         s = drv.step
@@ -41,17 +50,36 @@ def _proc(rank, world, port, outdir, mode):
         dist.destroy_process_group()
 
 
-def test_capgan_resume_bitwise_world2():
+@pytest.mark.parametrize("kw", [KW, KW_SWAP], ids=["capgan-eshare", "mdgan-dswap"])
+def test_resume_bitwise_world2(kw):
     with tempfile.TemporaryDirectory() as td:
         for mode in ("straight", "resumed"):
-            mp.spawn(_proc, args=(2, _free_port(), td, mode), nprocs=2, join=True)
+            mp.spawn(_proc, args=(2, _free_port(), td, mode, kw), nprocs=2, join=True)
         for r in range(2):
             a = torch.load(os.path.join(td, f"straight{r}.pt"), weights_only=True)
             b = torch.load(os.path.join(td, f"resumed{r}.pt"), weights_only=True)
             assert a["round"] == b["round"] == 4
             for k in ("g", "r", "d", "lam"):
                 assert torch.equal(a[k], b[k]), (r, k)
-        assert os.path.exists(os.path.join(td, "resume", "resume-capgan-rank1.pt"))
+        assert os.path.exists(os.path.join(td, "resume", f"resume-{kw['algo']}-rank1.pt"))
+
+
+def test_dswap_resume_changes_nothing_but_the_generator():
+    """Without the saved generator state the resumed MD-GAN run would restart the permutation sequence:
+    the 4 permutations of an uninterrupted run differ from 2 + 2 restarted ones (so the case above
+    really exercises the saved state)."""
+    from cglgan.exchange import DSwap
+    a = DSwap(2, 0)
+    straight = [a.next_perm() for _ in range(4)]
+    b, c = DSwap(2, 0), DSwap(2, 0)
+    restarted = [b.next_perm() for _ in range(2)] + [c.next_perm() for _ in range(2)]
+    assert straight != restarted
+
+
+def test_resume_rounds_must_agree_world2():
+    with tempfile.TemporaryDirectory() as td:
+        with pytest.raises(Exception, match="different rounds"):
+            mp.spawn(_proc, args=(2, _free_port(), td, "torn", KW), nprocs=2, join=True)
 
 
 def test_resume_file_roundtrip(tmp_path):
