@@ -54,7 +54,8 @@ def args_():
     p.add_argument("--eager", action="store_true", help="launch without hipGraph")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
-    p.add_argument("--profile-reps", type=int, default=20, help="back-to-back replays per launch when timing launches")
+    p.add_argument("--profile-rounds", type=int, default=10,
+                   help="rounds issued launch by launch with per-dispatch events (in-round launch durations)")
     p.add_argument("--model", choices=["mlp", "lsgan", "mixg", "mdgan", "ring"], default="mlp",
                    help="mlp: model/mnist_model.py CAPGAN round (BASELINE configs[1] at N=1, configs[2] at N>1, "
                         "the default workload); mixg: configs[3], Mix-G through cglgan.driver (num_servers=2 when N "
@@ -92,36 +93,44 @@ def make_exchange(step, world, a):
     return WorkerExchange(step, DistComm() if world > 1 else None, share_every=a.E if world > 1 else 0)
 
 
-def profile_launches(step, world, reps):
-    """Device time per launch of the round's plan: each launch is replayed `reps` times
-    back-to-back between two HIP events on the launch stream (the launches are idempotent up to
-    optimizer state, and this runs after the timed region), so the figure is the kernel's own
-    duration plus the back-to-back dispatch gap -- the quantity rocprofv3's kernel trace
-    reports as its average duration."""
+def profile_inround(step, world, rounds, ex=None):
+    """Device time per launch of the round's plan, measured IN the round: ``rounds`` extra rounds issued
+    launch by launch, every dispatch carrying its own start / stop event pair (cgl_gan_profile: the
+    dispatch's begin / end timestamps, the interval rocprofv3's kernel trace reports), each launch
+    reading the operands its producer has just written -- the timed rounds' data state.  Returns the
+    median over rounds per launch (this runs after the timed region; the rounds advance the state).
+    N > 1: phase A and phase B around this rank's collectives, as WorkerExchange.round issues them."""
     from cglgan._lib import PHASE_A, PHASE_ALL, PHASE_B
-    phases = [PHASE_ALL] if world == 1 else [PHASE_A, PHASE_B]
+    split = ex is not None and ex.comm is not None and ex.comm.size > 1
+    phases = [PHASE_A, PHASE_B] if split else [PHASE_ALL]
+    info = []
+    for ph in phases:
+        info += step.launches(ph)
+    runs = []
+    for _ in range(rounds):
+        if not split:
+            runs.append(step.profile_round(PHASE_ALL))
+        else:
+            a = step.profile_round(PHASE_A)
+            ex.comm.all_gather(step.losses_all, step.own_loss())
+            step.alpha_scale()
+            ex.comm.all_reduce_sum(step.exchange_buffer())
+            runs.append(a + step.profile_round(PHASE_B))
+    med = [sorted(col)[len(col) // 2] for col in zip(*runs)]
     per_kind = {}
     gemm_us, gemm_flops, gemm_n = [], 0.0, 0
-    s = torch.cuda.current_stream()
-    for ph in phases:
-        info = step.launches(ph)
-        for i, (kind, flops, grid) in enumerate(info):
-            step.launch_one(i, ph)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(s)
-            for _ in range(reps):
-                step.launch_one(i, ph)
-            e1.record(s)
-            e1.synchronize()
-            us = e0.elapsed_time(e1) * 1e3 / reps
-            k = per_kind.setdefault(kind, [0.0, 0])
-            k[0] += us
-            k[1] += 1
-            if kind == "gemm":
-                gemm_us.append(us)
-                gemm_flops += flops
-                gemm_n += 1
-    return per_kind, gemm_us, gemm_flops, gemm_n
+    for (kind, flops, grid), us in zip(info, med):
+        k = per_kind.setdefault(kind, [0.0, 0])
+        k[0] += us
+        k[1] += 1
+        if kind == "gemm":
+            gemm_us.append(us)
+            gemm_flops += flops
+            gemm_n += 1
+    launches = [{"kind": kind, "grid": grid, "gflop": round(flops / 1e9, 4), "us": round(us, 2),
+                 "tflops": round(flops / (us * 1e-6) / 1e12, 2) if flops else None}
+                for (kind, flops, grid), us in zip(info, med)]
+    return per_kind, gemm_us, gemm_flops, gemm_n, launches
 
 
 def _latest_profile(names):
@@ -194,11 +203,26 @@ def cpu_threads():
     return max(1, min(16, n))
 
 
-def cpu_baseline(a):
+def cpu_variants(leg):
+    """the CPU baseline at the process's CPU share (``value``; at most 16 threads -- the GPU
+    pool's per-GPU CPU share, OMP_NUM_THREADS there) and at 1 thread (``single_thread``).  The machine's
+    other logical CPUs (``host.host_logical_cpus``) belong to the other GPUs' jobs of a shared node, so a
+    whole-host figure is not taken on this pool."""
+    main = leg(None)
+    if main["cores"] > 1:
+        one = leg(1)
+        main["single_thread"] = {k: one[k] for k in ("value", "unit", "cores", "sample")}
+        main["speedup_vs_1_thread"] = round(main["value"] / one["value"], 2)
+    main["threads_note"] = ("value at the process's CPU share (<= 16 threads, the GPU pool's per-GPU share); "
+                            "single_thread at 1; the host's remaining logical CPUs serve other GPUs' jobs")
+    return main
+
+
+def cpu_baseline(a, threads=None):
     """The CPU oracle (torch-CPU restatement of the reference step) on this host's cores."""
     sys.path.insert(0, ROOT)
     from oracle import gan_oracle as O
-    threads = cpu_threads()
+    threads = threads or cpu_threads()
     torch.set_num_threads(threads)
     G, workers = O.build_capgan(1)
     srv = O.CapganServer(G, torch.tensor([1.0]))
@@ -283,11 +307,11 @@ def profile_conv_round(run_round):
     return out
 
 
-def conv_cpu_baseline(a):
+def conv_cpu_baseline(a, threads=None):
     """The conv oracle (torch-CPU restatement of the model/lsgan.py round) on this host's cores."""
     sys.path.insert(0, ROOT)
     from oracle import conv_oracle as CV
-    threads = cpu_threads()
+    threads = threads or cpu_threads()
     torch.set_num_threads(threads)
     torch.manual_seed(20211212)
     gp, gb = CV.init_params(CV.G_SPEC)
@@ -333,7 +357,7 @@ def main_lsgan(a, world, rank, local):
     stream = torch.cuda.Stream()
     with torch.cuda.stream(stream):
         g = torch.Generator(device="cuda").manual_seed(1000 + rank)
-        rows = (a.rows // a.batch) * a.batch
+        rows = a.rows                # every pass ends with its short batch (60,000 = 234 x 256 + 96)
         data = torch.rand(rows, 1024, device="cuda", generator=g) * 2 - 1
         # one worker per GPU: G replicated (same init and z stream), D and real shard per rank
         # the round replays as one hipGraph at N = 1 (device-side round state, cglgan.conv_step graph mode);
@@ -401,7 +425,7 @@ def main_lsgan(a, world, rank, local):
         "losses": {"d_loss": st["d_loss"], "g_loss": st["g_loss"], "round": st["round"]},
     }
     if world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = conv_cpu_baseline(a)
+        out["cpu_baseline"] = cpu_variants(lambda t: conv_cpu_baseline(a, t))
     print(json.dumps(out), flush=True)
     return out
 
@@ -466,12 +490,12 @@ def parity_vs_cpu(kind, B, rounds=10):
                          "z and real batches every round"}
 
 
-def cpu_rounds(kind, B, seconds):
+def cpu_rounds(kind, B, seconds, threads=None):
     """The CPU oracle's round rate on this host (kind: ring / mdgan / mixg; N = 1)."""
     sys.path.insert(0, ROOT)
     from cglgan.data import gmm
     from oracle import gan_oracle as O
-    threads = cpu_threads()
+    threads = threads or cpu_threads()
     torch.set_num_threads(threads)
     if kind == "ring":
         G, ws = O.build_ring(1, 1)
@@ -528,12 +552,13 @@ def timed_rounds(round_fn, a, world):
     return el
 
 
-def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None, parity_kind=None, extra=None):
-    """The bench line of a fused-round model (mlp / mixg / mdgan / ring): GEMM-family roofline from
-    per-launch HIP-event timing on the launch stream, CPU baseline and CPU parity at N = 1."""
-    per_kind, gemm_us, gemm_flops, gemm_n = profile_launches(step, world, a.profile_reps)
+def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None, parity_kind=None, extra=None,
+                 ex=None):
+    """The bench line of a fused-round model (mlp / mixg / mdgan / ring): GEMM-family roofline from the
+    in-round per-launch device durations (profile_inround), CPU baseline and CPU parity at N = 1."""
+    st = step.stats()           # the timed rounds' end state (the profile rounds below advance it)
+    per_kind, gemm_us, gemm_flops, gemm_n, launches = profile_inround(step, world, a.profile_rounds, ex)
     plan = step.plan_info()
-    st = step.stats()
     ms_step = el / a.steps * 1e3
     value = world * a.batch * a.steps / el
     if rank != 0:
@@ -554,6 +579,8 @@ def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None,
         "roofline": {"bound": "mfma", "kernel": "cgl_gemm_f32 (the round's GEMM launches)",
                      "achieved": round(gemm_tf, 3), "peak": PEAK_F32_MFMA, "unit": "TFLOP/s",
                      "frac": round(gemm_tf / PEAK_F32_MFMA, 4),
+                     "timing": f"median over {a.profile_rounds} rounds of each launch's in-round device duration "
+                               "(dispatch begin / end events on the launch stream, cgl_gan_profile)",
                      "traffic": traffic_per_gemm_launch()[0] if a.model == "mlp" else None,
                      "traffic_unit": "bytes per GEMM launch, all cgl_gemm_f32 instantiations (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                      "traffic_source": traffic_per_gemm_launch()[1] if a.model == "mlp" else None,
@@ -565,7 +592,8 @@ def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None,
                      "step_achieved_tflops": round(step_tf, 3),
                      "step_frac_mfma": round(step_tf / PEAK_F32_MFMA, 4),
                      "per_kind_us_per_round": {k: round(v[0], 2) for k, v in per_kind.items()},
-                     "launches_per_round": plan["launches"]},
+                     "device_us_per_round": round(sum(v[0] for v in per_kind.values()), 2),
+                     "launches_per_round": plan["launches"], "launches": launches},
         "losses": {"d_loss": st["d_loss"][0], "g_loss": st["g_loss"], "lambda": st["lambda"], "round": st["round"]},
     }
     if extra:
@@ -590,7 +618,7 @@ def main_mlp(a, world, rank):
               f"C3: CAPGAN {world} workers (1 per GPU), S=1, lambda-weighted G-gradient all-reduce + E={a.E} D "
               f"all-reduce over RCCL")
         return fused_report(a, world, rank, step, el, wl, {"img": "28x28x1", "dataset_rows_per_worker": a.rows},
-                            cpu_leg=lambda: cpu_baseline(a), parity_kind="capgan")
+                            cpu_leg=lambda: cpu_variants(lambda t: cpu_baseline(a, t)), parity_kind="capgan", ex=ex)
 
 
 def main_driver(a, world, rank, algo):
@@ -599,7 +627,7 @@ def main_driver(a, world, rank, algo):
     from cglgan.driver import Driver, DriverConfig
     S = 2 if (algo == "mixg" and world % 2 == 0) else 1
     cfg = DriverConfig(algo=algo, num_workers=world, num_servers=S, batch_size=a.batch,
-                       num_communication=a.warmup + a.steps + a.profile_reps + 8, cloud_epoch=1,
+                       num_communication=a.warmup + a.steps + a.profile_rounds + 8, cloud_epoch=1,
                        iid=1 if algo == "mdgan" else 0, swap_every=(a.E if (algo == "mdgan" and world > 1) else 0),
                        dataset_rows=max(60000, 8 * a.batch * world), graph=not a.eager)
     stream = torch.cuda.Stream()
@@ -633,8 +661,9 @@ def main_driver(a, world, rank, algo):
                               "<= 0.1-0.35 of their distance to the exact fp64 round)"}
         return fused_report(a, world, rank, drv.step, el, wl,
                             {"img": "28x28x1", "num_servers": S, "shard_rows": int(drv.step.real.shape[0])},
-                            cpu_leg=lambda: cpu_rounds(algo, a.batch, a.cpu_seconds), parity_kind=algo,
-                            extra={"lowp_variant": lowp} if lowp else None)
+                            cpu_leg=lambda: cpu_variants(lambda t: cpu_rounds(algo, a.batch, a.cpu_seconds, t)),
+                            parity_kind=algo,
+                            extra={"lowp_variant": lowp} if lowp else None, ex=drv.exchange)
 
 
 def main_ring(a, world, rank):
@@ -658,7 +687,8 @@ def main_ring(a, world, rank):
         wl = ("C1: CGLGAN/2DMG ring GAN (G 100-32-2, D 2-128-256-1 Sigmoid, BCE, closed-form lambda), 8-mode 2-D "
               "Gaussian mixture, 1 worker per GPU" + (f", {world} workers" if world > 1 else ""))
         return fused_report(a, world, rank, step, el, wl, {"data_points": int(data.shape[0])},
-                            cpu_leg=lambda: cpu_rounds("ring", a.batch, a.cpu_seconds), parity_kind="ring")
+                            cpu_leg=lambda: cpu_variants(lambda t: cpu_rounds("ring", a.batch, a.cpu_seconds, t)),
+                            parity_kind="ring", ex=ex)
 
 
 def main():

@@ -127,8 +127,8 @@ def _load():
         "cgl_conv3x3_bwd_data": (ci, [vp, vp, vp] + [ci] * 7 + [vp, i64, vp]),
         "cgl_conv3x3_bwd_weight": (ci, [vp, vp, vp, vp] + [ci] * 7 + [vp, i64, vp]),
         "cgl_bn2d_workspace_bytes": (i64, [ci] * 4),
-        "cgl_bn2d_fwd": (ci, [vp, ci, ci, ci, ci, vp, vp, cd, cd, vp, vp, ci, ci, cf, vp, vp, vp, vp, i64, vp]),
-        "cgl_bn2d_bwd": (ci, [vp, vp, vp, ci, ci, ci, ci, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, i64, vp]),
+        "cgl_bn2d_fwd": (ci, [vp, ci, ci, ci, ci, vp, vp, cd, cd, vp, vp, ci, ci, cf, vp, vp, vp, vp, vp, i64, vp]),
+        "cgl_bn2d_bwd": (ci, [vp, vp, vp, ci, ci, ci, ci, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, vp, i64, vp]),
         "cgl_act_drop_bwd": (ci, [vp, vp, vp, ci, ci, ci, cf, ci, vp, vp]),
         "cgl_dropout2d_mask": (ci, [vp, ci, ci, cd, ctypes.c_ulonglong, ctypes.c_ulonglong, vp]),
         "cgl_dropout2d_masks": (ci, [ci, P(vp), P(ci), P(ci), cd, ctypes.c_ulonglong, P(ctypes.c_ulonglong), vp]),
@@ -136,7 +136,7 @@ def _load():
         "cgl_dense1_bwd_data_nhwc": (ci, [vp, vp, vp, ci, ci, ci, vp]),
         "cgl_dense1_fwd_nhwc": (ci, [vp, vp, vp, vp, vp, ci, ci, ci, vp]),
         "cgl_nhwc_to_nchw": (ci, [vp, vp, ci, ci, ci, vp]),
-        "cgl_adv_loss": (ci, [vp, ci, ci, ci, ci, cd, vp, vp, vp]),
+        "cgl_adv_loss": (ci, [vp, ci, ci, ci, ci, cd, vp, vp, vp, vp]),
         "cgl_dense_workspace_bytes": (i64, [ci] * 3),
         "cgl_dense_fwd": (ci, [vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, i64, vp]),
         "cgl_dense_bwd_data": (ci, [vp, vp, vp, ci, ci, ci, vp, i64, vp]),
@@ -146,16 +146,17 @@ def _load():
         "cgl_conv3x3_fwd_packed": (ci, [vp, vp, vp, vp] + [ci] * 8 + [cf, vp, vp, i64, vp]),
         "cgl_conv3x3_bwd_data_packed": (ci, [vp, vp, vp, vp] + [ci] * 7 + [vp, i64, vp]),
         "cgl_conv3x3_stat_chunks": (i64, [ci] * 8),
-        "cgl_conv3x3_fwd_packed_stats": (ci, [vp, vp, vp, vp] + [ci] * 8 + [cf, vp, ci, vp, vp, i64, vp]),
-        "cgl_bn2d_fwd_stats": (ci, [vp, ci, vp, ci, ci, ci, ci, vp, vp, cd, cd, vp, vp, ci, cf, vp, vp, vp, vp, vp, i64, vp]),
+        "cgl_conv3x3_fwd_packed_stats": (ci, [vp, vp, vp, vp] + [ci] * 8 + [cf, vp, ci, vp, vp, vp, i64, vp]),
+        "cgl_bn2d_fwd_stats": (ci, [vp, ci, vp, ci, ci, ci, ci, vp, vp, cd, cd, vp, vp, ci, cf, vp, vp, vp, vp, vp, vp, i64,
+                                    vp]),
         "cgl_bn2d_fwd_stats_coef": (ci, [vp, ci, vp, ci, ci, ci, ci, vp, vp, cd, cd, vp, vp, ci, cf, vp, vp, vp, vp, vp, ci,
-                                         vp, i64, vp]),
+                                         vp, vp, i64, vp]),
         "cgl_conv3x3_fwd_packed_bnin": (ci, [vp, vp, vp, vp] + [ci] * 8 + [cf, vp, ci, vp, vp, ci, ci, cf, vp, i64, vp]),
         "cgl_bn2d_stats_scratch_bytes": (i64, [ci, ci]),
         "cgl_linear_desc_bytes": (i64, []),
         "cgl_conv3x3_bwd_stat_chunks": (i64, [ci] * 8),
         "cgl_conv3x3_bwd_data_packed_stats": (ci, [vp, vp, vp] + [ci] * 8 + [vp, vp, vp, vp, cf, vp, i64, vp]),
-        "cgl_bn2d_bwd_stats": (ci, [vp, ci, vp, vp, vp, ci, ci, ci, ci, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, i64, vp]),
+        "cgl_bn2d_bwd_stats": (ci, [vp, ci, vp, vp, vp, ci, ci, ci, ci, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, vp, i64, vp]),
         "cgl_linear_prepare": (ci, [ci, vp, vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, P(LinearLaunch)]),
         "cgl_linear_launch": (ci, [vp, P(LinearLaunch), vp]),
         "cgl_dense_fwd_packed": (ci, [vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, i64, vp]),
@@ -168,7 +169,7 @@ def _load():
         "cgl_normal_fill_dev": (ci, [vp, i64, ctypes.c_ulonglong, vp, ci, vp]),
         "cgl_dropout2d_masks_dev": (ci, [ci, P(vp), P(ci), P(ci), cd, ctypes.c_ulonglong, P(ctypes.c_ulonglong), vp,
                                          ctypes.c_ulonglong, vp]),
-        "cgl_sample_rows_dev": (ci, [vp, ci, ci, ci, ctypes.c_ulonglong, vp, vp, vp]),
+        "cgl_sample_rows_dev": (ci, [vp, ci, ci, ci, ctypes.c_ulonglong, vp, vp, vp, vp]),
         "cgl_counters_add": (ci, [vp, ci, ci, vp]),
         "cgl_version": (ctypes.c_char_p, []),
     }

@@ -98,14 +98,18 @@ def stat_chunks(n, h, wd, cin, cout, stride=1, up=0, groups=1, bwd=False):
 
 
 def conv3x3_fwd(x, w, b, y, n, h, wd, cin, cout, stride=1, up=0, act=ACT_NONE, slope=0.2, drop=None, wp=None,
-                stats=None, bn_in=None):
+                stats=None, bn_in=None, nvalid=None):
     """``wp``: the weights pre-packed by a PackSet (no per-call pack launch); ``w`` is then unused.
     ``stats`` = (part, groups): also write the next BatchNorm2d's {sum, M2} partials per 32-row chunk
     (float64 tensor of stat_chunks(...) * cout * 2) -- consumed by bn2d_fwd_stats.
     ``bn_in`` = (coef, groups, act, slope): ``x`` is the PRE-BatchNorm map; the BatchNorm (+ LeakyReLU)
-    whose scale / shift bn2d_fwd_stats(coef=...) wrote is applied as the operands are loaded (needs ``wp``)."""
+    whose scale / shift bn2d_fwd_stats(coef=...) wrote is applied as the operands are loaded (needs ``wp``).
+    ``nvalid`` (device int32, with ``stats``): the first forward call is a short batch of *nvalid images (the
+    rest padding, left out of the statistics; see bn2d_fwd)."""
     _chk(x, w, b, y, drop, wp)
     ws = workspace(conv_ws_bytes(n, h, wd, cin, cout, stride, up), x.device)
+    if nvalid is not None and (stats is None or bn_in is not None):
+        raise RuntimeError("conv3x3_fwd(nvalid=...): only with stats= and without bn_in=")
     if bn_in is not None:
         coef, groups_in, act_in, slope_in = bn_in
         _chk(coef)
@@ -122,8 +126,8 @@ def conv3x3_fwd(x, w, b, y, n, h, wd, cin, cout, stride=1, up=0, act=ACT_NONE, s
         if wp is None or not part.is_cuda or part.dtype != torch.float64:
             raise RuntimeError("conv3x3_fwd(stats=...): needs packed weights and a float64 CUDA partial buffer")
         C.check(C.lib.cgl_conv3x3_fwd_packed_stats(_p(x), _p(wp), _p(b), _p(y), n, h, wd, cin, cout, stride, up, act,
-                                                   float(slope), _p(drop), int(groups), _p(part), _p(ws), ws.numel(),
-                                                   _s()), "cgl_conv3x3_fwd_packed_stats")
+                                                   float(slope), _p(drop), int(groups), _p(part), _p(nvalid), _p(ws),
+                                                   ws.numel(), _s()), "cgl_conv3x3_fwd_packed_stats")
         return y
     if wp is not None:
         C.check(C.lib.cgl_conv3x3_fwd_packed(_p(x), _p(wp), _p(b), _p(y), n, h, wd, cin, cout, stride, up, act,
@@ -276,12 +280,15 @@ def bn2d_ws_bytes(n, hw, c, groups):
 
 
 def bn2d_fwd(x, n, hw, c, gamma, beta, y, groups=1, eps=0.8, momentum=0.1, running_mean=None, running_var=None,
-             train=True, act=ACT_NONE, slope=0.2, save_mean=None, save_invstd=None):
+             train=True, act=ACT_NONE, slope=0.2, save_mean=None, save_invstd=None, nvalid=None):
+    """``nvalid`` (device int32, may be None): the first of the ``groups`` forward calls is a short batch --
+    only its first *nvalid images are data (the D step's real call on DataLoader's short final batch,
+    capgan.py:282,326-331); its other images are padding, left out of the statistics."""
     _chk(x, gamma, beta, y, running_mean, running_var, save_mean, save_invstd)
     ws = workspace(bn2d_ws_bytes(n, hw, c, groups), x.device)
     C.check(C.lib.cgl_bn2d_fwd(_p(x), n, hw, c, groups, _p(gamma), _p(beta), float(eps), float(momentum),
                                _p(running_mean), _p(running_var), int(train), act, float(slope), _p(y), _p(save_mean),
-                               _p(save_invstd), _p(ws), ws.numel(), _s()), "cgl_bn2d_fwd")
+                               _p(save_invstd), _p(nvalid), _p(ws), ws.numel(), _s()), "cgl_bn2d_fwd")
     return y
 
 
@@ -295,7 +302,7 @@ def bn2d_stats_scratch(c, groups, device):
 
 def bn2d_fwd_stats(part, x, n, hw, c, gamma, beta, y, groups=1, eps=0.8, momentum=0.1, running_mean=None,
                    running_var=None, act=ACT_NONE, slope=0.2, save_mean=None, save_invstd=None, R=32, scratch=None,
-                   coef=None, apply_from=0):
+                   coef=None, apply_from=0, nvalid=None):
     """bn2d_fwd (train) from the partials a conv3x3_fwd(stats=...) wrote: finalize + apply.
     ``scratch``: bn2d_stats_scratch(c, max groups) kept with the layer (parallel finalize).
     ``coef`` ([2 * groups * c] float32): also keep the scale / shift (for a consumer's bn_in);
@@ -306,34 +313,34 @@ def bn2d_fwd_stats(part, x, n, hw, c, gamma, beta, y, groups=1, eps=0.8, momentu
         C.check(C.lib.cgl_bn2d_fwd_stats_coef(_p(part), int(R), _p(x), n, hw, c, groups, _p(gamma), _p(beta),
                                               float(eps), float(momentum), _p(running_mean), _p(running_var), act,
                                               float(slope), _p(y), _p(save_mean), _p(save_invstd), _p(scratch),
-                                              _p(coef), int(apply_from), _p(ws), ws.numel(), _s()),
+                                              _p(coef), int(apply_from), _p(nvalid), _p(ws), ws.numel(), _s()),
                 "cgl_bn2d_fwd_stats_coef")
         return y
     C.check(C.lib.cgl_bn2d_fwd_stats(_p(part), int(R), _p(x), n, hw, c, groups, _p(gamma), _p(beta), float(eps),
                                      float(momentum), _p(running_mean), _p(running_var), act, float(slope), _p(y),
-                                     _p(save_mean), _p(save_invstd), _p(scratch), _p(ws), ws.numel(), _s()),
-            "cgl_bn2d_fwd_stats")
+                                     _p(save_mean), _p(save_invstd), _p(scratch), _p(nvalid), _p(ws), ws.numel(),
+                                     _s()), "cgl_bn2d_fwd_stats")
     return y
 
 
 def bn2d_bwd(dy, x, n, hw, c, save_mean, save_invstd, gamma, dx, groups=1, post=None, post_out=None, drop=None,
-             dgamma=None, dbeta=None, slope=0.2):
+             dgamma=None, dbeta=None, slope=0.2, nvalid=None):
     _chk(dy, x, save_mean, save_invstd, gamma, dx, post, post_out, drop, dgamma, dbeta)
     ws = workspace(bn2d_ws_bytes(n, hw, c, groups), dy.device)
     C.check(C.lib.cgl_bn2d_bwd(_p(dy), _p(post), _p(x), n, hw, c, groups, _p(save_mean), _p(save_invstd), _p(gamma),
-                               float(slope), _p(post_out), _p(drop), _p(dx), _p(dgamma), _p(dbeta), _p(ws), ws.numel(),
-                               _s()), "cgl_bn2d_bwd")
+                               float(slope), _p(post_out), _p(drop), _p(dx), _p(dgamma), _p(dbeta), _p(nvalid), _p(ws),
+                               ws.numel(), _s()), "cgl_bn2d_bwd")
     return dx
 
 
 def bn2d_bwd_stats(part, dy, x, n, hw, c, save_mean, save_invstd, gamma, dx, groups=1, post=None, post_out=None,
-                   drop=None, dgamma=None, dbeta=None, slope=0.2, R=32):
+                   drop=None, dgamma=None, dbeta=None, slope=0.2, R=32, nvalid=None):
     """bn2d_bwd from the partials a conv3x3_bwd_data(stats=...) wrote: finalize + apply."""
     _chk(dy, x, save_mean, save_invstd, gamma, dx, post, post_out, drop, dgamma, dbeta)
     ws = workspace(bn2d_ws_bytes(n, hw, c, groups), dy.device)
     C.check(C.lib.cgl_bn2d_bwd_stats(_p(part), int(R), _p(dy), _p(post), _p(x), n, hw, c, groups, _p(save_mean),
                                      _p(save_invstd), _p(gamma), float(slope), _p(post_out), _p(drop), _p(dx),
-                                     _p(dgamma), _p(dbeta), _p(ws), ws.numel(), _s()), "cgl_bn2d_bwd_stats")
+                                     _p(dgamma), _p(dbeta), _p(nvalid), _p(ws), ws.numel(), _s()), "cgl_bn2d_bwd_stats")
     return dx
 
 
@@ -380,11 +387,13 @@ def normal_fill_dev(out, seed, round_dev, stream_id=0):
             "cgl_normal_fill_dev")
 
 
-def sample_rows_dev(src, nrows, seed, round_dev, dst):
-    """Real batch of round round_dev[0] from a device-resident [n, f] shard (keyed per-epoch permutation)."""
+def sample_rows_dev(src, nrows, seed, round_dev, dst, nv_out=None):
+    """Real batch of round round_dev[0] from a device-resident [n, f] shard (keyed per-pass permutation).
+    ``nv_out`` (device int32): DataLoader semantics, each pass ending with its short batch, whose real rows
+    land in nv_out[0]; None: whole batches only (drop_last)."""
     _chk(src, dst)
     C.check(C.lib.cgl_sample_rows_dev(_p(src), src.shape[0], nrows, src.shape[1], int(seed) & (2 ** 64 - 1),
-                                      _p(round_dev), _p(dst), _s()), "cgl_sample_rows_dev")
+                                      _p(round_dev), _p(dst), _p(nv_out), _s()), "cgl_sample_rows_dev")
     return dst
 
 
@@ -425,10 +434,12 @@ def nhwc_to_nchw(x, y, n, c, hw):
     return y
 
 
-def adv_loss(x, M, Cc, kind, target, weight, loss_out=None, grad=None):
+def adv_loss(x, M, Cc, kind, target, weight, loss_out=None, grad=None, nvalid=None):
+    """``nvalid`` (device int32, may be None): only the first *nvalid rows form the batch (mean over them,
+    zero gradient on the rest)."""
     _chk(x, loss_out, grad)
-    C.check(C.lib.cgl_adv_loss(_p(x), M, Cc, LOSS[kind], int(target), float(weight), _p(loss_out), _p(grad), _s()),
-            "cgl_adv_loss")
+    C.check(C.lib.cgl_adv_loss(_p(x), M, Cc, LOSS[kind], int(target), float(weight), _p(loss_out), _p(grad),
+                               _p(nvalid), _s()), "cgl_adv_loss")
 
 
 def adam_multi(params, grads, ms, vs, step, lr=2e-4, betas=(0.5, 0.999), eps=1e-8, step_dev=None):

@@ -190,6 +190,11 @@ class ConvGanStep:
         # captured round as a hipGraph (N = 1; phases stay eager for the multi-worker exchange)
         self.graph = bool(graph)
         self.dstate = torch.zeros(4, dtype=torch.int32, device=dev)
+        # dstate[3]: real images of this round's D-step real call (DataLoader's short final batch of a pass,
+        # capgan.py:282,326-331: a shard of n rows gives ceil(n / B) batches per pass, the last n mod B rows);
+        # the D-step kernels leave the padding images of a short call out (nvalid)
+        self.nv = self.dstate[3:4]
+        self.nv.fill_(batch)
         self._dstate_host = (0, 0, 0)         # host mirror of dstate after the last issued round
         self._cuda_graph = None
         self._phase_graphs = None      # (phase A, phase B) graphs of the split round (N > 1)
@@ -248,11 +253,13 @@ class ConvGanStep:
             self.bst_ok[key] = key in self.st_part and 0 < nb * ci * 2 <= self.st_part[key].numel()
         # sampler over a device-resident real shard [n, 1024] (DataLoader(shuffle=True), capgan.py:282)
         self.data = data
+        self.short = data is not None and data.shape[0] % batch != 0    # some batch of a pass is short
+        self._short_call = False          # this round's real call may be short (nvalid passed to the D step)
         self._perm, self._pos = None, 0
         self._gen = torch.Generator().manual_seed(seed + 1 + rank)
         if data is not None:
-            if data.dim() != 2 or data.shape[1] != 1024 or data.shape[0] < B:
-                raise ValueError("data must be a [n >= batch, 1024] tensor of 32x32 images")
+            if data.dim() != 2 or data.shape[1] != 1024 or data.shape[0] < 1:
+                raise ValueError("data must be a [n >= 1, 1024] tensor of 32x32 images")
             if not data.is_cuda or data.dtype != torch.float32:
                 raise ValueError("data must be float32 on the GPU")
 
@@ -315,13 +322,21 @@ class ConvGanStep:
 
     # ------------------------------------------------------------------ pieces
     def _sample_real(self):
+        """DataLoader(shuffle=True) over the shard (capgan.py:282,326-331): a fresh permutation per pass, cut
+        into batches of B, the pass's last batch short (n mod B rows); its padding rows repeat a real row."""
         B = self.B
         n = self.data.shape[0]
-        if self._perm is None or self._pos + B > n:
+        if self._perm is None or self._pos >= n:
             self._perm = torch.randperm(n, generator=self._gen).to(torch.int32).to(self.device, non_blocking=True)
             self._pos = 0
-        O.gather_rows(self.data, self._perm[self._pos:self._pos + B], 0, B, 1024, self.x3)
-        self._pos += B
+        take = min(B, n - self._pos)
+        idx = self._perm[self._pos:self._pos + take]
+        if take < B:
+            idx = torch.cat([idx, idx[:1].expand(B - take)])
+        O.gather_rows(self.data, idx, 0, B, 1024, self.x3)
+        if self.short:
+            self.nv.fill_(take)
+        self._pos += take
 
     def _g_forward(self):
         P, B2 = self.G.params, 2 * self.B
@@ -359,13 +374,14 @@ class ConvGanStep:
         part = self.st_part.get(key)
         return (part, groups) if part is not None else None
 
-    def _bn_fwd(self, key, fm, x, y, n, hw, c, groups, act, fold=False):
+    def _bn_fwd(self, key, fm, x, y, n, hw, c, groups, act, fold=False, nvalid=None):
         """BatchNorm2d (train) from the partials the producing conv wrote, else with its own pass.
         ``fold``: keep the scale / shift in self.coef[key] and apply to the last group (Xg) only."""
         P, R = fm.params, fm.running
         sm, si = (self.g_save if fm is self.G else self.d_save)[key]
         kw = dict(groups=groups, eps=BN_EPS, momentum=BN_MOM, running_mean=R[key + ".running_mean"],
-                  running_var=R[key + ".running_var"], act=act, slope=SLOPE, save_mean=sm, save_invstd=si)
+                  running_var=R[key + ".running_var"], act=act, slope=SLOPE, save_mean=sm, save_invstd=si,
+                  nvalid=nvalid)
         if fold:
             kw.update(coef=self.coef[key], apply_from=n - n // groups)
         if key in self.st_part:
@@ -391,22 +407,25 @@ class ConvGanStep:
                           self.seed * 7919 + self.rank,
                           [(self.round * 2 + call) * 4 + k for call in (0, 1) for k in range(4)])
 
-    def _d_forward(self, x, n, groups, masks):
+    def _d_forward(self, x, n, groups, masks, nvalid=None):
+        """``nvalid``: the first call (the real images) is a short batch of *nvalid images."""
         P, R = self.D.params, self.D.running
         inp = x
         for k, (ck, bk, ci, co, hw) in enumerate(D_CONVS):
+            st = self._stats(bk, groups) if bk else None
             O.conv3x3_fwd(inp, P[ck + ".weight"], P[ck + ".bias"], self.q[k], n, hw, hw, ci, co, 2, 0, act=O.ACT_LEAKY,
-                          slope=SLOPE, drop=masks[k], wp=self.pk[ck + "f"], stats=self._stats(bk, groups) if bk else None)
+                          slope=SLOPE, drop=masks[k], wp=self.pk[ck + "f"], stats=st,
+                          nvalid=nvalid if st is not None else None)
             inp = self.q[k]
             if bk:
-                self._bn_fwd(bk, self.D, self.q[k], self.r[k], n, (hw // 2) ** 2, co, groups, O.ACT_NONE)
+                self._bn_fwd(bk, self.D, self.q[k], self.r[k], n, (hw // 2) ** 2, co, groups, O.ACT_NONE, nvalid=nvalid)
                 inp = self.r[k]
         # out.view(B, -1) -> adv_layer (model/lsgan.py:96-97) from the NHWC map; the D step's call keeps the
         # NCHW view for adv_layer's weight gradient, the G-loss pass (no D weight gradient) does not
         O.dense1_fwd_nhwc(self.r[3], P["adv_layer.weight"], P["adv_layer.bias"], self.v, n, 128, 4,
                           flat=self.flat if masks is self.mask_d else None)
 
-    def _d_backward(self, x, n, groups, masks, wgrad, dx):
+    def _d_backward(self, x, n, groups, masks, wgrad, dx, nvalid=None):
         P, G = self.D.params, self.D.grads
         bst = set()     # BatchNorms whose backward partials the previous input-gradient conv wrote
         O.dense1_bwd_data_nhwc(self.dv, P["adv_layer.weight"], self.dr[3], n, 128, 4)
@@ -418,7 +437,7 @@ class ConvGanStep:
             if bk:
                 sm, si = self.d_save[bk]
                 kw = dict(groups=groups, post_out=self.q[k], drop=masks[k], dgamma=G[bk + ".weight"] if wgrad else None,
-                          dbeta=G[bk + ".bias"] if wgrad else None, slope=SLOPE)
+                          dbeta=G[bk + ".bias"] if wgrad else None, slope=SLOPE, nvalid=nvalid)
                 if bk in bst:
                     O.bn2d_bwd_stats(self.st_part[bk], self.dr[k], self.q[k], n, ho * ho, co, sm, si, P[bk + ".weight"],
                                      self.dc[k], **kw)
@@ -486,11 +505,24 @@ class ConvGanStep:
             else:
                 C.check(C.lib.cgl_normal_fill(ctypes_ptr(self.z), self.z.numel(), self.seed, self.round, 0,
                                               O._s()), "cgl_normal_fill")
+        self._short_call = self.short
         if real is not None:
-            O.gather_rows(real.reshape(-1, 1024), None, 0, B, 1024, self.x3)
+            # an explicit real batch; fewer than B rows = a short batch (padding rows repeat its first row)
+            real = real.reshape(-1, 1024)
+            nr = real.shape[0]
+            if not 1 <= nr <= B:
+                raise ValueError(f"real batch of {nr} rows: expected 1 .. {B}")
+            O.gather_rows(real, None, 0, nr, 1024, self.x3)
+            if nr < B:
+                O.gather_rows(real, torch.zeros(B - nr, dtype=torch.int32, device=self.device), 0, B - nr, 1024,
+                              self.x3[nr:])
+            self._short_call = nr < B or self.short
+            if self._short_call:
+                self.nv.fill_(nr)
         elif self.data is not None:
             if self.graph:
-                O.sample_rows_dev(self.data, B, self.seed + 1 + self.rank, self.dstate[0:1], self.x3)
+                O.sample_rows_dev(self.data, B, self.seed + 1 + self.rank, self.dstate[0:1], self.x3,
+                                  nv_out=self.nv if self.short else None)
             else:
                 self._sample_real()
         self.pk.run()
@@ -498,10 +530,11 @@ class ConvGanStep:
         self._g_forward()
         # local D step on [real; Xd]: two forward calls (statistics, masks per call), one backward
         half = 0.5 if self.loss == "mse" else 1.0
-        self._d_forward(self.x3, 2 * B, 2, self.mask_d)
-        O.adv_loss(self.v[:B], B, 1, self.loss, 1, half, self.lbuf[0:1], self.dv[:B])
+        nvd = self.nv if self._short_call else None     # the real call's images (short final batch)
+        self._d_forward(self.x3, 2 * B, 2, self.mask_d, nvalid=nvd)
+        O.adv_loss(self.v[:B], B, 1, self.loss, 1, half, self.lbuf[0:1], self.dv[:B], nvalid=nvd)
         O.adv_loss(self.v[B:2 * B], B, 1, self.loss, 0, half, self.lbuf[1:2], self.dv[B:2 * B])
-        self._d_backward(self.x3, 2 * B, 2, self.mask_d, wgrad=True, dx=None)
+        self._d_backward(self.x3, 2 * B, 2, self.mask_d, wgrad=True, dx=None, nvalid=nvd)
         self.D.adam(self.lr, self.betas, self.eps, step_dev=self.dstate[2:3] if self.graph else None)
         self.pk.run("D")
         # G loss through the updated D (its D weight gradient is discarded by the reference: skipped)

@@ -292,9 +292,13 @@ class ConvWorkerExchange:
     BatchNorm running statistics; D-swap moves both (the reference's copy_parameters keeps every
     non-scalar state-dict entry, MDGAN/MNIST/mdgan.py:233-238)."""
 
-    def __init__(self, step, comm=None, share_every: int = 0, swap_every: int = 0, server_rank: int = 0):
+    def __init__(self, step, comm=None, share_every: int = 0, swap_every: int = 0, server_rank: int = 0,
+                 force_split: bool = False):
         self.step, self.comm = step, comm
         self.share_every, self.swap_every = share_every, swap_every
+        # test hook (as WorkerExchange's): the N > 1 path in a one-rank group, so a one-GPU box runs the
+        # conv exchange over real RCCL
+        self.force_split = force_split
         n = comm.size if comm is not None else 1
         if n != step.n_workers:
             raise ValueError(f"step planned for {step.n_workers} workers, group has {n}")
@@ -312,7 +316,7 @@ class ConvWorkerExchange:
         s = self.step
         share = self.comm is not None and self.share_every > 0 and (r + 1) % self.share_every == 0
         swap = self.dswap is not None and (r + 1) % self.swap_every == 0
-        if self.comm is None or self.comm.size == 1:
+        if self.comm is None or (self.comm.size == 1 and not self.force_split):
             s.run(real, eager=eager)
         else:
             s.round_a(real, eager=eager)

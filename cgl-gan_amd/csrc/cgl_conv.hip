@@ -72,6 +72,10 @@ struct CglConvLaunch {
   const float* st_x;         // mode 1: the BatchNorm input x, the post-activation (or null) and the
   const float* st_post;      // saved per-call mean [groups][N], all at the stored tensor's positions
   const float* st_mean;
+  // forward statistics of a call whose first group (the D step's real call) holds a short batch: only its
+  // first *st_nv images are real (DataLoader's short final batch, capgan.py:282,326-331); the padding
+  // images' rows are left out of the partials (single-problem launches only; null: every row counts)
+  const int* st_nv;
   int ilv;                   // forward: the np problems share X and their tile grid -- tiles interleaved
                              // problem-minor (tile t of every problem back to back on one XCD)
   // forward with the input's BatchNorm2d folded into the operand load (the producer's bn2d finalize wrote
@@ -518,6 +522,37 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
           double* dst = L->st_part + (chunk * N + col) * 2;
           dst[0] = S;
           dst[1] = D;
+        }
+      }
+    } else if (L->st_part && L->st_nv && rowb < P->st_gr && rowb + 32 > min(gldi(L->st_nv), P->st_gr / hw) * hw) {
+      // a chunk of the short first call that holds padding rows: {sum, M2 about the mean} over its real rows
+      // only (the finalize derives every chunk's count from the same *st_nv)
+      const int nvr = min(gldi(L->st_nv), P->st_gr / hw) * hw;
+      const long chunk = P->st_off + rowb / 32;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        double sm = 0.0, cn = 0.0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const bool in = row0 + (r & 3) + 8 * (r >> 2) < nvr;
+          sm += in ? (double)acc[i][j][r] : 0.0;
+          cn += in ? 1.0 : 0.0;
+        }
+        sm += __shfl_xor(sm, 32);
+        cn += __shfl_xor(cn, 32);
+        const double mu = cn > 0.0 ? sm / cn : 0.0;
+        double m2 = 0.0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const double dd = (double)acc[i][j][r] - mu;
+          m2 += row0 + (r & 3) + 8 * (r >> 2) < nvr ? dd * dd : 0.0;
+        }
+        m2 += __shfl_xor(m2, 32);
+        const int col = n0 + 32 * j + li;
+        if (lh == 0 && col < N) {
+          double* dst = L->st_part + (chunk * N + col) * 2;
+          dst[0] = sm;
+          dst[1] = m2;
         }
       }
     } else if (L->st_part) {
@@ -1518,13 +1553,22 @@ struct CglChanArgs {
   const float* dY; const float* post; float slope;
   const float* mean;         // [groups][C] (mode 1)
   double* part;              // [nchunks][C][2]
+  const int* nv;             // mode 0: only rows < *nv * hw of the first group (rows < gr) count, or null
 };
+
+// rows of the first BatchNorm group that carry data: a short real call (DataLoader's short final batch)
+// holds *nv real images, the rest of its gr rows are padding; null = the whole group
+__device__ __forceinline__ int cgl_nv_rows(const int* nv, int hw, int gr) {
+  return nv ? min(gldi(nv) * hw, gr) : gr;
+}
 
 __global__ __launch_bounds__(256) void cgl_chan_reduce(CglChanArgs a) {
   __shared__ double s0[256], s1[256];
   const int C = a.C, rp = 256 / C;
   const int c = threadIdx.x % C, rl = threadIdx.x / C;
-  const int r0 = blockIdx.x * a.R, r1 = min(r0 + a.R, a.rows);
+  const int r0 = blockIdx.x * a.R;
+  int r1 = min(r0 + a.R, a.rows);
+  if (a.mode == 0 && a.nv && r0 < a.gr) r1 = max(r0, min(r1, cgl_nv_rows(a.nv, a.hw, a.gr)));
   double x0 = 0.0, x1 = 0.0;
   // rows r0 + rl + rp * i, issued 8 at a time (independent loads in flight), summed in order
   if (a.mode == 1) {
@@ -1566,7 +1610,7 @@ __global__ __launch_bounds__(256) void cgl_chan_reduce(CglChanArgs a) {
       s0[c] = t;
     }
     __syncthreads();
-    const double mean = s0[c] / (r1 - r0);
+    const double mean = s0[c] / max(r1 - r0, 1);
     double m2 = 0.0;
     for (int rb = r0 + rl; rb < r1; rb += 8 * rp) {
       float xv[8];
@@ -1610,7 +1654,9 @@ __global__ __launch_bounds__(256) void cgl_chan_reduce4(CglChanArgs a) {
   __shared__ double s0[1024], s1[1024], tot[256];
   const int C = a.C, CW = C >> 2, rp = 256 / CW;
   const int cs = threadIdx.x % CW, rl = threadIdx.x / CW, c = 4 * cs;
-  const int r0 = blockIdx.x * a.R, r1 = min(r0 + a.R, a.rows);
+  const int r0 = blockIdx.x * a.R;
+  int r1 = min(r0 + a.R, a.rows);
+  if (a.mode == 0 && a.nv && r0 < a.gr) r1 = max(r0, min(r1, cgl_nv_rows(a.nv, a.hw, a.gr)));
   double x0[4] = {0.0, 0.0, 0.0, 0.0}, x1[4] = {0.0, 0.0, 0.0, 0.0};
   if (a.mode == 1) {
     const f32x4 mu = *(gcf4p)(a.mean + (long)(r0 / a.gr) * C + c);
@@ -1668,7 +1714,7 @@ __global__ __launch_bounds__(256) void cgl_chan_reduce4(CglChanArgs a) {
     __syncthreads();
     double mean[4], m2[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) mean[j] = tot[c + j] / (r1 - r0);
+    for (int j = 0; j < 4; ++j) mean[j] = tot[c + j] / max(r1 - r0, 1);
     for (int rb = r0 + rl; rb < r1; rb += 8 * rp) {
       f32x4 xv[8];
 #pragma unroll
@@ -1757,7 +1803,16 @@ struct CglBnFinArgs {
   float* coef0; float* coef1;               // [groups][C]: fwd scale, shift; bwd gm, k
   float* dgamma; float* dbeta;              // bwd, or bias out (mode 2: dgamma)
   int nocache;                              // A/B switch: stream the partials twice (CGL_FIN_NOCACHE)
+  // a short first call (the D step's real call on DataLoader's short final batch): only its first *nv images
+  // (hw rows each) carry data -- group 0 counts nv * hw rows, and chunk q of it min(max(nv hw - q R, 0), R)
+  const int* nv; int hw;
 };
+
+// rows of group g and of chunk q of it (cgl_nv_rows for the short first call)
+__device__ __forceinline__ int cgl_fin_rows(const CglBnFinArgs& a, int g) {
+  return g == 0 ? cgl_nv_rows(a.nv, a.hw, a.gr) : a.gr;
+}
+__device__ __forceinline__ int cgl_fin_chunk_rows(int n, int q, int R) { return min(max(n - q * R, 0), R); }
 
 __device__ __forceinline__ double cgl_wave_sum_d(double x) {
 #pragma unroll
@@ -1776,8 +1831,10 @@ __device__ __forceinline__ double cgl_block_sum_d(double x, double* red) {
 
 // sum over chunks q = lane, lane + 256, ... < cnt of f(part pair at chunk q0 + q) -- 8 independent
 // 16-byte loads in flight per thread, accumulated in chunk order (the per-thread order is fixed)
+// (fn(pair, q): q = the chunk's index within its group, qbase = that of chunk q0)
 template <class Fn>
-__device__ __forceinline__ double cgl_fin_sum(const double* part, long q0, int cnt, int C, int c, int lane, Fn fn) {
+__device__ __forceinline__ double cgl_fin_sum(const double* part, long q0, int cnt, int C, int c, int lane, Fn fn,
+                                              int qbase = 0) {
   typedef double f64x2 __attribute__((ext_vector_type(2)));
   typedef const CGL_GLOBAL f64x2* gcd2p;
   double t = 0.0;
@@ -1787,7 +1844,7 @@ __device__ __forceinline__ double cgl_fin_sum(const double* part, long q0, int c
     for (int i = 0; i < 8; ++i) v[i] = *(gcd2p)(part + ((q0 + min(qb + 256 * i, cnt - 1)) * C + c) * 2);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-      if (qb + 256 * i < cnt) t += fn(v[i]);
+      if (qb + 256 * i < cnt) t += fn(v[i], qbase + qb + 256 * i);
   }
   return t;
 }
@@ -1815,12 +1872,12 @@ struct CglFinCache {
       }
   }
   template <class Fn>
-  __device__ __forceinline__ double sum(int g, Fn fn) const {
+  __device__ __forceinline__ double sum(int g, Fn fn, int qbase = 0) const {
     // the group is selected, not indexed: a runtime index into v[][] puts the cache in scratch
     double t = 0.0;
 #pragma unroll
     for (int i = 0; i < NI; ++i)
-      if (lane + 256 * i < cnt) t += fn(g ? v[1][i] : v[0][i]);
+      if (lane + 256 * i < cnt) t += fn(g ? v[1][i] : v[0][i], qbase + lane + 256 * i);
     return t;
   }
 };
@@ -1841,7 +1898,7 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
   };
   if (a.mode == 2) {
     const int nch = a.groups * a.chunks_per_group;
-    double t = cgl_fin_sum(part, 0, nch, C, c, lane, [](auto v) { return (double)v[0]; });
+    double t = cgl_fin_sum(part, 0, nch, C, c, lane, [](auto v, int) { return (double)v[0]; });
     t = cgl_block_sum_d(t, red);
     if (lane == 0) gst(a.dgamma + c, (float)t);
     return;
@@ -1850,14 +1907,15 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
   if (a.mode == 1) {
     double dg = 0.0, db = 0.0;
     for (int g = 0; g < a.groups; ++g) {
-      double S = gsum(g, [](auto v) { return (double)v[0]; });
-      double D = gsum(g, [](auto v) { return (double)v[1]; });
+      double S = gsum(g, [](auto v, int) { return (double)v[0]; });
+      double D = gsum(g, [](auto v, int) { return (double)v[1]; });
       S = cgl_block_sum_d(S, red);
       D = cgl_block_sum_d(D, red);
       const float invstd = gld(a.save_invstd + (long)g * C + c);
+      const int ng = cgl_fin_rows(a, g);
       if (lane == 0) {
-        gst(a.coef0 + (long)g * C + c, (float)(S / a.gr));
-        gst(a.coef1 + (long)g * C + c, (float)D * invstd * invstd / a.gr);
+        gst(a.coef0 + (long)g * C + c, (float)(S / ng));
+        gst(a.coef1 + (long)g * C + c, (float)D * invstd * invstd / ng);
       }
       dg += D * (double)invstd;
       db += S;
@@ -1881,12 +1939,16 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
   }
   float rm = a.run_mean ? gld(a.run_mean + c) : 0.f, rv = a.run_var ? gld(a.run_var + c) : 0.f;
   for (int g = 0; g < a.groups; ++g) {
-    double s = gsum(g, [](auto v) { return (double)v[0]; });
+    double s = gsum(g, [](auto v, int) { return (double)v[0]; });
     s = cgl_block_sum_d(s, red);
-    const double n = a.gr;
+    const int ng = cgl_fin_rows(a, g);
+    const double n = ng;
     const double mu = s / n;
-    const double cnt = a.R;
-    double m2 = gsum(g, [&](auto v) {
+    const double R = a.R;
+    const bool full = ng == a.gr;            // every chunk holds R rows (the common case: one code path)
+    double m2 = gsum(g, [&](auto v, int q) {
+      const double cnt = full ? R : (double)cgl_fin_chunk_rows(ng, q, a.R);
+      if (cnt == 0.0) return 0.0;
       const double dd = v[0] / cnt - mu;
       return (double)v[1] + cnt * dd * dd;
     });
@@ -1940,14 +2002,19 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize_sliced(CglBnFinSliced a) 
   for (int g = 0; g < G; ++g) {
     const long q0 = (long)g * cpg + q_lo;
     auto gsum = [&](auto fn) -> double {
-      return (G <= 2 && a.L <= 512) ? fc.sum(g, fn) : cgl_fin_sum(a.f.part, q0, cnt, C, c, lane, fn);
+      return (G <= 2 && a.L <= 512) ? fc.sum(g, fn, q_lo) : cgl_fin_sum(a.f.part, q0, cnt, C, c, lane, fn, q_lo);
     };
-    double sm = gsum([](auto v) { return (double)v[0]; });
+    const int ng = cgl_fin_rows(a.f, g);
+    const bool full = ng == a.f.gr;
+    const int srows = full ? cnt * a.f.R : min(max(ng - q_lo * a.f.R, 0), cnt * a.f.R);   // this slice's rows
+    double sm = gsum([](auto v, int) { return (double)v[0]; });
     sm = cgl_block_sum_d(sm, red);
-    const double mu = sm / (cnt * R);
-    double m2 = gsum([&](auto v) {
-      const double dd = v[0] / R - mu;
-      return (double)v[1] + R * dd * dd;
+    const double mu = full ? sm / (cnt * R) : (srows > 0 ? sm / srows : 0.0);
+    double m2 = gsum([&](auto v, int q) {
+      const double rq = full ? R : (double)cgl_fin_chunk_rows(ng, q, a.f.R);
+      if (rq == 0.0) return 0.0;
+      const double dd = v[0] / rq - mu;
+      return (double)v[1] + rq * dd * dd;
     });
     m2 = cgl_block_sum_d(m2, red);
     if (lane == 0) {
@@ -1975,14 +2042,21 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize_sliced(CglBnFinSliced a) 
     }
     __syncthreads();
     if (lane == 0) {
-      const double n = a.f.gr;
+      const int ng = cgl_fin_rows(a.f, g);
+      const bool full = ng == a.f.gr;
+      const double n = ng;
+      // rows of slice q (all of its chunks' R rows, or the short call's share of them)
+      auto qrows = [&](int q) -> double {
+        const int rq = (min((q + 1) * a.L, cpg) - q * a.L) * a.f.R;
+        return full ? (double)(min((q + 1) * a.L, cpg) - q * a.L) * R : (double)min(max(ng - q * a.L * a.f.R, 0), rq);
+      };
       double tot = 0.0;
-      for (int q = 0; q < S; ++q) tot += smu[q] * (min((q + 1) * a.L, cpg) - q * a.L) * R;
+      for (int q = 0; q < S; ++q) tot += full ? smu[q] * (min((q + 1) * a.L, cpg) - q * a.L) * R : smu[q] * qrows(q);
       const double mu = tot / n;
       double m2 = 0.0;
       for (int q = 0; q < S; ++q) {
         const double dd = smu[q] - mu;
-        m2 += sm2[q] + (min((q + 1) * a.L, cpg) - q * a.L) * R * dd * dd;
+        m2 += sm2[q] + qrows(q) * dd * dd;
       }
       const double invstd = 1.0 / sqrt(m2 / n + a.f.eps);
       const float sc = (float)invstd * w;
@@ -2064,12 +2138,14 @@ struct CglEltArgs {
   const float* coef0; const float* coef1; const float* mean; const float* invstd; const float* gamma;
   const float* post_out; const float* drop;
   float* out;
+  const int* nv;             // mode 1, short first call: rows >= *nv * hw of group 0 are padding -> dX = 0
 };
 
 __global__ __launch_bounds__(256) void cgl_eltwise(CglEltArgs a) {
   const long n4 = (long)a.rows * a.C / 4;
   const int C = a.C;
   const float sl = a.slope;
+  const int nvr = a.mode == 1 ? cgl_nv_rows(a.nv, a.hw, a.gr) : a.gr;
   // 32-bit index arithmetic when the tensor allows it (a 64-bit division per float4 costs more VALU
   // than the element work)
   const bool small = n4 < (1L << 29);
@@ -2117,6 +2193,7 @@ __global__ __launch_bounds__(256) void cgl_eltwise(CglEltArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] *= dm[j];
       }
+      if (g == 0 && r + a.row0 >= nvr) o = f32x4{0.f, 0.f, 0.f, 0.f};   // padding of a short first call
     } else if (a.mode == 2) {
       const f32x4 dy = *(gcf4p)(a.dY + e);
       o = dy;
@@ -2245,11 +2322,23 @@ __global__ __launch_bounds__(256) void cgl_transpose_k(const float* X, float* Y,
 //   2 MSE:  nn.MSELoss (LSGAN objective for the model/lsgan.py discriminator; parity vs torch)
 //   3 BCE on logits through nn.Sigmoid (Sigmoid + BCELoss, for the model/lsgan.py logit)
 // grad = weight * d(mean loss)/dx, written when non-null.
-__global__ __launch_bounds__(256) void cgl_adv_loss_k(const float* x, int M, int C, int loss, int target,
-                                                      float weight, float* loss_out, float* grad) {
+// nv (may be null): only the first *nv rows are a batch (DataLoader's short final batch): the mean runs
+// over them and the other rows get a zero gradient.
+__global__ __launch_bounds__(256) void cgl_adv_loss_k(const float* x, int Mall, int C, int loss, int target,
+                                                      float weight, float* loss_out, float* grad, const int* nv) {
   __shared__ double s[256];
   double acc = 0.0;
+  const int M = nv ? min(max(gldi(nv), 1), Mall) : Mall;
   const float invM = 1.f / (float)M;
+  if (grad && M < Mall)
+    for (int r = M + threadIdx.x; r < Mall; r += 256) {
+      if (loss == 0) {
+        gst(grad + 2 * r, 0.f);
+        gst(grad + 2 * r + 1, 0.f);
+      } else {
+        gst(grad + r, 0.f);
+      }
+    }
   for (int r = threadIdx.x; r < M; r += 256) {
     float l, g0 = 0.f, g1 = 0.f;
     if (loss == 0) {
@@ -2351,15 +2440,31 @@ __global__ __launch_bounds__(256) void cgl_normal_dev_k(float* out, long n, unsi
   cgl_normal_at((long)blockIdx.x * 256 + threadIdx.x, out, n, seed, (uint32_t)gldi(round), stream_id);
 }
 
-// real batch of round R: rows R*nrows .. R*nrows + nrows - 1 of the sample stream, data epoch e =
-// pos / per (per = whole batches per pass: drop_last), row = keyed Feistel permutation of [0, n_src)
-// per data epoch (the MLP prologue's sampler); one workgroup per row, float4 copies
+// real batch of round R (DataLoader(shuffle=True), capgan.py:282,326-331): each pass over the n_src rows is
+// a keyed Feistel permutation of [0, n_src) (the MLP prologue's sampler) cut into ceil(n_src / nrows)
+// batches, the last one short (n_src mod nrows rows); round R takes batch R of the stream.  nv_out (may be
+// null) receives the batch's real rows; rows past a short batch copy a valid dummy row (the consumers
+// leave them out: cgl_nv_rows).  With nv_out null the pass is cut drop_last (whole batches only).  One
+// workgroup per row, float4 copies.
 __global__ __launch_bounds__(256) void cgl_sample_rows_k(const float* src, int n_src, int nrows, int rowf,
-                                                         unsigned long long seed, const int* round, float* dst) {
+                                                         unsigned long long seed, const int* round, float* dst,
+                                                         int* nv_out) {
   const int r = blockIdx.x;
-  const long per = (long)(n_src / nrows) * nrows;
-  const long pos = (long)gldi(round) * nrows + r;
-  const uint32_t ep = (uint32_t)(pos / per), j = (uint32_t)(pos % per);
+  uint32_t ep, j;
+  if (nv_out) {
+    const long nb = (n_src + nrows - 1) / nrows;
+    const long bpos = gldi(round);
+    ep = (uint32_t)(bpos / nb);
+    const long b = bpos % nb;
+    const long jj = b * nrows + r;
+    j = (uint32_t)(jj < n_src ? jj : n_src - 1);
+    if (r == 0 && threadIdx.x == 0) nv_out[0] = (int)(n_src - b * nrows < nrows ? n_src - b * nrows : nrows);
+  } else {
+    const long per = (long)(n_src / nrows) * nrows;
+    const long pos = (long)gldi(round) * nrows + r;
+    ep = (uint32_t)(pos / per);
+    j = (uint32_t)(pos % per);
+  }
   const uint32_t idx = cgl_permute(j, (uint32_t)n_src, (uint32_t)seed ^ (ep * 0x85ebca6bu + 0x1234567u));
   const f32x4* s4 = (const f32x4*)(src + (long)idx * rowf);
   f32x4* d4 = (f32x4*)(dst + (long)r * rowf);
@@ -2733,7 +2838,7 @@ bool conv_halo_ok(const CglConvProb* P, int np) {
 
 int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float slope, const float* drop,
                     hipStream_t s, double* st_part = nullptr, int st_cpg = 0, const StatBwd* sb = nullptr,
-                    const BnIn* bi = nullptr) {
+                    const BnIn* bi = nullptr, const int* st_nv = nullptr) {
   const int N = P[0].N;
   CglConvLaunch L;
   std::memset(&L, 0, sizeof(L));
@@ -2751,6 +2856,8 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
   L.drop = drop;
   L.st_part = st_part;
   L.st_cpg = st_cpg;
+  L.st_nv = st_nv;
+  if (st_nv && (!st_part || sb || np != 1)) return CGL_E_ARG;   // forward statistics of one problem only
   if (sb) {
     L.st_mode = 1;
     L.st_x = sb->x;
@@ -2793,7 +2900,7 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
   }
   // the upsampling conv's 4 parity problems from one LDS-staged window per 64-row tile (CGL_CONV_HALO=0: off)
   const int halo_env = getenv("CGL_CONV_HALO") ? atoi(getenv("CGL_CONV_HALO")) : 1;   // read per launch (tests toggle it)
-  if (halo_env && !L.st_mode && conv_halo_ok(P, np)) {
+  if (halo_env && !L.st_mode && !L.st_nv && conv_halo_ok(P, np)) {
     const int lds = (64 / P[0].OW + 2) * (P[0].OW + 2) * (P[0].Cin + 4) * 4;
     L.WM = L.WN = L.WK = 1;
     for (int i = 0; i < np; ++i) {
@@ -2917,7 +3024,7 @@ bool c1_ok(const ConvGeom& g) {
 
 int conv_fwd_impl(const ConvGeom& g, const float* X, const float* W, const float* bias, float* Y, int act, float slope,
                   const float* drop, void* ws, int64_t wsb, hipStream_t s, const float* Wp = nullptr,
-                  double* st_part = nullptr, int st_groups = 1, const BnIn* bi = nullptr) {
+                  double* st_part = nullptr, int st_groups = 1, const BnIn* bi = nullptr, const int* st_nv = nullptr) {
   if (!X || !(W || Wp) || !Y || !ws || act < 0 || act > 3 || !al16(ws) || (Wp && !al16(Wp))) return CGL_E_ARG;
   if (wsb < conv_ws_bytes(g)) return CGL_E_SIZE;
   if ((g.cin % 4 == 0) && !al16(X)) return CGL_E_ARG;
@@ -2955,7 +3062,7 @@ int conv_fwd_impl(const ConvGeom& g, const float* X, const float* W, const float
   int rc;
   if (Wp) pack_layout(P, np, Wp);
   else if ((rc = launch_pack(W, g, 0, P, np, (float*)ws, s))) return rc;
-  return launch_conv_mma(P, np, bias, act, slope, drop, s, st_part, cpg, nullptr, bi);
+  return launch_conv_mma(P, np, bias, act, slope, drop, s, st_part, cpg, nullptr, bi, st_nv);
 }
 
 int conv_bwd_data_impl(const ConvGeom& g, const float* dY, const float* W, float* dX, void* ws, int64_t wsb,
@@ -3233,12 +3340,13 @@ int64_t cgl_conv3x3_stat_chunks(int n, int h, int w, int cin, int cout, int stri
 
 int cgl_conv3x3_fwd_packed_stats(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w,
                                  int cin, int cout, int stride, int up, int act, float slope, const float* drop,
-                                 int groups, double* part, void* ws, int64_t wsb, void* stream) {
+                                 int groups, double* part, const int* nvalid, void* ws, int64_t wsb, void* stream) {
   ConvGeom g;
   const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
   if (rc) return rc;
   if (!Wp || !part) return CGL_E_ARG;
-  return conv_fwd_impl(g, X, nullptr, bias, Y, act, slope, drop, ws, wsb, (hipStream_t)stream, Wp, part, groups);
+  return conv_fwd_impl(g, X, nullptr, bias, Y, act, slope, drop, ws, wsb, (hipStream_t)stream, Wp, part, groups,
+                       nullptr, nvalid);
 }
 
 int cgl_conv3x3_fwd_packed_bnin(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w,
@@ -3316,7 +3424,7 @@ int64_t cgl_bn2d_workspace_bytes(int n, int hw, int C, int groups) {
 
 int cgl_bn2d_fwd(const float* X, int n, int hw, int C, int groups, const float* gamma, const float* beta, double eps,
                  double momentum, float* running_mean, float* running_var, int train, int act, float slope, float* Y,
-                 float* save_mean, float* save_invstd, void* ws, int64_t wsb, void* stream) {
+                 float* save_mean, float* save_invstd, const int* nvalid, void* ws, int64_t wsb, void* stream) {
   if (!X || !Y || !gamma || !beta || !ws || !al16(ws) || !al16(X) || !al16(Y)) return CGL_E_ARG;
   if (n < 1 || hw < 1 || C % 4 != 0 || !pow2_le256(C) || groups < 1 || n % groups || (act != 0 && act != 1))
     return CGL_E_ARG;
@@ -3338,11 +3446,13 @@ int cgl_bn2d_fwd(const float* X, int n, int hw, int C, int groups, const float* 
     CglChanArgs a;
     std::memset(&a, 0, sizeof(a));
     a.X = X; a.rows = (int)rows; a.C = C; a.R = R; a.mode = 0; a.gr = (int)gr; a.part = part;
+    a.nv = nvalid; a.hw = hw;
     launch_chan_reduce(a, nch, s);
   }
   CglBnFinArgs f;
   std::memset(&f, 0, sizeof(f));
   f.part = part; f.C = C; f.groups = groups; f.chunks_per_group = (int)(gr / R); f.R = R; f.gr = (int)gr;
+  f.nv = train ? nvalid : nullptr; f.hw = hw;
   f.mode = 0; f.train = train; f.gamma = gamma; f.beta = beta; f.eps = eps; f.momentum = momentum;
   f.run_mean = running_mean; f.run_var = running_var; f.save_mean = save_mean; f.save_invstd = save_invstd;
   f.coef0 = c0; f.coef1 = c1;
@@ -3365,15 +3475,16 @@ int64_t cgl_bn2d_stats_scratch_bytes(int C, int groups) {
 int cgl_bn2d_fwd_stats(const double* part, int R, const float* X, int n, int hw, int C, int groups, const float* gamma,
                        const float* beta, double eps, double momentum, float* running_mean, float* running_var,
                        int act, float slope, float* Y, float* save_mean, float* save_invstd, void* scratch,
-                       void* ws, int64_t wsb, void* stream) {
+                       const int* nvalid, void* ws, int64_t wsb, void* stream) {
   return cgl_bn2d_fwd_stats_coef(part, R, X, n, hw, C, groups, gamma, beta, eps, momentum, running_mean, running_var,
-                                 act, slope, Y, save_mean, save_invstd, scratch, nullptr, 0, ws, wsb, stream);
+                                 act, slope, Y, save_mean, save_invstd, scratch, nullptr, 0, nvalid, ws, wsb, stream);
 }
 
 int cgl_bn2d_fwd_stats_coef(const double* part, int R, const float* X, int n, int hw, int C, int groups,
                             const float* gamma, const float* beta, double eps, double momentum, float* running_mean,
                             float* running_var, int act, float slope, float* Y, float* save_mean, float* save_invstd,
-                            void* scratch, float* coef, int apply_img0, void* ws, int64_t wsb, void* stream) {
+                            void* scratch, float* coef, int apply_img0, const int* nvalid, void* ws, int64_t wsb,
+                            void* stream) {
   if (!part || !X || !Y || !gamma || !beta || !ws || !al16(ws) || !al16(X) || !al16(Y)) return CGL_E_ARG;
   if ((coef && !al16(coef)) || apply_img0 < 0 || apply_img0 > n) return CGL_E_ARG;
   if (n < 1 || hw < 1 || C % 4 != 0 || !pow2_le256(C) || groups < 1 || n % groups || (act != 0 && act != 1))
@@ -3393,6 +3504,7 @@ int cgl_bn2d_fwd_stats_coef(const double* part, int R, const float* X, int n, in
   std::memset(&f, 0, sizeof(f));
   f.part = part; f.C = C; f.groups = groups; f.chunks_per_group = (int)(gr / R); f.R = R; f.gr = (int)gr;
   f.mode = 0; f.train = 1; f.gamma = gamma; f.beta = beta; f.eps = eps; f.momentum = momentum;
+  f.nv = nvalid; f.hw = hw;
   f.run_mean = running_mean; f.run_var = running_var; f.save_mean = save_mean; f.save_invstd = save_invstd;
   f.coef0 = c0; f.coef1 = c1;
   const int cpg = (int)(gr / R);
@@ -3427,7 +3539,7 @@ int cgl_bn2d_fwd_stats_coef(const double* part, int R, const float* X, int n, in
 int cgl_bn2d_bwd_stats(const double* part, int R, const float* dY, const float* post, const float* X, int n, int hw,
                        int C, int groups, const float* save_mean, const float* save_invstd, const float* gamma,
                        float slope, const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta,
-                       void* ws, int64_t wsb, void* stream) {
+                       const int* nvalid, void* ws, int64_t wsb, void* stream) {
   if (!part || !dY || !X || !save_mean || !save_invstd || !gamma || !dX || !ws || !al16(ws)) return CGL_E_ARG;
   if (!al16(dY) || !al16(X) || !al16(dX) || (post && !al16(post)) || (post_out && !al16(post_out))) return CGL_E_ARG;
   if (!al16(save_mean) || !al16(save_invstd) || !al16(gamma) || (drop && !al16(drop))) return CGL_E_ARG;
@@ -3446,13 +3558,14 @@ int cgl_bn2d_bwd_stats(const double* part, int R, const float* dY, const float* 
   f.part = part; f.C = C; f.groups = groups; f.chunks_per_group = (int)(gr / R); f.R = R; f.gr = (int)gr;
   f.mode = 1; f.gamma = gamma; f.save_invstd = const_cast<float*>(save_invstd); f.coef0 = c0; f.coef1 = c1;
   f.dgamma = dgamma; f.dbeta = dbeta;
+  f.nv = nvalid; f.hw = hw;
   f.nocache = fin_nocache();
   hipLaunchKernelGGL(cgl_bn_finalize, dim3(C), dim3(256), 0, s, f);
   CglEltArgs e;
   std::memset(&e, 0, sizeof(e));
   e.mode = 1; e.rows = (int)rows; e.C = C; e.gr = (int)gr; e.hw = hw; e.slope = slope;
   e.X = X; e.dY = dY; e.post = post; e.coef0 = c0; e.coef1 = c1; e.mean = save_mean; e.invstd = save_invstd;
-  e.gamma = gamma; e.post_out = post_out; e.drop = drop; e.out = dX;
+  e.gamma = gamma; e.post_out = post_out; e.drop = drop; e.out = dX; e.nv = nvalid;
   const long n4 = rows * C / 4;
   hipLaunchKernelGGL(cgl_eltwise, dim3((unsigned)std::min<long>((n4 + 255) / 256, 8192)), dim3(256), 0, s, e);
   return (int)hipGetLastError();
@@ -3460,8 +3573,8 @@ int cgl_bn2d_bwd_stats(const double* part, int R, const float* dY, const float* 
 
 int cgl_bn2d_bwd(const float* dY, const float* post, const float* X, int n, int hw, int C, int groups,
                  const float* save_mean, const float* save_invstd, const float* gamma, float slope,
-                 const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta, void* ws,
-                 int64_t wsb, void* stream) {
+                 const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta,
+                 const int* nvalid, void* ws, int64_t wsb, void* stream) {
   if (!dY || !X || !save_mean || !save_invstd || !gamma || !dX || !ws || !al16(ws)) return CGL_E_ARG;
   if (!al16(dY) || !al16(X) || !al16(dX) || (post && !al16(post)) || (post_out && !al16(post_out))) return CGL_E_ARG;
   if (!al16(save_mean) || !al16(save_invstd) || !al16(gamma) || (drop && !al16(drop))) return CGL_E_ARG;
@@ -3486,13 +3599,14 @@ int cgl_bn2d_bwd(const float* dY, const float* post, const float* X, int n, int 
   f.part = part; f.C = C; f.groups = groups; f.chunks_per_group = (int)(gr / R); f.R = R; f.gr = (int)gr;
   f.mode = 1; f.gamma = gamma; f.save_invstd = const_cast<float*>(save_invstd); f.coef0 = c0; f.coef1 = c1;
   f.dgamma = dgamma; f.dbeta = dbeta;
+  f.nv = nvalid; f.hw = hw;
   f.nocache = fin_nocache();
   hipLaunchKernelGGL(cgl_bn_finalize, dim3(C), dim3(256), 0, s, f);
   CglEltArgs e;
   std::memset(&e, 0, sizeof(e));
   e.mode = 1; e.rows = (int)rows; e.C = C; e.gr = (int)gr; e.hw = hw; e.slope = slope;
   e.X = X; e.dY = dY; e.post = post; e.coef0 = c0; e.coef1 = c1; e.mean = save_mean; e.invstd = save_invstd;
-  e.gamma = gamma; e.post_out = post_out; e.drop = drop; e.out = dX;
+  e.gamma = gamma; e.post_out = post_out; e.drop = drop; e.out = dX; e.nv = nvalid;
   const long n4 = rows * C / 4;
   hipLaunchKernelGGL(cgl_eltwise, dim3((unsigned)std::min<long>((n4 + 255) / 256, 8192)), dim3(256), 0, s, e);
   return (int)hipGetLastError();
@@ -3596,11 +3710,11 @@ int cgl_nhwc_to_nchw(const float* X, float* Y, int n, int c, int hw, void* strea
 }
 
 int cgl_adv_loss(const float* x, int M, int C, int loss, int target, double weight, float* loss_out, float* grad,
-                 void* stream) {
+                 const int* nvalid, void* stream) {
   if (!x || M < 1 || loss < 0 || loss > 3 || (target != 0 && target != 1)) return CGL_E_ARG;
   if ((loss == 0) != (C == 2) || (loss != 0 && C != 1)) return CGL_E_ARG;
   hipLaunchKernelGGL(cgl_adv_loss_k, dim3(1), dim3(256), 0, (hipStream_t)stream, x, M, C, loss, target,
-                     (float)weight, loss_out, grad);
+                     (float)weight, loss_out, grad, nvalid);
   return (int)hipGetLastError();
 }
 
@@ -3691,12 +3805,12 @@ int cgl_dropout2d_masks_dev(int nm, float* const* masks, const int* n, const int
 }
 
 int cgl_sample_rows_dev(const float* src, int n_src, int nrows, int row_floats, unsigned long long seed,
-                        const int* round_dev, float* dst, void* stream) {
-  if (!src || !dst || !round_dev || nrows < 1 || n_src < nrows || row_floats < 4 || row_floats % 4 ||
-      ((uintptr_t)src & 15) || ((uintptr_t)dst & 15))
+                        const int* round_dev, float* dst, int* nv_out, void* stream) {
+  if (!src || !dst || !round_dev || nrows < 1 || n_src < 1 || (!nv_out && n_src < nrows) || row_floats < 4 ||
+      row_floats % 4 || ((uintptr_t)src & 15) || ((uintptr_t)dst & 15))
     return CGL_E_ARG;
   hipLaunchKernelGGL(cgl_sample_rows_k, dim3(nrows), dim3(256), 0, (hipStream_t)stream, src, n_src, nrows, row_floats,
-                     seed, round_dev, dst);
+                     seed, round_dev, dst, nv_out);
   return (int)hipGetLastError();
 }
 

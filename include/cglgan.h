@@ -294,7 +294,8 @@ int cgl_conv3x3_bwd_data_packed(const float* dY, const float* W, const float* Wp
 int64_t cgl_conv3x3_stat_chunks(int n, int h, int w, int cin, int cout, int stride, int up, int groups);
 int cgl_conv3x3_fwd_packed_stats(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w,
                                  int cin, int cout, int stride, int up, int act, float slope, const float* drop,
-                                 int groups, double* part, void* workspace, int64_t ws_bytes, void* stream);
+                                 int groups, double* part, const int* nvalid, void* workspace, int64_t ws_bytes,
+                                 void* stream);
 /* cgl_conv3x3_fwd_packed(_stats) whose input X is the PRE-BatchNorm2d map of a bn2d_fwd_stats_coef call: the
  * BatchNorm (+ LeakyReLU when in_act = CGL_EPI_ACT_LEAKY) is applied to each operand as it is loaded, from
  * in_coef = [2][in_groups][cin] (scale, then shift, per forward call of n / in_groups images), with
@@ -323,11 +324,17 @@ int cgl_dense_bwd_data_packed(const float* dY, const float* Wp, float* dX, int M
 /* nn.BatchNorm2d(C, eps, momentum) [+ LeakyReLU(slope) when act == 1] on NHWC X[n][hw][C]
  * (model/lsgan.py:13,17,80).  `groups` independent forward calls are stacked along n (statistics
  * per group, running stats updated group by group in call order); save_mean / save_invstd are
- * [groups][C] (may be null).  train == 0: running statistics (eval). */
+ * [groups][C] (may be null).  train == 0: running statistics (eval).
+ * nvalid (device int32, may be null; here and in the _stats / bwd variants, cgl_conv3x3_fwd_packed_stats
+ * and cgl_adv_loss): the first call is a SHORT batch -- only its first *nvalid images are data (the D step's
+ * real call on DataLoader's short final batch, capgan.py:282,326-331); the rest of the call's n / groups
+ * images are padding: left out of its statistics (mean / variance over *nvalid images, running variance
+ * unbiased over them) and given a zero input gradient in the backward. */
 int64_t cgl_bn2d_workspace_bytes(int n, int hw, int C, int groups);
 int cgl_bn2d_fwd(const float* X, int n, int hw, int C, int groups, const float* gamma, const float* beta, double eps,
                  double momentum, float* running_mean, float* running_var, int train, int act, float slope, float* Y,
-                 float* save_mean, float* save_invstd, void* workspace, int64_t ws_bytes, void* stream);
+                 float* save_mean, float* save_invstd, const int* nvalid, void* workspace, int64_t ws_bytes,
+                 void* stream);
 /* Train-mode backward: dY is the gradient of the BatchNorm output, or of LeakyReLU(output) when
  * `post` (that activation's output) is given.  The result is optionally multiplied by
  * LeakyReLU'(post_out) and the Dropout2d scale drop[n][C] (the Conv -> LeakyReLU -> Dropout2d ->
@@ -340,7 +347,7 @@ int64_t cgl_bn2d_stats_scratch_bytes(int C, int groups);
 int cgl_bn2d_fwd_stats(const double* part, int R, const float* X, int n, int hw, int C, int groups, const float* gamma,
                        const float* beta, double eps, double momentum, float* running_mean, float* running_var,
                        int act, float slope, float* Y, float* save_mean, float* save_invstd, void* scratch,
-                       void* workspace, int64_t ws_bytes, void* stream);
+                       const int* nvalid, void* workspace, int64_t ws_bytes, void* stream);
 /* cgl_bn2d_fwd_stats, also writing the per-(group, channel) scale / shift it applies into coef
  * ([2][groups][C]: scale, then shift; may be null) and applying them to images [apply_img0, n) only:
  * the rest is left for a consumer that folds the BatchNorm into its operand load
@@ -348,16 +355,17 @@ int cgl_bn2d_fwd_stats(const double* part, int R, const float* X, int n, int hw,
 int cgl_bn2d_fwd_stats_coef(const double* part, int R, const float* X, int n, int hw, int C, int groups,
                             const float* gamma, const float* beta, double eps, double momentum, float* running_mean,
                             float* running_var, int act, float slope, float* Y, float* save_mean, float* save_invstd,
-                            void* scratch, float* coef, int apply_img0, void* ws, int64_t wsb, void* stream);
+                            void* scratch, float* coef, int apply_img0, const int* nvalid, void* ws, int64_t wsb,
+                            void* stream);
 /* cgl_bn2d_bwd from backward partials already computed (cgl_conv3x3_bwd_data_packed_stats, R = 32). */
 int cgl_bn2d_bwd_stats(const double* part, int R, const float* dY, const float* post, const float* X, int n, int hw,
                        int C, int groups, const float* save_mean, const float* save_invstd, const float* gamma,
                        float slope, const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta,
-                       void* workspace, int64_t ws_bytes, void* stream);
+                       const int* nvalid, void* workspace, int64_t ws_bytes, void* stream);
 int cgl_bn2d_bwd(const float* dY, const float* post, const float* X, int n, int hw, int C, int groups,
                  const float* save_mean, const float* save_invstd, const float* gamma, float slope,
-                 const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta, void* workspace,
-                 int64_t ws_bytes, void* stream);
+                 const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta,
+                 const int* nvalid, void* workspace, int64_t ws_bytes, void* stream);
 /* dX = dY * LeakyReLU'(post) * drop[n][C] (Dropout2d + LeakyReLU backward; post / drop may be
  * null), or with tanh_y != 0: dX = dY * (1 - post^2) (Tanh backward, post = the Tanh output). */
 int cgl_act_drop_bwd(const float* dY, const float* post, const float* drop, int n, int hw, int C, float slope,
@@ -386,7 +394,7 @@ int cgl_dense1_fwd_nhwc(const float* X, const float* W, const float* b, float* Y
  * (CGLGAN/2DMG/main.py:336), 2 MSELoss (LSGAN objective of model/lsgan.py's D), 3 Sigmoid + BCELoss
  * on logits.  target 0 (fake) or 1 (valid); loss_out: device scalar. */
 int cgl_adv_loss(const float* x, int M, int C, int loss, int target, double weight, float* loss_out, float* grad,
-                 void* stream);
+                 const int* nvalid, void* stream);
 /* Exchange weighting: alpha = weights(weighting, lambda, beta, losses[n]) (CGL_WEIGHT_*, the
  * reference's Server.train formulas), then x[0:nx] *= alpha[rank] in place (this worker's
  * contribution before the all-reduce(sum)); alpha_out[n] (device, may be null) receives every alpha.
@@ -418,11 +426,13 @@ int cgl_dropout2d_masks_dev(int nm, float* const* masks, const int* n, const int
 int cgl_adam_multi_dev(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
                        const int64_t* n, const int* step_dev, double lr, double beta1, double beta2, double eps,
                        void* stream);
-/* dst[r] = src[perm_e(pos % per)] for r < nrows, pos = (*round_dev) * nrows + r, data epoch e = pos / per
- * (per = whole batches per pass), perm_e a keyed Feistel permutation of [0, n_src) per data epoch
- * (DataLoader(shuffle=True) with drop_last semantics); rows of row_floats (% 4 == 0) floats, 16-byte aligned */
+/* The real batch of round *round_dev, DataLoader(shuffle=True) over the n_src resident rows
+ * (capgan.py:282,326-331): each pass is a keyed Feistel permutation of [0, n_src) cut into
+ * ceil(n_src / nrows) batches, the last one short; *nv_out receives the batch's real rows (rows past
+ * them copy a valid dummy row).  nv_out null: drop_last (whole batches only: pos = round * nrows + r,
+ * data epoch pos / per, per = whole batches per pass).  Rows of row_floats (% 4 == 0) floats, 16-byte aligned. */
 int cgl_sample_rows_dev(const float* src, int n_src, int nrows, int row_floats, unsigned long long seed,
-                        const int* round_dev, float* dst, void* stream);
+                        const int* round_dev, float* dst, int* nv_out, void* stream);
 /* p[i] += v for i < n (<= 64): advances the device round state */
 int cgl_counters_add(int* p, int n, int v, void* stream);
 

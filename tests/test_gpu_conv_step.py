@@ -117,8 +117,8 @@ def _run(B, loss, seed=3, rounds=1, follow_gpu=True):
     d_calls = []
     fwd = st._d_forward
 
-    def rec(x, n, groups, masks):      # keep each D forward call's LeakyReLU outputs (the G-loss pass
-        fwd(x, n, groups, masks)       # reuses the D-step buffers)
+    def rec(x, n, groups, masks, **kw):   # keep each D forward call's LeakyReLU outputs (the G-loss pass
+        fwd(x, n, groups, masks, **kw)    # reuses the D-step buffers)
         d_calls.append([q[:n].clone() for q in st.q])
     st._d_forward = rec
     outs = []
