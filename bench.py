@@ -143,7 +143,7 @@ def _latest_profile(names):
 
 def traffic_per_gemm_launch():
     """HBM-side bytes per GEMM dispatch (every cgl_gemm_f32 instantiation, dispatch-weighted) from the
-    newest committed FETCH_SIZE / WRITE_SIZE passes (tools/run_r03_traffic.sh -> tools/pmc_traffic.py).
+    newest committed FETCH_SIZE / WRITE_SIZE passes (tools/gpu_session.sh traffic -> tools/pmc_traffic.py).
     A static, labelled measurement: PMC passes cannot run inside the timed bench, so roofline.traffic
     names the profile file and the commit it was measured at (traffic_source).  None when absent."""
     name, d = _latest_profile(["r03_traffic.json", "r02_traffic.json"])

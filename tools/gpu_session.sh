@@ -1,0 +1,70 @@
+#!/bin/bash
+# One GPU-box session of named steps, each under its own time limit; a failing step ends the session.
+#   bash tools/gpu_session.sh TAG step [step ...]        (outputs under gpurun_out/TAG/)
+# steps:
+#   tests        the whole pytest -m gpu suite                      -> gputest.log
+#   tests:FILES  a subset (comma-separated test files)              -> gputest.log
+#   smoke        __graft_entry__.smoke()                            -> smoke.log
+#   bench        bench.py default line (N = 1, with CPU baseline)   -> bench.json
+#   bench:ARGS   bench.py with ARGS (commas become spaces)          -> bench_<n>.json
+#   lsgan        bench.py --model lsgan --no-cpu-baseline           -> bench_lsgan.json
+#   prof         rocprofv3 --kernel-trace --stats of a short MLP bench -> prof/ (kernel_stats.csv)
+#   proflsgan    the same for the conv round                        -> prof_lsgan/
+#   traffic      FETCH_SIZE and WRITE_SIZE passes (one counter per run) of the MLP bench -> mlp_FETCH_SIZE/ ...
+#   tiles[:ARGS] tools/tile_search.py (in-round per-descriptor tile search) -> tile_search.json / .log
+#   ab:T1=ENV1;T2=ENV2   the MLP bench under env settings, interleaved x3 -> ab_<T>_<i>.json
+#   rccl         the RCCL world-1 worker with the split-round timing -> rccl.log
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=$1; shift
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd $R
+n=0
+for st in "$@"; do
+  n=$((n + 1))
+  name=${st%%:*}; arg=""; [ "$name" != "$st" ] && arg=${st#*:}
+  echo "[$(date +%T)] step $n: $st" | tee -a $O/session.log
+  case $name in
+    tests)
+      files=tests; [ -n "$arg" ] && files=${arg//,/ }
+      timeout -k 10 1200 python3 -u -m pytest $files -m gpu -v --timeout 300 --timeout-method thread > $O/gputest.log 2>&1
+      rc=$?; echo "pytest rc=$rc" >> $O/gputest.log; tail -3 $O/gputest.log; [ $rc -le 1 ] || exit $rc ;;
+    smoke)
+      timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $? ;;
+    bench)
+      if [ -n "$arg" ]; then
+        timeout -k 10 400 python3 -u bench.py ${arg//,/ } > $O/bench_$n.json 2> $O/bench_$n.err || exit $?
+      else
+        timeout -k 10 400 python3 -u bench.py > $O/bench.json 2> $O/bench.err || exit $?
+      fi ;;
+    lsgan)
+      timeout -k 10 400 python3 -u bench.py --model lsgan --no-cpu-baseline > $O/bench_lsgan.json 2> $O/bench_lsgan.err || exit $? ;;
+    prof)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
+        python3 $R/bench.py --steps 50 --warmup 10 --no-cpu-baseline > $O/prof.log 2>&1) || exit $? ;;
+    proflsgan)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_lsgan -o run -- \
+        python3 $R/bench.py --model lsgan --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_lsgan.log 2>&1) || exit $? ;;
+    traffic)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/mlp_$c -o run -- \
+          python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/mlp_$c.log 2>&1) || exit $?
+      done ;;
+    tiles)
+      timeout -k 10 600 python3 -u tools/tile_search.py ${arg//,/ } --out $O/tile_search.json > $O/tile_search.log 2>&1 || exit $? ;;
+    ab)
+      IFS=';' read -ra pairs <<< "$arg"
+      for i in 1 2 3; do
+        for kv in "${pairs[@]}"; do
+          t=${kv%%=*}; envs=${kv#*=}
+          env $envs timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --steps 400 > $O/ab_${t}_$i.json 2> $O/ab_${t}_$i.err || exit $?
+        done
+      done ;;
+    rccl)
+      timeout -k 10 300 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+        --master-port 29517 tests/rccl_world1_worker.py --time > $O/rccl.log 2>&1 || exit $? ;;
+    *) echo "unknown step $st"; exit 2 ;;
+  esac
+done
+echo done > $O/done.txt

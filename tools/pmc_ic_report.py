@@ -1,4 +1,4 @@
-"""Per-dispatch-shape means of the I-cache / wait counters of a tools/run_r03_icache.sh pass."""
+"""Per-dispatch-shape means of the I-cache / wait counters of an I-cache counter pass (tools/pmc_icache.sh)."""
 import collections
 import csv
 import glob
