@@ -348,8 +348,33 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     const int xcd = local & 7, pos = local >> 3, q = nwg >> 3, r = nwg & 7;
     unit = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
   }
-  const int tile = unit / KS, kslice = unit - tile * KS;
-  const int tn = tile / d->tiles_m, tm = tile % d->tiles_m;
+  int tile = unit / KS;
+  const int kslice = unit - tile * KS;
+  int tn, tm;
+  if (d->xcd_pm > 0 && nwg >= 16) {
+    // XCD blocking: position `tile` of the XCD-contiguous sequence is tile `tile` of the slab-major order --
+    // slab x = (row slab x / pn, column slab x % pn) of a pm x pn cut of the tile grid, tiles m-minor inside
+    // a slab -- so the XCD running a range of the sequence reads one row slab of A and one column slab of B
+    // instead of all of A (the n-major order) or all of B.  Bijective for any grid.
+    const int pm = d->xcd_pm, pn = 8 / pm, TMt = d->tiles_m, TNt = d->tiles_n;
+    int rest = tile, x = 0, r0 = 0, r1 = 0, c0 = 0, c1 = 0;
+    for (; x < 8; ++x) {
+      r0 = (x / pn) * TMt / pm;
+      r1 = (x / pn + 1) * TMt / pm;
+      c0 = (x % pn) * TNt / pn;
+      c1 = (x % pn + 1) * TNt / pn;
+      const int sz = (r1 - r0) * (c1 - c0);
+      if (rest < sz) break;
+      rest -= sz;
+    }
+    const int h = r1 - r0;
+    tn = c0 + rest / h;
+    tm = r0 + rest % h;
+    tile = tn * TMt + tm;
+  } else {
+    tn = tile / d->tiles_m;
+    tm = tile % d->tiles_m;
+  }
   const int BM = 32 * TM * WM;
   const int m0 = tm * BM + wm * 32 * TM;            // first row of this wave's tile
   const int n0 = (tn * WN + wn) * 32 * TN;          // first column of this wave's tile

@@ -111,6 +111,8 @@ struct CglGemmDesc {
   int WM, WN, WK;         // wave arrangement, WM*WN*WK == 4
   int tiles_m, tiles_n;
   int wg_begin;           // first workgroup of this problem in a grouped launch
+  int xcd_pm;             // XCD blocking: the tile grid is cut into xcd_pm x (8 / xcd_pm) slabs, slab x on XCD x
+                          // (its L2 then holds 1 / xcd_pm of A and xcd_pm / 8 of B); 0 = n-major ranges
   int layout;             // 0: NT (A[m][k], B[n][k]); 1: NN (A[m][k], B[k][n]); 2: TN (A[k][m], B[k][n])
   int a_vec, b_vec;       // 16-byte vector loads allowed along each operand's contiguous dim
   int TM, TN;             // 32x32 accumulator blocks per wave (1x1 or 2x2)

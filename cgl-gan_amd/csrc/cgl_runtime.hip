@@ -585,6 +585,29 @@ bool gemm_tile_at_env(int i, int* o) {
   return false;
 }
 
+// XCD blocking of the tile order (cgl_gemm_body): the pm x (8 / pm) slab cut whose L2 working set -- every
+// XCD reads A / pm and B pm / 8 -- is smallest, i.e. the least fabric traffic A pn + B pm summed over the
+// XCDs (the n-major ranges, pm = 1, read all of A on every XCD).  CGL_XCD_BLOCK=0: n-major ranges;
+// =1/2/4/8: that pm where the grid allows it.
+void choose_xcd(CglGemmDesc& d) {
+  static int env = -2;
+  if (env == -2) env = getenv("CGL_XCD_BLOCK") ? atoi(getenv("CGL_XCD_BLOCK")) : -1;
+  d.xcd_pm = 0;
+  if (env == 0 || (long)d.tiles_m * d.tiles_n * (d.ksplit > 1 ? d.ksplit : 1) < 16) return;
+  const double A = (double)d.M * d.K, B = (double)(d.N - (d.layout != 0 ? d.b_ones_col : 0)) * d.K;
+  double best = 1e300;
+  for (int pm : {1, 2, 4, 8}) {
+    const int pn = 8 / pm;
+    if (pm > d.tiles_m || pn > d.tiles_n) continue;
+    if (env > 0 && pm != env) continue;
+    const double c = A * pn + B * pm;
+    if (c < best * (1.0 - 1e-9)) {
+      best = c;
+      d.xcd_pm = pm;
+    }
+  }
+}
+
 void set_tiles(CglGemmDesc& d, int wm, int wn, int wk, int t) {
   d.WM = wm;
   d.WN = wn;
@@ -646,6 +669,7 @@ void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
       }
     }
     d.tab_floats = cgl_gemm_tab_floats(d);
+    choose_xcd(d);
     L.abn = std::max(L.abn, d.a_bn);
     d.wg_begin = wg;
     wg += cgl_gemm_wgs(d);
@@ -661,8 +685,9 @@ void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
     for (int q = L.first; q < L.first + L.count; ++q) {
       const CglGemmDesc& d = c->gemm[q];
       fprintf(stderr, "gemm launch %zu: desc %d layout %d M %d N %d K %d WM %d WN %d WK %d TM %d TN %d tiles %dx%d "
-              "ks %d grid %d shmem %d blk %d vec %d/%d a_bn %d\n", ph.size(), q, d.layout, d.M, d.N, d.K, d.WM, d.WN,
-              d.WK, d.TM, d.TN, d.tiles_m, d.tiles_n, d.ksplit, L.grid, L.shmem, L.blk, d.a_vec, d.b_vec, d.a_bn);
+              "ks %d grid %d shmem %d blk %d vec %d/%d a_bn %d xcd_pm %d\n", ph.size(), q, d.layout, d.M, d.N, d.K, d.WM,
+              d.WN, d.WK, d.TM, d.TN, d.tiles_m, d.tiles_n, d.ksplit, L.grid, L.shmem, L.blk, d.a_vec, d.b_vec, d.a_bn,
+              d.xcd_pm);
     }
   }
   ph.push_back(L);
@@ -1850,6 +1875,7 @@ static int single_gemm(CglGemmDesc& d, void*, int64_t, hipStream_t s) {
   d.wg_begin = 0;
   set_vec(d);
   d.ksplit = 1;
+  choose_xcd(d);
   const int grid = cgl_gemm_wgs(d), shmem = cgl_gemm_stage_bytes(d);
   if (d.TM == 2)
     klaunch(cgl_gemm_f32_arg<2, 2>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d);
@@ -1941,6 +1967,7 @@ int cgl_linear_prepare(int op, const float* A, const float* B, const float* bias
   d.wg_begin = 0;
   set_vec(d);
   d.ksplit = 1;
+  choose_xcd(d);
   // the descriptor buffer may have been allocated / zeroed on a non-blocking stream that the null
   // stream's copy does not wait for: drain the device so that no pending fill overwrites it
   HIPCHK(hipDeviceSynchronize());
