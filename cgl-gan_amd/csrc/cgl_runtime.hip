@@ -587,11 +587,13 @@ bool gemm_tile_at_env(int i, int* o) {
 
 // XCD blocking of the tile order (cgl_gemm_body): the pm x (8 / pm) slab cut whose L2 working set -- every
 // XCD reads A / pm and B pm / 8 -- is smallest, i.e. the least fabric traffic A pn + B pm summed over the
-// XCDs (the n-major ranges, pm = 1, read all of A on every XCD).  CGL_XCD_BLOCK=0: n-major ranges;
-// =1/2/4/8: that pm where the grid allows it.
+// XCDs (the n-major ranges, pm = 1, read all of A on every XCD).  Measured SLOWER in the B = 256 round
+// (0.2666 vs 0.2464 ms, interleaved x3, profiles/r04_xcd_block_ab.txt): the n-major ranges keep a weight
+// panel hot in one XCD's L2 while consecutive workgroups sweep the (smaller) activation rows.  Opt-in:
+// CGL_XCD_BLOCK=-1 cost model, =1/2/4/8 that pm where the grid allows it; default 0 (n-major ranges).
 void choose_xcd(CglGemmDesc& d) {
   static int env = -2;
-  if (env == -2) env = getenv("CGL_XCD_BLOCK") ? atoi(getenv("CGL_XCD_BLOCK")) : -1;
+  if (env == -2) env = getenv("CGL_XCD_BLOCK") ? atoi(getenv("CGL_XCD_BLOCK")) : 0;
   d.xcd_pm = 0;
   if (env == 0 || (long)d.tiles_m * d.tiles_n * (d.ksplit > 1 ? d.ksplit : 1) < 16) return;
   const double A = (double)d.M * d.K, B = (double)(d.N - (d.layout != 0 ? d.b_ones_col : 0)) * d.K;

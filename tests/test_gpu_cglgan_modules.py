@@ -148,10 +148,20 @@ def test_cglgan_ring_round_through_modules_vs_oracle():
     finally:
         torch.set_default_dtype(prev)
     fails = []
-    for name, key in (("d_losses", "d_losses"), ("g_losses", "g_losses"), ("F", "F"), ("lam", "lam")):
+    for name, key in (("d_losses", "d_losses"), ("g_losses", "g_losses"), ("F", "F")):
         ok, e, a = within(out[name].cpu().reshape(-1), r32[key].reshape(-1), r64[key].reshape(-1), tol=STEP_TOL)
         if not ok:
             fails.append((name, e, a))
+    # lambda = 10 (sum l^2 gamma - sum l gamma F_gamma) (CGLGAN/2DMG/main.py:273-274) is a difference of two
+    # nearly equal sums: judged as the formula applied to the round's own (already judged) losses, within the
+    # fp32 rounding of its terms
+    l = out["g_losses"].double().cpu()
+    gam = torch.softmax(0.0 * l, dim=0)
+    Fg = (gam * l).sum()
+    terms = torch.cat([l * l * gam, l * gam * Fg])
+    lam_ref = 10 * ((l * l * gam).sum() - (l * gam * Fg).sum())
+    if abs(float(out["lam"]) - float(lam_ref)) > 10 * 8 * 2.0 ** -24 * float(terms.abs().sum()) + 1e-12:
+        fails.append(("lam", float(out["lam"]), float(lam_ref)))
     g32 = {k: v for n in [srv.G.trunk] + list(srv.G.heads) for k, v in n.params.items()}
     g64 = {k: v for n in [srv64.G.trunk] + list(srv64.G.heads) for k, v in n.params.items()}
     for k, p in net_g.named_parameters():
@@ -207,6 +217,9 @@ def test_module_forward_backward_graph_capture_bitwise():
     eager = {"out": out_e.detach().clone(), "loss": loss_e.detach().clone(),
              "grads": [p.grad.detach().clone() for p in list(G.parameters()) + list(D.parameters())],
              "sd": copy.deepcopy(G.state_dict())}
+    # drop the eager autograd graph: its AccumulateGrad nodes (bound to the default stream) would otherwise
+    # be reused by the captured backward (torch's capture recipe: no graph kept alive across the capture)
+    del out_e, loss_e
     # capture (torch's recipe: warm up on a side stream first), then restore the state and replay
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
