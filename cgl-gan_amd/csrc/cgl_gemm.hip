@@ -860,6 +860,40 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     }
   }
 
+  // the tile's stores first: they drain while the BatchNorm partials below are reduced (the partials only
+  // read the accumulators)
+  if (owner) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + 32 * j + li;
+      if (col >= N) continue;
+      const bool ones_col = b_ones && col == N - 1;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const float* v = (const float*)&acc[i][j];
+        if (ones_col) {
+          if (d->bias_out) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
+              if (row < M) gst(d->bias_out + row, v[r]);
+            }
+            if constexpr (ADAM) cgl_epi_adam(d, d->ad_pb, d->ad_mb, d->ad_vb, rbase + 32 * i, M, 0, 1, v);
+          }
+        } else {
+          float* __restrict__ C = d->C;
+          const int ldc = d->ldc;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
+            if (row < M) gst(C + (long)row * ldc + col, v[r]);
+          }
+          if constexpr (ADAM) cgl_epi_adam(d, d->ad_p, d->ad_m, d->ad_v, rbase + 32 * i, M, col, ldc, v);
+        }
+      }
+    }
+  }
+
   // backward BatchNorm partials of the stored gradient dy (the next GEMM's a_bn 2): per
   // (row tile, column) {sum dy, sum (y - mean) dy} in double over the workgroup's rows (lane
   // rows, then the two lane halves, then the WM waves of the column, fixed order)
@@ -893,13 +927,19 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
       }
       Sd += __shfl_xor(Sd, 32);
       Dd += __shfl_xor(Dd, 32);
-      if (owner && lh == 0) {
+      if (WM == 1) {           // one wave row per column tile: its sums are the tile's (no LDS, no barrier)
+        if (owner && lh == 0 && col < N) {
+          double* p = d->bnb_part + ((long)tm * N + col) * 2;
+          *(CGL_GLOBAL double*)p = Sd;
+          *(CGL_GLOBAL double*)(p + 1) = Dd;
+        }
+      } else if (owner && lh == 0) {
         s_bnd[(((wm * WN + wn) * TN + j) * 32 + li) * 2] = Sd;
         s_bnd[(((wm * WN + wn) * TN + j) * 32 + li) * 2 + 1] = Dd;
       }
     }
-    __syncthreads();
-    if (owner && wm == 0 && lh == 0) {
+    if (WM > 1) __syncthreads();
+    if (WM > 1 && owner && wm == 0 && lh == 0) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = n0 + 32 * j + li;
@@ -928,7 +968,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     const int gfirst = trow0 / gr;
     const int gsplit = (gfirst + 1) * gr;   // first row of slot 1
     float* s_st = (float*)s_bnd;            // [WM WN TN 32][3] {n, sum, M2} (s_bnd is free here)
-    if (d->bnb_part) __syncthreads();
+    if (d->bnb_part && WM > 1) __syncthreads();
     for (int s = 0; s < 2; ++s) {
       const int ra = max(trow0, (gfirst + s) * gr), rb = min(min(trow0 + BM, M), (gfirst + s + 1) * gr);
       if (rb - ra <= 0) {                   // workgroup-uniform
@@ -983,13 +1023,21 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
           sum = sa + s2;
           m2 = ma + m22 + (nt > 0.f ? dl * dl * (ca * c2 / nt) : 0.f);
         }
-        if (owner && lh == 0) {
+        if (WM == 1) {         // one wave row per column tile: its merge is the tile's (no LDS, no barrier;
+          const int col = n0 + 32 * j + li;   // the same values the one-entry merge below would store)
+          if (owner && lh == 0 && col < N) {
+            float* p = d->stat_part + ((long)(tm * 2 + s) * N + col) * 2;
+            gst(p, 0.f + sum);
+            gst(p + 1, 0.f + m2);
+          }
+        } else if (owner && lh == 0) {
           float* e = s_st + (((wm * WN + wn) * TN + j) * 32 + li) * 3;
           e[0] = cn;
           e[1] = sum;
           e[2] = m2;
         }
       }
+      if (WM == 1) continue;
       __syncthreads();
       if (owner && wm == 0 && lh == 0) {
 #pragma unroll
@@ -1038,37 +1086,6 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     }
   }
 
-  if (owner) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = n0 + 32 * j + li;
-      if (col >= N) continue;
-      const bool ones_col = b_ones && col == N - 1;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const float* v = (const float*)&acc[i][j];
-        if (ones_col) {
-          if (d->bias_out) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
-              if (row < M) gst(d->bias_out + row, v[r]);
-            }
-            if constexpr (ADAM) cgl_epi_adam(d, d->ad_pb, d->ad_mb, d->ad_vb, rbase + 32 * i, M, 0, 1, v);
-          }
-        } else {
-          float* __restrict__ C = d->C;
-          const int ldc = d->ldc;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
-            if (row < M) gst(C + (long)row * ldc + col, v[r]);
-          }
-          if constexpr (ADAM) cgl_epi_adam(d, d->ad_p, d->ad_m, d->ad_v, rbase + 32 * i, M, col, ldc, v);
-        }
-      }
-    }
-  }
 }
 
 // One kernel per per-wave block shape (TM x TN), shared by every GEMM of the step; a grouped
