@@ -830,6 +830,137 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad(CglConvLaunch args) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Weight gradient with LDS-staged panels (the large upsampling convs of the LSGAN generator: 16K - 64K
+// pixels per phase problem, N = 64 / 128 output channels, K = 512).  A workgroup owns an R x C result tile
+// (R = 64 WM output channels, C = 64 WN im2col columns; 4 waves of 2 x 2 32x32 blocks) over one pixel
+// split.  Per 16-pixel chunk its 256 threads fetch the dY panel [16][R] and the im2col panel [16][C] with
+// 16-byte loads (4 channels of one pixel) and stage them in LDS, where WN waves share each dY element and
+// WM waves each X element: the wave-unit kernel's 4-byte fragment loads (one per MFMA operand and wave)
+// become a quarter of the load instructions and 1 / WN + 1 / WM of the bytes.  Chunk c + 2's loads are in
+// flight while chunk c is multiplied (two register sets, two LDS buffers, one barrier per chunk).  Same
+// partials [split][N][Kp] and k permutation as cgl_conv_wgrad (pixel 8 lh + q of a chunk is lane half lh's
+// k of MFMA step q), so cgl_conv_wgrad_reduce is shared.  Requirements: wgrad_lds_ok.
+#define CGL_WLDS_PAD 4
+template <int WM, int WN>
+__global__ __launch_bounds__(256, 2) void cgl_conv_wgrad_lds(CglConvLaunch args) {
+  (void)args;
+  constexpr int R = 64 * WM, C = 64 * WN;
+  constexpr int RP = R + CGL_WLDS_PAD, CP = C + CGL_WLDS_PAD;   // padded rows: the lane halves (8 rows
+                                                                 // apart) land on disjoint banks
+  constexpr int FA = R / 4, FB = C / 4;                          // float4 per pixel row of each panel
+  constexpr int NA = 16 * FA / 256, NB = 16 * FB / 256;          // float4 loads per thread and chunk
+  static_assert(WM * WN == 4 && NA >= 1 && NB >= 1, "4 waves, whole panels");
+  __shared__ __attribute__((aligned(16))) float sa[2][16 * RP];
+  __shared__ __attribute__((aligned(16))) float sb[2][16 * CP];
+  CglKL L = cgl_conv_args();
+  const int pi = cgl_conv_prob(L, blockIdx.x);
+  CglKP P = &L->p[pi];
+  const int tiles = P->tiles_m * P->tiles_n;
+  const int local = cgl_xcd_tile(blockIdx.x - P->wg_begin, tiles * P->splits);
+  const int split = local / tiles, tile = local - split * tiles;
+  const int n0 = (tile / P->tiles_n) * R, k0 = (tile % P->tiles_n) * C;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, li = lane & 31, lhf = lane >> 5;
+  const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+  const int N = P->N, Kp = P->Kp, Cin = P->Cin;
+  const int IH = P->IH, IW = P->IW, ish = P->ish, XW = P->XW, XH = P->XH;
+  const int ldy = P->ldy, YH = P->YH, YW = P->YW;
+  const int osy = P->osy, osx = P->osx, ooy = P->ooy, oox = P->oox, isy = P->isy, isx = P->isx;
+  const int lw = __builtin_ctz(P->OW), lhw = __builtin_ctz(P->OW) + __builtin_ctz(P->OH);
+  const int mw = P->OW - 1, mh = P->OH - 1;
+  const float* __restrict__ X = P->X;
+  const float* __restrict__ dY = P->Y;
+  // this thread's fixed panel columns: dY channel n0 + 4 fa, im2col columns k0 + 4 fb .. + 3 (one tap)
+  const int fa = tid % FA, pa = tid / FA;
+  const int fb = tid % FB, pb = tid / FB;
+  const int kk = k0 + 4 * fb;
+  const int tap = kk / Cin, ci = kk - tap * Cin;
+  const int cdy = P->dy[tap / P->Tx], cdx = P->dx[tap - (tap / P->Tx) * P->Tx];
+
+  auto load = [&](int c, f32x4 (&ra)[NA], f32x4 (&rb)[NB]) {
+#pragma unroll
+    for (int r = 0; r < NA; ++r) {
+      const int m = c * 16 + pa + (256 / FA) * r;
+      const int ox = m & mw, oy = (m >> lw) & mh, img = m >> lhw;
+      ra[r] = *(gcf4p)(dY + (((long)img * YH + oy * osy + ooy) * YW + ox * osx + oox) * ldy + n0 + 4 * fa);
+    }
+#pragma unroll
+    for (int r = 0; r < NB; ++r) {
+      const int m = c * 16 + pb + (256 / FB) * r;
+      const int ox = m & mw, oy = (m >> lw) & mh, img = m >> lhw;
+      const int iy = oy * isy + cdy, ix = ox * isx + cdx;
+      const bool ok = (unsigned)iy < (unsigned)IH && (unsigned)ix < (unsigned)IW;
+      const long off = ok ? (((long)img * XH + (iy >> ish)) * XW + (ix >> ish)) * Cin + ci : ci;
+      const f32x4 v = *(gcf4p)(X + off);
+      rb[r] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto stage = [&](int buf, const f32x4 (&ra)[NA], const f32x4 (&rb)[NB]) {
+#pragma unroll
+    for (int r = 0; r < NA; ++r) *(f32x4*)&sa[buf][(pa + (256 / FA) * r) * RP + 4 * fa] = ra[r];
+#pragma unroll
+    for (int r = 0; r < NB; ++r) *(f32x4*)&sb[buf][(pb + (256 / FB) * r) * CP + 4 * fb] = rb[r];
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  auto compute = [&](int buf) {
+    const float* A = &sa[buf][wm * 64 + li];
+    const float* B = &sb[buf][wn * 64 + li];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int row = 8 * lhf + q;
+      const float a0 = A[row * RP], a1 = A[row * RP + 32];
+      const float b0 = B[row * CP], b1 = B[row * CP + 32];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+  };
+
+  const int nchk = P->M >> 4, splits = P->splits;
+  const int cb = (int)(((long)split * nchk) / splits), ce = (int)(((long)(split + 1) * nchk) / splits);
+  if (cb < ce) {
+    f32x4 r0a[NA], r0b[NB], r1a[NA], r1b[NB];
+    load(cb, r0a, r0b);
+    load(min(cb + 1, ce - 1), r1a, r1b);
+    stage(0, r0a, r0b);
+    __syncthreads();
+    int c = cb;
+    for (; c + 2 <= ce; c += 2) {
+      // buffer 0 holds chunk c, r1 chunk c + 1
+      load(min(c + 2, ce - 1), r0a, r0b);
+      compute(0);
+      stage(1, r1a, r1b);
+      __syncthreads();
+      load(min(c + 3, ce - 1), r1a, r1b);
+      compute(1);
+      stage(0, r0a, r0b);
+      __syncthreads();
+    }
+    if (c < ce) compute(0);   // an odd last chunk
+  }
+  float* __restrict__ part = P->part + (long)split * N * Kp;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int kc = k0 + wn * 64 + 32 * j + li;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = n0 + wm * 64 + 32 * i + 4 * lhf + (r & 3) + 8 * (r >> 2);
+        gst(part + (long)n * Kp + kc, acc[i][j][r]);
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // One-output-channel convolution on the vector ALUs (N == 1: Conv2d(64, 1) of the generator's
 // last layer, and the input gradient of the discriminator's Conv2d(1, 16)) -- an MFMA tile would
 // waste 31 of its 32 columns.  Channels run across lanes: L = Cin / 4 lanes own one pixel (one
@@ -3107,6 +3238,24 @@ bool wgrad_row_ok(const WgradPlan& pl) {
   return true;
 }
 
+// cgl_conv_wgrad_lds applies: no bias column, whole R x C tiles (N % R == 0, K % C == 0), 16-byte operand
+// rows (Cin % 4 == 0 so 4 columns are one tap, ldy % 4 == 0, aligned bases), whole 16-pixel chunks and
+// power-of-two output grids (shift / mask pixel decode).  Returns WM (WN = 4 / WM), 0 = not applicable.
+// CGL_WGRAD_LDS=0 keeps the wave-unit kernel (A/B).
+int wgrad_lds_wm(const WgradPlan& pl, bool bias_col, const float* dY, const float* X) {
+  static const int env = getenv("CGL_WGRAD_LDS") ? atoi(getenv("CGL_WGRAD_LDS")) : 1;
+  if (!env || bias_col || !al16(dY) || !al16(X)) return 0;
+  const int N = pl.P[0].N, K = pl.P[0].K;
+  const int wm = (N % 128 == 0 && K % 128 == 0) ? 2 : ((N % 64 == 0 && K % 256 == 0) ? 1 : 0);
+  if (!wm) return 0;
+  for (int i = 0; i < pl.np; ++i) {
+    const CglConvProb& P = pl.P[i];
+    if (P.N != N || P.K != K || P.Cin % 4 || P.ldy % 4 || P.M % 16 || P.M < 16 * 64) return 0;
+    if ((P.OW & (P.OW - 1)) || (P.OH & (P.OH - 1))) return 0;
+  }
+  return wm;
+}
+
 int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, float* dW, float* db, void* ws,
                          int64_t wsb, hipStream_t s) {
   if (!dY || !X || !dW || !ws || !al16(ws)) return CGL_E_ARG;
@@ -3163,7 +3312,21 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
     r.Ty[i] = P.Ty;
     for (int k = 0; k < 4; ++k) { r.ym[i][k] = P.ym[k]; r.xm[i][k] = P.xm[k]; }
   }
-  if (n1t)
+  const int lwm = valu ? 0 : wgrad_lds_wm(pl, bias_col, dY, X);
+  if (lwm) {
+    // workgroup tiles of 64 lwm x 256 / lwm over the plan's pixel splits (partials as sized by wgrad_plan)
+    int wgl = 0;
+    for (int i = 0; i < pl.np; ++i) {
+      CglConvProb& P = L.p[i];
+      P.tiles_m = P.N / (64 * lwm);
+      P.tiles_n = P.K / (256 / lwm);
+      P.wg_begin = wgl;
+      wgl += P.tiles_m * P.tiles_n * P.splits;
+    }
+    if (lwm == 2) hipLaunchKernelGGL((cgl_conv_wgrad_lds<2, 2>), dim3(wgl), dim3(256), 0, s, L);
+    else hipLaunchKernelGGL((cgl_conv_wgrad_lds<1, 4>), dim3(wgl), dim3(256), 0, s, L);
+  }
+  else if (n1t)
   {
     if (pl.P[0].Cin == 64 && pl.P[0].XW == 32 && pl.P[0].XH == 32 && pl.P[0].Ty * pl.P[0].Tx == 9)
     {

@@ -293,7 +293,15 @@ __device__ __forceinline__ void cgl_bn_bwd_body(const CglBnBwdDesc* __restrict__
   __shared__ double s_a[NRG][FPW], s_b[NRG][FPW];
   const int M = bd->M, F = bd->F;
   const int fl = threadIdx.x % FPW, rg = threadIdx.x / FPW;
-  const int f = blockIdx.x * FPW + fl;
+  // XCD-contiguous feature slices: workgroup b runs on XCD b % 8, so give each XCD a contiguous range of
+  // slices -- the 128 / (4 FPW) slices that share a row's 128-byte lines then fetch (and write) them through
+  // one L2 instead of up to four (FPW = 8: 4x the dA / post / Y fetch, profiles/r04_traffic.json)
+  int blk = blockIdx.x;
+  if (gridDim.x >= 16) {
+    const int nb = gridDim.x, xcd = blk & 7, pos = blk >> 3, q = nb >> 3, rr = nb & 7;
+    blk = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + pos;
+  }
+  const int f = blk * FPW + fl;
   const bool fok = f < F;
   const int fc = min(f, F - 1);
   const float sl = bd->slope;

@@ -619,6 +619,24 @@ void set_tiles(CglGemmDesc& d, int wm, int wn, int wk, int t) {
   d.tiles_n = (d.N + 32 * t * wn - 1) / (32 * t * wn);
 }
 
+// Measured table over the cost model (tools/tile_search.py, profiles/r04_tile_search.txt): the in-round
+// per-descriptor search of the B = 256 round found three problems where two wave rows sharing a column tile
+// with a 2-way k split beat the model's 1 x 1 x 4 (the two widest forward GEMMs of G, 512 x 1024 x 512 and
+// 512 x 784 x 1024, and G's 1024 x 513 x 256 weight gradient: -0.56 / -0.45 / -0.3 us each, -1.3 us combined
+// interleaved x5).  Keyed on the exact problem; everything else keeps the model.
+bool gemm_tile_pick(const CglGemmDesc& d, int* o) {
+  static const int tab[][7] = {{0, 512, 1024, 512, 2, 1, 2}, {0, 512, 784, 1024, 2, 1, 2}, {2, 1024, 513, 256, 2, 1, 2}};
+  if (getenv("CGL_TILE_TABLE") && atoi(getenv("CGL_TILE_TABLE")) == 0) return false;
+  for (auto& r : tab)
+    if (d.layout == r[0] && d.M == r[1] && d.N == r[2] && d.K == r[3]) {
+      o[0] = r[4];
+      o[1] = r[5];
+      o[2] = r[6];
+      return true;
+    }
+  return false;
+}
+
 // Add a grouped GEMM launch built from `descs` (workgroup offsets assigned here).
 void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> descs) {
   Launch L;
@@ -644,8 +662,11 @@ void push_gemm(cgl_gan* c, std::vector<Launch>& ph, std::vector<CglGemmDesc> des
   }
   for (int i = 0; i < (int)descs.size(); ++i) {
     CglGemmDesc& d = descs[i];
+    int pk[3];
     if (i < CGL_MAX_LAYERS * 4 && isf[i] && !d.a_bn)
       set_tiles(d, forced[i][0], forced[i][1], forced[i][2], blk);
+    else if (blk == 1 && !d.a_bn && !getenv("CGL_GEMM_TILE") && gemm_tile_pick(d, pk))
+      set_tiles(d, pk[0], pk[1], pk[2], 1);
     else if (d.TM != blk)
       choose_tiles(d, 0, blk);
   }

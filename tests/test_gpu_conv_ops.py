@@ -63,6 +63,10 @@ CONV_CASES = [
     (1, 5, 3, 16, 16, 1, 1, 1),       # ragged upsample
     (3, 7, 9, 64, 1, 1, 0, 2),        # one-output-channel conv, ragged (189 pixels: partial workgroups)
     (2, 20, 32, 64, 1, 1, 0, 2),      # tap-partial Conv2d(64, 1) with a partial 8-row tile
+    # >= 2^28 MACs (no bias column): the LDS-staged weight gradient (cgl_conv_wgrad_lds)
+    (16, 8, 8, 128, 128, 1, 1, 0),    # 128 x 128 workgroup tiles (WM = 2)
+    (8, 16, 16, 128, 64, 1, 1, 0),    # 64 x 256 workgroup tiles (WM = 1)
+    (32, 8, 8, 128, 128, 1, 0, 0),    # 9 direct taps, one tap per 128-column tile
 ]
 
 

@@ -11,8 +11,10 @@
 #   prof         rocprofv3 --kernel-trace --stats of a short MLP bench -> prof/ (kernel_stats.csv)
 #   proflsgan    the same for the conv round                        -> prof_lsgan/
 #   traffic      FETCH_SIZE and WRITE_SIZE passes (one counter per run) of the MLP bench -> mlp_FETCH_SIZE/ ...
+#   trafficlsgan the same two passes of the conv round (LSGAN bench)      -> lsgan_FETCH_SIZE/ ...
 #   tiles[:ARGS] tools/tile_search.py (in-round per-descriptor tile search) -> tile_search.json / .log
 #   ab:T1=ENV1;T2=ENV2   the MLP bench under env settings, interleaved x3 -> ab_<T>_<i>.json
+#   abl:T1=ENV1;T2=ENV2  the same for the LSGAN conv round, interleaved x2 -> abl_<T>_<i>.json
 #   rccl         the RCCL world-1 worker with the split-round timing -> rccl.log
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -48,8 +50,13 @@ for st in "$@"; do
         python3 $R/bench.py --model lsgan --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_lsgan.log 2>&1) || exit $? ;;
     traffic)
       for c in FETCH_SIZE WRITE_SIZE; do
-        (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/mlp_$c -o run -- \
+        (cd /tmp && export TMPDIR=/tmp CGL_PLAN_DEBUG=1 && timeout -s KILL 150 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/mlp_$c -o run -- \
           python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/mlp_$c.log 2>&1) || exit $?
+      done ;;
+    trafficlsgan)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 200 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/lsgan_$c -o run -- \
+          python3 $R/bench.py --model lsgan --steps 4 --warmup 2 --no-cpu-baseline > $O/lsgan_$c.log 2>&1) || exit $?
       done ;;
     tiles)
       timeout -k 10 600 python3 -u tools/tile_search.py ${arg//,/ } --out $O/tile_search.json > $O/tile_search.log 2>&1 || exit $? ;;
@@ -59,6 +66,14 @@ for st in "$@"; do
         for kv in "${pairs[@]}"; do
           t=${kv%%=*}; envs=${kv#*=}
           env $envs timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --steps 400 > $O/ab_${t}_$i.json 2> $O/ab_${t}_$i.err || exit $?
+        done
+      done ;;
+    abl)
+      IFS=';' read -ra pairs <<< "$arg"
+      for i in 1 2; do
+        for kv in "${pairs[@]}"; do
+          t=${kv%%=*}; envs=${kv#*=}
+          env $envs timeout -k 10 300 python3 -u bench.py --model lsgan --no-cpu-baseline > $O/abl_${t}_$i.json 2> $O/abl_${t}_$i.err || exit $?
         done
       done ;;
     rccl)

@@ -1,13 +1,15 @@
 #!/usr/bin/env python3
 """Per-launch durations and gaps of the graph-replayed MLP rounds from a rocprofv3 kernel trace.
 
-    python tools/graph_round_timeline.py KERNEL_TRACE.csv [--json OUT]
+    python tools/graph_round_timeline.py KERNEL_TRACE.csv [--json OUT] [--bench LOG]
 
 Rounds start at the fused prologue GEMM (cgl_gemm_pro).  Only rounds with the plan's full launch count and
 no host gap (graph replays back to back: the timed region) are used; per launch position the median of
 its duration, of the gap before it (previous end -> its start) and of the round period are reported, and
 the GEMM family's in-round average duration (cgl_gemm_f32 dispatches) -- the figure bench.py's
-roofline.avg_gemm_launch_us is checked against."""
+roofline.avg_gemm_launch_us is checked against.  --bench LOG (the stdout of the profiled bench.py run, its JSON
+line) recomputes the GEMM family's roofline fraction from the trace's timed rounds -- the line's
+gemm_flops_per_round over the summed in-round cgl_gemm_f32 durations -- and compares it with roofline.frac."""
 import argparse
 import csv
 import json
@@ -19,6 +21,7 @@ def main():
     p.add_argument("trace")
     p.add_argument("--json", default=None)
     p.add_argument("--marker", default="cgl_gemm_pro")
+    p.add_argument("--bench", default=None)
     a = p.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     starts = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
@@ -56,6 +59,16 @@ def main():
         print(f"{x['i']:3d} {x['us']:7.2f} gap {x['gap_us']:5.2f} wg {x['wg']:6d} {x['kernel'][:60]}")
     print(f"rounds {out['rounds']} launches {n} period {out['period_us']:.2f} us busy {out['busy_us']} gaps "
           f"{out['gaps_us']} gemm_f32 avg {out['gemm_f32_avg_us']} us over {len(gemm)} dispatches")
+    if a.bench:
+        line = [l for l in open(a.bench) if l.startswith('{"metric"')][-1]
+        rl = json.loads(line)["roofline"]
+        gus = sum(x["us"] for x in out["per_launch"] if x["kernel"].startswith("cgl_gemm_f32<"))
+        frac = rl["gemm_flops_per_round"] / (gus * 1e-6) / 1e12 / rl["peak"]
+        out["check"] = {"frac_trace": round(frac, 4), "frac_line": rl["frac"],
+                        "rel_diff": round(rl["frac"] / frac - 1.0, 4),
+                        "avg_gemm_us_trace": round(gus / max(1, rl["gemm_launches_per_round"]), 3),
+                        "avg_gemm_us_line": rl["avg_gemm_launch_us"]}
+        print("roofline check:", out["check"])
     if a.json:
         json.dump(out, open(a.json, "w"), indent=1)
 
