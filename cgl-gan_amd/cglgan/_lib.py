@@ -128,7 +128,8 @@ def _load():
         "cgl_conv3x3_bwd_weight": (ci, [vp, vp, vp, vp] + [ci] * 7 + [vp, i64, vp]),
         "cgl_bn2d_workspace_bytes": (i64, [ci] * 4),
         "cgl_bn2d_fwd": (ci, [vp, ci, ci, ci, ci, vp, vp, cd, cd, vp, vp, ci, ci, cf, vp, vp, vp, vp, vp, i64, vp]),
-        "cgl_bn2d_bwd": (ci, [vp, vp, vp, ci, ci, ci, ci, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, vp, i64, vp]),
+        "cgl_bn2d_bwd": (ci, [vp, vp, vp, ci, ci, ci, ci, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, ci, vp, vp, i64,
+                              vp]),
         "cgl_act_drop_bwd": (ci, [vp, vp, vp, ci, ci, ci, cf, ci, vp, vp]),
         "cgl_dropout2d_mask": (ci, [vp, ci, ci, cd, ctypes.c_ulonglong, ctypes.c_ulonglong, vp]),
         "cgl_dropout2d_masks": (ci, [ci, P(vp), P(ci), P(ci), cd, ctypes.c_ulonglong, P(ctypes.c_ulonglong), vp]),
@@ -156,7 +157,8 @@ def _load():
         "cgl_linear_desc_bytes": (i64, []),
         "cgl_conv3x3_bwd_stat_chunks": (i64, [ci] * 8),
         "cgl_conv3x3_bwd_data_packed_stats": (ci, [vp, vp, vp] + [ci] * 8 + [vp, vp, vp, vp, cf, vp, i64, vp]),
-        "cgl_bn2d_bwd_stats": (ci, [vp, ci, vp, vp, vp, ci, ci, ci, ci, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, vp, i64, vp]),
+        "cgl_bn2d_bwd_stats": (ci, [vp, ci, vp, vp, vp, ci, ci, ci, ci, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, ci, vp,
+                                    vp, i64, vp]),
         "cgl_linear_prepare": (ci, [ci, vp, vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, P(LinearLaunch)]),
         "cgl_linear_launch": (ci, [vp, P(LinearLaunch), vp]),
         "cgl_dense_fwd_packed": (ci, [vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, i64, vp]),

@@ -323,24 +323,38 @@ def bn2d_fwd_stats(part, x, n, hw, c, gamma, beta, y, groups=1, eps=0.8, momentu
     return y
 
 
+def _post_coef(post_coef, c):
+    """post_coef = (coef, group, groups): the [2][groups][c] scale / shift a bn2d_fwd_stats(coef=) call kept,
+    the forward call (group) whose rows this backward covers -> (pointer, ld) of cgl_bn2d_bwd."""
+    if post_coef is None:
+        return None, 0
+    coef, g, groups = post_coef
+    _chk(coef)
+    return coef[g * c:], groups * c
+
+
 def bn2d_bwd(dy, x, n, hw, c, save_mean, save_invstd, gamma, dx, groups=1, post=None, post_out=None, drop=None,
-             dgamma=None, dbeta=None, slope=0.2, nvalid=None):
+             dgamma=None, dbeta=None, slope=0.2, nvalid=None, post_coef=None):
+    """``post_coef`` = (coef, group, groups): LeakyReLU'(post) from the forward's own scale / shift (post unread)."""
     _chk(dy, x, save_mean, save_invstd, gamma, dx, post, post_out, drop, dgamma, dbeta)
     ws = workspace(bn2d_ws_bytes(n, hw, c, groups), dy.device)
+    pc, pld = _post_coef(post_coef, c)
     C.check(C.lib.cgl_bn2d_bwd(_p(dy), _p(post), _p(x), n, hw, c, groups, _p(save_mean), _p(save_invstd), _p(gamma),
-                               float(slope), _p(post_out), _p(drop), _p(dx), _p(dgamma), _p(dbeta), _p(nvalid), _p(ws),
-                               ws.numel(), _s()), "cgl_bn2d_bwd")
+                               float(slope), _p(post_out), _p(drop), _p(dx), _p(dgamma), _p(dbeta), _p(pc), int(pld),
+                               _p(nvalid), _p(ws), ws.numel(), _s()), "cgl_bn2d_bwd")
     return dx
 
 
 def bn2d_bwd_stats(part, dy, x, n, hw, c, save_mean, save_invstd, gamma, dx, groups=1, post=None, post_out=None,
-                   drop=None, dgamma=None, dbeta=None, slope=0.2, R=32, nvalid=None):
+                   drop=None, dgamma=None, dbeta=None, slope=0.2, R=32, nvalid=None, post_coef=None):
     """bn2d_bwd from the partials a conv3x3_bwd_data(stats=...) wrote: finalize + apply."""
     _chk(dy, x, save_mean, save_invstd, gamma, dx, post, post_out, drop, dgamma, dbeta)
     ws = workspace(bn2d_ws_bytes(n, hw, c, groups), dy.device)
+    pc, pld = _post_coef(post_coef, c)
     C.check(C.lib.cgl_bn2d_bwd_stats(_p(part), int(R), _p(dy), _p(post), _p(x), n, hw, c, groups, _p(save_mean),
                                      _p(save_invstd), _p(gamma), float(slope), _p(post_out), _p(drop), _p(dx),
-                                     _p(dgamma), _p(dbeta), _p(nvalid), _p(ws), ws.numel(), _s()), "cgl_bn2d_bwd_stats")
+                                     _p(dgamma), _p(dbeta), _p(pc), int(pld), _p(nvalid), _p(ws), ws.numel(), _s()),
+            "cgl_bn2d_bwd_stats")
     return dx
 
 

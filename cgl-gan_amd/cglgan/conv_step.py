@@ -241,6 +241,11 @@ class ConvGanStep:
         self.bn_fold = fold & 3 if all(k in self.st_part for k in ("conv_blocks.2", "conv_blocks.6")) else 0
         self.coef = {k: torch.zeros(4 * c, dtype=torch.float32, device=dev)
                      for k, c in (("conv_blocks.2", 128), ("conv_blocks.6", 64))}
+        # the G backward takes LeakyReLU'(a) of these BatchNorms from the sign of the kept scale / shift applied
+        # to y (cgl_bn2d_bwd post_coef) instead of reading a: bitwise the same mask, one tensor fewer read in the
+        # channel reduction and in the backward apply (CGL_CONV_POSTCOEF=0 reads a)
+        self.coef_kept = set()
+        self.post_coef_on = os.environ.get("CGL_CONV_POSTCOEF", "1") != "0"
         # backward statistics: the same buffers (the forward's partials are consumed by then), written
         # by the input-gradient conv that produces the BatchNorm's output gradient
         self.bst_ok = {}
@@ -384,12 +389,20 @@ class ConvGanStep:
                   nvalid=nvalid)
         if fold:
             kw.update(coef=self.coef[key], apply_from=n - n // groups)
+        elif key in self.coef and key in self.st_part:
+            kw.update(coef=self.coef[key], apply_from=0)     # applied to every call, scale / shift kept
+        if key in self.coef and key in self.st_part:
+            self.coef_kept.add(key)
         if key in self.st_part:
             O.bn2d_fwd_stats(self.st_part[key], x, n, hw, c, P[key + ".weight"], P[key + ".bias"], y,
                              scratch=self.st_scratch[key], **kw)
         else:
             O.bn2d_fwd(x, n, hw, c, P[key + ".weight"], P[key + ".bias"], y, train=True, **kw)
         fm.batches[key] += groups
+
+    def _post_coef(self, key):
+        """(coef, group 1 = Xg, 2 calls) for cgl_bn2d_bwd's post_coef when this round's forward kept them."""
+        return (self.coef[key], 1, 2) if (self.post_coef_on and key in self.coef_kept) else None
 
     def _g_bn(self, key, x, y, hw, c, fold=False):
         self._bn_fwd(key, self.G, x, y, 2 * self.B, hw, c, 2, O.ACT_LEAKY, fold=fold)
@@ -466,8 +479,10 @@ class ConvGanStep:
                              1, 1, 0)
         O.conv3x3_bwd_data(self.dc3g, P["conv_blocks.8.weight"], self.da2, B, 32, 32, 64, 1, 1, 0)
         sm, si = self.g_save["conv_blocks.6"]
+        pc6 = self._post_coef("conv_blocks.6")
         O.bn2d_bwd(self.da2, self.y2[B:], B, 1024, 64, sm[1], si[1], P["conv_blocks.6.weight"], self.dy2,
-                   post=self.a2[B:], dgamma=G["conv_blocks.6.weight"], dbeta=G["conv_blocks.6.bias"], slope=SLOPE)
+                   post=None if pc6 else self.a2[B:], post_coef=pc6, dgamma=G["conv_blocks.6.weight"],
+                   dbeta=G["conv_blocks.6.bias"], slope=SLOPE)
         O.conv3x3_bwd_weight(self.dy2, self.a1[B:], G["conv_blocks.5.weight"], G["conv_blocks.5.bias"], B, 16, 16, 128,
                              64, 1, 1)
         sm, si = self.g_save["conv_blocks.2"]
@@ -476,7 +491,9 @@ class ConvGanStep:
             st = (self.st_part["conv_blocks.2"], 1, self.y1[B:], self.a1[B:], sm[1], SLOPE)
         O.conv3x3_bwd_data(self.dy2, P["conv_blocks.5.weight"], self.da1, B, 16, 16, 128, 64, 1, 1, wp=self.pk["c5b"],
                            stats=st)
-        kw = dict(post=self.a1[B:], dgamma=G["conv_blocks.2.weight"], dbeta=G["conv_blocks.2.bias"], slope=SLOPE)
+        pc2 = self._post_coef("conv_blocks.2")
+        kw = dict(post=None if pc2 else self.a1[B:], post_coef=pc2, dgamma=G["conv_blocks.2.weight"],
+                  dbeta=G["conv_blocks.2.bias"], slope=SLOPE)
         if st is not None:
             O.bn2d_bwd_stats(self.st_part["conv_blocks.2"], self.da1, self.y1[B:], B, 256, 128, sm[1], si[1],
                              P["conv_blocks.2.weight"], self.dy1, **kw)

@@ -877,30 +877,47 @@ __global__ __launch_bounds__(256, 2) void cgl_conv_wgrad_lds(CglConvLaunch args)
   const int kk = k0 + 4 * fb;
   const int tap = kk / Cin, ci = kk - tap * Cin;
   const int cdy = P->dy[tap / P->Tx], cdx = P->dx[tap - (tap / P->Tx) * P->Tx];
-
-  auto load = [&](int c, f32x4 (&ra)[NA], f32x4 (&rb)[NB]) {
+  // A 16-pixel chunk never crosses an image (OH OW >= 16, powers of two): pixel c 16 + p decodes as the chunk's
+  // (img0, oy0, ox0) -- uniform, scalar -- plus (p >> lw, p & mw) without carries, so each load slot keeps a
+  // constant element offset from the chunk's base pointer and only the X bounds test is per chunk and lane.
+  int aoff[NA], bky[NB], bkx[NB], boff[NB];
 #pragma unroll
-    for (int r = 0; r < NA; ++r) {
-      const int m = c * 16 + pa + (256 / FA) * r;
-      const int ox = m & mw, oy = (m >> lw) & mh, img = m >> lhw;
-      ra[r] = *(gcf4p)(dY + (((long)img * YH + oy * osy + ooy) * YW + ox * osx + oox) * ldy + n0 + 4 * fa);
-    }
+  for (int r = 0; r < NA; ++r) {
+    const int p = pa + (256 / FA) * r, py = p >> lw, px = p & mw;
+    aoff[r] = (py * osy * YW + px * osx) * ldy + n0 + 4 * fa;
+  }
+#pragma unroll
+  for (int r = 0; r < NB; ++r) {
+    const int p = pb + (256 / FB) * r, py = p >> lw, px = p & mw;
+    bky[r] = py * isy + cdy;
+    bkx[r] = px * isx + cdx;
+    boff[r] = (bky[r] * XW + bkx[r]) * Cin + ci;
+  }
+  (void)ish; (void)XH;
+
+  // (the out-of-bounds taps' zeros are applied when staging, so nothing waits on a load before the MFMAs)
+  auto load = [&](int c, f32x4 (&ra)[NA], f32x4 (&rb)[NB], int& okb) {
+    const int m0 = c * 16;
+    const int img0 = m0 >> lhw, oy0 = (m0 >> lw) & mh, ox0 = m0 & mw;
+    const float* ya = dY + ((long)(img0 * YH + oy0 * osy + ooy) * YW + ox0 * osx + oox) * ldy;
+#pragma unroll
+    for (int r = 0; r < NA; ++r) ra[r] = *(gcf4p)(ya + aoff[r]);
+    const int Y0 = oy0 * isy, X0 = ox0 * isx;
+    const float* xa = X + ((long)img0 * XH * XW + (long)Y0 * XW + X0) * Cin;
+    okb = 0;
 #pragma unroll
     for (int r = 0; r < NB; ++r) {
-      const int m = c * 16 + pb + (256 / FB) * r;
-      const int ox = m & mw, oy = (m >> lw) & mh, img = m >> lhw;
-      const int iy = oy * isy + cdy, ix = ox * isx + cdx;
-      const bool ok = (unsigned)iy < (unsigned)IH && (unsigned)ix < (unsigned)IW;
-      const long off = ok ? (((long)img * XH + (iy >> ish)) * XW + (ix >> ish)) * Cin + ci : ci;
-      const f32x4 v = *(gcf4p)(X + off);
-      rb[r] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      const bool ok = (unsigned)(Y0 + bky[r]) < (unsigned)IH && (unsigned)(X0 + bkx[r]) < (unsigned)IW;
+      okb |= ok ? (1 << r) : 0;
+      rb[r] = *(gcf4p)(ok ? xa + boff[r] : X + ci);
     }
   };
-  auto stage = [&](int buf, const f32x4 (&ra)[NA], const f32x4 (&rb)[NB]) {
+  auto stage = [&](int buf, const f32x4 (&ra)[NA], const f32x4 (&rb)[NB], int okb) {
 #pragma unroll
     for (int r = 0; r < NA; ++r) *(f32x4*)&sa[buf][(pa + (256 / FA) * r) * RP + 4 * fa] = ra[r];
 #pragma unroll
-    for (int r = 0; r < NB; ++r) *(f32x4*)&sb[buf][(pb + (256 / FB) * r) * CP + 4 * fb] = rb[r];
+    for (int r = 0; r < NB; ++r)
+      *(f32x4*)&sb[buf][(pb + (256 / FB) * r) * CP + 4 * fb] = ((okb >> r) & 1) ? rb[r] : f32x4{0.f, 0.f, 0.f, 0.f};
   };
   f32x16 acc[2][2];
 #pragma unroll
@@ -909,18 +926,26 @@ __global__ __launch_bounds__(256, 2) void cgl_conv_wgrad_lds(CglConvLaunch args)
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // all 32 operands of the chunk are read from LDS before the first MFMA (the reads of step q + 1 do not
+  // wait behind step q's MFMAs; the waits are progressive)
   auto compute = [&](int buf) {
-    const float* A = &sa[buf][wm * 64 + li];
-    const float* B = &sb[buf][wn * 64 + li];
+    const float* A = &sa[buf][8 * lhf * RP + wm * 64 + li];
+    const float* B = &sb[buf][8 * lhf * CP + wn * 64 + li];
+    float a[8][2], b[8][2];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      const int row = 8 * lhf + q;
-      const float a0 = A[row * RP], a1 = A[row * RP + 32];
-      const float b0 = B[row * CP], b1 = B[row * CP + 32];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+      a[q][0] = A[q * RP];
+      a[q][1] = A[q * RP + 32];
+      b[q][0] = B[q * CP];
+      b[q][1] = B[q * CP + 32];
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead (the scheduler would sink them to their MFMAs)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q][0], b[q][0], acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q][0], b[q][1], acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q][1], b[q][0], acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q][1], b[q][1], acc[1][1], 0, 0, 0);
     }
   };
 
@@ -928,20 +953,21 @@ __global__ __launch_bounds__(256, 2) void cgl_conv_wgrad_lds(CglConvLaunch args)
   const int cb = (int)(((long)split * nchk) / splits), ce = (int)(((long)(split + 1) * nchk) / splits);
   if (cb < ce) {
     f32x4 r0a[NA], r0b[NB], r1a[NA], r1b[NB];
-    load(cb, r0a, r0b);
-    load(min(cb + 1, ce - 1), r1a, r1b);
-    stage(0, r0a, r0b);
+    int ok0, ok1;
+    load(cb, r0a, r0b, ok0);
+    load(min(cb + 1, ce - 1), r1a, r1b, ok1);
+    stage(0, r0a, r0b, ok0);
     __syncthreads();
     int c = cb;
     for (; c + 2 <= ce; c += 2) {
       // buffer 0 holds chunk c, r1 chunk c + 1
-      load(min(c + 2, ce - 1), r0a, r0b);
+      load(min(c + 2, ce - 1), r0a, r0b, ok0);
       compute(0);
-      stage(1, r1a, r1b);
+      stage(1, r1a, r1b, ok1);
       __syncthreads();
-      load(min(c + 3, ce - 1), r1a, r1b);
+      load(min(c + 3, ce - 1), r1a, r1b, ok1);
       compute(1);
-      stage(0, r0a, r0b);
+      stage(0, r0a, r0b, ok0);
       __syncthreads();
     }
     if (c < ce) compute(0);   // an odd last chunk
@@ -1685,6 +1711,10 @@ struct CglChanArgs {
   const float* mean;         // [groups][C] (mode 1)
   double* part;              // [nchunks][C][2]
   const int* nv;             // mode 0: only rows < *nv * hw of the first group (rows < gr) count, or null
+  // mode 1 without the post-activation tensor: LeakyReLU'(post) from the sign of the forward's own
+  // fmaf(x, scale, shift) (scale = psc[c], shift = psc[psc_ld + c]) -- post > 0 exactly when that value is
+  // (slope > 0), so the gradient is bitwise the one read from post, and post's bytes are not read
+  const float* psc; int psc_ld;
 };
 
 // rows of the first BatchNorm group that carry data: a short real call (DataLoader's short final batch)
@@ -1711,7 +1741,8 @@ __global__ __launch_bounds__(256) void cgl_chan_reduce(CglChanArgs a) {
         const int r = min(rb + i * rp, r1 - 1);
         const long o = (long)r * C + c;
         g[i] = gld(a.dY + o);
-        if (a.post) g[i] = gld(a.post + o) > 0.f ? g[i] : g[i] * a.slope;
+        if (a.psc) g[i] = fmaf(xv[i], a.psc[c], a.psc[a.psc_ld + c]) > 0.f ? g[i] : g[i] * a.slope;
+        else if (a.post) g[i] = gld(a.post + o) > 0.f ? g[i] : g[i] * a.slope;
         xv[i] = gld(a.X + o);
       }
 #pragma unroll
@@ -1791,6 +1822,7 @@ __global__ __launch_bounds__(256) void cgl_chan_reduce4(CglChanArgs a) {
   double x0[4] = {0.0, 0.0, 0.0, 0.0}, x1[4] = {0.0, 0.0, 0.0, 0.0};
   if (a.mode == 1) {
     const f32x4 mu = *(gcf4p)(a.mean + (long)(r0 / a.gr) * C + c);
+    const f32x4 ps = a.psc ? *(gcf4p)(a.psc + c) : mu, ph = a.psc ? *(gcf4p)(a.psc + a.psc_ld + c) : mu;
     for (int rb = r0 + rl; rb < r1; rb += 8 * rp) {
       f32x4 g[8], xv[8];
 #pragma unroll
@@ -1798,7 +1830,10 @@ __global__ __launch_bounds__(256) void cgl_chan_reduce4(CglChanArgs a) {
         const long o = (long)min(rb + i * rp, r1 - 1) * C + c;
         g[i] = *(gcf4p)(a.dY + o);
         xv[i] = *(gcf4p)(a.X + o);
-        if (a.post) {
+        if (a.psc) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) g[i][j] = fmaf(xv[i][j], ps[j], ph[j]) > 0.f ? g[i][j] : g[i][j] * a.slope;
+        } else if (a.post) {
           const f32x4 p = *(gcf4p)(a.post + o);
 #pragma unroll
           for (int j = 0; j < 4; ++j) g[i][j] = p[j] > 0.f ? g[i][j] : g[i][j] * a.slope;
@@ -2270,6 +2305,7 @@ struct CglEltArgs {
   const float* post_out; const float* drop;
   float* out;
   const int* nv;             // mode 1, short first call: rows >= *nv * hw of group 0 are padding -> dX = 0
+  const float* psc; int psc_ld;   // mode 1: LeakyReLU'(post) from the forward's scale / shift (CglChanArgs)
 };
 
 __global__ __launch_bounds__(256) void cgl_eltwise(CglEltArgs a) {
@@ -2308,10 +2344,17 @@ __global__ __launch_bounds__(256) void cgl_eltwise(CglEltArgs a) {
       const f32x4 gm = *(gcf4p)(a.coef0 + gc), kk = *(gcf4p)(a.coef1 + gc);
       const f32x4 mu = *(gcf4p)(a.mean + gc), is = *(gcf4p)(a.invstd + gc), w = *(gcf4p)(a.gamma + c);
       f32x4 p = dy;
-      if (a.post) p = *(gcf4p)(a.post + e);
+      if (a.psc) {
+        const f32x4 ps = *(gcf4p)(a.psc + c), ph = *(gcf4p)(a.psc + a.psc_ld + c);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) p[j] = fmaf(x[j], ps[j], ph[j]);
+      } else if (a.post) {
+        p = *(gcf4p)(a.post + e);
+      }
+      const bool pon = a.psc || a.post;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float gg = a.post ? (p[j] > 0.f ? dy[j] : dy[j] * sl) : dy[j];
+        const float gg = pon ? (p[j] > 0.f ? dy[j] : dy[j] * sl) : dy[j];
         o[j] = (gg - gm[j] - (x[j] - mu[j]) * kk[j]) * is[j] * w[j];
       }
       if (a.post_out) {
@@ -3239,8 +3282,8 @@ bool wgrad_row_ok(const WgradPlan& pl) {
 }
 
 // cgl_conv_wgrad_lds applies: no bias column, whole R x C tiles (N % R == 0, K % C == 0), 16-byte operand
-// rows (Cin % 4 == 0 so 4 columns are one tap, ldy % 4 == 0, aligned bases), whole 16-pixel chunks and
-// power-of-two output grids (shift / mask pixel decode).  Returns WM (WN = 4 / WM), 0 = not applicable.
+// rows (Cin % 4 == 0 so 4 columns are one tap, ldy % 4 == 0, aligned bases), whole 16-pixel chunks inside one
+// image (power-of-two output grids of >= 16 pixels: shift / mask decode), an unshifted input.  Returns WM (WN = 4 / WM), 0 = not applicable.
 // CGL_WGRAD_LDS=0 keeps the wave-unit kernel (A/B).
 int wgrad_lds_wm(const WgradPlan& pl, bool bias_col, const float* dY, const float* X) {
   static const int env = getenv("CGL_WGRAD_LDS") ? atoi(getenv("CGL_WGRAD_LDS")) : 1;
@@ -3250,8 +3293,8 @@ int wgrad_lds_wm(const WgradPlan& pl, bool bias_col, const float* dY, const floa
   if (!wm) return 0;
   for (int i = 0; i < pl.np; ++i) {
     const CglConvProb& P = pl.P[i];
-    if (P.N != N || P.K != K || P.Cin % 4 || P.ldy % 4 || P.M % 16 || P.M < 16 * 64) return 0;
-    if ((P.OW & (P.OW - 1)) || (P.OH & (P.OH - 1))) return 0;
+    if (P.N != N || P.K != K || P.Cin % 4 || P.ldy % 4 || P.M % 16 || P.M < 16 * 64 || P.ish != 0) return 0;
+    if ((P.OW & (P.OW - 1)) || (P.OH & (P.OH - 1)) || P.OW * P.OH < 16) return 0;
   }
   return wm;
 }
@@ -3702,7 +3745,9 @@ int cgl_bn2d_fwd_stats_coef(const double* part, int R, const float* X, int n, in
 int cgl_bn2d_bwd_stats(const double* part, int R, const float* dY, const float* post, const float* X, int n, int hw,
                        int C, int groups, const float* save_mean, const float* save_invstd, const float* gamma,
                        float slope, const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta,
-                       const int* nvalid, void* ws, int64_t wsb, void* stream) {
+                       const float* post_coef, int post_coef_ld, const int* nvalid, void* ws, int64_t wsb,
+                       void* stream) {
+  if (post_coef && (post || groups != 1 || !al16(post_coef) || post_coef_ld % 4)) return CGL_E_ARG;
   if (!part || !dY || !X || !save_mean || !save_invstd || !gamma || !dX || !ws || !al16(ws)) return CGL_E_ARG;
   if (!al16(dY) || !al16(X) || !al16(dX) || (post && !al16(post)) || (post_out && !al16(post_out))) return CGL_E_ARG;
   if (!al16(save_mean) || !al16(save_invstd) || !al16(gamma) || (drop && !al16(drop))) return CGL_E_ARG;
@@ -3729,6 +3774,7 @@ int cgl_bn2d_bwd_stats(const double* part, int R, const float* dY, const float* 
   e.mode = 1; e.rows = (int)rows; e.C = C; e.gr = (int)gr; e.hw = hw; e.slope = slope;
   e.X = X; e.dY = dY; e.post = post; e.coef0 = c0; e.coef1 = c1; e.mean = save_mean; e.invstd = save_invstd;
   e.gamma = gamma; e.post_out = post_out; e.drop = drop; e.out = dX; e.nv = nvalid;
+  e.psc = post_coef; e.psc_ld = post_coef_ld;
   const long n4 = rows * C / 4;
   hipLaunchKernelGGL(cgl_eltwise, dim3((unsigned)std::min<long>((n4 + 255) / 256, 8192)), dim3(256), 0, s, e);
   return (int)hipGetLastError();
@@ -3737,7 +3783,8 @@ int cgl_bn2d_bwd_stats(const double* part, int R, const float* dY, const float* 
 int cgl_bn2d_bwd(const float* dY, const float* post, const float* X, int n, int hw, int C, int groups,
                  const float* save_mean, const float* save_invstd, const float* gamma, float slope,
                  const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta,
-                 const int* nvalid, void* ws, int64_t wsb, void* stream) {
+                 const float* post_coef, int post_coef_ld, const int* nvalid, void* ws, int64_t wsb, void* stream) {
+  if (post_coef && (post || groups != 1 || !al16(post_coef) || post_coef_ld % 4)) return CGL_E_ARG;
   if (!dY || !X || !save_mean || !save_invstd || !gamma || !dX || !ws || !al16(ws)) return CGL_E_ARG;
   if (!al16(dY) || !al16(X) || !al16(dX) || (post && !al16(post)) || (post_out && !al16(post_out))) return CGL_E_ARG;
   if (!al16(save_mean) || !al16(save_invstd) || !al16(gamma) || (drop && !al16(drop))) return CGL_E_ARG;
@@ -3756,6 +3803,7 @@ int cgl_bn2d_bwd(const float* dY, const float* post, const float* X, int n, int 
   std::memset(&a, 0, sizeof(a));
   a.X = X; a.rows = (int)rows; a.C = C; a.R = R; a.mode = 1; a.gr = (int)gr; a.part = part;
   a.dY = dY; a.post = post; a.slope = slope; a.mean = save_mean;
+  a.psc = post_coef; a.psc_ld = post_coef_ld;
   launch_chan_reduce(a, nch, s);
   CglBnFinArgs f;
   std::memset(&f, 0, sizeof(f));
@@ -3770,6 +3818,7 @@ int cgl_bn2d_bwd(const float* dY, const float* post, const float* X, int n, int 
   e.mode = 1; e.rows = (int)rows; e.C = C; e.gr = (int)gr; e.hw = hw; e.slope = slope;
   e.X = X; e.dY = dY; e.post = post; e.coef0 = c0; e.coef1 = c1; e.mean = save_mean; e.invstd = save_invstd;
   e.gamma = gamma; e.post_out = post_out; e.drop = drop; e.out = dX; e.nv = nvalid;
+  e.psc = post_coef; e.psc_ld = post_coef_ld;
   const long n4 = rows * C / 4;
   hipLaunchKernelGGL(cgl_eltwise, dim3((unsigned)std::min<long>((n4 + 255) / 256, 8192)), dim3(256), 0, s, e);
   return (int)hipGetLastError();

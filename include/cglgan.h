@@ -361,11 +361,18 @@ int cgl_bn2d_fwd_stats_coef(const double* part, int R, const float* X, int n, in
 int cgl_bn2d_bwd_stats(const double* part, int R, const float* dY, const float* post, const float* X, int n, int hw,
                        int C, int groups, const float* save_mean, const float* save_invstd, const float* gamma,
                        float slope, const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta,
-                       const int* nvalid, void* workspace, int64_t ws_bytes, void* stream);
+                       const float* post_coef, int post_coef_ld, const int* nvalid, void* workspace, int64_t ws_bytes,
+                       void* stream);
+/* post_coef (may be null; then post as above): instead of reading post, take LeakyReLU'(post) from the sign of
+ * the forward's fmaf(X, scale, shift) with scale = post_coef[c], shift = post_coef[post_coef_ld + c] (the coef a
+ * cgl_bn2d_fwd_stats_coef call kept; its group g of G: post_coef = coef + g C, post_coef_ld = G C).  The forward
+ * wrote post = LeakyReLU(that value), so the two signs agree bit for bit and post's bytes are not read.
+ * Requires post == null and groups == 1 (one forward call's rows). */
 int cgl_bn2d_bwd(const float* dY, const float* post, const float* X, int n, int hw, int C, int groups,
                  const float* save_mean, const float* save_invstd, const float* gamma, float slope,
                  const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta,
-                 const int* nvalid, void* workspace, int64_t ws_bytes, void* stream);
+                 const float* post_coef, int post_coef_ld, const int* nvalid, void* workspace, int64_t ws_bytes,
+                 void* stream);
 /* dX = dY * LeakyReLU'(post) * drop[n][C] (Dropout2d + LeakyReLU backward; post / drop may be
  * null), or with tanh_y != 0: dX = dY * (1 - post^2) (Tanh backward, post = the Tanh output). */
 int cgl_act_drop_bwd(const float* dY, const float* post, const float* drop, int n, int hw, int C, float slope,
