@@ -245,6 +245,9 @@ class ConvGanStep:
         # to y (cgl_bn2d_bwd post_coef) instead of reading a: bitwise the same mask, one tensor fewer read in the
         # channel reduction and in the backward apply (CGL_CONV_POSTCOEF=0 reads a)
         self.coef_kept = set()
+        # D's inner BatchNorms folded into the next conv in the G-loss pass (_d_forward); [2][groups][C] scale / shift
+        self.d_fold = os.environ.get("CGL_CONV_DFOLD", "1") != "0"
+        self.dcoef = {bk: torch.zeros(4 * co, dtype=torch.float32, device=dev) for _, bk, _, co, _ in D_CONVS if bk}
         self.post_coef_on = os.environ.get("CGL_CONV_POSTCOEF", "1") != "0"
         # backward statistics: the same buffers (the forward's partials are consumed by then), written
         # by the input-gradient conv that produces the BatchNorm's output gradient
@@ -379,7 +382,7 @@ class ConvGanStep:
         part = self.st_part.get(key)
         return (part, groups) if part is not None else None
 
-    def _bn_fwd(self, key, fm, x, y, n, hw, c, groups, act, fold=False, nvalid=None):
+    def _bn_fwd(self, key, fm, x, y, n, hw, c, groups, act, fold=False, nvalid=None, coef_only=False):
         """BatchNorm2d (train) from the partials the producing conv wrote, else with its own pass.
         ``fold``: keep the scale / shift in self.coef[key] and apply to the last group (Xg) only."""
         P, R = fm.params, fm.running
@@ -387,7 +390,9 @@ class ConvGanStep:
         kw = dict(groups=groups, eps=BN_EPS, momentum=BN_MOM, running_mean=R[key + ".running_mean"],
                   running_var=R[key + ".running_var"], act=act, slope=SLOPE, save_mean=sm, save_invstd=si,
                   nvalid=nvalid)
-        if fold:
+        if coef_only:     # the consumer conv applies it (bn_in): keep scale / shift, write no activation
+            kw.update(coef=self.dcoef[key], apply_from=n)
+        elif fold:
             kw.update(coef=self.coef[key], apply_from=n - n // groups)
         elif key in self.coef and key in self.st_part:
             kw.update(coef=self.coef[key], apply_from=0)     # applied to every call, scale / shift kept
@@ -421,18 +426,27 @@ class ConvGanStep:
                           [(self.round * 2 + call) * 4 + k for call in (0, 1) for k in range(4)])
 
     def _d_forward(self, x, n, groups, masks, nvalid=None):
-        """``nvalid``: the first call (the real images) is a short batch of *nvalid images."""
+        """``nvalid``: the first call (the real images) is a short batch of *nvalid images.
+        The G-loss pass (masks = mask_g) folds each inner BatchNorm2d into the next conv's operand load
+        (its output r is read by nothing else there: no D weight gradient in that pass), so those BatchNorms
+        write no activation -- two cgl_eltwise passes fewer; CGL_CONV_DFOLD=0 applies them."""
         P, R = self.D.params, self.D.running
-        inp = x
+        fold_pass = self.d_fold and masks is self.mask_g and groups == 1 and nvalid is None
+        inp, bn_in = x, None
         for k, (ck, bk, ci, co, hw) in enumerate(D_CONVS):
             st = self._stats(bk, groups) if bk else None
             O.conv3x3_fwd(inp, P[ck + ".weight"], P[ck + ".bias"], self.q[k], n, hw, hw, ci, co, 2, 0, act=O.ACT_LEAKY,
                           slope=SLOPE, drop=masks[k], wp=self.pk[ck + "f"], stats=st,
-                          nvalid=nvalid if st is not None else None)
-            inp = self.q[k]
+                          nvalid=nvalid if st is not None else None, bn_in=bn_in)
+            inp, bn_in = self.q[k], None
             if bk:
-                self._bn_fwd(bk, self.D, self.q[k], self.r[k], n, (hw // 2) ** 2, co, groups, O.ACT_NONE, nvalid=nvalid)
-                inp = self.r[k]
+                fold = fold_pass and k + 1 < len(D_CONVS) and bk in self.st_part
+                self._bn_fwd(bk, self.D, self.q[k], self.r[k], n, (hw // 2) ** 2, co, groups, O.ACT_NONE, nvalid=nvalid,
+                             coef_only=fold)
+                if fold:
+                    bn_in = (self.dcoef[bk], groups, O.ACT_NONE, SLOPE)
+                else:
+                    inp = self.r[k]
         # out.view(B, -1) -> adv_layer (model/lsgan.py:96-97) from the NHWC map; the D step's call keeps the
         # NCHW view for adv_layer's weight gradient, the G-loss pass (no D weight gradient) does not
         O.dense1_fwd_nhwc(self.r[3], P["adv_layer.weight"], P["adv_layer.bias"], self.v, n, 128, 4,

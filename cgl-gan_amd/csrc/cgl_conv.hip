@@ -839,19 +839,24 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad(CglConvLaunch args) {
 // become a quarter of the load instructions and 1 / WN + 1 / WM of the bytes.  Chunk c + 2's loads are in
 // flight while chunk c is multiplied (two register sets, two LDS buffers, one barrier per chunk).  Same
 // partials [split][N][Kp] and k permutation as cgl_conv_wgrad (pixel 8 lh + q of a chunk is lane half lh's
-// k of MFMA step q), so cgl_conv_wgrad_reduce is shared.  Requirements: wgrad_lds_ok.
+// k of MFMA step q), so cgl_conv_wgrad_reduce is shared.  Requirements: wgrad_lds_wm.
+// KS = 2: 512-thread workgroups of two 4-wave halves that take alternate chunks of one (twice as long) pixel
+// split, each half with its own LDS buffers, summed through LDS at the end (half 0 + half 1, fixed order):
+// the same waves per SIMD with half the splits, so half the partials to write and to reduce.
 #define CGL_WLDS_PAD 4
-template <int WM, int WN>
-__global__ __launch_bounds__(256, 2) void cgl_conv_wgrad_lds(CglConvLaunch args) {
+template <int WM, int WN, int KS>
+__global__ __launch_bounds__(256 * KS, 2 / KS) void cgl_conv_wgrad_lds(CglConvLaunch args) {
   (void)args;
+  static_assert(KS == 1 || KS == 2, "one or two halves");
   constexpr int R = 64 * WM, C = 64 * WN;
   constexpr int RP = R + CGL_WLDS_PAD, CP = C + CGL_WLDS_PAD;   // padded rows: the lane halves (8 rows
                                                                  // apart) land on disjoint banks
   constexpr int FA = R / 4, FB = C / 4;                          // float4 per pixel row of each panel
   constexpr int NA = 16 * FA / 256, NB = 16 * FB / 256;          // float4 loads per thread and chunk
   static_assert(WM * WN == 4 && NA >= 1 && NB >= 1, "4 waves, whole panels");
-  __shared__ __attribute__((aligned(16))) float sa[2][16 * RP];
-  __shared__ __attribute__((aligned(16))) float sb[2][16 * CP];
+  constexpr int HALF = 2 * 16 * (RP + CP);                       // one half's two A and two B buffers
+  static_assert(KS == 1 || KS * HALF >= 256 * 64, "the halves' merge reuses the staging LDS");
+  __shared__ __attribute__((aligned(16))) float pool[KS * HALF];
   CglKL L = cgl_conv_args();
   const int pi = cgl_conv_prob(L, blockIdx.x);
   CglKP P = &L->p[pi];
@@ -859,10 +864,13 @@ __global__ __launch_bounds__(256, 2) void cgl_conv_wgrad_lds(CglConvLaunch args)
   const int local = cgl_xcd_tile(blockIdx.x - P->wg_begin, tiles * P->splits);
   const int split = local / tiles, tile = local - split * tiles;
   const int n0 = (tile / P->tiles_n) * R, k0 = (tile % P->tiles_n) * C;
-  const int tid = threadIdx.x;
+  const int half = KS == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 8);
+  const int tid = threadIdx.x & 255;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, li = lane & 31, lhf = lane >> 5;
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+  float* const sa0 = pool + half * HALF;                          // [2][16 RP]
+  float* const sb0 = sa0 + 2 * 16 * RP;                           // [2][16 CP]
   const int N = P->N, Kp = P->Kp, Cin = P->Cin;
   const int IH = P->IH, IW = P->IW, ish = P->ish, XW = P->XW, XH = P->XH;
   const int ldy = P->ldy, YH = P->YH, YW = P->YW;
@@ -914,10 +922,11 @@ __global__ __launch_bounds__(256, 2) void cgl_conv_wgrad_lds(CglConvLaunch args)
   };
   auto stage = [&](int buf, const f32x4 (&ra)[NA], const f32x4 (&rb)[NB], int okb) {
 #pragma unroll
-    for (int r = 0; r < NA; ++r) *(f32x4*)&sa[buf][(pa + (256 / FA) * r) * RP + 4 * fa] = ra[r];
+    for (int r = 0; r < NA; ++r) *(f32x4*)&sa0[buf * 16 * RP + (pa + (256 / FA) * r) * RP + 4 * fa] = ra[r];
 #pragma unroll
     for (int r = 0; r < NB; ++r)
-      *(f32x4*)&sb[buf][(pb + (256 / FB) * r) * CP + 4 * fb] = ((okb >> r) & 1) ? rb[r] : f32x4{0.f, 0.f, 0.f, 0.f};
+      *(f32x4*)&sb0[buf * 16 * CP + (pb + (256 / FB) * r) * CP + 4 * fb] =
+          ((okb >> r) & 1) ? rb[r] : f32x4{0.f, 0.f, 0.f, 0.f};
   };
   f32x16 acc[2][2];
 #pragma unroll
@@ -929,8 +938,8 @@ __global__ __launch_bounds__(256, 2) void cgl_conv_wgrad_lds(CglConvLaunch args)
   // all 32 operands of the chunk are read from LDS before the first MFMA (the reads of step q + 1 do not
   // wait behind step q's MFMAs; the waits are progressive)
   auto compute = [&](int buf) {
-    const float* A = &sa[buf][8 * lhf * RP + wm * 64 + li];
-    const float* B = &sb[buf][8 * lhf * CP + wn * 64 + li];
+    const float* A = &sa0[buf * 16 * RP + 8 * lhf * RP + wm * 64 + li];
+    const float* B = &sb0[buf * 16 * CP + 8 * lhf * CP + wn * 64 + li];
     float a[8][2], b[8][2];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -951,26 +960,51 @@ __global__ __launch_bounds__(256, 2) void cgl_conv_wgrad_lds(CglConvLaunch args)
 
   const int nchk = P->M >> 4, splits = P->splits;
   const int cb = (int)(((long)split * nchk) / splits), ce = (int)(((long)(split + 1) * nchk) / splits);
-  if (cb < ce) {
+  // this half's chunks: cb + half + KS i, i < ni (the same count for both halves: every barrier is shared;
+  // a half whose last chunk lies past ce loads a clamped one and skips its MFMAs)
+  const int ni = (ce - cb + KS - 1) / KS;
+  auto chunk = [&](int i) { return min(cb + half + KS * i, ce - 1); };
+  auto live = [&](int i) { return cb + half + KS * i < ce; };
+  if (ni > 0) {
     f32x4 r0a[NA], r0b[NB], r1a[NA], r1b[NB];
     int ok0, ok1;
-    load(cb, r0a, r0b, ok0);
-    load(min(cb + 1, ce - 1), r1a, r1b, ok1);
+    load(chunk(0), r0a, r0b, ok0);
+    load(chunk(min(1, ni - 1)), r1a, r1b, ok1);
     stage(0, r0a, r0b, ok0);
     __syncthreads();
-    int c = cb;
-    for (; c + 2 <= ce; c += 2) {
-      // buffer 0 holds chunk c, r1 chunk c + 1
-      load(min(c + 2, ce - 1), r0a, r0b, ok0);
-      compute(0);
+    int i = 0;
+    for (; i + 2 <= ni; i += 2) {
+      // buffer 0 holds step i, r1 step i + 1
+      load(chunk(min(i + 2, ni - 1)), r0a, r0b, ok0);
+      if (live(i)) compute(0);
       stage(1, r1a, r1b, ok1);
       __syncthreads();
-      load(min(c + 3, ce - 1), r1a, r1b, ok1);
-      compute(1);
+      load(chunk(min(i + 3, ni - 1)), r1a, r1b, ok1);
+      if (live(i + 1)) compute(1);
       stage(0, r0a, r0b, ok0);
       __syncthreads();
     }
-    if (c < ce) compute(0);   // an odd last chunk
+    if (i < ni && live(i)) compute(0);   // an odd last step
+  }
+  if constexpr (KS == 2) {
+    // half 1 hands its accumulators to half 0 through the (now idle) staging LDS
+    __syncthreads();
+    if (half == 1) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) pool[((i * 2 + j) * 16 + r) * 256 + tid] = acc[i][j][r];
+    }
+    __syncthreads();
+    if (half == 1) return;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] += pool[((i * 2 + j) * 16 + r) * 256 + tid];
   }
   float* __restrict__ part = P->part + (long)split * N * Kp;
 #pragma unroll
@@ -3357,17 +3391,28 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
   }
   const int lwm = valu ? 0 : wgrad_lds_wm(pl, bias_col, dY, X);
   if (lwm) {
-    // workgroup tiles of 64 lwm x 256 / lwm over the plan's pixel splits (partials as sized by wgrad_plan)
+    // workgroup tiles of 64 lwm x 256 / lwm over the plan's pixel splits (partials as sized by wgrad_plan);
+    // CGL_WGRAD_KS = 2: two-half workgroups over half as many (twice as long) splits.  Measured neutral
+    // (profiles/r04_conv_wgrad_ks_dfold.txt: the reduce gains 6.4 us per round, the two kernels lose 7.9 us),
+    // so opt-in
+    static const int ks = getenv("CGL_WGRAD_KS") && atoi(getenv("CGL_WGRAD_KS")) == 2 ? 2 : 1;
     int wgl = 0;
     for (int i = 0; i < pl.np; ++i) {
       CglConvProb& P = L.p[i];
       P.tiles_m = P.N / (64 * lwm);
       P.tiles_n = P.K / (256 / lwm);
+      P.splits = std::max(1, P.splits / ks);
+      r.splits[i] = P.splits;
       P.wg_begin = wgl;
       wgl += P.tiles_m * P.tiles_n * P.splits;
     }
-    if (lwm == 2) hipLaunchKernelGGL((cgl_conv_wgrad_lds<2, 2>), dim3(wgl), dim3(256), 0, s, L);
-    else hipLaunchKernelGGL((cgl_conv_wgrad_lds<1, 4>), dim3(wgl), dim3(256), 0, s, L);
+    if (ks == 2) {
+      if (lwm == 2) hipLaunchKernelGGL((cgl_conv_wgrad_lds<2, 2, 2>), dim3(wgl), dim3(512), 0, s, L);
+      else hipLaunchKernelGGL((cgl_conv_wgrad_lds<1, 4, 2>), dim3(wgl), dim3(512), 0, s, L);
+    } else {
+      if (lwm == 2) hipLaunchKernelGGL((cgl_conv_wgrad_lds<2, 2, 1>), dim3(wgl), dim3(256), 0, s, L);
+      else hipLaunchKernelGGL((cgl_conv_wgrad_lds<1, 4, 1>), dim3(wgl), dim3(256), 0, s, L);
+    }
   }
   else if (n1t)
   {

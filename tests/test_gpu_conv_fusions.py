@@ -1,0 +1,58 @@
+"""Two conv-round fusions that must leave every tensor of the round bitwise unchanged (model/lsgan.py:13-22,
+78-80), eager and graph-replayed, at B = 8 and the benchmarked B = 256:
+  * CGL_CONV_POSTCOEF: the G BatchNorm2d backward takes LeakyReLU'(a) from the sign of the forward's own
+    fmaf(y, scale, shift) (cgl_bn2d_bwd / cgl_bn2d_bwd_stats post_coef: the coef the forward finalize kept)
+    instead of reading the activation a -- the forward wrote a = LeakyReLU(that value);
+  * CGL_CONV_DFOLD: in the G-loss pass, D's inner BatchNorm2d layers are applied in the next conv's operand
+    load (bn_in, cgl_eltwise's fmaf) instead of an apply pass -- nothing else reads their output there."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _step(B, graph, data, env):
+    from cglgan.conv_step import ConvGanStep
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        st = ConvGanStep(B, seed=21, data=data, graph=graph)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    st.init_default(5, 6)
+    return st
+
+
+CASES = [("CGL_CONV_POSTCOEF", 8, False, "2"), ("CGL_CONV_POSTCOEF", 256, False, "0"),
+         ("CGL_CONV_POSTCOEF", 256, True, "2"), ("CGL_CONV_DFOLD", 8, False, "2"), ("CGL_CONV_DFOLD", 256, True, "2")]
+
+
+@pytest.mark.parametrize("var,B,graph,fold", CASES)
+def test_conv_round_fusion_bitwise(var, B, graph, fold):
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        data = torch.rand(4 * B + 3, 1024, device="cuda", generator=torch.Generator("cuda").manual_seed(3)) * 2 - 1
+        a = _step(B, graph, data, {var: "1", "CGL_CONV_BNFOLD": fold})
+        b = _step(B, graph, data, {var: "0", "CGL_CONV_BNFOLD": fold})
+        for _ in range(3):
+            a.run()
+            b.run()
+        torch.cuda.synchronize()
+    if var == "CGL_CONV_POSTCOEF":
+        assert a.post_coef_on and not b.post_coef_on
+        assert {"conv_blocks.2", "conv_blocks.6"} <= a.coef_kept
+    else:
+        assert a.d_fold and not b.d_fold
+    for name in ("p", "g", "m", "v"):
+        assert torch.equal(getattr(a.G, name), getattr(b.G, name)), ("G", name)
+        assert torch.equal(getattr(a.D, name), getattr(b.D, name)), ("D", name)
+    for k in a.D.running:
+        assert torch.equal(a.D.running[k], b.D.running[k]), k
+    assert torch.equal(a.x3, b.x3) and torch.equal(a.lbuf, b.lbuf)
+    assert torch.equal(a.dy1, b.dy1) and torch.equal(a.dy2, b.dy2)

@@ -46,8 +46,11 @@ for st in "$@"; do
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
         python3 $R/bench.py --steps 50 --warmup 10 --no-cpu-baseline > $O/prof.log 2>&1) || exit $? ;;
     proflsgan)
-      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_lsgan -o run -- \
-        python3 $R/bench.py --model lsgan --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_lsgan.log 2>&1) || exit $? ;;
+      # proflsgan:TAG=ENV1,ENV2 profiles under those env settings -> prof_lsgan_TAG/
+      d=prof_lsgan; envs=""
+      if [ -n "$arg" ]; then d=prof_lsgan_${arg%%=*}; envs=${arg#*=}; envs=${envs//,/ }; fi
+      (cd /tmp && export TMPDIR=/tmp $envs && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$d -o run -- \
+        python3 $R/bench.py --model lsgan --steps 10 --warmup 3 --no-cpu-baseline > $O/$d.log 2>&1) || exit $? ;;
     traffic)
       for c in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && export TMPDIR=/tmp CGL_PLAN_DEBUG=1 && timeout -s KILL 150 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/mlp_$c -o run -- \
