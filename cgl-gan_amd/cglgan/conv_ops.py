@@ -139,19 +139,22 @@ def conv3x3_fwd(x, w, b, y, n, h, wd, cin, cout, stride=1, up=0, act=ACT_NONE, s
 
 
 def conv3x3_bwd_data(dy, w, dx, n, h, wd, cin, cout, stride=1, up=0, wp=None, stats=None):
-    """``stats`` = (part, groups, x, post, mean, slope): also write the previous BatchNorm2d's backward
-    partials {sum g, sum g (x - mean)} per 32-row chunk of dx (g = dx * leaky'(post) if post) --
-    consumed by bn2d_bwd_stats; needs ``wp``."""
+    """``stats`` = (part, groups, x, post, mean, slope[, post_coef]): also write the previous BatchNorm2d's
+    backward partials {sum g, sum g (x - mean)} per 32-row chunk of dx (g = dx * leaky'(post) if post; with
+    post_coef = (coef, group, groups) and post None: leaky' from the forward's scale / shift, bn2d_bwd's
+    post_coef) -- consumed by bn2d_bwd_stats; needs ``wp``."""
     _chk(dy, w, dx, wp)
     ws = workspace(conv_ws_bytes(n, h, wd, cin, cout, stride, up), dy.device)
     if stats is not None:
-        part, groups, x, post, mean, slope = stats
+        part, groups, x, post, mean, slope = stats[:6]
+        pc, pld = _post_coef(stats[6] if len(stats) > 6 else None, cin)
         _chk(x, post, mean)
         if wp is None or not part.is_cuda or part.dtype != torch.float64:
             raise RuntimeError("conv3x3_bwd_data(stats=...): needs packed weights and a float64 CUDA partial buffer")
         C.check(C.lib.cgl_conv3x3_bwd_data_packed_stats(_p(dy), _p(wp), _p(dx), n, h, wd, cin, cout, stride, up,
-                                                        int(groups), _p(part), _p(x), _p(post), _p(mean), float(slope),
-                                                        _p(ws), ws.numel(), _s()), "cgl_conv3x3_bwd_data_packed_stats")
+                                                        int(groups), _p(part), _p(x), _p(post), _p(pc), int(pld),
+                                                        _p(mean), float(slope), _p(ws), ws.numel(), _s()),
+                "cgl_conv3x3_bwd_data_packed_stats")
         return dx
     if wp is not None:
         C.check(C.lib.cgl_conv3x3_bwd_data_packed(_p(dy), _p(w), _p(wp), _p(dx), n, h, wd, cin, cout, stride, up,
@@ -162,9 +165,18 @@ def conv3x3_bwd_data(dy, w, dx, n, h, wd, cin, cout, stride=1, up=0, wp=None, st
     return dx
 
 
-def conv3x3_bwd_weight(dy, x, dw, db, n, h, wd, cin, cout, stride=1, up=0):
+def conv3x3_bwd_weight(dy, x, dw, db, n, h, wd, cin, cout, stride=1, up=0, bn_in=None):
+    """``bn_in`` = (coef, group, groups, act, slope): ``x`` is the PRE-BatchNorm map of forward call ``group``;
+    the BatchNorm (+ LeakyReLU) is applied in the operand loads (cgl_conv3x3_bwd_weight_bnin)."""
     _chk(dy, x, dw, db)
     ws = workspace(conv_ws_bytes(n, h, wd, cin, cout, stride, up), dy.device)
+    if bn_in is not None:
+        coef, group, groups, act, slope = bn_in
+        _chk(coef)
+        C.check(C.lib.cgl_conv3x3_bwd_weight_bnin(_p(dy), _p(x), _p(dw), _p(db), n, h, wd, cin, cout, stride, up,
+                                                  _p(coef), int(groups), int(group), int(act), float(slope), _p(ws),
+                                                  ws.numel(), _s()), "cgl_conv3x3_bwd_weight_bnin")
+        return dw
     C.check(C.lib.cgl_conv3x3_bwd_weight(_p(dy), _p(x), _p(dw), _p(db), n, h, wd, cin, cout, stride, up, _p(ws),
                                          ws.numel(), _s()), "cgl_conv3x3_bwd_weight")
     return dw

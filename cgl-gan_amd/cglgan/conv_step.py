@@ -237,7 +237,11 @@ class ConvGanStep:
         # into the up-convolution conv_blocks.5, 2: conv_blocks.6 into conv_blocks.8), default 2: the up-convolution
         # reads each input 16 times (4 output parities x 4 taps), so its fold re-applies the BatchNorm 16 times per
         # element and measured slower than the separate pass (profiles/r03_conv_bnfold_ab.txt)
-        fold = int(os.environ.get("CGL_CONV_BNFOLD", "2"))
+        # CGL_CONV_ELIDE (default 1): with a layer folded, its activation is not stored at all -- the G backward
+        # applies the BatchNorm in the weight gradient's operand loads (cgl_conv3x3_bwd_weight_bnin) and takes
+        # LeakyReLU' from the kept scale / shift -- and the default fold mask becomes 3 (both layers)
+        self.elide_on = os.environ.get("CGL_CONV_ELIDE", "1") != "0"
+        fold = int(os.environ.get("CGL_CONV_BNFOLD", "3" if self.elide_on else "2"))
         self.bn_fold = fold & 3 if all(k in self.st_part for k in ("conv_blocks.2", "conv_blocks.6")) else 0
         self.coef = {k: torch.zeros(4 * c, dtype=torch.float32, device=dev)
                      for k, c in (("conv_blocks.2", 128), ("conv_blocks.6", 64))}
@@ -367,16 +371,26 @@ class ConvGanStep:
                       bn_in=bi("conv_blocks.6") if f2 else None)
 
     def g_act_xd(self, name):
-        """The Xd half (images 0 .. B) of a1 / a2: written by the unfolded forward; with the BatchNorm fold
-        (the consumer conv applied it in its loads) recomputed here from y and the kept scale / shift, in
-        double -- for inspection (signs, values), not used by the round."""
-        y, a, key = (self.y1, self.a1, "conv_blocks.2") if name == "a1" else (self.y2, self.a2, "conv_blocks.6")
-        if not (self.bn_fold & (1 if name == "a1" else 2)):
-            return a[:self.B]
-        c = y.shape[-1]
-        sc, sh = self.coef[key][:c].double(), self.coef[key][2 * c:3 * c].double()
-        v = y[:self.B].double() * sc + sh
-        return torch.where(v > 0, v, v * SLOPE).float()
+        """The Xd half (images 0 .. B) of a1 / a2 (see g_act)."""
+        return self.g_act(name)[:self.B]
+
+    def g_act(self, name):
+        """a1 / a2 over both calls (images 0 .. 2B): the stored tensor where the forward wrote it; with the
+        BatchNorm fold (the consumer conv applied it in its loads) the Xd half, and with the elision
+        (CGL_CONV_ELIDE) both halves, recomputed here from y and the kept scale / shift in double -- for
+        inspection (signs, values), not used by the round."""
+        y, a, key, bit = ((self.y1, self.a1, "conv_blocks.2", 1) if name == "a1" else
+                          (self.y2, self.a2, "conv_blocks.6", 2))
+        if not (self.bn_fold & bit):
+            return a
+        c, B = y.shape[-1], self.B
+
+        def rec(g, rows):
+            sc, sh = self.coef[key][g * c:(g + 1) * c].double(), self.coef[key][(2 + g) * c:(3 + g) * c].double()
+            v = rows.double() * sc + sh
+            return torch.where(v > 0, v, v * SLOPE).float()
+        xg = rec(1, y[B:]) if self._elided(key) else a[B:]
+        return torch.cat([rec(0, y[:B]), xg])
 
     def _stats(self, key, groups):
         part = self.st_part.get(key)
@@ -391,7 +405,7 @@ class ConvGanStep:
                   running_var=R[key + ".running_var"], act=act, slope=SLOPE, save_mean=sm, save_invstd=si,
                   nvalid=nvalid)
         if coef_only:     # the consumer conv applies it (bn_in): keep scale / shift, write no activation
-            kw.update(coef=self.dcoef[key], apply_from=n)
+            kw.update(coef=(self.coef if key in self.coef else self.dcoef)[key], apply_from=n)
         elif fold:
             kw.update(coef=self.coef[key], apply_from=n - n // groups)
         elif key in self.coef and key in self.st_part:
@@ -410,7 +424,14 @@ class ConvGanStep:
         return (self.coef[key], 1, 2) if (self.post_coef_on and key in self.coef_kept) else None
 
     def _g_bn(self, key, x, y, hw, c, fold=False):
-        self._bn_fwd(key, self.G, x, y, 2 * self.B, hw, c, 2, O.ACT_LEAKY, fold=fold)
+        self._bn_fwd(key, self.G, x, y, 2 * self.B, hw, c, 2, O.ACT_LEAKY, fold=fold,
+                     coef_only=fold and self._elided(key))
+
+    def _elided(self, key):
+        """The G activation after BatchNorm ``key`` is never stored (folded forward + BNIN weight gradient +
+        LeakyReLU' from the kept scale / shift); needs the post-coefficient path on."""
+        bit = 1 if key == "conv_blocks.2" else 2
+        return bool(self.elide_on and self.post_coef_on and (self.bn_fold & bit))
 
     def _masks(self):
         """Every Dropout2d mask of the round in one launch: the D step's (call 0, 2B images) and the
@@ -489,20 +510,30 @@ class ConvGanStep:
     def _g_backward(self):
         P, G, B = self.G.params, self.G.grads, self.B
         O.act_drop_bwd(self.dimg, self.x3[2 * B:], None, B, 1024, 1, self.dc3g, tanh_y=True)
-        O.conv3x3_bwd_weight(self.dc3g, self.a2[B:], G["conv_blocks.8.weight"], G["conv_blocks.8.bias"], B, 32, 32, 64,
-                             1, 1, 0)
+        e6, e2 = self._elided("conv_blocks.6"), self._elided("conv_blocks.2")
+        if e6:     # a2 = LeakyReLU(BN(y2)) applied in the operand loads
+            O.conv3x3_bwd_weight(self.dc3g, self.y2[B:], G["conv_blocks.8.weight"], G["conv_blocks.8.bias"], B, 32, 32,
+                                 64, 1, 1, 0, bn_in=(self.coef["conv_blocks.6"], 1, 2, O.ACT_LEAKY, SLOPE))
+        else:
+            O.conv3x3_bwd_weight(self.dc3g, self.a2[B:], G["conv_blocks.8.weight"], G["conv_blocks.8.bias"], B, 32, 32,
+                                 64, 1, 1, 0)
         O.conv3x3_bwd_data(self.dc3g, P["conv_blocks.8.weight"], self.da2, B, 32, 32, 64, 1, 1, 0)
         sm, si = self.g_save["conv_blocks.6"]
         pc6 = self._post_coef("conv_blocks.6")
         O.bn2d_bwd(self.da2, self.y2[B:], B, 1024, 64, sm[1], si[1], P["conv_blocks.6.weight"], self.dy2,
                    post=None if pc6 else self.a2[B:], post_coef=pc6, dgamma=G["conv_blocks.6.weight"],
                    dbeta=G["conv_blocks.6.bias"], slope=SLOPE)
-        O.conv3x3_bwd_weight(self.dy2, self.a1[B:], G["conv_blocks.5.weight"], G["conv_blocks.5.bias"], B, 16, 16, 128,
-                             64, 1, 1)
+        if e2:
+            O.conv3x3_bwd_weight(self.dy2, self.y1[B:], G["conv_blocks.5.weight"], G["conv_blocks.5.bias"], B, 16, 16,
+                                 128, 64, 1, 1, bn_in=(self.coef["conv_blocks.2"], 1, 2, O.ACT_LEAKY, SLOPE))
+        else:
+            O.conv3x3_bwd_weight(self.dy2, self.a1[B:], G["conv_blocks.5.weight"], G["conv_blocks.5.bias"], B, 16, 16,
+                                 128, 64, 1, 1)
         sm, si = self.g_save["conv_blocks.2"]
         st = None
         if self.bst_ok.get("conv_blocks.2"):
-            st = (self.st_part["conv_blocks.2"], 1, self.y1[B:], self.a1[B:], sm[1], SLOPE)
+            pc2s = self._post_coef("conv_blocks.2")
+            st = (self.st_part["conv_blocks.2"], 1, self.y1[B:], None if pc2s else self.a1[B:], sm[1], SLOPE, pc2s)
         O.conv3x3_bwd_data(self.dy2, P["conv_blocks.5.weight"], self.da1, B, 16, 16, 128, 64, 1, 1, wp=self.pk["c5b"],
                            stats=st)
         pc2 = self._post_coef("conv_blocks.2")

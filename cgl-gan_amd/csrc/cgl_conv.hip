@@ -85,6 +85,11 @@ struct CglConvLaunch {
   int in_groups, in_gimg;    // BatchNorm groups (forward calls) and input images per group
   int in_act;
   float in_slope;
+  int in_g0;                 // weight gradient (one call's rows): the input's BatchNorm group
+  // backward statistics without the post-activation tensor: LeakyReLU'(post) from the sign of the forward's
+  // fmaf(x, scale, shift), scale = st_psc[c], shift = st_psc[st_psc_ld + c] (cgl_bn2d_bwd's post_coef)
+  const float* st_psc;
+  int st_psc_ld;
 };
 
 typedef const CGL_AS4 CglConvLaunch* CglKL;
@@ -290,6 +295,13 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
     const int c4 = Cin >> 2;
     const float* __restrict__ Xi = X + (long)img * P->XH * XW * Cin;
     const int g = BNIN ? min(img / L->in_gimg, L->in_groups - 1) : 0;
+    // BNIN: when the staging stride keeps each thread on one channel quad, its scale / shift are loaded once
+    const bool qfix = (256 % c4) == 0;
+    f32x4 sc0 = {0.f, 0.f, 0.f, 0.f}, sh0 = sc0;
+    if (BNIN && qfix) {
+      sc0 = *(gcf4p)(L->in_coef + g * Cin + 4 * (tid % c4));
+      sh0 = *(gcf4p)(L->in_coef + (L->in_groups + g) * Cin + 4 * (tid % c4));
+    }
     for (int e = tid; e < WR * WC * c4; e += 256) {
       const int q = e % c4, pix = e / c4;
       const int wr = pix / WC, wc = pix - wr * WC;
@@ -298,8 +310,8 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
       if ((unsigned)iy < (unsigned)IH && (unsigned)ix < (unsigned)IW) {
         v = *(gcf4p)(Xi + ((long)iy * XW + ix) * Cin + 4 * q);
         if constexpr (BNIN) {
-          const f32x4 sc = *(gcf4p)(L->in_coef + g * Cin + 4 * q);
-          const f32x4 sh = *(gcf4p)(L->in_coef + (L->in_groups + g) * Cin + 4 * q);
+          const f32x4 sc = qfix ? sc0 : *(gcf4p)(L->in_coef + g * Cin + 4 * q);
+          const f32x4 sh = qfix ? sh0 : *(gcf4p)(L->in_coef + (L->in_groups + g) * Cin + 4 * q);
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             float w = fmaf(v[u], sc[u], sh[u]);
@@ -496,23 +508,30 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
       const auto rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(pp) + (long)pixb * ldy, (short)0,
                                                         0x7fffffff, 0x00020000);
       const float psl = L->st_slope;
+      const bool psc = L->st_psc != nullptr;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = n0 + 32 * j + li;
         const int colc = min(col, N - 1);
         const float mu = gld(L->st_mean + (long)g * N + colc);
+        const float sc = psc ? gld(L->st_psc + colc) : 0.f, sh = psc ? gld(L->st_psc + L->st_psc_ld + colc) : 0.f;
         float xv[16], pv[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int off = ((pix[r] - pixb) * ldy + colc) * 4;
           xv[r] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, off, 0, 0));
-          pv[r] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rp, off, 0, 0));
+          if (!psc) pv[r] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rp, off, 0, 0));
         }
+        if (psc) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) pv[r] = fmaf(xv[r], sc, sh);
+        }
+        const bool pon = psc || L->st_post;
         double S = 0.0, D = 0.0;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float y = acc[i][j][r];
-          const float gg = L->st_post ? (pv[r] > 0.f ? y : y * psl) : y;
+          const float gg = pon ? (pv[r] > 0.f ? y : y * psl) : y;
           S += (double)gg;
           D += (double)(gg * (xv[r] - mu));
         }
@@ -844,7 +863,9 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad(CglConvLaunch args) {
 // split, each half with its own LDS buffers, summed through LDS at the end (half 0 + half 1, fixed order):
 // the same waves per SIMD with half the splits, so half the partials to write and to reduce.
 #define CGL_WLDS_PAD 4
-template <int WM, int WN, int KS>
+// BNIN: X is the PRE-BatchNorm map of one forward call (group L->in_g0): the staged im2col values are
+// LeakyReLU(fmaf(x, scale, shift)) -- cgl_eltwise's arithmetic, so the panel equals the applied activation
+template <int WM, int WN, int KS, bool BNIN = false>
 __global__ __launch_bounds__(256 * KS, 2 / KS) void cgl_conv_wgrad_lds(CglConvLaunch args) {
   (void)args;
   static_assert(KS == 1 || KS == 2, "one or two halves");
@@ -885,6 +906,11 @@ __global__ __launch_bounds__(256 * KS, 2 / KS) void cgl_conv_wgrad_lds(CglConvLa
   const int kk = k0 + 4 * fb;
   const int tap = kk / Cin, ci = kk - tap * Cin;
   const int cdy = P->dy[tap / P->Tx], cdx = P->dx[tap - (tap / P->Tx) * P->Tx];
+  f32x4 bsc = {0.f, 0.f, 0.f, 0.f}, bsh = bsc;
+  if constexpr (BNIN) {
+    bsc = *(gcf4p)(L->in_coef + (long)L->in_g0 * Cin + ci);
+    bsh = *(gcf4p)(L->in_coef + (long)(L->in_groups + L->in_g0) * Cin + ci);
+  }
   // A 16-pixel chunk never crosses an image (OH OW >= 16, powers of two): pixel c 16 + p decodes as the chunk's
   // (img0, oy0, ox0) -- uniform, scalar -- plus (p >> lw, p & mw) without carries, so each load slot keeps a
   // constant element offset from the chunk's base pointer and only the X bounds test is per chunk and lane.
@@ -924,9 +950,19 @@ __global__ __launch_bounds__(256 * KS, 2 / KS) void cgl_conv_wgrad_lds(CglConvLa
 #pragma unroll
     for (int r = 0; r < NA; ++r) *(f32x4*)&sa0[buf * 16 * RP + (pa + (256 / FA) * r) * RP + 4 * fa] = ra[r];
 #pragma unroll
-    for (int r = 0; r < NB; ++r)
+    for (int r = 0; r < NB; ++r) {
+      f32x4 v = rb[r];
+      if constexpr (BNIN) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float w = fmaf(v[u], bsc[u], bsh[u]);
+          if (L->in_act == CGL_EPI_ACT_LEAKY) w = w > 0.f ? w : w * L->in_slope;
+          v[u] = w;
+        }
+      }
       *(f32x4*)&sb0[buf * 16 * CP + (pb + (256 / FB) * r) * CP + 4 * fb] =
-          ((okb >> r) & 1) ? rb[r] : f32x4{0.f, 0.f, 0.f, 0.f};
+          ((okb >> r) & 1) ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   };
   f32x16 acc[2][2];
 #pragma unroll
@@ -1320,7 +1356,9 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad_n1(CglConvLaunch args) {
 // STG > 0: the output-gradient window of the block's pixel range (linear dY indices qb - OW - 1 ..
 // qe + OW, host-checked to fit STG floats, dY dense with the input's height / width) is staged in LDS
 // once, so the T per-pixel gathers are LDS broadcasts instead of vector-memory instructions.
-template <int C4T, int XWT, int XHT, int CGL_N1T_PX, int REDN, int STG>
+// BNIN: X is the PRE-BatchNorm map of one forward call (group L->in_g0), applied per loaded float4 (each
+// lane's channel quad is fixed, so its scale / shift are loaded once)
+template <int C4T, int XWT, int XHT, int CGL_N1T_PX, int REDN, int STG, bool BNIN = false>
 __global__ __launch_bounds__(256) void cgl_conv_wgrad_n1t(CglConvLaunch args) {
   (void)args;
   __shared__ float red[REDN];
@@ -1338,6 +1376,11 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad_n1t(CglConvLaunch args) {
   f32x4 acc[16];
 #pragma unroll
   for (int t = 0; t < 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 isc = {0.f, 0.f, 0.f, 0.f}, ish = isc;
+  if constexpr (BNIN) {
+    isc = *(gcf4p)(L->in_coef + (long)L->in_g0 * Cin + 4 * q4);
+    ish = *(gcf4p)(L->in_coef + (long)(L->in_groups + L->in_g0) * Cin + 4 * q4);
+  }
   const float* __restrict__ dY = P->Y;
   const long wb = qb - OW - 1;
   if (STG) {
@@ -1376,6 +1419,16 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad_n1t(CglConvLaunch args) {
           d[u][t] = ok ? dv : 0.f;
         }
       }
+    }
+    if constexpr (BNIN) {
+#pragma unroll
+      for (int u = 0; u < CGL_N1T_PX; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float w = fmaf(x[u][e], isc[e], ish[e]);
+          if (L->in_act == CGL_EPI_ACT_LEAKY) w = w > 0.f ? w : w * L->in_slope;
+          x[u][e] = w;
+        }
     }
 #pragma unroll
     for (int u = 0; u < CGL_N1T_PX; ++u)
@@ -3020,9 +3073,12 @@ bool n1_ok(const CglConvProb* P, int np) {
   return true;
 }
 
-struct StatBwd { const float* x = nullptr; const float* post = nullptr; const float* mean = nullptr; float slope = 0.f; };
+struct StatBwd {
+  const float* x = nullptr; const float* post = nullptr; const float* mean = nullptr; float slope = 0.f;
+  const float* psc = nullptr; int psc_ld = 0;    // LeakyReLU'(post) from the forward's scale / shift (post null)
+};
 
-struct BnIn { const float* coef = nullptr; int groups = 1, gimg = 1, act = 0; float slope = 0.f; };
+struct BnIn { const float* coef = nullptr; int groups = 1, gimg = 1, act = 0; float slope = 0.f; int g0 = 0; };
 
 // The halo path: 4 problems over one input through one tile grid -- the output parities of an upsampling
 // conv (2x2 taps, offsets within one pixel), 64 output channels (one 2x2-block wave tile), whole 64-row
@@ -3070,6 +3126,8 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
     L.st_mode = 1;
     L.st_x = sb->x;
     L.st_post = sb->post;
+    L.st_psc = sb->psc;
+    L.st_psc_ld = sb->psc_ld;
     L.st_mean = sb->mean;
     L.st_slope = sb->slope;
   }
@@ -3333,12 +3391,16 @@ int wgrad_lds_wm(const WgradPlan& pl, bool bias_col, const float* dY, const floa
   return wm;
 }
 
+// bi (may be null): X is the PRE-BatchNorm map of one forward call, applied in the operand loads -- only the
+// LDS-staged MFMA weight gradient and the input-stationary one-output-channel one take it (CGL_E_ARG otherwise)
 int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, float* dW, float* db, void* ws,
-                         int64_t wsb, hipStream_t s) {
+                         int64_t wsb, hipStream_t s, const BnIn* bi = nullptr) {
   if (!dY || !X || !dW || !ws || !al16(ws)) return CGL_E_ARG;
   if (wsb < conv_ws_bytes(g)) return CGL_E_SIZE;
+  if (bi && (!bi->coef || !al16(bi->coef) || bi->g0 < 0 || bi->g0 >= bi->groups || g.cin % 4)) return CGL_E_ARG;
   if (g.cout > CGL_ZERO_PAGE || g.cin > CGL_ZERO_PAGE) return CGL_E_ARG;   // cgl_zero_page bound
   if (c1_ok(g)) {
+    if (bi) return CGL_E_ARG;
     const long npix = (long)g.n * g.ho * g.wo;
     CglC1Args a;
     std::memset(&a, 0, sizeof(a));
@@ -3361,6 +3423,14 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
   L.WM = 1;
   L.WN = 1;
   L.WK = 1;
+  if (bi) {
+    L.in_coef = bi->coef;
+    L.in_groups = bi->groups;
+    L.in_gimg = bi->gimg;
+    L.in_act = bi->act;
+    L.in_slope = bi->slope;
+    L.in_g0 = bi->g0;
+  }
   float* part = (float*)ws;
   const bool valu = g.cout == 1 && pl.np == 1;   // cgl_conv_wgrad_n1 (splits set by wgrad_plan)
   const bool n1t = valu && wgrad_n1t_ok(g, pl.P[0]);
@@ -3406,7 +3476,10 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
       P.wg_begin = wgl;
       wgl += P.tiles_m * P.tiles_n * P.splits;
     }
-    if (ks == 2) {
+    if (bi) {
+      if (lwm == 2) hipLaunchKernelGGL((cgl_conv_wgrad_lds<2, 2, 1, true>), dim3(wgl), dim3(256), 0, s, L);
+      else hipLaunchKernelGGL((cgl_conv_wgrad_lds<1, 4, 1, true>), dim3(wgl), dim3(256), 0, s, L);
+    } else if (ks == 2) {
       if (lwm == 2) hipLaunchKernelGGL((cgl_conv_wgrad_lds<2, 2, 2>), dim3(wgl), dim3(512), 0, s, L);
       else hipLaunchKernelGGL((cgl_conv_wgrad_lds<1, 4, 2>), dim3(wgl), dim3(512), 0, s, L);
     } else {
@@ -3414,6 +3487,8 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
       else hipLaunchKernelGGL((cgl_conv_wgrad_lds<1, 4, 1>), dim3(wgl), dim3(256), 0, s, L);
     }
   }
+  else if (bi && !(n1t && pl.P[0].Cin == 64 && pl.P[0].XW == 32 && pl.P[0].XH == 32 && pl.P[0].Ty * pl.P[0].Tx == 9))
+    return CGL_E_ARG;
   else if (n1t)
   {
     if (pl.P[0].Cin == 64 && pl.P[0].XW == 32 && pl.P[0].XH == 32 && pl.P[0].Ty * pl.P[0].Tx == 9)
@@ -3424,7 +3499,12 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
                          per_block + 2 * P0.OW + 2 <= 512;
       // one pixel per slot and step, dY window in LDS: 105 -> 57 us for the B=256 G Conv2d(64, 1)
       // (two / four pixels per step: 77 / 119 us; no staging: 90 us)
-      if (stage) hipLaunchKernelGGL((cgl_conv_wgrad_n1t<16, 32, 32, 1, 9216, 512>), dim3(P0.splits), dim3(256), 0, s, L);
+      if (bi && stage)
+        hipLaunchKernelGGL((cgl_conv_wgrad_n1t<16, 32, 32, 1, 9216, 512, true>), dim3(P0.splits), dim3(256), 0, s, L);
+      else if (bi)
+        hipLaunchKernelGGL((cgl_conv_wgrad_n1t<16, 32, 32, 1, 9216, 0, true>), dim3(P0.splits), dim3(256), 0, s, L);
+      else if (stage)
+        hipLaunchKernelGGL((cgl_conv_wgrad_n1t<16, 32, 32, 1, 9216, 512>), dim3(P0.splits), dim3(256), 0, s, L);
       else hipLaunchKernelGGL((cgl_conv_wgrad_n1t<16, 32, 32, 1, 9216, 0>), dim3(P0.splits), dim3(256), 0, s, L);
     }
     else
@@ -3497,6 +3577,24 @@ int cgl_conv3x3_bwd_weight(const float* dY, const float* X, float* dW, float* db
   const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
   if (rc) return rc;
   return conv_bwd_weight_impl(g, dY, X, dW, db, ws, wsb, (hipStream_t)stream);
+}
+
+int cgl_conv3x3_bwd_weight_bnin(const float* dY, const float* X, float* dW, float* db, int n, int h, int w, int cin,
+                                int cout, int stride, int up, const float* in_coef, int in_groups, int in_group,
+                                int in_act, float in_slope, void* ws, int64_t wsb, void* stream) {
+  ConvGeom g;
+  const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
+  if (rc) return rc;
+  if (!in_coef || in_groups < 1 || in_group < 0 || in_group >= in_groups || (in_act != 0 && in_act != 1))
+    return CGL_E_ARG;
+  BnIn bi;
+  bi.coef = in_coef;
+  bi.groups = in_groups;
+  bi.gimg = n;
+  bi.act = in_act;
+  bi.slope = in_slope;
+  bi.g0 = in_group;
+  return conv_bwd_weight_impl(g, dY, X, dW, db, ws, wsb, (hipStream_t)stream, &bi);
 }
 
 int64_t cgl_dense_workspace_bytes(int M, int K, int N) {
@@ -3627,14 +3725,15 @@ int64_t cgl_conv3x3_bwd_stat_chunks(int n, int h, int w, int cin, int cout, int 
 
 int cgl_conv3x3_bwd_data_packed_stats(const float* dY, const float* Wp, float* dX, int n, int h, int w, int cin,
                                       int cout, int stride, int up, int groups, double* part, const float* bn_x,
-                                      const float* bn_post, const float* bn_mean, float slope, void* ws, int64_t wsb,
-                                      void* stream) {
+                                      const float* bn_post, const float* bn_post_coef, int bn_post_coef_ld,
+                                      const float* bn_mean, float slope, void* ws, int64_t wsb, void* stream) {
   ConvGeom g;
   const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
   if (rc) return rc;
-  if (!Wp || !part) return CGL_E_ARG;
+  if (!Wp || !part || (bn_post_coef && (bn_post || groups != 1))) return CGL_E_ARG;
   StatBwd sb;
   sb.x = bn_x; sb.post = bn_post; sb.mean = bn_mean; sb.slope = slope;
+  sb.psc = bn_post_coef; sb.psc_ld = bn_post_coef_ld;
   return conv_bwd_data_impl(g, dY, nullptr, dX, ws, wsb, (hipStream_t)stream, Wp, part, groups, &sb);
 }
 

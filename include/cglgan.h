@@ -250,6 +250,15 @@ int cgl_conv3x3_bwd_data(const float* dY, const float* W, float* dX, int n, int 
 /* dW[cout][cin][3][3] and db[cout] (may be null) of the convolution from dY and its input X. */
 int cgl_conv3x3_bwd_weight(const float* dY, const float* X, float* dW, float* db, int n, int h, int w, int cin,
                            int cout, int stride, int up, void* workspace, int64_t ws_bytes, void* stream);
+/* cgl_conv3x3_bwd_weight with X the PRE-BatchNorm map of forward call in_group of in_groups: the convolution's
+ * input is LeakyReLU(fmaf(x, scale, shift)) (when in_act == 1; else the affine alone), scale / shift from
+ * in_coef [2][in_groups][cin] (cgl_bn2d_fwd_stats_coef's coef), applied in the operand loads -- cgl_eltwise's
+ * arithmetic, so the result equals the call on the applied activation bit for bit, and the activation need not
+ * be stored.  Supported where the weight gradient stages its operands (the LDS-staged MFMA kernel: the G
+ * up-convolutions of model/lsgan.py:11,15; the input-stationary Conv2d(64, 1) of :19); CGL_E_ARG elsewhere. */
+int cgl_conv3x3_bwd_weight_bnin(const float* dY, const float* X, float* dW, float* db, int n, int h, int w, int cin,
+                                int cout, int stride, int up, const float* in_coef, int in_groups, int in_group,
+                                int in_act, float in_slope, void* workspace, int64_t ws_bytes, void* stream);
 
 /* Stream-ordered dense layer on the same implicit-GEMM kernels (a 1x1 convolution of M "pixels"):
  * Y[M][N] = act(X[M][K] W[N][K]^T + b) -- nn.Linear of model/lsgan.py:8 (l1, 100 -> 8192) and
@@ -310,12 +319,15 @@ int cgl_conv3x3_fwd_packed_bnin(const float* X, const float* Wp, const float* bi
  * part [groups * chunks][cin][2] = {sum g, sum g (x - mean)} per 32-row chunk of dX, g = dX (*
  * leaky'(bn_post) when bn_post is given), x = bn_x (the BatchNorm input) and mean = bn_mean
  * [groups][cin] (the saved per-call mean), all at dX's positions.  Consumed by cgl_bn2d_bwd_stats.
+ * bn_post_coef (may be null; then bn_post): leaky' from the sign of fmaf(bn_x, scale, shift) with scale =
+ * bn_post_coef[c], shift = bn_post_coef[bn_post_coef_ld + c] (cgl_bn2d_bwd's post_coef; groups == 1).
  * cgl_conv3x3_bwd_stat_chunks: chunk count (0: unsupported). */
 int64_t cgl_conv3x3_bwd_stat_chunks(int n, int h, int w, int cin, int cout, int stride, int up, int groups);
 int cgl_conv3x3_bwd_data_packed_stats(const float* dY, const float* Wp, float* dX, int n, int h, int w, int cin,
                                       int cout, int stride, int up, int groups, double* part, const float* bn_x,
-                                      const float* bn_post, const float* bn_mean, float slope, void* workspace,
-                                      int64_t ws_bytes, void* stream);
+                                      const float* bn_post, const float* bn_post_coef, int bn_post_coef_ld,
+                                      const float* bn_mean, float slope, void* workspace, int64_t ws_bytes,
+                                      void* stream);
 int cgl_dense_fwd_packed(const float* X, const float* Wp, const float* b, float* Y, int M, int K, int N, int act,
                          float slope, void* workspace, int64_t ws_bytes, void* stream);
 int cgl_dense_bwd_data_packed(const float* dY, const float* Wp, float* dX, int M, int K, int N, void* workspace,

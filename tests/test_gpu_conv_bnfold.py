@@ -17,10 +17,12 @@ def _pair(B, graph, data, mask):
     steps = []
     for fold in (mask, 0):
         os.environ["CGL_CONV_BNFOLD"] = str(fold)
+        os.environ["CGL_CONV_ELIDE"] = "0"      # (the elision is tests/test_gpu_conv_fusions.py's)
         try:
             st = ConvGanStep(B, seed=21, data=data, graph=graph)
         finally:
             os.environ.pop("CGL_CONV_BNFOLD", None)
+            os.environ.pop("CGL_CONV_ELIDE", None)
         st.init_default(5, 6)
         steps.append(st)
     assert steps[0].bn_fold == mask and not steps[1].bn_fold

@@ -4,7 +4,10 @@
     fmaf(y, scale, shift) (cgl_bn2d_bwd / cgl_bn2d_bwd_stats post_coef: the coef the forward finalize kept)
     instead of reading the activation a -- the forward wrote a = LeakyReLU(that value);
   * CGL_CONV_DFOLD: in the G-loss pass, D's inner BatchNorm2d layers are applied in the next conv's operand
-    load (bn_in, cgl_eltwise's fmaf) instead of an apply pass -- nothing else reads their output there."""
+    load (bn_in, cgl_eltwise's fmaf) instead of an apply pass -- nothing else reads their output there;
+  * CGL_CONV_ELIDE: a folded G BatchNorm's activation (a1 / a2) is not stored at all -- the G backward's weight
+    gradients apply the BatchNorm in their operand loads (cgl_conv3x3_bwd_weight_bnin) and every LeakyReLU'
+    comes from the kept scale / shift (with the same fold mask on both sides)."""
 import os
 
 import pytest
@@ -30,7 +33,9 @@ def _step(B, graph, data, env):
 
 
 CASES = [("CGL_CONV_POSTCOEF", 8, False, "2"), ("CGL_CONV_POSTCOEF", 256, False, "0"),
-         ("CGL_CONV_POSTCOEF", 256, True, "2"), ("CGL_CONV_DFOLD", 8, False, "2"), ("CGL_CONV_DFOLD", 256, True, "2")]
+         ("CGL_CONV_POSTCOEF", 256, True, "2"), ("CGL_CONV_DFOLD", 8, False, "2"), ("CGL_CONV_DFOLD", 256, True, "2"),
+         ("CGL_CONV_ELIDE", 8, False, "3"), ("CGL_CONV_ELIDE", 256, False, "3"), ("CGL_CONV_ELIDE", 256, True, "3"),
+         ("CGL_CONV_ELIDE", 256, True, "2")]
 
 
 @pytest.mark.parametrize("var,B,graph,fold", CASES)
@@ -47,8 +52,12 @@ def test_conv_round_fusion_bitwise(var, B, graph, fold):
     if var == "CGL_CONV_POSTCOEF":
         assert a.post_coef_on and not b.post_coef_on
         assert {"conv_blocks.2", "conv_blocks.6"} <= a.coef_kept
-    else:
+    elif var == "CGL_CONV_DFOLD":
         assert a.d_fold and not b.d_fold
+    else:
+        assert a.elide_on and not b.elide_on and a.bn_fold == b.bn_fold
+        for k in ("a1", "a2"):
+            assert torch.allclose(a.g_act(k), b.g_act(k), rtol=1e-6, atol=1e-6), k
     for name in ("p", "g", "m", "v"):
         assert torch.equal(getattr(a.G, name), getattr(b.G, name)), ("G", name)
         assert torch.equal(getattr(a.D, name), getattr(b.D, name)), ("D", name)

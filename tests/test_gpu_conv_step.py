@@ -66,9 +66,9 @@ def _gpu_signs(st, d_calls):
     the sign, so y > 0 <=> x > 0 on the stored outputs (G: a1, a2; D: q_k = Dropout2d(LeakyReLU))."""
     B = st.B
     nchw = lambda t: t.permute(0, 3, 1, 2).cpu()
-    a1, a2 = nchw(st.a1 > 0), nchw(st.a2 > 0)
-    # the Xd half of a1 / a2 is not written when the G BatchNorm is folded into the next conv's load
-    signs = {"g1": [nchw(st.g_act_xd("a1") > 0), nchw(st.g_act_xd("a2") > 0)], "g2": [a1[B:], a2[B:]]}
+    # a1 / a2 are not stored (or only their Xg half) when the G BatchNorm is folded into the next conv's load
+    a1, a2 = nchw(st.g_act("a1") > 0), nchw(st.g_act("a2") > 0)
+    signs = {"g1": [a1[:B], a2[:B]], "g2": [a1[B:], a2[B:]]}
     valid = {"g1": [None, None], "g2": [None, None]}
     (dstep, dgl) = d_calls
     signs["dr"] = [nchw(q[:B] > 0) for q in dstep]
