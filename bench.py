@@ -146,7 +146,7 @@ def traffic_per_gemm_launch():
     newest committed FETCH_SIZE / WRITE_SIZE passes (tools/gpu_session.sh traffic -> tools/pmc_traffic.py).
     A static, labelled measurement: PMC passes cannot run inside the timed bench, so roofline.traffic
     names the profile file and the commit it was measured at (traffic_source).  None when absent."""
-    name, d = _latest_profile(["r03_traffic.json", "r02_traffic.json"])
+    name, d = _latest_profile(["r04_traffic.json", "r03_traffic.json", "r02_traffic.json"])
     if d is None:
         return None, None
     src = {"file": f"profiles/{name}", "commit": (d.get("_meta") or {}).get("commit"),
@@ -158,6 +158,24 @@ def traffic_per_gemm_launch():
         if "cgl_gemm_f32" in k:
             return round(v["bytes_per_dispatch"]), src
     return None, None
+
+
+def traffic_per_launch():
+    """Per-launch PMC traffic of the round's GEMM launches against each launch's own compulsory bytes
+    (A + B + C of its descriptors, f32), from the newest committed per-launch pass (tools/pmc_traffic.py
+    --plan): [{"i": position in the round, "bytes", "algorithmic", "ratio"}], plus the launch-summed ratio."""
+    name, d = _latest_profile(["r04_traffic.json"])
+    if not d or "per_launch" not in d:
+        return {}
+    rows = [{"i": e["i"], "kernel": e["kernel"].split("<")[0], "bytes": round(e["bytes"]),
+             "algorithmic": e["algorithmic_bytes"], "ratio": e["ratio"]}
+            for e in d["per_launch"] if "algorithmic_bytes" in e]
+    # the ratio over the cgl_gemm_f32 launches (the fused prologue also moves the round's operand packing)
+    g = [r for r in rows if r["kernel"] == "cgl_gemm_f32"]
+    tb, ta = sum(r["bytes"] for r in g), sum(r["algorithmic"] for r in g)
+    return {"traffic_per_launch": rows, "traffic_ratio_launch_sum": round(tb / ta, 3) if ta else None,
+            "traffic_per_launch_source": f"profiles/{name} (static PMC measurement, commit "
+                                         f"{(d.get('_meta') or {}).get('commit')})"}
 
 
 def mlp_traffic_algorithmic(B, gemm_n):
@@ -341,7 +359,8 @@ def conv_cpu_baseline(a, threads=None):
 def conv_traffic():
     """HBM-side traffic of the dominant conv op per dispatch from the newest committed PMC passes
     (tools/conv_traffic.py: FETCH_SIZE x2 + WRITE_SIZE; None when absent), labelled with its source."""
-    name, p = _latest_profile(["r03_conv_dominant_traffic.json", "r02_conv_dominant_traffic.json"])
+    name, p = _latest_profile(["r04_conv_dominant_traffic.json", "r03_conv_dominant_traffic.json",
+                               "r02_conv_dominant_traffic.json"])
     if p is None:
         return {"traffic": None}
     return {"traffic": round(p["bytes"]), "traffic_unit": f"bytes per {p['kernel']} dispatch of the dominant op "
@@ -597,6 +616,7 @@ def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None,
                      "traffic_unit": "bytes per GEMM launch, all cgl_gemm_f32 instantiations (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                      "traffic_source": traffic_per_gemm_launch()[1] if a.model == "mlp" else None,
                      **(mlp_traffic_algorithmic(a.batch, gemm_n) if a.model == "mlp" else {}),
+                     **(traffic_per_launch() if a.model == "mlp" else {}),
                      "gemm_launches_per_round": gemm_n, "gemm_flops_per_round": gemm_flops,
                      "flops_per_gemm_launch": gemm_flops / max(gemm_n, 1),
                      "avg_gemm_launch_us": round(sum(gemm_us) * scale / max(gemm_n, 1), 3),

@@ -154,7 +154,8 @@ def _load():
                                     vp]),
         "cgl_bn2d_fwd_stats_coef": (ci, [vp, ci, vp, ci, ci, ci, ci, vp, vp, cd, cd, vp, vp, ci, cf, vp, vp, vp, vp, vp, ci,
                                          vp, vp, i64, vp]),
-        "cgl_conv3x3_fwd_packed_bnin": (ci, [vp, vp, vp, vp] + [ci] * 8 + [cf, vp, ci, vp, vp, ci, ci, cf, vp, i64, vp]),
+        "cgl_conv3x3_fwd_packed_bnin": (ci, [vp, vp, vp, vp] + [ci] * 8 + [cf, vp, ci, vp, vp, ci, ci, cf, vp, vp, i64,
+                                                                      vp]),
         "cgl_bn2d_stats_scratch_bytes": (i64, [ci, ci]),
         "cgl_linear_desc_bytes": (i64, []),
         "cgl_conv3x3_bwd_stat_chunks": (i64, [ci] * 8),

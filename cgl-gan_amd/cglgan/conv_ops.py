@@ -108,8 +108,8 @@ def conv3x3_fwd(x, w, b, y, n, h, wd, cin, cout, stride=1, up=0, act=ACT_NONE, s
     rest padding, left out of the statistics; see bn2d_fwd)."""
     _chk(x, w, b, y, drop, wp)
     ws = workspace(conv_ws_bytes(n, h, wd, cin, cout, stride, up), x.device)
-    if nvalid is not None and (stats is None or bn_in is not None):
-        raise RuntimeError("conv3x3_fwd(nvalid=...): only with stats= and without bn_in=")
+    if nvalid is not None and stats is None:
+        raise RuntimeError("conv3x3_fwd(nvalid=...): only with stats=")
     if bn_in is not None:
         coef, groups_in, act_in, slope_in = bn_in
         _chk(coef)
@@ -118,8 +118,8 @@ def conv3x3_fwd(x, w, b, y, n, h, wd, cin, cout, stride=1, up=0, act=ACT_NONE, s
             raise RuntimeError("conv3x3_fwd(bn_in=...): needs packed weights")
         C.check(C.lib.cgl_conv3x3_fwd_packed_bnin(_p(x), _p(wp), _p(b), _p(y), n, h, wd, cin, cout, stride, up, act,
                                                   float(slope), _p(drop), int(groups), _p(part), _p(coef),
-                                                  int(groups_in), int(act_in), float(slope_in), _p(ws), ws.numel(),
-                                                  _s()), "cgl_conv3x3_fwd_packed_bnin")
+                                                  int(groups_in), int(act_in), float(slope_in), _p(nvalid), _p(ws),
+                                                  ws.numel(), _s()), "cgl_conv3x3_fwd_packed_bnin")
         return y
     if stats is not None:
         part, groups = stats
@@ -166,8 +166,9 @@ def conv3x3_bwd_data(dy, w, dx, n, h, wd, cin, cout, stride=1, up=0, wp=None, st
 
 
 def conv3x3_bwd_weight(dy, x, dw, db, n, h, wd, cin, cout, stride=1, up=0, bn_in=None):
-    """``bn_in`` = (coef, group, groups, act, slope): ``x`` is the PRE-BatchNorm map of forward call ``group``;
-    the BatchNorm (+ LeakyReLU) is applied in the operand loads (cgl_conv3x3_bwd_weight_bnin)."""
+    """``bn_in`` = (coef, group, groups, act, slope): ``x`` is the PRE-BatchNorm map of forward call ``group``
+    (-1: ``groups`` stacked calls of n / groups images); the BatchNorm (+ LeakyReLU) is applied in the operand
+    loads (cgl_conv3x3_bwd_weight_bnin)."""
     _chk(dy, x, dw, db)
     ws = workspace(conv_ws_bytes(n, h, wd, cin, cout, stride, up), dy.device)
     if bn_in is not None:

@@ -239,9 +239,11 @@ class ConvGanStep:
         # element and measured slower than the separate pass (profiles/r03_conv_bnfold_ab.txt)
         # CGL_CONV_ELIDE (default 1): with a layer folded, its activation is not stored at all -- the G backward
         # applies the BatchNorm in the weight gradient's operand loads (cgl_conv3x3_bwd_weight_bnin) and takes
-        # LeakyReLU' from the kept scale / shift -- and the default fold mask becomes 3 (both layers)
+        # LeakyReLU' from the kept scale / shift.  Measured (profiles/r04_conv_elide_ab.txt): a2 (fold bit 2, the
+        # default) -28 us per round; a1 (bit 1) costs more in the LDS weight gradient's staging (+43 us) than its
+        # apply pass saves, so the default mask stays 2
         self.elide_on = os.environ.get("CGL_CONV_ELIDE", "1") != "0"
-        fold = int(os.environ.get("CGL_CONV_BNFOLD", "3" if self.elide_on else "2"))
+        fold = int(os.environ.get("CGL_CONV_BNFOLD", "2"))
         self.bn_fold = fold & 3 if all(k in self.st_part for k in ("conv_blocks.2", "conv_blocks.6")) else 0
         self.coef = {k: torch.zeros(4 * c, dtype=torch.float32, device=dev)
                      for k, c in (("conv_blocks.2", 128), ("conv_blocks.6", 64))}
@@ -251,6 +253,10 @@ class ConvGanStep:
         self.coef_kept = set()
         # D's inner BatchNorms folded into the next conv in the G-loss pass (_d_forward); [2][groups][C] scale / shift
         self.d_fold = os.environ.get("CGL_CONV_DFOLD", "1") != "0"
+        # ... and in the D step too (CGL_CONV_DFOLD_STEP=1): correct and bitwise, but the wave-unit weight gradient's
+        # per-value BatchNorm costs +41 us against the two apply passes it saves (profiles/r04_conv_elide_ab.txt)
+        self.d_fold_step = os.environ.get("CGL_CONV_DFOLD_STEP", "0") == "1"
+        self._d_folded = set()   # D-step BatchNorms folded this round (their weight gradients apply them)
         self.dcoef = {bk: torch.zeros(4 * co, dtype=torch.float32, device=dev) for _, bk, _, co, _ in D_CONVS if bk}
         self.post_coef_on = os.environ.get("CGL_CONV_POSTCOEF", "1") != "0"
         # backward statistics: the same buffers (the forward's partials are consumed by then), written
@@ -448,11 +454,15 @@ class ConvGanStep:
 
     def _d_forward(self, x, n, groups, masks, nvalid=None):
         """``nvalid``: the first call (the real images) is a short batch of *nvalid images.
-        The G-loss pass (masks = mask_g) folds each inner BatchNorm2d into the next conv's operand load
-        (its output r is read by nothing else there: no D weight gradient in that pass), so those BatchNorms
-        write no activation -- two cgl_eltwise passes fewer; CGL_CONV_DFOLD=0 applies them."""
+        Each inner BatchNorm2d is folded into the next conv's operand load (bn_in) and writes no activation:
+        in the G-loss pass nothing else reads it; in the D step (opt-in, d_fold_step) the next conv's weight
+        gradient applies it in its operand loads too (cgl_conv3x3_bwd_weight_bnin) -- two cgl_eltwise passes fewer
+        per pass; CGL_CONV_DFOLD=0 applies them."""
         P, R = self.D.params, self.D.running
-        fold_pass = self.d_fold and masks is self.mask_g and groups == 1 and nvalid is None
+        fold_pass = self.d_fold and ((masks is self.mask_g and groups == 1) or
+                                     (masks is self.mask_d and self.d_fold_step))
+        if masks is self.mask_d:
+            self._d_folded = set()
         inp, bn_in = x, None
         for k, (ck, bk, ci, co, hw) in enumerate(D_CONVS):
             st = self._stats(bk, groups) if bk else None
@@ -466,6 +476,8 @@ class ConvGanStep:
                              coef_only=fold)
                 if fold:
                     bn_in = (self.dcoef[bk], groups, O.ACT_NONE, SLOPE)
+                    if masks is self.mask_d:
+                        self._d_folded.add(bk)
                 else:
                     inp = self.r[k]
         # out.view(B, -1) -> adv_layer (model/lsgan.py:96-97) from the NHWC map; the D step's call keeps the
@@ -494,7 +506,11 @@ class ConvGanStep:
             else:
                 O.act_drop_bwd(self.dq1, self.q[0], masks[0], n, ho * ho, co, self.dc[0], slope=SLOPE)
             inp = x if k == 0 else (self.q[0] if k == 1 else self.r[k - 1])
-            if wgrad:
+            pfold = k > 1 and D_CONVS[k - 1][1] in self._d_folded
+            if wgrad and pfold:     # r[k - 1] = BN(q[k - 1]) applied in the operand loads (both calls of the step)
+                O.conv3x3_bwd_weight(self.dc[k], self.q[k - 1], G[ck + ".weight"], G[ck + ".bias"], n, hw, hw, ci, co,
+                                     2, 0, bn_in=(self.dcoef[D_CONVS[k - 1][1]], -1, groups, O.ACT_NONE, SLOPE))
+            elif wgrad:
                 O.conv3x3_bwd_weight(self.dc[k], inp, G[ck + ".weight"], G[ck + ".bias"], n, hw, hw, ci, co, 2, 0)
             if k > 0:
                 pbk = D_CONVS[k - 1][1]

@@ -673,7 +673,9 @@ __device__ float cgl_zero_page[CGL_ZERO_PAGE];
 // ROW: every problem of the launch has OW % 8 == 0 and M % 16 == 0, so the 8 pixels of a lane
 // half are always valid and lie in one output row: one pixel decode per chunk, constant address
 // strides along the row, the tap's row bounds checked once (a fraction of the generic path's VALU).
-template <int TM, int TN, bool ROW>
+// BNIN: X is the PRE-BatchNorm map (groups of L->in_gimg images, scale / shift in L->in_coef): each valid
+// im2col value is fmaf(x, scale, shift) (+ LeakyReLU), cgl_eltwise's arithmetic; padded taps stay zero
+template <int TM, int TN, bool ROW, bool BNIN = false>
 __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local) {
 #ifndef CGL_WGRAD_S
 #define CGL_WGRAD_S 2
@@ -716,6 +718,24 @@ __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local)
     cdy[j] = P->dy[ty];
     cdx[j] = P->dx[tx];
   }
+  // BNIN: this lane's columns' scale / shift for up to two BatchNorm groups (the D step's two calls: group
+  // in_g0 + img / in_gimg)
+  float bsc[2][TN], bsh[2][TN];
+  const int bg = BNIN ? max(1, min(L->in_groups - L->in_g0, 2)) : 1;
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const long gq = L->in_g0 + min(q, bg - 1);
+      bsc[q][j] = BNIN ? gld(L->in_coef + gq * Cin + cci[j]) : 0.f;
+      bsh[q][j] = BNIN ? gld(L->in_coef + (L->in_groups + gq) * Cin + cci[j]) : 0.f;
+    }
+  auto bn = [&](float x, int img, int j) {
+    const int q = (bg > 1 && img >= L->in_gimg) ? 1 : 0;     // (<= 2 groups: no division per value)
+    float v = fmaf(x, q ? bsc[1][j] : bsc[0][j], q ? bsh[1][j] : bsh[0][j]);
+    if (L->in_act == CGL_EPI_ACT_LEAKY) v = v > 0.f ? v : v * L->in_slope;
+    return v;
+  };
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -750,6 +770,7 @@ __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local)
           const bool ok = rowok && (unsigned)ix < (unsigned)IW;
           const float* bb = ok ? rb + (long)(ix >> ish) * Cin : zp + cci[j];
           B[j][q] = *(gcfp)bb;
+          if (BNIN) B[j][q] = ok ? bn(B[j][q], img, j) : 0.f;
         }
       }
 #pragma unroll
@@ -787,6 +808,7 @@ __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local)
         const bool ok = mv && cok[j] && (unsigned)iy < (unsigned)IH && (unsigned)ix < (unsigned)IW;
         const float* bb = ok ? X + xo + ((long)(iy >> ish) * XW + (ix >> ish)) * Cin : zp;
         B[j][q] = ((gcfp)bb)[cci[j]];
+        if (BNIN) B[j][q] = ok ? bn(B[j][q], img, j) : 0.f;
         B[j][q] = cone[j] ? (mv ? 1.f : 0.f) : B[j][q];
       }
     }
@@ -838,14 +860,14 @@ __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local)
   }
 }
 
-template <int TM, int TN, bool ROW = false>
+template <int TM, int TN, bool ROW = false, bool BNIN = false>
 __global__ __launch_bounds__(256) void cgl_conv_wgrad(CglConvLaunch args) {
   (void)args;
   CglKL L = cgl_conv_args();
   const int bid = blockIdx.x;
   const int pi = cgl_conv_prob(L, bid);
   CglKP P = &L->p[pi];
-  cgl_conv_wgrad_body<TM, TN, ROW>(L, P, bid - P->wg_begin);
+  cgl_conv_wgrad_body<TM, TN, ROW, BNIN>(L, P, bid - P->wg_begin);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3460,6 +3482,7 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
     for (int k = 0; k < 4; ++k) { r.ym[i][k] = P.ym[k]; r.xm[i][k] = P.xm[k]; }
   }
   const int lwm = valu ? 0 : wgrad_lds_wm(pl, bias_col, dY, X);
+  if (bi && bi->gimg < g.n && (lwm || valu)) return CGL_E_ARG;   // stacked calls: the wave-unit kernel only
   if (lwm) {
     // workgroup tiles of 64 lwm x 256 / lwm over the plan's pixel splits (partials as sized by wgrad_plan);
     // CGL_WGRAD_KS = 2: two-half workgroups over half as many (twice as long) splits.  Measured neutral
@@ -3487,8 +3510,22 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
       else hipLaunchKernelGGL((cgl_conv_wgrad_lds<1, 4, 1>), dim3(wgl), dim3(256), 0, s, L);
     }
   }
-  else if (bi && !(n1t && pl.P[0].Cin == 64 && pl.P[0].XW == 32 && pl.P[0].XH == 32 && pl.P[0].Ty * pl.P[0].Tx == 9))
+  else if (bi && valu && !(n1t && pl.P[0].Cin == 64 && pl.P[0].XW == 32 && pl.P[0].XH == 32 &&
+                          pl.P[0].Ty * pl.P[0].Tx == 9))
     return CGL_E_ARG;
+  else if (bi && !valu) {
+    // the wave-unit MFMA weight gradient with the BatchNorm applied per loaded value (up to two groups)
+    if (bi->groups - bi->g0 > 2 && bi->gimg < g.n) return CGL_E_ARG;
+    if (wgrad_row_ok(pl)) {
+      if (pl.t.TM == 2 && pl.t.TN == 2) hipLaunchKernelGGL((cgl_conv_wgrad<2, 2, true, true>), dim3(wg), dim3(256), 0, s, L);
+      else if (pl.t.TN == 2) hipLaunchKernelGGL((cgl_conv_wgrad<1, 2, true, true>), dim3(wg), dim3(256), 0, s, L);
+      else if (pl.t.TM == 2) hipLaunchKernelGGL((cgl_conv_wgrad<2, 1, true, true>), dim3(wg), dim3(256), 0, s, L);
+      else hipLaunchKernelGGL((cgl_conv_wgrad<1, 1, true, true>), dim3(wg), dim3(256), 0, s, L);
+    } else if (pl.t.TM == 2 && pl.t.TN == 2) hipLaunchKernelGGL((cgl_conv_wgrad<2, 2, false, true>), dim3(wg), dim3(256), 0, s, L);
+    else if (pl.t.TN == 2) hipLaunchKernelGGL((cgl_conv_wgrad<1, 2, false, true>), dim3(wg), dim3(256), 0, s, L);
+    else if (pl.t.TM == 2) hipLaunchKernelGGL((cgl_conv_wgrad<2, 1, false, true>), dim3(wg), dim3(256), 0, s, L);
+    else hipLaunchKernelGGL((cgl_conv_wgrad<1, 1, false, true>), dim3(wg), dim3(256), 0, s, L);
+  }
   else if (n1t)
   {
     if (pl.P[0].Cin == 64 && pl.P[0].XW == 32 && pl.P[0].XH == 32 && pl.P[0].Ty * pl.P[0].Tx == 9)
@@ -3585,15 +3622,17 @@ int cgl_conv3x3_bwd_weight_bnin(const float* dY, const float* X, float* dW, floa
   ConvGeom g;
   const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
   if (rc) return rc;
-  if (!in_coef || in_groups < 1 || in_group < 0 || in_group >= in_groups || (in_act != 0 && in_act != 1))
+  // in_group >= 0: every image is of that forward call; -1: n / in_groups images per call, stacked
+  if (!in_coef || in_groups < 1 || in_group < -1 || in_group >= in_groups || (in_act != 0 && in_act != 1) ||
+      (in_group < 0 && n % in_groups))
     return CGL_E_ARG;
   BnIn bi;
   bi.coef = in_coef;
   bi.groups = in_groups;
-  bi.gimg = n;
+  bi.gimg = in_group >= 0 ? n : n / in_groups;
   bi.act = in_act;
   bi.slope = in_slope;
-  bi.g0 = in_group;
+  bi.g0 = in_group >= 0 ? in_group : 0;
   return conv_bwd_weight_impl(g, dY, X, dW, db, ws, wsb, (hipStream_t)stream, &bi);
 }
 
@@ -3701,7 +3740,7 @@ int cgl_conv3x3_fwd_packed_stats(const float* X, const float* Wp, const float* b
 int cgl_conv3x3_fwd_packed_bnin(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w,
                                 int cin, int cout, int stride, int up, int act, float slope, const float* drop,
                                 int groups, double* part, const float* in_coef, int in_groups, int in_act,
-                                float in_slope, void* ws, int64_t wsb, void* stream) {
+                                float in_slope, const int* nvalid, void* ws, int64_t wsb, void* stream) {
   ConvGeom g;
   const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
   if (rc) return rc;
@@ -3712,8 +3751,9 @@ int cgl_conv3x3_fwd_packed_bnin(const float* X, const float* Wp, const float* bi
   bi.gimg = n / in_groups;
   bi.act = in_act;
   bi.slope = in_slope;
+  if (nvalid && !part) return CGL_E_ARG;
   return conv_fwd_impl(g, X, nullptr, bias, Y, act, slope, drop, ws, wsb, (hipStream_t)stream, Wp, part,
-                       part ? groups : 1, &bi);
+                       part ? groups : 1, &bi, nvalid);
 }
 
 int64_t cgl_conv3x3_bwd_stat_chunks(int n, int h, int w, int cin, int cout, int stride, int up, int groups) {

@@ -886,7 +886,15 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
+#ifdef CGL_C_STORE_WT
+            // experiment: write-through (agent-scope) output stores, so no dirty C lines are left in L2 for the
+            // end-of-kernel write-back
+            if (row < M)
+              __hip_atomic_store((CGL_GLOBAL float*)(C + (long)row * ldc + col), v[r], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+#else
             if (row < M) gst(C + (long)row * ldc + col, v[r]);
+#endif
           }
           if constexpr (ADAM) cgl_epi_adam(d, d->ad_p, d->ad_m, d->ad_v, rbase + 32 * i, M, col, ldc, v);
         }

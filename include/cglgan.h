@@ -254,8 +254,10 @@ int cgl_conv3x3_bwd_weight(const float* dY, const float* X, float* dW, float* db
  * input is LeakyReLU(fmaf(x, scale, shift)) (when in_act == 1; else the affine alone), scale / shift from
  * in_coef [2][in_groups][cin] (cgl_bn2d_fwd_stats_coef's coef), applied in the operand loads -- cgl_eltwise's
  * arithmetic, so the result equals the call on the applied activation bit for bit, and the activation need not
- * be stored.  Supported where the weight gradient stages its operands (the LDS-staged MFMA kernel: the G
- * up-convolutions of model/lsgan.py:11,15; the input-stationary Conv2d(64, 1) of :19); CGL_E_ARG elsewhere. */
+ * be stored.  in_group = -1: X stacks in_groups forward calls of n / in_groups images each (the D step's real
+ * and fake calls; at most 2, the wave-unit MFMA weight gradient only).  Supported by the LDS-staged MFMA kernel
+ * (the G up-convolutions of model/lsgan.py:11,15), the input-stationary Conv2d(64, 1) of :19 (one call) and
+ * the wave-unit MFMA weight gradient (the D convolutions of :78); CGL_E_ARG elsewhere. */
 int cgl_conv3x3_bwd_weight_bnin(const float* dY, const float* X, float* dW, float* db, int n, int h, int w, int cin,
                                 int cout, int stride, int up, const float* in_coef, int in_groups, int in_group,
                                 int in_act, float in_slope, void* workspace, int64_t ws_bytes, void* stream);
@@ -314,7 +316,7 @@ int cgl_conv3x3_fwd_packed_stats(const float* X, const float* Wp, const float* b
 int cgl_conv3x3_fwd_packed_bnin(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w,
                                 int cin, int cout, int stride, int up, int act, float slope, const float* drop,
                                 int groups, double* part, const float* in_coef, int in_groups, int in_act,
-                                float in_slope, void* ws, int64_t wsb, void* stream);
+                                float in_slope, const int* nvalid, void* ws, int64_t wsb, void* stream);
 /* The input gradient with the previous BatchNorm2d's backward statistics computed in its epilogue:
  * part [groups * chunks][cin][2] = {sum g, sum g (x - mean)} per 32-row chunk of dX, g = dX (*
  * leaky'(bn_post) when bn_post is given), x = bn_x (the BatchNorm input) and mean = bn_mean
