@@ -886,9 +886,11 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
-#ifdef CGL_C_STORE_WT
-            // experiment: write-through (agent-scope) output stores, so no dirty C lines are left in L2 for the
-            // end-of-kernel write-back
+#ifndef CGL_C_STORE_WB
+            // write-through (agent-scope) output stores: no dirty C lines are left in the XCD's L2 for the
+            // end-of-kernel write-back, and the next launch (on any XCD) reads them from MALL either way.
+            // Measured -1.0 us per B = 256 round, interleaved x3 twice (profiles/r04_store_wt_ab.txt); making
+            // every plain store write-through (CGL_GST_WT) gave nothing.  -DCGL_C_STORE_WB: plain stores.
             if (row < M)
               __hip_atomic_store((CGL_GLOBAL float*)(C + (long)row * ldc + col), v[r], __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);

@@ -25,7 +25,15 @@ typedef CGL_GLOBAL float* gfp;
 typedef const CGL_GLOBAL f32x4* gcf4p;
 typedef CGL_GLOBAL f32x4* gf4p;
 __device__ __forceinline__ float gld(const float* p) { return *(gcfp)p; }
+#ifdef CGL_GST_WT
+// experiment: every plain store write-through at agent scope (no dirty lines left in L2 for the end-of-kernel
+// write-back)
+__device__ __forceinline__ void gst(float* p, float v) {
+  __hip_atomic_store((gfp)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#else
 __device__ __forceinline__ void gst(float* p, float v) { *(gfp)p = v; }
+#endif
 __device__ __forceinline__ int gldi(const int* p) { return *(const CGL_GLOBAL int*)p; }
 
 // Tanh of the generator output and its derivative.  The derivative 1 - t^2 cancels as |t| -> 1
