@@ -583,13 +583,16 @@ def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None,
     if rank != 0:
         return None
     # The graph-replayed timed rounds run their launches back to back (the rocprofv3 graph-round timeline,
-    # profiles/r04_graph_round_timeline.txt: 0.0 us between launches), so the timed period IS the sum of the
-    # round's launch durations.  Each launch's duration in the timed rounds = its eager in-round duration x
-    # (timed period / eager sum): the roofline then prices the same rounds `value` counts.  N > 1 (the period
-    # also holds the collectives) and --eager keep the eager durations.
+    # profiles/r04_final_graph_round_timeline.txt: 0.0 us between launches), so the timed period IS the sum of
+    # the round's launch durations.  An eager dispatch's event interval differs from the same launch's duration in
+    # a graph replay by about the same amount for every launch (rocprofv3 of both: 3.2-3.7 us on each of 27 of
+    # the 28 launches, gpurun_out/r04q), so each launch's duration in the timed rounds = its eager in-round
+    # duration + (timed period - eager sum) / launches: the roofline prices the same rounds `value` counts.
+    # N > 1 (the period also holds the collectives) and --eager keep the eager durations.
     eager_us = sum(v[0] for v in per_kind.values())
-    scale = (ms_step * 1e3 / eager_us) if (world == 1 and not a.eager and eager_us > 0) else 1.0
-    gemm_s = sum(gemm_us) * scale * 1e-6
+    nl = sum(v[1] for v in per_kind.values())
+    offset = ((ms_step * 1e3 - eager_us) / nl) if (world == 1 and not a.eager and nl > 0) else 0.0
+    gemm_s = (sum(gemm_us) + offset * gemm_n) * 1e-6
     gemm_tf = gemm_flops / gemm_s / 1e12 if gemm_s > 0 else 0.0
     step_flops = plan["gemm_flops"]
     step_tf = step_flops / (ms_step * 1e-3) / 1e12
@@ -606,12 +609,13 @@ def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None,
                      "achieved": round(gemm_tf, 3), "peak": PEAK_F32_MFMA, "unit": "TFLOP/s",
                      "frac": round(gemm_tf / PEAK_F32_MFMA, 4),
                      "timing": (f"each launch's in-round device duration (median over {a.profile_rounds} rounds of "
-                                "dispatch begin / end events on the launch stream, cgl_gan_profile) scaled to the "
-                                "timed graph-replay period (timed_scale = ms_per_step / eager device sum)"
-                                if scale != 1.0 else
+                                "dispatch begin / end events on the launch stream, cgl_gan_profile) plus the timed "
+                                "graph-replay period's per-launch offset (timed_offset_us = (ms_per_step - eager "
+                                "device sum) / launches)"
+                                if offset != 0.0 else
                                 f"median over {a.profile_rounds} rounds of each launch's in-round device duration "
                                 "(dispatch begin / end events on the launch stream, cgl_gan_profile)"),
-                     "timed_scale": round(scale, 4),
+                     "timed_offset_us": round(offset, 3),
                      "traffic": traffic_per_gemm_launch()[0] if a.model == "mlp" else None,
                      "traffic_unit": "bytes per GEMM launch, all cgl_gemm_f32 instantiations (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                      "traffic_source": traffic_per_gemm_launch()[1] if a.model == "mlp" else None,
@@ -619,7 +623,7 @@ def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None,
                      **(traffic_per_launch() if a.model == "mlp" else {}),
                      "gemm_launches_per_round": gemm_n, "gemm_flops_per_round": gemm_flops,
                      "flops_per_gemm_launch": gemm_flops / max(gemm_n, 1),
-                     "avg_gemm_launch_us": round(sum(gemm_us) * scale / max(gemm_n, 1), 3),
+                     "avg_gemm_launch_us": round(sum(gemm_us) / max(gemm_n, 1) + offset, 3),
                      "avg_gemm_launch_us_eager": round(sum(gemm_us) / max(gemm_n, 1), 3),
                      "gemm_launch_us": [round(u, 2) for u in gemm_us],
                      "step_achieved_tflops": round(step_tf, 3),

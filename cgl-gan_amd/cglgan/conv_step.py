@@ -239,11 +239,11 @@ class ConvGanStep:
         # element and measured slower than the separate pass (profiles/r03_conv_bnfold_ab.txt)
         # CGL_CONV_ELIDE (default 1): with a layer folded, its activation is not stored at all -- the G backward
         # applies the BatchNorm in the weight gradient's operand loads (cgl_conv3x3_bwd_weight_bnin) and takes
-        # LeakyReLU' from the kept scale / shift.  Measured (profiles/r04_conv_elide_ab.txt): a2 (fold bit 2, the
-        # default) -28 us per round; a1 (bit 1) costs more in the LDS weight gradient's staging (+43 us) than its
-        # apply pass saves, so the default mask stays 2
+        # LeakyReLU' from the kept scale / shift.  Measured (profiles/r04_conv_elide_ab.txt): a2 (fold bit 2)
+        # -28 us per round; a1 too (bit 1) another -6 us once the BatchNorm-in-load paths keep the activation
+        # flag and slope in registers, so with the elision the default mask is 3 (2 without it)
         self.elide_on = os.environ.get("CGL_CONV_ELIDE", "1") != "0"
-        fold = int(os.environ.get("CGL_CONV_BNFOLD", "2"))
+        fold = int(os.environ.get("CGL_CONV_BNFOLD", "3" if self.elide_on else "2"))
         self.bn_fold = fold & 3 if all(k in self.st_part for k in ("conv_blocks.2", "conv_blocks.6")) else 0
         self.coef = {k: torch.zeros(4 * c, dtype=torch.float32, device=dev)
                      for k, c in (("conv_blocks.2", 128), ("conv_blocks.6", 64))}

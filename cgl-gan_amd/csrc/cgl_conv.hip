@@ -297,6 +297,10 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
     const int g = BNIN ? min(img / L->in_gimg, L->in_groups - 1) : 0;
     // BNIN: when the staging stride keeps each thread on one channel quad, its scale / shift are loaded once
     const bool qfix = (256 % c4) == 0;
+    // the activation flag and slope in registers: read through the kernarg pointer inside the loop, the slope's
+    // scalar load sat under the LeakyReLU condition and became a branch per value
+    const bool in_lk = BNIN && L->in_act == CGL_EPI_ACT_LEAKY;
+    const float in_sl = BNIN ? L->in_slope : 0.f;
     f32x4 sc0 = {0.f, 0.f, 0.f, 0.f}, sh0 = sc0;
     if (BNIN && qfix) {
       sc0 = *(gcf4p)(L->in_coef + g * Cin + 4 * (tid % c4));
@@ -315,7 +319,7 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             float w = fmaf(v[u], sc[u], sh[u]);
-            if (L->in_act == CGL_EPI_ACT_LEAKY) w = w > 0.f ? w : w * L->in_slope;
+            if (in_lk) w = w > 0.f ? w : w * in_sl;
             v[u] = w;
           }
         }
@@ -730,10 +734,12 @@ __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local)
       bsc[q][j] = BNIN ? gld(L->in_coef + gq * Cin + cci[j]) : 0.f;
       bsh[q][j] = BNIN ? gld(L->in_coef + (L->in_groups + gq) * Cin + cci[j]) : 0.f;
     }
+  const bool in_lk = BNIN && L->in_act == CGL_EPI_ACT_LEAKY;   // (in registers: see the halo staging)
+  const float in_sl = BNIN ? L->in_slope : 0.f;
   auto bn = [&](float x, int img, int j) {
     const int q = (bg > 1 && img >= L->in_gimg) ? 1 : 0;     // (<= 2 groups: no division per value)
     float v = fmaf(x, q ? bsc[1][j] : bsc[0][j], q ? bsh[1][j] : bsh[0][j]);
-    if (L->in_act == CGL_EPI_ACT_LEAKY) v = v > 0.f ? v : v * L->in_slope;
+    if (in_lk) v = v > 0.f ? v : v * in_sl;
     return v;
   };
 
@@ -929,6 +935,8 @@ __global__ __launch_bounds__(256 * KS, 2 / KS) void cgl_conv_wgrad_lds(CglConvLa
   const int tap = kk / Cin, ci = kk - tap * Cin;
   const int cdy = P->dy[tap / P->Tx], cdx = P->dx[tap - (tap / P->Tx) * P->Tx];
   f32x4 bsc = {0.f, 0.f, 0.f, 0.f}, bsh = bsc;
+  const bool in_lk = BNIN && L->in_act == CGL_EPI_ACT_LEAKY;   // (in registers: see the halo staging)
+  const float in_sl = BNIN ? L->in_slope : 0.f;
   if constexpr (BNIN) {
     bsc = *(gcf4p)(L->in_coef + (long)L->in_g0 * Cin + ci);
     bsh = *(gcf4p)(L->in_coef + (long)(L->in_groups + L->in_g0) * Cin + ci);
@@ -978,7 +986,7 @@ __global__ __launch_bounds__(256 * KS, 2 / KS) void cgl_conv_wgrad_lds(CglConvLa
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           float w = fmaf(v[u], bsc[u], bsh[u]);
-          if (L->in_act == CGL_EPI_ACT_LEAKY) w = w > 0.f ? w : w * L->in_slope;
+          if (in_lk) w = w > 0.f ? w : w * in_sl;
           v[u] = w;
         }
       }
@@ -1399,6 +1407,8 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad_n1t(CglConvLaunch args) {
 #pragma unroll
   for (int t = 0; t < 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 isc = {0.f, 0.f, 0.f, 0.f}, ish = isc;
+  const bool in_lk = BNIN && L->in_act == CGL_EPI_ACT_LEAKY;   // (in registers: see the halo staging)
+  const float in_sl = BNIN ? L->in_slope : 0.f;
   if constexpr (BNIN) {
     isc = *(gcf4p)(L->in_coef + (long)L->in_g0 * Cin + 4 * q4);
     ish = *(gcf4p)(L->in_coef + (long)(L->in_groups + L->in_g0) * Cin + 4 * q4);
@@ -1448,7 +1458,7 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad_n1t(CglConvLaunch args) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float w = fmaf(x[u][e], isc[e], ish[e]);
-          if (L->in_act == CGL_EPI_ACT_LEAKY) w = w > 0.f ? w : w * L->in_slope;
+          if (in_lk) w = w > 0.f ? w : w * in_sl;
           x[u][e] = w;
         }
     }
