@@ -136,9 +136,10 @@ __device__ __forceinline__ int cgl_xcd_tile(int local, int nwg) {
 // the tap table.  One wave owns TM x TN 32x32 accumulators; WM x WN waves per workgroup.
 // FAST: Cin % 16 == 0, so a 16-k chunk lies inside one tap (uniform tap, 2 x 16-byte loads per
 // lane and block).  Otherwise each k is decoded per element (tiny-K layers: Cin = 1).
-template <int TM, int TN, bool FAST, bool BNIN = false, bool HALO = false>
+template <int TM, int TN, bool FAST, bool BNIN = false, bool HALO = false, bool LDSM = false>
 __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, float* s_red, bool direct = false) {
   constexpr int S = 3;
+  static_assert(!LDSM || (TM == 2 && TN == 2 && FAST && !BNIN && !HALO), "the LDS main loop: 2x2 blocks, FAST");
   static_assert(!BNIN || FAST, "the folded BatchNorm input needs the FAST (uniform-tap chunk) path");
   static_assert(!HALO || (TM == 2 && TN == 2 && FAST), "the halo path is the 2x2-block FAST path");
   const int tid = threadIdx.x;
@@ -282,7 +283,100 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
   // This wave's k-split: chunks [cb, ce).
   const int nch = Kp >> 4;
   const int cb = (wk * nch) / WK, ce = ((wk + 1) * nch) / WK;
-  if constexpr (HALO) {
+  if constexpr (LDSM) {
+    // LDS-staged operand panels (2 x 2 waves of 64 x 64, WK = 1; the input gradients of the upsampling convs):
+    // per 16-k chunk the workgroup's 256 threads fetch the A panel [128 rows][16 k] (two 16-byte im2col loads
+    // each) and the B panel [128 columns][16 k] (two 16-byte weight loads each) into LDS, where each element is
+    // read by the 2 waves sharing its row (column) block instead of loaded by each.  Rows padded to 20 floats:
+    // the 16 lanes of a 16-byte read phase cover the 64 banks once.  The next chunk's loads are in flight while
+    // this one is multiplied (two register sets, two LDS buffers, one barrier per chunk).  Fragment values and
+    // MFMA order are the direct path's (lane half lh holds k 8 lh .. 8 lh + 7 of the chunk), so the results are
+    // bitwise equal to it.
+    constexpr int RS = 20;
+    float* const la = s_red;                  // [2][128][RS]
+    float* const lb = s_red + 2 * 128 * RS;   // [2][128][RS]
+    const int tid2 = threadIdx.x;
+    const int sr = tid2 >> 2, sq = tid2 & 3;  // staging: rows sr and sr + 64, float4 sq of the chunk
+    const int mt = tm * 32 * TM * WM, nt = tn * 32 * TN * WN;
+    int say[2], sax[2];
+    long saoff[2];
+    const float* sbrow[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      int img, oy, ox;
+      cgl_conv_pix(P, min(mt + sr + 64 * h, M - 1), img, oy, ox);
+      say[h] = oy * P->isy;
+      sax[h] = ox * P->isx;
+      saoff[h] = (long)img * P->XH * XW * Cin;
+      sbrow[h] = P->Wp + (long)min(nt + sr + 64 * h, N - 1) * Kp;
+    }
+    auto gload = [&](int c, f32x4 (&ra)[2], f32x4 (&rb)[2], int& okm) {
+      const int k0 = c * 16, t = k0 / Cin, ci = k0 - t * Cin + 4 * sq;
+      const int ty = t / Tx, tx = t - ty * Tx;
+      const int dyv = P->dy[ty], dxv = P->dx[tx];
+      okm = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int iy = say[h] + dyv, ix = sax[h] + dxv;
+        const bool ok = (unsigned)iy < (unsigned)IH && (unsigned)ix < (unsigned)IW;
+        okm |= ok ? (1 << h) : 0;
+        const int cy = min(max(iy, 0), IH - 1) >> ish, cx = min(max(ix, 0), IW - 1) >> ish;
+        ra[h] = *(gcf4p)(X + saoff[h] + ((long)cy * XW + cx) * Cin + ci);
+        rb[h] = *(gcf4p)(sbrow[h] + k0 + 4 * sq);
+      }
+    };
+    auto stage = [&](int buf, const f32x4 (&ra)[2], const f32x4 (&rb)[2], int okm) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        *(f32x4*)&la[(buf * 128 + sr + 64 * h) * RS + 4 * sq] = ((okm >> h) & 1) ? ra[h] : f32x4{0.f, 0.f, 0.f, 0.f};
+        *(f32x4*)&lb[(buf * 128 + sr + 64 * h) * RS + 4 * sq] = rb[h];
+      }
+    };
+    const int ra0 = wm * 32 * TM + li, rb0 = wn * 32 * TN + li;
+    auto mmc = [&](int buf) {
+      float A[TM][8], B[TN][8];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const float* w = &la[(buf * 128 + ra0 + 32 * i) * RS + 8 * lh];
+        const f32x4 u = *(const f32x4*)w, v = *(const f32x4*)(w + 4);
+        A[i][0] = u[0]; A[i][1] = u[1]; A[i][2] = u[2]; A[i][3] = u[3];
+        A[i][4] = v[0]; A[i][5] = v[1]; A[i][6] = v[2]; A[i][7] = v[3];
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const float* w = &lb[(buf * 128 + rb0 + 32 * j) * RS + 8 * lh];
+        const f32x4 u = *(const f32x4*)w, v = *(const f32x4*)(w + 4);
+        B[j][0] = u[0]; B[j][1] = u[1]; B[j][2] = u[2]; B[j][3] = u[3];
+        B[j][4] = v[0]; B[j][5] = v[1]; B[j][6] = v[2]; B[j][7] = v[3];
+      }
+      __builtin_amdgcn_sched_barrier(0);   // all 8 LDS reads ahead of the 32 MFMAs
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[i][q], B[j][q], acc[i][j], 0, 0, 0);
+    };
+    f32x4 r0a[2], r0b[2], r1a[2], r1b[2];
+    int ok0, ok1;
+    gload(0, r0a, r0b, ok0);
+    gload(min(1, nch - 1), r1a, r1b, ok1);
+    stage(0, r0a, r0b, ok0);
+    __syncthreads();
+    int c = 0;
+    for (; c + 2 <= nch; c += 2) {
+      gload(min(c + 2, nch - 1), r0a, r0b, ok0);
+      mmc(0);
+      stage(1, r1a, r1b, ok1);
+      __syncthreads();
+      gload(min(c + 3, nch - 1), r1a, r1b, ok1);
+      mmc(1);
+      stage(0, r0a, r0b, ok0);
+      __syncthreads();
+    }
+    if (c < nch) mmc(0);
+  } else if constexpr (HALO) {
     // LDS-staged input window (the phase-form upsampling conv: 4 output parities x 2x2 taps, all reading one
     // low-res window).  The workgroup's tile is 64 enumerated rows = R = 64 / OW whole low-res rows of one
     // image; its window (rows y0 - 1 .. y0 + R, columns -1 .. OW, every channel, zeros outside the image) is
@@ -622,7 +716,7 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
   }
 }
 
-template <int TM, int TN, bool FAST, bool BNIN = false>
+template <int TM, int TN, bool FAST, bool BNIN = false, bool LDSM = false>
 __global__ __launch_bounds__(256) void cgl_conv_fwd(CglConvLaunch args) {
   (void)args;
   extern __shared__ float cgl_conv_lds[];
@@ -634,12 +728,12 @@ __global__ __launch_bounds__(256) void cgl_conv_fwd(CglConvLaunch args) {
     // units XCD-contiguous, so the np tiles reading one input window run back to back in one L2
     const int np = L->np;
     const int unit = cgl_xcd_tile(bid, L->p[0].tiles_m * L->p[0].tiles_n * np);
-    cgl_conv_fwd_body<TM, TN, FAST, BNIN>(L, &L->p[unit % np], unit / np, cgl_conv_lds, true);
+    cgl_conv_fwd_body<TM, TN, FAST, BNIN, false, LDSM>(L, &L->p[unit % np], unit / np, cgl_conv_lds, true);
     return;
   }
   const int pi = cgl_conv_prob(L, bid);
   CglKP P = &L->p[pi];
-  cgl_conv_fwd_body<TM, TN, FAST, BNIN>(L, P, bid - P->wg_begin, cgl_conv_lds);
+  cgl_conv_fwd_body<TM, TN, FAST, BNIN, false, LDSM>(L, P, bid - P->wg_begin, cgl_conv_lds);
 }
 
 // The phase-form upsampling conv with its input window staged in LDS (HALO path of cgl_conv_fwd_body): one
@@ -793,14 +887,18 @@ __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local)
       const int m = c * 16 + 8 * lh + q;
       const bool mv = m < M;
       if (q > 0) {
-        if (++ox == OW) {
-          ox = 0;
-          if (++oy == OH) {
-            oy = 0;
-            ++img;
-          }
-        }
-        if (!mv) { img = 0; oy = 0; ox = 0; }
+        // branch-free stepping (the nested ifs compiled to divergent exec-mask branches per pixel: the lane
+        // halves step different pixels)
+        ++ox;
+        const bool wx = ox == OW;
+        ox = wx ? 0 : ox;
+        oy += wx ? 1 : 0;
+        const bool wy = oy == OH;
+        oy = wy ? 0 : oy;
+        img += wy ? 1 : 0;
+        img = mv ? img : 0;
+        oy = mv ? oy : 0;
+        ox = mv ? ox : 0;
       }
       const long ya = (((long)img * YH + oy * osy + ooy) * YW + ox * osx + oox) * ldy;
       const float* ab = mv ? dY + ya : zp;
@@ -3243,7 +3341,12 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
     else hipLaunchKernelGGL((cgl_conv_fwd<1, 1, true, true>), dim3(wg), dim3(256), lds, s, L);
     return (int)hipGetLastError();
   }
-  if (t.TM == 2 && t.TN == 2) {
+  // the 2 x 2-wave 128 x 128 tiling of a FAST problem: LDS-staged operand panels (CGL_CONV_LDSM=0: the direct
+  // loads; bitwise the same results)
+  const int ldsm_env = getenv("CGL_CONV_LDSM") ? atoi(getenv("CGL_CONV_LDSM")) : 1;   // (per launch: tests toggle it)
+  if (t.TM == 2 && t.TN == 2 && fast && ldsm_env && t.WM == 2 && t.WN == 2 && t.WK == 1) {
+    hipLaunchKernelGGL((cgl_conv_fwd<2, 2, true, false, true>), dim3(wg), dim3(256), 2 * 2 * 128 * 20 * 4, s, L);
+  } else if (t.TM == 2 && t.TN == 2) {
     if (fast) hipLaunchKernelGGL((cgl_conv_fwd<2, 2, true>), dim3(wg), dim3(256), lds, s, L);
     else hipLaunchKernelGGL((cgl_conv_fwd<2, 2, false>), dim3(wg), dim3(256), lds, s, L);
   } else if (t.TM == 2) {
