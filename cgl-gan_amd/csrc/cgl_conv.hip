@@ -1140,15 +1140,15 @@ __global__ __launch_bounds__(256 * KS, 2 / KS) void cgl_conv_wgrad_lds(CglConvLa
     for (; i + 2 <= ni; i += 2) {
       // buffer 0 holds step i, r1 step i + 1
       load(chunk(min(i + 2, ni - 1)), r0a, r0b, ok0);
-      if (live(i)) compute(0);
+      if (KS == 1 || live(i)) compute(0);   // (KS 1: no branch, so the staging interleaves with the MFMAs)
       stage(1, r1a, r1b, ok1);
       __syncthreads();
       load(chunk(min(i + 3, ni - 1)), r1a, r1b, ok1);
-      if (live(i + 1)) compute(1);
+      if (KS == 1 || live(i + 1)) compute(1);
       stage(0, r0a, r0b, ok0);
       __syncthreads();
     }
-    if (i < ni && live(i)) compute(0);   // an odd last step
+    if (i < ni && (KS == 1 || live(i))) compute(0);   // an odd last step
   }
   if constexpr (KS == 2) {
     // half 1 hands its accumulators to half 0 through the (now idle) staging LDS
