@@ -35,6 +35,25 @@ def _s():
 
 
 @contextlib.contextmanager
+def launch_batch(enabled=True):
+    """cgl_conv_batch_begin / _end around the round start's pack / masks / z draw / sampler calls: one launch
+    instead of four (same results).  The block must stay on the current stream."""
+    if not enabled:
+        yield
+        return
+    s = _s()
+    C.check(C.lib.cgl_conv_batch_begin(s), "cgl_conv_batch_begin")
+    ok = False
+    try:
+        yield
+        ok = True
+    finally:
+        rc = C.lib.cgl_conv_batch_end(s)
+        if ok:
+            C.check(rc, "cgl_conv_batch_end")
+
+
+@contextlib.contextmanager
 def stream_cache():
     """Resolve the current torch stream once for a block of ops that all run on it (the fused conv
     round issues ~100 ops per round; looking the stream up per op was a visible share of the host

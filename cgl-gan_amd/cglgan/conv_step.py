@@ -253,6 +253,7 @@ class ConvGanStep:
         self.coef_kept = set()
         # D's inner BatchNorms folded into the next conv in the G-loss pass (_d_forward); [2][groups][C] scale / shift
         self.d_fold = os.environ.get("CGL_CONV_DFOLD", "1") != "0"
+        self.batch_on = os.environ.get("CGL_CONV_BATCH", "1") != "0"   # batched round start (_phase_a)
         # ... and in the D step too (CGL_CONV_DFOLD_STEP=1): correct and bitwise, but the wave-unit weight gradient's
         # per-value BatchNorm costs +41 us against the two apply passes it saves (profiles/r04_conv_elide_ab.txt)
         self.d_fold_step = os.environ.get("CGL_CONV_DFOLD_STEP", "0") == "1"
@@ -573,10 +574,8 @@ class ConvGanStep:
         with O.stream_cache():     # every op of the phase runs on the current stream
             self._phase_a(real)
 
-    def _phase_a(self, real=None):
+    def _round_start(self, real):
         B = self.B
-        if self.graph:
-            self._sync_dstate()
         if self.gen_z:
             if self.graph:
                 O.normal_fill_dev(self.z, self.seed, self.dstate[0:1])
@@ -605,6 +604,15 @@ class ConvGanStep:
                 self._sample_real()
         self.pk.run()
         self._masks()
+
+    def _phase_a(self, real=None):
+        B = self.B
+        if self.graph:
+            self._sync_dstate()
+        # graph rounds: the z draw, the sampler, the weight packing and the Dropout2d masks (independent, all
+        # reading the device round counters) go out as ONE launch (cgl_conv_batch_begin / _end)
+        with O.launch_batch(self.graph and real is None and self.batch_on):
+            self._round_start(real)
         self._g_forward()
         # local D step on [real; Xd]: two forward calls (statistics, masks per call), one backward
         half = 0.5 if self.loss == "mse" else 1.0

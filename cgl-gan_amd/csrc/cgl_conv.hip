@@ -1804,10 +1804,7 @@ struct CglPackMultiArgs {
   CglPackJobK j[CGL_PACKM_MAXJ];
 };
 
-__global__ __launch_bounds__(256) void cgl_conv_pack_multi(CglPackMultiArgs) {
-  typedef const CGL_AS4 CglPackMultiArgs* KA;
-  const KA A = (KA)__builtin_amdgcn_kernarg_segment_ptr();
-  const int b = blockIdx.x;
+__device__ __forceinline__ void cgl_conv_pack_at(const CGL_AS4 CglPackMultiArgs* A, int b) {
   int q = 0;
   for (int i = 1; i < A->nj; ++i)
     if (b >= A->j[i].blk_begin) q = i;
@@ -1831,6 +1828,11 @@ __global__ __launch_bounds__(256) void cgl_conv_pack_multi(CglPackMultiArgs) {
     }
   }
   gst(J->dst + local, v);
+}
+
+__global__ __launch_bounds__(256) void cgl_conv_pack_multi(CglPackMultiArgs) {
+  typedef const CGL_AS4 CglPackMultiArgs* KA;
+  cgl_conv_pack_at((KA)__builtin_amdgcn_kernarg_segment_ptr(), blockIdx.x);
 }
 
 // Weight-gradient reduction: dW[co][ci][kh][kw] = sum over problems, taps containing (kh, kw) and
@@ -2671,10 +2673,7 @@ struct CglMasksArgs {
   unsigned long long rstride;
 };
 
-__global__ __launch_bounds__(256) void cgl_dropout_masks_k(CglMasksArgs) {
-  typedef const CGL_AS4 CglMasksArgs* KA;
-  const KA A = (KA)__builtin_amdgcn_kernarg_segment_ptr();
-  const int b = blockIdx.x;
+__device__ __forceinline__ void cgl_dropout_masks_at(const CGL_AS4 CglMasksArgs* A, int b) {
   int q = 0;
   for (int j = 1; j < A->nm; ++j)
     if (b >= A->blk_begin[j]) q = j;
@@ -2686,6 +2685,11 @@ __global__ __launch_bounds__(256) void cgl_dropout_masks_k(CglMasksArgs) {
   cgl_philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
   const float u = (float)(c[0] >> 8) * (1.0f / 16777216.0f);
   gst(A->mask[q] + i, u < A->keep ? A->scale : 0.f);
+}
+
+__global__ __launch_bounds__(256) void cgl_dropout_masks_k(CglMasksArgs) {
+  typedef const CGL_AS4 CglMasksArgs* KA;
+  cgl_dropout_masks_at((KA)__builtin_amdgcn_kernarg_segment_ptr(), blockIdx.x);
 }
 
 // NCHW <-> NHWC for one batch: X [n][c][hw] -> Y [n][hw][c] (to_nhwc) or back.  32x32 tiles in LDS.
@@ -2837,10 +2841,9 @@ __global__ __launch_bounds__(256) void cgl_normal_dev_k(float* out, long n, unsi
 // null) receives the batch's real rows; rows past a short batch copy a valid dummy row (the consumers
 // leave them out: cgl_nv_rows).  With nv_out null the pass is cut drop_last (whole batches only).  One
 // workgroup per row, float4 copies.
-__global__ __launch_bounds__(256) void cgl_sample_rows_k(const float* src, int n_src, int nrows, int rowf,
-                                                         unsigned long long seed, const int* round, float* dst,
-                                                         int* nv_out) {
-  const int r = blockIdx.x;
+__device__ __forceinline__ void cgl_sample_rows_at(const float* src, int n_src, int nrows, int rowf,
+                                                   unsigned long long seed, const int* round, float* dst, int* nv_out,
+                                                   int r) {
   uint32_t ep, j;
   if (nv_out) {
     const long nb = (n_src + nrows - 1) / nrows;
@@ -2860,6 +2863,39 @@ __global__ __launch_bounds__(256) void cgl_sample_rows_k(const float* src, int n
   const f32x4* s4 = (const f32x4*)(src + (long)idx * rowf);
   f32x4* d4 = (f32x4*)(dst + (long)r * rowf);
   for (int c = threadIdx.x; c < rowf / 4; c += 256) *(gf4p)(d4 + c) = *(gcf4p)(s4 + c);
+}
+
+__global__ __launch_bounds__(256) void cgl_sample_rows_k(const float* src, int n_src, int nrows, int rowf,
+                                                         unsigned long long seed, const int* round, float* dst,
+                                                         int* nv_out) {
+  cgl_sample_rows_at(src, n_src, nrows, rowf, seed, round, dst, nv_out, blockIdx.x);
+}
+
+// The conv round's independent start-of-round launches as ONE launch (cgl_conv_batch_begin / _end): the weight
+// packing, the Dropout2d masks, the z draw and the real-batch sampler read and write disjoint buffers, so their
+// blocks can share a grid: [pack | masks | normal | sample] by block range, each block running its kernel's body.
+struct CglConvBeginArgs {
+  CglPackMultiArgs pack;
+  CglMasksArgs masks;
+  int pb, mb, nb, sb;                 // block counts of the four parts (0: absent)
+  float* n_out; long n_n; unsigned long long n_seed; const int* n_round; int n_sid;
+  const float* s_src; int s_nsrc, s_nrows, s_rowf; unsigned long long s_seed; const int* s_round; float* s_dst;
+  int* s_nv;
+};
+__global__ __launch_bounds__(256) void cgl_conv_begin_k(CglConvBeginArgs) {
+  typedef const CGL_AS4 CglConvBeginArgs* KA;
+  const KA A = (KA)__builtin_amdgcn_kernarg_segment_ptr();
+  int b = blockIdx.x;
+  if (b < A->pb) { cgl_conv_pack_at(&A->pack, b); return; }
+  b -= A->pb;
+  if (b < A->mb) { cgl_dropout_masks_at(&A->masks, b); return; }
+  b -= A->mb;
+  if (b < A->nb) {
+    cgl_normal_at((long)b * 256 + threadIdx.x, A->n_out, A->n_n, A->n_seed, (uint32_t)gldi(A->n_round), A->n_sid);
+    return;
+  }
+  b -= A->nb;
+  cgl_sample_rows_at(A->s_src, A->s_nsrc, A->s_nrows, A->s_rowf, A->s_seed, A->s_round, A->s_dst, A->s_nv, b);
 }
 
 __global__ __launch_bounds__(64) void cgl_counters_add_k(int* p, int n, int v) {
@@ -3790,6 +3826,36 @@ int64_t cgl_conv_packed_floats(int h, int w, int cin, int cout, int stride, int 
   return pack_layout(P, np, nullptr);
 }
 
+// Launch batching (cgl_conv_batch_begin / _end): between the two calls, cgl_conv_pack_multi,
+// cgl_dropout2d_masks_dev, cgl_normal_fill_dev and cgl_sample_rows_dev record their (validated) arguments
+// instead of launching (one of each at most); _end launches them as one cgl_conv_begin_k.
+namespace {
+struct ConvBatch {
+  bool on = false;
+  hipStream_t s = nullptr;
+  CglConvBeginArgs a{};
+};
+thread_local ConvBatch t_batch;
+}  // namespace
+
+int cgl_conv_batch_begin(void* stream) {
+  if (t_batch.on) return CGL_E_ARG;
+  t_batch.on = true;
+  t_batch.s = (hipStream_t)stream;
+  std::memset(&t_batch.a, 0, sizeof(t_batch.a));
+  return 0;
+}
+
+int cgl_conv_batch_end(void* stream) {
+  if (!t_batch.on || (hipStream_t)stream != t_batch.s) return CGL_E_ARG;
+  t_batch.on = false;
+  const CglConvBeginArgs& a = t_batch.a;
+  const int blk = a.pb + a.mb + a.nb + a.sb;
+  if (blk == 0) return 0;
+  hipLaunchKernelGGL(cgl_conv_begin_k, dim3(blk), dim3(256), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
 int cgl_conv_pack_multi(int njobs, const CglConvPackJob* jobs, void* stream) {
   if (njobs < 1 || !jobs) return CGL_E_ARG;
   CglPackMultiArgs a;
@@ -3818,6 +3884,12 @@ int cgl_conv_pack_multi(int njobs, const CglConvPackJob* jobs, void* stream) {
     }
   }
   a.nj = nj;
+  if (t_batch.on) {
+    if (t_batch.a.pb || (hipStream_t)stream != t_batch.s) return CGL_E_ARG;
+    t_batch.a.pack = a;
+    t_batch.a.pb = blk;
+    return 0;
+  }
   hipLaunchKernelGGL(cgl_conv_pack_multi, dim3(blk), dim3(256), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
@@ -4175,6 +4247,12 @@ static int dropout2d_masks_impl(int nm, float* const* masks, const int* n, const
   }
   a.rdev = round_dev;
   a.rstride = round_stride;
+  if (t_batch.on) {
+    if (t_batch.a.mb || (hipStream_t)stream != t_batch.s) return CGL_E_ARG;
+    t_batch.a.masks = a;
+    t_batch.a.mb = blk;
+    return 0;
+  }
   hipLaunchKernelGGL(cgl_dropout_masks_k, dim3(blk), dim3(256), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
@@ -4301,6 +4379,13 @@ int cgl_normal_fill_dev(float* out, int64_t n, unsigned long long seed, const in
                         void* stream) {
   if (!out || n < 0 || !round_dev) return CGL_E_ARG;
   if (n == 0) return 0;
+  if (t_batch.on) {
+    if (t_batch.a.nb || (hipStream_t)stream != t_batch.s) return CGL_E_ARG;
+    CglConvBeginArgs& b = t_batch.a;
+    b.n_out = out; b.n_n = (long)n; b.n_seed = seed; b.n_round = round_dev; b.n_sid = stream_id;
+    b.nb = (int)((n / 4 + 255) / 256);
+    return 0;
+  }
   hipLaunchKernelGGL(cgl_normal_dev_k, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, out,
                      (long)n, seed, round_dev, stream_id);
   return (int)hipGetLastError();
@@ -4318,6 +4403,14 @@ int cgl_sample_rows_dev(const float* src, int n_src, int nrows, int row_floats, 
   if (!src || !dst || !round_dev || nrows < 1 || n_src < 1 || (!nv_out && n_src < nrows) || row_floats < 4 ||
       row_floats % 4 || ((uintptr_t)src & 15) || ((uintptr_t)dst & 15))
     return CGL_E_ARG;
+  if (t_batch.on) {
+    if (t_batch.a.sb || (hipStream_t)stream != t_batch.s) return CGL_E_ARG;
+    CglConvBeginArgs& b = t_batch.a;
+    b.s_src = src; b.s_nsrc = n_src; b.s_nrows = nrows; b.s_rowf = row_floats; b.s_seed = seed; b.s_round = round_dev;
+    b.s_dst = dst; b.s_nv = nv_out;
+    b.sb = nrows;
+    return 0;
+  }
   hipLaunchKernelGGL(cgl_sample_rows_k, dim3(nrows), dim3(256), 0, (hipStream_t)stream, src, n_src, nrows, row_floats,
                      seed, round_dev, dst, nv_out);
   return (int)hipGetLastError();

@@ -289,6 +289,13 @@ int64_t cgl_conv_packed_floats(int h, int w, int cin, int cout, int stride, int 
 /* all jobs in one launch (at most 48 packed problems: a forward up-conv is 4, a stride-2
  * input gradient 4, everything else 1) */
 int cgl_conv_pack_multi(int njobs, const CglConvPackJob* jobs, void* stream);
+/* Launch batching of the conv round's start: between cgl_conv_batch_begin(stream) and cgl_conv_batch_end(stream),
+ * at most one each of cgl_conv_pack_multi, cgl_dropout2d_masks(_dev), cgl_normal_fill_dev and
+ * cgl_sample_rows_dev on that stream validate and record their arguments instead of launching; _end launches
+ * them as ONE kernel (their blocks by range: they read and write disjoint buffers).  Same results as the four
+ * launches; one launch floor instead of four. */
+int cgl_conv_batch_begin(void* stream);
+int cgl_conv_batch_end(void* stream);
 int cgl_conv3x3_fwd_packed(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w, int cin,
                            int cout, int stride, int up, int act, float slope, const float* drop, void* workspace,
                            int64_t ws_bytes, void* stream);

@@ -6,6 +6,8 @@
   * CGL_CONV_DFOLD: in the G-loss pass, D's inner BatchNorm2d layers are applied in the next conv's operand
     load (bn_in, cgl_eltwise's fmaf) instead of an apply pass -- nothing else reads their output there;
     CGL_CONV_DFOLD_STEP (opt-in): in the D step too, the weight gradients applying them in their loads;
+  * CGL_CONV_BATCH: the graph round's start (weight packing, Dropout2d masks, z draw, real-batch sampler) as one
+    launch (cgl_conv_batch_begin / _end);
   * CGL_CONV_ELIDE: a folded G BatchNorm's activation (a1 / a2) is not stored at all -- the G backward's weight
     gradients apply the BatchNorm in their operand loads (cgl_conv3x3_bwd_weight_bnin) and every LeakyReLU'
     comes from the kept scale / shift (with the same fold mask on both sides)."""
@@ -36,6 +38,7 @@ def _step(B, graph, data, env):
 CASES = [("CGL_CONV_POSTCOEF", 8, False, "2"), ("CGL_CONV_POSTCOEF", 256, False, "0"),
          ("CGL_CONV_POSTCOEF", 256, True, "2"), ("CGL_CONV_DFOLD", 8, False, "2"), ("CGL_CONV_DFOLD", 256, True, "2"),
          ("CGL_CONV_DFOLD_STEP", 8, False, "2"), ("CGL_CONV_DFOLD_STEP", 256, True, "2"),
+         ("CGL_CONV_BATCH", 8, True, "3"), ("CGL_CONV_BATCH", 256, True, "3"),
          ("CGL_CONV_ELIDE", 8, False, "3"), ("CGL_CONV_ELIDE", 256, False, "3"), ("CGL_CONV_ELIDE", 256, True, "3"),
          ("CGL_CONV_ELIDE", 256, True, "2")]
 
@@ -56,6 +59,8 @@ def test_conv_round_fusion_bitwise(var, B, graph, fold):
         assert {"conv_blocks.2", "conv_blocks.6"} <= a.coef_kept
     elif var == "CGL_CONV_DFOLD":
         assert a.d_fold and not b.d_fold
+    elif var == "CGL_CONV_BATCH":
+        assert a.batch_on and not b.batch_on
     elif var == "CGL_CONV_DFOLD_STEP":
         assert a.d_fold_step and not b.d_fold_step and a._d_folded and not b._d_folded
     else:
