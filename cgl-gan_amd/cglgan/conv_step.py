@@ -618,8 +618,9 @@ class ConvGanStep:
         half = 0.5 if self.loss == "mse" else 1.0
         nvd = self.nv if self._short_call else None     # the real call's images (short final batch)
         self._d_forward(self.x3, 2 * B, 2, self.mask_d, nvalid=nvd)
-        O.adv_loss(self.v[:B], B, 1, self.loss, 1, half, self.lbuf[0:1], self.dv[:B], nvalid=nvd)
-        O.adv_loss(self.v[B:2 * B], B, 1, self.loss, 0, half, self.lbuf[1:2], self.dv[B:2 * B])
+        with O.launch_batch(self.batch_on):     # the real and fake heads: one launch
+            O.adv_loss(self.v[:B], B, 1, self.loss, 1, half, self.lbuf[0:1], self.dv[:B], nvalid=nvd)
+            O.adv_loss(self.v[B:2 * B], B, 1, self.loss, 0, half, self.lbuf[1:2], self.dv[B:2 * B])
         self._d_backward(self.x3, 2 * B, 2, self.mask_d, wgrad=True, dx=None, nvalid=nvd)
         self.D.adam(self.lr, self.betas, self.eps, step_dev=self.dstate[2:3] if self.graph else None)
         self.pk.run("D")

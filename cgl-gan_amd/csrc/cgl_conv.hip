@@ -2719,8 +2719,8 @@ __global__ __launch_bounds__(256) void cgl_transpose_k(const float* X, float* Y,
 // grad = weight * d(mean loss)/dx, written when non-null.
 // nv (may be null): only the first *nv rows are a batch (DataLoader's short final batch): the mean runs
 // over them and the other rows get a zero gradient.
-__global__ __launch_bounds__(256) void cgl_adv_loss_k(const float* x, int Mall, int C, int loss, int target,
-                                                      float weight, float* loss_out, float* grad, const int* nv) {
+__device__ __forceinline__ void cgl_adv_loss_at(const float* x, int Mall, int C, int loss, int target, float weight,
+                                                float* loss_out, float* grad, const int* nv) {
   __shared__ double s[256];
   double acc = 0.0;
   const int M = nv ? min(max(gldi(nv), 1), Mall) : Mall;
@@ -2776,6 +2776,10 @@ __global__ __launch_bounds__(256) void cgl_adv_loss_k(const float* x, int Mall, 
     for (int q = 0; q < 256; ++q) t += s[q];
     if (loss_out) gst(loss_out, (float)(t / M));
   }
+}
+__global__ __launch_bounds__(256) void cgl_adv_loss_k(const float* x, int Mall, int C, int loss, int target,
+                                                      float weight, float* loss_out, float* grad, const int* nv) {
+  cgl_adv_loss_at(x, Mall, C, loss, target, weight, loss_out, grad, nv);
 }
 
 // Multi-tensor Adam (torch 2.10 _single_tensor_adam op order, see cgl_adam in cgl_kernels.hip);
@@ -2874,14 +2878,19 @@ __global__ __launch_bounds__(256) void cgl_sample_rows_k(const float* src, int n
 // The conv round's independent start-of-round launches as ONE launch (cgl_conv_batch_begin / _end): the weight
 // packing, the Dropout2d masks, the z draw and the real-batch sampler read and write disjoint buffers, so their
 // blocks can share a grid: [pack | masks | normal | sample] by block range, each block running its kernel's body.
+struct CglAdvArgs {
+  const float* x; int Mall, C, loss, target; float weight; float* loss_out; float* grad; const int* nv;
+};
 struct CglConvBeginArgs {
   CglPackMultiArgs pack;
   CglMasksArgs masks;
-  int pb, mb, nb, sb;                 // block counts of the four parts (0: absent)
+  CglAdvArgs adv[2];                  // up to two adversarial-loss heads (one block each: the D step's two calls)
+  int pb, mb, nb, sb, lb;             // block counts of the parts (0: absent)
   float* n_out; long n_n; unsigned long long n_seed; const int* n_round; int n_sid;
   const float* s_src; int s_nsrc, s_nrows, s_rowf; unsigned long long s_seed; const int* s_round; float* s_dst;
   int* s_nv;
 };
+static_assert(sizeof(CglConvBeginArgs) <= 4096, "the batched launch's arguments must fit the kernarg segment");
 __global__ __launch_bounds__(256) void cgl_conv_begin_k(CglConvBeginArgs) {
   typedef const CGL_AS4 CglConvBeginArgs* KA;
   const KA A = (KA)__builtin_amdgcn_kernarg_segment_ptr();
@@ -2895,7 +2904,13 @@ __global__ __launch_bounds__(256) void cgl_conv_begin_k(CglConvBeginArgs) {
     return;
   }
   b -= A->nb;
-  cgl_sample_rows_at(A->s_src, A->s_nsrc, A->s_nrows, A->s_rowf, A->s_seed, A->s_round, A->s_dst, A->s_nv, b);
+  if (b < A->sb) {
+    cgl_sample_rows_at(A->s_src, A->s_nsrc, A->s_nrows, A->s_rowf, A->s_seed, A->s_round, A->s_dst, A->s_nv, b);
+    return;
+  }
+  b -= A->sb;
+  const CGL_AS4 CglAdvArgs* q = &A->adv[b];
+  cgl_adv_loss_at(q->x, q->Mall, q->C, q->loss, q->target, q->weight, q->loss_out, q->grad, q->nv);
 }
 
 __global__ __launch_bounds__(64) void cgl_counters_add_k(int* p, int n, int v) {
@@ -3850,7 +3865,7 @@ int cgl_conv_batch_end(void* stream) {
   if (!t_batch.on || (hipStream_t)stream != t_batch.s) return CGL_E_ARG;
   t_batch.on = false;
   const CglConvBeginArgs& a = t_batch.a;
-  const int blk = a.pb + a.mb + a.nb + a.sb;
+  const int blk = a.pb + a.mb + a.nb + a.sb + a.lb;
   if (blk == 0) return 0;
   hipLaunchKernelGGL(cgl_conv_begin_k, dim3(blk), dim3(256), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
@@ -4300,6 +4315,13 @@ int cgl_adv_loss(const float* x, int M, int C, int loss, int target, double weig
                  const int* nvalid, void* stream) {
   if (!x || M < 1 || loss < 0 || loss > 3 || (target != 0 && target != 1)) return CGL_E_ARG;
   if ((loss == 0) != (C == 2) || (loss != 0 && C != 1)) return CGL_E_ARG;
+  if (t_batch.on) {
+    if (t_batch.a.lb >= 2 || (hipStream_t)stream != t_batch.s) return CGL_E_ARG;
+    CglAdvArgs& q = t_batch.a.adv[t_batch.a.lb++];
+    q.x = x; q.Mall = M; q.C = C; q.loss = loss; q.target = target; q.weight = (float)weight; q.loss_out = loss_out;
+    q.grad = grad; q.nv = nvalid;
+    return 0;
+  }
   hipLaunchKernelGGL(cgl_adv_loss_k, dim3(1), dim3(256), 0, (hipStream_t)stream, x, M, C, loss, target,
                      (float)weight, loss_out, grad, nvalid);
   return (int)hipGetLastError();

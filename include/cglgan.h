@@ -289,11 +289,12 @@ int64_t cgl_conv_packed_floats(int h, int w, int cin, int cout, int stride, int 
 /* all jobs in one launch (at most 48 packed problems: a forward up-conv is 4, a stride-2
  * input gradient 4, everything else 1) */
 int cgl_conv_pack_multi(int njobs, const CglConvPackJob* jobs, void* stream);
-/* Launch batching of the conv round's start: between cgl_conv_batch_begin(stream) and cgl_conv_batch_end(stream),
- * at most one each of cgl_conv_pack_multi, cgl_dropout2d_masks(_dev), cgl_normal_fill_dev and
- * cgl_sample_rows_dev on that stream validate and record their arguments instead of launching; _end launches
- * them as ONE kernel (their blocks by range: they read and write disjoint buffers).  Same results as the four
- * launches; one launch floor instead of four. */
+/* Launch batching (the conv round's start, the D step's two loss heads): between cgl_conv_batch_begin(stream) and
+ * cgl_conv_batch_end(stream), at most one each of cgl_conv_pack_multi, cgl_dropout2d_masks(_dev),
+ * cgl_normal_fill_dev and cgl_sample_rows_dev, and up to two cgl_adv_loss, on that stream validate and record
+ * their arguments instead of launching; _end launches them as ONE kernel (their blocks by range).  The batched
+ * calls must not depend on each other (they read and write disjoint buffers).  Same results as the separate
+ * launches; one launch floor instead of several. */
 int cgl_conv_batch_begin(void* stream);
 int cgl_conv_batch_end(void* stream);
 int cgl_conv3x3_fwd_packed(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w, int cin,
