@@ -7,8 +7,10 @@ Rounds start at the fused prologue GEMM (cgl_gemm_pro).  Only rounds with the pl
 no host gap (graph replays back to back: the timed region) are used; per launch position the median of
 its duration, of the gap before it (previous end -> its start) and of the round period are reported, and
 the GEMM family's in-round average duration (cgl_gemm_f32 dispatches) -- the figure bench.py's
-roofline.avg_gemm_launch_us is checked against.  --bench LOG (the stdout of the profiled bench.py run, its JSON
-line) recomputes the GEMM family's roofline fraction from the trace's timed rounds -- the line's
+roofline.avg_gemm_launch_us is checked against.  --bench LOG (a bench.py JSON line: use the same commit's
+UNPROFILED run -- under the kernel trace every eager launch's event timing grows ~4 us, which skews the line's
+eager sum and its per-launch offset; r04y: 13.7 vs 9.7 us eager average, -8.3% against the trace instead of
+-2.1%) recomputes the GEMM family's roofline fraction from the trace's timed rounds -- the line's
 gemm_flops_per_round over the summed in-round cgl_gemm_f32 durations -- and compares it with roofline.frac."""
 import argparse
 import csv
