@@ -161,15 +161,22 @@ def conv3x3_bwd_data(dy, w, dx, n, h, wd, cin, cout, stride=1, up=0, wp=None, st
     """``stats`` = (part, groups, x, post, mean, slope[, post_coef]): also write the previous BatchNorm2d's
     backward partials {sum g, sum g (x - mean)} per 32-row chunk of dx (g = dx * leaky'(post) if post; with
     post_coef = (coef, group, groups) and post None: leaky' from the forward's scale / shift, bn2d_bwd's
-    post_coef) -- consumed by bn2d_bwd_stats; needs ``wp``."""
+    post_coef) -- consumed by bn2d_bwd_stats (R = 32); with ``wp`` None only the one-output-channel 3x3
+    geometry, per 128-row chunk (bn2d_bwd_stats R = 128, bitwise bn2d_bwd)."""
     _chk(dy, w, dx, wp)
     ws = workspace(conv_ws_bytes(n, h, wd, cin, cout, stride, up), dy.device)
     if stats is not None:
         part, groups, x, post, mean, slope = stats[:6]
         pc, pld = _post_coef(stats[6] if len(stats) > 6 else None, cin)
         _chk(x, post, mean)
-        if wp is None or not part.is_cuda or part.dtype != torch.float64:
-            raise RuntimeError("conv3x3_bwd_data(stats=...): needs packed weights and a float64 CUDA partial buffer")
+        if not part.is_cuda or part.dtype != torch.float64:
+            raise RuntimeError("conv3x3_bwd_data(stats=...): needs a float64 CUDA partial buffer")
+        if wp is None:      # the vector one-output-channel kernel: partials per 128-row chunk
+            C.check(C.lib.cgl_conv3x3_bwd_data_stats(_p(dy), _p(w), _p(dx), n, h, wd, cin, cout, stride, up,
+                                                     int(groups), _p(part), _p(x), _p(post), _p(pc), int(pld),
+                                                     _p(mean), float(slope), _p(ws), ws.numel(), _s()),
+                    "cgl_conv3x3_bwd_data_stats")
+            return dx
         C.check(C.lib.cgl_conv3x3_bwd_data_packed_stats(_p(dy), _p(wp), _p(dx), n, h, wd, cin, cout, stride, up,
                                                         int(groups), _p(part), _p(x), _p(post), _p(pc), int(pld),
                                                         _p(mean), float(slope), _p(ws), ws.numel(), _s()),

@@ -270,6 +270,10 @@ class ConvGanStep:
         for key, (n, h, ci, co, st, up, grp) in bgeo.items():
             nb = O.stat_chunks(n, h, h, ci, co, st, up, grp, bwd=True)
             self.bst_ok[key] = key in self.st_part and 0 < nb * ci * 2 <= self.st_part[key].numel()
+        # conv_blocks.6's backward partials from the Conv2d(64, 1) input gradient itself (cgl_conv3x3_bwd_data_stats,
+        # 128-row chunks: bitwise the channel reduction it saves; CGL_CONV_N1STATS=0 keeps that launch)
+        self.n1_stats = (os.environ.get("CGL_CONV_N1STATS", "1") != "0" and "conv_blocks.6" in self.st_part and
+                         B * 1024 % 128 == 0 and B * 1024 // 128 * 64 * 2 <= self.st_part["conv_blocks.6"].numel())
         # sampler over a device-resident real shard [n, 1024] (DataLoader(shuffle=True), capgan.py:282)
         self.data = data
         self.short = data is not None and data.shape[0] % batch != 0    # some batch of a pass is short
@@ -534,12 +538,19 @@ class ConvGanStep:
         else:
             O.conv3x3_bwd_weight(self.dc3g, self.a2[B:], G["conv_blocks.8.weight"], G["conv_blocks.8.bias"], B, 32, 32,
                                  64, 1, 1, 0)
-        O.conv3x3_bwd_data(self.dc3g, P["conv_blocks.8.weight"], self.da2, B, 32, 32, 64, 1, 1, 0)
         sm, si = self.g_save["conv_blocks.6"]
         pc6 = self._post_coef("conv_blocks.6")
-        O.bn2d_bwd(self.da2, self.y2[B:], B, 1024, 64, sm[1], si[1], P["conv_blocks.6.weight"], self.dy2,
-                   post=None if pc6 else self.a2[B:], post_coef=pc6, dgamma=G["conv_blocks.6.weight"],
-                   dbeta=G["conv_blocks.6.bias"], slope=SLOPE)
+        kw = dict(post=None if pc6 else self.a2[B:], post_coef=pc6, dgamma=G["conv_blocks.6.weight"],
+                  dbeta=G["conv_blocks.6.bias"], slope=SLOPE)
+        if self.n1_stats:
+            part = self.st_part["conv_blocks.6"]
+            O.conv3x3_bwd_data(self.dc3g, P["conv_blocks.8.weight"], self.da2, B, 32, 32, 64, 1, 1, 0,
+                               stats=(part, 1, self.y2[B:], kw["post"], sm[1], SLOPE, pc6))
+            O.bn2d_bwd_stats(part, self.da2, self.y2[B:], B, 1024, 64, sm[1], si[1], P["conv_blocks.6.weight"],
+                             self.dy2, R=128, **kw)
+        else:
+            O.conv3x3_bwd_data(self.dc3g, P["conv_blocks.8.weight"], self.da2, B, 32, 32, 64, 1, 1, 0)
+            O.bn2d_bwd(self.da2, self.y2[B:], B, 1024, 64, sm[1], si[1], P["conv_blocks.6.weight"], self.dy2, **kw)
         if e2:
             O.conv3x3_bwd_weight(self.dy2, self.y1[B:], G["conv_blocks.5.weight"], G["conv_blocks.5.bias"], B, 16, 16,
                                  128, 64, 1, 1, bn_in=(self.coef["conv_blocks.2"], 1, 2, O.ACT_LEAKY, SLOPE))

@@ -1591,18 +1591,52 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad_n1t(CglConvLaunch args) {
 // the reference's OIHW W once (no packing launch) and stay in registers; the 9 dY scalars are
 // broadcast reads of a 4 KB image (L1 / L2 hits).  Taps are summed in (ky, kx) order.
 #define CGL_BN1_PPT 8
-template <int C4>
+// ST: also the next BatchNorm2d backward's per-chunk partials (cgl_chan_reduce4 mode 1 of dX, fused): a workgroup's
+// CGL_BN1_PPT x 16 pixels are one 128-row chunk, and lane (pixel slot rl, channel quad q) holds rows rl + 16 k in k
+// order -- the very rows, order and lane-then-slot sums of cgl_chan_reduce4 with R = 128, so the partials are
+// bitwise the ones cgl_bn2d_bwd computes from the stored dX.
+struct CglN1Stats {
+  const float* X;            // [npix][4 C4] the BatchNorm's input y (pre-normalisation)
+  const float* post;         // LeakyReLU'(post), or null
+  const float* psc; int psc_ld;   // or LeakyReLU' from the sign of fmaf(y, scale, shift)
+  const float* mean;         // [groups][4 C4]
+  float slope;
+  int gr;                    // rows per group (a multiple of 128)
+  double* part;              // [npix / 128][4 C4][2]
+};
+template <int C4, bool ST = false>
 __global__ __launch_bounds__(256) void cgl_conv_bwd_n1(const float* __restrict__ dY, const float* __restrict__ W,
-                                                       float* __restrict__ dX, int npix, int H, int Wd) {
+                                                       float* __restrict__ dX, int npix, int H, int Wd, CglN1Stats st) {
   const int q = threadIdx.x & (C4 - 1);
   f32x4 w[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int j = 0; j < 4; ++j) w[t][j] = gld(W + (4 * q + j) * 9 + t);
+  double x0[4] = {0.0, 0.0, 0.0, 0.0}, x1[4] = {0.0, 0.0, 0.0, 0.0};
+  f32x4 mu = {}, ps = {}, ph = {};
+  float slope = 0.f;
+  if constexpr (ST) {
+    const int r0 = blockIdx.x * (CGL_BN1_PPT * (256 / C4));
+    mu = *(gcf4p)(st.mean + (long)(r0 / st.gr) * (4 * C4) + 4 * q);
+    if (st.psc) {
+      ps = *(gcf4p)(st.psc + 4 * q);
+      ph = *(gcf4p)(st.psc + st.psc_ld + 4 * q);
+    }
+    slope = st.slope;
+  }
+  // the statistics' y values of all CGL_BN1_PPT pixels in flight before the first dY gather
+  f32x4 xs[ST ? CGL_BN1_PPT : 1];
+  if constexpr (ST) {
+#pragma unroll
+    for (int k = 0; k < CGL_BN1_PPT; ++k)
+      xs[k] = *(gcf4p)(st.X + ((long)((blockIdx.x * CGL_BN1_PPT + k) * (256 / C4) + (int)threadIdx.x / C4)) * (4 * C4) +
+                       4 * q);
+  }
   // CGL_BN1_PPT pixels per lane group (the weight loads amortised over them), consecutive groups of a
   // workgroup on consecutive pixels
-#pragma unroll 2
+  constexpr int kUnroll = ST ? CGL_BN1_PPT : 2;
+#pragma unroll kUnroll
   for (int k = 0; k < CGL_BN1_PPT; ++k) {
   const int p = (blockIdx.x * CGL_BN1_PPT + k) * (256 / C4) + (int)threadIdx.x / C4;
   const int pc = min(p, npix - 1);
@@ -1627,6 +1661,46 @@ __global__ __launch_bounds__(256) void cgl_conv_bwd_n1(const float* __restrict__
     acc[3] = fmaf(dv[t], w[t][3], acc[3]);
   }
   if (p < npix) *(gf4p)(dX + (long)p * (4 * C4) + 4 * q) = acc;
+  if constexpr (ST) {     // (the launch covers whole chunks: every p < npix)
+    const long o = (long)p * (4 * C4) + 4 * q;
+    const f32x4 xv = xs[ST ? k : 0];
+    f32x4 g = acc;
+    if (st.psc) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[j] = fmaf(xv[j], ps[j], ph[j]) > 0.f ? g[j] : g[j] * slope;
+    } else if (st.post) {
+      const f32x4 pv = *(gcf4p)(st.post + o);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[j] = pv[j] > 0.f ? g[j] : g[j] * slope;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x0[j] += (double)g[j];
+      x1[j] += (double)(g[j] * (xv[j] - mu[j]));
+    }
+  }
+  }
+  if constexpr (ST) {
+    __shared__ double s0[1024], s1[1024];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s0[threadIdx.x * 4 + j] = x0[j];
+      s1[threadIdx.x * 4 + j] = x1[j];
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < C4) {
+      constexpr int rp = 256 / C4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        double t0 = 0.0, t1 = 0.0;
+        for (int r = 0; r < rp; ++r) {
+          t0 += s0[(r * C4 + q) * 4 + j];
+          t1 += s1[(r * C4 + q) * 4 + j];
+        }
+        st.part[((long)blockIdx.x * (4 * C4) + 4 * q + j) * 2] = t0;
+        st.part[((long)blockIdx.x * (4 * C4) + 4 * q + j) * 2 + 1] = t1;
+      }
+    }
   }
 }
 
@@ -3531,7 +3605,8 @@ int conv_bwd_data_impl(const ConvGeom& g, const float* dY, const float* W, float
   if (!st_part && W && g.cout == 1 && g.cin == 64 && g.ks == 3 && g.stride == 1 && !g.up && al16(dX) &&
       (int64_t)g.n * g.h * g.w < (int64_t)1 << 30) {
     const int npix = g.n * g.h * g.w;
-    hipLaunchKernelGGL((cgl_conv_bwd_n1<16>), dim3((npix + 16 * CGL_BN1_PPT - 1) / (16 * CGL_BN1_PPT)), dim3(256), 0, s, dY, W, dX, npix, g.h, g.w);
+    hipLaunchKernelGGL((cgl_conv_bwd_n1<16>), dim3((npix + 16 * CGL_BN1_PPT - 1) / (16 * CGL_BN1_PPT)), dim3(256), 0, s, dY, W, dX, npix, g.h, g.w,
+                       CglN1Stats{});
     return (int)hipGetLastError();
   }
   CglConvProb P[CGL_CONV_MAXP];
@@ -3975,6 +4050,31 @@ int cgl_conv3x3_bwd_data_packed_stats(const float* dY, const float* Wp, float* d
   sb.x = bn_x; sb.post = bn_post; sb.mean = bn_mean; sb.slope = slope;
   sb.psc = bn_post_coef; sb.psc_ld = bn_post_coef_ld;
   return conv_bwd_data_impl(g, dY, nullptr, dX, ws, wsb, (hipStream_t)stream, Wp, part, groups, &sb);
+}
+
+int cgl_conv3x3_bwd_data_stats(const float* dY, const float* W, float* dX, int n, int h, int w, int cin, int cout,
+                               int stride, int up, int groups, double* part, const float* bn_x, const float* bn_post,
+                               const float* bn_post_coef, int bn_post_coef_ld, const float* bn_mean, float slope,
+                               void* ws, int64_t wsb, void* stream) {
+  ConvGeom g;
+  const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
+  if (rc) return rc;
+  // the vector one-output-channel input gradient (Conv2d(64, 1, 3, 1, 1)) only; partials per 128-row chunk
+  if (!dY || !W || !dX || !part || !bn_x || !bn_mean || (bn_post_coef && (bn_post || groups != 1))) return CGL_E_ARG;
+  if (g.cout != 1 || g.cin != 64 || g.ks != 3 || g.stride != 1 || g.up || groups < 1 || n % groups) return CGL_E_ARG;
+  if (!al16(dX) || !al16(bn_x) || !al16(bn_mean) || (bn_post && !al16(bn_post)) || ((uintptr_t)part & 15))
+    return CGL_E_ARG;
+  if (bn_post_coef && (!al16(bn_post_coef) || bn_post_coef_ld % 4)) return CGL_E_ARG;
+  const int64_t gr = (int64_t)(n / groups) * h * w;
+  if (gr % (16 * CGL_BN1_PPT) || (int64_t)n * h * w >= (int64_t)1 << 30) return CGL_E_ARG;
+  (void)ws; (void)wsb;
+  const int npix = n * h * w;
+  CglN1Stats st;
+  st.X = bn_x; st.post = bn_post; st.psc = bn_post_coef; st.psc_ld = bn_post_coef_ld; st.mean = bn_mean;
+  st.slope = slope; st.gr = (int)gr; st.part = part;
+  hipLaunchKernelGGL((cgl_conv_bwd_n1<16, true>), dim3(npix / (16 * CGL_BN1_PPT)), dim3(256), 0, (hipStream_t)stream,
+                     dY, W, dX, npix, g.h, g.w, st);
+  return (int)hipGetLastError();
 }
 
 int cgl_conv3x3_bwd_data_packed(const float* dY, const float* W, const float* Wp, float* dX, int n, int h, int w,

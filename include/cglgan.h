@@ -338,6 +338,14 @@ int cgl_conv3x3_bwd_data_packed_stats(const float* dY, const float* Wp, float* d
                                       const float* bn_post, const float* bn_post_coef, int bn_post_coef_ld,
                                       const float* bn_mean, float slope, void* workspace, int64_t ws_bytes,
                                       void* stream);
+/* The same statistics from the vector one-output-channel input gradient (Conv2d(64, 1, 3, 1, 1) + Tanh,
+ * model/lsgan.py:19-20; raw OIHW W, no packing) -- per 128-ROW chunk, the chunking of cgl_bn2d_bwd, so
+ * cgl_bn2d_bwd_stats(R = 128) gives bitwise cgl_bn2d_bwd's result on the stored dX (the channel reduction
+ * launch saved).  Other geometries: CGL_E_ARG.  (n / groups) h w must be a multiple of 128. */
+int cgl_conv3x3_bwd_data_stats(const float* dY, const float* W, float* dX, int n, int h, int w, int cin, int cout,
+                               int stride, int up, int groups, double* part, const float* bn_x, const float* bn_post,
+                               const float* bn_post_coef, int bn_post_coef_ld, const float* bn_mean, float slope,
+                               void* workspace, int64_t ws_bytes, void* stream);
 int cgl_dense_fwd_packed(const float* X, const float* Wp, const float* b, float* Y, int M, int K, int N, int act,
                          float slope, void* workspace, int64_t ws_bytes, void* stream);
 int cgl_dense_bwd_data_packed(const float* dY, const float* Wp, float* dX, int M, int K, int N, void* workspace,

@@ -150,3 +150,43 @@ def test_bwd_stats_canaries(n, h, cin, cout, stride, up, groups):
         scale = float(ref.abs().max())
         assert float((out - ref).abs().max()) <= 5e-5 * scale, f"bn bwd vs two-pass (rep {rep})"
         assert torch.allclose(dg, dg2, rtol=5e-5, atol=1e-4) and torch.allclose(db, db2, rtol=5e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("groups", [1, 2])
+def test_bwd_n1_stats_bitwise(groups):
+    """cgl_conv3x3_bwd_data_stats (the Conv2d(64, 1) input gradient with conv_blocks.6's backward partials per
+    128-row chunk) + bn2d_bwd_stats(R = 128) against cgl_conv3x3_bwd_data + bn2d_bwd: bitwise equal (same
+    chunks, rows, order), canaries intact, with post and with post_coef."""
+    O = ops()
+    torch.manual_seed(11 + groups)
+    n, h, cin = 2 * 16, 32, 64
+    hw = h * h
+    w = torch.randn(1, cin, 3, 3, device=DEV) * 0.1
+    dy = torch.randn(n, h, h, 1, device=DEV)
+    xbn = torch.randn(n, h, h, cin, device=DEV)
+    post = torch.randn(n, h, h, cin, device=DEV)
+    sm = torch.randn(groups, cin, device=DEV) * 0.1
+    si = 1 + 0.1 * torch.rand(groups, cin, device=DEV)
+    gam = 1 + 0.1 * torch.randn(cin, device=DEV)
+    coef = torch.randn(2 * cin, device=DEV)
+    for pc in ([None, (coef, 0, 1)] if groups == 1 else [None]):
+        kw = dict(post=None if pc else post, post_coef=pc) if pc else dict(post=post)
+        part, part_buf = padded(n * hw // 128 * cin * 2, torch.float64)
+        dx, dx_buf = padded(n * hw * cin)
+        dx = dx.view(n, h, h, cin)
+        O.conv3x3_bwd_data(dy, w, dx, n, h, h, cin, 1, 1, 0,
+                           stats=(part, groups, xbn, kw.get("post"), sm, 0.2) + ((pc,) if pc else ()))
+        out, out_buf = padded(n * hw * cin)
+        dg, db = torch.empty(cin, device=DEV), torch.empty(cin, device=DEV)
+        O.bn2d_bwd_stats(part, dx, xbn, n, hw, cin, sm, si, gam, out, groups=groups, dgamma=dg, dbeta=db, R=128, **kw)
+        dx2 = torch.empty(n, h, h, cin, device=DEV)
+        O.conv3x3_bwd_data(dy, w, dx2, n, h, h, cin, 1, 1, 0)
+        ref = torch.empty(n * hw * cin, device=DEV)
+        dg2, db2 = torch.empty(cin, device=DEV), torch.empty(cin, device=DEV)
+        O.bn2d_bwd(dx2, xbn, n, hw, cin, sm, si, gam, ref, groups=groups, dgamma=dg2, dbeta=db2, **kw)
+        torch.cuda.synchronize()
+        for t, bf, k in ((part, part_buf, "st_part"), (dx.view(-1), dx_buf, "dx"), (out, out_buf, "bn dx")):
+            canary_ok(bf, t.numel(), k)
+        assert torch.equal(dx, dx2) and torch.equal(out, ref), pc is not None
+        assert torch.equal(dg, dg2) and torch.equal(db, db2), pc is not None
+
