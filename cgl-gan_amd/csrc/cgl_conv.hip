@@ -136,6 +136,13 @@ __device__ __forceinline__ int cgl_xcd_tile(int local, int nwg) {
 // the tap table.  One wave owns TM x TN 32x32 accumulators; WM x WN waves per workgroup.
 // FAST: Cin % 16 == 0, so a 16-k chunk lies inside one tap (uniform tap, 2 x 16-byte loads per
 // lane and block).  Otherwise each k is decoded per element (tiny-K layers: Cin = 1).
+// The folded BatchNorm's activation slope: LeakyReLU(w) = max(w, w * slope) -- bitwise cgl_eltwise's
+// (w > 0 ? w : w * slope) for 0 <= slope <= 1 (the entry points require it), two VALU ops instead of three;
+// act none = slope 1 (max(w, w) = w), so the staging loops carry no activation branch.
+__device__ __forceinline__ float cgl_bnin_slope(CglKL L) {
+  return L->in_act == CGL_EPI_ACT_LEAKY ? L->in_slope : 1.f;
+}
+
 template <int TM, int TN, bool FAST, bool BNIN = false, bool HALO = false, bool LDSM = false>
 __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, float* s_red, bool direct = false) {
   constexpr int S = 3;
@@ -164,6 +171,7 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
   int cgo[TM];                 // BNIN: this row's BatchNorm group offset into the coefficient table
   float* s_coef = s_red;       // BNIN: [2][in_groups][Cin] scale / shift staged in LDS ahead of s_red
   const int coef_n = BNIN ? 2 * L->in_groups * Cin : 0;
+  const float bn_sl = BNIN ? cgl_bnin_slope(L) : 0.f;
   if constexpr (BNIN && !HALO) {
     for (int q = tid; q < coef_n; q += 256) s_coef[q] = gld(L->in_coef + q);
     s_red += (coef_n + 63) & ~63;
@@ -245,8 +253,7 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
       // padded taps and out-of-range channels stay zero, as in the applied activation)
       const int c0 = (okm >> 8) & 0xfff, c1 = (okm >> 20) & 0xfff;
       const int shb = coef_n >> 1;
-      const float sl = L->in_slope;
-      const bool lk = L->in_act == CGL_EPI_ACT_LEAKY;
+      const float sl = bn_sl;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const f32x4 s0 = *(const f32x4*)(s_coef + cgo[i] + c0), s1 = *(const f32x4*)(s_coef + cgo[i] + c1);
@@ -254,7 +261,7 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           float v = fmaf(A[i][q], q < 4 ? s0[q] : s1[q - 4], q < 4 ? h0[q] : h1[q - 4]);
-          if (lk) v = v > 0.f ? v : v * sl;
+          v = fmaxf(v, v * sl);
           A[i][q] = v;
         }
       }
@@ -393,8 +400,7 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
     const bool qfix = (256 % c4) == 0;
     // the activation flag and slope in registers: read through the kernarg pointer inside the loop, the slope's
     // scalar load sat under the LeakyReLU condition and became a branch per value
-    const bool in_lk = BNIN && L->in_act == CGL_EPI_ACT_LEAKY;
-    const float in_sl = BNIN ? L->in_slope : 0.f;
+    const float in_sl = BNIN ? cgl_bnin_slope(L) : 0.f;
     f32x4 sc0 = {0.f, 0.f, 0.f, 0.f}, sh0 = sc0;
     if (BNIN && qfix) {
       sc0 = *(gcf4p)(L->in_coef + g * Cin + 4 * (tid % c4));
@@ -413,7 +419,7 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             float w = fmaf(v[u], sc[u], sh[u]);
-            if (in_lk) w = w > 0.f ? w : w * in_sl;
+            w = fmaxf(w, w * in_sl);
             v[u] = w;
           }
         }
@@ -828,12 +834,11 @@ __device__ __forceinline__ void cgl_conv_wgrad_body(CglKL L, CglKP P, int local)
       bsc[q][j] = BNIN ? gld(L->in_coef + gq * Cin + cci[j]) : 0.f;
       bsh[q][j] = BNIN ? gld(L->in_coef + (L->in_groups + gq) * Cin + cci[j]) : 0.f;
     }
-  const bool in_lk = BNIN && L->in_act == CGL_EPI_ACT_LEAKY;   // (in registers: see the halo staging)
-  const float in_sl = BNIN ? L->in_slope : 0.f;
+  const float in_sl = BNIN ? cgl_bnin_slope(L) : 0.f;       // (in registers: see the halo staging)
   auto bn = [&](float x, int img, int j) {
     const int q = (bg > 1 && img >= L->in_gimg) ? 1 : 0;     // (<= 2 groups: no division per value)
     float v = fmaf(x, q ? bsc[1][j] : bsc[0][j], q ? bsh[1][j] : bsh[0][j]);
-    if (in_lk) v = v > 0.f ? v : v * in_sl;
+    v = fmaxf(v, v * in_sl);
     return v;
   };
 
@@ -1033,8 +1038,7 @@ __global__ __launch_bounds__(256 * KS, 2 / KS) void cgl_conv_wgrad_lds(CglConvLa
   const int tap = kk / Cin, ci = kk - tap * Cin;
   const int cdy = P->dy[tap / P->Tx], cdx = P->dx[tap - (tap / P->Tx) * P->Tx];
   f32x4 bsc = {0.f, 0.f, 0.f, 0.f}, bsh = bsc;
-  const bool in_lk = BNIN && L->in_act == CGL_EPI_ACT_LEAKY;   // (in registers: see the halo staging)
-  const float in_sl = BNIN ? L->in_slope : 0.f;
+  const float in_sl = BNIN ? cgl_bnin_slope(L) : 0.f;       // (in registers: see the halo staging)
   if constexpr (BNIN) {
     bsc = *(gcf4p)(L->in_coef + (long)L->in_g0 * Cin + ci);
     bsh = *(gcf4p)(L->in_coef + (long)(L->in_groups + L->in_g0) * Cin + ci);
@@ -1084,7 +1088,7 @@ __global__ __launch_bounds__(256 * KS, 2 / KS) void cgl_conv_wgrad_lds(CglConvLa
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           float w = fmaf(v[u], bsc[u], bsh[u]);
-          if (in_lk) w = w > 0.f ? w : w * in_sl;
+          w = fmaxf(w, w * in_sl);
           v[u] = w;
         }
       }
@@ -1373,8 +1377,7 @@ __global__ __launch_bounds__(256) void cgl_conv_n1_part(CglConvLaunch args) {
   }
   if (L->in_coef) {   // the input's BatchNorm2d (+ LeakyReLU) folded into the load (one group per image)
     const int cg = min(img / L->in_gimg, L->in_groups - 1) * C, shb = L->in_groups * C;
-    const float sl = L->in_slope;
-    const bool lk = L->in_act == CGL_EPI_ACT_LEAKY;
+    const float sl = cgl_bnin_slope(L);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const f32x4 sc = *(gcf4p)(L->in_coef + cg + 16 * j + 4 * i), sh = *(gcf4p)(L->in_coef + shb + cg + 16 * j + 4 * i);
@@ -1383,7 +1386,7 @@ __global__ __launch_bounds__(256) void cgl_conv_n1_part(CglConvLaunch args) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float v = fmaf(x[k][i][e], sc[e], sh[e]);
-          if (lk) v = v > 0.f ? v : v * sl;
+          v = fmaxf(v, v * sl);
           x[k][i][e] = v;
         }
     }
@@ -1505,8 +1508,7 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad_n1t(CglConvLaunch args) {
 #pragma unroll
   for (int t = 0; t < 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 isc = {0.f, 0.f, 0.f, 0.f}, ish = isc;
-  const bool in_lk = BNIN && L->in_act == CGL_EPI_ACT_LEAKY;   // (in registers: see the halo staging)
-  const float in_sl = BNIN ? L->in_slope : 0.f;
+  const float in_sl = BNIN ? cgl_bnin_slope(L) : 0.f;       // (in registers: see the halo staging)
   if constexpr (BNIN) {
     isc = *(gcf4p)(L->in_coef + (long)L->in_g0 * Cin + 4 * q4);
     ish = *(gcf4p)(L->in_coef + (long)(L->in_groups + L->in_g0) * Cin + 4 * q4);
@@ -1556,7 +1558,7 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad_n1t(CglConvLaunch args) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float w = fmaf(x[u][e], isc[e], ish[e]);
-          if (in_lk) w = w > 0.f ? w : w * in_sl;
+          w = fmaxf(w, w * in_sl);
           x[u][e] = w;
         }
     }
@@ -3370,6 +3372,7 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
     L.in_gimg = bi->gimg;
     L.in_act = bi->act;
     L.in_slope = bi->slope;
+    if (bi->act == CGL_EPI_ACT_LEAKY && !(bi->slope >= 0.f && bi->slope <= 1.f)) return CGL_E_ARG;   // (max form)
   }
   L.slope = slope;
   L.drop = drop;
@@ -3690,6 +3693,7 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
     L.in_gimg = bi->gimg;
     L.in_act = bi->act;
     L.in_slope = bi->slope;
+    if (bi->act == CGL_EPI_ACT_LEAKY && !(bi->slope >= 0.f && bi->slope <= 1.f)) return CGL_E_ARG;   // (max form)
     L.in_g0 = bi->g0;
   }
   float* part = (float*)ws;
