@@ -3493,9 +3493,14 @@ int fin_nocache() {
   return v;
 }
 
+// Rows per channel-reduction chunk (one workgroup each): 128, halved down to 32 while a BatchNorm call would
+// get fewer than 64 chunks -- the discriminator's 2 x 2 and 4 x 4 maps (1024-4096 rows per call) otherwise ran
+// their reduction on 8-32 workgroups, latency-bound (CGL_CHAN_MINCH=0: plain 128).
 int chan_chunk(int64_t gr) {
+  static const int minch = getenv("CGL_CHAN_MINCH") ? atoi(getenv("CGL_CHAN_MINCH")) : 64;
   int R = 128;
   while (R > 1 && gr % R != 0) R >>= 1;
+  while (R > 32 && gr / R < minch && gr % (R >> 1) == 0) R >>= 1;
   return R;
 }
 
