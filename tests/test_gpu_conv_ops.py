@@ -108,7 +108,8 @@ def test_conv3x3_fwd_bwd(n, h, w, cin, cout, stride, up, act):
     close(db, b2.grad, what="bias grad")
 
 
-@pytest.mark.parametrize("M,K,N,act", [(512, 100, 8192, 0), (64, 512, 1, 0), (37, 100, 70, 1), (16, 48, 33, 2)])
+@pytest.mark.parametrize("M,K,N,act", [(512, 100, 8192, 0), (64, 512, 1, 0), (512, 512, 1, 0), (7, 300, 1, 0),
+                                       (37, 100, 70, 1), (16, 48, 33, 2)])
 def test_dense(M, K, N, act):
     O = ops()
     g = torch.Generator().manual_seed(M + K + N)
