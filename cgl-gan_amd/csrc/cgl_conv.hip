@@ -2588,9 +2588,9 @@ __global__ __launch_bounds__(256) void cgl_dense1_fwd_nhwc_k(const float* __rest
 // Weight + bias gradient of a one-output Linear (the discriminator's adv_layer, model/lsgan.py:90-97, on the
 // NCHW-flattened map): dW[k] = sum_m dY[m] X[m][k], db = sum_m dY[m] in ONE launch (the implicit-GEMM weight
 // gradient took four: partial tiles, their reduce, the bias column sum and its finalize, for 0.27 MFLOP).
-// Block b < gridDim.x - 1: 64 columns x 4 row lanes (a wave reads 256 contiguous bytes of a row); lane l sums
-// rows l, l + 4, ... in order in double (exact products), 32 loads in flight; the 4 lanes are added in lane
-// order.  The last block: db, thread t summing rows t, t + 256, ... then the 256 partials in order.
+// Block b < gridDim.x - 1: 16 columns x 16 row lanes (a wave reads 4 rows x 64 contiguous bytes); lane l sums
+// rows l, l + 16, ... in order in double (exact products), 32 loads in flight (M <= 512: one batch); the 16 lanes
+// are added in lane order.  The last block: db, thread t summing rows t, t + 256, ... then the 256 partials in order.
 __global__ __launch_bounds__(256) void cgl_dense1_wgrad_k(const float* __restrict__ dY, const float* __restrict__ X,
                                                           float* __restrict__ dW, float* __restrict__ db, int M,
                                                           int K) {
@@ -2608,24 +2608,28 @@ __global__ __launch_bounds__(256) void cgl_dense1_wgrad_k(const float* __restric
     }
     return;
   }
-  const int kl = t & 63, ml = t >> 6;
-  const int k = blockIdx.x * 64 + kl, kc = min(k, K - 1);
+  const int kl = t & 15, ml = t >> 4;
+  const int k = blockIdx.x * 16 + kl, kc = min(k, K - 1);
   double acc = 0.0;
-  for (int m0 = ml; m0 < M; m0 += 4 * 32) {
+  for (int m0 = ml; m0 < M; m0 += 16 * 32) {
     float xv[32], dv[32];
 #pragma unroll
     for (int i = 0; i < 32; ++i) {
-      const int m = min(m0 + 4 * i, M - 1);
+      const int m = min(m0 + 16 * i, M - 1);
       xv[i] = gld(X + (long)m * K + kc);
       dv[i] = gld(dY + m);
     }
 #pragma unroll
     for (int i = 0; i < 32; ++i)
-      if (m0 + 4 * i < M) acc += (double)dv[i] * (double)xv[i];
+      if (m0 + 16 * i < M) acc += (double)dv[i] * (double)xv[i];
   }
   red[t] = acc;
   __syncthreads();
-  if (ml == 0 && k < K) gst(dW + k, (float)(((red[kl] + red[64 + kl]) + red[128 + kl]) + red[192 + kl]));
+  if (ml == 0 && k < K) {
+    double s = 0.0;
+    for (int l = 0; l < 16; ++l) s += red[16 * l + kl];
+    gst(dW + k, (float)s);
+  }
 }
 
 // Elementwise NHWC passes (float4 over channels; C % 4 == 0):
@@ -3958,7 +3962,7 @@ int cgl_dense_bwd_weight(const float* dY, const float* X, float* dW, float* db, 
   // N = 1 (adv_layer): the one-launch kernel (CGL_DENSE1_WG=0: the implicit-GEMM weight gradient)
   static const int d1 = getenv("CGL_DENSE1_WG") ? atoi(getenv("CGL_DENSE1_WG")) : 1;
   if (d1 && N == 1 && dY && X && dW && (int64_t)M * K < ((int64_t)1 << 31)) {
-    hipLaunchKernelGGL(cgl_dense1_wgrad_k, dim3((K + 63) / 64 + 1), dim3(256), 0, (hipStream_t)stream, dY, X, dW, db,
+    hipLaunchKernelGGL(cgl_dense1_wgrad_k, dim3((K + 15) / 16 + 1), dim3(256), 0, (hipStream_t)stream, dY, X, dW, db,
                        M, K);
     return (int)hipGetLastError();
   }
