@@ -30,7 +30,7 @@ EXPORTS = [
     # conv GAN path (model/lsgan.py)
     "cgl_conv3x3_workspace_bytes", "cgl_conv3x3_fwd", "cgl_conv3x3_bwd_data", "cgl_conv3x3_bwd_weight",
     "cgl_conv3x3_bwd_weight_bnin",
-    "cgl_bn2d_workspace_bytes", "cgl_bn2d_fwd", "cgl_bn2d_bwd", "cgl_act_drop_bwd", "cgl_dropout2d_mask", "cgl_dropout2d_masks",
+    "cgl_bn2d_workspace_bytes", "cgl_bn2d_fwd", "cgl_bn2d_bwd", "cgl_act_drop_bwd", "cgl_act_drop_bwd_colsum", "cgl_colsum_finalize", "cgl_dropout2d_mask", "cgl_dropout2d_masks",
     "cgl_nchw_to_nhwc", "cgl_nhwc_to_nchw", "cgl_dense1_bwd_data_nhwc", "cgl_dense1_fwd_nhwc", "cgl_adv_loss", "cgl_adam_multi", "cgl_dense_workspace_bytes",
     "cgl_dense_fwd", "cgl_dense_bwd_data", "cgl_dense_bwd_weight", "cgl_gather_rows", "cgl_weights_scale",
     "cgl_conv_packed_floats", "cgl_conv_pack_multi", "cgl_conv_batch_begin", "cgl_conv_batch_end", "cgl_conv3x3_fwd_packed", "cgl_conv3x3_bwd_data_packed",
@@ -133,6 +133,8 @@ def _load():
         "cgl_bn2d_bwd": (ci, [vp, vp, vp, ci, ci, ci, ci, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, ci, vp, vp, i64,
                               vp]),
         "cgl_act_drop_bwd": (ci, [vp, vp, vp, ci, ci, ci, cf, ci, vp, vp]),
+        "cgl_act_drop_bwd_colsum": (ci, [vp, vp, vp, ci, ci, ci, cf, ci, vp, vp, vp]),
+        "cgl_colsum_finalize": (ci, [vp, ci, ci, vp, vp]),
         "cgl_dropout2d_mask": (ci, [vp, ci, ci, cd, ctypes.c_ulonglong, ctypes.c_ulonglong, vp]),
         "cgl_dropout2d_masks": (ci, [ci, P(vp), P(ci), P(ci), cd, ctypes.c_ulonglong, P(ctypes.c_ulonglong), vp]),
         "cgl_nchw_to_nhwc": (ci, [vp, vp, ci, ci, ci, vp]),

@@ -397,11 +397,25 @@ def bn2d_bwd_stats(part, dy, x, n, hw, c, save_mean, save_invstd, gamma, dx, gro
     return dx
 
 
-def act_drop_bwd(dy, post, drop, n, hw, c, dx, slope=0.2, tanh_y=False):
+def act_drop_bwd(dy, post, drop, n, hw, c, dx, slope=0.2, tanh_y=False, colsum=None):
+    """``colsum`` (c == 1): float64 [(n hw + 255) // 256, 2] -- also the column-sum partials of dx per 256-row
+    chunk (cgl_act_drop_bwd_colsum; colsum_finalize turns them into the bias gradient)."""
     _chk(dy, post, drop, dx)
+    if colsum is not None:
+        if not colsum.is_cuda or colsum.dtype != torch.float64 or colsum.numel() < 2 * ((n * hw + 255) // 256):
+            raise RuntimeError("act_drop_bwd(colsum=...): float64 CUDA buffer of 2 per 256 rows")
+        C.check(C.lib.cgl_act_drop_bwd_colsum(_p(dy), _p(post), _p(drop), n, hw, c, float(slope), int(tanh_y), _p(dx),
+                                              _p(colsum), _s()), "cgl_act_drop_bwd_colsum")
+        return dx
     C.check(C.lib.cgl_act_drop_bwd(_p(dy), _p(post), _p(drop), n, hw, c, float(slope), int(tanh_y), _p(dx), _s()),
             "cgl_act_drop_bwd")
     return dx
+
+
+def colsum_finalize(part, nch, c, out):
+    _chk(out)
+    C.check(C.lib.cgl_colsum_finalize(_p(part), int(nch), int(c), _p(out), _s()), "cgl_colsum_finalize")
+    return out
 
 
 def dropout2d_mask(mask, n, c, p, seed, counter):

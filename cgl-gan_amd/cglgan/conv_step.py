@@ -274,6 +274,8 @@ class ConvGanStep:
         # 128-row chunks: bitwise the channel reduction it saves; CGL_CONV_N1STATS=0 keeps that launch)
         self.n1_stats = (os.environ.get("CGL_CONV_N1STATS", "1") != "0" and "conv_blocks.6" in self.st_part and
                          B * 1024 % 128 == 0 and B * 1024 // 128 * 64 * 2 <= self.st_part["conv_blocks.6"].numel())
+        self.bpart = (torch.zeros(2 * (B * 1024 // 256), dtype=torch.float64, device=dev)
+                      if os.environ.get("CGL_CONV_BIASFUSE", "1") != "0" and B * 1024 % 256 == 0 and B <= 2048 else None)
         # sampler over a device-resident real shard [n, 1024] (DataLoader(shuffle=True), capgan.py:282)
         self.data = data
         self.short = data is not None and data.shape[0] % batch != 0    # some batch of a pass is short
@@ -530,14 +532,21 @@ class ConvGanStep:
 
     def _g_backward(self):
         P, G, B = self.G.params, self.G.grads, self.B
-        O.act_drop_bwd(self.dimg, self.x3[2 * B:], None, B, 1024, 1, self.dc3g, tanh_y=True)
+        # the Tanh backward also writes conv_blocks.8's bias-gradient partials (CGL_CONV_BIASFUSE; bitwise the
+        # weight gradient's column sum over dc3g, one channel-reduction launch fewer)
+        bf = self.bpart is not None
+        O.act_drop_bwd(self.dimg, self.x3[2 * B:], None, B, 1024, 1, self.dc3g, tanh_y=True,
+                       colsum=self.bpart if bf else None)
+        db8 = None if bf else G["conv_blocks.8.bias"]
         e6, e2 = self._elided("conv_blocks.6"), self._elided("conv_blocks.2")
         if e6:     # a2 = LeakyReLU(BN(y2)) applied in the operand loads
-            O.conv3x3_bwd_weight(self.dc3g, self.y2[B:], G["conv_blocks.8.weight"], G["conv_blocks.8.bias"], B, 32, 32,
+            O.conv3x3_bwd_weight(self.dc3g, self.y2[B:], G["conv_blocks.8.weight"], db8, B, 32, 32,
                                  64, 1, 1, 0, bn_in=(self.coef["conv_blocks.6"], 1, 2, O.ACT_LEAKY, SLOPE))
         else:
-            O.conv3x3_bwd_weight(self.dc3g, self.a2[B:], G["conv_blocks.8.weight"], G["conv_blocks.8.bias"], B, 32, 32,
+            O.conv3x3_bwd_weight(self.dc3g, self.a2[B:], G["conv_blocks.8.weight"], db8, B, 32, 32,
                                  64, 1, 1, 0)
+        if bf:
+            O.colsum_finalize(self.bpart, B * 1024 // 256, 1, G["conv_blocks.8.bias"])
         sm, si = self.g_save["conv_blocks.6"]
         pc6 = self._post_coef("conv_blocks.6")
         kw = dict(post=None if pc6 else self.a2[B:], post_coef=pc6, dgamma=G["conv_blocks.6.weight"],

@@ -2648,6 +2648,9 @@ struct CglEltArgs {
   float* out;
   const int* nv;             // mode 1, short first call: rows >= *nv * hw of group 0 are padding -> dX = 0
   const float* psc; int psc_ld;   // mode 1: LeakyReLU'(post) from the forward's scale / shift (CglChanArgs)
+  // cgl_eltwise1, C == 1, one element per thread: also the column-sum partials of the output per 256-row chunk
+  // (= block), {sum, 0} -- bitwise cgl_chan_reduce mode 2 with R = 256 over the stored output
+  double* colsum;
 };
 
 __global__ __launch_bounds__(256) void cgl_eltwise(CglEltArgs a) {
@@ -2755,6 +2758,7 @@ __global__ __launch_bounds__(256) void cgl_dense1_bwd_nhwc_k(const float* __rest
 // Scalar fallback of mode 2 / 3 for C % 4 != 0 (single-channel tensors: the generator image).
 __global__ __launch_bounds__(256) void cgl_eltwise1(CglEltArgs a) {
   const long n = (long)a.rows * a.C;
+  float ov = 0.f;
   for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
     const int r = (int)(e / a.C), c = (int)(e - (long)r * a.C);
     float o = gld(a.dY + e);
@@ -2766,6 +2770,19 @@ __global__ __launch_bounds__(256) void cgl_eltwise1(CglEltArgs a) {
       if (a.drop) o *= gld(a.drop + (long)(r / a.hw) * a.C + c);
     }
     gst(a.out + e, o);
+    ov = o;
+  }
+  if (a.colsum) {      // (uniform) the chunk's rows summed in row order, as cgl_chan_reduce's thread 0 does
+    __shared__ double s0[256];
+    const long e = (long)blockIdx.x * 256 + threadIdx.x;
+    s0[threadIdx.x] = e < n ? (double)ov : 0.0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (int q = 0; q < 256; ++q) t += s0[q];
+      a.colsum[(long)blockIdx.x * 2] = t;
+      a.colsum[(long)blockIdx.x * 2 + 1] = 0.0;
+    }
   }
 }
 
@@ -4390,6 +4407,34 @@ int cgl_act_drop_bwd(const float* dY, const float* post, const float* drop, int 
     hipLaunchKernelGGL(cgl_eltwise, dim3((unsigned)std::min<long>((tot / 4 + 255) / 256, 8192)), dim3(256), 0, s, e);
   else
     hipLaunchKernelGGL(cgl_eltwise1, dim3((unsigned)std::min<long>((tot + 255) / 256, 8192)), dim3(256), 0, s, e);
+  return (int)hipGetLastError();
+}
+
+int cgl_act_drop_bwd_colsum(const float* dY, const float* post, const float* drop, int n, int hw, int C, float slope,
+                            int tanh_y, float* dX, double* part, void* stream) {
+  const long tot = (long)n * hw * C;
+  if (!dY || !dX || !part || n < 1 || hw < 1 || C != 1 || tot > 8192L * 256 || ((uintptr_t)part & 15)) return CGL_E_ARG;
+  if (tanh_y && !post) return CGL_E_ARG;
+  CglEltArgs e;
+  std::memset(&e, 0, sizeof(e));
+  e.mode = tanh_y ? 3 : 2;
+  e.rows = n * hw; e.C = C; e.gr = n * hw; e.hw = hw; e.slope = slope;
+  e.dY = dY; e.out = dX;
+  if (tanh_y) e.X = post;
+  else e.post_out = post;
+  e.drop = drop;
+  e.colsum = part;
+  hipLaunchKernelGGL(cgl_eltwise1, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream, e);
+  return (int)hipGetLastError();
+}
+
+int cgl_colsum_finalize(const double* part, int nch, int C, float* out, void* stream) {
+  if (!part || !out || nch < 1 || C < 1) return CGL_E_ARG;
+  CglBnFinArgs f;
+  std::memset(&f, 0, sizeof(f));
+  f.part = part; f.C = C; f.groups = 1; f.chunks_per_group = nch; f.mode = 2; f.dgamma = out;
+  f.nocache = fin_nocache();
+  hipLaunchKernelGGL(cgl_bn_finalize, dim3(C), dim3(256), 0, (hipStream_t)stream, f);
   return (int)hipGetLastError();
 }
 

@@ -407,6 +407,13 @@ int cgl_bn2d_bwd(const float* dY, const float* post, const float* X, int n, int 
  * null), or with tanh_y != 0: dX = dY * (1 - post^2) (Tanh backward, post = the Tanh output). */
 int cgl_act_drop_bwd(const float* dY, const float* post, const float* drop, int n, int hw, int C, float slope,
                      int tanh_y, float* dX, void* stream);
+/* cgl_act_drop_bwd for a one-channel map (C == 1, n hw <= 2^21) that also writes the column-sum partials of dX
+ * per 256-row chunk, part[(n hw + 255) / 256][2] -- bitwise the chunks the bias-gradient column sum of
+ * cgl_conv3x3_bwd_weight computes from dX (G Conv2d(64, 1)'s bias, model/lsgan.py:19-20) -- and
+ * cgl_colsum_finalize sums them in chunk order into out[C] (that column sum's finalize). */
+int cgl_act_drop_bwd_colsum(const float* dY, const float* post, const float* drop, int n, int hw, int C, float slope,
+                            int tanh_y, float* dX, double* part, void* stream);
+int cgl_colsum_finalize(const double* part, int nch, int C, float* out, void* stream);
 /* nn.Dropout2d(p) scales per (image, channel): 1/(1-p) with probability 1-p, else 0
  * (Philox4x32-10, counter-based: (seed, counter) selects the stream). */
 int cgl_dropout2d_mask(float* mask, int n, int C, double p, unsigned long long seed, unsigned long long counter,
