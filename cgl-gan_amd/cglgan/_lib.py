@@ -29,7 +29,7 @@ EXPORTS = [
     "cgl_bn1d_bwd",
     # conv GAN path (model/lsgan.py)
     "cgl_conv3x3_workspace_bytes", "cgl_conv3x3_fwd", "cgl_conv3x3_bwd_data", "cgl_conv3x3_bwd_weight",
-    "cgl_conv3x3_bwd_weight_bnin",
+    "cgl_conv3x3_bwd_weight_bnin", "cgl_conv3x3_bwd_weight_actdrop",
     "cgl_bn2d_workspace_bytes", "cgl_bn2d_fwd", "cgl_bn2d_bwd", "cgl_act_drop_bwd", "cgl_act_drop_bwd_colsum", "cgl_colsum_finalize", "cgl_dropout2d_mask", "cgl_dropout2d_masks",
     "cgl_nchw_to_nhwc", "cgl_nhwc_to_nchw", "cgl_dense1_bwd_data_nhwc", "cgl_dense1_fwd_nhwc", "cgl_adv_loss", "cgl_adam_multi", "cgl_dense_workspace_bytes",
     "cgl_dense_fwd", "cgl_dense_bwd_data", "cgl_dense_bwd_weight", "cgl_gather_rows", "cgl_weights_scale",
@@ -128,6 +128,7 @@ def _load():
         "cgl_conv3x3_bwd_data": (ci, [vp, vp, vp] + [ci] * 7 + [vp, i64, vp]),
         "cgl_conv3x3_bwd_weight": (ci, [vp, vp, vp, vp] + [ci] * 7 + [vp, i64, vp]),
         "cgl_conv3x3_bwd_weight_bnin": (ci, [vp, vp, vp, vp] + [ci] * 7 + [vp, ci, ci, ci, cf, vp, i64, vp]),
+        "cgl_conv3x3_bwd_weight_actdrop": (ci, [vp, vp, vp, cf, vp, vp, vp] + [ci] * 7 + [vp, i64, vp]),
         "cgl_bn2d_workspace_bytes": (i64, [ci] * 4),
         "cgl_bn2d_fwd": (ci, [vp, ci, ci, ci, ci, vp, vp, cd, cd, vp, vp, ci, ci, cf, vp, vp, vp, vp, vp, i64, vp]),
         "cgl_bn2d_bwd": (ci, [vp, vp, vp, ci, ci, ci, ci, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, ci, vp, vp, i64,

@@ -191,12 +191,21 @@ def conv3x3_bwd_data(dy, w, dx, n, h, wd, cin, cout, stride=1, up=0, wp=None, st
     return dx
 
 
-def conv3x3_bwd_weight(dy, x, dw, db, n, h, wd, cin, cout, stride=1, up=0, bn_in=None):
+def conv3x3_bwd_weight(dy, x, dw, db, n, h, wd, cin, cout, stride=1, up=0, bn_in=None, act_drop=None):
     """``bn_in`` = (coef, group, groups, act, slope): ``x`` is the PRE-BatchNorm map of forward call ``group``
     (-1: ``groups`` stacked calls of n / groups images); the BatchNorm (+ LeakyReLU) is applied in the operand
-    loads (cgl_conv3x3_bwd_weight_bnin)."""
+    loads (cgl_conv3x3_bwd_weight_bnin).  ``act_drop`` = (post, drop, slope), cin == 1 only: ``dy`` is the
+    gradient at the block's output, the LeakyReLU + Dropout2d backward applied per loaded value
+    (cgl_conv3x3_bwd_weight_actdrop, bitwise act_drop_bwd + this)."""
     _chk(dy, x, dw, db)
     ws = workspace(conv_ws_bytes(n, h, wd, cin, cout, stride, up), dy.device)
+    if act_drop is not None:
+        post, drop, slope = act_drop
+        _chk(post, drop)
+        C.check(C.lib.cgl_conv3x3_bwd_weight_actdrop(_p(dy), _p(post), _p(drop), float(slope), _p(x), _p(dw), _p(db),
+                                                     n, h, wd, cin, cout, stride, up, _p(ws), ws.numel(), _s()),
+                "cgl_conv3x3_bwd_weight_actdrop")
+        return dw
     if bn_in is not None:
         coef, group, groups, act, slope = bn_in
         _chk(coef)

@@ -274,6 +274,9 @@ class ConvGanStep:
         # 128-row chunks: bitwise the channel reduction it saves; CGL_CONV_N1STATS=0 keeps that launch)
         self.n1_stats = (os.environ.get("CGL_CONV_N1STATS", "1") != "0" and "conv_blocks.6" in self.st_part and
                          B * 1024 % 128 == 0 and B * 1024 // 128 * 64 * 2 <= self.st_part["conv_blocks.6"].numel())
+        # D's Conv2d(1, 16) weight gradient applies its block's LeakyReLU + Dropout2d backward in its loads in the D
+        # step (cgl_conv3x3_bwd_weight_actdrop; bitwise, one launch fewer; CGL_CONV_C1FUSE=0 keeps act_drop_bwd)
+        self.c1_fuse = os.environ.get("CGL_CONV_C1FUSE", "1") != "0"
         self.bpart = (torch.zeros(2 * (B * 1024 // 256), dtype=torch.float64, device=dev)
                       if os.environ.get("CGL_CONV_BIASFUSE", "1") != "0" and B * 1024 % 256 == 0 and B <= 2048 else None)
         # sampler over a device-resident real shard [n, 1024] (DataLoader(shuffle=True), capgan.py:282)
@@ -498,6 +501,7 @@ class ConvGanStep:
         O.dense1_bwd_data_nhwc(self.dv, P["adv_layer.weight"], self.dr[3], n, 128, 4)
         if wgrad:
             O.dense_bwd_weight(self.dv, self.flat, G["adv_layer.weight"], G["adv_layer.bias"], n, 512, 1)
+        c1f = False
         for k in (3, 2, 1, 0):
             ck, bk, ci, co, hw = D_CONVS[k]
             ho = hw // 2
@@ -510,11 +514,14 @@ class ConvGanStep:
                                      self.dc[k], **kw)
                 else:
                     O.bn2d_bwd(self.dr[k], self.q[k], n, ho * ho, co, sm, si, P[bk + ".weight"], self.dc[k], **kw)
-            else:
+            elif not (c1f := wgrad and dx is None and self.c1_fuse):
                 O.act_drop_bwd(self.dq1, self.q[0], masks[0], n, ho * ho, co, self.dc[0], slope=SLOPE)
             inp = x if k == 0 else (self.q[0] if k == 1 else self.r[k - 1])
             pfold = k > 1 and D_CONVS[k - 1][1] in self._d_folded
-            if wgrad and pfold:     # r[k - 1] = BN(q[k - 1]) applied in the operand loads (both calls of the step)
+            if k == 0 and not bk and c1f:   # dc[0] only feeds this weight gradient: its act / drop backward in the loads
+                O.conv3x3_bwd_weight(self.dq1, inp, G[ck + ".weight"], G[ck + ".bias"], n, hw, hw, ci, co, 2, 0,
+                                     act_drop=(self.q[0], masks[0], SLOPE))
+            elif wgrad and pfold:     # r[k - 1] = BN(q[k - 1]) applied in the operand loads (both calls of the step)
                 O.conv3x3_bwd_weight(self.dc[k], self.q[k - 1], G[ck + ".weight"], G[ck + ".bias"], n, hw, hw, ci, co,
                                      2, 0, bn_in=(self.dcoef[D_CONVS[k - 1][1]], -1, groups, O.ACT_NONE, SLOPE))
             elif wgrad:

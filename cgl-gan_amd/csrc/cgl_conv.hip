@@ -1721,6 +1721,9 @@ struct CglC1Args {
   const float* dY; float* part; float* dW; float* db;
   int n, h, w, ho, wo, cout, stride, act, nblk, chunk;
   float slope;
+  // weight gradient only: dY is the gradient at the block's OUTPUT -- the LeakyReLU (post = its output) and
+  // Dropout2d (drop [n][cout]) backward are applied per loaded value in cgl_act_drop_bwd's order (bitwise)
+  const float* post;
 };
 
 __global__ __launch_bounds__(256) void cgl_conv_c1_fwd(CglC1Args a) {
@@ -1779,7 +1782,10 @@ __global__ __launch_bounds__(256) void cgl_conv_c1_wgrad(CglC1Args a) {
     for (int u = 0; u < CGL_C1_PPT; ++u) {
       const long p = min(pb + (long)u * lanes, p1 - 1);
       const int img = (int)(p / hw), r = (int)(p - (long)img * hw), oy = r / a.wo, ox = r - oy * a.wo;
-      dy[u] = pb + (long)u * lanes < p1 ? gld(a.dY + p * cout + co) : 0.f;
+      float d = gld(a.dY + p * cout + co);
+      if (a.post) d = gld(a.post + p * cout + co) > 0.f ? d : d * a.slope;
+      if (a.drop) d *= gld(a.drop + (long)img * cout + co);
+      dy[u] = pb + (long)u * lanes < p1 ? d : 0.f;
       const float* xi = a.X + (long)img * a.h * a.w;
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
@@ -3727,7 +3733,8 @@ int wgrad_lds_wm(const WgradPlan& pl, bool bias_col, const float* dY, const floa
 // bi (may be null): X is the PRE-BatchNorm map of one forward call, applied in the operand loads -- only the
 // LDS-staged MFMA weight gradient and the input-stationary one-output-channel one take it (CGL_E_ARG otherwise)
 int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, float* dW, float* db, void* ws,
-                         int64_t wsb, hipStream_t s, const BnIn* bi = nullptr) {
+                         int64_t wsb, hipStream_t s, const BnIn* bi = nullptr, const float* ad_post = nullptr,
+                         const float* ad_drop = nullptr, float ad_slope = 0.f) {
   if (!dY || !X || !dW || !ws || !al16(ws)) return CGL_E_ARG;
   if (wsb < conv_ws_bytes(g)) return CGL_E_SIZE;
   if (bi && (!bi->coef || !al16(bi->coef) || bi->g0 < 0 || bi->g0 >= bi->groups || g.cin % 4)) return CGL_E_ARG;
@@ -3738,6 +3745,7 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
     CglC1Args a;
     std::memset(&a, 0, sizeof(a));
     a.X = X; a.dY = dY; a.dW = dW; a.db = db;
+    a.post = ad_post; a.drop = ad_drop; a.slope = ad_slope;
     a.n = g.n; a.h = g.h; a.w = g.w; a.ho = g.ho; a.wo = g.wo; a.cout = g.cout; a.stride = g.stride;
     a.chunk = 128;
     a.nblk = (int)((npix + a.chunk - 1) / a.chunk);
@@ -3926,6 +3934,16 @@ int cgl_conv3x3_bwd_weight(const float* dY, const float* X, float* dW, float* db
   const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
   if (rc) return rc;
   return conv_bwd_weight_impl(g, dY, X, dW, db, ws, wsb, (hipStream_t)stream);
+}
+
+int cgl_conv3x3_bwd_weight_actdrop(const float* dY, const float* post, const float* drop, float slope, const float* X,
+                                   float* dW, float* db, int n, int h, int w, int cin, int cout, int stride, int up,
+                                   void* ws, int64_t wsb, void* stream) {
+  ConvGeom g;
+  const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
+  if (rc) return rc;
+  if (!c1_ok(g)) return CGL_E_ARG;     // the one-input-channel weight gradient only
+  return conv_bwd_weight_impl(g, dY, X, dW, db, ws, wsb, (hipStream_t)stream, nullptr, post, drop, slope);
 }
 
 int cgl_conv3x3_bwd_weight_bnin(const float* dY, const float* X, float* dW, float* db, int n, int h, int w, int cin,

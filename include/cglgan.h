@@ -258,6 +258,13 @@ int cgl_conv3x3_bwd_weight(const float* dY, const float* X, float* dW, float* db
  * and fake calls; at most 2, the wave-unit MFMA weight gradient only).  Supported by the LDS-staged MFMA kernel
  * (the G up-convolutions of model/lsgan.py:11,15), the input-stationary Conv2d(64, 1) of :19 (one call) and
  * the wave-unit MFMA weight gradient (the D convolutions of :78); CGL_E_ARG elsewhere. */
+/* The weight gradient of a one-input-channel conv (the discriminator's Conv2d(1, 16, 3, 2, 1), model/lsgan.py:78)
+ * from the gradient at its block's OUTPUT: the LeakyReLU (post = its output) and Dropout2d (drop [n][cout], may be
+ * null) backward applied per loaded value, bitwise cgl_act_drop_bwd + cgl_conv3x3_bwd_weight.  Other geometries:
+ * CGL_E_ARG. */
+int cgl_conv3x3_bwd_weight_actdrop(const float* dY, const float* post, const float* drop, float slope, const float* X,
+                                   float* dW, float* db, int n, int h, int w, int cin, int cout, int stride, int up,
+                                   void* workspace, int64_t ws_bytes, void* stream);
 int cgl_conv3x3_bwd_weight_bnin(const float* dY, const float* X, float* dW, float* db, int n, int h, int w, int cin,
                                 int cout, int stride, int up, const float* in_coef, int in_groups, int in_group,
                                 int in_act, float in_slope, void* workspace, int64_t ws_bytes, void* stream);

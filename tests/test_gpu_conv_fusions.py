@@ -12,6 +12,8 @@
     (cgl_conv3x3_bwd_data_stats, 128-row chunks) instead of a channel reduction over the stored gradient;
   * CGL_CONV_BIASFUSE: conv_blocks.8's bias-gradient partials written by the Tanh backward (cgl_act_drop_bwd_colsum)
     instead of the weight gradient's column sum over the stored gradient;
+  * CGL_CONV_C1FUSE: D's Conv2d(1, 16) weight gradient in the D step applies its block's LeakyReLU + Dropout2d
+    backward in its loads (cgl_conv3x3_bwd_weight_actdrop) instead of after an act_drop_bwd pass;
   * CGL_CONV_ELIDE: a folded G BatchNorm's activation (a1 / a2) is not stored at all -- the G backward's weight
     gradients apply the BatchNorm in their operand loads (cgl_conv3x3_bwd_weight_bnin) and every LeakyReLU'
     comes from the kept scale / shift (with the same fold mask on both sides)."""
@@ -46,7 +48,8 @@ CASES = [("CGL_CONV_POSTCOEF", 8, False, "2"), ("CGL_CONV_POSTCOEF", 256, False,
          ("CGL_CONV_ELIDE", 8, False, "3"), ("CGL_CONV_ELIDE", 256, False, "3"), ("CGL_CONV_ELIDE", 256, True, "3"),
          ("CGL_CONV_ELIDE", 256, True, "2"), ("CGL_CONV_N1STATS", 8, False, "3"),
          ("CGL_CONV_N1STATS", 256, True, "3"), ("CGL_CONV_N1STATS", 256, False, "0"),
-         ("CGL_CONV_BIASFUSE", 8, False, "3"), ("CGL_CONV_BIASFUSE", 256, True, "3")]
+         ("CGL_CONV_BIASFUSE", 8, False, "3"), ("CGL_CONV_BIASFUSE", 256, True, "3"),
+         ("CGL_CONV_C1FUSE", 8, False, "3"), ("CGL_CONV_C1FUSE", 256, True, "3")]
 
 
 @pytest.mark.parametrize("var,B,graph,fold", CASES)
@@ -71,6 +74,8 @@ def test_conv_round_fusion_bitwise(var, B, graph, fold):
         assert a.n1_stats and not b.n1_stats
     elif var == "CGL_CONV_BIASFUSE":
         assert a.bpart is not None and b.bpart is None
+    elif var == "CGL_CONV_C1FUSE":
+        assert a.c1_fuse and not b.c1_fuse
     elif var == "CGL_CONV_DFOLD_STEP":
         assert a.d_fold_step and not b.d_fold_step and a._d_folded and not b._d_folded
     else:
