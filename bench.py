@@ -16,6 +16,9 @@ Workload (BASELINE.json configs[1] at N=1, configs[2] at N>1):
     round all_gather(G losses) -> lambda-weighting -> all_reduce(sum) of the weighted G-output
     gradient -> replicated G update, plus the E-share all_reduce(avg) of D every --E rounds (RCCL).
 A "step" is one round; value = images/s over all ranks = N * 256 * K / max-over-ranks time.
+At N = 1 the line also carries "conv_round": the model/lsgan.py conv GAN round (B=256) timed in its own
+graph-replayed region (--conv-steps rounds, default 60) with its own conv-family roofline -- a second,
+labelled workload of the same run, never part of `value`.
 """
 import argparse
 import json
@@ -63,6 +66,10 @@ def args_():
                         "rounds, bs512, fp32); ring: configs[0], the CGLGAN 2-D Gaussian-mixture round (B=64); "
                         "lsgan: the model/lsgan.py conv GAN round (32x32, MSE/LSGAN loss)")
     p.add_argument("--loss", choices=["mse", "bce"], default="mse", help="conv GAN objective (--model lsgan)")
+    p.add_argument("--conv-steps", type=int, default=60,
+                   help="--model mlp at N = 1: also time this many graph-replayed conv GAN rounds (model/lsgan.py, "
+                        "same batch) and report them as 'conv_round' beside the line (0: skip)")
+    p.add_argument("--conv-warmup", type=int, default=5)
     p.add_argument("--lowp", choices=["none", "f16", "bf16"], default="f16",
                    help="--model mdgan: also time the same round with 16-bit GEMM operands (BASELINE configs[4]'s "
                         "fp16) and report it beside the fp32 line as 'lowp_variant' (parity unpinned)")
@@ -370,7 +377,10 @@ def conv_traffic():
             "traffic_algorithmic": p["algorithmic_bytes"], "traffic_ratio": round(p["ratio"], 2)}
 
 
-def main_lsgan(a, world, rank, local):
+def conv_round_measure(a, world, rank, steps, warmup, with_cpu):
+    """The model/lsgan.py conv GAN round: W untimed + K timed graph-replayed rounds (barrier + synchronize on
+    both sides, max over ranks), then one eager round with every conv op bracketed by HIP events for the
+    conv-family roofline.  Returns (line, ms_step) on rank 0, (None, ms_step) elsewhere."""
     from cglgan.conv_step import ConvGanStep
     from cglgan.exchange import ConvWorkerExchange, DistComm
     stream = torch.cuda.Stream()
@@ -387,14 +397,14 @@ def main_lsgan(a, world, rank, local):
         ex = ConvWorkerExchange(step, DistComm() if world > 1 else None, share_every=a.E if world > 1 else 0)
         torch.cuda.synchronize()
         r = 0
-        for _ in range(a.warmup):
+        for _ in range(warmup):
             ex.round(r)
             r += 1
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
-        for _ in range(a.steps):
+        for _ in range(steps):
             ex.round(r)
             r += 1
         torch.cuda.synchronize()
@@ -408,19 +418,18 @@ def main_lsgan(a, world, rank, local):
         st = step.stats()
         # per-op timing needs the ops issued one by one: an eager round (same device round state)
         ops = profile_conv_round(lambda: step.run(eager=True) if world == 1 else ex.round(r, eager=True))
-    ms_step = el / a.steps * 1e3
-    value = world * a.batch * a.steps / el
+    ms_step = el / steps * 1e3
+    value = world * a.batch * steps / el
     if rank != 0:
-        return None
-    mma = [o for o in ops]
-    mma_us = sum(o["us"] for o in mma)
-    exe = sum(o["exec_flops"] for o in mma)
-    ref = sum(o["ref_flops"] for o in mma)
+        return None, ms_step
+    mma_us = sum(o["us"] for o in ops)
+    exe = sum(o["exec_flops"] for o in ops)
+    ref = sum(o["ref_flops"] for o in ops)
     tf = exe / (mma_us * 1e-6) / 1e12
-    dom = max(mma, key=lambda o: o["us"])
+    dom = max(ops, key=lambda o: o["us"])
     out = {
         "metric": METRIC + " [conv GAN model/lsgan.py variant]", "value": round(value, 1), "unit": "images/s",
-        "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 4),
+        "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": round(ms_step, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": f"model/lsgan.py conv GAN, CAPGAN worker round (G fwd x2, D step, G loss, G bwd, "
                                f"Adam G/D), {a.loss} objective, 32x32x1, 1 worker per GPU"
@@ -432,6 +441,8 @@ def main_lsgan(a, world, rank, local):
         "roofline": {"bound": "mfma", "kernel": "cgl_conv_fwd + cgl_conv_wgrad (+ pack / reduce), every conv op of "
                                                 "one round", "achieved": round(tf, 3), "peak": PEAK_F32_MFMA,
                      "unit": "TFLOP/s", "frac": round(tf / PEAK_F32_MFMA, 4), **conv_traffic(),
+                     "timing": "per conv op: HIP events on the launch stream around the op in one eager round "
+                               "(pack + MFMA kernel, + fixed-order reduction for weight gradients)",
                      "conv_exec_gflop_per_round": round(exe / 1e9, 3),
                      "conv_ref_gflop_per_round": round(ref / 1e9, 3),
                      "conv_us_per_round": round(mma_us, 1),
@@ -443,9 +454,29 @@ def main_lsgan(a, world, rank, local):
                               "tflops": round(o["exec_flops"] / (o["us"] * 1e-6) / 1e12, 2)} for o in ops]},
         "losses": {"d_loss": st["d_loss"], "g_loss": st["g_loss"], "round": st["round"]},
     }
-    if world == 1 and not a.no_cpu_baseline:
+    if with_cpu and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_variants(lambda t: conv_cpu_baseline(a, t))
-    print(json.dumps(out), flush=True)
+    return out, ms_step
+
+
+def main_lsgan(a, world, rank, local):
+    out, _ = conv_round_measure(a, world, rank, a.steps, a.warmup, with_cpu=True)
+    if out is not None:
+        print(json.dumps(out), flush=True)
+    return out
+
+
+def conv_extra(a, world, rank):
+    """The conv GAN round (model/lsgan.py) timed beside the default C2 line at N = 1: its own graph-replayed
+    timed region (--conv-steps rounds, default >= 50), its own conv-family roofline, no CPU leg (the conv
+    oracle runs ~300 images/s; `bench.py --model lsgan` reports it).  A labelled extra key, never `value`."""
+    if world != 1 or a.conv_steps <= 0:
+        return None
+    out, _ = conv_round_measure(a, world, rank, a.conv_steps, a.conv_warmup, with_cpu=False)
+    if out is None:
+        return None
+    out["note"] = ("second workload of the same bench run (model/lsgan.py conv GAN, B=%d), timed in its own "
+                   "region after the C2 line's; not part of `value`" % a.batch)
     return out
 
 
@@ -594,6 +625,9 @@ def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None,
     offset = ((ms_step * 1e3 - eager_us) / nl) if (world == 1 and not a.eager and nl > 0) else 0.0
     gemm_s = (sum(gemm_us) + offset * gemm_n) * 1e-6
     gemm_tf = gemm_flops / gemm_s / 1e12 if gemm_s > 0 else 0.0
+    # the unmodelled figure beside it: the raw in-round eager GEMM durations, no offset
+    gemm_raw_s = sum(gemm_us) * 1e-6
+    gemm_raw_tf = gemm_flops / gemm_raw_s / 1e12 if gemm_raw_s > 0 else 0.0
     step_flops = plan["gemm_flops"]
     step_tf = step_flops / (ms_step * 1e-3) / 1e12
     cfg = {"workload": workload, "global_batch": a.batch * world, "batch_per_worker": a.batch,
@@ -616,6 +650,9 @@ def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None,
                                 f"median over {a.profile_rounds} rounds of each launch's in-round device duration "
                                 "(dispatch begin / end events on the launch stream, cgl_gan_profile)"),
                      "timed_offset_us": round(offset, 3),
+                     "achieved_eager_raw": round(gemm_raw_tf, 3),
+                     "frac_eager_raw": round(gemm_raw_tf / PEAK_F32_MFMA, 4),
+                     "eager_raw_note": "GEMM FLOPs / the summed raw in-round eager GEMM durations (no offset model)",
                      "traffic": traffic_per_gemm_launch()[0] if a.model == "mlp" else None,
                      "traffic_unit": "bytes per GEMM launch, all cgl_gemm_f32 instantiations (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                      "traffic_source": traffic_per_gemm_launch()[1] if a.model == "mlp" else None,
@@ -650,12 +687,14 @@ def main_mlp(a, world, rank):
         step, _ = build_step(a, rank, world)
         ex = make_exchange(step, world, a)
         el = timed_rounds(lambda r: ex.round(r, graph=not a.eager), a, world)
+        conv = conv_extra(a, world, rank)
         wl = ("C2: model/mnist_model.py MLP GAN, CAPGAN worker round (G fwd x2, D step, G loss, G bwd, Adam G/D), "
               "1 worker per GPU" if world == 1 else
               f"C3: CAPGAN {world} workers (1 per GPU), S=1, lambda-weighted G-gradient all-reduce + E={a.E} D "
               f"all-reduce over RCCL")
         return fused_report(a, world, rank, step, el, wl, {"img": "28x28x1", "dataset_rows_per_worker": a.rows},
-                            cpu_leg=lambda: cpu_variants(lambda t: cpu_baseline(a, t)), parity_kind="capgan", ex=ex)
+                            cpu_leg=lambda: cpu_variants(lambda t: cpu_baseline(a, t)), parity_kind="capgan", ex=ex,
+                            extra={"conv_round": conv} if conv else None)
 
 
 def main_driver(a, world, rank, algo):

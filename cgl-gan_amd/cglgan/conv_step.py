@@ -271,9 +271,13 @@ class ConvGanStep:
             nb = O.stat_chunks(n, h, h, ci, co, st, up, grp, bwd=True)
             self.bst_ok[key] = key in self.st_part and 0 < nb * ci * 2 <= self.st_part[key].numel()
         # conv_blocks.6's backward partials from the Conv2d(64, 1) input gradient itself (cgl_conv3x3_bwd_data_stats,
-        # 128-row chunks: bitwise the channel reduction it saves; CGL_CONV_N1STATS=0 keeps that launch)
+        # 128-row chunks: bitwise the channel reduction it saves; CGL_CONV_N1STATS=0 keeps that launch).  Only where
+        # that reduction itself uses 128-row chunks (the library's chan_chunk halves them below CGL_CHAN_MINCH = 64
+        # chunks per call, i.e. B < 8), so both paths stay bitwise equal at every batch
+        minch = int(os.environ.get("CGL_CHAN_MINCH", "64"))
         self.n1_stats = (os.environ.get("CGL_CONV_N1STATS", "1") != "0" and "conv_blocks.6" in self.st_part and
-                         B * 1024 % 128 == 0 and B * 1024 // 128 * 64 * 2 <= self.st_part["conv_blocks.6"].numel())
+                         B * 1024 % 128 == 0 and B * 1024 // 128 >= minch and
+                         B * 1024 // 128 * 64 * 2 <= self.st_part["conv_blocks.6"].numel())
         # D's Conv2d(1, 16) weight gradient applies its block's LeakyReLU + Dropout2d backward in its loads in the D
         # step (cgl_conv3x3_bwd_weight_actdrop; bitwise, one launch fewer; CGL_CONV_C1FUSE=0 keeps act_drop_bwd)
         self.c1_fuse = os.environ.get("CGL_CONV_C1FUSE", "1") != "0"

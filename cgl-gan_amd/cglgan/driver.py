@@ -268,9 +268,13 @@ class Driver:
         self.lambda_list = []
         self.round = 0
         if cfg.resume_dir:
+            err = None
             if os.path.exists(self.resume_path()):
-                self.load_resume()
-            self._check_resumed_round()
+                try:
+                    self.load_resume()
+                except Exception as e:        # raised on every rank together below, not here alone
+                    err = e
+            self._check_resumed_round(err)
 
     def run(self, rounds: int = None, log=print):
         """``rounds`` communication rounds (default: num_communication), as Server.run's
@@ -303,7 +307,9 @@ class Driver:
         return os.path.join(self.cfg.resume_dir, f"resume-{self.cfg.algo}-rank{self.rank}.pt")
 
     # every knob that changes the trajectory or the schedule of a run: a file saved under other settings
-    # is refused instead of continuing a different run
+    # is refused instead of continuing a different run.  num_communication is one of them on purpose: the
+    # Mix-G Cloud schedule (mixg_cloud_due) and the CAPGAN S > 1 schedule are cut from it, so a resumed run
+    # with a larger round budget would not continue the run that was saved -- extending a run is refused.
     RESUME_KEYS = ("algo", "num_workers", "num_servers", "epoch", "batch_size", "num_communication", "cloud_epoch",
                    "segema", "iid", "num_class", "num_sample", "b1", "b2", "lr_g", "lr_d", "seed", "img_size",
                    "weighting", "share_every", "swap_every", "fedavg_compat_noop", "dataset_rows", "data_seed",
@@ -342,16 +348,25 @@ class Driver:
         if ds is not None:
             ds.rd.setstate((int(saved[0]), tuple(int(x) for x in saved[1]), saved[2]))
 
-    def _check_resumed_round(self):
+    def _check_resumed_round(self, err=None):
         """Every rank must continue from the same round (a crash between two ranks' file replacements
         leaves files of different rounds; the collectives would then pair different rounds or hang):
-        min and max of the resumed round over the world must agree."""
+        min and max of the resumed round over the world must agree.  A rank whose own load failed
+        (``err``) joins the same all-reduce with its error flag raised, so every rank raises together
+        instead of the others waiting in a collective until the process-group timeout."""
         if self.world == 1 or not (dist.is_available() and dist.is_initialized()):
+            if err is not None:
+                raise err
             return
         dev = self.step.g_params.device if dist.get_backend() == "nccl" else torch.device("cpu")
-        t = torch.tensor([self.round, -self.round], dtype=torch.int64, device=dev)
+        t = torch.tensor([1 if err is not None else 0, self.round, -self.round], dtype=torch.int64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        hi, lo = int(t[0]), -int(t[1])
+        bad, hi, lo = int(t[0]), int(t[1]), -int(t[2])
+        if err is not None:
+            raise err
+        if bad:
+            raise RuntimeError(f"rank {self.rank}: another rank failed to load its resume file in "
+                               f"{self.cfg.resume_dir}")
         if hi != lo:
             raise RuntimeError(f"rank {self.rank}: resume files of different rounds across the world "
                                f"(min {lo}, max {hi}) in {self.cfg.resume_dir}")

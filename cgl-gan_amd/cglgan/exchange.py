@@ -193,6 +193,8 @@ class WorkerExchange:
             self.cloud.all_reduce_mean(t, self.cloud_weights)
             if own is not None:     # segema * self_p + (1 - segema) * recv_p, in that order
                 torch.add(own * self.segema, t * (1.0 - self.segema), out=t)
+        if hasattr(self.step, "sync_params"):
+            self.step.sync_params()     # G's parameters changed outside the round: refresh its packed copies
 
 
 def mixg_cloud_due(num_communication: int, cloud_epoch: int):
@@ -284,6 +286,9 @@ def local_cloud_average(steps, weights, cloud_scope: str = "trunk", segema: floa
                 torch.add(t * segema, tot * (1.0 - segema), out=t)
             else:
                 t.copy_(tot)
+    for s in steps:
+        if hasattr(s, "sync_params"):
+            s.sync_params()
 
 
 class ConvWorkerExchange:

@@ -122,6 +122,7 @@ class GanStep:
         h = ctypes.c_void_p()
         C.check(C.lib.cgl_gan_create(ctypes.byref(cfg), ctypes.byref(bufs), ctypes.byref(h)), "cgl_gan_create")
         self._h = h
+        self._pk_ver = -1          # the packed G weight copies: refreshed before the first round (sync_params)
         self.g_views = self._views(g, C.MODEL_G, self.g_params)
         self.d_views = self._views(d, C.MODEL_D, self.d_params)
         self.g_grad_views = self._views(g, C.MODEL_G, self.g_grads)
@@ -182,6 +183,7 @@ class GanStep:
         b = beta if beta is not None else [1.0 / self.n_workers] * self.n_workers
         arr = (ctypes.c_float * len(b))(*[float(x) for x in b])
         C.check(C.lib.cgl_gan_reset(self._h, arr, _stream()), "cgl_gan_reset")
+        self._pk_ver = self.g_params._version        # (reset re-packs G's weights)
         for k, v in self.running.items():
             v.fill_(0.0 if k.endswith("running_mean") else 1.0)
 
@@ -251,7 +253,21 @@ class GanStep:
         torch.cuda.current_stream().synchronize()
 
     # ------------------------------------------------------------------ execution
+    def sync_params(self):
+        """Refresh the fragment-packed copies of G's weight matrices that its GEMMs read (cgl_gan_sync_params):
+        the G Adam launch keeps them current, so this is needed only after G's parameters were written from
+        outside the round (state-dict loads, init, the Cloud FedAvg).  Stream-ordered, no host sync."""
+        C.check(C.lib.cgl_gan_sync_params(self._h, _stream()), "cgl_gan_sync_params")
+        self._pk_ver = self.g_params._version
+
+    def _packed_current(self):
+        # any in-place torch write of G's parameters (through g_params or one of its views) moves the buffer's
+        # version counter; the library's own kernel writes do not, and they keep the packed copies current
+        if self.g_params._version != self._pk_ver:
+            self.sync_params()
+
     def run(self, phase=C.PHASE_ALL, graph=False):
+        self._packed_current()
         fn = C.lib.cgl_gan_run_graph if graph else C.lib.cgl_gan_run
         C.check(fn(self._h, phase, _stream()), "cgl_gan_run")
 
@@ -314,6 +330,7 @@ class GanStep:
         return out
 
     def launch_one(self, idx, phase=C.PHASE_ALL):
+        self._packed_current()
         C.check(C.lib.cgl_gan_launch_one(self._h, phase, idx, _stream()), "cgl_gan_launch_one")
 
     def profile_round(self, phase=C.PHASE_ALL):
@@ -321,6 +338,7 @@ class GanStep:
         [device microseconds of launch i] in plan order, measured in the round's own data state (each
         launch's inputs were just written by its producer, as in a replayed round).  Advances the training
         state like ``run``."""
+        self._packed_current()
         n = C.lib.cgl_gan_launch_count(self._h, phase)
         buf = (ctypes.c_float * max(n, 1))()
         C.check(C.lib.cgl_gan_profile(self._h, phase, _stream(), buf, n), "cgl_gan_profile")

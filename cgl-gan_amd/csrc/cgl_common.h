@@ -3,6 +3,15 @@
 // cgl_conv.hip + cgl_eval.hip).  Included by cgl_internal.h.
 #pragma once
 
+// Launch batching (cgl_conv_batch_begin / _end, cgl_conv.hip): while the calling thread has a batch open,
+// only the batchable entry points may be called (they record instead of launching); every other entry point
+// that would launch or synchronise returns CGL_E_STATE instead of running ahead of the deferred launches.
+bool cgl_launch_batch_open();
+#define CGL_BATCH_GUARD()                             \
+  do {                                                \
+    if (cgl_launch_batch_open()) return CGL_E_STATE;  \
+  } while (0)
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef CGL_GLOBAL unsigned int cgl_gu32;
 typedef CGL_GLOBAL unsigned long long cgl_gu64;

@@ -137,7 +137,8 @@ __device__ __forceinline__ int cgl_xcd_tile(int local, int nwg) {
 // FAST: Cin % 16 == 0, so a 16-k chunk lies inside one tap (uniform tap, 2 x 16-byte loads per
 // lane and block).  Otherwise each k is decoded per element (tiny-K layers: Cin = 1).
 // The folded BatchNorm's activation slope: LeakyReLU(w) = max(w, w * slope) -- bitwise cgl_eltwise's
-// (w > 0 ? w : w * slope) for 0 <= slope <= 1 (the entry points require it), two VALU ops instead of three;
+// (w > 0 ? w : w * slope) for 0 < slope <= 1 (the entry points require it: at slope 0 the select turns
+// w = -inf into -inf * 0 = NaN where the max form gives -inf), two VALU ops instead of three;
 // act none = slope 1 (max(w, w) = w), so the staging loops carry no activation branch.
 __device__ __forceinline__ float cgl_bnin_slope(CglKL L) {
   return L->in_act == CGL_EPI_ACT_LEAKY ? L->in_slope : 1.f;
@@ -3442,7 +3443,7 @@ int launch_conv_mma(CglConvProb* P, int np, const float* bias, int act, float sl
     L.in_gimg = bi->gimg;
     L.in_act = bi->act;
     L.in_slope = bi->slope;
-    if (bi->act == CGL_EPI_ACT_LEAKY && !(bi->slope >= 0.f && bi->slope <= 1.f)) return CGL_E_ARG;   // (max form)
+    if (bi->act == CGL_EPI_ACT_LEAKY && !(bi->slope > 0.f && bi->slope <= 1.f)) return CGL_E_ARG;   // (max form)
   }
   L.slope = slope;
   L.drop = drop;
@@ -3770,7 +3771,7 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
     L.in_gimg = bi->gimg;
     L.in_act = bi->act;
     L.in_slope = bi->slope;
-    if (bi->act == CGL_EPI_ACT_LEAKY && !(bi->slope >= 0.f && bi->slope <= 1.f)) return CGL_E_ARG;   // (max form)
+    if (bi->act == CGL_EPI_ACT_LEAKY && !(bi->slope > 0.f && bi->slope <= 1.f)) return CGL_E_ARG;   // (max form)
     L.in_g0 = bi->g0;
   }
   float* part = (float*)ws;
@@ -3914,6 +3915,7 @@ int64_t cgl_conv3x3_workspace_bytes(int n, int h, int w, int cin, int cout, int 
 int cgl_conv3x3_fwd(const float* X, const float* W, const float* bias, float* Y, int n, int h, int w, int cin,
                     int cout, int stride, int up, int act, float slope, const float* drop, void* ws, int64_t wsb,
                     void* stream) {
+  CGL_BATCH_GUARD();
   ConvGeom g;
   const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
   if (rc) return rc;
@@ -3922,6 +3924,7 @@ int cgl_conv3x3_fwd(const float* X, const float* W, const float* bias, float* Y,
 
 int cgl_conv3x3_bwd_data(const float* dY, const float* W, float* dX, int n, int h, int w, int cin, int cout,
                          int stride, int up, void* ws, int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   ConvGeom g;
   const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
   if (rc) return rc;
@@ -3930,6 +3933,7 @@ int cgl_conv3x3_bwd_data(const float* dY, const float* W, float* dX, int n, int 
 
 int cgl_conv3x3_bwd_weight(const float* dY, const float* X, float* dW, float* db, int n, int h, int w, int cin,
                            int cout, int stride, int up, void* ws, int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   ConvGeom g;
   const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
   if (rc) return rc;
@@ -3939,6 +3943,7 @@ int cgl_conv3x3_bwd_weight(const float* dY, const float* X, float* dW, float* db
 int cgl_conv3x3_bwd_weight_actdrop(const float* dY, const float* post, const float* drop, float slope, const float* X,
                                    float* dW, float* db, int n, int h, int w, int cin, int cout, int stride, int up,
                                    void* ws, int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   ConvGeom g;
   const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
   if (rc) return rc;
@@ -3949,6 +3954,7 @@ int cgl_conv3x3_bwd_weight_actdrop(const float* dY, const float* post, const flo
 int cgl_conv3x3_bwd_weight_bnin(const float* dY, const float* X, float* dW, float* db, int n, int h, int w, int cin,
                                 int cout, int stride, int up, const float* in_coef, int in_groups, int in_group,
                                 int in_act, float in_slope, void* ws, int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   ConvGeom g;
   const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
   if (rc) return rc;
@@ -3975,6 +3981,7 @@ int64_t cgl_dense_workspace_bytes(int M, int K, int N) {
 
 int cgl_dense_fwd(const float* X, const float* W, const float* b, float* Y, int M, int K, int N, int act, float slope,
                   void* ws, int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   ConvGeom g;
   const int rc = conv_geom(M, 1, 1, K, N, 1, 0, g, 1);
   if (rc) return rc;
@@ -3983,6 +3990,7 @@ int cgl_dense_fwd(const float* X, const float* W, const float* b, float* Y, int 
 
 int cgl_dense_bwd_data(const float* dY, const float* W, float* dX, int M, int K, int N, void* ws, int64_t wsb,
                        void* stream) {
+  CGL_BATCH_GUARD();
   ConvGeom g;
   const int rc = conv_geom(M, 1, 1, K, N, 1, 0, g, 1);
   if (rc) return rc;
@@ -3991,6 +3999,7 @@ int cgl_dense_bwd_data(const float* dY, const float* W, float* dX, int M, int K,
 
 int cgl_dense_bwd_weight(const float* dY, const float* X, float* dW, float* db, int M, int K, int N, void* ws,
                          int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   ConvGeom g;
   const int rc = conv_geom(M, 1, 1, K, N, 1, 0, g, 1);
   if (rc) return rc;
@@ -4015,8 +4024,10 @@ int64_t cgl_conv_packed_floats(int h, int w, int cin, int cout, int stride, int 
 }
 
 // Launch batching (cgl_conv_batch_begin / _end): between the two calls, cgl_conv_pack_multi,
-// cgl_dropout2d_masks_dev, cgl_normal_fill_dev and cgl_sample_rows_dev record their (validated) arguments
-// instead of launching (one of each at most); _end launches them as one cgl_conv_begin_k.
+// cgl_dropout2d_masks(_dev), cgl_normal_fill_dev, cgl_sample_rows_dev and cgl_adv_loss (two at most) record their
+// (validated) arguments instead of launching (one of each at most); _end launches them as one cgl_conv_begin_k.
+// Every other launching entry point of the library returns CGL_E_STATE while a batch is open on the calling
+// thread (CGL_BATCH_GUARD), so nothing can be launched ahead of the deferred calls on the stream.
 namespace {
 struct ConvBatch {
   bool on = false;
@@ -4025,6 +4036,10 @@ struct ConvBatch {
 };
 thread_local ConvBatch t_batch;
 }  // namespace
+
+}  // extern "C"
+bool cgl_launch_batch_open() { return t_batch.on; }
+extern "C" {
 
 int cgl_conv_batch_begin(void* stream) {
   if (t_batch.on) return CGL_E_ARG;
@@ -4085,6 +4100,7 @@ int cgl_conv_pack_multi(int njobs, const CglConvPackJob* jobs, void* stream) {
 int cgl_conv3x3_fwd_packed(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w, int cin,
                            int cout, int stride, int up, int act, float slope, const float* drop, void* ws,
                            int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   ConvGeom g;
   const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
   if (rc) return rc;
@@ -4102,6 +4118,7 @@ int64_t cgl_conv3x3_stat_chunks(int n, int h, int w, int cin, int cout, int stri
 int cgl_conv3x3_fwd_packed_stats(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w,
                                  int cin, int cout, int stride, int up, int act, float slope, const float* drop,
                                  int groups, double* part, const int* nvalid, void* ws, int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   ConvGeom g;
   const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
   if (rc) return rc;
@@ -4114,6 +4131,7 @@ int cgl_conv3x3_fwd_packed_bnin(const float* X, const float* Wp, const float* bi
                                 int cin, int cout, int stride, int up, int act, float slope, const float* drop,
                                 int groups, double* part, const float* in_coef, int in_groups, int in_act,
                                 float in_slope, const int* nvalid, void* ws, int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   ConvGeom g;
   const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
   if (rc) return rc;
@@ -4140,6 +4158,7 @@ int cgl_conv3x3_bwd_data_packed_stats(const float* dY, const float* Wp, float* d
                                       int cout, int stride, int up, int groups, double* part, const float* bn_x,
                                       const float* bn_post, const float* bn_post_coef, int bn_post_coef_ld,
                                       const float* bn_mean, float slope, void* ws, int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   ConvGeom g;
   const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
   if (rc) return rc;
@@ -4154,6 +4173,7 @@ int cgl_conv3x3_bwd_data_stats(const float* dY, const float* W, float* dX, int n
                                int stride, int up, int groups, double* part, const float* bn_x, const float* bn_post,
                                const float* bn_post_coef, int bn_post_coef_ld, const float* bn_mean, float slope,
                                void* ws, int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   ConvGeom g;
   const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
   if (rc) return rc;
@@ -4177,6 +4197,7 @@ int cgl_conv3x3_bwd_data_stats(const float* dY, const float* W, float* dX, int n
 
 int cgl_conv3x3_bwd_data_packed(const float* dY, const float* W, const float* Wp, float* dX, int n, int h, int w,
                                 int cin, int cout, int stride, int up, void* ws, int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   ConvGeom g;
   const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
   if (rc) return rc;
@@ -4186,6 +4207,7 @@ int cgl_conv3x3_bwd_data_packed(const float* dY, const float* W, const float* Wp
 
 int cgl_dense_fwd_packed(const float* X, const float* Wp, const float* b, float* Y, int M, int K, int N, int act,
                          float slope, void* ws, int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   ConvGeom g;
   const int rc = conv_geom(M, 1, 1, K, N, 1, 0, g, 1);
   if (rc) return rc;
@@ -4195,6 +4217,7 @@ int cgl_dense_fwd_packed(const float* X, const float* Wp, const float* b, float*
 
 int cgl_dense_bwd_data_packed(const float* dY, const float* Wp, float* dX, int M, int K, int N, void* ws, int64_t wsb,
                               void* stream) {
+  CGL_BATCH_GUARD();
   ConvGeom g;
   const int rc = conv_geom(M, 1, 1, K, N, 1, 0, g, 1);
   if (rc) return rc;
@@ -4213,6 +4236,7 @@ int64_t cgl_bn2d_workspace_bytes(int n, int hw, int C, int groups) {
 int cgl_bn2d_fwd(const float* X, int n, int hw, int C, int groups, const float* gamma, const float* beta, double eps,
                  double momentum, float* running_mean, float* running_var, int train, int act, float slope, float* Y,
                  float* save_mean, float* save_invstd, const int* nvalid, void* ws, int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   if (!X || !Y || !gamma || !beta || !ws || !al16(ws) || !al16(X) || !al16(Y)) return CGL_E_ARG;
   if (n < 1 || hw < 1 || C % 4 != 0 || !pow2_le256(C) || groups < 1 || n % groups || (act != 0 && act != 1))
     return CGL_E_ARG;
@@ -4264,6 +4288,7 @@ int cgl_bn2d_fwd_stats(const double* part, int R, const float* X, int n, int hw,
                        const float* beta, double eps, double momentum, float* running_mean, float* running_var,
                        int act, float slope, float* Y, float* save_mean, float* save_invstd, void* scratch,
                        const int* nvalid, void* ws, int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   return cgl_bn2d_fwd_stats_coef(part, R, X, n, hw, C, groups, gamma, beta, eps, momentum, running_mean, running_var,
                                  act, slope, Y, save_mean, save_invstd, scratch, nullptr, 0, nvalid, ws, wsb, stream);
 }
@@ -4273,6 +4298,7 @@ int cgl_bn2d_fwd_stats_coef(const double* part, int R, const float* X, int n, in
                             float* running_var, int act, float slope, float* Y, float* save_mean, float* save_invstd,
                             void* scratch, float* coef, int apply_img0, const int* nvalid, void* ws, int64_t wsb,
                             void* stream) {
+  CGL_BATCH_GUARD();
   if (!part || !X || !Y || !gamma || !beta || !ws || !al16(ws) || !al16(X) || !al16(Y)) return CGL_E_ARG;
   if ((coef && !al16(coef)) || apply_img0 < 0 || apply_img0 > n) return CGL_E_ARG;
   if (n < 1 || hw < 1 || C % 4 != 0 || !pow2_le256(C) || groups < 1 || n % groups || (act != 0 && act != 1))
@@ -4329,6 +4355,7 @@ int cgl_bn2d_bwd_stats(const double* part, int R, const float* dY, const float* 
                        float slope, const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta,
                        const float* post_coef, int post_coef_ld, const int* nvalid, void* ws, int64_t wsb,
                        void* stream) {
+  CGL_BATCH_GUARD();
   if (post_coef && (post || groups != 1 || !al16(post_coef) || post_coef_ld % 4)) return CGL_E_ARG;
   if (!part || !dY || !X || !save_mean || !save_invstd || !gamma || !dX || !ws || !al16(ws)) return CGL_E_ARG;
   if (!al16(dY) || !al16(X) || !al16(dX) || (post && !al16(post)) || (post_out && !al16(post_out))) return CGL_E_ARG;
@@ -4366,6 +4393,7 @@ int cgl_bn2d_bwd(const float* dY, const float* post, const float* X, int n, int 
                  const float* save_mean, const float* save_invstd, const float* gamma, float slope,
                  const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta,
                  const float* post_coef, int post_coef_ld, const int* nvalid, void* ws, int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   if (post_coef && (post || groups != 1 || !al16(post_coef) || post_coef_ld % 4)) return CGL_E_ARG;
   if (!dY || !X || !save_mean || !save_invstd || !gamma || !dX || !ws || !al16(ws)) return CGL_E_ARG;
   if (!al16(dY) || !al16(X) || !al16(dX) || (post && !al16(post)) || (post_out && !al16(post_out))) return CGL_E_ARG;
@@ -4408,6 +4436,7 @@ int cgl_bn2d_bwd(const float* dY, const float* post, const float* X, int n, int 
 
 int cgl_act_drop_bwd(const float* dY, const float* post, const float* drop, int n, int hw, int C, float slope,
                      int tanh_y, float* dX, void* stream) {
+  CGL_BATCH_GUARD();
   if (!dY || !dX || n < 1 || hw < 1 || C < 1) return CGL_E_ARG;
   if (tanh_y && !post) return CGL_E_ARG;
   hipStream_t s = (hipStream_t)stream;
@@ -4430,6 +4459,7 @@ int cgl_act_drop_bwd(const float* dY, const float* post, const float* drop, int 
 
 int cgl_act_drop_bwd_colsum(const float* dY, const float* post, const float* drop, int n, int hw, int C, float slope,
                             int tanh_y, float* dX, double* part, void* stream) {
+  CGL_BATCH_GUARD();
   const long tot = (long)n * hw * C;
   if (!dY || !dX || !part || n < 1 || hw < 1 || C != 1 || tot > 8192L * 256 || ((uintptr_t)part & 15)) return CGL_E_ARG;
   if (tanh_y && !post) return CGL_E_ARG;
@@ -4447,6 +4477,7 @@ int cgl_act_drop_bwd_colsum(const float* dY, const float* post, const float* dro
 }
 
 int cgl_colsum_finalize(const double* part, int nch, int C, float* out, void* stream) {
+  CGL_BATCH_GUARD();
   if (!part || !out || nch < 1 || C < 1) return CGL_E_ARG;
   CglBnFinArgs f;
   std::memset(&f, 0, sizeof(f));
@@ -4458,6 +4489,7 @@ int cgl_colsum_finalize(const double* part, int nch, int C, float* out, void* st
 
 int cgl_dropout2d_mask(float* mask, int n, int C, double p, unsigned long long seed, unsigned long long counter,
                        void* stream) {
+  CGL_BATCH_GUARD();
   if (!mask || n < 1 || C < 1 || !(p >= 0.0 && p < 1.0)) return CGL_E_ARG;
   const long tot = (long)n * C;
   const float keep = (float)(1.0 - p);
@@ -4504,6 +4536,7 @@ int cgl_dropout2d_masks(int nm, float* const* masks, const int* n, const int* C,
 }
 
 int cgl_nchw_to_nhwc(const float* X, float* Y, int n, int c, int hw, void* stream) {
+  CGL_BATCH_GUARD();
   if (!X || !Y || n < 1 || c < 1 || hw < 1) return CGL_E_ARG;
   hipLaunchKernelGGL(cgl_transpose_k, dim3((hw + 31) / 32, (c + 31) / 32, n), dim3(256), 0, (hipStream_t)stream, X, Y,
                      c, hw);
@@ -4512,6 +4545,7 @@ int cgl_nchw_to_nhwc(const float* X, float* Y, int n, int c, int hw, void* strea
 
 int cgl_dense1_fwd_nhwc(const float* X, const float* W, const float* b, float* Y, float* flat, int n, int c, int hw,
                         void* stream) {
+  CGL_BATCH_GUARD();
   const long per = (long)c * hw;
   if (!X || !W || !Y || n < 1 || c < 1 || hw < 1 || per % 256 || per > 1024 || (long)n * per >= (1L << 31) || !al16(W) ||
       (flat && !al16(flat)))
@@ -4522,6 +4556,7 @@ int cgl_dense1_fwd_nhwc(const float* X, const float* W, const float* b, float* Y
 }
 
 int cgl_dense1_bwd_data_nhwc(const float* dY, const float* W, float* dX, int n, int c, int hw, void* stream) {
+  CGL_BATCH_GUARD();
   if (!dY || !W || !dX || n < 1 || c < 4 || (c & 3) || hw < 1 || (long)n * c * hw >= (1L << 31) || !al16(dX))
     return CGL_E_ARG;   // (the kernel stores float4 into dX)
   const long q = (long)n * c * hw / 4;
@@ -4531,6 +4566,7 @@ int cgl_dense1_bwd_data_nhwc(const float* dY, const float* W, float* dX, int n, 
 }
 
 int cgl_nhwc_to_nchw(const float* X, float* Y, int n, int c, int hw, void* stream) {
+  CGL_BATCH_GUARD();
   if (!X || !Y || n < 1 || c < 1 || hw < 1) return CGL_E_ARG;
   hipLaunchKernelGGL(cgl_transpose_k, dim3((c + 31) / 32, (hw + 31) / 32, n), dim3(256), 0, (hipStream_t)stream, X, Y,
                      hw, c);
@@ -4555,6 +4591,7 @@ int cgl_adv_loss(const float* x, int M, int C, int loss, int target, double weig
 
 int cgl_weights_scale(int weighting, int n, int rank, float lam, const float* beta_host, const float* losses,
                       float* x, int64_t nx, float* alpha_out, void* stream) {
+  CGL_BATCH_GUARD();
   if (weighting < 0 || weighting > 4 || n < 1 || n > CGL_MAX_WORKERS || rank < 0 || rank >= n || !beta_host ||
       !losses || (nx > 0 && !x) || nx < 0)
     return CGL_E_ARG;
@@ -4570,6 +4607,7 @@ int cgl_weights_scale(int weighting, int n, int rank, float lam, const float* be
 
 int cgl_gather_rows(const float* src, const int* idx, int64_t row0, int nrows, int row_floats, float* dst,
                     void* stream) {
+  CGL_BATCH_GUARD();
   if (!src || !dst || nrows < 0 || row_floats < 1 || row0 < 0) return CGL_E_ARG;
   if (nrows == 0) return 0;
   const long n = (long)nrows * row_floats;
@@ -4612,6 +4650,7 @@ static int adam_multi_impl(int nt, float* const* p, const float* const* g, float
 
 int cgl_adam_multi(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
                    const int64_t* n, int step, double lr, double beta1, double beta2, double eps, void* stream) {
+  CGL_BATCH_GUARD();
   if (step < 1) return CGL_E_ARG;
   return adam_multi_impl(nt, p, g, m, v, n, step, nullptr, lr, beta1, beta2, eps, stream);
 }
@@ -4619,6 +4658,7 @@ int cgl_adam_multi(int nt, float* const* p, const float* const* g, float* const*
 int cgl_adam_multi_dev(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
                        const int64_t* n, const int* step_dev, double lr, double beta1, double beta2, double eps,
                        void* stream) {
+  CGL_BATCH_GUARD();
   if (!step_dev) return CGL_E_ARG;
   return adam_multi_impl(nt, p, g, m, v, n, 1, step_dev, lr, beta1, beta2, eps, stream);
 }
@@ -4665,6 +4705,7 @@ int cgl_sample_rows_dev(const float* src, int n_src, int nrows, int row_floats, 
 }
 
 int cgl_counters_add(int* p, int n, int v, void* stream) {
+  CGL_BATCH_GUARD();
   if (!p || n < 1 || n > 64) return CGL_E_ARG;
   hipLaunchKernelGGL(cgl_counters_add_k, dim3(1), dim3(64), 0, (hipStream_t)stream, p, n, v);
   return (int)hipGetLastError();

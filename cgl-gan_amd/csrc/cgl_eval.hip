@@ -137,6 +137,7 @@ extern "C" {
 
 int cgl_kl_score(const float* real, int64_t nr, int64_t real_stride, const float* gen, int64_t ng, int64_t gen_stride,
                  int bins, double lo0, double hi0, double lo1, double hi1, int* counts, double* kl, void* stream) {
+  CGL_BATCH_GUARD();
   if (!real || !gen || nr < 0 || ng < 0 || real_stride < 1 || gen_stride < 1 || bins < 1 || bins > CGL_HIST_MAXB ||
       !(hi0 > lo0) || !(hi1 > lo1) || (!counts && !kl))
     return CGL_E_ARG;

@@ -75,6 +75,121 @@ __device__ __forceinline__ void cgl_round_prologue_at(int bid, int nblk, const C
 }
 
 #ifndef CGL_GEMM_PART_TU
+// The packing jobs alone (cgl_gan_sync_params): after G's parameters were written from outside the round
+// (load, initialisation, a Cloud FedAvg) while the packed copies are maintained by the G Adam launch.
+__global__ __launch_bounds__(256) void cgl_pack_all(CglOpPack pk) {
+  const int b = blockIdx.x;
+  int j = 0;
+  for (int q = 1; q < pk.nj; ++q)
+    if (b >= pk.j[q].blk_begin) j = q;
+  cgl_pack_job(pk.j[j], (long)(b - pk.j[j].blk_begin) * 256 + threadIdx.x);
+}
+
+// G's Adam with the operand packing of the next round (CglAdamPack, plan flag pack_adam): the weight matrices
+// that carry packing jobs are updated in 4 x 4 tiles -- one thread loads 4 rows x 4 columns of p / g / m / v
+// with 16-byte loads, applies cgl_adam_update to each of the 16 values (the arithmetic of cgl_adam_at, element
+// by element), stores them back and writes the updated values straight into the packed forward operand
+// P(W; R, K) (4 consecutive k of a row = one float4) and the packed transposed operand P(W^T; K, R) (4
+// consecutive r of a column = one float4, transposed in registers).  Every other parameter (biases, BatchNorm,
+// unpacked layers, alignment padding) goes through cgl_adam_at over the element ranges.  The round prologue
+// then no longer re-packs G every round (25 MB of traffic per round, profiles/r04_traffic.json).
+#define CGL_APK_MAXT 8
+#define CGL_APK_MAXR 10
+struct CglAdamPackTile {
+  long off;               // first float of W [R][K] in the flat buffer
+  int R, K;               // R % 4 == K % 4 == 0
+  float* fwd;             // P(W; R, K), or null
+  float* trn;             // P(W^T; K, R), or null
+  int blk_begin;
+};
+struct CglAdamPack {
+  int nt, nr, tile_blocks;
+  CglAdamPackTile t[CGL_APK_MAXT];
+  long r0[CGL_APK_MAXR], r1[CGL_APK_MAXR];   // element ranges [r0, r1) of the flat buffer
+  int rblk[CGL_APK_MAXR];                     // first block of each range (after the tile blocks)
+};
+
+__device__ __forceinline__ void cgl_adam_tile_at(const CglAdamArgs& a, const CglAdamPackTile& T, long t) {
+  const int kq = T.K >> 2;
+  if (t >= (long)(T.R >> 2) * kq) return;
+  const int r = (int)(t / kq) * 4, k = (int)(t % kq) * 4;
+  const long e0 = T.off + (long)r * T.K + k;
+  const float ss = a.step_size ? gld(a.step_size) : a.step_size_v;
+  const float bc = a.bc2sqrt ? gld(a.bc2sqrt) : a.bc2sqrt_v;
+  f32x4 P[4], G[4], M[4], V[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long e = e0 + (long)i * T.K;
+    P[i] = *(gcf4p)(a.p + e);
+    G[i] = *(gcf4p)(a.g + e);
+    M[i] = *(gcf4p)(a.m + e);
+    V[i] = *(gcf4p)(a.v + e);
+  }
+  bool upd = true;
+  if (a.scale) {
+    const float inv = (float)(1.0 / (double)gld(a.scale));
+    upd = *(const CGL_GLOBAL unsigned int*)a.found == 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) G[i][j] = G[i][j] * inv;
+      *(gf4p)(a.g + e0 + (long)i * T.K) = G[i];
+    }
+  }
+  if (upd) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float pp = P[i][j], mm = M[i][j], vv = V[i][j];
+        cgl_adam_update(pp, G[i][j], mm, vv, ss, bc, a.b2, a.w1, a.w2, a.eps);
+        P[i][j] = pp;
+        M[i][j] = mm;
+        V[i][j] = vv;
+      }
+      const long e = e0 + (long)i * T.K;
+      *(gf4p)(a.m + e) = M[i];
+      *(gf4p)(a.v + e) = V[i];
+      *(gf4p)(a.p + e) = P[i];
+    }
+  }
+  if (T.fwd) {
+    const int kc = (T.K + 15) >> 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *(gf4p)(T.fwd + cgl_pk_off(r + i, k, kc)) = P[i];
+  }
+  if (T.trn) {
+    const int kc = (T.R + 15) >> 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      *(gf4p)(T.trn + cgl_pk_off(k + j, r, kc)) = f32x4{P[0][j], P[1][j], P[2][j], P[3][j]};
+  }
+}
+
+__global__ __launch_bounds__(256) void cgl_adam_pack(CglAdamArgs a, CglAdamPack pk, CglStepState* st, int tail) {
+  const int b = blockIdx.x;
+  if (b < pk.tile_blocks) {
+    int j = 0;
+    for (int q = 1; q < pk.nt; ++q)
+      if (b >= pk.t[q].blk_begin) j = q;
+    cgl_adam_tile_at(a, pk.t[j], (long)(b - pk.t[j].blk_begin) * 256 + threadIdx.x);
+  } else {
+    int j = 0;
+    for (int q = 1; q < pk.nr; ++q)
+      if (b >= pk.rblk[q]) j = q;
+    const long i = pk.r0[j] + (long)(b - pk.rblk[j]) * 256 + threadIdx.x;
+    if (i < pk.r1[j]) {
+      CglAdamArgs e = a;
+      e.n = pk.r1[j];
+      cgl_adam_at(e, st, 0, i);
+    }
+  }
+  if (tail && b == 0 && threadIdx.x == 0) {   // the round's scalar tail, as cgl_adam_at's thread 0
+    cgl_round_tail(st);
+    if (a.scale) st->scaler_pending = 1;
+  }
+}
+
 __global__ __launch_bounds__(256) void cgl_round_prologue(CglBeginArgs a, float* z, long nz, unsigned long long zseed,
                                                           int nb_norm, int* idx, int epoch, int br, int n,
                                                           unsigned long long sseed, CglOpPack pk) {

@@ -250,6 +250,7 @@ struct Launch {
   bool sk = false;      // GEMM launch holds a split-K problem
   int dt = CGL_DTYPE_F32;   // GEMM operand type (cgl_gan_config.gemm_dtype)
   int abn = 0;              // GEMM operand-transform instantiation (the launch's a_bn)
+  bool adpk = false;        // K_ADAM: the cgl_adam_pack form (cgl_gan.adam_pack)
 };
 
 // Every kernel of a plan is launched through klaunch.  Normally a plain launch; while cgl_gan_profile
@@ -495,7 +496,10 @@ struct cgl_gan {
   hipGraphExec_t gexec[3] = {nullptr, nullptr, nullptr};
   hipStream_t cap = nullptr;   // private capture stream (the legacy default stream cannot capture)
   hipStream_t side = nullptr;  // second stream: the real-row D chain of the first local D step
-  CglOpPack pack{};          // the round prologue's operand-packing jobs
+  CglOpPack pack{};          // the round prologue's operand-packing jobs (none when pack_adam)
+  CglOpPack pack_all{};      // every packing job of the plan (cgl_gan_sync_params)
+  bool pack_adam = false;    // G's packed weights written by the G Adam launch (cgl_adam_pack), not the prologue
+  CglAdamPack adam_pack{};
   hipEvent_t ev[2] = {nullptr, nullptr};   // fork (after the prologue), join (before the D-step head)
   bool two_streams = false;
   float* xchg = nullptr;
@@ -898,6 +902,72 @@ void fuse_prologue(cgl_gan* c) {
   F.record_ev = P.record_ev;
   A.erase(A.begin());
   A[0] = F;
+}
+
+// The packing of G's weights moves from the round prologue into the G Adam launch (cgl_adam_pack) when every
+// job is a G weight matrix with R, K multiples of 4 (the MNIST / ring / Mix-G specs) and that Adam is a plain
+// K_ADAM launch (not CGL_FUSE_GADAM's GEMM-carried form).  The packed copies then always hold the parameters
+// the last G Adam wrote; after any other write of G's parameters the caller runs cgl_gan_sync_params (GanStep
+// does so whenever the parameter buffer's torch version counter moved).  CGL_PACK_ADAM=0 keeps the prologue
+// packing.  Bitwise the same rounds (tests/test_gpu_pack_adam.py).
+bool plan_pack_adam(cgl_gan* c, std::vector<Launch>& ph) {
+  const int env = getenv("CGL_PACK_ADAM") ? atoi(getenv("CGL_PACK_ADAM")) : 1;   // read per plan
+  c->pack_adam = false;
+  if (!env || c->pack.nj == 0 || ph.empty()) return false;
+  Launch& A = ph.back();
+  if (A.kind != K_ADAM || A.adam.p != c->bufs.g_params) return false;
+  CglAdamPack pk;
+  std::memset(&pk, 0, sizeof(pk));
+  std::vector<std::pair<int64_t, int64_t>> spans;
+  for (int q = 0; q < c->pack.nj; ++q) {
+    const CglOpPackJob& J = c->pack.j[q];
+    const TensorRec* tr = nullptr;
+    for (auto& t : c->gl)
+      if (t.kind == 0 && c->bufs.g_params + t.off == J.src) tr = &t;
+    if (!tr || tr->rows % 4 || tr->cols % 4 || tr->off % 4) return false;
+    // the job's view of W [rows = fo][cols = fi]: forward P(W; fo, fi) or transposed P(W^T; fi, fo)
+    const bool fwd = !J.trans && J.R == tr->rows && J.K == tr->cols && J.ld == tr->cols;
+    const bool trn = J.trans && J.R == tr->cols && J.K == tr->rows && J.ld == tr->cols;
+    if (!fwd && !trn) return false;
+    int i = 0;
+    while (i < pk.nt && pk.t[i].off != tr->off) ++i;
+    if (i == pk.nt) {
+      if (pk.nt == CGL_APK_MAXT) return false;
+      pk.t[pk.nt++] = CglAdamPackTile{tr->off, tr->rows, tr->cols, nullptr, nullptr, 0};
+      spans.push_back({tr->off, tr->off + (int64_t)tr->rows * tr->cols});
+    }
+    (fwd ? pk.t[i].fwd : pk.t[i].trn) = J.dst;
+  }
+  int blk = 0;
+  for (int i = 0; i < pk.nt; ++i) {
+    pk.t[i].blk_begin = blk;
+    blk += (int)(((int64_t)(pk.t[i].R / 4) * (pk.t[i].K / 4) + 255) / 256);
+  }
+  pk.tile_blocks = blk;
+  // element ranges: [0, n) minus the tile tensors
+  std::sort(spans.begin(), spans.end());
+  int64_t at = 0;
+  const int64_t n = A.adam.n;
+  auto add = [&](int64_t a0, int64_t a1) {
+    if (a1 <= a0) return true;
+    if (pk.nr == CGL_APK_MAXR) return false;
+    pk.r0[pk.nr] = a0;
+    pk.r1[pk.nr] = a1;
+    pk.rblk[pk.nr] = blk;
+    blk += (int)((a1 - a0 + 255) / 256);
+    ++pk.nr;
+    return true;
+  };
+  for (auto& sp : spans) {
+    if (!add(at, sp.first)) return false;
+    at = sp.second;
+  }
+  if (!add(at, n)) return false;
+  A.adpk = true;
+  A.grid = blk;
+  c->adam_pack = pk;
+  c->pack_adam = true;
+  return true;
 }
 
 int build_plan(cgl_gan* c) {
@@ -1435,8 +1505,14 @@ int build_plan(cgl_gan* c) {
       blk += (int)((cgl_pk_floats(J.R, J.K) / 4 + 255) / 256);
     }
     c->pack.blocks = blk;
-    for (auto& Lq : A)
-      if (Lq.kind == K_PROLOGUE) Lq.grid += blk;
+    c->pack_all = c->pack;
+    if (plan_pack_adam(c, *ph)) {      // the G Adam launch writes the packed copies: no prologue packing
+      c->pack.nj = 0;
+      c->pack.blocks = 0;
+    } else {
+      for (auto& Lq : A)
+        if (Lq.kind == K_PROLOGUE) Lq.grid += blk;
+    }
   }
   fuse_prologue(c);
   defer_heads(c);
@@ -1477,7 +1553,10 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
         klaunch(cgl_bn_bwd, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
       break;
     case K_ADAM:
-      klaunch(cgl_adam, dim3(L.grid), dim3(256), 0, s, L.adam, c->ws.st, L.tail);
+      if (L.adpk)
+        klaunch(cgl_adam_pack, dim3(L.grid), dim3(256), 0, s, L.adam, c->adam_pack, c->ws.st, L.tail);
+      else
+        klaunch(cgl_adam, dim3(L.grid), dim3(256), 0, s, L.adam, c->ws.st, L.tail);
       break;
     case K_GEMM_PRO:       // grid_y = the GEMM's workgroups (fuse_prologue)
       if (L.blk == 2)
@@ -1573,6 +1652,7 @@ int64_t cgl_gan_workspace_bytes(const cgl_gan_config* cfg) {
 }
 
 int cgl_gan_create(const cgl_gan_config* cfg, const cgl_gan_buffers* bufs, cgl_gan** out) {
+  CGL_BATCH_GUARD();
   if (!out || !bufs) return CGL_E_ARG;
   *out = nullptr;
   const int v = validate(cfg);
@@ -1652,6 +1732,7 @@ int cgl_gan_destroy(cgl_gan* c) {
 }
 
 int cgl_gan_reset(cgl_gan* c, const float* beta_host, void* stream) {
+  CGL_BATCH_GUARD();
   if (!c) return CGL_E_ARG;
   CglStepState h;
   std::memset(&h, 0, sizeof(h));
@@ -1665,16 +1746,30 @@ int cgl_gan_reset(cgl_gan* c, const float* beta_host, void* stream) {
   HIPCHK(hipMemcpyAsync(c->ws.st, &h, sizeof(h), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemsetAsync(c->ws.counters, 0, kCounters * sizeof(unsigned int), s));
   HIPCHK(hipMemsetAsync(c->ws.kcount, 0, kSplitKCounters * sizeof(unsigned int), s));
+  if (c->pack_adam && c->pack_all.blocks > 0) {       // the packed G weights from the current parameters
+    hipLaunchKernelGGL(cgl_pack_all, dim3(c->pack_all.blocks), dim3(256), 0, s, c->pack_all);
+    HIPCHK(hipGetLastError());
+  }
   HIPCHK(hipStreamSynchronize(s));
   return CGL_OK;
 }
 
+int cgl_gan_sync_params(cgl_gan* c, void* stream) {
+  CGL_BATCH_GUARD();
+  if (!c) return CGL_E_ARG;
+  if (!c->pack_adam || c->pack_all.blocks == 0) return CGL_OK;   // the prologue re-packs every round
+  hipLaunchKernelGGL(cgl_pack_all, dim3(c->pack_all.blocks), dim3(256), 0, (hipStream_t)stream, c->pack_all);
+  return (int)hipGetLastError();
+}
+
 int cgl_gan_run(cgl_gan* c, int phase, void* stream) {
+  CGL_BATCH_GUARD();
   if (!c || phase < 0 || phase > 2) return CGL_E_ARG;
   return run_phase(c, phase, (hipStream_t)stream);
 }
 
 int cgl_gan_run_graph(cgl_gan* c, int phase, void* stream) {
+  CGL_BATCH_GUARD();
   if (!c || phase < 0 || phase > 2) return CGL_E_ARG;
   hipStream_t s = (hipStream_t)stream;
   if (!c->gexec[phase]) {
@@ -1698,6 +1793,7 @@ int cgl_gan_run_graph(cgl_gan* c, int phase, void* stream) {
 }
 
 int cgl_gan_profile(cgl_gan* c, int phase, void* stream, float* us, int n) {
+  CGL_BATCH_GUARD();
   if (!c || phase < 0 || phase > 2 || !us) return CGL_E_ARG;
   const int nl = cgl_gan_launch_count(c, phase);
   if (n < nl) return CGL_E_SIZE;
@@ -1726,6 +1822,7 @@ int cgl_gan_profile(cgl_gan* c, int phase, void* stream, float* us, int n) {
 }
 
 int cgl_gan_alpha_scale(cgl_gan* c, void* stream) {
+  CGL_BATCH_GUARD();
   if (!c || !c->xchg) return CGL_E_STATE;
   const long n = (long)c->xchg_n;
   const int grid = (int)std::min<long>((n + 255) / 256, 1024);
@@ -1804,6 +1901,7 @@ int cgl_gan_tensor(cgl_gan* c, int which, float** ptr, int64_t* n) {
 }
 
 int cgl_gan_read_stats(cgl_gan* c, cgl_gan_stats* out, void* stream) {
+  CGL_BATCH_GUARD();
   if (!c || !out) return CGL_E_ARG;
   CglStepState h;
   hipStream_t s = (hipStream_t)stream;
@@ -1881,6 +1979,7 @@ int cgl_gan_launch_info(cgl_gan* c, int phase, int idx, int* kind, double* flops
 }
 
 int cgl_gan_launch_one(cgl_gan* c, int phase, int idx, void* stream) {
+  CGL_BATCH_GUARD();
   if (!c || phase < 0 || phase > 2 || idx < 0 || idx >= cgl_gan_launch_count(c, phase)) return CGL_E_ARG;
   int li;
   const std::vector<Launch>* v = phase_list(c, phase, idx, &li);
@@ -1909,6 +2008,7 @@ static int single_gemm(CglGemmDesc& d, void*, int64_t, hipStream_t s) {
 
 int cgl_linear_fwd(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, int act,
                    float slope, void* ws, int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   if (!X || !W || !Y || M < 1 || N < 1 || K < 1 || act < 0 || act > 3) return CGL_E_ARG;
   CglGemmDesc d = make_gemm(0, M, N, K);
   d.a = rows(X, K);
@@ -1925,6 +2025,7 @@ int cgl_linear_fwd(const float* X, const float* W, const float* b, float* Y, int
 
 int cgl_linear_bwd_data(const float* dY, const float* W, float* dX, int M, int N, int K, void* ws, int64_t wsb,
                         void* stream) {
+  CGL_BATCH_GUARD();
   if (!dY || !W || !dX || M < 1 || N < 1 || K < 1) return CGL_E_ARG;
   CglGemmDesc d = make_gemm(1, M, K, N);
   d.a = rows(dY, N);
@@ -1937,6 +2038,7 @@ int cgl_linear_bwd_data(const float* dY, const float* W, float* dX, int M, int N
 
 int cgl_linear_bwd_weight(const float* dY, const float* X, float* dW, float* db, int M, int N, int K, void* ws,
                           int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   if (!dY || !X || !dW || M < 1 || N < 1 || K < 1) return CGL_E_ARG;
   CglGemmDesc d = make_gemm(2, N, K + (db ? 1 : 0), M);
   d.a = rows(dY, N);
@@ -1955,6 +2057,7 @@ int64_t cgl_linear_desc_bytes(void) { return (int64_t)((sizeof(CglGemmDesc) + 25
 
 int cgl_linear_prepare(int op, const float* A, const float* B, const float* bias, float* C, float* db, int M, int N,
                        int K, int act, float slope, void* desc, CglLinearLaunch* launch) {
+  CGL_BATCH_GUARD();
   if (!A || !B || !C || !desc || !launch || M < 1 || N < 1 || K < 1 || act < 0 || act > 3 || !al16(desc))
     return CGL_E_ARG;
   CglGemmDesc d;
@@ -2003,6 +2106,7 @@ int cgl_linear_prepare(int op, const float* A, const float* B, const float* bias
 }
 
 int cgl_linear_launch(const void* desc, const CglLinearLaunch* launch, void* stream) {
+  CGL_BATCH_GUARD();
   if (!desc || !launch || launch->grid < 1 || (launch->tm != 1 && launch->tm != 2)) return CGL_E_ARG;
   HIPCHK(gemm_lds_attr());
   launch_gemm(launch->tm, launch->grid, launch->shmem, (hipStream_t)stream, (const CglGemmDesc*)desc, 1);
@@ -2010,6 +2114,7 @@ int cgl_linear_launch(const void* desc, const CglLinearLaunch* launch, void* str
 }
 
 int cgl_act_fwd(const float* X, int64_t n, int act, float slope, float* Y, void* stream) {
+  CGL_BATCH_GUARD();
   if (!X || !Y || n < 0 || act < 0 || act > 3) return CGL_E_ARG;
   if (n == 0) return 0;
   const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
@@ -2019,6 +2124,7 @@ int cgl_act_fwd(const float* X, int64_t n, int act, float slope, float* Y, void*
 }
 
 int cgl_act_bwd(const float* dY, const float* Y, int64_t n, int act, float slope, float* dX, void* stream) {
+  CGL_BATCH_GUARD();
   if (!dY || !Y || !dX || n < 0 || act < 0 || act > 3) return CGL_E_ARG;
   if (n == 0) return 0;
   const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
@@ -2030,6 +2136,7 @@ int cgl_act_bwd(const float* dY, const float* Y, int64_t n, int act, float slope
 int cgl_bn1d_fwd(const float* X, int M, int F, int ldx, const float* gamma, const float* beta, double eps,
                  double momentum, float* running_mean, float* running_var, int train, int act, float slope, float* Y,
                  float* save_mean, float* save_invstd, void* ws, int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   if (!X || !Y || !gamma || !beta || M < 1 || F < 1 || ldx < F || (act != 0 && act != 1)) return CGL_E_ARG;
   if (!train && (!running_mean || !running_var)) return CGL_E_ARG;
   if (train && M < 2) return CGL_E_ARG;   // torch: "Expected more than 1 value per channel when training"
@@ -2051,6 +2158,7 @@ int cgl_bn1d_fwd(const float* X, int M, int F, int ldx, const float* gamma, cons
 int cgl_bn1d_bwd(const float* dY, const float* Y, const float* X, int M, int F, const float* save_mean,
                  const float* save_invstd, const float* gamma, int act, float slope, float* dX, float* dgamma,
                  float* dbeta, void* ws, int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   if (!dY || !X || !save_mean || !save_invstd || !gamma || !dX || M < 1 || F < 1) return CGL_E_ARG;
   if ((act != 0 && act != 1) || (act == 1 && !Y)) return CGL_E_ARG;
   // gamma / beta grads land in the workspace when the caller does not want them
@@ -2075,6 +2183,7 @@ int cgl_bn1d_bwd(const float* dY, const float* Y, const float* X, int M, int F, 
 
 int cgl_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int step, double lr, double beta1,
                   double beta2, double eps, void* ws, int64_t wsb, void* stream) {
+  CGL_BATCH_GUARD();
   if (!p || !g || !m || !v || n < 0 || step < 1) return CGL_E_ARG;
   (void)ws;
   (void)wsb;
@@ -2102,6 +2211,7 @@ int cgl_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int s
 }
 
 int cgl_normal_fill(float* out, int64_t n, unsigned long long seed, int round, int stream_id, void* stream) {
+  CGL_BATCH_GUARD();
   if (!out || n < 0) return CGL_E_ARG;
   if (n == 0) return 0;
   hipLaunchKernelGGL(cgl_normal, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, out,

@@ -137,8 +137,14 @@ int64_t cgl_gan_workspace_bytes(const cgl_gan_config* cfg);
 int cgl_gan_create(const cgl_gan_config* cfg, const cgl_gan_buffers* bufs, cgl_gan** out);
 int cgl_gan_destroy(cgl_gan* ctx);
 /* Zero the round counters / lambda, set the data-size weights beta[n_workers]
- * (capgan.py:149-153) -- host array. */
+ * (capgan.py:149-153) -- host array.  Also refreshes the packed G weight copies (cgl_gan_sync_params). */
 int cgl_gan_reset(cgl_gan* ctx, const float* beta_host, void* stream);
+/* G's GEMMs read fragment-packed copies of its weight matrices, which the G Adam launch writes as it updates
+ * the parameters (the round prologue packed them every round before round 5).  After writing G's parameters
+ * from OUTSIDE the round -- loading a state dict, an initialisation, the Cloud FedAvg (mixed-gan.py:104-124) --
+ * call this once (stream-ordered, no host sync) before the next round; cgl_gan_reset does it too.  A no-op when
+ * the plan keeps the prologue packing (CGL_PACK_ADAM=0, or shapes it does not cover). */
+int cgl_gan_sync_params(cgl_gan* ctx, void* stream);
 /* Run one round (CGL_PHASE_ALL) or its halves around the exchange: phase A ends with this
  * worker's (unscaled) exchange gradient and G loss; phase B consumes the all-reduced one. */
 int cgl_gan_run(cgl_gan* ctx, int phase, void* stream);
@@ -257,7 +263,8 @@ int cgl_conv3x3_bwd_weight(const float* dY, const float* X, float* dW, float* db
  * be stored.  in_group = -1: X stacks in_groups forward calls of n / in_groups images each (the D step's real
  * and fake calls; at most 2, the wave-unit MFMA weight gradient only).  Supported by the LDS-staged MFMA kernel
  * (the G up-convolutions of model/lsgan.py:11,15), the input-stationary Conv2d(64, 1) of :19 (one call) and
- * the wave-unit MFMA weight gradient (the D convolutions of :78); CGL_E_ARG elsewhere. */
+ * the wave-unit MFMA weight gradient (the D convolutions of :78); CGL_E_ARG elsewhere.  With in_act =
+ * CGL_EPI_ACT_LEAKY, in_slope must be in (0, 1] (the activation is computed as max(w, w * slope)). */
 /* The weight gradient of a one-input-channel conv (the discriminator's Conv2d(1, 16, 3, 2, 1), model/lsgan.py:78)
  * from the gradient at its block's OUTPUT: the LeakyReLU (post = its output) and Dropout2d (drop [n][cout], may be
  * null) backward applied per loaded value, bitwise cgl_act_drop_bwd + cgl_conv3x3_bwd_weight.  Other geometries:
@@ -301,7 +308,9 @@ int cgl_conv_pack_multi(int njobs, const CglConvPackJob* jobs, void* stream);
  * cgl_normal_fill_dev and cgl_sample_rows_dev, and up to two cgl_adv_loss, on that stream validate and record
  * their arguments instead of launching; _end launches them as ONE kernel (their blocks by range).  The batched
  * calls must not depend on each other (they read and write disjoint buffers).  Same results as the separate
- * launches; one launch floor instead of several. */
+ * launches; one launch floor instead of several.  While a batch is open on the calling thread every OTHER
+ * entry point that launches or synchronises (convs, BatchNorm, gather, the MLP step and single ops, ...)
+ * returns CGL_E_STATE without launching, so nothing can run ahead of the deferred calls. */
 int cgl_conv_batch_begin(void* stream);
 int cgl_conv_batch_end(void* stream);
 int cgl_conv3x3_fwd_packed(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w, int cin,
@@ -327,7 +336,8 @@ int cgl_conv3x3_fwd_packed_stats(const float* X, const float* Wp, const float* b
  * in_coef = [2][in_groups][cin] (scale, then shift, per forward call of n / in_groups images), with
  * cgl_eltwise's arithmetic -- the convolution of the applied activation, without that map being written
  * (model/lsgan.py:15-17,20-22: BatchNorm2d -> LeakyReLU -> Upsample -> Conv2d).  part may be null (no
- * statistics of the output). */
+ * statistics of the output).  With in_act = CGL_EPI_ACT_LEAKY, in_slope must be in (0, 1] (CGL_E_ARG otherwise:
+ * the activation is computed as max(w, w * slope), the select's value for every input only then). */
 int cgl_conv3x3_fwd_packed_bnin(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w,
                                 int cin, int cout, int stride, int up, int act, float slope, const float* drop,
                                 int groups, double* part, const float* in_coef, int in_groups, int in_act,
@@ -348,7 +358,9 @@ int cgl_conv3x3_bwd_data_packed_stats(const float* dY, const float* Wp, float* d
 /* The same statistics from the vector one-output-channel input gradient (Conv2d(64, 1, 3, 1, 1) + Tanh,
  * model/lsgan.py:19-20; raw OIHW W, no packing) -- per 128-ROW chunk, the chunking of cgl_bn2d_bwd, so
  * cgl_bn2d_bwd_stats(R = 128) gives bitwise cgl_bn2d_bwd's result on the stored dX (the channel reduction
- * launch saved).  Other geometries: CGL_E_ARG.  (n / groups) h w must be a multiple of 128. */
+ * launch saved) whenever cgl_bn2d_bwd itself reduces in 128-row chunks, i.e. a call of at least 64 such chunks
+ * ((n / groups) h w >= 8192; smaller calls get 32-64-row chunks there, a different but equally valid order).
+ * Other geometries: CGL_E_ARG.  (n / groups) h w must be a multiple of 128. */
 int cgl_conv3x3_bwd_data_stats(const float* dY, const float* W, float* dX, int n, int h, int w, int cin, int cout,
                                int stride, int up, int groups, double* part, const float* bn_x, const float* bn_post,
                                const float* bn_post_coef, int bn_post_coef_ld, const float* bn_mean, float slope,

@@ -4,7 +4,8 @@ Driver, as a restarted process would build it) ends bitwise where the uninterrup
 G, G running statistics, D, and lambda -- on the CPU stand-in step (tests/dist_oracle_step.py).
 Cases: CAPGAN with the E-share every round, and MD-GAN with the D-swap every round (the swap
 permutations come from the server's Random(server + 100), whose state travels in the resume file).
-Ranks whose resume files hold different rounds refuse to start."""
+Ranks whose resume files hold different rounds refuse to start, and a file that fails to load on one
+rank makes every rank raise (no rank left waiting in a collective)."""
 import os
 import tempfile
 
@@ -39,7 +40,21 @@ def _proc(rank, world, port, outdir, mode, kw=KW):
             del first
             if mode == "torn" and rank == 1:            # a crash before rank 1 replaced its file
                 os.remove(os.path.join(rd, f"resume-{kw['algo']}-rank1.pt"))
+            if mode == "corrupt" and rank == 1:         # a damaged file: only rank 1's load raises
+                with open(os.path.join(rd, f"resume-{kw['algo']}-rank1.pt"), "wb") as f:
+                    f.write(b"not a checkpoint")
             dist.barrier()
+            if mode == "corrupt":
+                # every rank must raise (rank 0 too, from the shared all-reduce) instead of rank 0 waiting
+                # in a collective for the process-group timeout
+                try:
+                    Driver(_cfg(resume_dir=rd, **kw), step_factory=oracle_step_factory, device="cpu")
+                    msg = "no error"
+                except Exception as e:
+                    msg = f"{type(e).__name__}: {e}"
+                with open(os.path.join(outdir, f"corrupt{rank}.txt"), "w") as f:
+                    f.write(msg)
+                return
             drv = Driver(_cfg(resume_dir=rd, **kw), step_factory=oracle_step_factory, device="cpu")
             assert drv.round == 2 and drv.step.round == 2
             drv.run(2, log=None)
@@ -80,6 +95,16 @@ def test_resume_rounds_must_agree_world2():
     with tempfile.TemporaryDirectory() as td:
         with pytest.raises(Exception, match="different rounds"):
             mp.spawn(_proc, args=(2, _free_port(), td, "torn", KW), nprocs=2, join=True)
+
+
+def test_resume_load_failure_raises_on_every_rank():
+    """a resume file that fails to load on one rank makes every rank raise together."""
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(_proc, args=(2, _free_port(), td, "corrupt", KW), nprocs=2, join=True)
+        m0 = open(os.path.join(td, "corrupt0.txt")).read()
+        m1 = open(os.path.join(td, "corrupt1.txt")).read()
+        assert "another rank failed to load" in m0, m0
+        assert m1 != "no error" and "another rank" not in m1, m1
 
 
 def test_resume_file_roundtrip(tmp_path):

@@ -174,8 +174,14 @@ def test_config3_capgan_8_workers_eshare(shards):
     _feed(steps, z1, z2, reals)
     comm.round(1)
     torch.cuda.synchronize()
-    MaskedRun(srv.G, workers, [gpu_masks(s) for s in steps])
-    _traj(steps, srv.round(workers, z1, z2, [[x] for x in reals]), "round 2")
+    # the fp32 and fp64 oracles both follow the round's LeakyReLU decisions, and the decisions are checked against
+    # the fp64 run's own signs (as in round 1)
+    m32, m64 = masked_pair(srv.G, workers, srv64.G, workers64, [gpu_masks(s) for s in steps])
+    out = srv.round(workers, z1, z2, [[x] for x in reals])
+    _round64(srv64, workers64, z1, z2, [[x] for x in reals])
+    m64.check_signs()
+    m32.check_signs()
+    _traj(steps, out, "round 2")
 
 
 def test_config4_mixg_8_workers_2_servers_cloud_fedavg(shards):
@@ -250,8 +256,13 @@ def test_config4_mixg_8_workers_2_servers_cloud_fedavg(shards):
         _feed(groups[s], z1, z2, reals)
         LocalComm(groups[s]).round(1)
         torch.cuda.synchronize()
-        MaskedRun(srvs[s].G, wss[s], [gpu_masks(st) for st in groups[s]], head_layer=XL)
-        _traj(groups[s], srvs[s].round(wss[s], z1, z2, [[x] for x in reals]), f"round 2 server {s}")
+        m32, m64 = masked_pair(srvs[s].G, wss[s], o64[s][0].G, o64[s][1], [gpu_masks(st) for st in groups[s]],
+                               head_layer=XL)
+        out = srvs[s].round(wss[s], z1, z2, [[x] for x in reals])
+        _round64w(o64[s][0], o64[s][1], z1, z2, [[x] for x in reals])
+        m64.check_signs()
+        m32.check_signs()
+        _traj(groups[s], out, f"round 2 server {s}")
 
 
 def test_config5_mdgan_8_workers_noniid_dswap_bs512(shards):
@@ -296,8 +307,12 @@ def test_config5_mdgan_8_workers_noniid_dswap_bs512(shards):
     _feed(steps, z1, z2, reals)
     comm.round(1)
     torch.cuda.synchronize()
-    MaskedRun(srv.G, workers, [gpu_masks(s) for s in steps])
-    _traj(steps, srv.round(workers, z1, z2, [[x] for x in reals], weighting="mean"), "round 2")
+    m32, m64 = masked_pair(srv.G, workers, srv64.G, workers64, [gpu_masks(s) for s in steps])
+    out = srv.round(workers, z1, z2, [[x] for x in reals], weighting="mean")
+    _round64w(srv64, workers64, z1, z2, [[x] for x in reals], weighting="mean")
+    m64.check_signs()
+    m32.check_signs()
+    _traj(steps, out, "round 2")
 
 
 def test_mixg_double_softmax_weighting():
@@ -334,8 +349,11 @@ def test_mixg_double_softmax_weighting():
     _feed(steps, z1, z2, reals)
     LocalComm(steps).round(1)
     torch.cuda.synchronize()
-    MaskedRun(srv.G, workers, [gpu_masks(s) for s in steps], head_layer=XL)
+    m32, m64 = masked_pair(srv.G, workers, srv64.G, workers64, [gpu_masks(s) for s in steps], head_layer=XL)
     out = srv.round(workers, z1, z2, [[x] for x in reals])
+    _round64w(srv64, workers64, z1, z2, [[x] for x in reals])
+    m64.check_signs()
+    m32.check_signs()
     _traj(steps, out, "round 2")
     st = steps[0].stats()
     assert rel_scalar(st["F"], out["F"]) <= TRAJ_TOL and abs(st["lambda"] - float(out["lam"])) <= 1e-7

@@ -142,3 +142,19 @@ def test_ops_reject_bad_args():
     assert C.lib.cgl_linear_fwd(None, None, None, None, 1, 1, 1, 0, 0.2, None, 0, None) == C_E_ARG
     assert C.lib.cgl_adam_step(None, None, None, None, 1, 1, 1e-3, 0.5, 0.999, 1e-8, None, 0, None) == C_E_ARG
     assert C.lib.cgl_op_workspace_bytes() >= 64
+
+
+def test_open_launch_batch_refuses_other_launches():
+    """while cgl_conv_batch_begin is open on this thread, a non-batchable entry point must not
+    launch ahead of the deferred calls: it returns CGL_E_STATE (-2) before touching the device (so this runs
+    on CPU).  After _end (an empty batch launches nothing) the same call is validated normally again."""
+    E_ARG, E_STATE = -1, -2
+    lib = C.lib
+    assert lib.cgl_conv_batch_begin(None) == 0
+    try:
+        assert lib.cgl_conv_batch_begin(None) == E_ARG          # nested begin
+        assert lib.cgl_gather_rows(None, None, 0, 1, 4, None, None) == E_STATE
+        assert lib.cgl_act_fwd(None, 0, 0, 0.2, None, None) == E_STATE
+    finally:
+        assert lib.cgl_conv_batch_end(None) == 0
+    assert lib.cgl_gather_rows(None, None, 0, 1, 4, None, None) == E_ARG

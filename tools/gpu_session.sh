@@ -44,7 +44,7 @@ for st in "$@"; do
       timeout -k 10 400 python3 -u bench.py --model lsgan --no-cpu-baseline > $O/bench_lsgan.json 2> $O/bench_lsgan.err || exit $? ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
-        python3 $R/bench.py --steps 50 --warmup 10 --no-cpu-baseline > $O/prof.log 2>&1) || exit $? ;;
+        python3 $R/bench.py --steps 50 --warmup 10 --no-cpu-baseline --conv-steps 0 > $O/prof.log 2>&1) || exit $? ;;
     proflsgan)
       # proflsgan:TAG=ENV1,ENV2 profiles under those env settings -> prof_lsgan_TAG/
       d=prof_lsgan; envs=""
@@ -54,7 +54,7 @@ for st in "$@"; do
     traffic)
       for c in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && export TMPDIR=/tmp CGL_PLAN_DEBUG=1 && timeout -s KILL 150 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/mlp_$c -o run -- \
-          python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/mlp_$c.log 2>&1) || exit $?
+          python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --conv-steps 0 > $O/mlp_$c.log 2>&1) || exit $?
       done ;;
     trafficlsgan)
       for c in FETCH_SIZE WRITE_SIZE; do
@@ -68,7 +68,7 @@ for st in "$@"; do
       for i in 1 2 3; do
         for kv in "${pairs[@]}"; do
           t=${kv%%=*}; envs=${kv#*=}
-          env $envs timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --steps 400 > $O/ab_${t}_$i.json 2> $O/ab_${t}_$i.err || exit $?
+          env $envs timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --conv-steps 0 --steps 400 > $O/ab_${t}_$i.json 2> $O/ab_${t}_$i.err || exit $?
         done
       done ;;
     abl)
