@@ -22,7 +22,7 @@ MODEL_G, MODEL_D = 0, 1
 # every symbol include/cglgan.h declares (checked by tests/test_lib_exports.py)
 EXPORTS = [
     "cgl_gan_param_count", "cgl_gan_param_tensor", "cgl_gan_running_count", "cgl_gan_workspace_bytes",
-    "cgl_gan_create", "cgl_gan_destroy", "cgl_gan_reset", "cgl_gan_sync_params", "cgl_gan_run", "cgl_gan_run_graph",
+    "cgl_gan_create", "cgl_gan_destroy", "cgl_gan_reset", "cgl_gan_sync_params", "cgl_gan_gemm_trace", "cgl_gan_run", "cgl_gan_run_graph",
     "cgl_gan_alpha_scale", "cgl_gan_exchange_buffer", "cgl_gan_tensor", "cgl_gan_read_stats",
     "cgl_gan_plan_info", "cgl_gan_launch_count", "cgl_gan_launch_info", "cgl_gan_launch_one", "cgl_gan_profile", "cgl_linear_fwd", "cgl_linear_bwd_data", "cgl_linear_bwd_weight", "cgl_adam_step",
     "cgl_normal_fill", "cgl_op_workspace_bytes", "cgl_version", "cgl_act_fwd", "cgl_act_bwd", "cgl_bn1d_fwd",
@@ -87,11 +87,30 @@ class GanStats(ctypes.Structure):
                 ("loss_scale", ctypes.c_float * 2), ("last_skipped", ctypes.c_int * 2), ("skipped", ctypes.c_int * 2)]
 
 
+def _hip_runtimes():
+    """Paths of every libamdhip64 mapped into this process (Linux)."""
+    try:
+        with open("/proc/self/maps") as f:
+            return {ln.split()[-1] for ln in f if "libamdhip64" in ln and "/" in ln}
+    except OSError:
+        return set()
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libcglgan_hip.so not built ({LIB_PATH}); run `make -C cgl-gan_amd` "
                           "(there is no CPU fallback)")
+    # torch first: its HIP runtime (libamdhip64.so.7 in torch/lib) must be the one the library binds to, so that
+    # both share one device context, the streams torch hands us and torch.cuda.graph capture.  Loaded the other
+    # way round, the dynamic loader resolves our libamdhip64.so.7 to /opt/rocm's copy and torch later maps its own:
+    # two runtimes in one process, and every library call fails (hipErrorNoDevice, seen on the GPU box when a test
+    # module imported cglgan before torch).
+    import torch  # noqa: F401
     lib = ctypes.CDLL(LIB_PATH)
+    rts = _hip_runtimes()
+    if len(rts) > 1:
+        raise ImportError(f"two HIP runtimes are mapped into this process ({sorted(rts)}): import torch before "
+                          "loading libcglgan_hip.so by any other path")
     P = ctypes.POINTER
     vp, i64, ci, cf, cd = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_double
     sig = {
@@ -103,6 +122,7 @@ def _load():
         "cgl_gan_destroy": (ci, [vp]),
         "cgl_gan_reset": (ci, [vp, P(cf), vp]),
         "cgl_gan_sync_params": (ci, [vp, vp]),
+        "cgl_gan_gemm_trace": (i64, [vp, vp, i64]),
         "cgl_gan_run": (ci, [vp, ci, vp]),
         "cgl_gan_run_graph": (ci, [vp, ci, vp]),
         "cgl_gan_alpha_scale": (ci, [vp, vp]),

@@ -325,7 +325,7 @@ struct CglPipe {
 template <int LAYOUT, int VEC, int TM, int TN, bool SK, int DT = 0, int ABN = 0, bool ADAM = false>
 __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d, int bid, float* __restrict__ s_dyn,
                                               int* __restrict__ s_flag,
-                                              double* __restrict__ s_bnd) {
+                                              double* __restrict__ s_bnd, unsigned long long t_entry = 0) {
   constexpr int S = CglPipe<TM, TN>::S;
   const int M = d->M, N = d->N, K = d->K;
   const int WN = d->WN, WK = d->WK, WM = d->WM;
@@ -375,6 +375,13 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     tn = tile / d->tiles_m;
     tm = tile % d->tiles_m;
   }
+#ifdef CGL_GEMM_TRACE
+  unsigned long long* trc = (d->trace && local < CGL_GEMM_TRACE_WGS) ? d->trace + (long)local * CGL_GEMM_TRACE_W : nullptr;
+  if (trc && tid == 0) {
+    trc[0] = t_entry;
+    trc[1] = wall_clock64();
+  }
+#endif
   const int BM = 32 * TM * WM;
   const int m0 = tm * BM + wm * 32 * TM;            // first row of this wave's tile
   const int n0 = (tn * WN + wn) * 32 * TN;          // first column of this wave's tile
@@ -473,6 +480,9 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 #pragma unroll
     for (int r = 0; r < 16; ++r) accx[x][r] = 0.f;
 
+#ifdef CGL_GEMM_TRACE
+  if (trc && tid == 0) trc[2] = wall_clock64();
+#endif
   {
   const int nch = (K + CGL_GEMM_KCHUNK - 1) / CGL_GEMM_KCHUNK;
   // chunk range of this wave: slice kslice * WK + wk of KS * WK equal slices of the K chunks
@@ -688,6 +698,9 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         compute_chunk(full, c + s, xa[s], xy[s], xb[s]);
+#ifdef CGL_GEMM_TRACE
+        if (trc && tid == 0 && c == cb && s == 0) trc[3] = wall_clock64();   // chunk 0's operands arrived
+#endif
         load_chunk(full, min(c + s + S, cfull - 1), xa[s], xy[s], xb[s]);
       }
     }
@@ -735,6 +748,9 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     }
   }
 
+#ifdef CGL_GEMM_TRACE
+  if (trc && tid == 0) trc[4] = wall_clock64();
+#endif
   // ---------------- cross-workgroup split-K combine (ksplit > 1)
   // Every k-slice workgroup publishes its tile partial with 16-byte write-through (sc1) buffer
   // stores, drains them (vmcnt(0) in every storing wave, then the workgroup barrier) and takes a
@@ -1095,7 +1111,12 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
       if (bad) atomicOr(d->inf_flag, 1u);
     }
   }
-
+#ifdef CGL_GEMM_TRACE
+  if (trc) {
+    __syncthreads();
+    if (tid == 0) trc[5] = wall_clock64();
+  }
+#endif
 }
 
 // One kernel per per-wave block shape (TM x TN), shared by every GEMM of the step; a grouped
@@ -1105,6 +1126,11 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 // Dynamic LDS: the operand-transform tables, then the split-K partials of the waves with wk > 0.
 template <int TM, int TN, bool SK = false, int DT = CGL_DTYPE_F32, int ABN = 0>
 __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDesc* __restrict__ descs, int ndesc) {
+#ifdef CGL_GEMM_TRACE
+  const unsigned long long t_entry = wall_clock64();
+#else
+  const unsigned long long t_entry = 0;
+#endif
   extern __shared__ float cgl_dyn_lds[];
   __shared__ int s_flag[1];                     // split-K: this workgroup reduces its tile
   __shared__ double s_bnd[4 * TN * 32 * 2];     // per-column BatchNorm partials across waves (WM WN <= 4)
@@ -1124,9 +1150,9 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
 #define CGL_BODY(L)                                               \
   do {                                                            \
     if (vec)                                                      \
-      cgl_gemm_body<L, 1, TM, TN, SK, DT, ABN>(d, bid, cgl_dyn_lds, s_flag, s_bnd);    \
+      cgl_gemm_body<L, 1, TM, TN, SK, DT, ABN>(d, bid, cgl_dyn_lds, s_flag, s_bnd, t_entry);    \
     else                                                          \
-      cgl_gemm_body<L, 0, TM, TN, SK, DT, ABN>(d, bid, cgl_dyn_lds, s_flag, s_bnd);    \
+      cgl_gemm_body<L, 0, TM, TN, SK, DT, ABN>(d, bid, cgl_dyn_lds, s_flag, s_bnd, t_entry);    \
   } while (0)
   if (layout == 0)
     CGL_BODY(0);

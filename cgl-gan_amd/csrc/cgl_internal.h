@@ -174,7 +174,13 @@ struct CglGemmDesc {
   float ad_b2, ad_w1, ad_w2, ad_eps;
   const struct CglHeadDesc* fin_head;   // desc 0 of a launch: the previous head launch's deferred loss reduction,
                                          // run by one extra workgroup (the launch's last)
+  // diagnostics (builds with -DCGL_GEMM_TRACE only, env CGL_GEMM_TRACE=1): per workgroup of this problem,
+  // CGL_GEMM_TRACE_W wall-clock stamps (100 MHz, tools/gemm_trace.py)
+  unsigned long long* trace;
 };
+#define CGL_GEMM_TRACE_WGS 4096   // workgroups per problem with trace slots
+#define CGL_GEMM_TRACE_W 8        // words per workgroup: kernel entry, body, k-loop start, chunk 0 consumed,
+                                  // k-loop end, exit
 
 // BatchNorm1d(train) + LeakyReLU over the whole [mtot][F] output of one G layer.
 struct CglBnApplyDesc {

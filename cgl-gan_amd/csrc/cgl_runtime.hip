@@ -127,6 +127,7 @@ struct Carve {
 };
 
 constexpr int kMaxGemmDescs = 128;
+constexpr int64_t kTraceWords = CGL_GEMM_TRACE_W * CGL_GEMM_TRACE_WGS;   // CGL_GEMM_TRACE stamps
 constexpr int kMaxHeadDescs = 2 * CGL_MAX_EPOCH + 4;
 constexpr int kMaxBnDescs = 2 * CGL_MAX_LAYERS;
 constexpr int kSplitKCounters = 8192;           // split-K tickets (one per tile of a launch)
@@ -500,6 +501,8 @@ struct cgl_gan {
   CglOpPack pack_all{};      // every packing job of the plan (cgl_gan_sync_params)
   bool pack_adam = false;    // G's packed weights written by the G Adam launch (cgl_adam_pack), not the prologue
   CglAdamPack adam_pack{};
+  unsigned long long* trace = nullptr;   // CGL_GEMM_TRACE diagnostics buffer (kTraceWords per GEMM descriptor)
+  int64_t trace_words = 0;
   hipEvent_t ev[2] = {nullptr, nullptr};   // fork (after the prologue), join (before the D-step head)
   bool two_streams = false;
   float* xchg = nullptr;
@@ -514,6 +517,7 @@ struct cgl_gan {
     if (side) (void)hipStreamDestroy(side);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
+    if (trace) (void)hipFree(trace);
   }
 };
 
@@ -908,10 +912,13 @@ void fuse_prologue(cgl_gan* c) {
 // job is a G weight matrix with R, K multiples of 4 (the MNIST / ring / Mix-G specs) and that Adam is a plain
 // K_ADAM launch (not CGL_FUSE_GADAM's GEMM-carried form).  The packed copies then always hold the parameters
 // the last G Adam wrote; after any other write of G's parameters the caller runs cgl_gan_sync_params (GanStep
-// does so whenever the parameter buffer's torch version counter moved).  CGL_PACK_ADAM=0 keeps the prologue
-// packing.  Bitwise the same rounds (tests/test_gpu_pack_adam.py).
+// does so whenever the parameter buffer's torch version counter moved).  Bitwise the same rounds
+// (tests/test_gpu_pack_adam.py), but measured SLOWER in the B = 256 round (profiles/r05_pack_adam_ab.txt,
+// interleaved x3: 0.2433 vs 0.2403 ms): the prologue launch only loses 1.5 us (its packing blocks ran beside
+// G's first GEMM on otherwise idle CUs), while the bandwidth-bound G Adam grows 8.2 -> 13.7 us (the 11.6 MB of
+// packed writes, and 4 x 4 tiles per thread leave it too few waves).  Opt-in: CGL_PACK_ADAM=1.
 bool plan_pack_adam(cgl_gan* c, std::vector<Launch>& ph) {
-  const int env = getenv("CGL_PACK_ADAM") ? atoi(getenv("CGL_PACK_ADAM")) : 1;   // read per plan
+  const int env = getenv("CGL_PACK_ADAM") ? atoi(getenv("CGL_PACK_ADAM")) : 0;   // read per plan
   c->pack_adam = false;
   if (!env || c->pack.nj == 0 || ph.empty()) return false;
   Launch& A = ph.back();
@@ -1700,6 +1707,17 @@ int cgl_gan_create(const cgl_gan_config* cfg, const cgl_gan_buffers* bufs, cgl_g
     delete c;
     return e;
   }
+  // diagnostics: per-workgroup wall-clock stamps of every GEMM problem (only a -DCGL_GEMM_TRACE build writes them)
+  if (getenv("CGL_GEMM_TRACE") && atoi(getenv("CGL_GEMM_TRACE")) == 1) {
+    c->trace_words = (int64_t)c->gemm.size() * kTraceWords;
+    hipError_t te = hipMalloc(&c->trace, c->trace_words * 8);
+    if (te == hipSuccess) te = hipMemset(c->trace, 0, c->trace_words * 8);
+    if (te != hipSuccess) {
+      delete c;
+      return (int)te;
+    }
+    for (size_t q = 0; q < c->gemm.size(); ++q) c->gemm[q].trace = c->trace + q * kTraceWords;
+  }
   // upload descriptors, zero counters / state.  The caller's workspace may still have work pending on
   // a non-blocking stream (torch.zeros on a side stream: such streams do not order against the
   // legacy null stream these synchronous copies use), and a fill that lands after the upload zeroes
@@ -1752,6 +1770,16 @@ int cgl_gan_reset(cgl_gan* c, const float* beta_host, void* stream) {
   }
   HIPCHK(hipStreamSynchronize(s));
   return CGL_OK;
+}
+
+int64_t cgl_gan_gemm_trace(cgl_gan* c, unsigned long long* host_out, int64_t n) {
+  if (!c) return CGL_E_ARG;
+  if (!c->trace) return 0;
+  if (!host_out || n <= 0) return c->trace_words;
+  const int64_t k = std::min<int64_t>(n, c->trace_words);
+  hipError_t te = hipDeviceSynchronize();
+  if (te == hipSuccess) te = hipMemcpy(host_out, c->trace, k * 8, hipMemcpyDeviceToHost);
+  return te == hipSuccess ? k : -(int64_t)te;
 }
 
 int cgl_gan_sync_params(cgl_gan* c, void* stream) {

@@ -145,6 +145,12 @@ int cgl_gan_reset(cgl_gan* ctx, const float* beta_host, void* stream);
  * call this once (stream-ordered, no host sync) before the next round; cgl_gan_reset does it too.  A no-op when
  * the plan keeps the prologue packing (CGL_PACK_ADAM=0, or shapes it does not cover). */
 int cgl_gan_sync_params(cgl_gan* ctx, void* stream);
+/* Diagnostics: with CGL_GEMM_TRACE=1 in the environment at create time and a library built with
+ * -DCGL_GEMM_TRACE (tools/build_variant.sh), every GEMM workgroup of the last round stamps the 100 MHz wall
+ * clock at kernel entry, body start, k-loop start, first chunk consumed, k-loop end and exit: 8 words per
+ * workgroup (6 used), 32768 words per GEMM descriptor in plan order.  Copies min(n, size) words (device-synchronising) and returns the count; returns the buffer size
+ * for host_out == null, 0 when tracing is off, a negative HIP error otherwise. */
+int64_t cgl_gan_gemm_trace(cgl_gan* ctx, unsigned long long* host_out, int64_t n);
 /* Run one round (CGL_PHASE_ALL) or its halves around the exchange: phase A ends with this
  * worker's (unscaled) exchange gradient and G loss; phase B consumes the all-reduced one. */
 int cgl_gan_run(cgl_gan* ctx, int phase, void* stream);

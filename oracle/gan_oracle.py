@@ -534,7 +534,8 @@ class CglganServer:
         grad = (ld * ld * gamma).sum() - (ld * gamma * Fg).sum()
         self.lam = self.lam + 10 * grad
         self.opt.step()
-        return dict(Xd=torch.cat(list(Xd)).detach(), Xg=outg.detach(), d_losses=torch.stack(d_losses),
+        return dict(Xd=torch.cat(list(Xd)).detach(), Xg=outg.detach(),
+                    d_losses=torch.stack(d_losses) if d_losses else torch.zeros(0),   # (no D step: [[]] reals)
                     g_losses=ld, gamma=gamma, F=F_max.detach(), lam=self.lam.clone())
 
 

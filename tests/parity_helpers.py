@@ -183,6 +183,29 @@ def _scalar_ok(gpu, s32, s64):
     return e <= max(STEP_TOL * abs(float(s64)), 2 * abs(float(s32) - float(s64)), 1e-12), (gpu, s32, s64)
 
 
+def cglgan_lambda(lam0, losses):
+    """CGLGAN/2DMG/main.py:261-274 (= CGLGAN/MNIST/main.py:271-290) in fp64: lambda0 + 10 (sum l^2 gamma -
+    sum l gamma F_gamma), gamma = softmax(lambda0 l).  Returns (lambda, the six-term sum of |terms|)."""
+    l = torch.as_tensor(losses).double().flatten()
+    g = torch.softmax(float(lam0) * l, dim=0)
+    fg = (g * l).sum()
+    a, b = l * l * g, l * g * fg
+    return float(lam0) + 10.0 * float(a.sum() - b.sum()), float(a.abs().sum() + b.abs().sum())
+
+
+def lambda_within(lam_gpu, l_gpu, lam64, l64, lam0=0.0, k=8):
+    """The closed-form lambda judged against the fp64 oracle's lambda (not against itself).  lambda is a
+    difference of two nearly equal sums, so its error budget is explicit: (1) the propagated loss error --
+    the fp64 formula applied to the round's own losses minus the fp64 oracle's lambda (exact propagation
+    of the already-judged loss differences), plus (2) the fp32 evaluation of the formula, bounded by
+    10 k eps_32 sum |terms| (k ~ the rounding steps per term: square, exp / softmax, products, the sums).
+    Returns (ok, error, allowed)."""
+    lam_prop, mag = cglgan_lambda(lam0, l_gpu)
+    err = abs(float(lam_gpu) - float(lam64))
+    allowed = abs(lam_prop - float(lam64)) + 10.0 * k * 2.0 ** -24 * mag + 1e-12
+    return err <= allowed, err, allowed
+
+
 def check_single_round(kind, B, Br=None, epoch=1, seed0=7):
     """Run one round on the HIP path and on the fp32 + fp64 oracles from identical state; return
     (failures, stats).  Every tensor is judged with ``within`` (module docstring)."""

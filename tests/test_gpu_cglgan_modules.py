@@ -19,7 +19,7 @@ import pytest
 import torch
 
 from oracle import gan_oracle as O
-from parity_helpers import STEP_TOL, dist, to_double, within
+from parity_helpers import STEP_TOL, dist, lambda_within, to_double, within
 
 RING_KEYS_G = ["model.0.weight", "model.0.bias", "paths.0.0.weight", "paths.0.0.bias", "paths.1.0.weight",
                "paths.1.0.bias"]
@@ -72,16 +72,19 @@ def _ring_inputs(srv, workers, B, seed0):
     raise RuntimeError("no well-conditioned seed")
 
 
-def _reference_round(net_g, opti_g, nets_d, optis_d, lam, beta, z1, z2, reals):
+def _reference_round(net_g, opti_g, nets_d, optis_d, lam, beta, z1, z2, reals, d_step=True):
     """One round of CGLGAN/2DMG/main.py with iid != 0 (one head per worker), written as the reference
-    driver writes it: Server.train :225-278 around Worker.train :344-375 (one local step, epoch = 1)."""
+    driver writes it: Server.train :225-278 around Worker.train :344-375 (one local step, epoch = 1).
+    The MNIST driver (CGLGAN/MNIST/main.py:203-296 around :363-394) is the same round, except that its
+    Worker.train iterates its D step over an always-empty list (``Xs = []`` at :365, ``for idx, X in Xs``
+    at :376): the literal driver never updates D (``d_step=False``)."""
     loss_fn = torch.nn.BCELoss()
     N = len(nets_d)
     with torch.no_grad():
         Xd = torch.chunk(net_g(z1), N, dim=0)
     Xg = torch.chunk(net_g(z2), N, dim=0)
     d_losses = []
-    for i in range(N):                                    # Worker.train: the D step on (real, Xd_i)
+    for i in range(N if d_step else 0):                   # Worker.train: the D step on (real, Xd_i)
         net_d, opti_d = nets_d[i], optis_d[i]
         valid = torch.ones(reals[i].shape[0], 1, device=z1.device)
         opti_d.zero_grad()
@@ -111,7 +114,8 @@ def _reference_round(net_g, opti_g, nets_d, optis_d, lam, beta, z1, z2, reals):
     grad = (loss * loss * gamma).sum() - (loss * gamma * F_gamma).sum()
     lam = lam + 10 * grad
     opti_g.step()
-    return dict(d_losses=torch.stack(d_losses).detach(), g_losses=loss.detach(), F=F_max.detach(), lam=lam.detach())
+    return dict(d_losses=torch.stack(d_losses).detach() if d_losses else torch.zeros(0), g_losses=loss.detach(),
+                F=F_max.detach(), lam=lam.detach())
 
 
 @pytest.mark.gpu
@@ -152,16 +156,12 @@ def test_cglgan_ring_round_through_modules_vs_oracle():
         ok, e, a = within(out[name].cpu().reshape(-1), r32[key].reshape(-1), r64[key].reshape(-1), tol=STEP_TOL)
         if not ok:
             fails.append((name, e, a))
-    # lambda = 10 (sum l^2 gamma - sum l gamma F_gamma) (CGLGAN/2DMG/main.py:273-274) is a difference of two
-    # nearly equal sums: judged as the formula applied to the round's own (already judged) losses, within the
-    # fp32 rounding of its terms
-    l = out["g_losses"].double().cpu()
-    gam = torch.softmax(0.0 * l, dim=0)
-    Fg = (gam * l).sum()
-    terms = torch.cat([l * l * gam, l * gam * Fg])
-    lam_ref = 10 * ((l * l * gam).sum() - (l * gam * Fg).sum())
-    if abs(float(out["lam"]) - float(lam_ref)) > 10 * 8 * 2.0 ** -24 * float(terms.abs().sum()) + 1e-12:
-        fails.append(("lam", float(out["lam"]), float(lam_ref)))
+    # lambda = 10 (sum l^2 gamma - sum l gamma F_gamma) (CGLGAN/2DMG/main.py:273-274), a difference of two
+    # nearly equal sums: judged against the fp64 oracle's lambda with the explicit cancellation bound of
+    # parity_helpers.lambda_within (propagated loss error + fp32 evaluation of the formula)
+    ok, e, a = lambda_within(out["lam"].cpu(), out["g_losses"].cpu(), r64["lam"], r64["g_losses"])
+    if not ok:
+        fails.append(("lam", e, a))
     g32 = {k: v for n in [srv.G.trunk] + list(srv.G.heads) for k, v in n.params.items()}
     g64 = {k: v for n in [srv64.G.trunk] + list(srv64.G.heads) for k, v in n.params.items()}
     for k, p in net_g.named_parameters():
@@ -176,6 +176,111 @@ def test_cglgan_ring_round_through_modules_vs_oracle():
     for i, d in enumerate(nets_d):
         for k, p in d.named_parameters():
             q32, q64 = workers[i].D.params[k], workers64[i].D.params[k]
+            gd = p.grad.detach().double().cpu().flatten() - q64.grad.detach().double().flatten()
+            extra = 1.5 * float((2e-4 * gd.abs() / (q64.grad.detach().double().flatten().abs() + 1e-8)).norm())
+            ok, e, a = within(p, q32, q64, extra)
+            if not ok:
+                fails.append(("D param", i, k, e, a))
+    assert not fails, fails
+
+
+def _mnist_inputs(srv, workers, B, seed0):
+    """z1, z2 and one real batch per worker (uniform(-1, 1) 28x28 images) whose LeakyReLU inputs lie
+    >= 1e-6 sigma from the kink in the fp32 oracle's forward calls of the round."""
+    for s in range(seed0, seed0 + 64):
+        g = torch.Generator().manual_seed(s)
+        z1, z2 = torch.randn(B, 100, generator=g), torch.randn(B, 100, generator=g)
+        reals = [torch.rand(B, 784, generator=g) * 2 - 1 for _ in workers]
+        tr = []
+        with torch.no_grad():
+            G = copy.deepcopy(srv.G)
+            xd, xg = G.forward(z1, trace=tr), G.forward(z2, trace=tr)
+            for w, r, a, b in zip(workers, reals, torch.chunk(xd, len(workers)), torch.chunk(xg, len(workers))):
+                D = copy.deepcopy(w.D)
+                for x in (r, a, b):
+                    D.forward(x, trace=tr)
+        if min(float(t.abs().min() / (t.std() + 1e-30)) for t in tr) >= 1e-6:
+            return z1, z2, reals
+    raise RuntimeError("no well-conditioned seed")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d_step", [True, False], ids=["d_step", "literal_no_d_step"])
+def test_cglgan_mnist_round_through_modules_vs_oracle(d_step):
+    """The CGLGAN MNIST round through ``cglgan.cglgan_mnist`` (CGLGAN/MNIST/mnist_model.py:30-86: MixGenerator
+    trunk + one head per worker, Sigmoid D) driven as CGLGAN/MNIST/main.py:203-296 / :363-394 drive it -- BCE,
+    torch.optim.Adam, the two-phase backward with the ``requires_grad_`` toggles (heads from sum(l), trunk from
+    F_max) -- against the oracle's CglganServer round in fp32 and fp64 at the 1e-5 step tolerance.  d_step:
+    the intended worker D step (as the 2DMG worker); literal_no_d_step: the MNIST worker's D loop never runs."""
+    from cglgan import cglgan_mnist as M
+    N, B = 2, 64
+    torch.manual_seed(20211213)
+    net_g = M.Generator((1, 28, 28), N).cuda()
+    nets_d = [M.Discriminator((1, 28, 28), N).cuda() for _ in range(N)]
+    srv = O.CglganServer(O.MixNet(O.mnist_mixgen_trunk_spec(), [O.mnist_mixgen_head_spec(h) for h in range(N)]),
+                         torch.full((N,), 1.0 / N))
+    _load_oracle(srv.G, net_g)
+    for n in [srv.G.trunk] + list(srv.G.heads):          # BatchNorm running statistics too
+        for k in list(n.buffers):
+            n.buffers[k] = net_g.state_dict()[k].detach().cpu().clone()
+    workers = []
+    for d in nets_d:
+        w = O.Worker(O.SeqNet(O.mnist_discriminator_spec(sigmoid=True)), "bce")
+        _load_oracle(w.D, d)
+        w.opt = O.Adam(w.D.parameters())
+        workers.append(w)
+    srv.opt = O.Adam(srv.G.parameters())
+    srv64, workers64 = copy.deepcopy(srv), copy.deepcopy(workers)
+    to_double(srv64, workers64)
+    z1, z2, reals = _mnist_inputs(srv, workers, B, 101)
+    opti_g = torch.optim.Adam(net_g.parameters(), lr=O.LR, betas=(O.B1, O.B2))
+    optis_d = [torch.optim.Adam(d.parameters(), lr=O.LR, betas=(O.B1, O.B2)) for d in nets_d]
+    lam0 = torch.tensor(0.0, device="cuda")
+    out = _reference_round(net_g, opti_g, nets_d, optis_d, lam0, torch.full((N,), 1.0 / N, device="cuda"),
+                           z1.cuda(), z2.cuda(), [r.cuda() for r in reals], d_step=d_step)
+    torch.cuda.synchronize()
+    orc = [[r] for r in reals] if d_step else [[] for _ in reals]
+    r32 = srv.round(workers, z1, z2, orc)
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    try:
+        r64 = srv64.round(workers64, z1.double(), z2.double(), [[r.double() for r in rs] for rs in orc])
+    finally:
+        torch.set_default_dtype(prev)
+    fails = []
+    names = (("d_losses", "d_losses"),) if d_step else ()
+    for name, key in names + (("g_losses", "g_losses"), ("F", "F")):
+        ok, e, a = within(out[name].cpu().reshape(-1), r32[key].reshape(-1), r64[key].reshape(-1), tol=STEP_TOL)
+        if not ok:
+            fails.append((name, e, a))
+    ok, e, a = lambda_within(out["lam"].cpu(), out["g_losses"].cpu(), r64["lam"], r64["g_losses"])
+    if not ok:
+        fails.append(("lam", e, a))
+    g32 = {k: v for n in [srv.G.trunk] + list(srv.G.heads) for k, v in n.params.items()}
+    g64 = {k: v for n in [srv64.G.trunk] + list(srv64.G.heads) for k, v in n.params.items()}
+    for k, p in net_g.named_parameters():
+        gd = p.grad.detach().double().cpu().flatten() - g64[k].grad.detach().double().flatten()
+        ok, e, a = within(p.grad, g32[k].grad, g64[k].grad)
+        if not ok:
+            fails.append(("G grad", k, e, a))
+        extra = 1.5 * float((2e-4 * gd.abs() / (g64[k].grad.detach().double().flatten().abs() + 1e-8)).norm())
+        ok, e, a = within(p, g32[k], g64[k], extra)
+        if not ok:
+            fails.append(("G param", k, e, a))
+    b32 = {k: v for n in [srv.G.trunk] + list(srv.G.heads) for k, v in n.buffers.items()}
+    b64 = {k: v for n in [srv64.G.trunk] + list(srv64.G.heads) for k, v in n.buffers.items()}
+    for k, v in net_g.state_dict().items():
+        if k in b32 and "running" in k:
+            ok, e, a = within(v, b32[k], b64[k])
+            if not ok:
+                fails.append(("G buffer", k, e, a))
+    for i, d in enumerate(nets_d):
+        for k, p in d.named_parameters():
+            q32, q64 = workers[i].D.params[k], workers64[i].D.params[k]
+            if not d_step:
+                if not torch.equal(p.detach().cpu(), q32.detach()):
+                    fails.append(("D param moved", i, k))
+                continue
             gd = p.grad.detach().double().cpu().flatten() - q64.grad.detach().double().flatten()
             extra = 1.5 * float((2e-4 * gd.abs() / (q64.grad.detach().double().flatten().abs() + 1e-8)).norm())
             ok, e, a = within(p, q32, q64, extra)

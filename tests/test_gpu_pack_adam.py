@@ -1,5 +1,6 @@
-"""G's packed weight copies written by the G Adam launch (cgl_round.h cgl_adam_pack, plan_pack_adam; round 5)
-instead of re-packed by every round's prologue (CGL_PACK_ADAM=0): bitwise the same rounds.
+"""G's packed weight copies written by the G Adam launch (cgl_round.h cgl_adam_pack, plan_pack_adam; round 5;
+opt-in CGL_PACK_ADAM=1, measured slower than the default) instead of re-packed by every round's prologue
+(CGL_PACK_ADAM=0, the default): bitwise the same rounds.
 
 The packed operands P(W; fo, fi) (forward B) and P(W^T; fi, fo) (input-gradient B) of the MNIST G's wide
 layers are written from the updated parameters in 4 x 4 tiles by the Adam launch; every other parameter

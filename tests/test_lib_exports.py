@@ -158,3 +158,20 @@ def test_open_launch_batch_refuses_other_launches():
     finally:
         assert lib.cgl_conv_batch_end(None) == 0
     assert lib.cgl_gather_rows(None, None, 0, 1, 4, None, None) == E_ARG
+
+
+def test_one_hip_runtime_whatever_the_import_order():
+    """Importing cglgan before torch must not map a second HIP runtime: the library has to bind to torch's
+    libamdhip64 (one device context, torch's streams, graph capture).  Round 5 found the GPU suite failing
+    with hipErrorNoDevice on every library call when a test module imported cglgan first (/opt/rocm's
+    runtime beside torch's); cglgan._lib now loads torch first and refuses a second runtime."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import cglgan\n"
+            "from cglgan import _lib\n"
+            "rts = _lib._hip_runtimes()\n"
+            "assert len(rts) == 1 and 'torch' in next(iter(rts)), rts\n"
+            "print('ONE-RUNTIME')\n") % os.path.join(ROOT, "cgl-gan_amd")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ONE-RUNTIME" in r.stdout, r.stdout + r.stderr

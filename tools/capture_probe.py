@@ -1,6 +1,12 @@
 #!/usr/bin/env python3
 """Which single op breaks torch.cuda.graph capture?  Each case runs in its own subprocess (a crash in one
-does not hide the others):  python tools/capture_probe.py  -> one line per case (ok / rc)."""
+does not hide the others):  python tools/capture_probe.py  -> one line per case (ok / rc).
+
+Round 5 adds the r04 segfault's own pattern (tests/test_gpu_cglgan_modules.py, an eager G -> D -> CE ->
+backward step whose outputs -- and so its autograd graph -- stay alive across the side-stream warm-up and
+the capture) in four forms: the library's modules or plain torch modules (nn.Linear / BatchNorm1d /
+LeakyReLU / Tanh, no libcglgan call at all), eager graph alive or deleted before the capture:
+alive_hip, del_hip, alive_torch, del_torch."""
 import os
 import subprocess
 import sys
@@ -8,7 +14,66 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CASES = ["linear_fwd", "linear_fwd_act", "linear_bwd_data", "linear_bwd_weight", "bn1d_fwd", "bn1d_bwd", "act_fwd",
          "gen_fwd", "disc_fwd", "gen_fwd_bwd", "torch_only", "g_sum_none", "gd_sum_keep", "gd_ce_keep", "gd_ce_none",
-         "d_ce_none", "g_bn_only_none", "test_exact", "test_b64", "test_noeager", "test_nosnap"]
+         "d_ce_none", "g_bn_only_none", "test_exact", "test_b64", "test_noeager", "test_nosnap",
+         "alive_torch", "del_torch", "alive_hip", "del_hip"]
+
+
+def torch_models():
+    """model/mnist_model.py's Generator / Discriminator as plain torch modules (reference structure)."""
+    import torch.nn as nn
+
+    def block(i, o, bn=True):
+        layers = [nn.Linear(i, o)] + ([nn.BatchNorm1d(o, 0.8)] if bn else []) + [nn.LeakyReLU(0.2)]
+        return layers
+    G = nn.Sequential(*block(100, 128, False), *block(128, 256), *block(256, 512), *block(512, 1024),
+                      nn.Linear(1024, 784), nn.Tanh())
+    D = nn.Sequential(nn.Linear(784, 512), nn.LeakyReLU(0.2), nn.Linear(512, 256), nn.LeakyReLU(0.2),
+                      nn.Linear(256, 2))
+    return G, D
+
+
+def run_alive(name):
+    """The r04 test's flow; ``alive_*`` keeps the eager step's outputs (its autograd graph) across the capture."""
+    sys.path.insert(0, os.path.join(ROOT, "cgl-gan_amd"))
+    import torch
+    torch.manual_seed(5)
+    if name.endswith("_hip"):
+        from cglgan import model as CM
+        G, D = CM.Generator((1, 28, 28)).cuda(), CM.Discriminator((1, 28, 28)).cuda()
+        fwd = lambda z: D(G(z))
+    else:
+        G, D = torch_models()
+        G, D = G.cuda(), D.cuda()
+        fwd = lambda z: D(G(z).view(z.shape[0], -1))
+    z = torch.randn(128, 100, device="cuda")
+    params = list(G.parameters()) + list(D.parameters())
+
+    def step():
+        out = fwd(z)
+        loss = torch.nn.functional.cross_entropy(out, torch.ones(out.shape[0], dtype=torch.long, device="cuda"))
+        loss.backward()
+        return out, loss
+    for q in params:
+        q.grad = None
+    keep = step()
+    if name.startswith("del_"):
+        del keep
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            for q in params:
+                q.grad = None
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    for q in params:
+        q.grad = None
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    g.replay()
+    torch.cuda.synchronize()
+    print("CASE-OK", name, flush=True)
 
 
 def run_test_like(name):
@@ -58,6 +123,8 @@ def run_test_like(name):
 def run_case(name):
     if name.startswith("test_"):
         return run_test_like(name)
+    if name.startswith("alive_") or name.startswith("del_"):
+        return run_alive(name)
     sys.path.insert(0, os.path.join(ROOT, "cgl-gan_amd"))
     import torch
     from cglgan import model as CM

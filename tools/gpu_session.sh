@@ -15,7 +15,9 @@
 #   tiles[:ARGS] tools/tile_search.py (in-round per-descriptor tile search) -> tile_search.json / .log
 #   ab:T1=ENV1;T2=ENV2   the MLP bench under env settings, interleaved x3 -> ab_<T>_<i>.json
 #   abl:T1=ENV1;T2=ENV2  the same for the LSGAN conv round, interleaved x2 -> abl_<T>_<i>.json
+#   capprobe     tools/capture_probe.py, every case (torch.cuda.graph capture cases, one subprocess each) -> capture_probe.txt
 #   rccl         the RCCL world-1 worker with the split-round timing -> rccl.log
+#   gemmtrace[:TAG]  per-workgroup GEMM phase stamps in the graph round (lib_TAG, default lib_trace) -> gemm_trace_TAG.json
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1; shift
@@ -79,6 +81,12 @@ for st in "$@"; do
           env $envs timeout -k 10 300 python3 -u bench.py --model lsgan --no-cpu-baseline > $O/abl_${t}_$i.json 2> $O/abl_${t}_$i.err || exit $?
         done
       done ;;
+    gemmtrace)
+      t=${arg:-trace}
+      CGL_PLAN_DEBUG=1 CGL_LIB_PATH=$R/cgl-gan_amd/lib_$t/libcglgan_hip.so timeout -k 10 200 python3 -u tools/gemm_trace.py \
+        --out $O/gemm_trace_$t.json > $O/gemm_trace_$t.log 2>&1 || exit $? ;;
+    capprobe)
+      timeout -k 10 600 python3 -u tools/capture_probe.py > $O/capture_probe.txt 2>&1 || exit $? ;;
     rccl)
       timeout -k 10 300 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
         --master-port 29517 tests/rccl_world1_worker.py --time > $O/rccl.log 2>&1 || exit $? ;;
