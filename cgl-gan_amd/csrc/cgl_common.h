@@ -88,10 +88,17 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // capgan.py:158,312): m = lerp(m, g, 1 - beta1), v = v beta2 + (1 - beta2) g g,
 // p += -step_size m / (sqrt(v) / sqrt(bias_correction2) + eps).  Shared by cgl_adam and the Adam
 // folded into the GEMM launches (cgl_gemm.hip) so that both round identically.
+// torch's _single_tensor_adam step for one element.  The fused multiply-adds are written out and contraction is
+// off for the rest, so every kernel that inlines this (cgl_adam, the GEMM-epilogue Adam, the tiled cgl_adam_pack)
+// computes bitwise the same value whatever the surrounding code lets the compiler fuse (a vectorised caller had
+// been contracted differently).  The FMAs are the ones the compiler chose for the scalar kernel before: exp_avg.lerp_
+// (at::lerp's two branches as FMAs), exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2) = fma((1 - b2) g, g, v b2).
 __device__ __forceinline__ void cgl_adam_update(float& p, float g, float& m, float& v, float ss, float bc, float b2,
                                                 float w1, float w2, float eps) {
-  m = cgl_lerp(m, g, w1);
-  v = __fadd_rn(__fmul_rn(v, b2), __fmul_rn(__fmul_rn(w2, g), g));
+#pragma clang fp contract(off)
+  const float d = g - m;
+  m = fabsf(w1) < 0.5f ? fmaf(w1, d, m) : fmaf(-d, 1.f - w1, g);
+  v = fmaf(w2 * g, g, v * b2);
   const float denom = sqrtf(v) / bc + eps;
   p = p + (-ss) * m / denom;
 }

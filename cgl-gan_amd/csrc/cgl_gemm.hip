@@ -327,8 +327,26 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
                                               int* __restrict__ s_flag,
                                               double* __restrict__ s_bnd, unsigned long long t_entry = 0) {
   constexpr int S = CglPipe<TM, TN>::S;
+  // The descriptor fields the set-up and the k-loop prologue need, read in ONE round of scalar loads before the
+  // first branch and pinned there: left to the compiler, each load is issued in the block that uses it, after
+  // that block's branch -- a chain of dependent scalar round trips (~0.16 us each, tools/launch_probe.hip) at
+  // every launch start (tools/gemm_trace.py: ~1.7 us from kernel entry to the k-loop in the round 4 build).
   const int M = d->M, N = d->N, K = d->K;
   const int WN = d->WN, WK = d->WK, WM = d->WM;
+  const int h_tm = d->tiles_m, h_tn = d->tiles_n, h_wg0 = d->wg_begin, h_ks = SK ? d->ksplit : 1;
+  const int h_xcd = d->xcd_pm, h_tab = d->tab_floats, h_gen = d->a_gen, h_abn = ABN ? d->a_bn : 0;
+  const int h_ones = (LAYOUT != 0) ? d->b_ones_col : 0, h_apk = d->a_pk, h_bpk = d->b_pk;
+  const float* const h_bias = d->bias;
+  const float* const h_mref = d->mask_ref;
+  const float* const h_tref = d->tanh_ref;
+  const int h_mld = d->mask_ld, h_tld = d->tanh_ld, h_crow0 = d->a_copy_row0;
+  float* const h_copy = d->a_copy;
+  const CglRowSrc h_a = d->a, h_b = d->b;
+  asm volatile("" ::"s"(M), "s"(N), "s"(K), "s"(WN), "s"(WK), "s"(WM), "s"(h_tm), "s"(h_tn), "s"(h_wg0), "s"(h_ks),
+               "s"(h_xcd), "s"(h_tab), "s"(h_gen), "s"(h_abn), "s"(h_ones), "s"(h_apk), "s"(h_bpk));
+  asm volatile("" ::"s"(h_bias), "s"(h_mref), "s"(h_tref), "s"(h_mld), "s"(h_tld), "s"(h_crow0), "s"(h_copy),
+               "s"(h_a.p0), "s"(h_a.p1), "s"(h_a.idx0), "s"(h_a.idx_off), "s"(h_a.split), "s"(h_a.ld), "s"(h_b.p0),
+               "s"(h_b.p1), "s"(h_b.idx0), "s"(h_b.idx_off), "s"(h_b.split), "s"(h_b.ld));
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
@@ -339,9 +357,9 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   // range of (tile, k-slice) units in n-major order, so its L2 holds ~1/8 of the B panels (the
   // weights) plus the A panels, instead of all of both, and the k-slices of one tile share an XCD
   // (their partials stay XCD-local).  Bijective for any count (guide T1).
-  const int KS = (SK && d->ksplit > 1) ? d->ksplit : 1;   // SK: the split-K instantiation
-  const int local = bid - d->wg_begin;
-  const int ntile = d->tiles_m * d->tiles_n;
+  const int KS = (SK && h_ks > 1) ? h_ks : 1;   // SK: the split-K instantiation
+  const int local = bid - h_wg0;
+  const int ntile = h_tm * h_tn;
   const int nwg = ntile * KS;
   int unit = local;
   if (nwg >= 16) {
@@ -351,12 +369,12 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   int tile = unit / KS;
   const int kslice = unit - tile * KS;
   int tn, tm;
-  if (d->xcd_pm > 0 && nwg >= 16) {
+  if (h_xcd > 0 && nwg >= 16) {
     // XCD blocking: position `tile` of the XCD-contiguous sequence is tile `tile` of the slab-major order --
     // slab x = (row slab x / pn, column slab x % pn) of a pm x pn cut of the tile grid, tiles m-minor inside
     // a slab -- so the XCD running a range of the sequence reads one row slab of A and one column slab of B
     // instead of all of A (the n-major order) or all of B.  Bijective for any grid.
-    const int pm = d->xcd_pm, pn = 8 / pm, TMt = d->tiles_m, TNt = d->tiles_n;
+    const int pm = h_xcd, pn = 8 / pm, TMt = h_tm, TNt = h_tn;
     int rest = tile, x = 0, r0 = 0, r1 = 0, c0 = 0, c1 = 0;
     for (; x < 8; ++x) {
       r0 = (x / pn) * TMt / pm;
@@ -372,8 +390,8 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     tm = r0 + rest % h;
     tile = tn * TMt + tm;
   } else {
-    tn = tile / d->tiles_m;
-    tm = tile % d->tiles_m;
+    tn = tile / h_tm;
+    tm = tile % h_tm;
   }
 #ifdef CGL_GEMM_TRACE
   unsigned long long* trc = (d->trace && local < CGL_GEMM_TRACE_WGS) ? d->trace + (long)local * CGL_GEMM_TRACE_W : nullptr;
@@ -386,22 +404,22 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   const int m0 = tm * BM + wm * 32 * TM;            // first row of this wave's tile
   const int n0 = (tn * WN + wn) * 32 * TN;          // first column of this wave's tile
   float* __restrict__ s_tab = s_dyn;                // operand-transform tables
-  float* __restrict__ s_red = s_dyn + d->tab_floats;   // split-K partials
+  float* __restrict__ s_red = s_dyn + h_tab;   // split-K partials
 
   // ---------------- generated A rows (the fused round prologue): this tile's rows of z, drawn here
-  if (d->a_gen) {
+  if (h_gen) {
     const int r0 = tm * BM, r1 = min(r0 + BM, M);
     const long q0 = ((long)r0 * K) >> 2, q1 = ((long)r1 * K + 3) >> 2;
     const uint32_t rnd = (uint32_t)(gldi(d->gen_round) + 1);
     for (long q = q0 + tid; q < q1; q += CGL_GEMM_THREADS)
-      cgl_normal_at(q, const_cast<float*>(d->a.p0), d->gen_n, d->gen_seed, rnd, 0);
+      cgl_normal_at(q, const_cast<float*>(h_a.p0), d->gen_n, d->gen_seed, rnd, 0);
     __syncthreads();   // (workgroup release / acquire: the rows are read back below, by every wave)
   }
 
   // ---------------- operand-transform prologue (before any operand load is consumed)
   // ABN: the instantiation carrying the operand transforms (0: none compiled in; 1 / 2: the mode
   // of the launch's problems, a problem with a_bn 0 beside them runs untransformed)
-  const int abn = ABN ? d->a_bn : 0;
+  const int abn = h_abn;
   if (ABN == 1 && abn == 1) {                 // forward BatchNorm of A (k-contiguous, every k)
     cgl_abn_fwd_prologue(d->a_bnf, K, (tm * BM) / d->a_bnf.gr, local == 0 && kslice == 0, s_tab,
                          s_tab + CGL_BN_MAXF + 16);
@@ -439,12 +457,12 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   float pf_bias[TN], pf_ref[EPF ? TM : 1][EPF ? TN : 1][16];
   if constexpr (EPF) {
     if (wk == 0) {
-      const float* ref = d->mask_ref ? d->mask_ref : d->tanh_ref;
-      const long ldr = d->mask_ref ? d->mask_ld : d->tanh_ld;
+      const float* ref = h_mref ? h_mref : h_tref;
+      const long ldr = h_mref ? h_mld : h_tld;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int colc = min(n0 + 32 * j + li, N - 1);
-        pf_bias[j] = d->bias ? gld(d->bias + colc) : 0.f;
+        pf_bias[j] = h_bias ? gld(h_bias + colc) : 0.f;
         if (ref) {
 #pragma unroll
           for (int i = 0; i < TM; ++i)
@@ -459,7 +477,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   }
 
   // ---------------- main loop
-  const int b_ones = (LAYOUT != 0) ? d->b_ones_col : 0;
+  const int b_ones = h_ones;
   const int nmem = N - b_ones;     // columns of B actually in memory
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -488,11 +506,11 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   // chunk range of this wave: slice kslice * WK + wk of KS * WK equal slices of the K chunks
   const int nsl = KS * WK, sl = kslice * WK + wk;
   const int cb = (sl * nch) / nsl, ce = ((sl + 1) * nch) / nsl;
-  const int lda = d->a.ld, ldb = d->b.ld;
-  float* __restrict__ a_copy = d->a_copy;
+  const int lda = h_a.ld, ldb = h_b.ld;
+  float* __restrict__ a_copy = h_copy;
   // copy-out: chunk c of a row block is written by the one wave of the (tiles_n x WN) that load
   // it whose column index equals c modulo their count (the copy work spread over every workgroup)
-  const int copy_n = d->tiles_n * WN, copy_me = tn * WN + wn;
+  const int copy_n = h_tn * WN, copy_me = tn * WN + wn;
   const bool ybn = ABN == 2 && abn == 2;        // A under a_bn 2 streams the BatchNorm input y
   const float* __restrict__ ybase = d->a_bnb.y;
   const int ldy = d->a_bnb.ldy;
@@ -503,22 +521,22 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   const float* b_base[TN];
   bool b_is_ones[TN], copy_row[TM];
   const int kcn = (K + CGL_GEMM_KCHUNK - 1) / CGL_GEMM_KCHUNK;   // k chunks (packed block stride)
-  const bool apk = LAYOUT == 0 && d->a_pk, bpk = LAYOUT == 0 && d->b_pk;
+  const bool apk = LAYOUT == 0 && h_apk, bpk = LAYOUT == 0 && h_bpk;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int am = m0 + 32 * i + li;      // A row (kc) or A column (mn)
-    a_base[i] = (LAYOUT != 2) ? cgl_row(d->a, min(am, M - 1)) : d->a.p0 + min(am, M - 1);
+    a_base[i] = (LAYOUT != 2) ? cgl_row(h_a, min(am, M - 1)) : h_a.p0 + min(am, M - 1);
     // packed A: the lane's float4 of chunk 0 of its (clamped) 32-row block
-    if (apk) a_base[i] = d->a.p0 + (long)(min(m0 + 32 * i, (M - 1) & ~31) >> 5) * kcn * 512 + lane * 4;
+    if (apk) a_base[i] = h_a.p0 + (long)(min(m0 + 32 * i, (M - 1) & ~31) >> 5) * kcn * 512 + lane * 4;
     y_base[i] = ybn ? ((LAYOUT != 2) ? ybase + (long)min(am, M - 1) * ldy : ybase + min(am, M - 1)) : a_base[i];
-    copy_row[i] = (LAYOUT != 2) && a_copy && am < M && am >= d->a_copy_row0;
+    copy_row[i] = (LAYOUT != 2) && a_copy && am < M && am >= h_crow0;
   }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int bc = n0 + 32 * j + li;      // B row (NT) or B column (NN/TN)
     b_is_ones[j] = b_ones && (bc == N - 1);
-    b_base[j] = (LAYOUT == 0) ? cgl_row(d->b, min(bc, N - 1)) : d->b.p0 + max(0, min(bc, nmem - 1));
-    if (bpk) b_base[j] = d->b.p0 + (long)(min(n0 + 32 * j, (N - 1) & ~31) >> 5) * kcn * 512 + lane * 4;
+    b_base[j] = (LAYOUT == 0) ? cgl_row(h_b, min(bc, N - 1)) : h_b.p0 + max(0, min(bc, nmem - 1));
+    if (bpk) b_base[j] = h_b.p0 + (long)(min(n0 + 32 * j, (N - 1) & ~31) >> 5) * kcn * 512 + lane * 4;
   }
 
   // Full chunks (k + 16 <= K) load without clamps and multiply without masks: rows / columns
@@ -1124,8 +1142,11 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 // layer side by side).  Separate symbols keep the 1x1 variant's register budget (and so its
 // occupancy) independent of the 2x2 variant's.
 // Dynamic LDS: the operand-transform tables, then the split-K partials of the waves with wk > 0.
+// sel (kernel arguments): the launch's problem selection -- first workgroup of problems 1 and 2 (INT_MAX: absent), each
+// problem's layout | vec << 2 in 4 bits, and whether d[0] carries a deferred head reduction -- so that a workgroup finds
+// its problem and body without reading the descriptor array first.
 template <int TM, int TN, bool SK = false, int DT = CGL_DTYPE_F32, int ABN = 0>
-__global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDesc* __restrict__ descs, int ndesc) {
+__global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDesc* __restrict__ descs, CglGemmSel sel) {
 #ifdef CGL_GEMM_TRACE
   const unsigned long long t_entry = wall_clock64();
 #else
@@ -1136,17 +1157,16 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
   __shared__ double s_bnd[4 * TN * 32 * 2];     // per-column BatchNorm partials across waves (WM WN <= 4)
   const int bid = blockIdx.x;
   // the previous head launch's deferred batch-mean loss reduction rides in one extra workgroup (the last)
-  if (descs[0].fin_head && bid == (int)gridDim.x - 1) {
+  if (sel.fin && bid == (int)gridDim.x - 1) {
     cgl_head_finish(descs[0].fin_head, descs[0].fin_head->nwg, cgl_dyn_lds);
     return;
   }
-  int di = 0;
-  for (int q = 1; q < ndesc; ++q)
-    if (bid >= descs[q].wg_begin) di = q;
+  const int di = bid >= sel.wg2 ? 2 : (bid >= sel.wg1 ? 1 : 0);
   const CglGemmDesc* __restrict__ d = descs + di;
-  const int layout = d->layout;
+  const int meta = (sel.meta >> (4 * di)) & 15;
+  const int layout = meta & 3;
   // VEC: every operand allows 16-byte loads along its contiguous dimension
-  const int vec = d->a_vec && d->b_vec;
+  const int vec = (meta >> 2) & 1;
 #define CGL_BODY(L)                                               \
   do {                                                            \
     if (vec)                                                      \

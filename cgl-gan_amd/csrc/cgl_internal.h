@@ -178,6 +178,12 @@ struct CglGemmDesc {
   // CGL_GEMM_TRACE_W wall-clock stamps (100 MHz, tools/gemm_trace.py)
   unsigned long long* trace;
 };
+// Problem selection of a grouped GEMM launch (cgl_gemm_f32 kernel arguments; at most 3 problems per launch)
+struct CglGemmSel {
+  int wg1, wg2;     // first workgroup of problems 1 and 2 (INT_MAX: absent)
+  int meta;         // per problem q: (layout | (a_vec && b_vec) << 2) << 4 q
+  int fin;          // problem 0 carries fin_head (the previous head launch's deferred loss reduction)
+};
 #define CGL_GEMM_TRACE_WGS 4096   // workgroups per problem with trace slots
 #define CGL_GEMM_TRACE_W 8        // words per workgroup: kernel entry, body, k-loop start, chunk 0 consumed,
                                   // k-loop end, exit

@@ -21,6 +21,7 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -291,7 +292,7 @@ hipError_t gemm_lds_attr() {
 }
 
 template <int DT>
-void launch_gemm16(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, int n, bool sk) {
+void launch_gemm16(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, CglGemmSel n, bool sk) {
   if (sk) {
     if (blk == 2)
       klaunch(cgl_gemm_f32<2, 2, true, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
@@ -304,7 +305,19 @@ void launch_gemm16(int blk, int grid, int shmem, hipStream_t s, const CglGemmDes
   }
 }
 
-void launch_gemm(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, int n, bool sk = false,
+// The problem selection of a launch (CglGemmSel) from the host copies of its n problems.
+CglGemmSel gemm_sel(const CglGemmDesc* hd, int n) {
+  CglGemmSel q;
+  q.wg1 = n > 1 ? hd[1].wg_begin : INT_MAX;
+  q.wg2 = n > 2 ? hd[2].wg_begin : INT_MAX;
+  q.meta = 0;
+  for (int i = 0; i < n && i < 3; ++i) q.meta |= (hd[i].layout | ((hd[i].a_vec && hd[i].b_vec) ? 4 : 0)) << (4 * i);
+  q.fin = hd[0].fin_head ? 1 : 0;
+  return q;
+}
+
+// d: the device descriptors of the launch, n: their selection (gemm_sel of the host copies)
+void launch_gemm(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, CglGemmSel n, bool sk = false,
                  int dt = CGL_DTYPE_F32, int abn = 0) {
   if (abn == 1) {          // fp32, no split-K (planner)
     if (blk == 2)
@@ -1541,7 +1554,9 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
   }
   switch (L.kind) {
     case K_GEMM:
-      launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, L.count, L.sk, L.dt, L.abn);
+      if (L.count > 3) return CGL_E_SIZE;
+      launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, gemm_sel(c->gemm.data() + L.first, L.count), L.sk,
+                  L.dt, L.abn);
       break;
     case K_HEAD:
       klaunch(cgl_head_loss, dim3(L.grid), dim3(256), 0, s, c->ws.head + L.first);
@@ -2129,7 +2144,7 @@ int cgl_linear_prepare(int op, const float* A, const float* B, const float* bias
   launch->tm = d.TM;
   launch->grid = cgl_gemm_wgs(d);
   launch->shmem = cgl_gemm_stage_bytes(d);
-  launch->flags = 0;
+  launch->flags = 0x100 | d.layout | ((d.a_vec && d.b_vec) ? 4 : 0);   // the kernel's problem selection (CglGemmSel)
   return 0;
 }
 
@@ -2137,7 +2152,12 @@ int cgl_linear_launch(const void* desc, const CglLinearLaunch* launch, void* str
   CGL_BATCH_GUARD();
   if (!desc || !launch || launch->grid < 1 || (launch->tm != 1 && launch->tm != 2)) return CGL_E_ARG;
   HIPCHK(gemm_lds_attr());
-  launch_gemm(launch->tm, launch->grid, launch->shmem, (hipStream_t)stream, (const CglGemmDesc*)desc, 1);
+  if (!(launch->flags & 0x100)) return CGL_E_ARG;        // not filled by cgl_linear_prepare
+  CglGemmSel sel;
+  sel.wg1 = sel.wg2 = INT_MAX;
+  sel.meta = launch->flags & 15;
+  sel.fin = 0;
+  launch_gemm(launch->tm, launch->grid, launch->shmem, (hipStream_t)stream, (const CglGemmDesc*)desc, sel);
   return (int)hipGetLastError();
 }
 

@@ -234,7 +234,9 @@ int64_t cgl_op_workspace_bytes(void);
  * cgl_linear_launch then runs it stream-ordered without any upload or synchronisation, reading the
  * operand pointers given at preparation.  op 0: C[M][N] = act(A[M][K] B[N][K]^T + bias);
  * op 1: C[M][K] = A[M][N] B[N][K]; op 2: C[N][K] = A[M][N]^T B[M][K] and db[N] = column sums of A. */
-typedef struct CglLinearLaunch { int tm, grid, shmem, flags; } CglLinearLaunch;
+typedef struct CglLinearLaunch { int tm, grid, shmem, flags; } CglLinearLaunch;   /* filled by cgl_linear_prepare;
+                                                                                   flags: the kernel's layout / vector
+                                                                                   selection (opaque) */
 int64_t cgl_linear_desc_bytes(void);
 int cgl_linear_prepare(int op, const float* A, const float* B, const float* bias, float* C, float* db, int M, int N,
                        int K, int act, float slope, void* desc, CglLinearLaunch* launch);

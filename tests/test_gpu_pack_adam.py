@@ -47,7 +47,8 @@ def _same(a, b, tag=""):
     torch.cuda.synchronize()
     for name in NAMES:
         x, y = getattr(a, name), getattr(b, name)
-        assert torch.equal(x, y), (tag, name, (x - y).abs().max().item())
+        same = (x == y) | (torch.isnan(x) & torch.isnan(y))      # (an overflowing f16 round stores NaN gradients)
+        assert bool(same.all()), (tag, name, (x - y).abs().max().item())
     sa, sb = a.stats(), b.stats()
     for k in ("round", "g_loss", "F", "lambda", "d_loss", "loss_scale", "skipped"):
         assert sa[k] == sb[k], (tag, k, sa[k], sb[k])
