@@ -321,6 +321,12 @@ struct CglPipe {
   static constexpr int S = (TM * TN == 1) ? CGL_GEMM_STAGES1 : CGL_GEMM_STAGES;
 };
 
+// Compile-time flags of a main-loop version: packed A, packed B (layout 0 only), A copy-out.
+template <bool A_, bool B_, bool C_>
+struct CglLoopFl {
+  static constexpr bool PA = A_, PB = B_, CP = C_;
+};
+
 // Dynamic LDS layout: [operand-transform tables (cgl_gemm_tab_floats)] [split-K partials]
 template <int LAYOUT, int VEC, int TM, int TN, bool SK, int DT = 0, int ABN = 0, bool ADAM = false>
 __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d, int bid, float* __restrict__ s_dyn,
@@ -542,12 +548,13 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   // Full chunks (k + 16 <= K) load without clamps and multiply without masks: rows / columns
   // past M / N come from clamped (valid) addresses and only feed accumulator rows / columns
   // that are never stored.  Only the K-tail chunk clamps its k and zeroes k >= K.
-  auto load_a = [&](auto tail, int c, const float* const (&base)[TM], int ld, float (&A_)[TM][8], bool pk) {
+  auto load_a = [&](auto tail, int c, const float* const (&base)[TM], int ld, float (&A_)[TM][8], auto pkc) {
     constexpr bool T = decltype(tail)::value;
+    constexpr bool pk = decltype(pkc)::value;
     const int k = c * CGL_GEMM_KCHUNK + 8 * lh;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      if (LAYOUT == 0 && pk) {          // packed: two contiguous 1 KB wave loads (padding past K)
+      if constexpr (LAYOUT == 0 && pk) {          // packed: two contiguous 1 KB wave loads (padding past K)
         const f32x4 x = *(gcf4p)(base[i] + c * 512), y = *(gcf4p)(base[i] + c * 512 + 256);
         A_[i][0] = x[0]; A_[i][1] = x[1]; A_[i][2] = x[2]; A_[i][3] = x[3];
         A_[i][4] = y[0]; A_[i][5] = y[1]; A_[i][6] = y[2]; A_[i][7] = y[3];
@@ -573,15 +580,16 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
       }
     }
   };
-  auto load_chunk = [&](auto tail, int c, float (&A_)[TM][8], auto& Y_, float (&B_)[TN][8]) {
+  // fl: the loop version's compile-time flags (LoopFl: packed A, packed B, copy-out) -- see run_loop below
+  auto load_chunk = [&](auto tail, int c, float (&A_)[TM][8], auto& Y_, float (&B_)[TN][8], auto fl) {
     constexpr bool T = decltype(tail)::value;
     const int k = c * CGL_GEMM_KCHUNK + 8 * lh;
-    load_a(tail, c, a_base, lda, A_, apk);
+    load_a(tail, c, a_base, lda, A_, std::integral_constant<bool, decltype(fl)::PA>());
     if constexpr (ABN == 2)
-      if (ybn) load_a(tail, c, y_base, ldy, Y_, false);
+      if (ybn) load_a(tail, c, y_base, ldy, Y_, std::integral_constant<bool, false>());
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      if (LAYOUT == 0 && bpk) {
+      if constexpr (LAYOUT == 0 && decltype(fl)::PB) {
         const f32x4 x = *(gcf4p)(b_base[j] + c * 512), y = *(gcf4p)(b_base[j] + c * 512 + 256);
         B_[j][0] = x[0]; B_[j][1] = x[1]; B_[j][2] = x[2]; B_[j][3] = x[3];
         B_[j][4] = y[0]; B_[j][5] = y[1]; B_[j][6] = y[2]; B_[j][7] = y[3];
@@ -607,7 +615,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
       }
     }
   };
-  auto compute_chunk = [&](auto tail, int c, float (&A_)[TM][8], auto& Y_, float (&B_)[TN][8]) {
+  auto compute_chunk = [&](auto tail, int c, float (&A_)[TM][8], auto& Y_, float (&B_)[TN][8], auto fl) {
     constexpr bool T = decltype(tail)::value;
     const int k = c * CGL_GEMM_KCHUNK + 8 * lh;
     if (ABN == 1 && abn == 1 && LAYOUT == 0) {
@@ -651,11 +659,11 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
       }
      }
     }
-    const bool own = (c % copy_n) == copy_me;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       if (T) cgl_mask(A_[i], true, k, K);
-      if (copy_row[i] && own) {
+      if constexpr (!decltype(fl)::CP) continue;
+      if (copy_row[i] && (c % copy_n) == copy_me) {
         float* dst = a_copy + (long)(m0 + 32 * i + li) * d->a_copy_ld;
         if (VEC && (!T || k + 7 < K)) {
           *(gf4p)(dst + k) = f32x4{A_[i][0], A_[i][1], A_[i][2], A_[i][3]};
@@ -702,34 +710,60 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 
   // S register sets in rotation: set s holds chunk c + s; after its MFMAs are issued it is
   // refilled with chunk c + s + S, so S - 1 chunks of loads are always in flight.  The bulk
-  // loop body is branch-free (refills past the end re-load the last full chunk, harmlessly), so
-  // every s_waitcnt waits for exactly the set it consumes.
+  // loop body must be branch-free (refills past the end re-load the last full chunk, harmlessly), so
+  // that every s_waitcnt waits for exactly the set it consumes: the operand forms (packed A / B) and the
+  // A copy-out are therefore compile-time flags of a loop VERSION (run_loop, dispatched once below).  With them
+  // as run-time branches inside the loop (rounds 1-4) the compiler could not count the loads across the
+  // branch merges and drained every load at the top of each rotation (s_waitcnt vmcnt(0)): one chunk in three
+  // waited for all loads in flight (tools/gemm_trace.py per-chunk stamps: 0.32 / 0.32 / 0.52 us).
   const int cfull = min(ce, K / CGL_GEMM_KCHUNK);   // end of this wave's full chunks
   std::integral_constant<bool, false> full;
   std::integral_constant<bool, true> tailc;
-  if (cb < cfull) {
-    float xa[S][TM][8], xy[S][ABN == 2 ? TM : 1][8], xb[S][TN][8];
+  auto run_loop = [&](auto fl) {
+    if (cb < cfull) {
+      float xa[S][TM][8], xy[S][ABN == 2 ? TM : 1][8], xb[S][TN][8];
 #pragma unroll
-    for (int s = 0; s < S; ++s) load_chunk(full, min(cb + s, cfull - 1), xa[s], xy[s], xb[s]);
-    int c = cb;
-    for (; c + S <= cfull; c += S) {
+      for (int s = 0; s < S; ++s) load_chunk(full, min(cb + s, cfull - 1), xa[s], xy[s], xb[s], fl);
+      int c = cb;
+      for (; c + S <= cfull; c += S) {
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
-        compute_chunk(full, c + s, xa[s], xy[s], xb[s]);
+        for (int s = 0; s < S; ++s) {
+          compute_chunk(full, c + s, xa[s], xy[s], xb[s], fl);
 #ifdef CGL_GEMM_TRACE
-        if (trc && tid == 0 && c == cb && s == 0) trc[3] = wall_clock64();   // chunk 0's operands arrived
+          if (trc && tid == 0 && c == cb && s == 0) trc[3] = wall_clock64();   // chunk 0's operands arrived
+#ifdef CGL_GEMM_TRACE_CHUNKS
+          if (trc && tid == 0 && c + s - cb < CGL_GEMM_TRACE_W - 8) trc[8 + c + s - cb] = wall_clock64();
 #endif
-        load_chunk(full, min(c + s + S, cfull - 1), xa[s], xy[s], xb[s]);
+#endif
+          // the refill stays right behind the chunk it replaces: without the fences the scheduler sinks all S
+          // refills to the end of the rotation, where the next rotation's first chunk waits on them at once
+          __builtin_amdgcn_sched_barrier(0);
+          load_chunk(full, min(c + s + S, cfull - 1), xa[s], xy[s], xb[s], fl);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
-    }
 #pragma unroll
-    for (int s = 0; s < S - 1; ++s)
-      if (c + s < cfull) compute_chunk(full, c + s, xa[s], xy[s], xb[s]);
-  }
-  if (cfull < ce) {   // the K tail (at most one chunk, owned by the last k-group)
-    float xa[TM][8], xy[ABN == 2 ? TM : 1][8], xb[TN][8];
-    load_chunk(tailc, cfull, xa, xy, xb);
-    compute_chunk(tailc, cfull, xa, xy, xb);
+      for (int s = 0; s < S - 1; ++s)
+        if (c + s < cfull) compute_chunk(full, c + s, xa[s], xy[s], xb[s], fl);
+    }
+    if (cfull < ce) {   // the K tail (at most one chunk, owned by the last k-group)
+      float xa[TM][8], xy[ABN == 2 ? TM : 1][8], xb[TN][8];
+      load_chunk(tailc, cfull, xa, xy, xb, fl);
+      compute_chunk(tailc, cfull, xa, xy, xb, fl);
+    }
+  };
+  const bool cp = LAYOUT != 2 && a_copy != nullptr;
+  if constexpr (LAYOUT == 0) {
+    if (apk && bpk)
+      cp ? run_loop(CglLoopFl<true, true, true>()) : run_loop(CglLoopFl<true, true, false>());
+    else if (apk)
+      cp ? run_loop(CglLoopFl<true, false, true>()) : run_loop(CglLoopFl<true, false, false>());
+    else if (bpk)
+      cp ? run_loop(CglLoopFl<false, true, true>()) : run_loop(CglLoopFl<false, true, false>());
+    else
+      cp ? run_loop(CglLoopFl<false, false, true>()) : run_loop(CglLoopFl<false, false, false>());
+  } else {
+    cp ? run_loop(CglLoopFl<false, false, true>()) : run_loop(CglLoopFl<false, false, false>());
   }
   }   // (register-pipelined main loop)
 

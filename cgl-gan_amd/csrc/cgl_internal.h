@@ -185,8 +185,11 @@ struct CglGemmSel {
   int fin;          // problem 0 carries fin_head (the previous head launch's deferred loss reduction)
 };
 #define CGL_GEMM_TRACE_WGS 4096   // workgroups per problem with trace slots
+#ifdef CGL_GEMM_TRACE_CHUNKS      // + wave 0's stamp after each of its first 64 chunks (words 8 ..)
+#define CGL_GEMM_TRACE_W 72
+#else
 #define CGL_GEMM_TRACE_W 8        // words per workgroup: kernel entry, body, k-loop start, chunk 0 consumed,
-                                  // k-loop end, exit
+#endif                            // k-loop end, exit
 
 // BatchNorm1d(train) + LeakyReLU over the whole [mtot][F] output of one G layer.
 struct CglBnApplyDesc {

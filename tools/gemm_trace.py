@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=30)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--words", type=int, default=8, help="CGL_GEMM_TRACE_W of the build (72 with -DCGL_GEMM_TRACE_CHUNKS)")
     a = ap.parse_args()
     from cglgan import GanStep, specs
     from cglgan import _lib as C
@@ -61,7 +62,7 @@ def main():
         buf = (ctypes.c_ulonglong * n)()
         got = C.lib.cgl_gan_gemm_trace(st._h, buf, n)
         assert got == n, got
-    W, NW = 8, 4096          # CGL_GEMM_TRACE_W words per workgroup, CGL_GEMM_TRACE_WGS workgroups per problem
+    W, NW = a.words, 4096    # CGL_GEMM_TRACE_W words per workgroup, CGL_GEMM_TRACE_WGS workgroups per problem
     rows, prev_end, t00 = [], None, None
     us = lambda x: x / 100.0      # 100 MHz ticks -> us
     med = lambda xs: round(us(statistics.median(xs)), 2) if xs else None
@@ -88,6 +89,15 @@ def main():
                "per_chunk_rest": None,
                "epi": med([w[5] - w[4] for w in ws if w[5]]),
                "gap": round(us(t0 - prev_end), 2) if prev_end is not None else None}
+        if W > 8:     # per-chunk stamps of wave 0: median over workgroups of each chunk-to-chunk interval
+            ch = []
+            for i in range(len(ws)):
+                base = (q * NW + i) * W
+                ts = [buf[base + 8 + j] for j in range(W - 8)]
+                ts = [t for t in ts if t]
+                ch.append([ts[j + 1] - ts[j] for j in range(len(ts) - 1)])
+            m = max(len(c) for c in ch) if ch else 0
+            row["chunk_us"] = [round(us(statistics.median([c[j] for c in ch if len(c) > j])), 3) for j in range(m)]
         prev_end = t_end
         rows.append(row)
         print(json.dumps(row), flush=True)

@@ -82,9 +82,9 @@ for st in "$@"; do
         done
       done ;;
     gemmtrace)
-      t=${arg:-trace}
+      t=${arg:-trace}; w=8; [ "$t" != trace ] && w=72
       CGL_PLAN_DEBUG=1 CGL_LIB_PATH=$R/cgl-gan_amd/lib_$t/libcglgan_hip.so timeout -k 10 200 python3 -u tools/gemm_trace.py \
-        --out $O/gemm_trace_$t.json > $O/gemm_trace_$t.log 2>&1 || exit $? ;;
+        --words $w --out $O/gemm_trace_$t.json > $O/gemm_trace_$t.log 2>&1 || exit $? ;;
     capprobe)
       timeout -k 10 600 python3 -u tools/capture_probe.py > $O/capture_probe.txt 2>&1 || exit $? ;;
     rccl)
