@@ -250,6 +250,7 @@ class GanStep:
         if sd["device_state"].shape != st.shape:
             raise ValueError("resume state: device round state of another build / configuration")
         st.copy_(sd["device_state"])
+        self.sync_params()          # the packed G weights and the next round's z from the loaded state
         torch.cuda.current_stream().synchronize()
 
     # ------------------------------------------------------------------ execution

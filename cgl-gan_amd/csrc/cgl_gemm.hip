@@ -350,6 +350,14 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   const CglRowSrc h_a = d->a, h_b = d->b;
   asm volatile("" ::"s"(M), "s"(N), "s"(K), "s"(WN), "s"(WK), "s"(WM), "s"(h_tm), "s"(h_tn), "s"(h_wg0), "s"(h_ks),
                "s"(h_xcd), "s"(h_tab), "s"(h_gen), "s"(h_abn), "s"(h_ones), "s"(h_apk), "s"(h_bpk));
+  // the epilogue's fields too (they would otherwise cost one more scalar round trip after the k-loop)
+  const int e_act = d->act, e_ldc = d->ldc, e_gr = d->stat_gr;
+  const float e_slope = d->slope;
+  float* const e_C = d->C;
+  float* const e_bout = d->bias_out;
+  float* const e_stat = d->stat_part;
+  double* const e_bnb = d->bnb_part;
+  asm volatile("" ::"s"(e_act), "s"(e_ldc), "s"(e_gr), "s"(e_slope), "s"(e_C), "s"(e_bout), "s"(e_stat), "s"(e_bnb));
   asm volatile("" ::"s"(h_bias), "s"(h_mref), "s"(h_tref), "s"(h_mld), "s"(h_tld), "s"(h_crow0), "s"(h_copy),
                "s"(h_a.p0), "s"(h_a.p1), "s"(h_a.idx0), "s"(h_a.idx_off), "s"(h_a.split), "s"(h_a.ld), "s"(h_b.p0),
                "s"(h_b.p1), "s"(h_b.idx0), "s"(h_b.idx_off), "s"(h_b.split), "s"(h_b.ld));
@@ -876,27 +884,27 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     if (owner && colok && !ones_col) {
       float bb;
       if constexpr (EPF) bb = pf_bias[j];
-      else bb = d->bias ? gld(d->bias + col) : 0.f;
+      else bb = h_bias ? gld(h_bias + col) : 0.f;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         float* v = (float*)&acc[i][j];
-        if (d->bias) {
+        if (h_bias) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) v[r] += bb;
         }
-        if (d->act == CGL_EPI_ACT_LEAKY) {
-          const float sl = d->slope;
+        if (e_act == CGL_EPI_ACT_LEAKY) {
+          const float sl = e_slope;
 #pragma unroll
           for (int r = 0; r < 16; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * sl;
-        } else if (d->act == CGL_EPI_ACT_TANH) {
+        } else if (e_act == CGL_EPI_ACT_TANH) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) v[r] = tanhf(v[r]);   // (double tanh here costs ~4 us on G L4)
-        } else if (d->act == CGL_EPI_ACT_SIGMOID) {
+        } else if (e_act == CGL_EPI_ACT_SIGMOID) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) v[r] = 1.f / (1.f + expf(-v[r]));
         }
-        if (d->mask_ref) {
-          const float sl = d->slope;
+        if (h_mref) {
+          const float sl = e_slope;
           float ref[16];
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -904,13 +912,13 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
               ref[r] = pf_ref[i][j][r];
             } else {
               const int row = min(rbase + 32 * i + (r & 3) + 8 * (r >> 2), M - 1);
-              ref[r] = gld(d->mask_ref + (long)row * d->mask_ld + col);
+              ref[r] = gld(h_mref + (long)row * h_mld + col);
             }
           }
 #pragma unroll
           for (int r = 0; r < 16; ++r) v[r] = ref[r] > 0.f ? v[r] : v[r] * sl;
         }
-        if (d->tanh_ref) {
+        if (h_tref) {
           float t[16];
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -918,7 +926,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
               t[r] = pf_ref[i][j][r];
             } else {
               const int row = min(rbase + 32 * i + (r & 3) + 8 * (r >> 2), M - 1);
-              t[r] = gld(d->tanh_ref + (long)row * d->tanh_ld + col);
+              t[r] = gld(h_tref + (long)row * h_tld + col);
             }
           }
 #pragma unroll
@@ -940,17 +948,17 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
       for (int i = 0; i < TM; ++i) {
         const float* v = (const float*)&acc[i][j];
         if (ones_col) {
-          if (d->bias_out) {
+          if (e_bout) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
-              if (row < M) gst(d->bias_out + row, v[r]);
+              if (row < M) gst(e_bout + row, v[r]);
             }
             if constexpr (ADAM) cgl_epi_adam(d, d->ad_pb, d->ad_mb, d->ad_vb, rbase + 32 * i, M, 0, 1, v);
           }
         } else {
-          float* __restrict__ C = d->C;
-          const int ldc = d->ldc;
+          float* __restrict__ C = e_C;
+          const int ldc = e_ldc;
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
@@ -975,7 +983,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   // backward BatchNorm partials of the stored gradient dy (the next GEMM's a_bn 2): per
   // (row tile, column) {sum dy, sum (y - mean) dy} in double over the workgroup's rows (lane
   // rows, then the two lane halves, then the WM waves of the column, fixed order)
-  if (d->bnb_part) {
+  if (e_bnb) {
     const int ldy = d->bnb_ld;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -1007,7 +1015,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
       Dd += __shfl_xor(Dd, 32);
       if (WM == 1) {           // one wave row per column tile: its sums are the tile's (no LDS, no barrier)
         if (owner && lh == 0 && col < N) {
-          double* p = d->bnb_part + ((long)tm * N + col) * 2;
+          double* p = e_bnb + ((long)tm * N + col) * 2;
           *(CGL_GLOBAL double*)p = Sd;
           *(CGL_GLOBAL double*)(p + 1) = Dd;
         }
@@ -1027,7 +1035,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
           Dd += s_bnd[(((q * WN + wn) * TN + j) * 32 + li) * 2 + 1];
         }
         if (col < N) {
-          double* p = d->bnb_part + ((long)tm * N + col) * 2;
+          double* p = e_bnb + ((long)tm * N + col) * 2;
           *(CGL_GLOBAL double*)p = Sd;
           *(CGL_GLOBAL double*)(p + 1) = Dd;
         }
@@ -1040,13 +1048,13 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   // M2 about its own mean), the two lane halves and then the WM waves of the column are merged by
   // Chan's pairwise update in a fixed order: one workgroup barrier per slot, and a slot holding none
   // of the tile's rows (a tile spans <= 2 forward calls; usually one) costs nothing.
-  if (d->stat_part) {
-    const int gr = d->stat_gr;
+  if (e_stat) {
+    const int gr = e_gr;
     const int trow0 = tm * BM;
     const int gfirst = trow0 / gr;
     const int gsplit = (gfirst + 1) * gr;   // first row of slot 1
     float* s_st = (float*)s_bnd;            // [WM WN TN 32][3] {n, sum, M2} (s_bnd is free here)
-    if (d->bnb_part && WM > 1) __syncthreads();
+    if (e_bnb && WM > 1) __syncthreads();
     for (int s = 0; s < 2; ++s) {
       const int ra = max(trow0, (gfirst + s) * gr), rb = min(min(trow0 + BM, M), (gfirst + s + 1) * gr);
       if (rb - ra <= 0) {                   // workgroup-uniform
@@ -1055,7 +1063,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
           for (int j = 0; j < TN; ++j) {
             const int col = n0 + 32 * j + li;
             if (col < N) {
-              float* p = d->stat_part + ((long)(tm * 2 + s) * N + col) * 2;
+              float* p = e_stat + ((long)(tm * 2 + s) * N + col) * 2;
               gst(p, 0.f);
               gst(p + 1, 0.f);
             }
@@ -1104,7 +1112,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
         if (WM == 1) {         // one wave row per column tile: its merge is the tile's (no LDS, no barrier;
           const int col = n0 + 32 * j + li;   // the same values the one-entry merge below would store)
           if (owner && lh == 0 && col < N) {
-            float* p = d->stat_part + ((long)(tm * 2 + s) * N + col) * 2;
+            float* p = e_stat + ((long)(tm * 2 + s) * N + col) * 2;
             gst(p, 0.f + sum);
             gst(p + 1, 0.f + m2);
           }
@@ -1132,7 +1140,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
             cn = nt;
           }
           if (col < N) {
-            float* p = d->stat_part + ((long)(tm * 2 + s) * N + col) * 2;
+            float* p = e_stat + ((long)(tm * 2 + s) * N + col) * 2;
             gst(p, sum);
             gst(p + 1, m2);
           }

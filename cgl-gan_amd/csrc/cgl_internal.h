@@ -293,6 +293,8 @@ struct CglStepState {
   int last_skipped[2];
   int scaler_pending;
   unsigned int err;                 // sticky: an in-launch rendezvous timed out (never expected)
+  int cur_round;                    // the round in progress (1-based; written by its prologue): the G Adam
+                                    // launch draws the NEXT round's z with counter cur_round + 1
 };
 
 enum { CGL_W_CAPGAN = 0, CGL_W_MEAN = 1, CGL_W_MIX_SINGLE = 2, CGL_W_MIX_DOUBLE = 3, CGL_W_CGLGAN = 4 };

@@ -52,7 +52,7 @@ __device__ void cgl_head_finish(const CglHeadDesc* __restrict__ hd, int nwg, flo
 
 #define CGL_HEAD_MAXQ 4   // float4 per lane kept in registers: F <= 1024
 #ifndef CGL_GEMM_PART_TU   // (the GEMM-instantiation translation units compile only device functions)
-__global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restrict__ hd) {
+__device__ __forceinline__ void cgl_head_loss_body(const CglHeadDesc* __restrict__ hd) {
   // Each wave owns rows r0 + wave + 4 i; a row is a dot product of F features (F % 4 == 0)
   // over 16-byte loads held in registers, a 64-lane reduction, the loss and its gradient, then
   // the gradient into the last hidden layer (dlogits . W) * LeakyReLU'(P) from the same
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc* __restri
 // reference's forward calls (Xd then Xg, capgan.py:215-220).
 #define CGL_BNA_ROWS 32
 #ifndef CGL_GEMM_PART_TU   // (the GEMM-instantiation translation units compile only device functions)
-__global__ __launch_bounds__(256) void cgl_bn_apply(const CglBnApplyDesc* __restrict__ ad) {
+__device__ __forceinline__ void cgl_bn_apply_body(const CglBnApplyDesc* __restrict__ ad) {
   __shared__ float s_sc[2][64], s_sh[2][64];
   __shared__ double s_mean[2][64], s_m2[2][64];
   __shared__ int s_n[2];
@@ -414,10 +414,15 @@ __device__ __forceinline__ void cgl_bn_bwd_body(const CglBnBwdDesc* __restrict__
 }
 
 #ifndef CGL_GEMM_PART_TU   // (the GEMM-instantiation translation units compile only device functions)
-__global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc* __restrict__ bd) { cgl_bn_bwd_body<32>(bd); }
-__global__ __launch_bounds__(256) void cgl_bn_bwd16(const CglBnBwdDesc* __restrict__ bd) { cgl_bn_bwd_body<16>(bd); }
-__global__ __launch_bounds__(256) void cgl_bn_bwd8(const CglBnBwdDesc* __restrict__ bd) { cgl_bn_bwd_body<8>(bd); }
-__global__ __launch_bounds__(256) void cgl_bn_bwd4(const CglBnBwdDesc* __restrict__ bd) { cgl_bn_bwd_body<4>(bd); }
+// The round's small kernels take their descriptor BY VALUE (the kernel arguments): its fields arrive with the
+// kernarg fetch instead of one more dependent scalar round trip to a descriptor in memory (tools/launch_probe.hip:
+// ~0.16 us per dependent scalar load).  The workspace copies stay (the deferred head reduction reads its head's).
+__global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc d) { cgl_head_loss_body(&d); }
+__global__ __launch_bounds__(256) void cgl_bn_apply(const CglBnApplyDesc d) { cgl_bn_apply_body(&d); }
+__global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc d) { cgl_bn_bwd_body<32>(&d); }
+__global__ __launch_bounds__(256) void cgl_bn_bwd16(const CglBnBwdDesc d) { cgl_bn_bwd_body<16>(&d); }
+__global__ __launch_bounds__(256) void cgl_bn_bwd8(const CglBnBwdDesc d) { cgl_bn_bwd_body<8>(&d); }
+__global__ __launch_bounds__(256) void cgl_bn_bwd4(const CglBnBwdDesc d) { cgl_bn_bwd_body<4>(&d); }
 // the single-op entry point (cgl_bn1d_bwd): the descriptor travels in the kernel arguments
 __global__ __launch_bounds__(256) void cgl_bn_bwd_arg(const CglBnBwdDesc d) { cgl_bn_bwd_body<32>(&d); }
 #endif   // CGL_GEMM_PART_TU
@@ -559,7 +564,20 @@ struct CglAdamArgs {
   // step_size / bc2sqrt == null: the values themselves, passed in the kernel arguments (cgl_adam_step: no
   // upload, so the single-op Adam needs no host synchronisation and can be captured)
   float step_size_v, bc2sqrt_v;
+  // z one round ahead (the G Adam launch, plan z_ahead): blocks [zblk0, grid) draw the next round's z into znext
+  // (nz floats, Philox stream 0 of seed zseed, counter = the round in progress + 1: the draw the next round's
+  // prologue made before), while the other blocks update the parameters
+  float* znext;
+  long nz;
+  unsigned long long zseed;
+  int zblk0;
 };
+__device__ __forceinline__ bool cgl_adam_zblock(const CglAdamArgs& a, const CglStepState* st) {
+  if (!a.znext || (int)blockIdx.x < a.zblk0) return false;
+  cgl_normal_at((long)(blockIdx.x - a.zblk0) * 256 + threadIdx.x, a.znext, a.nz, a.zseed,
+                (uint32_t)(st->cur_round + 1), 0);
+  return true;
+}
 
 
 
@@ -660,7 +678,15 @@ __device__ __forceinline__ void cgl_adam_at(const CglAdamArgs& a, CglStepState* 
 
 #ifndef CGL_GEMM_PART_TU   // (the GEMM-instantiation translation units compile only device functions)
 __global__ __launch_bounds__(256) void cgl_adam(CglAdamArgs a, CglStepState* st, int tail) {
+  if (cgl_adam_zblock(a, st)) return;
   cgl_adam_at(a, st, tail, (long)blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// The next round's z from the device round state (cgl_gan_create / _reset / _sync_params): counter st->round + 1,
+// the draw that round's prologue would make
+__global__ __launch_bounds__(256) void cgl_znext_draw(float* out, long n, unsigned long long seed,
+                                                      const CglStepState* st) {
+  cgl_normal_at((long)blockIdx.x * 256 + threadIdx.x, out, n, seed, (uint32_t)(st->round + 1), 0);
 }
 #endif   // CGL_GEMM_PART_TU
 
@@ -755,6 +781,7 @@ __device__ void cgl_begin_at(const CglBeginArgs& a, int r) {
   }
   st->alpha = 1.f;
   st->bn_batches += 2;
+  st->cur_round = r;
 }
 
 // ------------------------------------------------------------------------------------------

@@ -167,6 +167,7 @@ __device__ __forceinline__ void cgl_adam_tile_at(const CglAdamArgs& a, const Cgl
 }
 
 __global__ __launch_bounds__(256) void cgl_adam_pack(CglAdamArgs a, CglAdamPack pk, CglStepState* st, int tail) {
+  if (cgl_adam_zblock(a, st)) return;
   const int b = blockIdx.x;
   if (b < pk.tile_blocks) {
     int j = 0;

@@ -136,6 +136,7 @@ constexpr int kCounters = 64;                    // head-loss tickets
 constexpr int64_t kSplitKFloats = 4 << 20;       // split-K partials of one launch (16 MiB)
 
 struct WS {
+  float* znext;                     // z_ahead: the next round's z [2B][z_dim], drawn by the G Adam launch
   // G forward (2B rows)
   float* gout[CGL_MAX_LAYERS];
   float* gact[CGL_MAX_LAYERS];
@@ -213,6 +214,7 @@ WS carve_ws(const cgl_gan_config& c, void* base) {
   w.hpart = cv.take<float>((int64_t)((Md + kHeadRows - 1) / kHeadRows) * 2);
   w.hpart2 = cv.take<float>((int64_t)((Md + kHeadRows - 1) / kHeadRows) * 2);
   w.idx = cv.take<int>((int64_t)c.epoch * c.batch_real);
+  w.znext = cv.take<float>((int64_t)2 * B * g.dims[0]);
   // split-K scratch last, so that the layout of everything the default plan touches is unchanged
   w.kpart = cv.take<float>(kSplitKFloats);
   w.kcount = cv.take<unsigned int>(kSplitKCounters);
@@ -513,6 +515,7 @@ struct cgl_gan {
   CglOpPack pack{};          // the round prologue's operand-packing jobs (none when pack_adam)
   CglOpPack pack_all{};      // every packing job of the plan (cgl_gan_sync_params)
   bool pack_adam = false;    // G's packed weights written by the G Adam launch (cgl_adam_pack), not the prologue
+  bool z_ahead = false;      // z drawn one round ahead by the G Adam launch into ws.znext (plan_z_ahead)
   CglAdamPack adam_pack{};
   unsigned long long* trace = nullptr;   // CGL_GEMM_TRACE diagnostics buffer (kTraceWords per GEMM descriptor)
   int64_t trace_words = 0;
@@ -897,10 +900,10 @@ void fuse_prologue(cgl_gan* c) {
   CglGemmDesc& d = c->gemm[G.first];
   // (b_pk: layer 0's packed weights are written by the prologue's pack blocks, which would run in this same
   // launch with no ordering against the GEMM tiles reading them -- keep two launches then)
-  if (d.layout != 0 || d.a.p0 != c->bufs.z || d.a.idx0 || d.a.split != 0x7fffffff || d.a_pk || d.b_pk ||
-      d.ksplit > 1)
+  if (d.layout != 0 || d.a.p0 != (c->z_ahead ? c->ws.znext : c->bufs.z) || d.a.idx0 || d.a.split != 0x7fffffff ||
+      d.a_pk || d.b_pk || d.ksplit > 1)
     return;
-  if (c->cfg.gen_z) {
+  if (c->cfg.gen_z && !c->z_ahead) {
     if (d.M != 2 * c->cfg.batch || d.K != c->cfg.g.dims[0] || d.a.ld != d.K) return;   // the tiles cover every z row
     d.a_gen = 1;
     d.gen_round = &c->ws.st->round;
@@ -984,6 +987,10 @@ bool plan_pack_adam(cgl_gan* c, std::vector<Launch>& ph) {
   }
   if (!add(at, n)) return false;
   A.adpk = true;
+  if (A.adam.znext) {           // the z-ahead blocks come after the parameter blocks
+    A.adam.zblk0 = blk;
+    blk += (int)((A.adam.nz / 4 + 255) / 256);
+  }
   A.grid = blk;
   c->adam_pack = pk;
   c->pack_adam = true;
@@ -1004,6 +1011,18 @@ int build_plan(cgl_gan* c) {
   std::vector<Launch>& A = c->phA;
   std::vector<Launch>& Bp = c->phB;
 
+  // ---- z one round ahead (z_ahead): the G Adam launch that ends round r draws round r + 1's z into ws.znext
+  // (cgl_adam_zblock; create / reset / cgl_gan_sync_params draw it from the device round state), and G's first
+  // GEMM reads it there, copying the rows out to bufs.z (the round's z, read by its weight gradient and the
+  // caller).  Before, the workgroups of that GEMM drew their rows of z themselves (a_gen, every column tile of a
+  // row tile the same rows: ~3 us of Philox + Box-Muller in front of its k-loop, tools/gemm_trace.py), on the
+  // round's critical path; in the Adam launch the draw runs beside the bandwidth-bound parameter update.  Same
+  // Philox stream and counter: bitwise the same z.  CGL_Z_AHEAD=0 keeps the in-round draw.
+  {
+    const int zenv = getenv("CGL_Z_AHEAD") ? atoi(getenv("CGL_Z_AHEAD")) : 1;        // read per plan
+    const int genv = getenv("CGL_FUSE_GADAM") ? atoi(getenv("CGL_FUSE_GADAM")) : 0;  // (its Adam rides in a GEMM)
+    c->z_ahead = cf.gen_z && zenv && !genv && !c->two_streams;
+  }
   // ---- round prologue: per-round scalars, z draw, real-batch sampling (one launch)
   const int* real_idx = c->bufs.real_idx;
   {
@@ -1017,7 +1036,7 @@ int build_plan(cgl_gan* c) {
     Lp.begin.b2 = cf.beta2;
     Lp.begin.scaling = cf.loss_scale > 0.f ? 1 : 0;
     Lp.begin.growth_interval = cf.scale_growth_interval > 0 ? cf.scale_growth_interval : 2000;
-    if (cf.gen_z) {
+    if (cf.gen_z && !c->z_ahead) {
       Lp.nptr = c->bufs.z;
       Lp.nn = (long)2 * B * g.dims[0];
       Lp.nb_norm = (int)((Lp.nn / 4 + 255) / 256);
@@ -1044,7 +1063,12 @@ int build_plan(cgl_gan* c) {
     CglGemmDesc e = make_gemm(0, 2 * B, fo, fi);
     if (l + 1 < L && g.bn[l] && B < 64) choose_tiles(e, 1);  // keep producer tiles <= one call
     if (l == 0) {
-      e.a = rows(c->bufs.z, fi);
+      e.a = rows(c->z_ahead ? w.znext : c->bufs.z, fi);
+      if (c->z_ahead) {           // the round's z rows copied out to bufs.z as the GEMM loads them
+        e.a_copy = c->bufs.z;
+        e.a_copy_ld = fi;
+        e.a_copy_row0 = 0;
+      }
     } else {
       e.a = rows(w.gout[l - 1], fi);
     }
@@ -1515,6 +1539,14 @@ int build_plan(cgl_gan* c) {
   param_layout(g, &ng);
   push_adam(c, *ph, c->bufs.g_params, c->bufs.g_grads, c->bufs.g_m, c->bufs.g_v, (long)ng, &st->g_step_size,
             &st->g_bc2sqrt, 1, scaling ? &st->scale[1] : nullptr, scaling ? &st->found[1] : nullptr);
+  if (c->z_ahead) {
+    Launch& Ag = ph->back();
+    Ag.adam.znext = w.znext;
+    Ag.adam.nz = (long)2 * B * g.dims[0];
+    Ag.adam.zseed = cf.seed;
+    Ag.adam.zblk0 = Ag.grid;
+    Ag.grid += (int)((Ag.adam.nz / 4 + 255) / 256);
+  }
   fuse_wgrad_adam(c, *ph, CGL_MODEL_G);
   // the packing jobs run as the round prologue's last blocks
   {
@@ -1559,20 +1591,20 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
                   L.dt, L.abn);
       break;
     case K_HEAD:
-      klaunch(cgl_head_loss, dim3(L.grid), dim3(256), 0, s, c->ws.head + L.first);
+      klaunch(cgl_head_loss, dim3(L.grid), dim3(256), 0, s, c->head[L.first]);
       break;
     case K_BNAPPLY:
-      klaunch(cgl_bn_apply, dim3(L.grid, L.grid_y), dim3(256), 0, s, c->ws.bna + L.first);
+      klaunch(cgl_bn_apply, dim3(L.grid, L.grid_y), dim3(256), 0, s, c->bna[L.first]);
       break;
     case K_BNBWD:
       if (L.blk == 16)
-        klaunch(cgl_bn_bwd16, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
+        klaunch(cgl_bn_bwd16, dim3(L.grid), dim3(256), 0, s, c->bnb[L.first]);
       else if (L.blk == 8)
-        klaunch(cgl_bn_bwd8, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
+        klaunch(cgl_bn_bwd8, dim3(L.grid), dim3(256), 0, s, c->bnb[L.first]);
       else if (L.blk == 4)
-        klaunch(cgl_bn_bwd4, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
+        klaunch(cgl_bn_bwd4, dim3(L.grid), dim3(256), 0, s, c->bnb[L.first]);
       else
-        klaunch(cgl_bn_bwd, dim3(L.grid), dim3(256), 0, s, c->ws.bnb + L.first);
+        klaunch(cgl_bn_bwd, dim3(L.grid), dim3(256), 0, s, c->bnb[L.first]);
       break;
     case K_ADAM:
       if (L.adpk)
@@ -1749,6 +1781,13 @@ int cgl_gan_create(const cgl_gan_config* cfg, const cgl_gan_buffers* bufs, cgl_g
   if (he == hipSuccess) he = hipMemset(c->ws.counters, 0, kCounters * sizeof(unsigned int));
   if (he == hipSuccess) he = hipMemset(c->ws.kcount, 0, kSplitKCounters * sizeof(unsigned int));
   if (he == hipSuccess) he = hipMemset(c->ws.st, 0, sizeof(CglStepState));
+  if (he == hipSuccess && c->z_ahead) {   // round 1's z
+    const long nz = (long)2 * cfg->batch * cfg->g.dims[0];
+    hipLaunchKernelGGL(cgl_znext_draw, dim3((unsigned)((nz / 4 + 255) / 256)), dim3(256), 0, nullptr, c->ws.znext, nz,
+                       cfg->seed, (const CglStepState*)c->ws.st);
+    he = hipGetLastError();
+    if (he == hipSuccess) he = hipDeviceSynchronize();
+  }
   if (he == hipSuccess) he = hipDeviceSynchronize();
   if (he != hipSuccess) {
     delete c;
@@ -1783,6 +1822,12 @@ int cgl_gan_reset(cgl_gan* c, const float* beta_host, void* stream) {
     hipLaunchKernelGGL(cgl_pack_all, dim3(c->pack_all.blocks), dim3(256), 0, s, c->pack_all);
     HIPCHK(hipGetLastError());
   }
+  if (c->z_ahead) {                                   // the next round's z from the (reset) round counter
+    const long nz = (long)2 * c->cfg.batch * c->cfg.g.dims[0];
+    hipLaunchKernelGGL(cgl_znext_draw, dim3((unsigned)((nz / 4 + 255) / 256)), dim3(256), 0, s, c->ws.znext, nz,
+                       c->cfg.seed, (const CglStepState*)c->ws.st);
+    HIPCHK(hipGetLastError());
+  }
   HIPCHK(hipStreamSynchronize(s));
   return CGL_OK;
 }
@@ -1800,8 +1845,13 @@ int64_t cgl_gan_gemm_trace(cgl_gan* c, unsigned long long* host_out, int64_t n) 
 int cgl_gan_sync_params(cgl_gan* c, void* stream) {
   CGL_BATCH_GUARD();
   if (!c) return CGL_E_ARG;
-  if (!c->pack_adam || c->pack_all.blocks == 0) return CGL_OK;   // the prologue re-packs every round
-  hipLaunchKernelGGL(cgl_pack_all, dim3(c->pack_all.blocks), dim3(256), 0, (hipStream_t)stream, c->pack_all);
+  if (c->pack_adam && c->pack_all.blocks > 0)   // (otherwise the prologue re-packs every round)
+    hipLaunchKernelGGL(cgl_pack_all, dim3(c->pack_all.blocks), dim3(256), 0, (hipStream_t)stream, c->pack_all);
+  if (c->z_ahead) {
+    const long nz = (long)2 * c->cfg.batch * c->cfg.g.dims[0];
+    hipLaunchKernelGGL(cgl_znext_draw, dim3((unsigned)((nz / 4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       c->ws.znext, nz, c->cfg.seed, (const CglStepState*)c->ws.st);
+  }
   return (int)hipGetLastError();
 }
 

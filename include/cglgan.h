@@ -142,8 +142,10 @@ int cgl_gan_reset(cgl_gan* ctx, const float* beta_host, void* stream);
 /* G's GEMMs read fragment-packed copies of its weight matrices, which the G Adam launch writes as it updates
  * the parameters (the round prologue packed them every round before round 5).  After writing G's parameters
  * from OUTSIDE the round -- loading a state dict, an initialisation, the Cloud FedAvg (mixed-gan.py:104-124) --
- * call this once (stream-ordered, no host sync) before the next round; cgl_gan_reset does it too.  A no-op when
- * the plan keeps the prologue packing (CGL_PACK_ADAM=0, or shapes it does not cover). */
+ * call this once (stream-ordered, no host sync) before the next round; cgl_gan_reset does it too.  It also
+ * redraws the next round's z (gen_z: the G Adam launch draws round r + 1's z at the end of round r; after the
+ * device round state was written from outside -- a resumed run -- call this so that z follows the loaded round
+ * counter).  Cheap and idempotent between rounds. */
 int cgl_gan_sync_params(cgl_gan* ctx, void* stream);
 /* Diagnostics: with CGL_GEMM_TRACE=1 in the environment at create time and a library built with
  * -DCGL_GEMM_TRACE (tools/build_variant.sh), every GEMM workgroup of the last round stamps the 100 MHz wall
