@@ -119,9 +119,7 @@ def profile_inround(step, world, rounds, ex=None):
             runs.append(step.profile_round(PHASE_ALL))
         else:
             a = step.profile_round(PHASE_A)
-            ex.comm.all_gather(step.losses_all, step.own_loss())
-            step.alpha_scale()
-            ex.comm.all_reduce_sum(step.exchange_buffer())
+            ex.exchange_mid()
             runs.append(a + step.profile_round(PHASE_B))
     med = [sorted(col)[len(col) // 2] for col in zip(*runs)]
     per_kind = {}

@@ -15,6 +15,10 @@ round's queue traffic becomes collectives:
     server group, plus the Cloud's data-size-weighted trunk average every cloud_epoch rounds
     (mixed-gan.py:104-124, 193-200; the reference's load of it is a no-op, SURVEY F4, kept
     reproducible with ``fedavg_compat_noop``).
+  Gathered form (``exchange="gather"``, the default for groups of up to GATHER_MAX_WORKERS): ONE
+    all_gather of every worker's [gradient | loss] slot replaces the loss all_gather, alpha and the
+    gradient all_reduce; phase B starts with the alpha + rank-ordered weighted sum on device
+    (cgl_gan_exchange_mode), so the sum no longer depends on the collective's reduction order.
   E-share (new behaviour): mean of the D parameters every E rounds.
   D-swap (MD-GAN, MDGAN/MNIST/mdgan.py:158-164, 258-262 -- commented out in the reference, parity
     unpinned): every E rounds the server shuffles the N discriminators with Random(server + 100) and
@@ -26,12 +30,19 @@ tests).  Both expose the same three collectives, so ``WorkerExchange`` is writte
 """
 from __future__ import annotations
 
+import os
 import random
 
 import torch
 import torch.distributed as dist
 
 from . import _lib as C
+
+
+# Largest group that takes the gathered exchange by default: each rank receives (N - 1) gradient slots (N = 8:
+# 5.6 MB of a B = 256 round) where the ring all-reduce moves 2 (N - 1) / N of one (1.4 MB); up to 4 workers the
+# removed loss all_gather and alpha launch outweigh the extra bytes on xGMI, beyond that the reduce form is kept.
+GATHER_MAX_WORKERS = 4
 
 
 class DistComm:
@@ -41,6 +52,8 @@ class DistComm:
         self.group = group
         self.rank = dist.get_rank(group)
         self.size = dist.get_world_size(group)
+        # RCCL collectives can be captured into a graph (WorkerExchange.round_graph); gloo's cannot
+        self.capturable = dist.get_backend(group) == "nccl"
 
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor):
         dist.all_gather_into_tensor(out, inp, group=self.group)
@@ -108,7 +121,7 @@ class WorkerExchange:
     def __init__(self, step, comm=None, share_every: int = 0, cloud=None, cloud_every: int = 0,
                  cloud_weights=None, fedavg_compat_noop: bool = False, swap_every: int = 0,
                  cloud_scope: str = "trunk", segema: float = 0.0, cloud_due=None, server_rank: int = 0,
-                 force_split: bool = False):
+                 force_split: bool = False, exchange: str = "auto"):
         self.step = step
         self.comm = comm
         # test hook: take the N > 1 path (phase A, collectives, phase B) even in a one-rank group, so a
@@ -127,6 +140,33 @@ class WorkerExchange:
         n = comm.size if comm is not None else 1
         if n != step.n_workers:
             raise ValueError(f"step planned for {step.n_workers} workers, group has {n}")
+        if exchange not in ("auto", "gather", "reduce"):
+            raise ValueError("exchange must be 'auto', 'gather' or 'reduce'")
+        if exchange == "auto":
+            exchange = "gather" if n <= GATHER_MAX_WORKERS and hasattr(step, "set_exchange") else "reduce"
+        if exchange == "gather" and comm is not None:
+            step.set_exchange("gather")
+        self.exchange = exchange
+        # whole-round graph (graph=True rounds without a D exchange): phase A, this rank's collective(s) and phase B
+        # captured as ONE torch CUDA graph once a split round has run eagerly through the group (RCCL's
+        # communicator and buffers exist), replayed after -- the library's two graph launches, the collective
+        # calls and (reduce form) the alpha launch leave the host path.  Only over a capturable group (RCCL);
+        # CGL_ROUND_GRAPH=0 keeps the split path.
+        self.round_graph = (os.environ.get("CGL_ROUND_GRAPH", "1") != "0" and
+                            bool(getattr(comm, "capturable", False)) and hasattr(step, "g_params") and
+                            step.g_params.is_cuda)
+        self._rgraph, self._split_ran = None, False
+
+    def exchange_mid(self):
+        """The collectives between phase A and phase B of one round (this rank's side)."""
+        s = self.step
+        if self.exchange == "gather":
+            send, recv = s.gather_buffers()
+            self.comm.all_gather(recv, send)
+        else:
+            self.comm.all_gather(s.losses_all, s.own_loss())
+            s.alpha_scale()
+            self.comm.all_reduce_sum(s.exchange_buffer())
 
     def round(self, r: int, graph: bool = True):
         s = self.step
@@ -136,11 +176,15 @@ class WorkerExchange:
         swap = self.dswap is not None and (r + 1) % self.swap_every == 0
         if self.comm is None or (self.comm.size == 1 and not self.force_split):
             s.run(C.PHASE_ALL, graph=graph)
+        elif graph and self.round_graph and self._split_ran and not (share or swap):
+            if self._rgraph is None:
+                self._rgraph = self._capture_round()
+            s._packed_current()          # (host-side check of G's packed copies, as s.run does)
+            self._rgraph.replay()
         else:
+            self._split_ran = True
             s.run(C.PHASE_A, graph=graph)
-            self.comm.all_gather(s.losses_all, s.own_loss())
-            s.alpha_scale()
-            self.comm.all_reduce_sum(s.exchange_buffer())
+            self.exchange_mid()
             side = self._side_stream() if (share or swap) else None
             if side is not None:
                 # phase B (G backward + Adam G) never touches D: the E-share all-reduce / D-swap of
@@ -159,6 +203,16 @@ class WorkerExchange:
         if (self.cloud is not None and self.cloud_due is None and self.cloud_every > 0 and
                 (r + 1) % self.cloud_every == 0):
             self.cloud_average()
+
+    def _capture_round(self):
+        s = self.step
+        s._packed_current()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):       # (captures only: the caller replays it for this round)
+            s.run(C.PHASE_A, graph=False)
+            self.exchange_mid()
+            s.run(C.PHASE_B, graph=False)
+        return g
 
     def _d_exchange(self, r, share, swap):
         s = self.step

@@ -275,6 +275,25 @@ class GanStep:
     def alpha_scale(self):
         C.check(C.lib.cgl_gan_alpha_scale(self._h, _stream()), "cgl_gan_alpha_scale")
 
+    exchange_mode = "reduce"
+
+    def set_exchange(self, mode):
+        """"reduce": the caller gathers the losses, calls alpha_scale and all-reduces exchange_buffer();
+        "gather": the caller all-gathers gather_buffers()[0] into gather_buffers()[1] and phase B combines
+        (include/cglgan.h cgl_gan_exchange_mode)."""
+        C.check(C.lib.cgl_gan_exchange_mode(self._h, {"reduce": 0, "gather": 1}[mode]), "cgl_gan_exchange_mode")
+        self.exchange_mode = mode
+
+    def gather_buffers(self):
+        """(send [slot], recv [n_workers * slot]): this worker's [exchange gradient | G loss | pad] slot, written
+        by phase A, and the all-gather target phase B's combine reads."""
+        if getattr(self, "_gbufs", None) is None:
+            s, r, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
+            C.check(C.lib.cgl_gan_gather_buffers(self._h, ctypes.byref(s), ctypes.byref(r), ctypes.byref(n)),
+                    "cgl_gan_gather_buffers")
+            self._gbufs = (self._wrap(s.value, n.value), self._wrap(r.value, max(self.n_workers, 1) * n.value))
+        return self._gbufs
+
     def exchange_buffer(self):
         p, n = ctypes.c_void_p(), ctypes.c_int64()
         C.check(C.lib.cgl_gan_exchange_buffer(self._h, ctypes.byref(p), ctypes.byref(n)))
@@ -318,7 +337,8 @@ class GanStep:
         C.check(C.lib.cgl_gan_plan_info(self._h, phase, ctypes.byref(nl), ctypes.byref(ng), ctypes.byref(fl)))
         return {"launches": nl.value, "gemm_launches": ng.value, "gemm_flops": fl.value}
 
-    LAUNCH_KINDS = {0: "gemm", 1: "head", 2: "bn_bwd", 3: "adam", 4: "prologue", 5: "bn_apply", 6: "gemm_adam", 7: "gemm_prologue"}
+    LAUNCH_KINDS = {0: "gemm", 1: "head", 2: "bn_bwd", 3: "adam", 4: "prologue", 5: "bn_apply", 6: "gemm_adam", 7: "gemm_prologue",
+                    8: "alpha_combine"}
 
     def launches(self, phase=C.PHASE_ALL):
         """[(kind, flops, grid)] of the planned launches of a phase, in stream order."""

@@ -218,6 +218,7 @@ struct CglHeadDesc {
   unsigned int* counter;  // last-arriver ticket (zero at rest)
   float* loss_out0;       // mean loss of segment 0 / 1 (written by the last workgroup), may be null
   float* loss_out1;
+  float* loss_out2;       // a second copy of segment 0's mean (the exchange slot's loss word), may be null
   const float* scale_dev; // dynamic loss scaling: the dlogits (and dP) carry this factor, the loss does not
   float combine;          // D_loss = (seg0 + seg1) * combine  (0.5: capgan.py:339, 1: CGLGAN/2DMG/main.py:364)
   float* combine_out;     // optional

@@ -45,6 +45,7 @@ __device__ void cgl_head_finish(const CglHeadDesc* __restrict__ hd, int nwg, flo
     const float l0 = n0 > 0 ? (float)(s0 / n0) : (hd->combine_in0 ? gld(hd->combine_in0) : 0.f);
     const float l1 = n1 > 0 ? (float)(s1 / n1) : 0.f;
     if (hd->loss_out0 && n0 > 0) gst(hd->loss_out0, l0);
+    if (hd->loss_out2 && n0 > 0) gst(hd->loss_out2, l0);
     if (hd->loss_out1 && n1 > 0) gst(hd->loss_out1, l1);
     if (hd->combine_out) gst(hd->combine_out, (l0 + l1) * hd->combine);
   }
@@ -815,6 +816,46 @@ __global__ __launch_bounds__(256) void cgl_alpha_scale(CglStepState* st, const f
   const float a = s_alpha;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     x[i] *= a;
+}
+
+// The gathered exchange (cgl_gan_exchange_mode 1), the head of phase B: slot q of g holds worker q's
+// unscaled exchange gradient (n floats) followed by its G loss (word n).  alpha from the N losses exactly as
+// cgl_alpha_scale computes it, then x = sum_q alpha_q g_q summed in rank order with every product rounded
+// (tot = a_0 g_0; tot += a_1 g_1; ...): bitwise what cgl_alpha_scale on each worker followed by LocalComm's
+// rank-ordered sum gives, and the same on every rank (no reduction order left to the collective).
+__global__ __launch_bounds__(256) void cgl_alpha_combine(CglStepState* st, const float* __restrict__ g, long slot,
+                                                         long n, float* __restrict__ x) {
+#pragma clang fp contract(off)
+  __shared__ float al[CGL_MAX_WORKERS], s_l[CGL_MAX_WORKERS], s_t[2][CGL_MAX_WORKERS];
+  const int N = st->n_workers;
+  if ((int)threadIdx.x < N) s_l[threadIdx.x] = g[threadIdx.x * slot + n];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    cgl_weights(st->weighting, N, st->lambda, st->beta, s_l, al, s_t[0], s_t[1]);
+    if (blockIdx.x == 0) {
+      for (int q = 0; q < N; ++q) {
+        st->losses[q] = s_l[q];
+        st->alphas[q] = al[q];
+      }
+      st->alpha = al[st->rank];
+    }
+  }
+  __syncthreads();
+  const long n4 = n >> 2;   // (n % 4 == 0 and 16-byte aligned slots: checked by the planner)
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const f32x4 v0 = *(gcf4p)(g + 4 * i);
+    const float a0 = al[0];
+    f32x4 t = {a0 * v0[0], a0 * v0[1], a0 * v0[2], a0 * v0[3]};
+    for (int q = 1; q < N; ++q) {
+      const f32x4 v = *(gcf4p)(g + q * slot + 4 * i);
+      const float a = al[q];
+      t[0] = t[0] + a * v[0];
+      t[1] = t[1] + a * v[1];
+      t[2] = t[2] + a * v[2];
+      t[3] = t[3] + a * v[3];
+    }
+    *(gf4p)(x + 4 * i) = t;
+  }
 }
 
 // y[i] = sum over `parts` contiguous buffers (loopback reduction used by single-device

@@ -135,6 +135,16 @@ constexpr int kSplitKCounters = 8192;           // split-K tickets (one per tile
 constexpr int kCounters = 64;                    // head-loss tickets
 constexpr int64_t kSplitKFloats = 4 << 20;       // split-K partials of one launch (16 MiB)
 
+// An exchange buffer (dYL, or a Mix-G trunk gradient gdA / gG) is followed by kXchgPad floats: the gathered
+// exchange (cgl_gan_exchange_mode 1) sends [gradient | G loss | padding] as one slot of xchg_slot(n) floats.
+constexpr int64_t kXchgPad = 64;
+inline int64_t xchg_slot(int64_t n) { return (n + 1 + 63) & ~(int64_t)63; }
+inline int64_t xchg_slot_max(const cgl_gan_config& c) {
+  int f = c.g.dims[c.g.n_layers];
+  for (int l = 1; l < c.g.n_layers; ++l) f = std::max(f, c.g.dims[l]);
+  return xchg_slot((int64_t)c.batch * f);
+}
+
 struct WS {
   float* znext;                     // z_ahead: the next round's z [2B][z_dim], drawn by the G Adam launch
   // G forward (2B rows)
@@ -166,6 +176,7 @@ struct WS {
   float* wpk[CGL_MAX_LAYERS];       // packed G weights P(W_l; fo, fi) (the forward GEMM's B)
   float* wtpk[CGL_MAX_LAYERS];      // packed transposed G weights P(W_l^T; fi, fo) (input-gradient B)
   float* gGpk[CGL_MAX_LAYERS];      // packed cgl_bn_bwd output P(dZ_l; B, f) (input-gradient A)
+  float* gath;                      // gathered exchange: n_workers slots of xchg_slot_max() floats
   CglStepState* st;
   int* idx;       // sampler output when sample_n > 0
   CglGemmDesc* gemm;
@@ -197,9 +208,9 @@ WS carve_ws(const cgl_gan_config& c, void* base) {
       w.gpart[l] = cv.take<float>(tiles * 2 * f * 2);
       w.gmean[l] = cv.take<float>((int64_t)2 * f);
       w.ginvstd[l] = cv.take<float>((int64_t)2 * f);
-      w.gdA[l] = cv.take<float>((int64_t)B * f);
+      w.gdA[l] = cv.take<float>((int64_t)B * f + kXchgPad);
     }
-    if (l + 1 < L) w.gG[l] = cv.take<float>((int64_t)B * f);
+    if (l + 1 < L) w.gG[l] = cv.take<float>((int64_t)B * f + kXchgPad);
   }
   w.R = cv.take<float>((int64_t)Md * d.dims[0]);
   for (int j = 0; j + 1 < J; ++j) {
@@ -210,11 +221,12 @@ WS carve_ws(const cgl_gan_config& c, void* base) {
     w.dS[j] = cv.take<float>((int64_t)B * f);
   }
   w.dlog = cv.take<float>((int64_t)Md * d.dims[J]);
-  w.dYL = cv.take<float>((int64_t)B * g.dims[L]);
+  w.dYL = cv.take<float>((int64_t)B * g.dims[L] + kXchgPad);
   w.hpart = cv.take<float>((int64_t)((Md + kHeadRows - 1) / kHeadRows) * 2);
   w.hpart2 = cv.take<float>((int64_t)((Md + kHeadRows - 1) / kHeadRows) * 2);
   w.idx = cv.take<int>((int64_t)c.epoch * c.batch_real);
   w.znext = cv.take<float>((int64_t)2 * B * g.dims[0]);
+  w.gath = cv.take<float>((int64_t)std::max(c.n_workers, 1) * xchg_slot_max(c));
   // split-K scratch last, so that the layout of everything the default plan touches is unchanged
   w.kpart = cv.take<float>(kSplitKFloats);
   w.kcount = cv.take<unsigned int>(kSplitKCounters);
@@ -231,7 +243,7 @@ WS carve_ws(const cgl_gan_config& c, void* base) {
 }
 
 // ----------------------------------------------------------------------------------------
-enum LaunchKind { K_GEMM, K_HEAD, K_BNBWD, K_ADAM, K_PROLOGUE, K_BNAPPLY, K_GEMM_ADAM, K_GEMM_PRO };
+enum LaunchKind { K_GEMM, K_HEAD, K_BNBWD, K_ADAM, K_PROLOGUE, K_BNAPPLY, K_GEMM_ADAM, K_GEMM_PRO, K_COMBINE };
 
 struct Launch {
   LaunchKind kind;
@@ -523,6 +535,9 @@ struct cgl_gan {
   bool two_streams = false;
   float* xchg = nullptr;
   int64_t xchg_n = 0;
+  int xmode = 0;                     // cgl_gan_exchange_mode: 0 reduce (alpha_scale + all-reduce), 1 gathered
+  int ghead = -1;                    // the G-loss head descriptor (its loss_out2 = the exchange slot's loss word)
+  std::vector<Launch> phBhead;       // phase B's head under xmode 1: cgl_alpha_combine
   // parameter tensor pointers
   std::vector<TensorRec> gl, dl;
   int64_t run_mean_off[CGL_MAX_LAYERS], run_var_off[CGL_MAX_LAYERS];
@@ -1345,6 +1360,7 @@ int build_plan(cgl_gan* c) {
     h.part = w.hpart;
     h.counter = w.counters + CGL_MAX_EPOCH;
     h.loss_out0 = &st->g_loss_parts[0];
+    c->ghead = (int)c->head.size();
     h.combine = 1.0f;
     h.scale_dev = scaling ? &st->scale[1] : nullptr;
     h.rows_per_wg = kHeadRows;
@@ -1593,6 +1609,10 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
     case K_HEAD:
       klaunch(cgl_head_loss, dim3(L.grid), dim3(256), 0, s, c->head[L.first]);
       break;
+    case K_COMBINE:
+      klaunch(cgl_alpha_combine, dim3(L.grid), dim3(256), 0, s, c->ws.st, (const float*)c->ws.gath,
+              (long)xchg_slot(c->xchg_n), (long)c->xchg_n, c->xchg);
+      break;
     case K_BNAPPLY:
       klaunch(cgl_bn_apply, dim3(L.grid, L.grid_y), dim3(256), 0, s, c->bna[L.first]);
       break;
@@ -1648,6 +1668,11 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
 int run_phase(cgl_gan* c, int phase, hipStream_t s) {
   if (phase == CGL_PHASE_ALL || phase == CGL_PHASE_A)
     for (auto& L : c->phA) {
+      const int e = exec_launch(c, L, s);
+      if (e) return e;
+    }
+  if (phase == CGL_PHASE_B && c->xmode == 1)
+    for (auto& L : c->phBhead) {
       const int e = exec_launch(c, L, s);
       if (e) return e;
     }
@@ -1753,6 +1778,15 @@ int cgl_gan_create(const cgl_gan_config* cfg, const cgl_gan_buffers* bufs, cgl_g
   if (e) {
     delete c;
     return e;
+  }
+  // the gathered exchange (cgl_gan_exchange_mode 1): the G-loss head also writes the loss into the word after the
+  // exchange gradient, and phase B can start with cgl_alpha_combine over the gathered slots
+  if (c->xchg && c->ghead >= 0 && c->xchg_n % 4 == 0 && xchg_slot(c->xchg_n) <= xchg_slot_max(c->cfg)) {
+    c->head[c->ghead].loss_out2 = c->xchg + c->xchg_n;
+    Launch L;
+    L.kind = K_COMBINE;
+    L.grid = (int)std::min<int64_t>((c->xchg_n / 4 + 255) / 256, 1024);
+    c->phBhead.push_back(L);
   }
   // diagnostics: per-workgroup wall-clock stamps of every GEMM problem (only a -DCGL_GEMM_TRACE build writes them)
   if (getenv("CGL_GEMM_TRACE") && atoi(getenv("CGL_GEMM_TRACE")) == 1) {
@@ -1925,6 +1959,27 @@ int cgl_gan_alpha_scale(cgl_gan* c, void* stream) {
   return e == hipSuccess ? 0 : (int)e;
 }
 
+int cgl_gan_exchange_mode(cgl_gan* c, int mode) {
+  CGL_BATCH_GUARD();
+  if (!c || (mode != 0 && mode != 1)) return CGL_E_ARG;
+  if (mode == 1 && c->phBhead.empty()) return CGL_E_STATE;
+  if (mode != c->xmode && c->gexec[CGL_PHASE_B]) {   // phase B's graph changes: re-captured on next use
+    (void)hipGraphExecDestroy(c->gexec[CGL_PHASE_B]);
+    c->gexec[CGL_PHASE_B] = nullptr;
+  }
+  c->xmode = mode;
+  return CGL_OK;
+}
+
+int cgl_gan_gather_buffers(cgl_gan* c, float** send, float** recv, int64_t* slot) {
+  if (!c || !send || !recv || !slot) return CGL_E_ARG;
+  if (c->phBhead.empty()) return CGL_E_STATE;
+  *send = c->xchg;
+  *recv = c->ws.gath;
+  *slot = xchg_slot(c->xchg_n);
+  return CGL_OK;
+}
+
 int cgl_gan_exchange_buffer(cgl_gan* c, float** ptr, int64_t* n) {
   if (!c || !ptr || !n) return CGL_E_ARG;
   *ptr = c->xchg;
@@ -2036,6 +2091,7 @@ int cgl_gan_plan_info(cgl_gan* c, int phase, int* n_launches, int* n_gemm, doubl
     }
   };
   if (phase == CGL_PHASE_ALL || phase == CGL_PHASE_A) acc(c->phA);
+  if (phase == CGL_PHASE_B && c->xmode == 1) acc(c->phBhead);
   if (phase == CGL_PHASE_ALL || phase == CGL_PHASE_B) acc(c->phB);
   if (n_launches) *n_launches = nl;
   if (n_gemm) *n_gemm = ngm;
@@ -2050,13 +2106,17 @@ static const std::vector<Launch>* phase_list(cgl_gan* c, int phase, int idx, int
     return &c->phA;
   }
   *local = phase == CGL_PHASE_ALL ? idx - (int)c->phA.size() : idx;
+  if (phase == CGL_PHASE_B && c->xmode == 1) {   // phase B under the gathered exchange: the combine head first
+    if (*local < (int)c->phBhead.size()) return &c->phBhead;
+    *local -= (int)c->phBhead.size();
+  }
   return &c->phB;
 }
 
 int cgl_gan_launch_count(cgl_gan* c, int phase) {
   if (!c || phase < 0 || phase > 2) return CGL_E_ARG;
   if (phase == CGL_PHASE_A) return (int)c->phA.size();
-  if (phase == CGL_PHASE_B) return (int)c->phB.size();
+  if (phase == CGL_PHASE_B) return (int)(c->phB.size() + (c->xmode == 1 ? c->phBhead.size() : 0));
   return (int)(c->phA.size() + c->phB.size());
 }
 

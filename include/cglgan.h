@@ -161,6 +161,16 @@ int cgl_gan_run_graph(cgl_gan* ctx, int phase, void* stream);
 /* Exchange step: alpha from losses_all (already gathered), then scale this worker's exchange
  * gradient by alpha[rank] in place, ready for an all-reduce(sum). */
 int cgl_gan_alpha_scale(cgl_gan* ctx, void* stream);
+/* Exchange form.  mode 0 (default, "reduce"): the caller gathers the N losses into losses_all, calls
+ * cgl_gan_alpha_scale and all-reduces (sum) the exchange buffer between phase A and phase B.  mode 1
+ * ("gathered"): the caller all-gathers each worker's slot (cgl_gan_gather_buffers: [exchange gradient | G loss |
+ * padding], slot floats, written by phase A) into the recv buffer [n_workers][slot]; phase B then starts with
+ * cgl_alpha_combine -- alpha from the gathered losses, exchange buffer = sum_q alpha_q g_q in rank order
+ * (products rounded, bitwise what mode 0 with a rank-ordered sum gives, identical on every rank).  One
+ * collective per round instead of two, and alpha runs inside phase B (and its graph).  Changing the mode
+ * drops phase B's captured graph.  CGL_E_STATE when the plan has no gathered form. */
+int cgl_gan_exchange_mode(cgl_gan* ctx, int mode);
+int cgl_gan_gather_buffers(cgl_gan* ctx, float** send, float** recv, int64_t* slot);
 /* The exchange gradient buffer (device pointer, float count). */
 int cgl_gan_exchange_buffer(cgl_gan* ctx, float** ptr, int64_t* n);
 /* Device pointer of an internal tensor: 0 = G output [2B][img] (Xd rows then Xg rows),

@@ -55,6 +55,8 @@ class OracleWorkerStep:
         if phase == C.PHASE_ALL:
             self.losses_all.copy_(self.own_loss())
             self.alpha_scale()
+        if phase == C.PHASE_B and self.exchange_mode == "gather":
+            self._combine()
         if phase in (C.PHASE_B, C.PHASE_ALL):
             self.G.zero_grad()
             self.Xg.backward(self._x)
@@ -67,7 +69,7 @@ class OracleWorkerStep:
     def own_loss(self):
         return self.loss.detach().reshape(1).clone()
 
-    def alpha_scale(self):
+    def _alpha(self):
         l = self.losses_all.clone()
         if self.weighting == "capgan":
             a = O.capgan_alpha(self.lsgd.lam.detach(), l, self.beta)
@@ -75,7 +77,36 @@ class OracleWorkerStep:
         else:
             a = torch.full((self.n_workers,), 1.0 / self.n_workers)
             self.F = float(l.mean())
-        self._x.mul_(a[self.rank])
+        return a
+
+    def alpha_scale(self):
+        self._x.mul_(self._alpha()[self.rank])
+
+    # the gathered exchange (GanStep.set_exchange("gather")): one all_gather of [gradient | loss | pad] slots,
+    # then alpha and the rank-ordered weighted sum at the start of phase B (cgl_alpha_combine)
+    exchange_mode = "reduce"
+
+    def set_exchange(self, mode):
+        self.exchange_mode = mode
+
+    def gather_buffers(self):
+        n = self._x.numel()
+        self._slot = (n + 1 + 63) // 64 * 64
+        send = torch.zeros(self._slot, dtype=self._x.dtype)
+        send[:n] = self._x.flatten()
+        send[n] = self.loss.detach()
+        self._recv = torch.zeros(self.n_workers * self._slot, dtype=self._x.dtype)
+        return send, self._recv
+
+    def _combine(self):
+        n = self._x.numel()
+        g = self._recv.view(self.n_workers, self._slot)
+        self.losses_all.copy_(g[:, n])
+        a = self._alpha()
+        tot = g[0, :n] * a[0]
+        for q in range(1, self.n_workers):
+            tot += g[q, :n] * a[q]
+        self._x = tot.view_as(self._x).clone()
 
     def exchange_buffer(self):
         return self._x

@@ -12,8 +12,10 @@ compared bitwise with the same rounds run without a group (a one-rank all_gather
     AND BatchNorm running statistics, against the same rounds run unsplit (ConvGanStep.run).
 The MD-GAN D-swap of a one-rank group is the identity permutation (DistComm.swap returns before any
 send / recv), so it has no RCCL coverage here; its semantics are tested over gloo (tests/test_dist_swap_fedavg.py).
-Also times the MLP B = 256 round with the forced split against the unsplit round (the fixed host / launch
-cost of the N > 1 structure: two graph launches, three collectives, the alpha kernel).
+  * the whole-round graph of WorkerExchange (phase A + the collective(s) + phase B captured as one torch CUDA
+    graph), both exchange forms, against the unsplit rounds.
+Also times the MLP B = 256 round with the forced split against the unsplit round (the fixed cost of the N > 1
+structure) in both exchange forms, with and without the whole-round graph.
 Prints "RCCL-WORLD1 OK ..." on success."""
 import json
 import os
@@ -53,10 +55,10 @@ def same(a, b, names):
         assert torch.equal(x, y), (name, (x - y).abs().max().item())
 
 
-def check_mlp_round():
+def check_mlp_round(exchange="gather"):
     from cglgan.exchange import DistComm, WorkerExchange
     a, b = mlp_step(), mlp_step()
-    ex = WorkerExchange(a, DistComm(), share_every=1, force_split=True)
+    ex = WorkerExchange(a, DistComm(), share_every=1, force_split=True, exchange=exchange)
     ref = WorkerExchange(b, None)
     for r in range(4):
         ex.round(r, graph=(r % 2 == 1))
@@ -116,12 +118,42 @@ def check_conv_round():
     return sa["g_loss"]
 
 
-def time_split(rounds=200):
-    """Device + host time per B = 256 round: forced split over RCCL vs the unsplit graph (both replayed)."""
+def _ex(s, exchange, round_graph):
     from cglgan.exchange import DistComm, WorkerExchange
-    out = {}
+    ex = WorkerExchange(s, DistComm(), force_split=True, exchange=exchange)
+    assert ex.round_graph        # (RCCL: capturable)
+    ex.round_graph = round_graph
+    return ex
+
+
+def check_round_graph(exchange):
+    """WorkerExchange's whole-round graph (phase A + collective(s) + phase B as one torch CUDA graph, captured
+    after the first split round): bitwise the unsplit rounds, graph and eager rounds interleaved."""
+    from cglgan.exchange import WorkerExchange
+    a, b = mlp_step(), mlp_step()
+    ex, ref = _ex(a, exchange, True), WorkerExchange(b, None)
+    for r in range(6):
+        ex.round(r, graph=(r != 3))
+        ref.round(r, graph=(r != 3))
+    torch.cuda.synchronize()
+    assert ex._rgraph is not None
+    same(a, b, ("g_params", "g_m", "g_v", "d_params", "d_m", "d_v", "g_running"))
+    assert a.stats()["round"] == b.stats()["round"] == 6
+
+
+def time_split(rounds=200):
+    """Device + host time per B = 256 round, all graph-replayed: the unsplit round vs the forced split over RCCL
+    in the reduce form (loss all_gather, alpha, gradient all_reduce) and the gathered form (one all_gather,
+    alpha + sum at phase B's head), each as two library graphs around the collective calls and as
+    WorkerExchange's whole-round graph.  Each form's state after the rounds is compared bitwise with the
+    unsplit one's."""
+    from cglgan.exchange import WorkerExchange
+    out, states = {}, {}
     for name, mk in (("unsplit", lambda s: WorkerExchange(s, None)),
-                     ("split_rccl", lambda s: WorkerExchange(s, DistComm(), force_split=True))):
+                     ("split_reduce", lambda s: _ex(s, "reduce", False)),
+                     ("split_gather", lambda s: _ex(s, "gather", False)),
+                     ("round_graph_reduce", lambda s: _ex(s, "reduce", True)),
+                     ("round_graph_gather", lambda s: _ex(s, "gather", True))):
         s = mlp_step(B=256, rows=60000)
         ex = mk(s)
         for r in range(20):
@@ -132,8 +164,14 @@ def time_split(rounds=200):
             ex.round(20 + r, graph=True)
         torch.cuda.synchronize()
         out[name] = (time.perf_counter() - t0) / rounds * 1e6
-    out["delta_us"] = out["split_rccl"] - out["unsplit"]
-    return {k: round(v, 2) for k, v in out.items()}
+        states[name] = (s.g_params.clone(), s.d_params.clone(), s.stats()["round"])
+    for name in list(states):
+        if name != "unsplit":
+            out["delta_" + name + "_us"] = out[name] - out["unsplit"]
+            gp, dp, rd = states[name]
+            out["bitwise_" + name] = bool(torch.equal(gp, states["unsplit"][0]) and
+                                          torch.equal(dp, states["unsplit"][1]) and rd == states["unsplit"][2])
+    return {k: (round(v, 2) if isinstance(v, float) else v) for k, v in out.items()}
 
 
 def main():
@@ -142,7 +180,10 @@ def main():
     assert dist.get_world_size() == 1 and dist.get_backend() == "nccl"
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
-        sa = check_mlp_round()
+        sa = check_mlp_round("gather")
+        check_mlp_round("reduce")
+        check_round_graph("gather")
+        check_round_graph("reduce")
         ga = check_cloud("capgan", "all")
         gt = check_cloud("mixg", "trunk")
         gc = check_conv_round()

@@ -36,7 +36,7 @@ def _inputs(r):
     return z1, z2, [rs[0] for rs in reals]
 
 
-def _worker(rank, port, outdir, kind, share_every):
+def _worker(rank, port, outdir, kind, share_every, exchange):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(1)
@@ -47,7 +47,7 @@ def _worker(rank, port, outdir, kind, share_every):
         from dist_oracle_step import OracleWorkerStep
         loss, weighting = ("ce", "capgan") if kind == "capgan" else ("bce", "mean")
         step = OracleWorkerStep(N, rank, loss=loss, weighting=weighting)
-        ex = WorkerExchange(step, DistComm(), share_every=share_every)
+        ex = WorkerExchange(step, DistComm(), share_every=share_every, exchange=exchange)
         Fs = []
         for r in range(ROUNDS):
             z1, z2, reals = _inputs(r)
@@ -93,11 +93,15 @@ def _rel(a, b):
     return float((a.double() - b.double()).norm() / max(float(b.double().norm()), 1e-30))
 
 
-@pytest.mark.parametrize("kind,share_every", [("capgan", 0), ("capgan", 1), ("mdgan", 2)])
-def test_two_worker_exchange_matches_oracle(kind, share_every):
+# exchange: "reduce" = loss all_gather, alpha, gradient all_reduce; "gather" = one all_gather of [gradient | loss]
+# slots, alpha and the rank-ordered weighted sum at the start of phase B (cglgan.exchange module docstring)
+@pytest.mark.parametrize("kind,share_every,exchange", [("capgan", 0, "reduce"), ("capgan", 0, "gather"),
+                                                       ("capgan", 1, "gather"), ("mdgan", 2, "reduce"),
+                                                       ("mdgan", 2, "gather")])
+def test_two_worker_exchange_matches_oracle(kind, share_every, exchange):
     port = _free_port()
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(port, d, kind, share_every), nprocs=N, join=True)
+        mp.spawn(_worker, args=(port, d, kind, share_every, exchange), nprocs=N, join=True)
         res = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(N)]
     G, workers, Fs = _reference(kind, share_every)
     # replicated G: bitwise identical on both ranks

@@ -1,6 +1,7 @@
 """WorkerExchange (the MLP round's cross-worker exchange) over a real process group with its E-share
 all-reduce and D-swap on a side stream, concurrent with phase B: two processes on the box's GPU,
-one CAPGAN worker (cglgan.GanStep, B=64) each, gloo on host-staged copies of the device tensors
+one CAPGAN worker (cglgan.GanStep, B=64) each, both exchange forms (gathered / reduce), gloo on host-staged
+copies of the device tensors
 (one GPU: RCCL needs one per rank), E-share every round and a D-swap every second round; compared
 BITWISE with the same two workers in one process through LocalComm (with two ranks a + b == b + a
 exactly, and the side stream must change nothing but the overlap)."""
@@ -71,7 +72,7 @@ class HostComm:
             t.copy_(h.to(t.device))
 
 
-def _proc(rank, world, port, outdir):
+def _proc(rank, world, port, outdir, exchange):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -79,7 +80,7 @@ def _proc(rank, world, port, outdir):
         from cglgan.exchange import WorkerExchange
         torch.cuda.set_device(0)
         st = _make(rank, world)
-        ex = WorkerExchange(st, HostComm(), share_every=1, swap_every=2)
+        ex = WorkerExchange(st, HostComm(), share_every=1, swap_every=2, exchange=exchange)
         for r in range(ROUNDS):
             ex.round(r, graph=True)
         torch.cuda.synchronize()
@@ -89,10 +90,13 @@ def _proc(rank, world, port, outdir):
         dist.destroy_process_group()
 
 
-def test_worker_exchange_side_stream_matches_local():
+# "gather": one all_gather of [gradient | loss] slots, alpha + the rank-ordered sum at phase B's head (on
+# device); "reduce": loss all_gather, alpha_scale, gradient all_reduce.  Both bitwise LocalComm's round.
+@pytest.mark.parametrize("exchange", ["gather", "reduce"])
+def test_worker_exchange_side_stream_matches_local(exchange):
     world = 2
     with tempfile.TemporaryDirectory() as td:
-        mp.spawn(_proc, args=(world, _free_port(), td), nprocs=world, join=True)
+        mp.spawn(_proc, args=(world, _free_port(), td, exchange), nprocs=world, join=True)
         res = [torch.load(os.path.join(td, f"r{r}.pt"), weights_only=True) for r in range(world)]
     from cglgan.exchange import LocalComm
     steps = [_make(r, world) for r in range(world)]
