@@ -545,6 +545,16 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     y_base[i] = ybn ? ((LAYOUT != 2) ? ybase + (long)min(am, M - 1) * ldy : ybase + min(am, M - 1)) : a_base[i];
     copy_row[i] = (LAYOUT != 2) && a_copy && am < M && am >= h_crow0;
   }
+  // A copy-out in the main loop (full chunks, 16-byte form) as buffer stores whose offset is pushed out of range
+  // for the lanes / chunks that do not write: no branch in the loop body, so every s_waitcnt there still counts
+  // exactly the loads of the set it consumes (a conditional store made the compiler drain vmcnt(0) at the top of
+  // every rotation).  The range check drops the out-of-range stores.
+  const auto rc_copy = __builtin_amdgcn_make_buffer_rsrc(a_copy ? a_copy : const_cast<float*>(h_a.p0), (short)0,
+                                                         0x7fffffff, 0x00020000);
+  unsigned copy_off[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+    copy_off[i] = copy_row[i] ? (unsigned)((m0 + 32 * i + li) * d->a_copy_ld) * 4u : 0x7fffffffu;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int bc = n0 + 32 * j + li;      // B row (NT) or B column (NN/TN)
@@ -671,7 +681,11 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
     for (int i = 0; i < TM; ++i) {
       if (T) cgl_mask(A_[i], true, k, K);
       if constexpr (!decltype(fl)::CP) continue;
-      if (copy_row[i] && (c % copy_n) == copy_me) {
+      if (VEC && !T) {
+        const unsigned off = (c % copy_n) == copy_me ? copy_off[i] + 4u * k : 0x7fffffffu;
+        __builtin_amdgcn_raw_buffer_store_b128(f32x4{A_[i][0], A_[i][1], A_[i][2], A_[i][3]}, rc_copy, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(f32x4{A_[i][4], A_[i][5], A_[i][6], A_[i][7]}, rc_copy, off + 16u, 0, 0);
+      } else if (copy_row[i] && (c % copy_n) == copy_me) {
         float* dst = a_copy + (long)(m0 + 32 * i + li) * d->a_copy_ld;
         if (VEC && (!T || k + 7 < K)) {
           *(gf4p)(dst + k) = f32x4{A_[i][0], A_[i][1], A_[i][2], A_[i][3]};

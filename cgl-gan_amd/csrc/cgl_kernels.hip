@@ -53,7 +53,7 @@ __device__ void cgl_head_finish(const CglHeadDesc* __restrict__ hd, int nwg, flo
 
 #define CGL_HEAD_MAXQ 4   // float4 per lane kept in registers: F <= 1024
 #ifndef CGL_GEMM_PART_TU   // (the GEMM-instantiation translation units compile only device functions)
-__device__ __forceinline__ void cgl_head_loss_body(const CglHeadDesc* __restrict__ hd) {
+__device__ __forceinline__ void cgl_head_loss_body(const CglHeadDesc* __restrict__ hd, int bid, int nwg) {
   // Each wave owns rows r0 + wave + 4 i; a row is a dot product of F features (F % 4 == 0)
   // over 16-byte loads held in registers, a 64-lane reduction, the loss and its gradient, then
   // the gradient into the last hidden layer (dlogits . W) * LeakyReLU'(P) from the same
@@ -67,7 +67,7 @@ __device__ __forceinline__ void cgl_head_loss_body(const CglHeadDesc* __restrict
   const float wr0 = hd->n0_dev ? hd->combine / (float)n0 : hd->w0;   // real-segment dlogit weight
   const float lsc = hd->scale_dev ? gld(hd->scale_dev) : 1.f;         // dynamic loss scale (power of 2)
   const int lane = threadIdx.x & 63;
-  const int r0 = blockIdx.x * hd->rows_per_wg;
+  const int r0 = bid * hd->rows_per_wg;
   const int r1 = min(r0 + hd->rows_per_wg, M);
   const float* __restrict__ Pb = hd->P;
   const float* __restrict__ W = hd->W;
@@ -163,8 +163,8 @@ __device__ __forceinline__ void cgl_head_loss_body(const CglHeadDesc* __restrict
         a += s_loss[q][0];
         b += s_loss[q][1];
       }
-      gst(hd->part + blockIdx.x * 2 + 0, a);
-      gst(hd->part + blockIdx.x * 2 + 1, b);
+      gst(hd->part + bid * 2 + 0, a);
+      gst(hd->part + bid * 2 + 1, b);
     }
     return;
   }
@@ -176,18 +176,18 @@ __device__ __forceinline__ void cgl_head_loss_body(const CglHeadDesc* __restrict
     }
     // last-arriver reduction: partials are published with agent-coherent (sc1) stores and
     // complete before the ticket is taken; the last workgroup reads them back coherently
-    __hip_atomic_store((CGL_GLOBAL float*)(hd->part + blockIdx.x * 2 + 0), a, __ATOMIC_RELAXED,
+    __hip_atomic_store((CGL_GLOBAL float*)(hd->part + bid * 2 + 0), a, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((CGL_GLOBAL float*)(hd->part + blockIdx.x * 2 + 1), b, __ATOMIC_RELAXED,
+    __hip_atomic_store((CGL_GLOBAL float*)(hd->part + bid * 2 + 1), b, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned int ticket =
         __hip_atomic_fetch_add(hd->counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (ticket == gridDim.x - 1);
+    s_last = (ticket == nwg - 1);
   }
   __syncthreads();
   if (!s_last) return;
-  cgl_head_finish(hd, (int)gridDim.x, s_part);
+  cgl_head_finish(hd, nwg, s_part);
   if (threadIdx.x == 0) __hip_atomic_store(hd->counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 #endif   // CGL_GEMM_PART_TU
@@ -204,7 +204,7 @@ __device__ __forceinline__ void cgl_head_loss_body(const CglHeadDesc* __restrict
 // reference's forward calls (Xd then Xg, capgan.py:215-220).
 #define CGL_BNA_ROWS 32
 #ifndef CGL_GEMM_PART_TU   // (the GEMM-instantiation translation units compile only device functions)
-__device__ __forceinline__ void cgl_bn_apply_body(const CglBnApplyDesc* __restrict__ ad) {
+__device__ __forceinline__ void cgl_bn_apply_body(const CglBnApplyDesc* __restrict__ ad, int bx, int by) {
   __shared__ float s_sc[2][64], s_sh[2][64];
   __shared__ double s_mean[2][64], s_m2[2][64];
   __shared__ int s_n[2];
@@ -212,7 +212,7 @@ __device__ __forceinline__ void cgl_bn_apply_body(const CglBnApplyDesc* __restri
   const int F = ad->F, mtot = bn.mtot;
   const int ngroups = (mtot + bn.gr - 1) / bn.gr;   // <= 2
   const int tid = threadIdx.x, fl = tid & 63, rl = tid >> 6;
-  const int f0 = blockIdx.x * 64, r0 = blockIdx.y * CGL_BNA_ROWS;
+  const int f0 = bx * 64, r0 = by * CGL_BNA_ROWS;
   const int f = f0 + fl, fc = min(f, F - 1);
   // this thread's rows, loaded before the statistics are ready
   constexpr int RPT = CGL_BNA_ROWS / 4;
@@ -238,13 +238,13 @@ __device__ __forceinline__ void cgl_bn_apply_body(const CglBnApplyDesc* __restri
     s_mean[g][fl] = mean[0];
     s_m2[g][fl] = m2[0];
     if (fl == 0) s_n[g] = n;
-    if (blockIdx.y == 0 && f < F && bn.save_mean) {
+    if (by == 0 && f < F && bn.save_mean) {
       gst(bn.save_mean + (long)g * F + f, (float)mean[0]);
       gst(bn.save_invstd + (long)g * F + f, (float)invstd);
     }
   }
   __syncthreads();
-  if (blockIdx.y == 0 && bn.run_mean && tid < 64 && f < F) {
+  if (by == 0 && bn.run_mean && tid < 64 && f < F) {
     const double mom = bn.momentum;
     float rm = rm0, rv = rv0;
     for (int g = 0; g < ngroups; ++g) {
@@ -418,8 +418,12 @@ __device__ __forceinline__ void cgl_bn_bwd_body(const CglBnBwdDesc* __restrict__
 // The round's small kernels take their descriptor BY VALUE (the kernel arguments): its fields arrive with the
 // kernarg fetch instead of one more dependent scalar round trip to a descriptor in memory (tools/launch_probe.hip:
 // ~0.16 us per dependent scalar load).  The workspace copies stay (the deferred head reduction reads its head's).
-__global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc d) { cgl_head_loss_body(&d); }
-__global__ __launch_bounds__(256) void cgl_bn_apply(const CglBnApplyDesc d) { cgl_bn_apply_body(&d); }
+__global__ __launch_bounds__(256) void cgl_head_loss(const CglHeadDesc d) {
+  cgl_head_loss_body(&d, blockIdx.x, gridDim.x);
+}
+__global__ __launch_bounds__(256) void cgl_bn_apply(const CglBnApplyDesc d) {
+  cgl_bn_apply_body(&d, blockIdx.x, blockIdx.y);
+}
 __global__ __launch_bounds__(256) void cgl_bn_bwd(const CglBnBwdDesc d) { cgl_bn_bwd_body<32>(&d); }
 __global__ __launch_bounds__(256) void cgl_bn_bwd16(const CglBnBwdDesc d) { cgl_bn_bwd_body<16>(&d); }
 __global__ __launch_bounds__(256) void cgl_bn_bwd8(const CglBnBwdDesc d) { cgl_bn_bwd_body<8>(&d); }

@@ -85,6 +85,35 @@ __global__ __launch_bounds__(256) void cgl_pack_all(CglOpPack pk) {
   cgl_pack_job(pk.j[j], (long)(b - pk.j[j].blk_begin) * 256 + threadIdx.x);
 }
 
+// cgl_bn_apply with operand-packing jobs riding in blocks [nbn, grid) (plan_pack_carriers); blocks [0, nbn) are the
+// BatchNorm apply's (gx, nbn / gx) grid, row-major
+__global__ __launch_bounds__(256) void cgl_bn_apply_pk(const CglBnApplyDesc d, int gx, int nbn, const CglOpPack pk) {
+  const int b = blockIdx.x;
+  if (b < nbn) {
+    cgl_bn_apply_body(&d, b % gx, b / gx);
+    return;
+  }
+  const int q = b - nbn;
+  int j = 0;
+  for (int i = 1; i < pk.nj; ++i)
+    if (q >= pk.j[i].blk_begin) j = i;
+  cgl_pack_job(pk.j[j], (long)(q - pk.j[j].blk_begin) * 256 + threadIdx.x);
+}
+
+// a deferred cgl_head_loss (its partials reduced by the next launch) with packing jobs in blocks [nhead, grid)
+__global__ __launch_bounds__(256) void cgl_head_loss_pk(const CglHeadDesc d, int nhead, const CglOpPack pk) {
+  const int b = blockIdx.x;
+  if (b < nhead) {
+    cgl_head_loss_body(&d, b, nhead);
+    return;
+  }
+  const int q = b - nhead;
+  int j = 0;
+  for (int i = 1; i < pk.nj; ++i)
+    if (q >= pk.j[i].blk_begin) j = i;
+  cgl_pack_job(pk.j[j], (long)(q - pk.j[j].blk_begin) * 256 + threadIdx.x);
+}
+
 // G's Adam with the operand packing of the next round (CglAdamPack, plan flag pack_adam): the weight matrices
 // that carry packing jobs are updated in 4 x 4 tiles -- one thread loads 4 rows x 4 columns of p / g / m / v
 // with 16-byte loads, applies cgl_adam_update to each of the 16 values (the arithmetic of cgl_adam_at, element

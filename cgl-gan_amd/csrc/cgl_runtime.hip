@@ -267,6 +267,8 @@ struct Launch {
   int dt = CGL_DTYPE_F32;   // GEMM operand type (cgl_gan_config.gemm_dtype)
   int abn = 0;              // GEMM operand-transform instantiation (the launch's a_bn)
   bool adpk = false;        // K_ADAM: the cgl_adam_pack form (cgl_gan.adam_pack)
+  int layer = -1;           // K_BNAPPLY: the G layer whose forward GEMM reads this launch's output
+  int pk = -1;              // K_BNAPPLY: index of the packing jobs it carries (cgl_gan.carry), -1: none
 };
 
 // Every kernel of a plan is launched through klaunch.  Normally a plain launch; while cgl_gan_profile
@@ -529,6 +531,8 @@ struct cgl_gan {
   bool pack_adam = false;    // G's packed weights written by the G Adam launch (cgl_adam_pack), not the prologue
   bool z_ahead = false;      // z drawn one round ahead by the G Adam launch into ws.znext (plan_z_ahead)
   CglAdamPack adam_pack{};
+  std::vector<CglOpPack> carry;   // packing jobs carried by the forward cgl_bn_apply launches (plan_pack_carriers)
+  std::vector<int> pack_need;     // per prologue packing job: the G layer whose forward reads it (INT_MAX: backward)
   unsigned long long* trace = nullptr;   // CGL_GEMM_TRACE diagnostics buffer (kTraceWords per GEMM descriptor)
   int64_t trace_words = 0;
   hipEvent_t ev[2] = {nullptr, nullptr};   // fork (after the prologue), join (before the D-step head)
@@ -948,6 +952,59 @@ void fuse_prologue(cgl_gan* c) {
 // interleaved x3: 0.2433 vs 0.2403 ms): the prologue launch only loses 1.5 us (its packing blocks ran beside
 // G's first GEMM on otherwise idle CUs), while the bandwidth-bound G Adam grows 8.2 -> 13.7 us (the 11.6 MB of
 // packed writes, and 4 x 4 tiles per thread leave it too few waves).  Opt-in: CGL_PACK_ADAM=1.
+// The packing jobs ride in the forward cgl_bn_apply launches (CGL_PACK_CARRY, default on): those launches have
+// 4-16 workgroups on a latency chain of ~4.5 us and leave the chip's bandwidth idle, while in the round prologue
+// the jobs (G's packed weights P(W) / P(W^T), ~24 MB of traffic) lengthened the launch G's first GEMM rides in.
+// A job whose packed copy the forward GEMM of G layer l reads goes to a carrier ahead of that GEMM (carrier
+// layer <= l); the backward copies may go to any carrier.  Earliest deadline first, each job to the least loaded
+// carrier it may use (bytes), so the carriers' pack blocks stay within their own latency.  Returns false (all
+// jobs stay in the prologue) when there is no carrier; a job no carrier may take stays in the prologue.
+bool plan_pack_carriers(cgl_gan* c, std::vector<Launch>& A) {
+  const char* env = getenv("CGL_PACK_CARRY");
+  if ((env && atoi(env) == 0) || c->pack.nj == 0 || (int)c->pack_need.size() != c->pack.nj) return false;
+  // carriers: the forward cgl_bn_apply launches (layer = the G layer reading their output) and, for the backward
+  // copies only, the deferred loss heads of the D step / G-loss pass (layer INT_MAX - 1: after every G forward)
+  std::vector<Launch*> car;
+  bool gfwd_done = false;
+  for (auto& L : A) {
+    if (L.kind == K_BNAPPLY && L.layer >= 0) car.push_back(&L);
+    if (L.kind == K_HEAD) gfwd_done = true;
+    if (L.kind == K_HEAD && gfwd_done && c->head[L.first].deferred) {
+      L.layer = INT_MAX - 1;
+      car.push_back(&L);
+    }
+  }
+  if (car.empty()) return false;
+  std::vector<int> order(c->pack.nj);
+  for (int q = 0; q < c->pack.nj; ++q) order[q] = q;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return c->pack_need[a] < c->pack_need[b]; });
+  std::vector<double> load(car.size(), 0.0);
+  std::vector<CglOpPack> cp(car.size());
+  for (auto& p : cp) std::memset(&p, 0, sizeof(p));
+  CglOpPack rest;
+  std::memset(&rest, 0, sizeof(rest));
+  for (int q : order) {
+    const CglOpPackJob& J = c->pack.j[q];
+    int best = -1;
+    for (int k = 0; k < (int)car.size(); ++k)
+      if (car[k]->layer <= c->pack_need[q] && cp[k].nj < CGL_PACK_MAXJ && (best < 0 || load[k] < load[best])) best = k;
+    CglOpPack& dst = best >= 0 ? cp[best] : rest;
+    CglOpPackJob& D = dst.j[dst.nj++];
+    D = J;
+    D.blk_begin = dst.blocks;
+    dst.blocks += (int)((cgl_pk_floats(J.R, J.K) / 4 + 255) / 256);
+    if (best >= 0) load[best] += (double)cgl_pk_floats(J.R, J.K);
+  }
+  c->carry.clear();
+  for (size_t k = 0; k < car.size(); ++k) {
+    if (cp[k].nj == 0) continue;
+    car[k]->pk = (int)c->carry.size();
+    c->carry.push_back(cp[k]);
+  }
+  c->pack = rest;
+  return true;
+}
+
 bool plan_pack_adam(cgl_gan* c, std::vector<Launch>& ph) {
   const int env = getenv("CGL_PACK_ADAM") ? atoi(getenv("CGL_PACK_ADAM")) : 0;   // read per plan
   c->pack_adam = false;
@@ -1098,6 +1155,7 @@ int build_plan(cgl_gan* c) {
       J.K = fi;
       J.ld = fi;
       J.trans = 0;
+      c->pack_need.push_back(l);
       e.b_pk = 1;
     }
     if (pend_on) {
@@ -1122,6 +1180,7 @@ int build_plan(cgl_gan* c) {
           e.a_pk = 1;
         }
         push_bna(c, A, ap);
+        A.back().layer = l;
         e.a = rows(e.a_pk ? w.gpk[l - 1] : w.gact[l - 1], fi);
       }
       pend_on = false;
@@ -1470,6 +1529,7 @@ int build_plan(cgl_gan* c) {
         J.K = fo;
         J.ld = fi;
         J.trans = 1;
+        c->pack_need.push_back(INT_MAX);
         n.b = rows(w.wtpk[l], fo);
         n.b_pk = 1;
         if (l < L - 1 && gG_packed[l]) {
@@ -1564,6 +1624,7 @@ int build_plan(cgl_gan* c) {
     Ag.grid += (int)((Ag.adam.nz / 4 + 255) / 256);
   }
   fuse_wgrad_adam(c, *ph, CGL_MODEL_G);
+  defer_heads(c);      // (before the packing plan: the deferred heads can carry packing jobs)
   // the packing jobs run as the round prologue's last blocks
   {
     int blk = 0;
@@ -1577,13 +1638,16 @@ int build_plan(cgl_gan* c) {
     if (plan_pack_adam(c, *ph)) {      // the G Adam launch writes the packed copies: no prologue packing
       c->pack.nj = 0;
       c->pack.blocks = 0;
+    } else if (plan_pack_carriers(c, A)) {
+      blk = c->pack.blocks;            // (the jobs no carrier could take stay in the prologue)
+      for (auto& Lq : A)
+        if (Lq.kind == K_PROLOGUE) Lq.grid += blk;
     } else {
       for (auto& Lq : A)
         if (Lq.kind == K_PROLOGUE) Lq.grid += blk;
     }
   }
   fuse_prologue(c);
-  defer_heads(c);
   if ((int)c->gemm.size() > kMaxGemmDescs || (int)c->head.size() > kMaxHeadDescs ||
       (int)c->bnb.size() > kMaxBnDescs || (int)c->bna.size() > kMaxBnDescs)
     return CGL_E_SIZE;
@@ -1607,14 +1671,22 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
                   L.dt, L.abn);
       break;
     case K_HEAD:
-      klaunch(cgl_head_loss, dim3(L.grid), dim3(256), 0, s, c->head[L.first]);
+      if (L.pk >= 0)
+        klaunch(cgl_head_loss_pk, dim3(L.grid + c->carry[L.pk].blocks), dim3(256), 0, s, c->head[L.first], L.grid,
+                c->carry[L.pk]);
+      else
+        klaunch(cgl_head_loss, dim3(L.grid), dim3(256), 0, s, c->head[L.first]);
       break;
     case K_COMBINE:
       klaunch(cgl_alpha_combine, dim3(L.grid), dim3(256), 0, s, c->ws.st, (const float*)c->ws.gath,
               (long)xchg_slot(c->xchg_n), (long)c->xchg_n, c->xchg);
       break;
     case K_BNAPPLY:
-      klaunch(cgl_bn_apply, dim3(L.grid, L.grid_y), dim3(256), 0, s, c->bna[L.first]);
+      if (L.pk >= 0)
+        klaunch(cgl_bn_apply_pk, dim3(L.grid * L.grid_y + c->carry[L.pk].blocks), dim3(256), 0, s, c->bna[L.first],
+                L.grid, L.grid * L.grid_y, c->carry[L.pk]);
+      else
+        klaunch(cgl_bn_apply, dim3(L.grid, L.grid_y), dim3(256), 0, s, c->bna[L.first]);
       break;
     case K_BNBWD:
       if (L.blk == 16)
@@ -2127,7 +2199,10 @@ int cgl_gan_launch_info(cgl_gan* c, int phase, int idx, int* kind, double* flops
   const Launch& L = (*v)[li];
   if (kind) *kind = (int)L.kind;
   if (flops) *flops = L.flops;
-  if (grid) *grid = L.grid;
+  if (grid) {   // workgroups dispatched (2-D BatchNorm grids flattened, carried packing blocks included)
+    *grid = L.kind == K_BNAPPLY ? L.grid * L.grid_y : L.grid;
+    if ((L.kind == K_BNAPPLY || L.kind == K_HEAD) && L.pk >= 0) *grid += c->carry[L.pk].blocks;
+  }
   return CGL_OK;
 }
 

@@ -19,10 +19,11 @@ pytestmark = pytest.mark.gpu
 NAMES = ("g_params", "g_grads", "g_m", "g_v", "d_params", "d_m", "d_v", "g_running", "z")
 
 
-def _step(on, B=256, kind="capgan", **kw):
+def _step(on, B=256, kind="capgan", carry=1, **kw):
     from cglgan import GanStep, specs
     from cglgan.init import default_init
     os.environ["CGL_PACK_ADAM"] = "1" if on else "0"
+    os.environ["CGL_PACK_CARRY"] = str(carry)
     try:
         if kind == "mixg":
             gm, extra = specs.mixgen_worker(0), dict(weighting="mix_single", exchange_layer=specs.MIXGEN_HEAD_LAYER)
@@ -35,6 +36,7 @@ def _step(on, B=256, kind="capgan", **kw):
                      **extra, **kw)
     finally:
         os.environ.pop("CGL_PACK_ADAM", None)
+        os.environ.pop("CGL_PACK_CARRY", None)
     torch.manual_seed(20211212)
     default_init(gm, st.g_views)
     torch.manual_seed(4242)
@@ -55,10 +57,31 @@ def _same(a, b, tag=""):
 
 
 def test_plan_moves_packing_into_adam():
-    a, b = _step(True), _step(False)
+    a, b = _step(True), _step(False, carry=0)
     la, lb = a.launches(), b.launches()
     assert [k for k, _, _ in la] == [k for k, _, _ in lb]
     assert la[0][2] < lb[0][2], (la[0], lb[0])       # the prologue launch lost its packing blocks
+
+
+def test_plan_carries_packing_in_small_launches():
+    """Default plan (CGL_PACK_CARRY=1): the packing jobs ride in the forward cgl_bn_apply launches and the
+    deferred loss heads; the prologue keeps none, and the plan's launch sequence is unchanged."""
+    c, b = _step(False), _step(False, carry=0)
+    lc, lb = c.launches(), b.launches()
+    assert [k for k, _, _ in lc] == [k for k, _, _ in lb]
+    assert lc[0][2] < lb[0][2], (lc[0], lb[0])
+    grew = [k for (k, _, gc), (_, _, gb) in zip(lc, lb) if gc > gb]
+    assert grew and set(grew) <= {"bn_apply", "head"}, grew
+    assert sum(gc - gb for (_, _, gc), (_, _, gb) in zip(lc, lb)) == lb[0][2] - lc[0][2]
+
+
+@pytest.mark.parametrize("kind", ["capgan", "mixg"])
+def test_pack_carry_bitwise(kind):
+    a, b = _step(False, 256, kind), _step(False, 256, kind, carry=0)
+    for r in range(5):
+        a.run(graph=r >= 2)
+        b.run(graph=r >= 2)
+    _same(a, b, kind)
 
 
 @pytest.mark.parametrize("B", [64, 256])
