@@ -72,7 +72,7 @@ def test_plan_carries_packing_in_small_launches():
     assert lc[0][2] < lb[0][2], (lc[0], lb[0])
     grew = [k for (k, _, gc), (_, _, gb) in zip(lc, lb) if gc > gb]
     assert grew and set(grew) <= {"bn_apply", "head"}, grew
-    assert sum(gc - gb for (_, _, gc), (_, _, gb) in zip(lc, lb)) == lb[0][2] - lc[0][2]
+    assert sum(gc - gb for (_, _, gc), (_, _, gb) in zip(lc[1:], lb[1:])) == lb[0][2] - lc[0][2]
 
 
 @pytest.mark.parametrize("kind", ["capgan", "mixg"])
