@@ -122,7 +122,7 @@ class GanStep:
         h = ctypes.c_void_p()
         C.check(C.lib.cgl_gan_create(ctypes.byref(cfg), ctypes.byref(bufs), ctypes.byref(h)), "cgl_gan_create")
         self._h = h
-        self._pk_ver = -1          # the packed G weight copies: refreshed before the first round (sync_params)
+        self._pk_ver = None        # the packed weight copies (G, D): refreshed before the first round (sync_params)
         self.g_views = self._views(g, C.MODEL_G, self.g_params)
         self.d_views = self._views(d, C.MODEL_D, self.d_params)
         self.g_grad_views = self._views(g, C.MODEL_G, self.g_grads)
@@ -183,7 +183,7 @@ class GanStep:
         b = beta if beta is not None else [1.0 / self.n_workers] * self.n_workers
         arr = (ctypes.c_float * len(b))(*[float(x) for x in b])
         C.check(C.lib.cgl_gan_reset(self._h, arr, _stream()), "cgl_gan_reset")
-        self._pk_ver = self.g_params._version        # (reset re-packs G's weights)
+        self._pk_ver = self._pver()                  # (reset re-packs the weights)
         for k, v in self.running.items():
             v.fill_(0.0 if k.endswith("running_mean") else 1.0)
 
@@ -259,12 +259,15 @@ class GanStep:
         the G Adam launch keeps them current, so this is needed only after G's parameters were written from
         outside the round (state-dict loads, init, the Cloud FedAvg).  Stream-ordered, no host sync."""
         C.check(C.lib.cgl_gan_sync_params(self._h, _stream()), "cgl_gan_sync_params")
-        self._pk_ver = self.g_params._version
+        self._pk_ver = self._pver()
+
+    def _pver(self):
+        return (self.g_params._version, self.d_params._version)
 
     def _packed_current(self):
         # any in-place torch write of G's parameters (through g_params or one of its views) moves the buffer's
         # version counter; the library's own kernel writes do not, and they keep the packed copies current
-        if self.g_params._version != self._pk_ver:
+        if self._pver() != self._pk_ver:
             self.sync_params()
 
     def run(self, phase=C.PHASE_ALL, graph=False):

@@ -176,6 +176,8 @@ struct WS {
   float* wpk[CGL_MAX_LAYERS];       // packed G weights P(W_l; fo, fi) (the forward GEMM's B)
   float* wtpk[CGL_MAX_LAYERS];      // packed transposed G weights P(W_l^T; fi, fo) (input-gradient B)
   float* gGpk[CGL_MAX_LAYERS];      // packed cgl_bn_bwd output P(dZ_l; B, f) (input-gradient A)
+  float* dwpk[CGL_MAX_LAYERS];      // packed D weights P(V_j; fo, fi) (the D forward GEMMs' B), written by D's Adam
+  float* dwtpk[CGL_MAX_LAYERS];     // packed transposed D weights P(V_j^T; fi, fo) (the D input gradients' B)
   float* gath;                      // gathered exchange: n_workers slots of xchg_slot_max() floats
   CglStepState* st;
   int* idx;       // sampler output when sample_n > 0
@@ -227,6 +229,10 @@ WS carve_ws(const cgl_gan_config& c, void* base) {
   w.idx = cv.take<int>((int64_t)c.epoch * c.batch_real);
   w.znext = cv.take<float>((int64_t)2 * B * g.dims[0]);
   w.gath = cv.take<float>((int64_t)std::max(c.n_workers, 1) * xchg_slot_max(c));
+  for (int j = 0; j + 1 < J; ++j) {
+    w.dwpk[j] = cv.take<float>(cgl_pk_floats(d.dims[j + 1], d.dims[j]));
+    w.dwtpk[j] = cv.take<float>(cgl_pk_floats(d.dims[j], d.dims[j + 1]));
+  }
   // split-K scratch last, so that the layout of everything the default plan touches is unchanged
   w.kpart = cv.take<float>(kSplitKFloats);
   w.kcount = cv.take<unsigned int>(kSplitKCounters);
@@ -266,7 +272,8 @@ struct Launch {
   bool sk = false;      // GEMM launch holds a split-K problem
   int dt = CGL_DTYPE_F32;   // GEMM operand type (cgl_gan_config.gemm_dtype)
   int abn = 0;              // GEMM operand-transform instantiation (the launch's a_bn)
-  bool adpk = false;        // K_ADAM: the cgl_adam_pack form (cgl_gan.adam_pack)
+  bool adpk = false;        // K_ADAM: the cgl_adam_pack form (cgl_gan.adam_pack, or adam_pack_d for D's Adam)
+  int apk_d = 0;            // K_ADAM adpk: 1 = D's (cgl_gan.adam_pack_d)
   int layer = -1;           // K_BNAPPLY: the G layer whose forward GEMM reads this launch's output
   int pk = -1;              // K_BNAPPLY: index of the packing jobs it carries (cgl_gan.carry), -1: none
 };
@@ -531,6 +538,9 @@ struct cgl_gan {
   bool pack_adam = false;    // G's packed weights written by the G Adam launch (cgl_adam_pack), not the prologue
   bool z_ahead = false;      // z drawn one round ahead by the G Adam launch into ws.znext (plan_z_ahead)
   CglAdamPack adam_pack{};
+  CglAdamPack adam_pack_d{};      // D's Adam writing D's packed forward weights (plan_d_pack)
+  bool d_pack = false;            // the D forward GEMMs read P(V_j) from ws.dwpk, kept by D's Adam (plan_d_pack)
+  std::vector<CglOpPackJob> d_jobs;
   std::vector<CglOpPack> carry;   // packing jobs carried by the forward cgl_bn_apply launches (plan_pack_carriers)
   std::vector<int> pack_need;     // per prologue packing job: the G layer whose forward reads it (INT_MAX: backward)
   unsigned long long* trace = nullptr;   // CGL_GEMM_TRACE diagnostics buffer (kTraceWords per GEMM descriptor)
@@ -1005,20 +1015,18 @@ bool plan_pack_carriers(cgl_gan* c, std::vector<Launch>& A) {
   return true;
 }
 
-bool plan_pack_adam(cgl_gan* c, std::vector<Launch>& ph) {
-  const int env = getenv("CGL_PACK_ADAM") ? atoi(getenv("CGL_PACK_ADAM")) : 0;   // read per plan
-  c->pack_adam = false;
-  if (!env || c->pack.nj == 0 || ph.empty()) return false;
-  Launch& A = ph.back();
-  if (A.kind != K_ADAM || A.adam.p != c->bufs.g_params) return false;
+// The packing jobs `jobs` of one model's weight matrices (tensor list tl, parameters at pbase) written by that
+// model's Adam launch A (cgl_adam_pack): the tiles of the matrices that carry jobs, element ranges for the rest.
+bool build_adam_pack(const CglOpPackJob* jobs, int nj, const std::vector<TensorRec>& tl, const float* pbase,
+                     Launch& A, CglAdamPack& out) {
   CglAdamPack pk;
   std::memset(&pk, 0, sizeof(pk));
   std::vector<std::pair<int64_t, int64_t>> spans;
-  for (int q = 0; q < c->pack.nj; ++q) {
-    const CglOpPackJob& J = c->pack.j[q];
+  for (int q = 0; q < nj; ++q) {
+    const CglOpPackJob& J = jobs[q];
     const TensorRec* tr = nullptr;
-    for (auto& t : c->gl)
-      if (t.kind == 0 && c->bufs.g_params + t.off == J.src) tr = &t;
+    for (auto& t : tl)
+      if (t.kind == 0 && pbase + t.off == J.src) tr = &t;
     if (!tr || tr->rows % 4 || tr->cols % 4 || tr->off % 4) return false;
     // the job's view of W [rows = fo][cols = fi]: forward P(W; fo, fi) or transposed P(W^T; fi, fo)
     const bool fwd = !J.trans && J.R == tr->rows && J.K == tr->cols && J.ld == tr->cols;
@@ -1064,9 +1072,89 @@ bool plan_pack_adam(cgl_gan* c, std::vector<Launch>& ph) {
     blk += (int)((A.adam.nz / 4 + 255) / 256);
   }
   A.grid = blk;
-  c->adam_pack = pk;
+  out = pk;
+  return true;
+}
+
+bool plan_pack_adam(cgl_gan* c, std::vector<Launch>& ph) {
+  const int env = getenv("CGL_PACK_ADAM") ? atoi(getenv("CGL_PACK_ADAM")) : 0;   // read per plan
+  c->pack_adam = false;
+  if (!env || c->pack.nj == 0 || ph.empty()) return false;
+  Launch& A = ph.back();
+  if (A.kind != K_ADAM || A.adam.p != c->bufs.g_params) return false;
+  if (!build_adam_pack(c->pack.j, c->pack.nj, c->gl, c->bufs.g_params, A, c->adam_pack)) return false;
   c->pack_adam = true;
   return true;
+}
+
+// D's hidden-layer weights in the fragment-packed layout for the D forward GEMMs (round 5, CGL_DPACK, default on):
+// D's parameters change only in D's Adam launch, which writes the packed copy P(V_j; fo, fi) beside each updated
+// matrix (cgl_adam_pack), so every D forward -- the next local D step's and the G-loss pass through the updated
+// D -- reads two contiguous 1 KB wave loads per 16-k chunk instead of 32 rows x 64 B.  Decided before the D
+// forward descriptors are built (the layers whose matrices qualify); the Adam launches take the jobs later.
+bool plan_d_pack(cgl_gan* c) {
+  const char* env = getenv("CGL_DPACK");
+  const char* fd = getenv("CGL_FUSE_DADAM");
+  c->d_pack = false;
+  c->d_jobs.clear();
+  const int mask = env ? atoi(env) : 3;   // bit 0: forward copies P(V_j), bit 1: transposed copies P(V_j^T)
+  if (!mask || (fd && atoi(fd) != 0) || !pack_enabled()) return false;
+  const cgl_mlp_spec& d = c->cfg.d;
+  for (int j = 0; j + 1 < d.n_layers; ++j) {
+    const int fi = d.dims[j], fo = d.dims[j + 1];
+    if (fi < 256) continue;
+    const float* src = dparam(c, j, 0);
+    bool ok = false;
+    for (auto& t : c->dl)
+      if (t.kind == 0 && c->bufs.d_params + t.off == src) ok = t.rows % 4 == 0 && t.cols % 4 == 0 && t.off % 4 == 0;
+    if (!ok || (int)c->d_jobs.size() + 2 > CGL_APK_MAXT) continue;
+    CglOpPackJob J;
+    std::memset(&J, 0, sizeof(J));
+    J.src = src;
+    J.ld = fi;
+    if (mask & 1) {
+      J.dst = c->ws.dwpk[j];
+      J.R = fo;
+      J.K = fi;
+      J.trans = 0;
+      c->d_jobs.push_back(J);
+    }
+    if (mask & 2) {
+      J.dst = c->ws.dwtpk[j];
+      J.R = fi;
+      J.K = fo;
+      J.trans = 1;
+      c->d_jobs.push_back(J);
+    }
+  }
+  c->d_pack = !c->d_jobs.empty();
+  return c->d_pack;
+}
+// the packed copy of D layer j, or null (the forward GEMM reads V_j row-major)
+const float* d_packed(cgl_gan* c, int j, int trans = 0) {
+  if (!c->d_pack) return nullptr;
+  for (auto& J : c->d_jobs)
+    if (J.src == dparam(c, j, 0) && J.trans == trans) return J.dst;
+  return nullptr;
+}
+// The input gradient dX = dY V_j of D layer j ([rows][fo] x [fo][fi]): NT on the packed transpose P(V_j^T) kept by
+// D's Adam, or NN on the row-major V_j.  The caller sets the epilogue.
+CglGemmDesc d_input_grad(cgl_gan* c, int j, int rows_, const float* dY) {
+  const cgl_mlp_spec& d = c->cfg.d;
+  const int fi = d.dims[j], fo = d.dims[j + 1];
+  const float* pkt = d_packed(c, j, 1);
+  CglGemmDesc n = make_gemm(pkt ? 0 : 1, rows_, fi, fo);
+  n.a = rows(dY, fo);
+  n.a_vec = (fo % 4 == 0);
+  if (pkt) {
+    n.b = rows(pkt, fo);
+    n.b_pk = 1;
+    n.b_vec = 1;
+    choose_tiles(n);
+  } else {
+    n.b = rows(dparam(c, j, 0), fi);
+  }
+  return n;
 }
 
 int build_plan(cgl_gan* c) {
@@ -1231,6 +1319,7 @@ int build_plan(cgl_gan* c) {
   const float combine = cf.loss == CGL_LOSS_CE2 ? 0.5f : 1.0f;
   // hidden-layer forwards of the D-step input rows [row0, row0 + nrows): part 0 = real rows
   // (through the sampler's index list), part 1 = Xd rows, part 2 = both (one 2-segment GEMM)
+  plan_d_pack(c);
   auto d_forward = [&](int ep, int part, int stream, int wait_ev) {
     const int row0 = part == 1 ? Br : 0;
     const int nrows = part == 0 ? Br : part == 1 ? B : Md;
@@ -1267,6 +1356,12 @@ int build_plan(cgl_gan* c) {
       }
       e.b = rows(dparam(c, j, 0), fi);
       e.b_vec = (fi % 4 == 0);
+      if (const float* pkd = d_packed(c, j)) {
+        e.b = rows(pkd, fi);
+        e.b_pk = 1;
+        e.b_vec = 1;
+        choose_tiles(e);
+      }
       e.bias = dparam(c, j, 1);
       e.act = CGL_EPI_ACT_LEAKY;
       e.slope = sl;
@@ -1361,10 +1456,7 @@ int build_plan(cgl_gan* c) {
         grp.push_back(t);
       }
       if (j >= 1) {
-        CglGemmDesc n = make_gemm(1, Md, d.dims[j], d.dims[j + 1]);
-        n.a = rows(w.dQ[j], d.dims[j + 1]);
-        n.a_vec = (d.dims[j + 1] % 4 == 0);
-        n.b = rows(dparam(c, j, 0), d.dims[j]);
+        CglGemmDesc n = d_input_grad(c, j, Md, w.dQ[j]);
         n.mask_ref = w.P[j - 1];
         n.mask_ld = d.dims[j];
         n.slope = sl;
@@ -1379,6 +1471,12 @@ int build_plan(cgl_gan* c) {
     push_adam(c, A, c->bufs.d_params, c->bufs.d_grads, c->bufs.d_m, c->bufs.d_v, (long)nd,
               &st->d_step_size[ep], &st->d_bc2sqrt[ep], 0, scaling ? &st->scale[0] : nullptr,
               scaling ? &st->found[0] : nullptr);
+    if (c->d_pack) {    // D's Adam keeps the packed copies (the D forwards after it read them)
+      if (!build_adam_pack(c->d_jobs.data(), (int)c->d_jobs.size(), c->dl, c->bufs.d_params, A.back(),
+                           c->adam_pack_d))
+        return CGL_E_STATE;   // (plan_d_pack admitted only matrices build_adam_pack accepts)
+      A.back().apk_d = 1;
+    }
     fuse_wgrad_adam(c, A, CGL_MODEL_D);
   }
 
@@ -1390,6 +1488,12 @@ int build_plan(cgl_gan* c) {
     e.a_vec = (fi % 4 == 0);
     e.b = rows(dparam(c, j, 0), fi);
     e.b_vec = (fi % 4 == 0);
+    if (const float* pkd = d_packed(c, j)) {
+      e.b = rows(pkd, fi);
+      e.b_pk = 1;
+      e.b_vec = 1;
+      choose_tiles(e);
+    }
     e.bias = dparam(c, j, 1);
     e.act = CGL_EPI_ACT_LEAKY;
     e.slope = sl;
@@ -1427,10 +1531,7 @@ int build_plan(cgl_gan* c) {
   }
   for (int j = J - 2; j >= 0; --j) {
     // dS[j-1] = (dS[j] V_j) * leaky'(S[j-1]);  j == 0: dXg = dS[0] V_0, then Tanh'
-    CglGemmDesc n = make_gemm(1, B, d.dims[j], d.dims[j + 1]);
-    n.a = rows(w.dS[j], d.dims[j + 1]);
-    n.a_vec = (d.dims[j + 1] % 4 == 0);
-    n.b = rows(dparam(c, j, 0), d.dims[j]);
+    CglGemmDesc n = d_input_grad(c, j, B, w.dS[j]);
     n.slope = sl;
     if (j >= 1) {
       n.mask_ref = w.S[j - 1];
@@ -1635,6 +1736,13 @@ int build_plan(cgl_gan* c) {
     }
     c->pack.blocks = blk;
     c->pack_all = c->pack;
+    for (auto& J : c->d_jobs) {        // D's packed copies too (sync_params / reset: D written from outside)
+      if (c->pack_all.nj == CGL_PACK_MAXJ) return CGL_E_SIZE;
+      CglOpPackJob& D = c->pack_all.j[c->pack_all.nj++];
+      D = J;
+      D.blk_begin = c->pack_all.blocks;
+      c->pack_all.blocks += (int)((cgl_pk_floats(J.R, J.K) / 4 + 255) / 256);
+    }
     if (plan_pack_adam(c, *ph)) {      // the G Adam launch writes the packed copies: no prologue packing
       c->pack.nj = 0;
       c->pack.blocks = 0;
@@ -1700,7 +1808,8 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
       break;
     case K_ADAM:
       if (L.adpk)
-        klaunch(cgl_adam_pack, dim3(L.grid), dim3(256), 0, s, L.adam, c->adam_pack, c->ws.st, L.tail);
+        klaunch(cgl_adam_pack, dim3(L.grid), dim3(256), 0, s, L.adam, L.apk_d ? c->adam_pack_d : c->adam_pack,
+                c->ws.st, L.tail);
       else
         klaunch(cgl_adam, dim3(L.grid), dim3(256), 0, s, L.adam, c->ws.st, L.tail);
       break;
@@ -1924,7 +2033,7 @@ int cgl_gan_reset(cgl_gan* c, const float* beta_host, void* stream) {
   HIPCHK(hipMemcpyAsync(c->ws.st, &h, sizeof(h), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemsetAsync(c->ws.counters, 0, kCounters * sizeof(unsigned int), s));
   HIPCHK(hipMemsetAsync(c->ws.kcount, 0, kSplitKCounters * sizeof(unsigned int), s));
-  if (c->pack_adam && c->pack_all.blocks > 0) {       // the packed G weights from the current parameters
+  if ((c->pack_adam || c->d_pack) && c->pack_all.blocks > 0) {   // the packed weights from the current parameters
     hipLaunchKernelGGL(cgl_pack_all, dim3(c->pack_all.blocks), dim3(256), 0, s, c->pack_all);
     HIPCHK(hipGetLastError());
   }
@@ -1951,7 +2060,7 @@ int64_t cgl_gan_gemm_trace(cgl_gan* c, unsigned long long* host_out, int64_t n) 
 int cgl_gan_sync_params(cgl_gan* c, void* stream) {
   CGL_BATCH_GUARD();
   if (!c) return CGL_E_ARG;
-  if (c->pack_adam && c->pack_all.blocks > 0)   // (otherwise the prologue re-packs every round)
+  if ((c->pack_adam || c->d_pack) && c->pack_all.blocks > 0)   // (the prologue / carriers re-pack G every round)
     hipLaunchKernelGGL(cgl_pack_all, dim3(c->pack_all.blocks), dim3(256), 0, (hipStream_t)stream, c->pack_all);
   if (c->z_ahead) {
     const long nz = (long)2 * c->cfg.batch * c->cfg.g.dims[0];

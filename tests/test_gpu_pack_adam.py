@@ -139,7 +139,7 @@ def test_stale_packed_copy_would_be_caught():
     for s in (a, b):
         with torch.no_grad():
             s.g_views["model.11.weight"].mul_(0.5)
-    a._pk_ver = a.g_params._version          # pretend the write was seen: the packed copies stay stale
+    a._pk_ver = a._pver()                     # pretend the write was seen: the packed copies stay stale
     a.run()
     b.run()
     torch.cuda.synchronize()
