@@ -130,6 +130,7 @@ struct CglAdamPackTile {
   float* fwd;             // P(W; R, K), or null
   float* trn;             // P(W^T; K, R), or null
   int blk_begin;
+  int t32;                // 1: 32 x 64 workgroup tiles through LDS (K % 8 == 0), 0: 4 x 4 thread tiles
 };
 struct CglAdamPack {
   int nt, nr, tile_blocks;
@@ -195,14 +196,106 @@ __device__ __forceinline__ void cgl_adam_tile_at(const CglAdamArgs& a, const Cgl
   }
 }
 
+// The same update for a 32-row x 64-column tile of W per workgroup (t32): thread (ri = tid / 8, 8 consecutive
+// columns) loads its row segment with 16-byte loads (a row's 64 columns = 256 contiguous bytes), updates, stores
+// p / m / v back, and drops the new values into LDS at their packed positions; the tile's forward image P(W) is
+// then 4 consecutive 2 KB blocks (chunks k0 / 16 ..) and its transposed image P(W^T) 2 x 2 blocks, each written
+// with contiguous 16-byte stores.  Positions past R / K inside a block hold zeros (the packing's padding).
+__device__ __forceinline__ void cgl_adam_tile32_at(const CglAdamArgs& a, const CglAdamPackTile& T, int t,
+                                                   float* s_f, float* s_t) {
+  const int nkt = (T.K + 63) >> 6;
+  const int rb = t / nkt, k0 = (t - rb * nkt) * 64;
+  const int tid = threadIdx.x, ri = tid >> 3, kq = (tid & 7) * 8;
+  const int r = rb * 32 + ri, k = k0 + kq;
+  const bool ok = r < T.R && k < T.K;            // (K % 8 == 0: the 8 columns are all in or all out)
+  const long e0 = T.off + (long)min(r, T.R - 1) * T.K + min(k, T.K - 8);
+  const float ss = a.step_size ? gld(a.step_size) : a.step_size_v;
+  const float bc = a.bc2sqrt ? gld(a.bc2sqrt) : a.bc2sqrt_v;
+  f32x4 P[2], G[2], M[2], V[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    P[h] = *(gcf4p)(a.p + e0 + 4 * h);
+    G[h] = *(gcf4p)(a.g + e0 + 4 * h);
+    M[h] = *(gcf4p)(a.m + e0 + 4 * h);
+    V[h] = *(gcf4p)(a.v + e0 + 4 * h);
+  }
+  bool upd = true;
+  if (a.scale) {
+    const float inv = (float)(1.0 / (double)gld(a.scale));
+    upd = *(const CGL_GLOBAL unsigned int*)a.found == 0u;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) G[h][j] = G[h][j] * inv;
+      if (ok) *(gf4p)(a.g + e0 + 4 * h) = G[h];
+    }
+  }
+  if (upd) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float pp = P[h][j], mm = M[h][j], vv = V[h][j];
+        cgl_adam_update(pp, G[h][j], mm, vv, ss, bc, a.b2, a.w1, a.w2, a.eps);
+        P[h][j] = pp;
+        M[h][j] = mm;
+        V[h][j] = vv;
+      }
+      if (ok) {
+        *(gf4p)(a.m + e0 + 4 * h) = M[h];
+        *(gf4p)(a.v + e0 + 4 * h) = V[h];
+        *(gf4p)(a.p + e0 + 4 * h) = P[h];
+      }
+    }
+  }
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const f32x4 v = ok ? P[h] : z;
+    const int kk = kq + 4 * h;
+    // forward image: ((kk / 16) * 2 + (kk / 4) % 2) * 256 + (ri + 32 ((kk / 8) % 2)) * 4 + kk % 4
+    *(f32x4*)(s_f + ((kk >> 4) * 2 + ((kk >> 2) & 1)) * 256 + (ri + 32 * ((kk >> 3) & 1)) * 4) = v;
+    // transposed image: region kk / 32, then ((ri / 16) * 2 + (ri / 4) % 2) * 256 + (kk % 32 + 32 ((ri / 8) % 2)) * 4
+    // + ri % 4
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = kk + j;
+      s_t[(c >> 5) * 1024 + ((ri >> 4) * 2 + ((ri >> 2) & 1)) * 256 + ((c & 31) + 32 * ((ri >> 3) & 1)) * 4 + (ri & 3)] =
+          v[j];
+    }
+  }
+  __syncthreads();
+  const int q = tid * 8;     // this thread's 8 floats of each 2048-float image
+  if (T.fwd) {
+    const int kc = (T.K + 15) >> 4;
+    if ((k0 >> 4) + (q >> 9) < kc) {
+      float* dst = T.fwd + ((long)rb * kc + (k0 >> 4)) * 512 + q;
+      *(gf4p)dst = *(const f32x4*)(s_f + q);
+      *(gf4p)(dst + 4) = *(const f32x4*)(s_f + q + 4);
+    }
+  }
+  if (T.trn) {
+    const int kc = (T.R + 15) >> 4, rbt = (k0 >> 5) + (q >> 10), ct = 2 * rb + ((q >> 9) & 1);
+    if (rbt < ((T.K + 31) >> 5) && ct < kc) {
+      float* dst = T.trn + ((long)rbt * kc + ct) * 512 + (q & 511);
+      *(gf4p)dst = *(const f32x4*)(s_t + q);
+      *(gf4p)(dst + 4) = *(const f32x4*)(s_t + q + 4);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void cgl_adam_pack(CglAdamArgs a, CglAdamPack pk, CglStepState* st, int tail) {
+  __shared__ float s_img[2][2048];
   if (cgl_adam_zblock(a, st)) return;
   const int b = blockIdx.x;
   if (b < pk.tile_blocks) {
     int j = 0;
     for (int q = 1; q < pk.nt; ++q)
       if (b >= pk.t[q].blk_begin) j = q;
-    cgl_adam_tile_at(a, pk.t[j], (long)(b - pk.t[j].blk_begin) * 256 + threadIdx.x);
+    if (pk.t[j].t32)
+      cgl_adam_tile32_at(a, pk.t[j], b - pk.t[j].blk_begin, s_img[0], s_img[1]);
+    else
+      cgl_adam_tile_at(a, pk.t[j], (long)(b - pk.t[j].blk_begin) * 256 + threadIdx.x);
   } else {
     int j = 0;
     for (int q = 1; q < pk.nr; ++q)

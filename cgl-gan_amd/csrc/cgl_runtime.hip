@@ -1015,6 +1015,12 @@ bool plan_pack_carriers(cgl_gan* c, std::vector<Launch>& A) {
   return true;
 }
 
+// cgl_adam_pack's 32 x 64 workgroup tiles through LDS (CGL_ADAM_T32, default on; 0: the 4 x 4 thread tiles)
+bool adam_t32() {
+  const char* e = getenv("CGL_ADAM_T32");
+  return !e || atoi(e) != 0;
+}
+
 // The packing jobs `jobs` of one model's weight matrices (tensor list tl, parameters at pbase) written by that
 // model's Adam launch A (cgl_adam_pack): the tiles of the matrices that carry jobs, element ranges for the rest.
 bool build_adam_pack(const CglOpPackJob* jobs, int nj, const std::vector<TensorRec>& tl, const float* pbase,
@@ -1036,7 +1042,7 @@ bool build_adam_pack(const CglOpPackJob* jobs, int nj, const std::vector<TensorR
     while (i < pk.nt && pk.t[i].off != tr->off) ++i;
     if (i == pk.nt) {
       if (pk.nt == CGL_APK_MAXT) return false;
-      pk.t[pk.nt++] = CglAdamPackTile{tr->off, tr->rows, tr->cols, nullptr, nullptr, 0};
+      pk.t[pk.nt++] = CglAdamPackTile{tr->off, tr->rows, tr->cols, nullptr, nullptr, 0, adam_t32() && tr->cols % 8 == 0};
       spans.push_back({tr->off, tr->off + (int64_t)tr->rows * tr->cols});
     }
     (fwd ? pk.t[i].fwd : pk.t[i].trn) = J.dst;
@@ -1044,7 +1050,8 @@ bool build_adam_pack(const CglOpPackJob* jobs, int nj, const std::vector<TensorR
   int blk = 0;
   for (int i = 0; i < pk.nt; ++i) {
     pk.t[i].blk_begin = blk;
-    blk += (int)(((int64_t)(pk.t[i].R / 4) * (pk.t[i].K / 4) + 255) / 256);
+    blk += pk.t[i].t32 ? ((pk.t[i].R + 31) / 32) * ((pk.t[i].K + 63) / 64)
+                       : (int)(((int64_t)(pk.t[i].R / 4) * (pk.t[i].K / 4) + 255) / 256);
   }
   pk.tile_blocks = blk;
   // element ranges: [0, n) minus the tile tensors
