@@ -45,7 +45,7 @@ def main():
     out = {"rounds": len(rounds), "launches": n, "period_us": S.median(r[2] for r in rounds), "per_launch": []}
     gemm = []
     for j in range(n):
-        name = rounds[0][0][j]["Kernel_Name"].split("(")[0].replace("void ", "")
+        name = rounds[0][0][j]["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
         du = [(int(r[0][j]["End_Timestamp"]) - int(r[0][j]["Start_Timestamp"])) / 1e3 for r in rounds]
         ga = [r[1][j] for r in rounds]
         wg = int(rounds[0][0][j]["Grid_Size_X"]) // int(rounds[0][0][j]["Workgroup_Size_X"])

@@ -28,7 +28,7 @@ def load(path, name):
     per = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == name:
-            per[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
+            per[kname(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     return per
 
 
@@ -36,9 +36,14 @@ def load_rows(path, name):
     rows = []
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == name:
-            rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"].split("(")[0], float(r["Counter_Value"])))
+            rows.append((int(r["Dispatch_Id"]), kname(r["Kernel_Name"]), float(r["Counter_Value"])))
     rows.sort()
     return rows
+
+
+def kname(k):
+    """Kernel name without its argument list ('(anonymous namespace)::' prefixes dropped first)."""
+    return k.replace("(anonymous namespace)::", "").split("(")[0]
 
 
 def rounds_of(rows, marker="cgl_gemm_pro"):
