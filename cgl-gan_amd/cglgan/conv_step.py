@@ -736,13 +736,13 @@ class ConvGanStep:
         torch.cuda.current_stream().synchronize()
         if split:      # phase A and phase B as two graphs (the exchange runs between their replays)
             ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(ga):
+            with torch.cuda.graph(ga, capture_error_mode="thread_local"):
                 self.phase_a(None)
-            with torch.cuda.graph(gb):
+            with torch.cuda.graph(gb, capture_error_mode="thread_local"):
                 self.phase_b()
         else:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self.phase_a(None)
                 self.phase_b()
         after = self._host_state()

@@ -208,7 +208,9 @@ class WorkerExchange:
         s = self.step
         s._packed_current()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):       # (captures only: the caller replays it for this round)
+        # thread-local capture mode: another thread's CUDA call (RCCL's watchdog polling its events) must not
+        # invalidate this capture
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):   # (captures only: the caller replays it)
             s.run(C.PHASE_A, graph=False)
             self.exchange_mid()
             s.run(C.PHASE_B, graph=False)

@@ -33,4 +33,6 @@ def test_exchange_over_rccl_world1():
     env = dict(os.environ)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     out = r.stdout + r.stderr
+    if r.returncode != 0:
+        print(out[-12000:])          # (the worker's traceback, whole, in the test log)
     assert r.returncode == 0 and "RCCL-WORLD1 OK" in out, out[-4000:]
