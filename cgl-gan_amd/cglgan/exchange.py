@@ -176,10 +176,8 @@ class WorkerExchange:
         swap = self.dswap is not None and (r + 1) % self.swap_every == 0
         if self.comm is None or (self.comm.size == 1 and not self.force_split):
             s.run(C.PHASE_ALL, graph=graph)
-        elif graph and self.round_graph and self._split_ran and not (share or swap):
-            if self._rgraph is None:
-                self._rgraph = self._capture_round()
-            s._packed_current()          # (host-side check of G's packed copies, as s.run does)
+        elif graph and self.round_graph and self._split_ran and not (share or swap) and self._ensure_round_graph():
+            s._packed_current()          # (host-side check of the packed weight copies, as s.run does)
             self._rgraph.replay()
         else:
             self._split_ran = True
@@ -203,6 +201,19 @@ class WorkerExchange:
         if (self.cloud is not None and self.cloud_due is None and self.cloud_every > 0 and
                 (r + 1) % self.cloud_every == 0):
             self.cloud_average()
+
+    def _ensure_round_graph(self):
+        """Capture the whole-round graph on first use; a capture the stack refuses (an RCCL or HIP build without
+        collective capture) turns the whole-round graph off and the round takes the split path."""
+        if self._rgraph is None:
+            try:
+                self._rgraph = self._capture_round()
+            except RuntimeError as e:     # (a capture error leaves no work queued: nothing was issued)
+                import warnings
+                warnings.warn(f"whole-round graph capture failed, split rounds from now on: {e}")
+                self.round_graph = False
+                return False
+        return True
 
     def _capture_round(self):
         s = self.step
