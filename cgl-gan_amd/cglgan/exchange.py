@@ -62,10 +62,13 @@ class DistComm:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
 
     def all_reduce_mean(self, t: torch.Tensor, weights=None):
-        """sum_i w_i t_i (w = 1/N when None); identical result on every rank."""
+        """sum_i w_i t_i (w = 1/N when None); identical result on every rank.  Over RCCL the plain mean is one
+        ReduceOp.AVG collective (no separate division launch); gloo sums and divides."""
         if weights is not None:
             t.mul_(float(weights[self.rank]))
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        elif self.capturable:
+            dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group)
         else:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
             t.div_(self.size)
@@ -155,7 +158,11 @@ class WorkerExchange:
         self.round_graph = (os.environ.get("CGL_ROUND_GRAPH", "1") != "0" and
                             bool(getattr(comm, "capturable", False)) and hasattr(step, "g_params") and
                             step.g_params.is_cuda)
-        self._rgraph, self._split_ran = None, False
+        self._rgraph, self._split_ran = {}, False
+        # D's exchange (E-share / D-swap) after phase B on the main stream (default), or on a side stream beside
+        # phase B (CGL_DX_SIDE=1).  Measured at world 1: the side branch slows every phase-B launch it runs beside
+        # (+64 us per round for a ~15 us exchange, tests/rccl_world1_worker.py --time); serial it costs its own time.
+        self.d_side = os.environ.get("CGL_DX_SIDE", "0") != "0"
 
     def exchange_mid(self):
         """The collectives between phase A and phase B of one round (this rank's side)."""
@@ -176,14 +183,15 @@ class WorkerExchange:
         swap = self.dswap is not None and (r + 1) % self.swap_every == 0
         if self.comm is None or (self.comm.size == 1 and not self.force_split):
             s.run(C.PHASE_ALL, graph=graph)
-        elif graph and self.round_graph and self._split_ran and not (share or swap) and self._ensure_round_graph():
+        elif graph and self.round_graph and self._split_ran and not swap and self._ensure_round_graph(share):
             s._packed_current()          # (host-side check of the packed weight copies, as s.run does)
-            self._rgraph.replay()
+            self._rgraph[share].replay()
+            share = False                # (the E-share ran inside the graph)
         else:
             self._split_ran = True
             s.run(C.PHASE_A, graph=graph)
             self.exchange_mid()
-            side = self._side_stream() if (share or swap) else None
+            side = self._side_stream() if ((share or swap) and self.d_side) else None
             if side is not None:
                 # phase B (G backward + Adam G) never touches D: the E-share all-reduce / D-swap of
                 # this round's updated D run on a side stream concurrently with it (issued in the
@@ -202,12 +210,13 @@ class WorkerExchange:
                 (r + 1) % self.cloud_every == 0):
             self.cloud_average()
 
-    def _ensure_round_graph(self):
-        """Capture the whole-round graph on first use; a capture the stack refuses (an RCCL or HIP build without
-        collective capture) turns the whole-round graph off and the round takes the split path."""
-        if self._rgraph is None:
+    def _ensure_round_graph(self, share):
+        """Capture the whole-round graph (one per round form: with / without the E-share) on first use; a capture
+        the stack refuses (an RCCL or HIP build without collective capture) turns the whole-round graph off and the
+        round takes the split path."""
+        if share not in self._rgraph:
             try:
-                self._rgraph = self._capture_round()
+                self._rgraph[share] = self._capture_round(share)
             except RuntimeError as e:     # (a capture error leaves no work queued: nothing was issued)
                 import warnings
                 warnings.warn(f"whole-round graph capture failed, split rounds from now on: {e}")
@@ -215,7 +224,7 @@ class WorkerExchange:
                 return False
         return True
 
-    def _capture_round(self):
+    def _capture_round(self, share=False):
         s = self.step
         s._packed_current()
         g = torch.cuda.CUDAGraph()
@@ -224,7 +233,18 @@ class WorkerExchange:
         with torch.cuda.graph(g, capture_error_mode="thread_local"):   # (captures only: the caller replays it)
             s.run(C.PHASE_A, graph=False)
             self.exchange_mid()
-            s.run(C.PHASE_B, graph=False)
+            if share and self.d_side:   # the E-share of D on a side stream beside phase B
+                main = torch.cuda.current_stream()
+                side = self._side_stream()
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    self._d_exchange(-1, True, False)
+                s.run(C.PHASE_B, graph=False)
+                main.wait_stream(side)
+            else:
+                s.run(C.PHASE_B, graph=False)
+                if share:
+                    self._d_exchange(-1, True, False)
         return g
 
     def _d_exchange(self, r, share, swap):
@@ -233,6 +253,8 @@ class WorkerExchange:
             self.comm.all_reduce_mean(s.d_params)
         if swap:
             self.comm.swap([s.d_params], self.dswap.next_perm())
+        if (share or swap) and hasattr(s, "sync_params_d"):
+            s.sync_params_d()        # D's packed copies from the exchanged parameters (same stream)
 
     def _side_stream(self):
         if not self.step.d_params.is_cuda:

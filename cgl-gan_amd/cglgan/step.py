@@ -261,6 +261,13 @@ class GanStep:
         C.check(C.lib.cgl_gan_sync_params(self._h, _stream()), "cgl_gan_sync_params")
         self._pk_ver = self._pver()
 
+    def sync_params_d(self):
+        """Refresh D's packed copies only (cgl_gan_sync_params_d): after D's parameters were written from outside the
+        round by an E-share / D-swap.  Stream-ordered and capturable (the whole-round graph of a share round)."""
+        C.check(C.lib.cgl_gan_sync_params_d(self._h, _stream()), "cgl_gan_sync_params_d")
+        if self._pk_ver is not None:
+            self._pk_ver = (self._pk_ver[0], self.d_params._version)
+
     def _pver(self):
         return (self.g_params._version, self.d_params._version)
 

@@ -535,6 +535,7 @@ struct cgl_gan {
   hipStream_t side = nullptr;  // second stream: the real-row D chain of the first local D step
   CglOpPack pack{};          // the round prologue's operand-packing jobs (none when pack_adam)
   CglOpPack pack_all{};      // every packing job of the plan (cgl_gan_sync_params)
+  CglOpPack pack_d{};        // D's packing jobs alone (cgl_gan_sync_params_d)
   bool pack_adam = false;    // G's packed weights written by the G Adam launch (cgl_adam_pack), not the prologue
   bool z_ahead = false;      // z drawn one round ahead by the G Adam launch into ws.znext (plan_z_ahead)
   CglAdamPack adam_pack{};
@@ -1743,12 +1744,17 @@ int build_plan(cgl_gan* c) {
     }
     c->pack.blocks = blk;
     c->pack_all = c->pack;
+    std::memset(&c->pack_d, 0, sizeof(c->pack_d));
     for (auto& J : c->d_jobs) {        // D's packed copies too (sync_params / reset: D written from outside)
-      if (c->pack_all.nj == CGL_PACK_MAXJ) return CGL_E_SIZE;
+      if (c->pack_all.nj == CGL_PACK_MAXJ || c->pack_d.nj == CGL_PACK_MAXJ) return CGL_E_SIZE;
       CglOpPackJob& D = c->pack_all.j[c->pack_all.nj++];
       D = J;
       D.blk_begin = c->pack_all.blocks;
       c->pack_all.blocks += (int)((cgl_pk_floats(J.R, J.K) / 4 + 255) / 256);
+      CglOpPackJob& E = c->pack_d.j[c->pack_d.nj++];
+      E = J;
+      E.blk_begin = c->pack_d.blocks;
+      c->pack_d.blocks += (int)((cgl_pk_floats(J.R, J.K) / 4 + 255) / 256);
     }
     if (plan_pack_adam(c, *ph)) {      // the G Adam launch writes the packed copies: no prologue packing
       c->pack.nj = 0;
@@ -2074,6 +2080,14 @@ int cgl_gan_sync_params(cgl_gan* c, void* stream) {
     hipLaunchKernelGGL(cgl_znext_draw, dim3((unsigned)((nz / 4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                        c->ws.znext, nz, c->cfg.seed, (const CglStepState*)c->ws.st);
   }
+  return (int)hipGetLastError();
+}
+
+int cgl_gan_sync_params_d(cgl_gan* c, void* stream) {
+  CGL_BATCH_GUARD();
+  if (!c) return CGL_E_ARG;
+  if (c->d_pack && c->pack_d.blocks > 0)
+    hipLaunchKernelGGL(cgl_pack_all, dim3(c->pack_d.blocks), dim3(256), 0, (hipStream_t)stream, c->pack_d);
   return (int)hipGetLastError();
 }
 

@@ -139,14 +139,17 @@ int cgl_gan_destroy(cgl_gan* ctx);
 /* Zero the round counters / lambda, set the data-size weights beta[n_workers]
  * (capgan.py:149-153) -- host array.  Also refreshes the packed G weight copies (cgl_gan_sync_params). */
 int cgl_gan_reset(cgl_gan* ctx, const float* beta_host, void* stream);
-/* G's GEMMs read fragment-packed copies of its weight matrices, which the G Adam launch writes as it updates
- * the parameters (the round prologue packed them every round before round 5).  After writing G's parameters
- * from OUTSIDE the round -- loading a state dict, an initialisation, the Cloud FedAvg (mixed-gan.py:104-124) --
- * call this once (stream-ordered, no host sync) before the next round; cgl_gan_reset does it too.  It also
- * redraws the next round's z (gen_z: the G Adam launch draws round r + 1's z at the end of round r; after the
- * device round state was written from outside -- a resumed run -- call this so that z follows the loaded round
- * counter).  Cheap and idempotent between rounds. */
+/* The GEMMs read fragment-packed copies of the weight matrices: G's are re-packed every round by launches of the
+ * round itself (carried by the forward BatchNorm-apply and loss-head launches; by the G Adam launch with
+ * CGL_PACK_ADAM=1), D's are written by D's Adam launch as it updates the parameters.  After writing parameters
+ * from OUTSIDE the round -- loading a state dict, an initialisation, the Cloud FedAvg (mixed-gan.py:104-124), an
+ * E-share or D-swap of D -- call this once (stream-ordered, no host sync) before the next round; cgl_gan_reset
+ * does it too.  It also redraws the next round's z (gen_z: the G Adam launch draws round r + 1's z at the end of
+ * round r; after the device round state was written from outside -- a resumed run -- call this so that z follows
+ * the loaded round counter).  Cheap and idempotent between rounds. */
 int cgl_gan_sync_params(cgl_gan* ctx, void* stream);
+/* D's packed copies only (after an E-share / D-swap of D's parameters; capturable, no host sync). */
+int cgl_gan_sync_params_d(cgl_gan* ctx, void* stream);
 /* Diagnostics: with CGL_GEMM_TRACE=1 in the environment at create time and a library built with
  * -DCGL_GEMM_TRACE (tools/build_variant.sh), every GEMM workgroup of the last round stamps the 100 MHz wall
  * clock at kernel entry, body start, k-loop start, first chunk consumed, k-loop end and exit: 8 words per

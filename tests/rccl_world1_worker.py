@@ -118,25 +118,31 @@ def check_conv_round():
     return sa["g_loss"]
 
 
-def _ex(s, exchange, round_graph):
+def _ex(s, exchange, round_graph, share_every=0):
     from cglgan.exchange import DistComm, WorkerExchange
-    ex = WorkerExchange(s, DistComm(), force_split=True, exchange=exchange)
+    ex = WorkerExchange(s, DistComm(), force_split=True, exchange=exchange, share_every=share_every)
     assert ex.round_graph        # (RCCL: capturable)
     ex.round_graph = round_graph
     return ex
 
 
-def check_round_graph(exchange):
+def _side(ex):
+    ex.d_side = True       # D's exchange on a side stream beside phase B (CGL_DX_SIDE=1)
+    return ex
+
+
+def check_round_graph(exchange, share_every=0):
     """WorkerExchange's whole-round graph (phase A + collective(s) + phase B as one torch CUDA graph, captured
-    after the first split round): bitwise the unsplit rounds, graph and eager rounds interleaved."""
+    after the first split round; with share_every, the E-share of D and D's packed-copy refresh on a side stream
+    inside it): bitwise the unsplit rounds, graph and eager rounds interleaved."""
     from cglgan.exchange import WorkerExchange
     a, b = mlp_step(), mlp_step()
-    ex, ref = _ex(a, exchange, True), WorkerExchange(b, None)
+    ex, ref = _ex(a, exchange, True, share_every), WorkerExchange(b, None)
     for r in range(6):
         ex.round(r, graph=(r != 3))
         ref.round(r, graph=(r != 3))
     torch.cuda.synchronize()
-    assert ex._rgraph is not None
+    assert ex._rgraph and ex.round_graph
     same(a, b, ("g_params", "g_m", "g_v", "d_params", "d_m", "d_v", "g_running"))
     assert a.stats()["round"] == b.stats()["round"] == 6
 
@@ -153,7 +159,10 @@ def time_split(rounds=200):
                      ("split_reduce", lambda s: _ex(s, "reduce", False)),
                      ("split_gather", lambda s: _ex(s, "gather", False)),
                      ("round_graph_reduce", lambda s: _ex(s, "reduce", True)),
-                     ("round_graph_gather", lambda s: _ex(s, "gather", True))):
+                     ("round_graph_gather", lambda s: _ex(s, "gather", True)),
+                     ("split_gather_eshare1", lambda s: _ex(s, "gather", False, 1)),
+                     ("round_graph_gather_eshare1", lambda s: _ex(s, "gather", True, 1)),
+                     ("round_graph_gather_eshare1_side", lambda s: _side(_ex(s, "gather", True, 1)))):
         s = mlp_step(B=256, rows=60000)
         ex = mk(s)
         for r in range(20):
@@ -184,6 +193,8 @@ def main():
         check_mlp_round("reduce")
         check_round_graph("gather")
         check_round_graph("reduce")
+        check_round_graph("gather", share_every=1)
+        check_round_graph("reduce", share_every=2)
         ga = check_cloud("capgan", "all")
         gt = check_cloud("mixg", "trunk")
         gc = check_conv_round()

@@ -72,7 +72,7 @@ class HostComm:
             t.copy_(h.to(t.device))
 
 
-def _proc(rank, world, port, outdir, exchange):
+def _proc(rank, world, port, outdir, exchange, side):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -81,10 +81,11 @@ def _proc(rank, world, port, outdir, exchange):
         torch.cuda.set_device(0)
         st = _make(rank, world)
         ex = WorkerExchange(st, HostComm(), share_every=1, swap_every=2, exchange=exchange)
+        ex.d_side = side
         for r in range(ROUNDS):
             ex.round(r, graph=True)
         torch.cuda.synchronize()
-        torch.save({"g": st.g_params.cpu(), "d": st.d_params.cpu(), "side": ex._side is not None},
+        torch.save({"g": st.g_params.cpu(), "d": st.d_params.cpu(), "side": getattr(ex, "_side", None) is not None},
                    os.path.join(outdir, f"r{rank}.pt"))
     finally:
         dist.destroy_process_group()
@@ -92,11 +93,12 @@ def _proc(rank, world, port, outdir, exchange):
 
 # "gather": one all_gather of [gradient | loss] slots, alpha + the rank-ordered sum at phase B's head (on
 # device); "reduce": loss all_gather, alpha_scale, gradient all_reduce.  Both bitwise LocalComm's round.
-@pytest.mark.parametrize("exchange", ["gather", "reduce"])
-def test_worker_exchange_side_stream_matches_local(exchange):
+# side: D's exchange on a side stream beside phase B (CGL_DX_SIDE=1) or after it on the main stream (default)
+@pytest.mark.parametrize("exchange,side", [("gather", False), ("reduce", False), ("gather", True)])
+def test_worker_exchange_side_stream_matches_local(exchange, side):
     world = 2
     with tempfile.TemporaryDirectory() as td:
-        mp.spawn(_proc, args=(world, _free_port(), td, exchange), nprocs=world, join=True)
+        mp.spawn(_proc, args=(world, _free_port(), td, exchange, side), nprocs=world, join=True)
         res = [torch.load(os.path.join(td, f"r{r}.pt"), weights_only=True) for r in range(world)]
     from cglgan.exchange import LocalComm
     steps = [_make(r, world) for r in range(world)]
@@ -105,7 +107,7 @@ def test_worker_exchange_side_stream_matches_local(exchange):
         comm.round(r, graph=True)
     torch.cuda.synchronize()
     for i, s in enumerate(steps):
-        assert res[i]["side"]
+        assert res[i]["side"] == side
         assert torch.equal(res[i]["g"], s.g_params.cpu()), i
         assert torch.equal(res[i]["d"], s.d_params.cpu()), i
     assert torch.equal(res[0]["g"], res[1]["g"])     # replicated G
