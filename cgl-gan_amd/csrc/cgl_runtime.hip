@@ -678,14 +678,19 @@ void set_tiles(CglGemmDesc& d, int wm, int wn, int wk, int t) {
 // with a 2-way k split beat the model's 1 x 1 x 4 (the two widest forward GEMMs of G, 512 x 1024 x 512 and
 // 512 x 784 x 1024, and G's 1024 x 513 x 256 weight gradient: -0.56 / -0.45 / -0.3 us each, -1.3 us combined
 // interleaved x5).  Keyed on the exact problem; everything else keeps the model.
+// Round 5 (profiles/r05_tile_search.txt, after D's packed weights): D's 512 x 512 x 256 input gradient (row-major A,
+// packed B; the same shape as G2's forward, told apart by its unpacked A) on 1 x 4 x 1, and D0's 512 x 785 x 512
+// weight gradient on 2 x 1 x 2: -1.2 / -1.3 us, -2.1 us combined.  Columns: layout, M, N, K, a_pk (-1 any), WM, WN, WK.
 bool gemm_tile_pick(const CglGemmDesc& d, int* o) {
-  static const int tab[][7] = {{0, 512, 1024, 512, 2, 1, 2}, {0, 512, 784, 1024, 2, 1, 2}, {2, 1024, 513, 256, 2, 1, 2}};
+  static const int tab[][8] = {{0, 512, 1024, 512, -1, 2, 1, 2}, {0, 512, 784, 1024, -1, 2, 1, 2},
+                               {2, 1024, 513, 256, -1, 2, 1, 2}, {0, 512, 512, 256, 0, 1, 4, 1},
+                               {2, 512, 785, 512, -1, 2, 1, 2}};
   if (getenv("CGL_TILE_TABLE") && atoi(getenv("CGL_TILE_TABLE")) == 0) return false;
   for (auto& r : tab)
-    if (d.layout == r[0] && d.M == r[1] && d.N == r[2] && d.K == r[3]) {
-      o[0] = r[4];
-      o[1] = r[5];
-      o[2] = r[6];
+    if (d.layout == r[0] && d.M == r[1] && d.N == r[2] && d.K == r[3] && (r[4] < 0 || d.a_pk == r[4])) {
+      o[0] = r[5];
+      o[1] = r[6];
+      o[2] = r[7];
       return true;
     }
   return false;
