@@ -17,6 +17,8 @@ def _step(fuse, B=256, var="CGL_FUSE_GADAM"):
     from cglgan import GanStep, specs
     from cglgan.init import default_init
     os.environ[var] = "1" if fuse else "0"
+    if var == "CGL_FUSE_DADAM":     # (the fused D Adam turns D's packed weights off: compare against that plan)
+        os.environ["CGL_DPACK"] = "0"
     try:
         gm, dm = specs.mnist_generator(), specs.mnist_discriminator()
         g = torch.Generator().manual_seed(3)
@@ -25,6 +27,7 @@ def _step(fuse, B=256, var="CGL_FUSE_GADAM"):
                      seed=99)
     finally:
         os.environ.pop(var, None)
+        os.environ.pop("CGL_DPACK", None)
     torch.manual_seed(20211212)
     default_init(gm, st.g_views)
     torch.manual_seed(4242)
