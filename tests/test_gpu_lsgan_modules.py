@@ -1,8 +1,12 @@
 """cglgan.lsgan nn.Module drop-ins (model/lsgan.py Generator / Discriminator / MixGenerator) on the
 GPU vs the float64 conv oracle from the same state: forward, backward (parameter and input grads),
 BatchNorm2d running statistics, Dropout2d (masks read back from the module), eval-mode sampling.
-Tolerance: 2e-5 relative to each tensor's max magnitude (fp32 vs fp64), gradients of conv biases
-that feed BatchNorm2d excluded (analytically zero, rounding noise)."""
+Tolerance: the survey's 1e-5 relative to each tensor's max magnitude (fp32 vs fp64) for forwards, every
+gradient and the running statistics (largest observed 1.0e-6, `dz`, profiles/r05_lsgan_module_errors.txt;
+CGL_PRINT_ERR=1 prints each ratio); gradients of conv biases that feed BatchNorm2d excluded (analytically
+zero, rounding noise)."""
+import os
+
 import pytest
 import torch
 
@@ -12,11 +16,13 @@ pytestmark = pytest.mark.gpu
 NOISE = {"conv_blocks.1.bias", "conv_blocks.5.bias", "model.3.bias"}
 
 
-def close(got, ref, rel=2e-5, what=""):
+def close(got, ref, rel=1e-5, what=""):
     got = got.detach().double().cpu()
     ref = ref.detach().double().cpu()
     scale = max(float(ref.abs().max()), 1e-12)
     err = float((got - ref).abs().max())
+    if os.environ.get("CGL_PRINT_ERR"):
+        print(f"ERR {what}: {err / scale:.3e} (bound {rel:.0e})")
     assert err <= rel * scale, f"{what}: max err {err:.3e} vs scale {scale:.3e}"
 
 
@@ -46,8 +52,8 @@ def test_generator_forward_backward_eval():
     (ref * dy.double()).sum().backward()
     for k, p in g.named_parameters():
         if k not in NOISE:
-            close(p.grad, P[k].grad, rel=5e-5, what="G grad " + k)
-    close(zc.grad, z64.grad, rel=5e-5, what="dz")
+            close(p.grad, P[k].grad, rel=1e-5, what="G grad " + k)
+    close(zc.grad, z64.grad, rel=1e-5, what="dz")
     for k, v in g.state_dict().items():
         if "running" in k:
             close(v, Bf[k], what=k)
@@ -78,8 +84,8 @@ def test_discriminator_forward_backward(hw):
     ref.sum().backward()
     for k, p in d.named_parameters():
         if k not in NOISE:
-            close(p.grad, P[k].grad, rel=5e-5, what="D grad " + k)
-    close(xc.grad, x64.grad, rel=5e-5, what="d img")
+            close(p.grad, P[k].grad, rel=1e-5, what="D grad " + k)
+    close(xc.grad, x64.grad, rel=1e-5, what="d img")
     d.eval()
     with torch.no_grad():
         close(d(x.cuda()), CV.d_forward(P, Bf, x.double(), None, train=False), what="D eval")
@@ -100,4 +106,4 @@ def test_mixgenerator_heads():
     (ref * dy.double()).sum().backward()
     for k, p in m.named_parameters():
         if k not in ("model.3.bias", "model.7.bias"):   # feed BatchNorm2d: gradient is rounding noise
-            close(p.grad, P[k].grad, rel=5e-5, what="MixG grad " + k)
+            close(p.grad, P[k].grad, rel=1e-5, what="MixG grad " + k)
