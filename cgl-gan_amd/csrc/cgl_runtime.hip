@@ -274,6 +274,7 @@ struct Launch {
   int abn = 0;              // GEMM operand-transform instantiation (the launch's a_bn)
   bool adpk = false;        // K_ADAM: the cgl_adam_pack form (cgl_gan.adam_pack, or adam_pack_d for D's Adam)
   int apk_d = 0;            // K_ADAM adpk: 1 = D's (cgl_gan.adam_pack_d)
+  bool v4 = false;          // K_ADAM (not adpk): the four-elements-per-thread form (cgl_adam4)
   int layer = -1;           // K_BNAPPLY: the G layer whose forward GEMM reads this launch's output
   int pk = -1;              // K_BNAPPLY: index of the packing jobs it carries (cgl_gan.carry), -1: none
 };
@@ -830,6 +831,12 @@ void push_adam(cgl_gan* c, std::vector<Launch>& ph, float* p, float* g, float* m
   L.adam.found = found;
   L.tail = tail;
   L.grid = (int)((n + 255) / 256);
+  // four elements per thread (cgl_adam4) when the buffers allow 16-byte access (CGL_ADAM4=0: one per thread)
+  const char* e4 = getenv("CGL_ADAM4");
+  if (!(e4 && atoi(e4) == 0) && n % 4 == 0 && al16(p) && al16(g) && al16(m) && al16(v)) {
+    L.v4 = true;
+    L.grid = (int)((n / 4 + 255) / 256);
+  }
   ph.push_back(L);
 }
 
@@ -1828,6 +1835,8 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
       if (L.adpk)
         klaunch(cgl_adam_pack, dim3(L.grid), dim3(256), 0, s, L.adam, L.apk_d ? c->adam_pack_d : c->adam_pack,
                 c->ws.st, L.tail);
+      else if (L.v4)
+        klaunch(cgl_adam4, dim3(L.grid), dim3(256), 0, s, L.adam, c->ws.st, L.tail);
       else
         klaunch(cgl_adam, dim3(L.grid), dim3(256), 0, s, L.adam, c->ws.st, L.tail);
       break;

@@ -56,3 +56,23 @@ def test_fused_launch_bitwise(B, var, kind, pos):
     sa, sb = a.stats(), b.stats()
     for k in ("round", "g_loss", "F", "lambda", "d_loss"):
         assert sa[k] == sb[k], (k, sa[k], sb[k])
+
+
+def test_adam4_bitwise():
+    """cgl_adam4 (four elements per thread, 16-byte accesses; default) vs cgl_adam (CGL_ADAM4=0): the same
+    pinned per-element arithmetic, so the same rounds bit for bit."""
+    os.environ["CGL_ADAM4"] = "0"
+    try:
+        b = _step(False, 256, "CGL_FUSE_GADAM")
+    finally:
+        os.environ.pop("CGL_ADAM4", None)
+    a = _step(False, 256, "CGL_FUSE_GADAM")
+    assert [g for k, _, g in a.launches() if k == "adam"] != [g for k, _, g in b.launches() if k == "adam"]
+    for r in range(5):
+        a.run(graph=r >= 2)
+        b.run(graph=r >= 2)
+    torch.cuda.synchronize()
+    for name in ("g_params", "g_grads", "g_m", "g_v", "d_params", "d_m", "d_v", "g_running", "z"):
+        x, y = getattr(a, name), getattr(b, name)
+        assert torch.equal(x, y), (name, (x - y).abs().max().item())
+    assert a.stats()["lambda"] == b.stats()["lambda"] and a.stats()["F"] == b.stats()["F"]
