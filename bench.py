@@ -73,6 +73,13 @@ def args_():
     p.add_argument("--lowp", choices=["none", "f16", "bf16"], default="f16",
                    help="--model mdgan: also time the same round with 16-bit GEMM operands (BASELINE configs[4]'s "
                         "fp16) and report it beside the fp32 line as 'lowp_variant' (parity unpinned)")
+    p.add_argument("--ring-steps", type=int, default=400,
+                   help="--model mlp at N = 1: also time this many graph-replayed CGLGAN 2-D Gaussian-mixture rounds "
+                        "(configs[0], B=64) and report them as 'ring_round' beside the line (0: skip)")
+    p.add_argument("--graph-rounds", type=int, default=int(os.environ.get("CGL_GRAPH_ROUNDS", "10")),
+                   help="N = 1 fused rounds: this many complete rounds per hipGraph launch in the timed region "
+                        "(cgl_gan_run_graph_rounds; 1 = one graph launch per round)")
+    p.add_argument("--launch-selftest", choices=["ok", "fail"], default=None, help=argparse.SUPPRESS)
     a = p.parse_args()
     if a.batch is None:
         a.batch = default_batch(a.model)
@@ -578,8 +585,24 @@ def cpu_rounds(kind, B, seconds, threads=None):
                       f"{t_total:.1f} s, torch {torch.__version__}"}
 
 
-def timed_rounds(round_fn, a, world):
-    """W untimed rounds, then K rounds between barrier + synchronize; max over ranks."""
+def round_chunks(k, per):
+    """k rounds as multi-round graph launches of `per` rounds plus one of the remainder."""
+    out = [per] * (k // per)
+    if k % per:
+        out.append(k % per)
+    return out
+
+
+def timed_rounds(round_fn, a, world, ex=None):
+    """W untimed rounds, then K rounds between barrier + synchronize; max over ranks.  With ``ex`` (an N = 1
+    WorkerExchange, graph mode) the rounds run as multi-round graphs of --graph-rounds rounds (GanStep.run_rounds:
+    every round complete, no graph-launch boundary inside a launch); their graphs are captured before the timed
+    region."""
+    chunks = None
+    if ex is not None and world == 1 and not a.eager and a.graph_rounds > 1 and ex.comm is None:
+        chunks = round_chunks(a.steps, a.graph_rounds)
+        for n in sorted(set(chunks)):
+            ex.step.prepare_rounds(n)
     torch.cuda.synchronize()
     for r in range(a.warmup):
         round_fn(r)
@@ -587,8 +610,14 @@ def timed_rounds(round_fn, a, world):
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for r in range(a.steps):
-        round_fn(a.warmup + r)
+    if chunks is not None:
+        r = a.warmup
+        for n in chunks:
+            ex.rounds(r, n, graph=True)
+            r += n
+    else:
+        for r in range(a.steps):
+            round_fn(a.warmup + r)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -601,7 +630,7 @@ def timed_rounds(round_fn, a, world):
 
 
 def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None, parity_kind=None, extra=None,
-                 ex=None):
+                 ex=None, emit=True):
     """The bench line of a fused-round model (mlp / mixg / mdgan / ring): GEMM-family roofline from the
     in-round per-launch device durations (profile_inround), CPU baseline and CPU parity at N = 1."""
     st = step.stats()           # the timed rounds' end state (the profile rounds below advance it)
@@ -675,7 +704,8 @@ def fused_report(a, world, rank, step, el, workload, config_extra, cpu_leg=None,
             out["cpu_baseline"] = cpu_leg()
         if parity_kind is not None:
             out["parity"] = parity_vs_cpu(parity_kind, a.batch)
-    print(json.dumps(out), flush=True)
+    if emit:
+        print(json.dumps(out), flush=True)
     return out
 
 
@@ -684,15 +714,18 @@ def main_mlp(a, world, rank):
     with torch.cuda.stream(stream):
         step, _ = build_step(a, rank, world)
         ex = make_exchange(step, world, a)
-        el = timed_rounds(lambda r: ex.round(r, graph=not a.eager), a, world)
+        el = timed_rounds(lambda r: ex.round(r, graph=not a.eager), a, world, ex=ex)
         conv = conv_extra(a, world, rank)
+    ring = ring_extra(a, world, rank)
+    extra = {k: v for k, v in (("conv_round", conv), ("ring_round", ring)) if v}
+    with torch.cuda.stream(stream):
         wl = ("C2: model/mnist_model.py MLP GAN, CAPGAN worker round (G fwd x2, D step, G loss, G bwd, Adam G/D), "
               "1 worker per GPU" if world == 1 else
               f"C3: CAPGAN {world} workers (1 per GPU), S=1, lambda-weighted G-gradient all-reduce + E={a.E} D "
               f"all-reduce over RCCL")
         return fused_report(a, world, rank, step, el, wl, {"img": "28x28x1", "dataset_rows_per_worker": a.rows},
                             cpu_leg=lambda: cpu_variants(lambda t: cpu_baseline(a, t)), parity_kind="capgan", ex=ex,
-                            extra={"conv_round": conv} if conv else None)
+                            extra=extra or None)
 
 
 def main_driver(a, world, rank, algo):
@@ -740,7 +773,7 @@ def main_driver(a, world, rank, algo):
                             extra={"lowp_variant": lowp} if lowp else None, ex=drv.exchange)
 
 
-def main_ring(a, world, rank):
+def main_ring(a, world, rank, emit=True):
     """BASELINE configs[0]: CGLGAN/2DMG, one worker, the 2-D Gaussian-mixture ring (num_class=8), B=64."""
     from cglgan import GanStep, specs
     from cglgan.data import gmm
@@ -757,22 +790,121 @@ def main_ring(a, world, rank):
         default_init(dm, step.d_views)
         step.reset()
         ex = make_exchange(step, world, a)
-        el = timed_rounds(lambda r: ex.round(r, graph=not a.eager), a, world)
+        el = timed_rounds(lambda r: ex.round(r, graph=not a.eager), a, world, ex=ex)
         wl = ("C1: CGLGAN/2DMG ring GAN (G 100-32-2, D 2-128-256-1 Sigmoid, BCE, closed-form lambda), 8-mode 2-D "
               "Gaussian mixture, 1 worker per GPU" + (f", {world} workers" if world > 1 else ""))
         return fused_report(a, world, rank, step, el, wl, {"data_points": int(data.shape[0])},
                             cpu_leg=lambda: cpu_variants(lambda t: cpu_rounds("ring", a.batch, a.cpu_seconds, t)),
-                            parity_kind="ring", ex=ex)
+                            parity_kind="ring", ex=ex, emit=emit)
+
+
+def ring_extra(a, world, rank):
+    """BASELINE configs[0] (the CGLGAN/2DMG 2-D Gaussian-mixture round, B=64) timed beside the default C2 line at
+    N = 1: its own graph-replayed timed region (--ring-steps rounds), GEMM-family roofline, 10-round CPU parity and a
+    short CPU-oracle sample.  A labelled extra key, never `value`."""
+    if world != 1 or a.ring_steps <= 0:
+        return None
+    ra = argparse.Namespace(**vars(a))
+    ra.model, ra.batch, ra.steps, ra.warmup = "ring", default_batch("ring"), a.ring_steps, 20
+    ra.cpu_seconds = min(a.cpu_seconds, 3.0)
+    out = main_ring(ra, world, rank, emit=False)
+    if out is None:
+        return None
+    out["metric"] = METRIC + " [configs[0]: CGLGAN/2DMG 2-D Gaussian-mixture round]"
+    out["note"] = ("third workload of the same bench run (BASELINE configs[0], B=%d), timed in its own region after "
+                   "the C2 line's; not part of `value`; cpu_baseline is a %.0f s sample" % (ra.batch, ra.cpu_seconds))
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# --gpus N > 1 without a launcher: this process spawns torch.distributed.run as a CHILD (never an exec) before
+# anything touches the GPU, forwards the ranks' stdout (rank 0's JSON line) and exits with the launcher's status.
+_RANK_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
+             "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT",
+             "TORCHELASTIC_MAX_RESTARTS")
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launcher_cmd(argv, n, port):
+    """The child command: one rank per GPU on this node, rendezvous on 127.0.0.1 (the container's hostname may
+    not resolve), this script with the caller's arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launcher_env(base=None):
+    """The children's environment: the parent's, without any rank variables (the launcher sets its own), with
+    dmabuf IPC for RCCL (HSA_ENABLE_IPC_MODE_LEGACY=0, the only IPC mode of this pool's host driver)."""
+    env = dict(os.environ if base is None else base)
+    for k in _RANK_ENV:
+        env.pop(k, None)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["PYTHONUNBUFFERED"] = "1"
+    return env
+
+
+def self_launch(n, argv):
+    """Run this bench on n ranks through torch.distributed.run as a child process: every stdout line of the
+    ranks is forwarded as it arrives; returns the launcher's exit status, or 1 when it succeeded without
+    printing the JSON line."""
+    import subprocess
+    cmd = launcher_cmd(argv, n, free_port())
+    print("bench: launching " + " ".join(cmd), file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, env=launcher_env(), stdout=subprocess.PIPE, text=True, bufsize=1)
+    lines = 0
+    for line in p.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+        if line.lstrip().startswith("{"):
+            lines += 1
+    rc = p.wait()
+    if rc != 0:
+        print(f"bench: torch.distributed.run exited with status {rc}", file=sys.stderr, flush=True)
+        return rc
+    if lines == 0:
+        print("bench: no JSON line from rank 0", file=sys.stderr, flush=True)
+        return 1
+    return 0
+
+
+def launch_selftest(mode):
+    """The launcher plumbing on CPU (tests/test_bench_launcher.py): gloo group over the launcher's env, one
+    all_reduce, rank 0 prints a JSON line with what each rank saw; mode "fail" makes rank 1 exit with status 3."""
+    world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+    if mode == "fail" and rank == 1:
+        sys.exit(3)
+    dist.init_process_group("gloo")
+    t = torch.tensor([float(rank + 1)])
+    dist.all_reduce(t)
+    seen = [None] * world
+    dist.all_gather_object(seen, {"rank": rank, "local_rank": int(os.environ["LOCAL_RANK"]),
+                                  "master": f"{os.environ['MASTER_ADDR']}:{os.environ['MASTER_PORT']}",
+                                  "ipc_legacy": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")})
+    if rank == 0:
+        print(json.dumps({"selftest": True, "world": world, "sum": float(t.item()), "ranks": seen}), flush=True)
+    dist.destroy_process_group()
 
 
 def main():
     a = args_()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        # (nothing has initialised the GPU yet: the child launcher owns the devices)
+        sys.exit(self_launch(a.gpus, sys.argv[1:]))
+    if a.launch_selftest:
+        return launch_selftest(a.launch_selftest)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            raise SystemExit("--gpus N > 1 needs torch.distributed.run with N processes")
+        print(f"bench: --gpus {a.gpus}, the launcher started {world} ranks: measuring {world}", file=sys.stderr)
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))

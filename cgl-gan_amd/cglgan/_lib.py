@@ -22,7 +22,7 @@ MODEL_G, MODEL_D = 0, 1
 # every symbol include/cglgan.h declares (checked by tests/test_lib_exports.py)
 EXPORTS = [
     "cgl_gan_param_count", "cgl_gan_param_tensor", "cgl_gan_running_count", "cgl_gan_workspace_bytes",
-    "cgl_gan_create", "cgl_gan_destroy", "cgl_gan_reset", "cgl_gan_sync_params", "cgl_gan_sync_params_d", "cgl_gan_gemm_trace", "cgl_gan_run", "cgl_gan_run_graph",
+    "cgl_gan_create", "cgl_gan_destroy", "cgl_gan_reset", "cgl_gan_sync_params", "cgl_gan_sync_params_d", "cgl_gan_gemm_trace", "cgl_gan_run", "cgl_gan_run_graph", "cgl_gan_run_graph_rounds", "cgl_gan_prepare_graph_rounds",
     "cgl_gan_alpha_scale", "cgl_gan_exchange_mode", "cgl_gan_gather_buffers",
     "cgl_gan_exchange_buffer", "cgl_gan_tensor", "cgl_gan_read_stats",
     "cgl_gan_plan_info", "cgl_gan_launch_count", "cgl_gan_launch_info", "cgl_gan_launch_one", "cgl_gan_profile", "cgl_linear_fwd", "cgl_linear_bwd_data", "cgl_linear_bwd_weight", "cgl_adam_step",
@@ -127,6 +127,8 @@ def _load():
         "cgl_gan_gemm_trace": (i64, [vp, vp, i64]),
         "cgl_gan_run": (ci, [vp, ci, vp]),
         "cgl_gan_run_graph": (ci, [vp, ci, vp]),
+        "cgl_gan_run_graph_rounds": (ci, [vp, ci, vp]),
+        "cgl_gan_prepare_graph_rounds": (ci, [vp, ci, vp]),
         "cgl_gan_alpha_scale": (ci, [vp, vp]),
         "cgl_gan_exchange_mode": (ci, [vp, ci]),
         "cgl_gan_gather_buffers": (ci, [vp, vp, vp, vp]),

@@ -61,14 +61,16 @@ class DistComm:
     def all_reduce_sum(self, t: torch.Tensor):
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
 
+    def all_reduce_min(self, t: torch.Tensor):
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+
     def all_reduce_mean(self, t: torch.Tensor, weights=None):
-        """sum_i w_i t_i (w = 1/N when None); identical result on every rank.  Over RCCL the plain mean is one
-        ReduceOp.AVG collective (no separate division launch); gloo sums and divides."""
+        """sum_i w_i t_i (w = 1/N when None); identical result on every rank.  The plain mean is the sum divided by
+        N on every backend (RCCL's ReduceOp.AVG computes sum(x_i * (1/N)), which is not the gloo / LocalComm value
+        for N not a power of two); the division is one captured launch inside the whole-round graph."""
         if weights is not None:
             t.mul_(float(weights[self.rank]))
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
-        elif self.capturable:
-            dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group)
         else:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
             t.div_(self.size)
@@ -145,20 +147,35 @@ class WorkerExchange:
             raise ValueError(f"step planned for {step.n_workers} workers, group has {n}")
         if exchange not in ("auto", "gather", "reduce"):
             raise ValueError("exchange must be 'auto', 'gather' or 'reduce'")
-        if exchange == "auto":
+        auto = exchange == "auto"
+        if auto:
             exchange = "gather" if n <= GATHER_MAX_WORKERS and hasattr(step, "set_exchange") else "reduce"
-        if exchange == "gather" and comm is not None:
-            step.set_exchange("gather")
+        if comm is not None and hasattr(step, "set_exchange"):
+            # the library's mode is set for BOTH forms: a step keeps its mode, so a later exchange in the other form
+            # must not run phase B's combine over a stale gather buffer
+            try:
+                step.set_exchange(exchange)
+            except RuntimeError:
+                # the gathered form needs the combine head, planned only when the exchange tensor's size is a
+                # multiple of 4 floats (cgl_gan_exchange_mode returns CGL_E_STATE otherwise): auto falls back
+                if not (auto and exchange == "gather"):
+                    raise
+                exchange = "reduce"
+                step.set_exchange(exchange)
         self.exchange = exchange
-        # whole-round graph (graph=True rounds without a D exchange): phase A, this rank's collective(s) and phase B
+        # whole-round graph (graph=True rounds without a D-swap): phase A, this rank's collective(s) and phase B
         # captured as ONE torch CUDA graph once a split round has run eagerly through the group (RCCL's
         # communicator and buffers exist), replayed after -- the library's two graph launches, the collective
         # calls and (reduce form) the alpha launch leave the host path.  Only over a capturable group (RCCL);
-        # CGL_ROUND_GRAPH=0 keeps the split path.
+        # CGL_ROUND_GRAPH=0 keeps the split path.  The first replay of each captured form is checked against the
+        # split path on the same state (``_verify_round_graph``: bitwise, agreed over the group), so a stack whose
+        # captured collectives misbehave falls back to the split rounds instead of training on wrong values.
         self.round_graph = (os.environ.get("CGL_ROUND_GRAPH", "1") != "0" and
                             bool(getattr(comm, "capturable", False)) and hasattr(step, "g_params") and
                             step.g_params.is_cuda)
         self._rgraph, self._split_ran = {}, False
+        self.round_graph_checks = []      # (share, local verdict, group verdict) of every verification run
+        self._rgraph_verified = set()
         # D's exchange (E-share / D-swap) after phase B on the main stream (default), or on a side stream beside
         # phase B (CGL_DX_SIDE=1).  Measured at world 1: the side branch slows every phase-B launch it runs beside
         # (+64 us per round for a ~15 us exchange, tests/rccl_world1_worker.py --time); serial it costs its own time.
@@ -184,31 +201,90 @@ class WorkerExchange:
         if self.comm is None or (self.comm.size == 1 and not self.force_split):
             s.run(C.PHASE_ALL, graph=graph)
         elif graph and self.round_graph and self._split_ran and not swap and self._ensure_round_graph(share):
-            s._packed_current()          # (host-side check of the packed weight copies, as s.run does)
-            self._rgraph[share].replay()
-            share = False                # (the E-share ran inside the graph)
-        else:
-            self._split_ran = True
-            s.run(C.PHASE_A, graph=graph)
-            self.exchange_mid()
-            side = self._side_stream() if ((share or swap) and self.d_side) else None
-            if side is not None:
-                # phase B (G backward + Adam G) never touches D: the E-share all-reduce / D-swap of
-                # this round's updated D run on a side stream concurrently with it (issued in the
-                # same order on every rank), joined before the next round's D step
-                main = torch.cuda.current_stream()
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    self._d_exchange(r, share, swap)
-                s.run(C.PHASE_B, graph=graph)
-                main.wait_stream(side)
-                share = swap = False
+            if share in self._rgraph_verified:
+                s._packed_current()          # (host-side check of the packed weight copies, as s.run does)
+                self._rgraph[share].replay()
             else:
-                s.run(C.PHASE_B, graph=graph)
+                self._verify_round_graph(r, share)
+            share = False                # (the E-share ran inside the graph, or inside the verified split round)
+        else:
+            self._split_round(r, share, swap, graph)
+            share = swap = False
         self._d_exchange(r, share, swap)
         if (self.cloud is not None and self.cloud_due is None and self.cloud_every > 0 and
                 (r + 1) % self.cloud_every == 0):
             self.cloud_average()
+
+    def rounds(self, r0: int, n: int, graph: bool = True):
+        """Rounds r0 .. r0 + n - 1.  A worker with no group and no Cloud step (N = 1) runs them as multi-round graphs
+        (GanStep.run_rounds); otherwise round by round."""
+        if n <= 0:
+            return
+        if self.comm is None and self.cloud is None and graph and hasattr(self.step, "run_rounds"):
+            self.step.run_rounds(n, graph=True)
+            return
+        for r in range(r0, r0 + n):
+            self.round(r, graph=graph)
+
+    def _split_round(self, r, share, swap, graph):
+        """Phase A, the collective(s), phase B as separate calls, then D's exchange (E-share / D-swap)."""
+        s = self.step
+        self._split_ran = True
+        s.run(C.PHASE_A, graph=graph)
+        self.exchange_mid()
+        side = self._side_stream() if ((share or swap) and self.d_side) else None
+        if side is not None:
+            # phase B (G backward + Adam G) never touches D: the E-share all-reduce / D-swap of
+            # this round's updated D run on a side stream concurrently with it (issued in the
+            # same order on every rank), joined before the next round's D step
+            main = torch.cuda.current_stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self._d_exchange(r, share, swap)
+            s.run(C.PHASE_B, graph=graph)
+            main.wait_stream(side)
+        else:
+            s.run(C.PHASE_B, graph=graph)
+            self._d_exchange(r, share, swap)
+
+    _STATE = ("g_params", "g_grads", "g_m", "g_v", "g_running", "d_params", "d_grads", "d_m", "d_v", "losses_all",
+              "workspace")
+    _COMPARED = ("g_params", "g_m", "g_v", "g_running", "d_params", "d_m", "d_v")
+
+    @torch.no_grad()
+    def _verify_round_graph(self, r, share):
+        """First use of a captured whole-round graph: round r runs through the split path (the reference form), the
+        step's buffers are put back, the graph replays round r, and the two end states are compared bitwise (G, D,
+        both Adams' moments, the running statistics, the round's losses).  Every rank of the group must agree
+        (MIN-all-reduce of the verdict) before the graph is used; otherwise the split result is restored and the
+        whole-round graph is turned off for this exchange.  Costs one extra round's work, once per captured form."""
+        s = self.step
+        s._packed_current()
+        before = {k: getattr(s, k).clone() for k in self._STATE}
+        self._split_round(r, share, False, True)
+        split = {k: getattr(s, k).clone() for k in self._STATE}
+        st_split = s.stats()
+        for k in self._STATE:
+            getattr(s, k).copy_(before[k])
+        s.sync_params()                   # (the restored parameters' packed copies and the next z)
+        self._rgraph[share].replay()
+        st_graph = s.stats()
+        ok = all(torch.equal(getattr(s, k), split[k]) for k in self._COMPARED)
+        ok = ok and all(st_graph[k] == st_split[k] for k in ("round", "d_loss", "g_loss", "lambda", "F"))
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=s.g_params.device)
+        self.comm.all_reduce_min(flag)
+        ok_all = bool(flag.item())
+        self.round_graph_checks.append((share, ok, ok_all))
+        if ok_all:
+            self._rgraph_verified.add(share)
+            return
+        import warnings
+        warnings.warn("whole-round graph replay differs from the split round on this stack (local %s): split rounds "
+                      "from now on" % ok)
+        for k in self._STATE:
+            getattr(s, k).copy_(split[k])
+        s.sync_params()
+        self.round_graph = False
 
     def _ensure_round_graph(self, share):
         """Capture the whole-round graph (one per round form: with / without the E-share) on first use; a capture
@@ -316,6 +392,8 @@ class LocalComm:
         for s in steps:
             if s.n_workers != self.size:
                 raise ValueError(f"step planned for {s.n_workers} workers, group has {self.size}")
+            if self.size > 1 and hasattr(s, "set_exchange"):
+                s.set_exchange("reduce")      # (this rehearsal runs alpha_scale + the summed exchange buffer)
 
     def round(self, r: int, graph: bool = False, share_every: int = None):
         ss = self.steps

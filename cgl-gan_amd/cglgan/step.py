@@ -282,6 +282,24 @@ class GanStep:
         fn = C.lib.cgl_gan_run_graph if graph else C.lib.cgl_gan_run
         C.check(fn(self._h, phase, _stream()), "cgl_gan_run")
 
+    def run_rounds(self, rounds: int, graph: bool = True):
+        """``rounds`` complete rounds (N = 1 or the caller's own lockstep): with ``graph`` one hipGraph launch holding
+        them back to back (cgl_gan_run_graph_rounds: no graph-launch boundary between the rounds), else that many
+        ``run()`` calls.  Identical to ``rounds`` calls of ``run(graph=graph)``."""
+        if rounds <= 0:
+            return
+        if not graph:
+            for _ in range(rounds):
+                self.run(C.PHASE_ALL, graph=False)
+            return
+        self._packed_current()
+        C.check(C.lib.cgl_gan_run_graph_rounds(self._h, int(rounds), _stream()), "cgl_gan_run_graph_rounds")
+
+    def prepare_rounds(self, rounds: int):
+        """Capture the ``rounds``-round graph ahead of its first use (one stream synchronisation)."""
+        if rounds >= 2:
+            C.check(C.lib.cgl_gan_prepare_graph_rounds(self._h, int(rounds), _stream()), "cgl_gan_prepare_graph_rounds")
+
     def alpha_scale(self):
         C.check(C.lib.cgl_gan_alpha_scale(self._h, _stream()), "cgl_gan_alpha_scale")
 

@@ -532,6 +532,10 @@ struct cgl_gan {
   std::vector<CglBnApplyDesc> bna;
   std::vector<Launch> phA, phB;
   hipGraphExec_t gexec[3] = {nullptr, nullptr, nullptr};
+  // whole rounds back to back in one graph (cgl_gan_run_graph_rounds): gexec_k[i] holds kRoundGraphs[i] rounds
+  static constexpr int kRoundGraphs = 4;
+  hipGraphExec_t gexec_k[kRoundGraphs] = {nullptr, nullptr, nullptr, nullptr};
+  int gexec_kn[kRoundGraphs] = {0, 0, 0, 0};
   hipStream_t cap = nullptr;   // private capture stream (the legacy default stream cannot capture)
   hipStream_t side = nullptr;  // second stream: the real-row D chain of the first local D step
   CglOpPack pack{};          // the round prologue's operand-packing jobs (none when pack_adam)
@@ -559,6 +563,8 @@ struct cgl_gan {
   int64_t run_mean_off[CGL_MAX_LAYERS], run_var_off[CGL_MAX_LAYERS];
   ~cgl_gan() {
     for (auto& g : gexec)
+      if (g) (void)hipGraphExecDestroy(g);
+    for (auto& g : gexec_k)
       if (g) (void)hipGraphExecDestroy(g);
     if (cap) (void)hipStreamDestroy(cap);
     if (side) (void)hipStreamDestroy(side);
@@ -2132,6 +2138,65 @@ int cgl_gan_run_graph(cgl_gan* c, int phase, void* stream) {
     c->gexec[phase] = ex;
   }
   HIPCHK(hipGraphLaunch(c->gexec[phase], s));
+  return CGL_OK;
+}
+
+// the cached graph of `rounds` whole rounds (captured and instantiated on first use; *slot its cache entry)
+static int graph_rounds_slot(cgl_gan* c, int rounds, hipStream_t s, int* slot_out) {
+  int slot = -1;
+  for (int i = 0; i < cgl_gan::kRoundGraphs && slot < 0; ++i)
+    if (c->gexec_kn[i] == rounds) slot = i;
+  if (slot < 0) {
+    // every round reads its per-round values (round counter, z, sampler position, Adam steps, schedules) from the
+    // device state the previous round advanced, so `rounds` copies of the round's launch sequence captured back to
+    // back are those rounds; the graph launch boundary between rounds (and its completion signal) is gone
+    for (int i = 0; i < cgl_gan::kRoundGraphs && slot < 0; ++i)
+      if (!c->gexec_k[i]) slot = i;
+    if (slot < 0) {                                    // (a small cache: the oldest entry makes room)
+      (void)hipGraphExecDestroy(c->gexec_k[0]);
+      for (int i = 1; i < cgl_gan::kRoundGraphs; ++i) {
+        c->gexec_k[i - 1] = c->gexec_k[i];
+        c->gexec_kn[i - 1] = c->gexec_kn[i];
+      }
+      slot = cgl_gan::kRoundGraphs - 1;
+      c->gexec_k[slot] = nullptr;
+      c->gexec_kn[slot] = 0;
+    }
+    if (!c->cap) HIPCHK(hipStreamCreateWithFlags(&c->cap, hipStreamNonBlocking));
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipStreamBeginCapture(c->cap, hipStreamCaptureModeThreadLocal));
+    int e = 0;
+    for (int r = 0; r < rounds && !e; ++r) e = run_phase(c, CGL_PHASE_ALL, c->cap);
+    hipGraph_t g;
+    const hipError_t ec = hipStreamEndCapture(c->cap, &g);
+    if (e) return e;
+    HIPCHK(ec);
+    hipGraphExec_t ex;
+    const hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    HIPCHK(ei);
+    c->gexec_k[slot] = ex;
+    c->gexec_kn[slot] = rounds;
+  }
+  *slot_out = slot;
+  return CGL_OK;
+}
+
+int cgl_gan_prepare_graph_rounds(cgl_gan* c, int rounds, void* stream) {
+  CGL_BATCH_GUARD();
+  if (!c || rounds < 2 || rounds > CGL_MAX_GRAPH_ROUNDS) return CGL_E_ARG;
+  int slot;
+  return graph_rounds_slot(c, rounds, (hipStream_t)stream, &slot);
+}
+
+int cgl_gan_run_graph_rounds(cgl_gan* c, int rounds, void* stream) {
+  CGL_BATCH_GUARD();
+  if (!c || rounds < 1 || rounds > CGL_MAX_GRAPH_ROUNDS) return CGL_E_ARG;
+  if (rounds == 1) return cgl_gan_run_graph(c, CGL_PHASE_ALL, stream);
+  int slot;
+  const int e = graph_rounds_slot(c, rounds, (hipStream_t)stream, &slot);
+  if (e) return e;
+  HIPCHK(hipGraphLaunch(c->gexec_k[slot], (hipStream_t)stream));
   return CGL_OK;
 }
 

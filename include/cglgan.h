@@ -161,6 +161,17 @@ int64_t cgl_gan_gemm_trace(cgl_gan* ctx, unsigned long long* host_out, int64_t n
 int cgl_gan_run(cgl_gan* ctx, int phase, void* stream);
 /* Same, through a captured hipGraph (captured on first use, replayed after). */
 int cgl_gan_run_graph(cgl_gan* ctx, int phase, void* stream);
+/* `rounds` complete rounds (phase CGL_PHASE_ALL, 1 <= rounds <= CGL_MAX_GRAPH_ROUNDS) as ONE hipGraph launch: the
+ * round's launch sequence captured `rounds` times back to back (captured on first use per count, a few counts
+ * cached).  Every round reads its per-round values from the device state the previous one advanced, so this is
+ * exactly `rounds` calls of cgl_gan_run_graph(ctx, CGL_PHASE_ALL, stream) without the graph-launch boundary
+ * between them (N = 1 worker loops: capgan.py:211-262 + :316-349 repeated over num_communication).  Stats read
+ * afterwards describe the last round. */
+#define CGL_MAX_GRAPH_ROUNDS 64
+int cgl_gan_run_graph_rounds(cgl_gan* ctx, int rounds, void* stream);
+/* Capture and instantiate the `rounds`-round graph (2 <= rounds <= CGL_MAX_GRAPH_ROUNDS) without launching it
+ * (synchronises `stream` once), so a timed or latency-critical loop never pays the capture. */
+int cgl_gan_prepare_graph_rounds(cgl_gan* ctx, int rounds, void* stream);
 /* Exchange step: alpha from losses_all (already gathered), then scale this worker's exchange
  * gradient by alpha[rank] in place, ready for an all-reduce(sum). */
 int cgl_gan_alpha_scale(cgl_gan* ctx, void* stream);

@@ -143,6 +143,9 @@ def check_round_graph(exchange, share_every=0):
         ref.round(r, graph=(r != 3))
     torch.cuda.synchronize()
     assert ex._rgraph and ex.round_graph
+    # every captured form's first replay was verified against the split round (bitwise, group verdict)
+    assert ex.round_graph_checks and all(ok and ok_all for _, ok, ok_all in ex.round_graph_checks), \
+        ex.round_graph_checks
     same(a, b, ("g_params", "g_m", "g_v", "d_params", "d_m", "d_v", "g_running"))
     assert a.stats()["round"] == b.stats()["round"] == 6
 
