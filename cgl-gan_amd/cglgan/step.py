@@ -47,6 +47,14 @@ class GanStep:
 
     Knobs mirror the reference drivers' module globals: ``batch`` (batch_size, capgan.py:48),
     ``epoch`` (local D steps, capgan.py:50), ``b1``/``b2`` (capgan.py:52-53), lr 2e-4 (:122).
+
+    Packed weight copies: the GEMMs read fragment-packed copies of G's and D's weight matrices, kept current by
+    the rounds' own Adam launches.  A write of ``g_params`` / ``d_params`` (or of any view of them) from outside the
+    round is noticed through torch's version counter and the copies are refreshed before the next round.  Writes the
+    counter does not see -- through ``.data``, DLPack or another library, or an in-place collective issued by the
+    caller on the raw buffer -- must be followed by ``sync_params()`` (both models) or ``sync_params_d()`` (D only);
+    otherwise the next rounds run on the old weights.  (G's copies are re-packed inside every round by the forward
+    BatchNorm / loss-head launches; D's copies and the next round's z are the ones a missed write leaves stale.)
     """
 
     def __init__(self, g: MlpModel, d: MlpModel, batch: int, batch_real: int = None, epoch: int = 1,
