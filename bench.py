@@ -405,13 +405,22 @@ def conv_round_measure(a, world, rank, steps, warmup, with_cpu):
         for _ in range(warmup):
             ex.round(r)
             r += 1
+        # N = 1 graph rounds: --graph-rounds whole rounds per graph replay (ConvGanStep.run_rounds), captured here
+        chunks = (round_chunks(steps, a.graph_rounds) if world == 1 and not a.eager and a.graph_rounds > 1
+                  else [1] * steps)
+        for n in sorted(set(chunks)):
+            if n > 1:
+                step.prepare_rounds(n)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
-        for _ in range(steps):
-            ex.round(r)
-            r += 1
+        for n in chunks:
+            if n == 1:
+                ex.round(r)
+            else:
+                ex.rounds(r, n)
+            r += n
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()

@@ -32,7 +32,7 @@ EXPORTS = [
     "cgl_conv3x3_workspace_bytes", "cgl_conv3x3_fwd", "cgl_conv3x3_bwd_data", "cgl_conv3x3_bwd_weight",
     "cgl_conv3x3_bwd_weight_bnin", "cgl_conv3x3_bwd_weight_actdrop",
     "cgl_bn2d_workspace_bytes", "cgl_bn2d_fwd", "cgl_bn2d_bwd", "cgl_act_drop_bwd", "cgl_act_drop_bwd_colsum", "cgl_colsum_finalize", "cgl_dropout2d_mask", "cgl_dropout2d_masks",
-    "cgl_nchw_to_nhwc", "cgl_nhwc_to_nchw", "cgl_dense1_bwd_data_nhwc", "cgl_dense1_fwd_nhwc", "cgl_adv_loss", "cgl_adam_multi", "cgl_dense_workspace_bytes",
+    "cgl_nchw_to_nhwc", "cgl_nhwc_to_nchw", "cgl_dense1_bwd_data_nhwc", "cgl_dense1_fwd_nhwc", "cgl_dense1_head_nhwc", "cgl_adv_loss", "cgl_adam_multi", "cgl_dense_workspace_bytes",
     "cgl_dense_fwd", "cgl_dense_bwd_data", "cgl_dense_bwd_weight", "cgl_gather_rows", "cgl_weights_scale",
     "cgl_conv_packed_floats", "cgl_conv_pack_multi", "cgl_conv_batch_begin", "cgl_conv_batch_end", "cgl_conv3x3_fwd_packed", "cgl_conv3x3_bwd_data_packed",
     "cgl_dense_fwd_packed", "cgl_dense_bwd_data_packed", "cgl_conv3x3_stat_chunks", "cgl_conv3x3_fwd_packed_stats",
@@ -170,6 +170,8 @@ def _load():
         "cgl_dense1_fwd_nhwc": (ci, [vp, vp, vp, vp, vp, ci, ci, ci, vp]),
         "cgl_nhwc_to_nchw": (ci, [vp, vp, ci, ci, ci, vp]),
         "cgl_adv_loss": (ci, [vp, ci, ci, ci, ci, cd, vp, vp, vp, vp]),
+        "cgl_dense1_head_nhwc": (ci, [vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, cd, vp, vp, ci, cd, vp, vp,
+                                      vp]),
         "cgl_dense_workspace_bytes": (i64, [ci] * 3),
         "cgl_dense_fwd": (ci, [vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, i64, vp]),
         "cgl_dense_bwd_data": (ci, [vp, vp, vp, ci, ci, ci, vp, i64, vp]),

@@ -510,6 +510,23 @@ def nhwc_to_nchw(x, y, n, c, hw):
     return y
 
 
+def dense1_head_nhwc(x, w, b, y, dy, dx, n, c, hw, kind, calls, scratch, flat=None):
+    """adv_layer forward + loss + input gradient in one launch (cgl_dense1_head_nhwc).  ``calls``: [(rows, target,
+    weight, loss_out, nvalid)] -- one or two calls over consecutive rows (nvalid: the first call only).
+    ``scratch``: >= n + 16 floats, zeroed once before its first use (a monotonic ticket + the loss terms)."""
+    _chk(x, w, b, y, dy, dx, flat, scratch)
+    if len(calls) not in (1, 2) or sum(cl[0] for cl in calls) != n:
+        raise ValueError("dense1_head_nhwc: one or two calls covering the n rows")
+    if (x.numel() < n * c * hw or w.numel() < c * hw or y.numel() < n or dy.numel() < n or dx.numel() < n * c * hw or
+            scratch.numel() < n + 16 or (flat is not None and flat.numel() < n * c * hw)):
+        raise ValueError("dense1_head_nhwc: tensor too small for the geometry")
+    (n0, t0, w0, l0, nv0) = calls[0]
+    (t1, w1, l1) = (calls[1][1], calls[1][2], calls[1][3]) if len(calls) > 1 else (0, 0.0, None)
+    C.check(C.lib.cgl_dense1_head_nhwc(_p(x), _p(w), _p(b), _p(y), _p(flat), _p(dy), _p(dx), n, c, hw, LOSS[kind],
+                                       n0, int(t0), float(w0), _p(l0), _p(nv0), int(t1), float(w1), _p(l1),
+                                       _p(scratch), _s()), "cgl_dense1_head_nhwc")
+
+
 def adv_loss(x, M, Cc, kind, target, weight, loss_out=None, grad=None, nvalid=None):
     """``nvalid`` (device int32, may be None): only the first *nvalid rows form the batch (mean over them,
     zero gradient on the rest)."""

@@ -197,6 +197,7 @@ class ConvGanStep:
         self.nv.fill_(batch)
         self._dstate_host = (0, 0, 0)         # host mirror of dstate after the last issued round
         self._cuda_graph = None
+        self._kgraphs = {}             # rounds -> graph of that many whole rounds (run_rounds)
         self._phase_graphs = None      # (phase A, phase B) graphs of the split round (N > 1)
         self._split_graph = False
         self._graph_delta = None
@@ -281,6 +282,11 @@ class ConvGanStep:
         # D's Conv2d(1, 16) weight gradient applies its block's LeakyReLU + Dropout2d backward in its loads in the D
         # step (cgl_conv3x3_bwd_weight_actdrop; bitwise, one launch fewer; CGL_CONV_C1FUSE=0 keeps act_drop_bwd)
         self.c1_fuse = os.environ.get("CGL_CONV_C1FUSE", "1") != "0"
+        # the D head (adv_layer forward, the loss head(s), adv_layer's input gradient) as ONE launch per pass
+        # (cgl_dense1_head_nhwc, bitwise the separate launches; CGL_CONV_HEADFUSE=0 keeps them).  Each pass has its
+        # own scratch: a monotonic ticket counted modulo that launch's grid + the per-row loss terms
+        self.head_fuse = os.environ.get("CGL_CONV_HEADFUSE", "1") != "0"
+        self.hscr_d, self.hscr_g = torch.zeros(B2 + 16, device=dev), torch.zeros(B + 16, device=dev)
         self.bpart = (torch.zeros(2 * (B * 1024 // 256), dtype=torch.float64, device=dev)
                       if os.environ.get("CGL_CONV_BIASFUSE", "1") != "0" and B * 1024 % 256 == 0 and B <= 2048 else None)
         # sampler over a device-resident real shard [n, 1024] (DataLoader(shuffle=True), capgan.py:282)
@@ -496,13 +502,21 @@ class ConvGanStep:
                     inp = self.r[k]
         # out.view(B, -1) -> adv_layer (model/lsgan.py:96-97) from the NHWC map; the D step's call keeps the
         # NCHW view for adv_layer's weight gradient, the G-loss pass (no D weight gradient) does not
-        O.dense1_fwd_nhwc(self.r[3], P["adv_layer.weight"], P["adv_layer.bias"], self.v, n, 128, 4,
-                          flat=self.flat if masks is self.mask_d else None)
+        if not self.head_fuse:      # (fused: the head launch of _head computes it)
+            O.dense1_fwd_nhwc(self.r[3], P["adv_layer.weight"], P["adv_layer.bias"], self.v, n, 128, 4,
+                              flat=self.flat if masks is self.mask_d else None)
+
+    def _head(self, n, calls, scratch, flat):
+        """adv_layer forward + the loss head(s) + adv_layer's input gradient (dr[3]) as one launch."""
+        P = self.D.params
+        O.dense1_head_nhwc(self.r[3], P["adv_layer.weight"], P["adv_layer.bias"], self.v, self.dv, self.dr[3], n, 128,
+                           4, self.loss, calls, scratch, flat=flat)
 
     def _d_backward(self, x, n, groups, masks, wgrad, dx, nvalid=None):
         P, G = self.D.params, self.D.grads
         bst = set()     # BatchNorms whose backward partials the previous input-gradient conv wrote
-        O.dense1_bwd_data_nhwc(self.dv, P["adv_layer.weight"], self.dr[3], n, 128, 4)
+        if not self.head_fuse:      # (fused: the head launch wrote dr[3])
+            O.dense1_bwd_data_nhwc(self.dv, P["adv_layer.weight"], self.dr[3], n, 128, 4)
         if wgrad:
             O.dense_bwd_weight(self.dv, self.flat, G["adv_layer.weight"], G["adv_layer.bias"], n, 512, 1)
         c1f = False
@@ -649,15 +663,22 @@ class ConvGanStep:
         half = 0.5 if self.loss == "mse" else 1.0
         nvd = self.nv if self._short_call else None     # the real call's images (short final batch)
         self._d_forward(self.x3, 2 * B, 2, self.mask_d, nvalid=nvd)
-        with O.launch_batch(self.batch_on):     # the real and fake heads: one launch
-            O.adv_loss(self.v[:B], B, 1, self.loss, 1, half, self.lbuf[0:1], self.dv[:B], nvalid=nvd)
-            O.adv_loss(self.v[B:2 * B], B, 1, self.loss, 0, half, self.lbuf[1:2], self.dv[B:2 * B])
+        if self.head_fuse:
+            self._head(2 * B, [(B, 1, half, self.lbuf[0:1], nvd), (B, 0, half, self.lbuf[1:2], None)], self.hscr_d,
+                       self.flat)
+        else:
+            with O.launch_batch(self.batch_on):     # the real and fake heads: one launch
+                O.adv_loss(self.v[:B], B, 1, self.loss, 1, half, self.lbuf[0:1], self.dv[:B], nvalid=nvd)
+                O.adv_loss(self.v[B:2 * B], B, 1, self.loss, 0, half, self.lbuf[1:2], self.dv[B:2 * B])
         self._d_backward(self.x3, 2 * B, 2, self.mask_d, wgrad=True, dx=None, nvalid=nvd)
         self.D.adam(self.lr, self.betas, self.eps, step_dev=self.dstate[2:3] if self.graph else None)
         self.pk.run("D")
         # G loss through the updated D (its D weight gradient is discarded by the reference: skipped)
         self._d_forward(self.x3[2 * B:], B, 1, self.mask_g)
-        O.adv_loss(self.v[:B], B, 1, self.loss, 1, 1.0, self.lbuf[2:3], self.dv[:B])
+        if self.head_fuse:
+            self._head(B, [(B, 1, 1.0, self.lbuf[2:3], None)], self.hscr_g, None)
+        else:
+            O.adv_loss(self.v[:B], B, 1, self.loss, 1, 1.0, self.lbuf[2:3], self.dv[:B])
         self._d_backward(self.x3[2 * B:], B, 1, self.mask_g, wgrad=False, dx=self.dimg)
 
     def phase_b(self):
@@ -692,6 +713,49 @@ class ConvGanStep:
         self._sync_dstate()
         self._cuda_graph.replay()
         self._apply_host_delta()
+
+    def run_rounds(self, rounds: int):
+        """``rounds`` rounds with N = 1 drawing their own real batches: with graph=True one replay of a graph
+        holding ``rounds`` captured rounds back to back (each round reads its per-round values from the device
+        counter block the previous one advanced, so this is exactly ``rounds`` calls of ``run()`` without the
+        graph-launch boundary between them); otherwise ``rounds`` calls of ``run()``."""
+        if rounds <= 0:
+            return
+        if not self.graph or self.data is None or self.round == 0 or rounds == 1 or self.n_workers != 1:
+            for _ in range(rounds):
+                self.run()
+            return
+        g = self._kgraphs.get(rounds)
+        if g is None:
+            g = self._kgraphs[rounds] = self._capture_rounds(rounds)
+        self._sync_dstate()
+        g.replay()
+        for _ in range(rounds):
+            self._apply_host_delta()
+
+    def prepare_rounds(self, rounds: int):
+        """Capture the ``rounds``-round graph ahead of its first use (graph=True, N = 1, after the first round)."""
+        if self.graph and self.data is not None and self.round > 0 and rounds > 1 and rounds not in self._kgraphs:
+            self._kgraphs[rounds] = self._capture_rounds(rounds)
+
+    def _capture_rounds(self, rounds):
+        if self._graph_delta is None:
+            self._capture()            # (the one-round graph also records the host delta of one round)
+        before = self._host_state()
+        self._sync_dstate()
+        torch.cuda.current_stream().synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            for _ in range(rounds):
+                self.phase_a(None)
+                self.phase_b()
+        # capturing issued nothing: restore the host bookkeeping (run_rounds applies the delta per replayed round)
+        self.round, self.G.step, self.D.step = before[0], before[1], before[2]
+        self.G.batches.update(before[3])
+        self.D.batches.update(before[4])
+        self.lam = before[5]
+        self._dstate_host = (self.round, self.G.step, self.D.step)
+        return g
 
     # ------------------------------------------------------------------ split round (N > 1)
     def round_a(self, real=None, eager=False):

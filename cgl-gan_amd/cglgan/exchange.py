@@ -480,6 +480,14 @@ class ConvWorkerExchange:
     def _d_state(self):
         return [self.step.D.p] + list(self.step.D.running.values())
 
+    def rounds(self, r0: int, n: int):
+        """Rounds r0 .. r0 + n - 1; with no group (N = 1) as multi-round graphs (ConvGanStep.run_rounds)."""
+        if self.comm is None:
+            self.step.run_rounds(n)
+            return
+        for r in range(r0, r0 + n):
+            self.round(r)
+
     def round(self, r: int, real=None, eager=False):
         """One round.  N > 1: phase A, the exchange, phase B -- with a ConvGanStep(graph=True) drawing its
         own real batches, phase A and phase B replay as hipGraphs from the second round on

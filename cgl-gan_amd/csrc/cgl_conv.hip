@@ -2554,11 +2554,25 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize_sliced(CglBnFinSliced a) 
 // 4 (q + 64 b) + j, fma-chained over b then j from 0, lanes combined by the same xor tree, then + bias --
 // so Y is bitwise what nhwc_to_nchw + dense_fwd(N = 1) produced.  `flat` (may be null) receives the
 // NCHW view for adv_layer's weight gradient.
-__global__ __launch_bounds__(256) void cgl_dense1_fwd_nhwc_k(const float* __restrict__ X, const float* __restrict__ W,
-                                                             const float* __restrict__ b, float* __restrict__ Y,
-                                                             float* __restrict__ flat, int n, int C, int hw) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), q = threadIdx.x & 63;
-  if (row >= n) return;                      // wave-uniform
+// One row of a one-logit loss (cgl_adv_loss_at's loss 1 / 2 / 3): its loss term l and weight * d(mean loss)/dz (invM = 1 / M)
+__device__ __forceinline__ void cgl_adv_row1(float z, int loss, int target, float weight, float invM, float& l,
+                                             float& g0) {
+  if (loss == 2) {
+    const float d = z - (float)target;
+    l = d * d;
+    g0 = weight * (2.f * d * invM);
+  } else {
+    const float pr = loss == 3 ? 1.f / (1.f + expf(-z)) : z;
+    const float y = (float)target;
+    const float lp = fmaxf(logf(pr), -100.f), l1p = fmaxf(logf(1.f - pr), -100.f);
+    l = -(y * lp + (1.f - y) * l1p);
+    const float gp = weight * invM * (pr - y) / fmaxf((1.f - pr) * pr, 1e-12f);
+    g0 = loss == 3 ? gp * (1.f - pr) * pr : gp;
+  }
+}
+
+__device__ __forceinline__ float cgl_dense1_row(const float* __restrict__ X, const float* __restrict__ W,
+                                                float* __restrict__ flat, int row, int q, int C, int hw) {
   const int per = C * hw, nb = per >> 8;     // per % 256 == 0, nb <= 4
   const float* __restrict__ x = X + (long)row * per;
   f32x4 v[4], w[4];
@@ -2589,7 +2603,102 @@ __global__ __launch_bounds__(256) void cgl_dense1_fwd_nhwc_k(const float* __rest
     for (int bb = 0; bb < 4; ++bb)
       if (bb < nb) *(gf4p)(flat + (long)row * per + 4 * (q + 64 * bb)) = v[bb];
   }
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void cgl_dense1_fwd_nhwc_k(const float* __restrict__ X, const float* __restrict__ W,
+                                                             const float* __restrict__ b, float* __restrict__ Y,
+                                                             float* __restrict__ flat, int n, int C, int hw) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), q = threadIdx.x & 63;
+  if (row >= n) return;                      // wave-uniform
+  const float acc = cgl_dense1_row(X, W, flat, row, q, C, hw);
   if (q == 0) gst(Y + row, acc + (b ? gld(b) : 0.f));
+}
+
+// The discriminator head of model/lsgan.py as ONE launch: adv_layer's forward from the NHWC map
+// (cgl_dense1_fwd_nhwc's arithmetic; `flat` as there), each row's adversarial-loss term and gradient
+// (cgl_adv_loss_at's arithmetic, cgl_adv_row1) and the row's input gradient into the NHWC map
+// (cgl_dense1_bwd_nhwc_k's products) -- everything of a row depends on that row alone, so the three launches
+// (forward, loss head(s), input gradient) become one.  The calls (the D step's real and fake halves, or the
+// G-loss pass's one call) each keep their own target, weight and batch mean; a short first call (nv) gives its
+// padding rows no loss and a zero gradient.  The batch-mean losses: every wave publishes its row's loss term
+// (agent-scope atomic store), the workgroup takes a monotonic ticket, and the last workgroup to arrive sums
+// the terms in cgl_adv_loss_at's order (thread t: rows t, t + 256, ... in double; then the 256 partials in
+// order), so every output is bitwise what the three separate launches give.
+struct CglHeadCall {
+  int n0, n, target;
+  float weight;
+  float* loss_out;
+  const int* nv;
+};
+struct CglDHeadArgs {
+  const float* X; const float* W; const float* b;
+  float* Y; float* flat; float* dY; float* dX;
+  int n, C, hw, loss, ncalls;
+  CglHeadCall call[2];
+  float* lrow;               // [n] published loss terms
+  unsigned int* ticket;      // monotonic (zeroed once by the caller)
+};
+__global__ __launch_bounds__(256) void cgl_dense1_head_k(CglDHeadArgs a) {
+  __shared__ double s_acc[256];
+  __shared__ int s_last;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), q = threadIdx.x & 63;
+  if (row < a.n) {                           // wave-uniform
+    const float acc = cgl_dense1_row(a.X, a.W, a.flat, row, q, a.C, a.hw);
+    const float z = acc + (a.b ? gld(a.b) : 0.f);
+    const int ci = (a.ncalls > 1 && row >= a.call[1].n0) ? 1 : 0;
+    const int n0 = ci ? a.call[1].n0 : a.call[0].n0, nc = ci ? a.call[1].n : a.call[0].n;
+    const int* nvp = ci ? a.call[1].nv : a.call[0].nv;
+    const int M = nvp ? min(max(gldi(nvp), 1), nc) : nc;
+    const float invM = 1.f / (float)M;
+    float l = 0.f, g = 0.f;
+    if (row - n0 < M)
+      cgl_adv_row1(z, a.loss, ci ? a.call[1].target : a.call[0].target, ci ? a.call[1].weight : a.call[0].weight,
+                   invM, l, g);
+    if (q == 0) {
+      gst(a.Y + row, z);
+      gst(a.dY + row, g);
+      __hip_atomic_store((cgl_gu32*)(a.lrow + row), __float_as_uint(l), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // input gradient, NHWC: dX[row][s][c] = g * W[c * hw + s] (float4 per lane, cgl_dense1_bwd_nhwc_k's products)
+    const int per = a.C * a.hw, nb = per >> 8;
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb)
+      if (bb < nb) {
+        const int e = 4 * (q + 64 * bb);
+        const int sp = e / a.C, c = e - sp * a.C;
+        f32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = g * gld(a.W + (long)(c + j) * a.hw + sp);
+        *(gf4p)(a.dX + (long)row * per + e) = o;
+      }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's published term has landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned int old = __hip_atomic_fetch_add((cgl_gu32*)a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (old % gridDim.x) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  for (int ci = 0; ci < a.ncalls; ++ci) {
+    const int n0 = ci ? a.call[1].n0 : a.call[0].n0, nc = ci ? a.call[1].n : a.call[0].n;
+    const int* nvp = ci ? a.call[1].nv : a.call[0].nv;
+    const int M = nvp ? min(max(gldi(nvp), 1), nc) : nc;
+    double acc = 0.0;
+    for (int r = threadIdx.x; r < M; r += 256)
+      acc += (double)__uint_as_float(
+          __hip_atomic_load((cgl_gu32*)(a.lrow + n0 + r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    s_acc[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (int k = 0; k < 256; ++k) t += s_acc[k];
+      float* lo = ci ? a.call[1].loss_out : a.call[0].loss_out;
+      if (lo) gst(lo, (float)(t / M));
+    }
+    __syncthreads();
+  }
 }
 
 // Weight + bias gradient of a one-output Linear (the discriminator's adv_layer, model/lsgan.py:90-97, on the
@@ -2892,19 +3001,8 @@ __device__ __forceinline__ void cgl_adv_loss_at(const float* x, int Mall, int C,
       const float w = weight * invM;
       g0 = (target == 0 ? -w : 0.f) + expf(o0) * w;
       g1 = (target == 1 ? -w : 0.f) + expf(o1) * w;
-    } else if (loss == 2) {
-      const float z = gld(x + r);
-      const float d = z - (float)target;
-      l = d * d;
-      g0 = weight * (2.f * d * invM);
     } else {
-      const float z = gld(x + r);
-      const float pr = loss == 3 ? 1.f / (1.f + expf(-z)) : z;
-      const float y = (float)target;
-      const float lp = fmaxf(logf(pr), -100.f), l1p = fmaxf(logf(1.f - pr), -100.f);
-      l = -(y * lp + (1.f - y) * l1p);
-      const float gp = weight * invM * (pr - y) / fmaxf((1.f - pr) * pr, 1e-12f);
-      g0 = loss == 3 ? gp * (1.f - pr) * pr : gp;
+      cgl_adv_row1(gld(x + r), loss, target, weight, invM, l, g0);
     }
     acc += (double)l;
     if (grad) {
@@ -4562,6 +4660,28 @@ int cgl_dense1_bwd_data_nhwc(const float* dY, const float* W, float* dX, int n, 
   const long q = (long)n * c * hw / 4;
   const int grid = (int)std::min<long>((q + 255) / 256, 8192);
   hipLaunchKernelGGL(cgl_dense1_bwd_nhwc_k, dim3(grid), dim3(256), 0, (hipStream_t)stream, dY, W, dX, n, c, hw);
+  return (int)hipGetLastError();
+}
+
+int cgl_dense1_head_nhwc(const float* X, const float* W, const float* b, float* Y, float* flat, float* dY, float* dX,
+                         int n, int c, int hw, int loss, int n0, int target0, double weight0, float* loss_out0,
+                         const int* nvalid0, int target1, double weight1, float* loss_out1, float* scratch,
+                         void* stream) {
+  CGL_BATCH_GUARD();
+  const long per = (long)c * hw;
+  if (!X || !W || !Y || !dY || !dX || !scratch || n < 1 || c < 4 || (c & 3) || hw < 1 || per % 256 || per > 1024 ||
+      (long)n * per >= (1L << 31) || !al16(W) || !al16(dX) || (flat && !al16(flat)) || loss < 1 || loss > 3 ||
+      n0 < 1 || n0 > n || (target0 != 0 && target0 != 1) || (n0 < n && target1 != 0 && target1 != 1))
+    return CGL_E_ARG;
+  CglDHeadArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.X = X; a.W = W; a.b = b; a.Y = Y; a.flat = flat; a.dY = dY; a.dX = dX;
+  a.n = n; a.C = c; a.hw = hw; a.loss = loss; a.ncalls = n0 < n ? 2 : 1;
+  a.call[0] = CglHeadCall{0, n0, target0, (float)weight0, loss_out0, nvalid0};
+  a.call[1] = CglHeadCall{n0, n - n0, target1, (float)weight1, loss_out1, nullptr};
+  a.ticket = (unsigned int*)scratch;
+  a.lrow = scratch + 16;
+  hipLaunchKernelGGL(cgl_dense1_head_k, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 

@@ -486,6 +486,18 @@ int cgl_dense1_bwd_data_nhwc(const float* dY, const float* W, float* dX, int n, 
  * NCHW view (model/lsgan.py:96 out.view(B, -1)). b may be null. c * hw % 256 == 0, <= 1024. */
 int cgl_dense1_fwd_nhwc(const float* X, const float* W, const float* b, float* Y, float* flat, int n, int c, int hw,
                         void* stream);
+/* The discriminator head of model/lsgan.py (out.view(B, -1) -> adv_layer, :96-97) with its adversarial loss and
+ * its input gradient in ONE launch: Y = cgl_dense1_fwd_nhwc (flat as there), per call the mean loss and
+ * dY = weight * its gradient as cgl_adv_loss gives them (loss 1 / 2 / 3; one logit), dX = cgl_dense1_bwd_data_nhwc
+ * of dY -- bitwise what the three (or, with two calls, four) separate launches produce.  Call 0 is rows [0, n0)
+ * (target0, weight0, loss_out0, nvalid0: a short first call as cgl_adv_loss), call 1 rows [n0, n) when n0 < n
+ * (the D step's real and fake halves, capgan.py:332-340).  scratch: >= n + 16 floats, zeroed ONCE before the first
+ * use (its first word is a monotonic ticket; the last workgroup reduces the losses).  c % 4 == 0,
+ * c * hw % 256 == 0, <= 1024. */
+int cgl_dense1_head_nhwc(const float* X, const float* W, const float* b, float* Y, float* flat, float* dY, float* dX,
+                         int n, int c, int hw, int loss, int n0, int target0, double weight0, float* loss_out0,
+                         const int* nvalid0, int target1, double weight1, float* loss_out1, float* scratch,
+                         void* stream);
 /* Mean adversarial loss of one forward call and weight * its gradient (grad may be null):
  * loss 0 CrossEntropy on 2 logits (capgan.py:311), 1 BCELoss on probabilities
  * (CGLGAN/2DMG/main.py:336), 2 MSELoss (LSGAN objective of model/lsgan.py's D), 3 Sigmoid + BCELoss

@@ -16,7 +16,9 @@
     backward in its loads (cgl_conv3x3_bwd_weight_actdrop) instead of after an act_drop_bwd pass;
   * CGL_CONV_ELIDE: a folded G BatchNorm's activation (a1 / a2) is not stored at all -- the G backward's weight
     gradients apply the BatchNorm in their operand loads (cgl_conv3x3_bwd_weight_bnin) and every LeakyReLU'
-    comes from the kept scale / shift (with the same fold mask on both sides)."""
+    comes from the kept scale / shift (with the same fold mask on both sides);
+  * CGL_CONV_HEADFUSE: the discriminator head (adv_layer forward, the loss head(s), adv_layer's input gradient) as
+    one launch per pass (cgl_dense1_head_nhwc), its batch-mean losses reduced by the last workgroup."""
 import os
 
 import pytest
@@ -49,7 +51,8 @@ CASES = [("CGL_CONV_POSTCOEF", 8, False, "2"), ("CGL_CONV_POSTCOEF", 256, False,
          ("CGL_CONV_ELIDE", 256, True, "2"), ("CGL_CONV_N1STATS", 8, False, "3"),
          ("CGL_CONV_N1STATS", 256, True, "3"), ("CGL_CONV_N1STATS", 256, False, "0"),
          ("CGL_CONV_BIASFUSE", 8, False, "3"), ("CGL_CONV_BIASFUSE", 256, True, "3"),
-         ("CGL_CONV_C1FUSE", 8, False, "3"), ("CGL_CONV_C1FUSE", 256, True, "3")]
+         ("CGL_CONV_C1FUSE", 8, False, "3"), ("CGL_CONV_C1FUSE", 256, True, "3"),
+         ("CGL_CONV_HEADFUSE", 8, False, "3"), ("CGL_CONV_HEADFUSE", 256, True, "3")]
 
 
 @pytest.mark.parametrize("var,B,graph,fold", CASES)
@@ -76,6 +79,9 @@ def test_conv_round_fusion_bitwise(var, B, graph, fold):
         assert a.bpart is not None and b.bpart is None
     elif var == "CGL_CONV_C1FUSE":
         assert a.c1_fuse and not b.c1_fuse
+    elif var == "CGL_CONV_HEADFUSE":
+        assert a.head_fuse and not b.head_fuse
+        assert torch.equal(a.v, b.v) and torch.equal(a.dv, b.dv) and torch.equal(a.dr[3], b.dr[3])
     elif var == "CGL_CONV_DFOLD_STEP":
         assert a.d_fold_step and not b.d_fold_step and a._d_folded and not b._d_folded
     else:
@@ -89,3 +95,35 @@ def test_conv_round_fusion_bitwise(var, B, graph, fold):
         assert torch.equal(a.D.running[k], b.D.running[k]), k
     assert torch.equal(a.x3, b.x3) and torch.equal(a.lbuf, b.lbuf)
     assert torch.equal(a.dy1, b.dy1) and torch.equal(a.dy2, b.dy2)
+
+
+@pytest.mark.parametrize("loss,B", [("mse", 8), ("bce", 8), ("bce", 256)])
+def test_head_fuse_short_batch(loss, B):
+    """The fused head over a pass with a short final real batch (3 real rows): its nvalid call, both losses."""
+    from cglgan.conv_step import ConvGanStep
+    s = torch.cuda.Stream()
+    outs = []
+    with torch.cuda.stream(s):
+        data = torch.rand(2 * B + 3, 1024, device="cuda", generator=torch.Generator("cuda").manual_seed(4)) * 2 - 1
+        for on in ("1", "0"):
+            old = os.environ.get("CGL_CONV_HEADFUSE")
+            os.environ["CGL_CONV_HEADFUSE"] = on
+            try:
+                st = ConvGanStep(B, loss=loss, seed=31, data=data, graph=True)
+            finally:
+                if old is None:
+                    os.environ.pop("CGL_CONV_HEADFUSE", None)
+                else:
+                    os.environ["CGL_CONV_HEADFUSE"] = old
+            st.init_default(7, 8)
+            lb = []
+            for _ in range(4):            # rounds 0, 1 full, round 2 the short batch (3 rows), round 3 full
+                st.run()
+                lb.append(st.lbuf.clone())
+            torch.cuda.synchronize()
+            outs.append((st, lb))
+    (a, la), (b, lb) = outs
+    assert a.head_fuse and not b.head_fuse and a.short
+    assert all(torch.equal(x, y) for x, y in zip(la, lb))
+    assert torch.equal(a.D.p, b.D.p) and torch.equal(a.G.p, b.G.p) and torch.equal(a.D.g, b.D.g)
+    assert torch.equal(a.v, b.v) and torch.equal(a.dv, b.dv) and torch.equal(a.dr[3], b.dr[3])

@@ -234,3 +234,35 @@ def test_conv_round_graph_replay(B):
     # the sampler drew real rows of the shard: every image of the last real batch is a row of `data`
     x = b.x3[:B].reshape(B, 1024)
     assert all(bool((data == x[i]).all(dim=1).any()) for i in range(B))
+
+
+@pytest.mark.parametrize("B", [8, 256])
+def test_conv_multi_round_graph(B):
+    """ConvGanStep.run_rounds(k): k whole rounds as ONE graph replay equal k single-round replays bitwise (device
+    round state, sampler across a pass boundary, Adam steps, running statistics, host bookkeeping)."""
+    from cglgan.conv_step import ConvGanStep
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        data = torch.rand(3 * B + 5, 1024, device="cuda", generator=torch.Generator("cuda").manual_seed(7)) * 2 - 1
+        a = ConvGanStep(B, seed=23, data=data, graph=True)
+        b = ConvGanStep(B, seed=23, data=data, graph=True)
+        a.init_default(8, 9)
+        b.init_default(8, 9)
+        a.run()
+        b.run()
+        b.prepare_rounds(3)
+        for n in (3, 4, 3):
+            a.run_rounds(n)
+            for _ in range(n):
+                b.run()
+        torch.cuda.synchronize()
+    assert set(a._kgraphs) == {3, 4}
+    assert a.round == b.round == 11 and a.G.step == b.G.step and a.D.step == b.D.step
+    assert torch.equal(a.G.p, b.G.p) and torch.equal(a.D.p, b.D.p)
+    assert torch.equal(a.G.m, b.G.m) and torch.equal(a.D.v, b.D.v)
+    assert torch.equal(a.lbuf, b.lbuf) and torch.equal(a.x3, b.x3) and torch.equal(a.dstate, b.dstate)
+    assert a.G.batches == b.G.batches and a.D.batches == b.D.batches and a.lam == b.lam
+    for k in a.G.running:
+        assert torch.equal(a.G.running[k], b.G.running[k]), k
+    for k in a.D.running:
+        assert torch.equal(a.D.running[k], b.D.running[k]), k
