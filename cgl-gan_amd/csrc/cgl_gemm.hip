@@ -348,8 +348,6 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   const int h_mld = d->mask_ld, h_tld = d->tanh_ld, h_crow0 = d->a_copy_row0;
   float* const h_copy = d->a_copy;
   const CglRowSrc h_a = d->a, h_b = d->b;
-  asm volatile("" ::"s"(M), "s"(N), "s"(K), "s"(WN), "s"(WK), "s"(WM), "s"(h_tm), "s"(h_tn), "s"(h_wg0), "s"(h_ks),
-               "s"(h_xcd), "s"(h_tab), "s"(h_gen), "s"(h_abn), "s"(h_ones), "s"(h_apk), "s"(h_bpk));
   // the epilogue's fields too (they would otherwise cost one more scalar round trip after the k-loop)
   const int e_act = d->act, e_ldc = d->ldc, e_gr = d->stat_gr;
   const float e_slope = d->slope;
@@ -357,6 +355,11 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   float* const e_bout = d->bias_out;
   float* const e_stat = d->stat_part;
   double* const e_bnb = d->bnb_part;
+  // every read above issued before anything uses one of them: ONE batch of scalar loads and one wait (left to
+  // itself the scheduler started the tile arithmetic on the first batch and waited a second time)
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::"s"(M), "s"(N), "s"(K), "s"(WN), "s"(WK), "s"(WM), "s"(h_tm), "s"(h_tn), "s"(h_wg0), "s"(h_ks),
+               "s"(h_xcd), "s"(h_tab), "s"(h_gen), "s"(h_abn), "s"(h_ones), "s"(h_apk), "s"(h_bpk));
   asm volatile("" ::"s"(e_act), "s"(e_ldc), "s"(e_gr), "s"(e_slope), "s"(e_C), "s"(e_bout), "s"(e_stat), "s"(e_bnb));
   asm volatile("" ::"s"(h_bias), "s"(h_mref), "s"(h_tref), "s"(h_mld), "s"(h_tld), "s"(h_crow0), "s"(h_copy),
                "s"(h_a.p0), "s"(h_a.p1), "s"(h_a.idx0), "s"(h_a.idx_off), "s"(h_a.split), "s"(h_a.ld), "s"(h_b.p0),
@@ -1202,7 +1205,10 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 // problem's layout | vec << 2 in 4 bits, and whether d[0] carries a deferred head reduction -- so that a workgroup finds
 // its problem and body without reading the descriptor array first.
 template <int TM, int TN, bool SK = false, int DT = CGL_DTYPE_F32, int ABN = 0>
-__global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDesc* __restrict__ descs, CglGemmSel sel) {
+__global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDesc* __restrict__ descs, int sel_wg1,
+                                                                 int sel_wg2, int sel_meta, int sel_fin) {
+  // (the selection as scalar kernel arguments: with kernarg preloading they arrive in SGPRs at wave start)
+  const CglGemmSel sel{sel_wg1, sel_wg2, sel_meta, sel_fin};
 #ifdef CGL_GEMM_TRACE
   const unsigned long long t_entry = wall_clock64();
 #else

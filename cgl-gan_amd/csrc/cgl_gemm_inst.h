@@ -12,7 +12,7 @@
 #endif
 
 #define CGL_INST_F32(TM, TN, SK, DT, ABN) \
-  CGL_INST_PREFIX __global__ void cgl_gemm_f32<TM, TN, SK, DT, ABN>(const CglGemmDesc* __restrict__, CglGemmSel);
+  CGL_INST_PREFIX __global__ void cgl_gemm_f32<TM, TN, SK, DT, ABN>(const CglGemmDesc* __restrict__, int, int, int, int);
 #define CGL_INST_ARG(TM, TN) \
   CGL_INST_PREFIX __global__ void cgl_gemm_f32_arg<TM, TN>(const CglGemmDesc);
 #define CGL_INST_PRO(TM, TN)                                                                                    \

@@ -319,13 +319,13 @@ template <int DT>
 void launch_gemm16(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, CglGemmSel n, bool sk) {
   if (sk) {
     if (blk == 2)
-      klaunch(cgl_gemm_f32<2, 2, true, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
+      klaunch(cgl_gemm_f32<2, 2, true, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
     else
-      klaunch(cgl_gemm_f32<1, 1, true, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
+      klaunch(cgl_gemm_f32<1, 1, true, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
   } else if (blk == 2) {
-    klaunch(cgl_gemm_f32<2, 2, false, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
+    klaunch(cgl_gemm_f32<2, 2, false, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
   } else {
-    klaunch(cgl_gemm_f32<1, 1, false, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
+    klaunch(cgl_gemm_f32<1, 1, false, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
   }
 }
 
@@ -345,27 +345,27 @@ void launch_gemm(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc*
                  int dt = CGL_DTYPE_F32, int abn = 0) {
   if (abn == 1) {          // fp32, no split-K (planner)
     if (blk == 2)
-      klaunch(cgl_gemm_f32<2, 2, false, CGL_DTYPE_F32, 1>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
+      klaunch(cgl_gemm_f32<2, 2, false, CGL_DTYPE_F32, 1>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
     else
-      klaunch(cgl_gemm_f32<1, 1, false, CGL_DTYPE_F32, 1>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
+      klaunch(cgl_gemm_f32<1, 1, false, CGL_DTYPE_F32, 1>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
   } else if (abn == 2) {
     if (blk == 2)
-      klaunch(cgl_gemm_f32<2, 2, false, CGL_DTYPE_F32, 2>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
+      klaunch(cgl_gemm_f32<2, 2, false, CGL_DTYPE_F32, 2>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
     else
-      klaunch(cgl_gemm_f32<1, 1, false, CGL_DTYPE_F32, 2>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
+      klaunch(cgl_gemm_f32<1, 1, false, CGL_DTYPE_F32, 2>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
   } else if (dt == CGL_DTYPE_F16) {
     launch_gemm16<CGL_DTYPE_F16>(blk, grid, shmem, s, d, n, sk);
   } else if (dt == CGL_DTYPE_BF16) {
     launch_gemm16<CGL_DTYPE_BF16>(blk, grid, shmem, s, d, n, sk);
   } else if (sk) {   // a launch with a split-K problem: the instantiation carrying the combine
     if (blk == 2)
-      klaunch(cgl_gemm_f32<2, 2, true>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
+      klaunch(cgl_gemm_f32<2, 2, true>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
     else
-      klaunch(cgl_gemm_f32<1, 1, true>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
+      klaunch(cgl_gemm_f32<1, 1, true>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
   } else if (blk == 2) {
-    klaunch(cgl_gemm_f32<2, 2>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
+    klaunch(cgl_gemm_f32<2, 2>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
   } else {
-    klaunch(cgl_gemm_f32<1, 1>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n);
+    klaunch(cgl_gemm_f32<1, 1>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
   }
 }
 

@@ -5,7 +5,7 @@
 set -e
 tag=$1; defs=$2
 cd "$(dirname "$0")/../cgl-gan_amd"
-FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-result"
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-result -mllvm -amdgpu-kernarg-preload-count=16"
 mkdir -p build lib_$tag
 /opt/rocm/bin/hipcc $FLAGS $defs -c csrc/cgl_runtime.hip -o build/var_$tag.o &
 for p in 1 2 3 4; do
