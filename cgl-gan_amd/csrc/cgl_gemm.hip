@@ -1206,7 +1206,8 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 // its problem and body without reading the descriptor array first.
 template <int TM, int TN, bool SK = false, int DT = CGL_DTYPE_F32, int ABN = 0>
 __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDesc* __restrict__ descs, int sel_wg1,
-                                                                 int sel_wg2, int sel_meta, int sel_fin) {
+                                                                 int sel_wg2, int sel_meta, int sel_fin,
+                                                                 const int* __restrict__ pf, int pf_lines) {
   // (the selection as scalar kernel arguments: with kernarg preloading they arrive in SGPRs at wave start)
   const CglGemmSel sel{sel_wg1, sel_wg2, sel_meta, sel_fin};
 #ifdef CGL_GEMM_TRACE
@@ -1223,6 +1224,12 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
     cgl_head_finish(descs[0].fin_head, descs[0].fin_head->nwg, cgl_dyn_lds);
     return;
   }
+  // L2 warm-up of the next GEMM launch's descriptors: they are read once per round, through the scalar cache,
+  // at the head of that launch's dependent chain (descriptor -> operand addresses -> operands); after a round's
+  // streaming they have left L2.  Workgroups 0..7 land on XCDs 0..7 (round-robin dispatch), one line per lane;
+  // the value is held to the end of the kernel, so the load is issued here and never waited on early.
+  int pfv = 0;
+  if (bid < 8 && (int)threadIdx.x < pf_lines) pfv = pf[threadIdx.x * 32];
   const int di = bid >= sel.wg2 ? 2 : (bid >= sel.wg1 ? 1 : 0);
   const CglGemmDesc* __restrict__ d = descs + di;
   const int meta = (sel.meta >> (4 * di)) & 15;
@@ -1243,6 +1250,7 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_f32(const CglGemmDe
   else
     CGL_BODY(2);
 #undef CGL_BODY
+  asm volatile("" ::"v"(pfv));
 }
 
 // One problem whose descriptor travels in the kernel arguments (the single-op entry points cgl_linear_*):

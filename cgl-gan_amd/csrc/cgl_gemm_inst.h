@@ -12,11 +12,12 @@
 #endif
 
 #define CGL_INST_F32(TM, TN, SK, DT, ABN) \
-  CGL_INST_PREFIX __global__ void cgl_gemm_f32<TM, TN, SK, DT, ABN>(const CglGemmDesc* __restrict__, int, int, int, int);
+  CGL_INST_PREFIX __global__ void cgl_gemm_f32<TM, TN, SK, DT, ABN>(const CglGemmDesc* __restrict__, int, int, int, int, \
+                                                                     const int* __restrict__, int);
 #define CGL_INST_ARG(TM, TN) \
   CGL_INST_PREFIX __global__ void cgl_gemm_f32_arg<TM, TN>(const CglGemmDesc);
 #define CGL_INST_PRO(TM, TN)                                                                                    \
-  CGL_INST_PREFIX __global__ void cgl_gemm_pro<TM, TN>(const CglGemmDesc* __restrict__, int, CglBeginArgs, float*, \
+  CGL_INST_PREFIX __global__ void cgl_gemm_pro<TM, TN>(const CglGemmDesc* __restrict__, int, const int* __restrict__, int, CglBeginArgs, float*, \
                                                        long, unsigned long long, int*, int, int, int,            \
                                                        unsigned long long, CglOpPack);
 #define CGL_INST_ADAM(TM, TN)                                                                                   \

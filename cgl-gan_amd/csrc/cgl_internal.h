@@ -183,6 +183,10 @@ struct CglGemmSel {
   int wg1, wg2;     // first workgroup of problems 1 and 2 (INT_MAX: absent)
   int meta;         // per problem q: (layout | (a_vec && b_vec) << 2) << 4 q
   int fin;          // problem 0 carries fin_head (the previous head launch's deferred loss reduction)
+  // (host side only) the next GEMM launch's descriptors, from 128-byte line pf, pf_lines lines: warmed into
+  // every XCD's L2 by this launch (cgl_gemm_f32's pf / pf_lines arguments; nullptr / 0: none)
+  const int* pf = nullptr;
+  int pf_lines = 0;
 };
 #define CGL_GEMM_TRACE_WGS 4096   // workgroups per problem with trace slots
 #ifdef CGL_GEMM_TRACE_CHUNKS      // + wave 0's stamp after each of its first 64 chunks (words 8 ..)

@@ -327,7 +327,7 @@ __global__ __launch_bounds__(256) void cgl_round_prologue(CglBeginArgs a, float*
 
 template <int TM, int TN>
 __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_pro(const CglGemmDesc* __restrict__ descs, int gemm_wgs,
-                                                                CglBeginArgs a, float* z, long nz,
+                                                                const int* __restrict__ pf, int pf_lines, CglBeginArgs a, float* z, long nz,
                                                                 unsigned long long zseed, int* idx, int epoch, int br,
                                                                 int n, unsigned long long sseed, CglOpPack pk) {
   extern __shared__ float cgl_dyn_lds[];
@@ -338,10 +338,13 @@ __global__ __launch_bounds__(CGL_GEMM_THREADS) void cgl_gemm_pro(const CglGemmDe
     cgl_round_prologue_at(bid - gemm_wgs, (int)gridDim.x - gemm_wgs, a, z, nz, zseed, 0, idx, epoch, br, n, sseed, pk);
     return;
   }
+  int pfv = 0;     // the next GEMM launch's descriptors into every XCD's L2 (as cgl_gemm_f32)
+  if (bid < 8 && (int)threadIdx.x < pf_lines) pfv = pf[threadIdx.x * 32];
   const CglGemmDesc* __restrict__ d = descs;
   if (d->layout != 0) return;     // planner: an NT problem (A = z rows)
   if (d->a_vec && d->b_vec)
     cgl_gemm_body<0, 1, TM, TN, false, CGL_DTYPE_F32, 0>(d, bid, cgl_dyn_lds, s_flag, s_bnd);
   else
     cgl_gemm_body<0, 0, TM, TN, false, CGL_DTYPE_F32, 0>(d, bid, cgl_dyn_lds, s_flag, s_bnd);
+  asm volatile("" ::"v"(pfv));
 }

@@ -277,6 +277,7 @@ struct Launch {
   bool v4 = false;          // K_ADAM (not adpk): the four-elements-per-thread form (cgl_adam4)
   int layer = -1;           // K_BNAPPLY: the G layer whose forward GEMM reads this launch's output
   int pk = -1;              // K_BNAPPLY: index of the packing jobs it carries (cgl_gan.carry), -1: none
+  int pf_first = -1, pf_count = 0;   // K_GEMM: the next GEMM launch's descriptor range (link_gemm_prefetch)
 };
 
 // Every kernel of a plan is launched through klaunch.  Normally a plain launch; while cgl_gan_profile
@@ -319,13 +320,13 @@ template <int DT>
 void launch_gemm16(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc* d, CglGemmSel n, bool sk) {
   if (sk) {
     if (blk == 2)
-      klaunch(cgl_gemm_f32<2, 2, true, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
+      klaunch(cgl_gemm_f32<2, 2, true, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin, n.pf, n.pf_lines);
     else
-      klaunch(cgl_gemm_f32<1, 1, true, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
+      klaunch(cgl_gemm_f32<1, 1, true, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin, n.pf, n.pf_lines);
   } else if (blk == 2) {
-    klaunch(cgl_gemm_f32<2, 2, false, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
+    klaunch(cgl_gemm_f32<2, 2, false, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin, n.pf, n.pf_lines);
   } else {
-    klaunch(cgl_gemm_f32<1, 1, false, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
+    klaunch(cgl_gemm_f32<1, 1, false, DT>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin, n.pf, n.pf_lines);
   }
 }
 
@@ -345,27 +346,27 @@ void launch_gemm(int blk, int grid, int shmem, hipStream_t s, const CglGemmDesc*
                  int dt = CGL_DTYPE_F32, int abn = 0) {
   if (abn == 1) {          // fp32, no split-K (planner)
     if (blk == 2)
-      klaunch(cgl_gemm_f32<2, 2, false, CGL_DTYPE_F32, 1>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
+      klaunch(cgl_gemm_f32<2, 2, false, CGL_DTYPE_F32, 1>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin, n.pf, n.pf_lines);
     else
-      klaunch(cgl_gemm_f32<1, 1, false, CGL_DTYPE_F32, 1>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
+      klaunch(cgl_gemm_f32<1, 1, false, CGL_DTYPE_F32, 1>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin, n.pf, n.pf_lines);
   } else if (abn == 2) {
     if (blk == 2)
-      klaunch(cgl_gemm_f32<2, 2, false, CGL_DTYPE_F32, 2>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
+      klaunch(cgl_gemm_f32<2, 2, false, CGL_DTYPE_F32, 2>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin, n.pf, n.pf_lines);
     else
-      klaunch(cgl_gemm_f32<1, 1, false, CGL_DTYPE_F32, 2>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
+      klaunch(cgl_gemm_f32<1, 1, false, CGL_DTYPE_F32, 2>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin, n.pf, n.pf_lines);
   } else if (dt == CGL_DTYPE_F16) {
     launch_gemm16<CGL_DTYPE_F16>(blk, grid, shmem, s, d, n, sk);
   } else if (dt == CGL_DTYPE_BF16) {
     launch_gemm16<CGL_DTYPE_BF16>(blk, grid, shmem, s, d, n, sk);
   } else if (sk) {   // a launch with a split-K problem: the instantiation carrying the combine
     if (blk == 2)
-      klaunch(cgl_gemm_f32<2, 2, true>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
+      klaunch(cgl_gemm_f32<2, 2, true>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin, n.pf, n.pf_lines);
     else
-      klaunch(cgl_gemm_f32<1, 1, true>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
+      klaunch(cgl_gemm_f32<1, 1, true>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin, n.pf, n.pf_lines);
   } else if (blk == 2) {
-    klaunch(cgl_gemm_f32<2, 2>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
+    klaunch(cgl_gemm_f32<2, 2>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin, n.pf, n.pf_lines);
   } else {
-    klaunch(cgl_gemm_f32<1, 1>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin);
+    klaunch(cgl_gemm_f32<1, 1>, dim3(grid), dim3(CGL_GEMM_THREADS), shmem, s, d, n.wg1, n.wg2, n.meta, n.fin, n.pf, n.pf_lines);
   }
 }
 
@@ -1183,6 +1184,26 @@ CglGemmDesc d_input_grad(cgl_gan* c, int j, int rows_, const float* dY) {
   return n;
 }
 
+// Each plain GEMM launch (and the prologue-fused one) warms the descriptors of the next GEMM-kind launch in execution order (phase A, phase
+// B's head, phase B, then round to the next round's first) into L2 (cgl_gemm_f32's pf argument).  Env
+// CGL_GEMM_PF=0 disables it (A/B runs).
+void link_gemm_prefetch(cgl_gan* c) {
+  const char* e = getenv("CGL_GEMM_PF");
+  if (e && atoi(e) == 0) return;
+  std::vector<Launch*> order;
+  for (std::vector<Launch>* ph : {&c->phA, &c->phBhead, &c->phB})
+    for (auto& L : *ph)
+      if (L.kind == K_GEMM || L.kind == K_GEMM_PRO || L.kind == K_GEMM_ADAM) order.push_back(&L);
+  const int n = (int)order.size();
+  for (int i = 0; i < n; ++i) {
+    Launch& L = *order[i];
+    if ((L.kind != K_GEMM && L.kind != K_GEMM_PRO) || n < 2) continue;
+    const Launch& nx = *order[(i + 1) % n];
+    L.pf_first = nx.first;
+    L.pf_count = nx.kind == K_GEMM_PRO ? 1 : nx.count;
+  }
+}
+
 int build_plan(cgl_gan* c) {
   const cgl_gan_config& cf = c->cfg;
   const cgl_mlp_spec &g = cf.g, &d = cf.d;
@@ -1787,12 +1808,25 @@ int build_plan(cgl_gan* c) {
     }
   }
   fuse_prologue(c);
+  link_gemm_prefetch(c);
   if ((int)c->gemm.size() > kMaxGemmDescs || (int)c->head.size() > kMaxHeadDescs ||
       (int)c->bnb.size() > kMaxBnDescs || (int)c->bna.size() > kMaxBnDescs)
     return CGL_E_SIZE;
   return CGL_OK;
 }
 
+
+// The prefetch range of a GEMM launch (link_gemm_prefetch) as whole 128-byte lines
+CglGemmSel gemm_prefetch(const cgl_gan* c, const Launch& L) {
+  CglGemmSel q{};
+  if (L.pf_first >= 0) {
+    const uintptr_t b = (uintptr_t)(c->ws.gemm + L.pf_first) & ~uintptr_t(127);
+    const uintptr_t e = (uintptr_t)(c->ws.gemm + L.pf_first + L.pf_count);
+    q.pf = (const int*)b;
+    q.pf_lines = std::min(64, (int)((e - b + 127) / 128));
+  }
+  return q;
+}
 
 int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = true) {
   hipStream_t s = s_main;
@@ -1806,9 +1840,14 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
   switch (L.kind) {
     case K_GEMM:
       if (L.count > 3) return CGL_E_SIZE;
-      launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, gemm_sel(c->gemm.data() + L.first, L.count), L.sk,
-                  L.dt, L.abn);
+    {
+      CglGemmSel q = gemm_sel(c->gemm.data() + L.first, L.count);
+      const CglGemmSel pq = gemm_prefetch(c, L);
+      q.pf = pq.pf;
+      q.pf_lines = pq.pf_lines;
+      launch_gemm(L.blk, L.grid, L.shmem, s, c->ws.gemm + L.first, q, L.sk, L.dt, L.abn);
       break;
+    }
     case K_HEAD:
       if (L.pk >= 0)
         klaunch(cgl_head_loss_pk, dim3(L.grid + c->carry[L.pk].blocks), dim3(256), 0, s, c->head[L.first], L.grid,
@@ -1846,18 +1885,20 @@ int exec_launch(cgl_gan* c, const Launch& L, hipStream_t s_main, bool events = t
       else
         klaunch(cgl_adam, dim3(L.grid), dim3(256), 0, s, L.adam, c->ws.st, L.tail);
       break;
-    case K_GEMM_PRO:       // grid_y = the GEMM's workgroups (fuse_prologue)
+    case K_GEMM_PRO: {     // grid_y = the GEMM's workgroups (fuse_prologue)
+      const CglGemmSel pq = gemm_prefetch(c, L);
       if (L.blk == 2)
-        klaunch(cgl_gemm_pro<2, 2>, dim3(L.grid), dim3(CGL_GEMM_THREADS), L.shmem, s, c->ws.gemm + L.first, L.grid_y, L.begin, L.nptr,
+        klaunch(cgl_gemm_pro<2, 2>, dim3(L.grid), dim3(CGL_GEMM_THREADS), L.shmem, s, c->ws.gemm + L.first, L.grid_y, pq.pf, pq.pf_lines, L.begin, L.nptr,
                                                                       L.nn, c->cfg.seed, c->ws.idx, c->cfg.epoch,
                                                                       c->cfg.batch_real, c->cfg.sample_n,
                                                                       c->cfg.seed ^ 0x5bd1e995ULL, c->pack);
       else
-        klaunch(cgl_gemm_pro<1, 1>, dim3(L.grid), dim3(CGL_GEMM_THREADS), L.shmem, s, c->ws.gemm + L.first, L.grid_y, L.begin, L.nptr,
+        klaunch(cgl_gemm_pro<1, 1>, dim3(L.grid), dim3(CGL_GEMM_THREADS), L.shmem, s, c->ws.gemm + L.first, L.grid_y, pq.pf, pq.pf_lines, L.begin, L.nptr,
                                                                       L.nn, c->cfg.seed, c->ws.idx, c->cfg.epoch,
                                                                       c->cfg.batch_real, c->cfg.sample_n,
                                                                       c->cfg.seed ^ 0x5bd1e995ULL, c->pack);
       break;
+    }
     case K_GEMM_ADAM:      // grid_y = the GEMM's workgroups (fuse_wgrad_adam)
       if (L.blk == 2)
         klaunch(cgl_gemm_adam<2, 2>, dim3(L.grid), dim3(CGL_GEMM_THREADS), L.shmem, s, c->ws.gemm + L.first, L.count, L.grid_y, L.adam,
