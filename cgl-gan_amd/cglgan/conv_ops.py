@@ -53,6 +53,31 @@ def launch_batch(enabled=True):
             C.check(rc, "cgl_conv_batch_end")
 
 
+_WDEFER = False     # a wgrad_defer block is open (its weight gradients need workspaces of their own)
+
+
+@contextlib.contextmanager
+def wgrad_defer(enabled=True):
+    """cgl_conv_wgrad_defer_begin / _end around a backward pass: the weight gradients' split reductions (and the
+    single-input-channel kernel's finish) run as ONE launch at the end of the block, on the current stream
+    (bitwise the separate launches).  Every conv3x3_bwd_weight inside must get its own ``ws``."""
+    global _WDEFER
+    if not enabled:
+        yield
+        return
+    C.check(C.lib.cgl_conv_wgrad_defer_begin(), "cgl_conv_wgrad_defer_begin")
+    _WDEFER = True
+    ok = False
+    try:
+        yield
+        ok = True
+    finally:
+        _WDEFER = False
+        rc = C.lib.cgl_conv_wgrad_defer_end(_s())
+        if ok:
+            C.check(rc, "cgl_conv_wgrad_defer_end")
+
+
 @contextlib.contextmanager
 def stream_cache():
     """Resolve the current torch stream once for a block of ops that all run on it (the fused conv
@@ -191,14 +216,21 @@ def conv3x3_bwd_data(dy, w, dx, n, h, wd, cin, cout, stride=1, up=0, wp=None, st
     return dx
 
 
-def conv3x3_bwd_weight(dy, x, dw, db, n, h, wd, cin, cout, stride=1, up=0, bn_in=None, act_drop=None):
+def conv3x3_bwd_weight(dy, x, dw, db, n, h, wd, cin, cout, stride=1, up=0, bn_in=None, act_drop=None, ws=None):
     """``bn_in`` = (coef, group, groups, act, slope): ``x`` is the PRE-BatchNorm map of forward call ``group``
     (-1: ``groups`` stacked calls of n / groups images); the BatchNorm (+ LeakyReLU) is applied in the operand
     loads (cgl_conv3x3_bwd_weight_bnin).  ``act_drop`` = (post, drop, slope), cin == 1 only: ``dy`` is the
     gradient at the block's output, the LeakyReLU + Dropout2d backward applied per loaded value
-    (cgl_conv3x3_bwd_weight_actdrop, bitwise act_drop_bwd + this)."""
+    (cgl_conv3x3_bwd_weight_actdrop, bitwise act_drop_bwd + this).  ``ws``: a uint8 workspace of its own
+    (inside wgrad_defer: the deferred reduction reads its partials from it), else the stream's shared one."""
     _chk(dy, x, dw, db)
-    ws = workspace(conv_ws_bytes(n, h, wd, cin, cout, stride, up), dy.device)
+    need = conv_ws_bytes(n, h, wd, cin, cout, stride, up)
+    if ws is None:
+        if _WDEFER:
+            raise RuntimeError("conv3x3_bwd_weight inside wgrad_defer: pass a workspace of its own (ws=)")
+        ws = workspace(need, dy.device)
+    elif ws.numel() < need or ws.dtype != torch.uint8:
+        raise RuntimeError(f"conv3x3_bwd_weight: workspace of {need} bytes (uint8) needed")
     if act_drop is not None:
         post, drop, slope = act_drop
         _chk(post, drop)

@@ -287,6 +287,17 @@ class ConvGanStep:
         # own scratch: a monotonic ticket counted modulo that launch's grid + the per-row loss terms
         self.head_fuse = os.environ.get("CGL_CONV_HEADFUSE", "1") != "0"
         self.hscr_d, self.hscr_g = torch.zeros(B2 + 16, device=dev), torch.zeros(B + 16, device=dev)
+        # the split reductions of a backward pass's weight gradients (and Conv2d(1, 16)'s finish) as ONE launch at the
+        # end of the pass (cgl_conv_wgrad_defer; bitwise the separate launches; CGL_CONV_WDEFER=0 launches each with
+        # its MFMA kernel): every deferred weight gradient writes its partials into a workspace of its own
+        self.wdefer = os.environ.get("CGL_CONV_WDEFER", "1") != "0"
+        self.wws = {}
+        if self.wdefer:
+            geoms = {ck: (B2, hw, hw, ci, co, 2, 0) for ck, _, ci, co, hw in D_CONVS}
+            geoms.update({"conv_blocks.8": (B, 32, 32, 64, 1, 1, 0), "conv_blocks.5": (B, 16, 16, 128, 64, 1, 1),
+                          "conv_blocks.1": (B, 8, 8, 128, 128, 1, 1)})
+            for k, geo in geoms.items():
+                self.wws[k] = torch.empty(O.conv_ws_bytes(*geo), dtype=torch.uint8, device=dev)
         self.bpart = (torch.zeros(2 * (B * 1024 // 256), dtype=torch.float64, device=dev)
                       if os.environ.get("CGL_CONV_BIASFUSE", "1") != "0" and B * 1024 % 256 == 0 and B <= 2048 else None)
         # sampler over a device-resident real shard [n, 1024] (DataLoader(shuffle=True), capgan.py:282)
@@ -513,7 +524,12 @@ class ConvGanStep:
                            4, self.loss, calls, scratch, flat=flat)
 
     def _d_backward(self, x, n, groups, masks, wgrad, dx, nvalid=None):
+        with O.wgrad_defer(wgrad and self.wdefer):
+            self._d_backward_ops(x, n, groups, masks, wgrad, dx, nvalid)
+
+    def _d_backward_ops(self, x, n, groups, masks, wgrad, dx, nvalid=None):
         P, G = self.D.params, self.D.grads
+        wws = self.wws if wgrad else {}
         bst = set()     # BatchNorms whose backward partials the previous input-gradient conv wrote
         if not self.head_fuse:      # (fused: the head launch wrote dr[3])
             O.dense1_bwd_data_nhwc(self.dv, P["adv_layer.weight"], self.dr[3], n, 128, 4)
@@ -538,12 +554,14 @@ class ConvGanStep:
             pfold = k > 1 and D_CONVS[k - 1][1] in self._d_folded
             if k == 0 and not bk and c1f:   # dc[0] only feeds this weight gradient: its act / drop backward in the loads
                 O.conv3x3_bwd_weight(self.dq1, inp, G[ck + ".weight"], G[ck + ".bias"], n, hw, hw, ci, co, 2, 0,
-                                     act_drop=(self.q[0], masks[0], SLOPE))
+                                     act_drop=(self.q[0], masks[0], SLOPE), ws=wws.get(ck))
             elif wgrad and pfold:     # r[k - 1] = BN(q[k - 1]) applied in the operand loads (both calls of the step)
                 O.conv3x3_bwd_weight(self.dc[k], self.q[k - 1], G[ck + ".weight"], G[ck + ".bias"], n, hw, hw, ci, co,
-                                     2, 0, bn_in=(self.dcoef[D_CONVS[k - 1][1]], -1, groups, O.ACT_NONE, SLOPE))
+                                     2, 0, bn_in=(self.dcoef[D_CONVS[k - 1][1]], -1, groups, O.ACT_NONE, SLOPE),
+                                     ws=wws.get(ck))
             elif wgrad:
-                O.conv3x3_bwd_weight(self.dc[k], inp, G[ck + ".weight"], G[ck + ".bias"], n, hw, hw, ci, co, 2, 0)
+                O.conv3x3_bwd_weight(self.dc[k], inp, G[ck + ".weight"], G[ck + ".bias"], n, hw, hw, ci, co, 2, 0,
+                                     ws=wws.get(ck))
             if k > 0:
                 pbk = D_CONVS[k - 1][1]
                 st = None
@@ -556,7 +574,12 @@ class ConvGanStep:
                 O.conv3x3_bwd_data(self.dc[0], P[ck + ".weight"], dx, n, hw, hw, ci, co, 2, 0, wp=self.pk[ck + "b"])
 
     def _g_backward(self):
+        with O.wgrad_defer(self.wdefer):
+            self._g_backward_ops()
+
+    def _g_backward_ops(self):
         P, G, B = self.G.params, self.G.grads, self.B
+        wws = self.wws
         # the Tanh backward also writes conv_blocks.8's bias-gradient partials (CGL_CONV_BIASFUSE; bitwise the
         # weight gradient's column sum over dc3g, one channel-reduction launch fewer)
         bf = self.bpart is not None
@@ -566,10 +589,11 @@ class ConvGanStep:
         e6, e2 = self._elided("conv_blocks.6"), self._elided("conv_blocks.2")
         if e6:     # a2 = LeakyReLU(BN(y2)) applied in the operand loads
             O.conv3x3_bwd_weight(self.dc3g, self.y2[B:], G["conv_blocks.8.weight"], db8, B, 32, 32,
-                                 64, 1, 1, 0, bn_in=(self.coef["conv_blocks.6"], 1, 2, O.ACT_LEAKY, SLOPE))
+                                 64, 1, 1, 0, bn_in=(self.coef["conv_blocks.6"], 1, 2, O.ACT_LEAKY, SLOPE),
+                                 ws=wws.get("conv_blocks.8"))
         else:
             O.conv3x3_bwd_weight(self.dc3g, self.a2[B:], G["conv_blocks.8.weight"], db8, B, 32, 32,
-                                 64, 1, 1, 0)
+                                 64, 1, 1, 0, ws=wws.get("conv_blocks.8"))
         if bf:
             O.colsum_finalize(self.bpart, B * 1024 // 256, 1, G["conv_blocks.8.bias"])
         sm, si = self.g_save["conv_blocks.6"]
@@ -587,10 +611,11 @@ class ConvGanStep:
             O.bn2d_bwd(self.da2, self.y2[B:], B, 1024, 64, sm[1], si[1], P["conv_blocks.6.weight"], self.dy2, **kw)
         if e2:
             O.conv3x3_bwd_weight(self.dy2, self.y1[B:], G["conv_blocks.5.weight"], G["conv_blocks.5.bias"], B, 16, 16,
-                                 128, 64, 1, 1, bn_in=(self.coef["conv_blocks.2"], 1, 2, O.ACT_LEAKY, SLOPE))
+                                 128, 64, 1, 1, bn_in=(self.coef["conv_blocks.2"], 1, 2, O.ACT_LEAKY, SLOPE),
+                                 ws=wws.get("conv_blocks.5"))
         else:
             O.conv3x3_bwd_weight(self.dy2, self.a1[B:], G["conv_blocks.5.weight"], G["conv_blocks.5.bias"], B, 16, 16,
-                                 128, 64, 1, 1)
+                                 128, 64, 1, 1, ws=wws.get("conv_blocks.5"))
         sm, si = self.g_save["conv_blocks.2"]
         st = None
         if self.bst_ok.get("conv_blocks.2"):
@@ -607,7 +632,7 @@ class ConvGanStep:
         else:
             O.bn2d_bwd(self.da1, self.y1[B:], B, 256, 128, sm[1], si[1], P["conv_blocks.2.weight"], self.dy1, **kw)
         O.conv3x3_bwd_weight(self.dy1, self.h0[B:], G["conv_blocks.1.weight"], G["conv_blocks.1.bias"], B, 8, 8, 128,
-                             128, 1, 1)
+                             128, 1, 1, ws=wws.get("conv_blocks.1"))
         O.conv3x3_bwd_data(self.dy1, P["conv_blocks.1.weight"], self.dh0, B, 8, 8, 128, 128, 1, 1, wp=self.pk["c1b"])
         O.nhwc_to_nchw(self.dh0, self.dh, B, 128, 64)
         self.l1_wgrad()

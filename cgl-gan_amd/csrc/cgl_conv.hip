@@ -1818,9 +1818,9 @@ __device__ __forceinline__ double cgl_block_sum_d(double x, double* red);
 
 // one workgroup per (tap, channel) output: blocks b = thread, thread + 256, ... summed in order,
 // then the fixed-order block sum
-__global__ __launch_bounds__(256) void cgl_conv_c1_wgrad_fin(CglC1Args a) {
-  __shared__ double red[4];
-  const int o = blockIdx.x, cout = a.cout, tid = threadIdx.x;
+template <class CA>
+__device__ __forceinline__ void cgl_conv_c1_wgrad_fin_at(const CA& a, int o, double* red) {
+  const int cout = a.cout, tid = threadIdx.x;
   double v = 0.0;
   for (int b = tid; b < a.nblk; b += 256) v += (double)gld(a.part + (long)b * cout * 10 + o);
   v = cgl_block_sum_d(v, red);
@@ -1829,6 +1829,11 @@ __global__ __launch_bounds__(256) void cgl_conv_c1_wgrad_fin(CglC1Args a) {
     if (t < 9) gst(a.dW + c * 9 + t, (float)v);
     else if (a.db) gst(a.db + c, (float)v);
   }
+}
+
+__global__ __launch_bounds__(256) void cgl_conv_c1_wgrad_fin(CglC1Args a) {
+  __shared__ double red[4];
+  cgl_conv_c1_wgrad_fin_at(a, (int)blockIdx.x, red);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1934,16 +1939,18 @@ struct CglWgradReduceArgs {
   int ym[CGL_CONV_MAXP][4], xm[CGL_CONV_MAXP][4];
 };
 
-__global__ __launch_bounds__(256) void cgl_conv_wgrad_reduce(CglWgradReduceArgs a) {
-  __shared__ double red[256];
+// block bid of a weight gradient's fixed-order split reduction (cgl_conv_wgrad_reduce, cgl_conv_wgrad_reduce_multi);
+// RA: the by-value argument or its copy inside the multi-launch's kernarg block; red: 256 doubles of LDS
+template <class RA>
+__device__ __forceinline__ void cgl_conv_wgrad_reduce_at(const RA& a, int bid, double* red) {
   const int EB = a.EB, SG = a.SG;
   const int el = threadIdx.x % EB, sg = threadIdx.x / EB;
-  const int e = blockIdx.x * EB + el;
+  const int e = bid * EB + el;
   const int cin = a.cin, ks = a.ks;
   const int E = a.cout * ks * ks * cin;
-  if (a.db && (int)blockIdx.x >= a.wblocks) {   // uniform per block
+  if (a.db && bid >= a.wblocks) {   // uniform per block
     // bias gradient: db[co] = sum over problems and splits of part[s][co][K]
-    const int eb = ((int)blockIdx.x - a.wblocks) * EB + el;
+    const int eb = (bid - a.wblocks) * EB + el;
     const int co = min(eb, a.cout - 1);
     double acc = 0.0;
     for (int p = 0; p < a.np; ++p) {
@@ -1999,6 +2006,37 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad_reduce(CglWgradReduceArgs 
     for (int g = 0; g < SG; ++g) t += red[g * EB + el];
     gst(a.dW + ((long)co * cin + ci) * ks * ks + kh * ks + kw, (float)t);
   }
+}
+
+__global__ __launch_bounds__(256) void cgl_conv_wgrad_reduce(CglWgradReduceArgs a) {
+  __shared__ double red[256];
+  cgl_conv_wgrad_reduce_at(a, (int)blockIdx.x, red);
+}
+
+// The deferred split reductions of several weight gradients (cgl_conv_wgrad_defer_begin / _end) and the
+// single-input-channel kernel's finish (cgl_conv_c1_wgrad_fin) as ONE launch: block ranges [begin[q],
+// begin[q + 1]) run reduction q, blocks from begin[n] the c1 finish.  Each block computes exactly what it
+// computes in its own launch (same function, same block index), so the gradients are bitwise unchanged.
+#define CGL_WDEFER_MAX 4
+struct CglWgradReduceMulti {
+  int n, c1_blocks;
+  int begin[CGL_WDEFER_MAX + 1];
+  CglWgradReduceArgs r[CGL_WDEFER_MAX];
+  CglC1Args c1;
+};
+
+__global__ __launch_bounds__(256) void cgl_conv_wgrad_reduce_multi(CglWgradReduceMulti) {
+  typedef const CGL_AS4 CglWgradReduceMulti* KA;
+  const KA A = (KA)__builtin_amdgcn_kernarg_segment_ptr();
+  __shared__ double red[256];
+  const int b = blockIdx.x, n = A->n;
+  if (b >= A->begin[n]) {
+    cgl_conv_c1_wgrad_fin_at(A->c1, b - A->begin[n], red);
+    return;
+  }
+  int q = 0;
+  while (q + 1 < n && b >= A->begin[q + 1]) ++q;
+  cgl_conv_wgrad_reduce_at(A->r[q], b - A->begin[q], red);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3831,6 +3869,16 @@ int wgrad_lds_wm(const WgradPlan& pl, bool bias_col, const float* dY, const floa
 
 // bi (may be null): X is the PRE-BatchNorm map of one forward call, applied in the operand loads -- only the
 // LDS-staged MFMA weight gradient and the input-stationary one-output-channel one take it (CGL_E_ARG otherwise)
+// Deferred weight-gradient reductions (cgl_conv_wgrad_defer_begin / _end): while open on the calling thread, a
+// weight gradient launches its MFMA kernel and records its split reduction (or the c1 kernel's finish) here;
+// _end launches every recorded one as one cgl_conv_wgrad_reduce_multi.
+struct WgradDefer {
+  bool on = false;
+  CglWgradReduceMulti m{};
+  bool has_c1 = false;
+};
+thread_local WgradDefer t_wdefer;
+
 int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, float* dW, float* db, void* ws,
                          int64_t wsb, hipStream_t s, const BnIn* bi = nullptr, const float* ad_post = nullptr,
                          const float* ad_drop = nullptr, float ad_slope = 0.f) {
@@ -3851,6 +3899,12 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
     if ((int64_t)a.nblk * g.cout * 10 * 4 > wsb) return CGL_E_SIZE;
     a.part = (float*)ws;
     hipLaunchKernelGGL(cgl_conv_c1_wgrad, dim3(a.nblk), dim3(256), 0, s, a);
+    if (t_wdefer.on && !t_wdefer.has_c1) {   // the finish rides in the deferred reductions' launch
+      t_wdefer.m.c1 = a;
+      t_wdefer.m.c1_blocks = g.cout * 10;
+      t_wdefer.has_c1 = true;
+      return (int)hipGetLastError();
+    }
     hipLaunchKernelGGL(cgl_conv_c1_wgrad_fin, dim3(g.cout * 10), dim3(256), 0, s, a);
     return (int)hipGetLastError();
   }
@@ -3989,6 +4043,13 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
   r.wblocks = (int)((nred + EB - 1) / EB);
   r.db = bias_col ? db : nullptr;
   const int bblocks = bias_col ? (g.cout + EB - 1) / EB : 0;
+  if (t_wdefer.on && (!db || bias_col) && t_wdefer.m.n < CGL_WDEFER_MAX) {
+    CglWgradReduceMulti& m = t_wdefer.m;
+    m.r[m.n] = r;
+    m.begin[m.n + 1] = m.begin[m.n] + r.wblocks + bblocks;
+    ++m.n;
+    return 0;
+  }
   hipLaunchKernelGGL(cgl_conv_wgrad_reduce, dim3((unsigned)(r.wblocks + bblocks)), dim3(256), 0, s, r);
   if ((rc = (int)hipGetLastError())) return rc;
   if (db && !bias_col) {
@@ -4119,6 +4180,24 @@ int64_t cgl_conv_packed_floats(int h, int w, int cin, int cout, int stride, int 
   CglConvProb P[CGL_CONV_MAXP];
   const int np = dir ? bwd_probs(g, P) : fwd_probs(g, P);
   return pack_layout(P, np, nullptr);
+}
+
+int cgl_conv_wgrad_defer_begin(void) {
+  if (t_wdefer.on) return CGL_E_STATE;
+  t_wdefer = WgradDefer{};
+  t_wdefer.on = true;
+  return CGL_OK;
+}
+
+int cgl_conv_wgrad_defer_end(void* stream) {
+  if (!t_wdefer.on) return CGL_E_STATE;
+  t_wdefer.on = false;
+  CglWgradReduceMulti& m = t_wdefer.m;
+  const int blocks = m.begin[m.n] + (t_wdefer.has_c1 ? m.c1_blocks : 0);
+  if (blocks == 0) return CGL_OK;
+  if (!t_wdefer.has_c1) m.c1_blocks = 0;
+  hipLaunchKernelGGL(cgl_conv_wgrad_reduce_multi, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, m);
+  return (int)hipGetLastError();
 }
 
 // Launch batching (cgl_conv_batch_begin / _end): between the two calls, cgl_conv_pack_multi,

@@ -347,6 +347,16 @@ int cgl_conv_pack_multi(int njobs, const CglConvPackJob* jobs, void* stream);
  * returns CGL_E_STATE without launching, so nothing can run ahead of the deferred calls. */
 int cgl_conv_batch_begin(void* stream);
 int cgl_conv_batch_end(void* stream);
+/* Deferred weight-gradient reductions (the conv round's D and G backward): between cgl_conv_wgrad_defer_begin()
+ * and cgl_conv_wgrad_defer_end(stream), cgl_conv3x3_bwd_weight(_bnin / _actdrop) on the calling thread launch
+ * their MFMA kernel and record their fixed-order split reduction (up to 4; and one single-input-channel finish)
+ * instead of launching it; _end launches every recorded one as ONE kernel on that stream.  Bitwise the separate
+ * launches.  The recorded reductions read their partials from the workspace each call was given, so every
+ * deferred call needs its OWN workspace, untouched until _end; dW / db are written at _end.  A call the batch
+ * cannot take (a fifth reduction, a bias gradient by column sums) launches its reduction at once, as outside a
+ * batch.  Other entry points are unaffected.  Returns CGL_E_STATE for a nested begin or an end without begin. */
+int cgl_conv_wgrad_defer_begin(void);
+int cgl_conv_wgrad_defer_end(void* stream);
 int cgl_conv3x3_fwd_packed(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w, int cin,
                            int cout, int stride, int up, int act, float slope, const float* drop, void* workspace,
                            int64_t ws_bytes, void* stream);
