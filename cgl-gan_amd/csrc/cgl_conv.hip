@@ -2013,31 +2013,6 @@ __global__ __launch_bounds__(256) void cgl_conv_wgrad_reduce(CglWgradReduceArgs 
   cgl_conv_wgrad_reduce_at(a, (int)blockIdx.x, red);
 }
 
-// The deferred split reductions of several weight gradients (cgl_conv_wgrad_defer_begin / _end) and the
-// single-input-channel kernel's finish (cgl_conv_c1_wgrad_fin) as ONE launch: block ranges [begin[q],
-// begin[q + 1]) run reduction q, blocks from begin[n] the c1 finish.  Each block computes exactly what it
-// computes in its own launch (same function, same block index), so the gradients are bitwise unchanged.
-#define CGL_WDEFER_MAX 4
-struct CglWgradReduceMulti {
-  int n, c1_blocks;
-  int begin[CGL_WDEFER_MAX + 1];
-  CglWgradReduceArgs r[CGL_WDEFER_MAX];
-  CglC1Args c1;
-};
-
-__global__ __launch_bounds__(256) void cgl_conv_wgrad_reduce_multi(CglWgradReduceMulti) {
-  typedef const CGL_AS4 CglWgradReduceMulti* KA;
-  const KA A = (KA)__builtin_amdgcn_kernarg_segment_ptr();
-  __shared__ double red[256];
-  const int b = blockIdx.x, n = A->n;
-  if (b >= A->begin[n]) {
-    cgl_conv_c1_wgrad_fin_at(A->c1, b - A->begin[n], red);
-    return;
-  }
-  int q = 0;
-  while (q + 1 < n && b >= A->begin[q + 1]) ++q;
-  cgl_conv_wgrad_reduce_at(A->r[q], b - A->begin[q], red);
-}
 
 // ------------------------------------------------------------------------------------------
 // Per-channel reductions over an NHWC tensor [rows][C] (C a power of two <= 256), one chunk of R
@@ -2388,10 +2363,11 @@ struct CglFinCache {
   }
 };
 
-__global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
-  __shared__ double red[4];
+// channel c's finalize by one workgroup (cgl_bn_finalize; the deferred column-sum finish of
+// cgl_conv_wgrad_reduce_multi); red: 4 doubles of LDS
+template <class FA>
+__device__ __forceinline__ void cgl_bn_finalize_at(const FA& a, int c, double* red) {
   const int lane = threadIdx.x;          // thread index within the channel's workgroup
-  const int c = blockIdx.x;
   const int C = a.C;
   const double* part = a.part;
   // <= 1024 chunks per call and <= 2 calls: every partial this thread needs is loaded once, up front
@@ -2479,6 +2455,47 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
     gst(a.run_mean + c, rm);
     gst(a.run_var + c, rv);
   }
+}
+
+__global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
+  __shared__ double red[4];
+  cgl_bn_finalize_at(a, (int)blockIdx.x, red);
+}
+
+// The deferred split reductions of several weight gradients (cgl_conv_wgrad_defer_begin / _end) and the
+// single-input-channel kernel's finish (cgl_conv_c1_wgrad_fin) as ONE launch: block ranges [begin[q],
+// begin[q + 1]) run reduction q, blocks from begin[n] the c1 finish.  Each block computes exactly what it
+// computes in its own launch (same function, same block index), so the gradients are bitwise unchanged.
+#define CGL_WDEFER_MAX 4
+#define CGL_WDEFER_FIN 3
+struct CglWgradReduceMulti {
+  int n, c1_blocks, nfin;
+  int begin[CGL_WDEFER_MAX + 1];
+  int fbeg[CGL_WDEFER_FIN + 1];   // block offsets of the column-sum finishes, from begin[n] + c1_blocks
+  CglWgradReduceArgs r[CGL_WDEFER_MAX];
+  CglC1Args c1;
+  CglBnFinArgs fin[CGL_WDEFER_FIN];   // deferred column-sum finishes (bias gradients: cgl_colsum_finalize, col_sum)
+};
+
+__global__ __launch_bounds__(256) void cgl_conv_wgrad_reduce_multi(CglWgradReduceMulti m) {
+  __shared__ double red[256];
+  const int b = blockIdx.x, n = m.n;
+  if (b >= m.begin[n] + m.c1_blocks) {
+    const int f = b - m.begin[n] - m.c1_blocks;
+    if (m.nfin > 2 && f >= m.fbeg[2]) cgl_bn_finalize_at(m.fin[2], f - m.fbeg[2], red);
+    else if (m.nfin > 1 && f >= m.fbeg[1]) cgl_bn_finalize_at(m.fin[1], f - m.fbeg[1], red);
+    else cgl_bn_finalize_at(m.fin[0], f, red);
+    return;
+  }
+  if (b >= m.begin[n]) {
+    cgl_conv_c1_wgrad_fin_at(m.c1, b - m.begin[n], red);
+    return;
+  }
+  // (constant member indices: a runtime index into the by-value argument would copy it to scratch)
+  if (n > 3 && b >= m.begin[3]) cgl_conv_wgrad_reduce_at(m.r[3], b - m.begin[3], red);
+  else if (n > 2 && b >= m.begin[2]) cgl_conv_wgrad_reduce_at(m.r[2], b - m.begin[2], red);
+  else if (n > 1 && b >= m.begin[1]) cgl_conv_wgrad_reduce_at(m.r[1], b - m.begin[1], red);
+  else cgl_conv_wgrad_reduce_at(m.r[0], b, red);
 }
 
 // Sliced training-mode BatchNorm2d finalize for statistics with many chunks (the 32-row chunks a
@@ -3715,7 +3732,8 @@ bool pow2_le256(int C) { return C >= 1 && C <= 256 && (C & (C - 1)) == 0; }
 
 // per-column sum of X [rows][C] into out[C] (bias gradient): chunk partials (double), then a
 // fixed-order sum over chunks (cgl_bn_finalize mode 2)
-int col_sum(const float* X, int64_t rows, int C, double* part, float* out, hipStream_t s) {
+// the column sums' partial pass (launched) and their finalize's arguments (f: launched by the caller)
+int col_sum_part(const float* X, int64_t rows, int C, double* part, float* out, hipStream_t s, CglBnFinArgs& f) {
   int nch;
   if (pow2_le256(C)) {
     const int R = 256;
@@ -3729,10 +3747,16 @@ int col_sum(const float* X, int64_t rows, int C, double* part, float* out, hipSt
     nch = (int)((rows + R - 1) / R);
     hipLaunchKernelGGL(cgl_colsum_k, dim3((C + 255) / 256, nch), dim3(256), 0, s, X, (int)rows, C, R, part);
   }
-  CglBnFinArgs f;
   std::memset(&f, 0, sizeof(f));
   f.part = part; f.C = C; f.groups = 1; f.chunks_per_group = nch; f.mode = 2; f.dgamma = out;
   f.nocache = fin_nocache();
+  return (int)hipGetLastError();
+}
+
+int col_sum(const float* X, int64_t rows, int C, double* part, float* out, hipStream_t s) {
+  CglBnFinArgs f;
+  const int rc = col_sum_part(X, rows, C, part, out, s, f);
+  if (rc) return rc;
   hipLaunchKernelGGL(cgl_bn_finalize, dim3(C), dim3(256), 0, s, f);
   return (int)hipGetLastError();
 }
@@ -3876,6 +3900,13 @@ struct WgradDefer {
   bool on = false;
   CglWgradReduceMulti m{};
   bool has_c1 = false;
+  bool add_fin(const CglBnFinArgs& f) {
+    if (m.nfin >= CGL_WDEFER_FIN) return false;
+    m.fin[m.nfin] = f;
+    m.fbeg[m.nfin + 1] = m.fbeg[m.nfin] + f.C;
+    ++m.nfin;
+    return true;
+  }
 };
 thread_local WgradDefer t_wdefer;
 
@@ -4043,11 +4074,17 @@ int conv_bwd_weight_impl(const ConvGeom& g, const float* dY, const float* X, flo
   r.wblocks = (int)((nred + EB - 1) / EB);
   r.db = bias_col ? db : nullptr;
   const int bblocks = bias_col ? (g.cout + EB - 1) / EB : 0;
-  if (t_wdefer.on && (!db || bias_col) && t_wdefer.m.n < CGL_WDEFER_MAX) {
+  if (t_wdefer.on && t_wdefer.m.n < CGL_WDEFER_MAX && (!db || bias_col || t_wdefer.m.nfin < CGL_WDEFER_FIN)) {
     CglWgradReduceMulti& m = t_wdefer.m;
     m.r[m.n] = r;
     m.begin[m.n + 1] = m.begin[m.n] + r.wblocks + bblocks;
     ++m.n;
+    if (db && !bias_col) {   // the bias gradient's column-sum pass now, its finish with the reductions
+      double* bp = (double*)(((uintptr_t)part + 255) & ~(uintptr_t)255);
+      CglBnFinArgs f;
+      if ((rc = col_sum_part(dY, (int64_t)g.n * g.ho * g.wo, g.cout, bp, db, s, f))) return rc;
+      t_wdefer.add_fin(f);
+    }
     return 0;
   }
   hipLaunchKernelGGL(cgl_conv_wgrad_reduce, dim3((unsigned)(r.wblocks + bblocks)), dim3(256), 0, s, r);
@@ -4193,9 +4230,9 @@ int cgl_conv_wgrad_defer_end(void* stream) {
   if (!t_wdefer.on) return CGL_E_STATE;
   t_wdefer.on = false;
   CglWgradReduceMulti& m = t_wdefer.m;
-  const int blocks = m.begin[m.n] + (t_wdefer.has_c1 ? m.c1_blocks : 0);
-  if (blocks == 0) return CGL_OK;
   if (!t_wdefer.has_c1) m.c1_blocks = 0;
+  const int blocks = m.begin[m.n] + m.c1_blocks + m.fbeg[m.nfin];
+  if (blocks == 0) return CGL_OK;
   hipLaunchKernelGGL(cgl_conv_wgrad_reduce_multi, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, m);
   return (int)hipGetLastError();
 }
@@ -4660,6 +4697,7 @@ int cgl_colsum_finalize(const double* part, int nch, int C, float* out, void* st
   std::memset(&f, 0, sizeof(f));
   f.part = part; f.C = C; f.groups = 1; f.chunks_per_group = nch; f.mode = 2; f.dgamma = out;
   f.nocache = fin_nocache();
+  if (t_wdefer.on && t_wdefer.add_fin(f)) return CGL_OK;   // rides in the deferred reductions' launch
   hipLaunchKernelGGL(cgl_bn_finalize, dim3(C), dim3(256), 0, (hipStream_t)stream, f);
   return (int)hipGetLastError();
 }

@@ -349,12 +349,13 @@ int cgl_conv_batch_begin(void* stream);
 int cgl_conv_batch_end(void* stream);
 /* Deferred weight-gradient reductions (the conv round's D and G backward): between cgl_conv_wgrad_defer_begin()
  * and cgl_conv_wgrad_defer_end(stream), cgl_conv3x3_bwd_weight(_bnin / _actdrop) on the calling thread launch
- * their MFMA kernel and record their fixed-order split reduction (up to 4; and one single-input-channel finish)
- * instead of launching it; _end launches every recorded one as ONE kernel on that stream.  Bitwise the separate
- * launches.  The recorded reductions read their partials from the workspace each call was given, so every
+ * their MFMA kernel and record their fixed-order split reduction (up to 4; and one single-input-channel finish;
+ * and one cgl_colsum_finalize, whose partials must likewise stay untouched until _end) instead of launching it;
+ * _end launches every recorded one as ONE kernel on that stream.  Bitwise the separate launches.  The recorded reductions read their partials from the workspace each call was given, so every
  * deferred call needs its OWN workspace, untouched until _end; dW / db are written at _end.  A call the batch
- * cannot take (a fifth reduction, a bias gradient by column sums) launches its reduction at once, as outside a
- * batch.  Other entry points are unaffected.  Returns CGL_E_STATE for a nested begin or an end without begin. */
+ * cannot take (a fifth reduction; a fourth column-sum bias finish) launches its reduction at once, as outside a
+ * batch.  A bias gradient by column sums (no bias column in the reduction) runs its column-sum pass at once and
+ * its finish with the reductions.  Other entry points are unaffected.  Returns CGL_E_STATE for a nested begin or an end without begin. */
 int cgl_conv_wgrad_defer_begin(void);
 int cgl_conv_wgrad_defer_end(void* stream);
 int cgl_conv3x3_fwd_packed(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w, int cin,
