@@ -171,7 +171,7 @@ def _load():
         "cgl_nhwc_to_nchw": (ci, [vp, vp, ci, ci, ci, vp]),
         "cgl_adv_loss": (ci, [vp, ci, ci, ci, ci, cd, vp, vp, vp, vp]),
         "cgl_dense1_head_nhwc": (ci, [vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, cd, vp, vp, ci, cd, vp, vp,
-                                      vp]),
+                                      ci, vp, vp]),
         "cgl_dense_workspace_bytes": (i64, [ci] * 3),
         "cgl_dense_fwd": (ci, [vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, i64, vp]),
         "cgl_dense_bwd_data": (ci, [vp, vp, vp, ci, ci, ci, vp, i64, vp]),

@@ -542,11 +542,16 @@ def nhwc_to_nchw(x, y, n, c, hw):
     return y
 
 
-def dense1_head_nhwc(x, w, b, y, dy, dx, n, c, hw, kind, calls, scratch, flat=None):
+def dense1_head_nhwc(x, w, b, y, dy, dx, n, c, hw, kind, calls, scratch, flat=None, bn_in=None):
     """adv_layer forward + loss + input gradient in one launch (cgl_dense1_head_nhwc).  ``calls``: [(rows, target,
     weight, loss_out, nvalid)] -- one or two calls over consecutive rows (nvalid: the first call only).
-    ``scratch``: >= n + 16 floats, zeroed once before its first use (a monotonic ticket + the loss terms)."""
-    _chk(x, w, b, y, dy, dx, flat, scratch)
+    ``scratch``: >= n + 16 floats, zeroed once before its first use (a monotonic ticket + the loss terms).
+    ``bn_in`` = (coef, groups): ``x`` is the pre-BatchNorm map, its BatchNorm (bn2d_fwd_stats(coef=)'s scale /
+    shift, act none) applied in the loads."""
+    coef, groups = bn_in if bn_in is not None else (None, 1)
+    _chk(x, w, b, y, dy, dx, flat, scratch, coef)
+    if coef is not None and coef.numel() < 2 * groups * c:
+        raise ValueError("dense1_head_nhwc: bn_in coefficients [2][groups][c] expected")
     if len(calls) not in (1, 2) or sum(cl[0] for cl in calls) != n:
         raise ValueError("dense1_head_nhwc: one or two calls covering the n rows")
     if (x.numel() < n * c * hw or w.numel() < c * hw or y.numel() < n or dy.numel() < n or dx.numel() < n * c * hw or
@@ -556,7 +561,7 @@ def dense1_head_nhwc(x, w, b, y, dy, dx, n, c, hw, kind, calls, scratch, flat=No
     (t1, w1, l1) = (calls[1][1], calls[1][2], calls[1][3]) if len(calls) > 1 else (0, 0.0, None)
     C.check(C.lib.cgl_dense1_head_nhwc(_p(x), _p(w), _p(b), _p(y), _p(flat), _p(dy), _p(dx), n, c, hw, LOSS[kind],
                                        n0, int(t0), float(w0), _p(l0), _p(nv0), int(t1), float(w1), _p(l1),
-                                       _p(scratch), _s()), "cgl_dense1_head_nhwc")
+                                       _p(coef), int(groups), _p(scratch), _s()), "cgl_dense1_head_nhwc")
 
 
 def adv_loss(x, M, Cc, kind, target, weight, loss_out=None, grad=None, nvalid=None):

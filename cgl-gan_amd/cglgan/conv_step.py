@@ -286,6 +286,10 @@ class ConvGanStep:
         # (cgl_dense1_head_nhwc, bitwise the separate launches; CGL_CONV_HEADFUSE=0 keeps them).  Each pass has its
         # own scratch: a monotonic ticket counted modulo that launch's grid + the per-row loss terms
         self.head_fuse = os.environ.get("CGL_CONV_HEADFUSE", "1") != "0"
+        # ... and with it, D's last BatchNorm (model.14) applied in the head's loads (its finalize keeps the scale /
+        # shift only: one cgl_eltwise fewer per pass; bitwise, CGL_CONV_HEADBN=0 applies it)
+        self.head_bn = self.head_fuse and os.environ.get("CGL_CONV_HEADBN", "1") != "0"
+        self._head_coef = None
         self.hscr_d, self.hscr_g = torch.zeros(B2 + 16, device=dev), torch.zeros(B + 16, device=dev)
         # the split reductions of a backward pass's weight gradients (and Conv2d(1, 16)'s finish) as ONE launch at the
         # end of the pass (cgl_conv_wgrad_defer; bitwise the separate launches; CGL_CONV_WDEFER=0 launches each with
@@ -490,6 +494,7 @@ class ConvGanStep:
         gradient applies it in its operand loads too (cgl_conv3x3_bwd_weight_bnin) -- two cgl_eltwise passes fewer
         per pass; CGL_CONV_DFOLD=0 applies them."""
         P, R = self.D.params, self.D.running
+        self._head_coef = None
         fold_pass = self.d_fold and ((masks is self.mask_g and groups == 1) or
                                      (masks is self.mask_d and self.d_fold_step))
         if masks is self.mask_d:
@@ -502,10 +507,14 @@ class ConvGanStep:
                           nvalid=nvalid if st is not None else None, bn_in=bn_in)
             inp, bn_in = self.q[k], None
             if bk:
-                fold = fold_pass and k + 1 < len(D_CONVS) and bk in self.st_part
+                last = k + 1 == len(D_CONVS)
+                hfold = last and self.head_bn and bk in self.st_part     # the head applies it
+                fold = (fold_pass and not last and bk in self.st_part) or hfold
                 self._bn_fwd(bk, self.D, self.q[k], self.r[k], n, (hw // 2) ** 2, co, groups, O.ACT_NONE, nvalid=nvalid,
                              coef_only=fold)
-                if fold:
+                if hfold:
+                    self._head_coef = (self.dcoef[bk], groups)
+                elif fold:
                     bn_in = (self.dcoef[bk], groups, O.ACT_NONE, SLOPE)
                     if masks is self.mask_d:
                         self._d_folded.add(bk)
@@ -520,8 +529,9 @@ class ConvGanStep:
     def _head(self, n, calls, scratch, flat):
         """adv_layer forward + the loss head(s) + adv_layer's input gradient (dr[3]) as one launch."""
         P = self.D.params
-        O.dense1_head_nhwc(self.r[3], P["adv_layer.weight"], P["adv_layer.bias"], self.v, self.dv, self.dr[3], n, 128,
-                           4, self.loss, calls, scratch, flat=flat)
+        hc = self._head_coef if self.head_bn else None
+        O.dense1_head_nhwc(self.q[3] if hc else self.r[3], P["adv_layer.weight"], P["adv_layer.bias"], self.v, self.dv,
+                           self.dr[3], n, 128, 4, self.loss, calls, scratch, flat=flat, bn_in=hc)
 
     def _d_backward(self, x, n, groups, masks, wgrad, dx, nvalid=None):
         with O.wgrad_defer(wgrad and self.wdefer):

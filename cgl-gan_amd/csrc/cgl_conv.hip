@@ -2462,41 +2462,6 @@ __global__ __launch_bounds__(256) void cgl_bn_finalize(CglBnFinArgs a) {
   cgl_bn_finalize_at(a, (int)blockIdx.x, red);
 }
 
-// The deferred split reductions of several weight gradients (cgl_conv_wgrad_defer_begin / _end) and the
-// single-input-channel kernel's finish (cgl_conv_c1_wgrad_fin) as ONE launch: block ranges [begin[q],
-// begin[q + 1]) run reduction q, blocks from begin[n] the c1 finish.  Each block computes exactly what it
-// computes in its own launch (same function, same block index), so the gradients are bitwise unchanged.
-#define CGL_WDEFER_MAX 4
-#define CGL_WDEFER_FIN 3
-struct CglWgradReduceMulti {
-  int n, c1_blocks, nfin;
-  int begin[CGL_WDEFER_MAX + 1];
-  int fbeg[CGL_WDEFER_FIN + 1];   // block offsets of the column-sum finishes, from begin[n] + c1_blocks
-  CglWgradReduceArgs r[CGL_WDEFER_MAX];
-  CglC1Args c1;
-  CglBnFinArgs fin[CGL_WDEFER_FIN];   // deferred column-sum finishes (bias gradients: cgl_colsum_finalize, col_sum)
-};
-
-__global__ __launch_bounds__(256) void cgl_conv_wgrad_reduce_multi(CglWgradReduceMulti m) {
-  __shared__ double red[256];
-  const int b = blockIdx.x, n = m.n;
-  if (b >= m.begin[n] + m.c1_blocks) {
-    const int f = b - m.begin[n] - m.c1_blocks;
-    if (m.nfin > 2 && f >= m.fbeg[2]) cgl_bn_finalize_at(m.fin[2], f - m.fbeg[2], red);
-    else if (m.nfin > 1 && f >= m.fbeg[1]) cgl_bn_finalize_at(m.fin[1], f - m.fbeg[1], red);
-    else cgl_bn_finalize_at(m.fin[0], f, red);
-    return;
-  }
-  if (b >= m.begin[n]) {
-    cgl_conv_c1_wgrad_fin_at(m.c1, b - m.begin[n], red);
-    return;
-  }
-  // (constant member indices: a runtime index into the by-value argument would copy it to scratch)
-  if (n > 3 && b >= m.begin[3]) cgl_conv_wgrad_reduce_at(m.r[3], b - m.begin[3], red);
-  else if (n > 2 && b >= m.begin[2]) cgl_conv_wgrad_reduce_at(m.r[2], b - m.begin[2], red);
-  else if (n > 1 && b >= m.begin[1]) cgl_conv_wgrad_reduce_at(m.r[1], b - m.begin[1], red);
-  else cgl_conv_wgrad_reduce_at(m.r[0], b, red);
-}
 
 // Sliced training-mode BatchNorm2d finalize for statistics with many chunks (the 32-row chunks a
 // conv epilogue writes: 8192 per forward call of the generator's last BatchNorm at B=256): block
@@ -2626,8 +2591,11 @@ __device__ __forceinline__ void cgl_adv_row1(float z, int loss, int target, floa
   }
 }
 
+// coef: the row's BatchNorm applied to every loaded value (v = fmaf(x, coef[cg + c], coef[shb + cg + c]), the
+// cgl_eltwise mode-0 arithmetic, act none: the head of the D step / G-loss pass reads the PRE-BatchNorm map)
 __device__ __forceinline__ float cgl_dense1_row(const float* __restrict__ X, const float* __restrict__ W,
-                                                float* __restrict__ flat, int row, int q, int C, int hw) {
+                                                float* __restrict__ flat, int row, int q, int C, int hw,
+                                                const float* __restrict__ coef = nullptr, int cg = 0, int shb = 0) {
   const int per = C * hw, nb = per >> 8;     // per % 256 == 0, nb <= 4
   const float* __restrict__ x = X + (long)row * per;
   f32x4 v[4], w[4];
@@ -2639,6 +2607,7 @@ __device__ __forceinline__ float cgl_dense1_row(const float* __restrict__ X, con
       for (int j = 0; j < 4; ++j) {
         const int c = (k0 + j) / hw, s = k0 + j - c * hw;
         v[bb][j] = gld(x + s * C + c);
+        if (coef) v[bb][j] = fmaf(v[bb][j], gld(coef + cg + c), gld(coef + shb + cg + c));
       }
       w[bb] = *(gcf4p)(W + k0);
     }
@@ -2693,13 +2662,15 @@ struct CglDHeadArgs {
   CglHeadCall call[2];
   float* lrow;               // [n] published loss terms
   unsigned int* ticket;      // monotonic (zeroed once by the caller)
+  const float* coef; int groups;   // X's BatchNorm [2][groups][C] applied in the loads (cgl_dense1_row), or null
 };
 __global__ __launch_bounds__(256) void cgl_dense1_head_k(CglDHeadArgs a) {
   __shared__ double s_acc[256];
   __shared__ int s_last;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), q = threadIdx.x & 63;
   if (row < a.n) {                           // wave-uniform
-    const float acc = cgl_dense1_row(a.X, a.W, a.flat, row, q, a.C, a.hw);
+    const int bg = a.coef ? min(row / (a.n / a.groups), a.groups - 1) : 0;
+    const float acc = cgl_dense1_row(a.X, a.W, a.flat, row, q, a.C, a.hw, a.coef, bg * a.C, a.groups * a.C);
     const float z = acc + (a.b ? gld(a.b) : 0.f);
     const int ci = (a.ncalls > 1 && row >= a.call[1].n0) ? 1 : 0;
     const int n0 = ci ? a.call[1].n0 : a.call[0].n0, nc = ci ? a.call[1].n : a.call[0].n;
@@ -2762,12 +2733,12 @@ __global__ __launch_bounds__(256) void cgl_dense1_head_k(CglDHeadArgs a) {
 // Block b < gridDim.x - 1: 16 columns x 16 row lanes (a wave reads 4 rows x 64 contiguous bytes); lane l sums
 // rows l, l + 16, ... in order in double (exact products), 32 loads in flight (M <= 512: one batch); the 16 lanes
 // are added in lane order.  The last block: db, thread t summing rows t, t + 256, ... then the 256 partials in order.
-__global__ __launch_bounds__(256) void cgl_dense1_wgrad_k(const float* __restrict__ dY, const float* __restrict__ X,
-                                                          float* __restrict__ dW, float* __restrict__ db, int M,
-                                                          int K) {
-  __shared__ double red[256];
+// block bid of nblk (cgl_dense1_wgrad_k; the deferred reductions' launch, cgl_conv_wgrad_reduce_multi)
+__device__ __forceinline__ void cgl_dense1_wgrad_at(const float* __restrict__ dY, const float* __restrict__ X,
+                                                    float* __restrict__ dW, float* __restrict__ db, int M, int K,
+                                                    int bid, int nblk, double* red) {
   const int t = threadIdx.x;
-  if ((int)blockIdx.x == (int)gridDim.x - 1) {      // the bias block (uniform)
+  if (bid == nblk - 1) {      // the bias block (uniform)
     double acc = 0.0;
     for (int m = t; m < M; m += 256) acc += (double)gld(dY + m);
     red[t] = acc;
@@ -2780,7 +2751,7 @@ __global__ __launch_bounds__(256) void cgl_dense1_wgrad_k(const float* __restric
     return;
   }
   const int kl = t & 15, ml = t >> 4;
-  const int k = blockIdx.x * 16 + kl, kc = min(k, K - 1);
+  const int k = bid * 16 + kl, kc = min(k, K - 1);
   double acc = 0.0;
   for (int m0 = ml; m0 < M; m0 += 16 * 32) {
     float xv[32], dv[32];
@@ -2801,6 +2772,57 @@ __global__ __launch_bounds__(256) void cgl_dense1_wgrad_k(const float* __restric
     for (int l = 0; l < 16; ++l) s += red[16 * l + kl];
     gst(dW + k, (float)s);
   }
+}
+
+__global__ __launch_bounds__(256) void cgl_dense1_wgrad_k(const float* __restrict__ dY, const float* __restrict__ X,
+                                                          float* __restrict__ dW, float* __restrict__ db, int M,
+                                                          int K) {
+  __shared__ double red[256];
+  cgl_dense1_wgrad_at(dY, X, dW, db, M, K, (int)blockIdx.x, (int)gridDim.x, red);
+}
+
+// The deferred split reductions of several weight gradients (cgl_conv_wgrad_defer_begin / _end) and the
+// single-input-channel kernel's finish (cgl_conv_c1_wgrad_fin) as ONE launch: block ranges [begin[q],
+// begin[q + 1]) run reduction q, blocks from begin[n] the c1 finish, then the column-sum finishes, then the
+// one-output dense weight gradient.  Each block computes exactly what it
+// computes in its own launch (same function, same block index), so the gradients are bitwise unchanged.
+#define CGL_WDEFER_MAX 4
+#define CGL_WDEFER_FIN 3
+struct CglWgradReduceMulti {
+  int n, c1_blocks, nfin;
+  int begin[CGL_WDEFER_MAX + 1];
+  int fbeg[CGL_WDEFER_FIN + 1];   // block offsets of the column-sum finishes, from begin[n] + c1_blocks
+  CglWgradReduceArgs r[CGL_WDEFER_MAX];
+  CglC1Args c1;
+  CglBnFinArgs fin[CGL_WDEFER_FIN];   // deferred column-sum finishes (bias gradients: cgl_colsum_finalize, col_sum)
+  // a deferred one-output dense weight gradient (cgl_dense1_wgrad_k: the D head's adv_layer), d1_blocks > 0
+  const float* d1_dy; const float* d1_x; float* d1_dw; float* d1_db; int d1_M, d1_K, d1_blocks;
+};
+
+__global__ __launch_bounds__(256) void cgl_conv_wgrad_reduce_multi(CglWgradReduceMulti m) {
+  __shared__ double red[256];
+  const int b = blockIdx.x, n = m.n;
+  const int fend = m.begin[n] + m.c1_blocks + m.fbeg[m.nfin];
+  if (b >= fend) {
+    cgl_dense1_wgrad_at(m.d1_dy, m.d1_x, m.d1_dw, m.d1_db, m.d1_M, m.d1_K, b - fend, m.d1_blocks, red);
+    return;
+  }
+  if (b >= m.begin[n] + m.c1_blocks) {
+    const int f = b - m.begin[n] - m.c1_blocks;
+    if (m.nfin > 2 && f >= m.fbeg[2]) cgl_bn_finalize_at(m.fin[2], f - m.fbeg[2], red);
+    else if (m.nfin > 1 && f >= m.fbeg[1]) cgl_bn_finalize_at(m.fin[1], f - m.fbeg[1], red);
+    else cgl_bn_finalize_at(m.fin[0], f, red);
+    return;
+  }
+  if (b >= m.begin[n]) {
+    cgl_conv_c1_wgrad_fin_at(m.c1, b - m.begin[n], red);
+    return;
+  }
+  // (constant member indices: a runtime index into the by-value argument would copy it to scratch)
+  if (n > 3 && b >= m.begin[3]) cgl_conv_wgrad_reduce_at(m.r[3], b - m.begin[3], red);
+  else if (n > 2 && b >= m.begin[2]) cgl_conv_wgrad_reduce_at(m.r[2], b - m.begin[2], red);
+  else if (n > 1 && b >= m.begin[1]) cgl_conv_wgrad_reduce_at(m.r[1], b - m.begin[1], red);
+  else cgl_conv_wgrad_reduce_at(m.r[0], b, red);
 }
 
 // Elementwise NHWC passes (float4 over channels; C % 4 == 0):
@@ -4202,6 +4224,12 @@ int cgl_dense_bwd_weight(const float* dY, const float* X, float* dW, float* db, 
   // N = 1 (adv_layer): the one-launch kernel (CGL_DENSE1_WG=0: the implicit-GEMM weight gradient)
   static const int d1 = getenv("CGL_DENSE1_WG") ? atoi(getenv("CGL_DENSE1_WG")) : 1;
   if (d1 && N == 1 && dY && X && dW && (int64_t)M * K < ((int64_t)1 << 31)) {
+    if (t_wdefer.on && t_wdefer.m.d1_blocks == 0) {   // rides in the deferred reductions' launch
+      CglWgradReduceMulti& m = t_wdefer.m;
+      m.d1_dy = dY; m.d1_x = X; m.d1_dw = dW; m.d1_db = db; m.d1_M = M; m.d1_K = K;
+      m.d1_blocks = (K + 15) / 16 + 1;
+      return CGL_OK;
+    }
     hipLaunchKernelGGL(cgl_dense1_wgrad_k, dim3((K + 15) / 16 + 1), dim3(256), 0, (hipStream_t)stream, dY, X, dW, db,
                        M, K);
     return (int)hipGetLastError();
@@ -4231,7 +4259,7 @@ int cgl_conv_wgrad_defer_end(void* stream) {
   t_wdefer.on = false;
   CglWgradReduceMulti& m = t_wdefer.m;
   if (!t_wdefer.has_c1) m.c1_blocks = 0;
-  const int blocks = m.begin[m.n] + m.c1_blocks + m.fbeg[m.nfin];
+  const int blocks = m.begin[m.n] + m.c1_blocks + m.fbeg[m.nfin] + m.d1_blocks;
   if (blocks == 0) return CGL_OK;
   hipLaunchKernelGGL(cgl_conv_wgrad_reduce_multi, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, m);
   return (int)hipGetLastError();
@@ -4782,10 +4810,11 @@ int cgl_dense1_bwd_data_nhwc(const float* dY, const float* W, float* dX, int n, 
 
 int cgl_dense1_head_nhwc(const float* X, const float* W, const float* b, float* Y, float* flat, float* dY, float* dX,
                          int n, int c, int hw, int loss, int n0, int target0, double weight0, float* loss_out0,
-                         const int* nvalid0, int target1, double weight1, float* loss_out1, float* scratch,
-                         void* stream) {
+                         const int* nvalid0, int target1, double weight1, float* loss_out1, const float* in_coef,
+                         int in_groups, float* scratch, void* stream) {
   CGL_BATCH_GUARD();
   const long per = (long)c * hw;
+  if (in_coef && (in_groups < 1 || n % in_groups)) return CGL_E_ARG;
   if (!X || !W || !Y || !dY || !dX || !scratch || n < 1 || c < 4 || (c & 3) || hw < 1 || per % 256 || per > 1024 ||
       (long)n * per >= (1L << 31) || !al16(W) || !al16(dX) || (flat && !al16(flat)) || loss < 1 || loss > 3 ||
       n0 < 1 || n0 > n || (target0 != 0 && target0 != 1) || (n0 < n && target1 != 0 && target1 != 1))
@@ -4798,6 +4827,8 @@ int cgl_dense1_head_nhwc(const float* X, const float* W, const float* b, float* 
   a.call[1] = CglHeadCall{n0, n - n0, target1, (float)weight1, loss_out1, nullptr};
   a.ticket = (unsigned int*)scratch;
   a.lrow = scratch + 16;
+  a.coef = in_coef;
+  a.groups = in_coef ? in_groups : 1;
   hipLaunchKernelGGL(cgl_dense1_head_k, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }

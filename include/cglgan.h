@@ -348,14 +348,16 @@ int cgl_conv_pack_multi(int njobs, const CglConvPackJob* jobs, void* stream);
 int cgl_conv_batch_begin(void* stream);
 int cgl_conv_batch_end(void* stream);
 /* Deferred weight-gradient reductions (the conv round's D and G backward): between cgl_conv_wgrad_defer_begin()
- * and cgl_conv_wgrad_defer_end(stream), cgl_conv3x3_bwd_weight(_bnin / _actdrop) on the calling thread launch
- * their MFMA kernel and record their fixed-order split reduction (up to 4; and one single-input-channel finish;
- * and one cgl_colsum_finalize, whose partials must likewise stay untouched until _end) instead of launching it;
- * _end launches every recorded one as ONE kernel on that stream.  Bitwise the separate launches.  The recorded reductions read their partials from the workspace each call was given, so every
- * deferred call needs its OWN workspace, untouched until _end; dW / db are written at _end.  A call the batch
- * cannot take (a fifth reduction; a fourth column-sum bias finish) launches its reduction at once, as outside a
- * batch.  A bias gradient by column sums (no bias column in the reduction) runs its column-sum pass at once and
- * its finish with the reductions.  Other entry points are unaffected.  Returns CGL_E_STATE for a nested begin or an end without begin. */
+ * and cgl_conv_wgrad_defer_end(stream), these calls on the calling thread record their last step instead of
+ * launching it: cgl_conv3x3_bwd_weight(_bnin / _actdrop) launch their MFMA kernel and record the fixed-order split
+ * reduction (up to 4) or the single-input-channel kernel's finish (one); a column-sum bias gradient (no bias
+ * column in the reduction) runs its column-sum pass at once and records its finish, as cgl_colsum_finalize does
+ * (up to 3 finishes); one cgl_dense_bwd_weight with N = 1 records its whole launch.  _end launches every recorded
+ * step as ONE kernel on that stream.  Bitwise the separate launches.  Each recorded step reads its partials or
+ * inputs when _end runs, so every deferred weight gradient needs its OWN workspace, and those buffers and the
+ * dense inputs stay untouched until _end; dW / db are written at _end.  A call the batch cannot take (a fifth
+ * reduction, a fourth finish) launches at once, as outside a batch.  Other entry points are unaffected.
+ * Returns CGL_E_STATE for a nested begin or an end without begin. */
 int cgl_conv_wgrad_defer_begin(void);
 int cgl_conv_wgrad_defer_end(void* stream);
 int cgl_conv3x3_fwd_packed(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w, int cin,
@@ -503,12 +505,14 @@ int cgl_dense1_fwd_nhwc(const float* X, const float* W, const float* b, float* Y
  * of dY -- bitwise what the three (or, with two calls, four) separate launches produce.  Call 0 is rows [0, n0)
  * (target0, weight0, loss_out0, nvalid0: a short first call as cgl_adv_loss), call 1 rows [n0, n) when n0 < n
  * (the D step's real and fake halves, capgan.py:332-340).  scratch: >= n + 16 floats, zeroed ONCE before the first
- * use (its first word is a monotonic ticket; the last workgroup reduces the losses).  c % 4 == 0,
- * c * hw % 256 == 0, <= 1024. */
+ * use (its first word is a monotonic ticket; the last workgroup reduces the losses).  in_coef (may be null): X is
+ * the PRE-BatchNorm map and its BatchNorm2d (act none) is applied to every loaded value, scale in_coef[g c + ch],
+ * shift in_coef[in_groups c + g c + ch] for rows of group g = row / (n / in_groups) (cgl_bn2d_fwd_stats_coef's
+ * coef; bitwise its applied map, which flat receives).  c % 4 == 0, c * hw % 256 == 0, <= 1024. */
 int cgl_dense1_head_nhwc(const float* X, const float* W, const float* b, float* Y, float* flat, float* dY, float* dX,
                          int n, int c, int hw, int loss, int n0, int target0, double weight0, float* loss_out0,
-                         const int* nvalid0, int target1, double weight1, float* loss_out1, float* scratch,
-                         void* stream);
+                         const int* nvalid0, int target1, double weight1, float* loss_out1, const float* in_coef,
+                         int in_groups, float* scratch, void* stream);
 /* Mean adversarial loss of one forward call and weight * its gradient (grad may be null):
  * loss 0 CrossEntropy on 2 logits (capgan.py:311), 1 BCELoss on probabilities
  * (CGLGAN/2DMG/main.py:336), 2 MSELoss (LSGAN objective of model/lsgan.py's D), 3 Sigmoid + BCELoss
