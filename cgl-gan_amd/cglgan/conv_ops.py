@@ -426,15 +426,20 @@ def bn2d_bwd(dy, x, n, hw, c, save_mean, save_invstd, gamma, dx, groups=1, post=
 
 
 def bn2d_bwd_stats(part, dy, x, n, hw, c, save_mean, save_invstd, gamma, dx, groups=1, post=None, post_out=None,
-                   drop=None, dgamma=None, dbeta=None, slope=0.2, R=32, nvalid=None, post_coef=None):
-    """bn2d_bwd from the partials a conv3x3_bwd_data(stats=...) wrote: finalize + apply."""
+                   drop=None, dgamma=None, dbeta=None, slope=0.2, R=32, nvalid=None, post_coef=None, colsum=None):
+    """bn2d_bwd from the partials a conv3x3_bwd_data(stats=...) wrote: finalize + apply.  ``colsum``: float64
+    [n hw / 256, c, 2] -- also dx's column sums per 256-row chunk (colsum_finalize(colsum, n hw // 256, c, db):
+    bitwise the bias gradient conv3x3_bwd_weight computes from dx)."""
+    if colsum is not None and (not colsum.is_cuda or colsum.dtype != torch.float64 or
+                               colsum.numel() < (n * hw // 256) * c * 2):
+        raise RuntimeError("bn2d_bwd_stats(colsum=...): float64 CUDA buffer of [n hw / 256][c][2]")
     _chk(dy, x, save_mean, save_invstd, gamma, dx, post, post_out, drop, dgamma, dbeta)
     ws = workspace(bn2d_ws_bytes(n, hw, c, groups), dy.device)
     pc, pld = _post_coef(post_coef, c)
     C.check(C.lib.cgl_bn2d_bwd_stats(_p(part), int(R), _p(dy), _p(post), _p(x), n, hw, c, groups, _p(save_mean),
                                      _p(save_invstd), _p(gamma), float(slope), _p(post_out), _p(drop), _p(dx),
-                                     _p(dgamma), _p(dbeta), _p(pc), int(pld), _p(nvalid), _p(ws), ws.numel(), _s()),
-            "cgl_bn2d_bwd_stats")
+                                     _p(dgamma), _p(dbeta), _p(pc), int(pld), _p(nvalid), _p(colsum), _p(ws),
+                                     ws.numel(), _s()), "cgl_bn2d_bwd_stats")
     return dx
 
 

@@ -294,6 +294,16 @@ class ConvGanStep:
         # the split reductions of a backward pass's weight gradients (and Conv2d(1, 16)'s finish) as ONE launch at the
         # end of the pass (cgl_conv_wgrad_defer; bitwise the separate launches; CGL_CONV_WDEFER=0 launches each with
         # its MFMA kernel): every deferred weight gradient writes its partials into a workspace of its own
+        # the G BatchNorm backward applies (conv_blocks.6 / .2, from producer statistics) also write their output's
+        # column sums per 256-row chunk: conv_blocks.5 / .1's bias gradients without their own pass over dy2 / dy1
+        # (cgl_bn2d_bwd_stats colsum_part + cgl_colsum_finalize; bitwise; CGL_CONV_BNBCOL=0: the weight gradient's)
+        # (only where the weight gradient itself sums columns of dY: cgl_conv3x3_bias_by_colsum)
+        self.bnb_col = os.environ.get("CGL_CONV_BNBCOL", "1") != "0"
+        self.bcs = {}
+        for k, hw, c, geo in (("conv_blocks.6", 1024, 64, (B, 16, 16, 128, 64, 1, 1)),
+                              ("conv_blocks.2", 256, 128, (B, 8, 8, 128, 128, 1, 1))):
+            if self.bnb_col and C.lib.cgl_conv3x3_bias_by_colsum(*geo) == 1:
+                self.bcs[k] = torch.zeros(B * hw // 256 * c * 2, dtype=torch.float64, device=dev)
         self.wdefer = os.environ.get("CGL_CONV_WDEFER", "1") != "0"
         self.wws = {}
         if self.wdefer:
@@ -615,17 +625,21 @@ class ConvGanStep:
             O.conv3x3_bwd_data(self.dc3g, P["conv_blocks.8.weight"], self.da2, B, 32, 32, 64, 1, 1, 0,
                                stats=(part, 1, self.y2[B:], kw["post"], sm[1], SLOPE, pc6))
             O.bn2d_bwd_stats(part, self.da2, self.y2[B:], B, 1024, 64, sm[1], si[1], P["conv_blocks.6.weight"],
-                             self.dy2, R=128, **kw)
+                             self.dy2, R=128, colsum=self.bcs.get("conv_blocks.6"), **kw)
         else:
             O.conv3x3_bwd_data(self.dc3g, P["conv_blocks.8.weight"], self.da2, B, 32, 32, 64, 1, 1, 0)
             O.bn2d_bwd(self.da2, self.y2[B:], B, 1024, 64, sm[1], si[1], P["conv_blocks.6.weight"], self.dy2, **kw)
+        c6 = self.n1_stats and "conv_blocks.6" in self.bcs       # conv_blocks.5's bias from the apply's sums
+        db5 = None if c6 else G["conv_blocks.5.bias"]
         if e2:
-            O.conv3x3_bwd_weight(self.dy2, self.y1[B:], G["conv_blocks.5.weight"], G["conv_blocks.5.bias"], B, 16, 16,
+            O.conv3x3_bwd_weight(self.dy2, self.y1[B:], G["conv_blocks.5.weight"], db5, B, 16, 16,
                                  128, 64, 1, 1, bn_in=(self.coef["conv_blocks.2"], 1, 2, O.ACT_LEAKY, SLOPE),
                                  ws=wws.get("conv_blocks.5"))
         else:
-            O.conv3x3_bwd_weight(self.dy2, self.a1[B:], G["conv_blocks.5.weight"], G["conv_blocks.5.bias"], B, 16, 16,
+            O.conv3x3_bwd_weight(self.dy2, self.a1[B:], G["conv_blocks.5.weight"], db5, B, 16, 16,
                                  128, 64, 1, 1, ws=wws.get("conv_blocks.5"))
+        if c6:
+            O.colsum_finalize(self.bcs["conv_blocks.6"], B * 1024 // 256, 64, G["conv_blocks.5.bias"])
         sm, si = self.g_save["conv_blocks.2"]
         st = None
         if self.bst_ok.get("conv_blocks.2"):
@@ -636,13 +650,16 @@ class ConvGanStep:
         pc2 = self._post_coef("conv_blocks.2")
         kw = dict(post=None if pc2 else self.a1[B:], post_coef=pc2, dgamma=G["conv_blocks.2.weight"],
                   dbeta=G["conv_blocks.2.bias"], slope=SLOPE)
+        c2 = st is not None and "conv_blocks.2" in self.bcs     # conv_blocks.1's bias from the apply's sums
         if st is not None:
             O.bn2d_bwd_stats(self.st_part["conv_blocks.2"], self.da1, self.y1[B:], B, 256, 128, sm[1], si[1],
-                             P["conv_blocks.2.weight"], self.dy1, **kw)
+                             P["conv_blocks.2.weight"], self.dy1, colsum=self.bcs.get("conv_blocks.2"), **kw)
         else:
             O.bn2d_bwd(self.da1, self.y1[B:], B, 256, 128, sm[1], si[1], P["conv_blocks.2.weight"], self.dy1, **kw)
-        O.conv3x3_bwd_weight(self.dy1, self.h0[B:], G["conv_blocks.1.weight"], G["conv_blocks.1.bias"], B, 8, 8, 128,
-                             128, 1, 1, ws=wws.get("conv_blocks.1"))
+        O.conv3x3_bwd_weight(self.dy1, self.h0[B:], G["conv_blocks.1.weight"], None if c2 else G["conv_blocks.1.bias"],
+                             B, 8, 8, 128, 128, 1, 1, ws=wws.get("conv_blocks.1"))
+        if c2:
+            O.colsum_finalize(self.bcs["conv_blocks.2"], B * 256 // 256, 128, G["conv_blocks.1.bias"])
         O.conv3x3_bwd_data(self.dy1, P["conv_blocks.1.weight"], self.dh0, B, 8, 8, 128, 128, 1, 1, wp=self.pk["c1b"])
         O.nhwc_to_nchw(self.dh0, self.dh, B, 128, 64)
         self.l1_wgrad()

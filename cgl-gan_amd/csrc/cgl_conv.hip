@@ -2846,6 +2846,85 @@ struct CglEltArgs {
   double* colsum;
 };
 
+// one float4 of cgl_eltwise mode 1 (the BatchNorm2d backward apply) at element e = (row r, channel c), BatchNorm
+// group g (gc = g C + c), nvr: the data rows of a short first call (cgl_eltwise, cgl_bnb_apply_colsum)
+__device__ __forceinline__ f32x4 cgl_elt_bnb4(const CglEltArgs& a, long e, int r, int c, int g, long gc, int nvr) {
+  const float sl = a.slope;
+  f32x4 o;
+  const f32x4 x = *(gcf4p)(a.X + e), dy = *(gcf4p)(a.dY + e);
+  const f32x4 gm = *(gcf4p)(a.coef0 + gc), kk = *(gcf4p)(a.coef1 + gc);
+  const f32x4 mu = *(gcf4p)(a.mean + gc), is = *(gcf4p)(a.invstd + gc), w = *(gcf4p)(a.gamma + c);
+  f32x4 p = dy;
+  if (a.psc) {
+    const f32x4 ps = *(gcf4p)(a.psc + c), ph = *(gcf4p)(a.psc + a.psc_ld + c);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p[j] = fmaf(x[j], ps[j], ph[j]);
+  } else if (a.post) {
+    p = *(gcf4p)(a.post + e);
+  }
+  const bool pon = a.psc || a.post;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float gg = pon ? (p[j] > 0.f ? dy[j] : dy[j] * sl) : dy[j];
+    o[j] = (gg - gm[j] - (x[j] - mu[j]) * kk[j]) * is[j] * w[j];
+  }
+  if (a.post_out) {
+    const f32x4 po = *(gcf4p)(a.post_out + e);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = po[j] > 0.f ? o[j] : o[j] * sl;
+  }
+  if (a.drop) {
+    const f32x4 dm = *(gcf4p)(a.drop + (long)(r / a.hw) * a.C + c);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] *= dm[j];
+  }
+  if (g == 0 && r + a.row0 >= nvr) o = f32x4{0.f, 0.f, 0.f, 0.f};   // padding of a short first call
+  return o;
+}
+
+// cgl_eltwise mode 1 (the BatchNorm2d backward apply) over 256-row chunks, one per workgroup, that also writes the
+// per-chunk column sums of its output in cgl_chan_reduce4 mode 2's lane mapping, order and layout (R = 256:
+// part[chunk][c] = {sum, 0}) -- bitwise the apply followed by col_sum's channel reduction over the stored output
+// (the bias gradient of the conv whose output gradient this is), one pass over the tensor fewer.  Rows of a lane
+// in batches of NB (their loads in flight together), accumulated in row order.
+template <int NB>
+__global__ __launch_bounds__(256) void cgl_bnb_apply_colsum(CglEltArgs a, double* __restrict__ part) {
+  __shared__ double s0[1024];
+  const int C = a.C, CW = C >> 2, rp = 256 / CW;
+  const int cs = threadIdx.x % CW, rl = threadIdx.x / CW, c = 4 * cs;
+  const int r0 = blockIdx.x * 256, r1 = min(r0 + 256, a.rows);
+  const int nvr = cgl_nv_rows(a.nv, a.hw, a.gr);
+  double x0[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int rb = r0 + rl; rb < r1; rb += NB * rp) {
+    f32x4 o[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int r = min(rb + i * rp, r1 - 1);
+      const int g = (r + a.row0) / a.gr;
+      o[i] = cgl_elt_bnb4(a, (long)r * C + c, r, c, g, (long)g * C + c, nvr);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      if (rb + i * rp < r1) {
+        *(gf4p)(a.out + (long)(rb + i * rp) * C + c) = o[i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x0[j] += (double)o[i][j];
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s0[threadIdx.x * 4 + j] = x0[j];
+  __syncthreads();
+  if (rl == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      double t0 = 0.0, t1 = 0.0;
+      for (int q = 0; q < rp; ++q) t0 += s0[(q * CW + cs) * 4 + j];
+      part[((long)blockIdx.x * C + c + j) * 2] = t0;
+      part[((long)blockIdx.x * C + c + j) * 2 + 1] = t1;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void cgl_eltwise(CglEltArgs a) {
   const long n4 = (long)a.rows * a.C / 4;
   const int C = a.C;
@@ -2878,34 +2957,7 @@ __global__ __launch_bounds__(256) void cgl_eltwise(CglEltArgs a) {
         o[j] = v;
       }
     } else if (a.mode == 1) {
-      const f32x4 x = *(gcf4p)(a.X + e), dy = *(gcf4p)(a.dY + e);
-      const f32x4 gm = *(gcf4p)(a.coef0 + gc), kk = *(gcf4p)(a.coef1 + gc);
-      const f32x4 mu = *(gcf4p)(a.mean + gc), is = *(gcf4p)(a.invstd + gc), w = *(gcf4p)(a.gamma + c);
-      f32x4 p = dy;
-      if (a.psc) {
-        const f32x4 ps = *(gcf4p)(a.psc + c), ph = *(gcf4p)(a.psc + a.psc_ld + c);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) p[j] = fmaf(x[j], ps[j], ph[j]);
-      } else if (a.post) {
-        p = *(gcf4p)(a.post + e);
-      }
-      const bool pon = a.psc || a.post;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float gg = pon ? (p[j] > 0.f ? dy[j] : dy[j] * sl) : dy[j];
-        o[j] = (gg - gm[j] - (x[j] - mu[j]) * kk[j]) * is[j] * w[j];
-      }
-      if (a.post_out) {
-        const f32x4 po = *(gcf4p)(a.post_out + e);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = po[j] > 0.f ? o[j] : o[j] * sl;
-      }
-      if (a.drop) {
-        const f32x4 dm = *(gcf4p)(a.drop + (long)(r / a.hw) * C + c);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] *= dm[j];
-      }
-      if (g == 0 && r + a.row0 >= nvr) o = f32x4{0.f, 0.f, 0.f, 0.f};   // padding of a short first call
+      o = cgl_elt_bnb4(a, e, r, c, g, gc, nvr);
     } else if (a.mode == 2) {
       const f32x4 dy = *(gcf4p)(a.dY + e);
       o = dy;
@@ -4130,6 +4182,15 @@ int64_t cgl_conv3x3_workspace_bytes(int n, int h, int w, int cin, int cout, int 
   return conv_ws_bytes(g);
 }
 
+int cgl_conv3x3_bias_by_colsum(int n, int h, int w, int cin, int cout, int stride, int up) {
+  ConvGeom g;
+  const int rc = conv_geom(n, h, w, cin, cout, stride, up, g);
+  if (rc) return rc;
+  if (c1_ok(g)) return 0;
+  const WgradPlan pl = wgrad_plan(g, true);
+  return (wgrad_bias_col(g, pl.P, pl.np) || !pow2_le256(cout)) ? 0 : 1;
+}
+
 int cgl_conv3x3_fwd(const float* X, const float* W, const float* bias, float* Y, int n, int h, int w, int cin,
                     int cout, int stride, int up, int act, float slope, const float* drop, void* ws, int64_t wsb,
                     void* stream) {
@@ -4595,10 +4656,12 @@ int cgl_bn2d_fwd_stats_coef(const double* part, int R, const float* X, int n, in
 int cgl_bn2d_bwd_stats(const double* part, int R, const float* dY, const float* post, const float* X, int n, int hw,
                        int C, int groups, const float* save_mean, const float* save_invstd, const float* gamma,
                        float slope, const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta,
-                       const float* post_coef, int post_coef_ld, const int* nvalid, void* ws, int64_t wsb,
-                       void* stream) {
+                       const float* post_coef, int post_coef_ld, const int* nvalid, double* colsum_part, void* ws,
+                       int64_t wsb, void* stream) {
   CGL_BATCH_GUARD();
   if (post_coef && (post || groups != 1 || !al16(post_coef) || post_coef_ld % 4)) return CGL_E_ARG;
+  if (colsum_part && (((uintptr_t)colsum_part & 15) || C % 4 || 256 % (C / 4) || ((int64_t)n * hw) % 256))
+    return CGL_E_ARG;
   if (!part || !dY || !X || !save_mean || !save_invstd || !gamma || !dX || !ws || !al16(ws)) return CGL_E_ARG;
   if (!al16(dY) || !al16(X) || !al16(dX) || (post && !al16(post)) || (post_out && !al16(post_out))) return CGL_E_ARG;
   if (!al16(save_mean) || !al16(save_invstd) || !al16(gamma) || (drop && !al16(drop))) return CGL_E_ARG;
@@ -4627,6 +4690,10 @@ int cgl_bn2d_bwd_stats(const double* part, int R, const float* dY, const float* 
   e.gamma = gamma; e.post_out = post_out; e.drop = drop; e.out = dX; e.nv = nvalid;
   e.psc = post_coef; e.psc_ld = post_coef_ld;
   const long n4 = rows * C / 4;
+  if (colsum_part) {   // + the output's column sums per 256-row chunk (a bias gradient's col_sum partials)
+    hipLaunchKernelGGL(cgl_bnb_apply_colsum<4>, dim3((unsigned)(rows / 256)), dim3(256), 0, s, e, colsum_part);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(cgl_eltwise, dim3((unsigned)std::min<long>((n4 + 255) / 256, 8192)), dim3(256), 0, s, e);
   return (int)hipGetLastError();
 }

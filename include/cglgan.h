@@ -453,12 +453,20 @@ int cgl_bn2d_fwd_stats_coef(const double* part, int R, const float* X, int n, in
                             float* running_var, int act, float slope, float* Y, float* save_mean, float* save_invstd,
                             void* scratch, float* coef, int apply_img0, const int* nvalid, void* ws, int64_t wsb,
                             void* stream);
-/* cgl_bn2d_bwd from backward partials already computed (cgl_conv3x3_bwd_data_packed_stats, R = 32). */
+/* 1 when cgl_conv3x3_bwd_weight(_bnin) of this geometry computes its bias gradient by column sums of dY in
+ * 256-row chunks (cgl_bn2d_bwd_stats colsum_part + cgl_colsum_finalize reproduce it bitwise), 0 when its
+ * reduction carries a bias column (or the single-input-channel kernel sums it); < 0 for a bad geometry. */
+int cgl_conv3x3_bias_by_colsum(int n, int h, int w, int cin, int cout, int stride, int up);
+/* cgl_bn2d_bwd from backward partials already computed (cgl_conv3x3_bwd_data_packed_stats, R = 32).
+ * colsum_part (may be null): also the column sums of dX per 256-row chunk, double [n hw / 256][C][2] ({sum, 0}),
+ * in the order of the channel reduction cgl_conv3x3_bwd_weight runs for a bias gradient without a bias column --
+ * cgl_colsum_finalize(colsum_part, n hw / 256, C, db) then gives that bias gradient bitwise, without the pass
+ * over dX.  Needs C % 4 == 0, 256 % (C / 4) == 0, n hw % 256 == 0. */
 int cgl_bn2d_bwd_stats(const double* part, int R, const float* dY, const float* post, const float* X, int n, int hw,
                        int C, int groups, const float* save_mean, const float* save_invstd, const float* gamma,
                        float slope, const float* post_out, const float* drop, float* dX, float* dgamma, float* dbeta,
-                       const float* post_coef, int post_coef_ld, const int* nvalid, void* workspace, int64_t ws_bytes,
-                       void* stream);
+                       const float* post_coef, int post_coef_ld, const int* nvalid, double* colsum_part,
+                       void* workspace, int64_t ws_bytes, void* stream);
 /* post_coef (may be null; then post as above): instead of reading post, take LeakyReLU'(post) from the sign of
  * the forward's fmaf(X, scale, shift) with scale = post_coef[c], shift = post_coef[post_coef_ld + c] (the coef a
  * cgl_bn2d_fwd_stats_coef call kept; its group g of G: post_coef = coef + g C, post_coef_ld = G C).  The forward
