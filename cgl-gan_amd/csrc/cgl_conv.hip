@@ -144,6 +144,9 @@ __device__ __forceinline__ float cgl_bnin_slope(CglKL L) {
   return L->in_act == CGL_EPI_ACT_LEAKY ? L->in_slope : 1.f;
 }
 
+#ifndef CGL_HALO_SB
+#define CGL_HALO_SB 8   // the halo window's staging loads in flight per thread (1: one load, then its store)
+#endif
 template <int TM, int TN, bool FAST, bool BNIN = false, bool HALO = false, bool LDSM = false>
 __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, float* s_red, bool direct = false) {
   constexpr int S = 3;
@@ -407,25 +410,44 @@ __device__ __forceinline__ void cgl_conv_fwd_body(CglKL L, CglKP P, int local, f
       sc0 = *(gcf4p)(L->in_coef + g * Cin + 4 * (tid % c4));
       sh0 = *(gcf4p)(L->in_coef + (L->in_groups + g) * Cin + 4 * (tid % c4));
     }
-    for (int e = tid; e < WR * WC * c4; e += 256) {
-      const int q = e % c4, pix = e / c4;
-      const int wr = pix / WC, wc = pix - wr * WC;
-      const int iy = y0 - 1 + wr, ix = wc - 1;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if ((unsigned)iy < (unsigned)IH && (unsigned)ix < (unsigned)IW) {
-        v = *(gcf4p)(Xi + ((long)iy * XW + ix) * Cin + 4 * q);
-        if constexpr (BNIN) {
-          const f32x4 sc = qfix ? sc0 : *(gcf4p)(L->in_coef + g * Cin + 4 * q);
-          const f32x4 sh = qfix ? sh0 : *(gcf4p)(L->in_coef + (L->in_groups + g) * Cin + 4 * q);
+    // SB staging loads in flight per thread (a load-then-store loop kept ~2 in flight: ~7 serial round trips for
+    // a 57 KB window), then the transform and the LDS stores
+    constexpr int SB = CGL_HALO_SB;
+    const int tot = WR * WC * c4;
+    for (int e0 = tid; e0 < tot; e0 += 256 * SB) {
+      f32x4 v[SB];
+      int okm = 0;
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            float w = fmaf(v[u], sc[u], sh[u]);
-            w = fmaxf(w, w * in_sl);
-            v[u] = w;
-          }
+      for (int u = 0; u < SB; ++u) {
+        const int e = e0 + 256 * u;
+        const int q = e % c4, pix = e / c4;
+        const int wr = pix / WC, wc = pix - wr * WC;
+        const int iy = y0 - 1 + wr, ix = wc - 1;
+        v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (e < tot && (unsigned)iy < (unsigned)IH && (unsigned)ix < (unsigned)IW) {
+          v[u] = *(gcf4p)(Xi + ((long)iy * XW + ix) * Cin + 4 * q);
+          okm |= 1 << u;
         }
       }
-      *(f32x4*)(s_red + pix * CS + 4 * q) = v;
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        const int e = e0 + 256 * u;
+        if (e >= tot) break;
+        const int q = e % c4, pix = e / c4;
+        if constexpr (BNIN) {
+          if ((okm >> u) & 1) {
+            const f32x4 sc = qfix ? sc0 : *(gcf4p)(L->in_coef + g * Cin + 4 * q);
+            const f32x4 sh = qfix ? sh0 : *(gcf4p)(L->in_coef + (L->in_groups + g) * Cin + 4 * q);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              float w = fmaf(v[u][t], sc[t], sh[t]);
+              w = fmaxf(w, w * in_sl);
+              v[u][t] = w;
+            }
+          }
+        }
+        *(f32x4*)(s_red + pix * CS + 4 * q) = v[u];
+      }
     }
     __syncthreads();
     // this lane's window pixel (tap offset 0) per row block

@@ -7,5 +7,6 @@ cd "$(dirname "$0")/../cgl-gan_amd"
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-result -mllvm -amdgpu-kernarg-preload-count=16"
 mkdir -p build lib_$tag
 /opt/rocm/bin/hipcc $FLAGS $defs -c csrc/cgl_conv_tu.hip -o build/cvar_$tag.o
-/opt/rocm/bin/hipcc $FLAGS -shared build/cgl_runtime.o build/cvar_$tag.o -o lib_$tag/libcglgan_hip.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -fPIC -shared build/cgl_runtime.o build/cgl_gemm_p*.o build/cvar_$tag.o \
+  -o lib_$tag/libcglgan_hip.so
 echo "built lib_$tag ($defs)"
