@@ -1931,10 +1931,23 @@ __device__ __forceinline__ void cgl_conv_pack_at(const CGL_AS4 CglPackMultiArgs*
     const int ks = J->ks;
     const float* w = J->W + ((long)co * J->cin + ci) * ks * ks;
     const int ymk = (J->tapm >> (4 * ty)) & 15, xmk = (J->tapm >> (16 + 4 * tx)) & 15;
-    for (int kh = 0; kh < ks; ++kh) {
-      if (!((ymk >> kh) & 1)) continue;
-      for (int kw = 0; kw < ks; ++kw)
-        if ((xmk >> kw) & 1) v += gld(w + kh * ks + kw);
+    if (ks == 3) {
+      // every tap's weight loaded up front (one memory round trip, not one per combined tap), then summed in the
+      // same (kh, kw) order over the combined taps: the same value
+      float wv[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) wv[i] = gld(w + i);
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+          if (((ymk >> kh) & 1) && ((xmk >> kw) & 1)) v += wv[kh * 3 + kw];
+    } else {
+      for (int kh = 0; kh < ks; ++kh) {
+        if (!((ymk >> kh) & 1)) continue;
+        for (int kw = 0; kw < ks; ++kw)
+          if ((xmk >> kw) & 1) v += gld(w + kh * ks + kw);
+      }
     }
   }
   gst(J->dst + local, v);

@@ -46,7 +46,7 @@ for st in "$@"; do
       timeout -k 10 400 python3 -u bench.py --model lsgan --no-cpu-baseline > $O/bench_lsgan.json 2> $O/bench_lsgan.err || exit $? ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
-        python3 $R/bench.py --steps 50 --warmup 10 --no-cpu-baseline --conv-steps 0 > $O/prof.log 2>&1) || exit $? ;;
+        python3 $R/bench.py --steps 50 --warmup 10 --no-cpu-baseline --conv-steps 0 --ring-steps 0 > $O/prof.log 2>&1) || exit $? ;;
     proflsgan)
       # proflsgan:TAG=ENV1,ENV2 profiles under those env settings -> prof_lsgan_TAG/
       d=prof_lsgan; envs=""

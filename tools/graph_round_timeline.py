@@ -24,11 +24,12 @@ def main():
     p.add_argument("--json", default=None)
     p.add_argument("--marker", default="cgl_gemm_pro")
     p.add_argument("--bench", default=None)
+    p.add_argument("--launches", type=int, default=None, help="launches per round (default: the most frequent count)")
     a = p.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     starts = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
     lens = [starts[k + 1] - starts[k] for k in range(len(starts) - 1)]
-    n = S.mode(lens)
+    n = a.launches or S.mode(lens)
     rounds = []
     for k in range(len(starts) - 1):
         i0 = starts[k]
