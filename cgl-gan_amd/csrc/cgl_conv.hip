@@ -2922,6 +2922,9 @@ __device__ __forceinline__ f32x4 cgl_elt_bnb4(const CglEltArgs& a, long e, int r
 // part[chunk][c] = {sum, 0}) -- bitwise the apply followed by col_sum's channel reduction over the stored output
 // (the bias gradient of the conv whose output gradient this is), one pass over the tensor fewer.  Rows of a lane
 // in batches of NB (their loads in flight together), accumulated in row order.
+#ifndef CGL_BNB_NB
+#define CGL_BNB_NB 4   // rows of a lane in flight together (16 measured the same, gpurun_out/r06zg)
+#endif
 template <int NB>
 __global__ __launch_bounds__(256) void cgl_bnb_apply_colsum(CglEltArgs a, double* __restrict__ part) {
   __shared__ double s0[1024];
@@ -4726,7 +4729,7 @@ int cgl_bn2d_bwd_stats(const double* part, int R, const float* dY, const float* 
   e.psc = post_coef; e.psc_ld = post_coef_ld;
   const long n4 = rows * C / 4;
   if (colsum_part) {   // + the output's column sums per 256-row chunk (a bias gradient's col_sum partials)
-    hipLaunchKernelGGL(cgl_bnb_apply_colsum<4>, dim3((unsigned)(rows / 256)), dim3(256), 0, s, e, colsum_part);
+    hipLaunchKernelGGL(cgl_bnb_apply_colsum<CGL_BNB_NB>, dim3((unsigned)(rows / 256)), dim3(256), 0, s, e, colsum_part);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(cgl_eltwise, dim3((unsigned)std::min<long>((n4 + 255) / 256, 8192)), dim3(256), 0, s, e);
