@@ -56,7 +56,7 @@ for st in "$@"; do
     traffic)
       for c in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && export TMPDIR=/tmp CGL_PLAN_DEBUG=1 && timeout -s KILL 150 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/mlp_$c -o run -- \
-          python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --conv-steps 0 > $O/mlp_$c.log 2>&1) || exit $?
+          python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --conv-steps 0 --ring-steps 0 > $O/mlp_$c.log 2>&1) || exit $?
       done ;;
     trafficlsgan)
       for c in FETCH_SIZE WRITE_SIZE; do
