@@ -2,8 +2,11 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/gemm_bench.hip -o tools/gemm_bench && tools/gemm_bench
 // Prints, per shape and wave arrangement (WM,WN,WK), the mean device time of back-to-back
 // launches (hipEvent over 200 launches) and the achieved fp32 TFLOP/s.
+#define CGL_GEMM_PART_TU 1   // (device functions of cgl_kernels.hip only: the deferred head finish)
 #include "../cgl-gan_amd/csrc/cgl_gemm.hip"
+#include "../cgl-gan_amd/csrc/cgl_kernels.hip"
 
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -35,16 +38,19 @@ static double time_desc(CglGemmDesc d, CglGemmDesc* dd, int reps) {
   (void)hipMemcpy(dd, &d, sizeof(d), hipMemcpyHostToDevice);
   const int grid = cgl_gemm_wgs(d);
   const int sh = cgl_gemm_stage_bytes(d);
+  // one problem: no second / third problem, its layout and vector flags as the selection, no deferred head,
+  // no next-launch descriptor warm-up
+  const int meta = d.layout | ((d.a_vec && d.b_vec) ? 4 : 0);
   auto go = [&]() {
     if (d.ksplit > 1) {
       if (d.TM == 2)
-        cgl_gemm_f32<2, 2, true><<<grid, 256, sh, 0>>>(dd, 1);
+        cgl_gemm_f32<2, 2, true><<<grid, 256, sh, 0>>>(dd, INT_MAX, INT_MAX, meta, 0, nullptr, 0);
       else
-        cgl_gemm_f32<1, 1, true><<<grid, 256, sh, 0>>>(dd, 1);
+        cgl_gemm_f32<1, 1, true><<<grid, 256, sh, 0>>>(dd, INT_MAX, INT_MAX, meta, 0, nullptr, 0);
     } else if (d.TM == 2) {
-      cgl_gemm_f32<2, 2><<<grid, 256, sh, 0>>>(dd, 1);
+      cgl_gemm_f32<2, 2><<<grid, 256, sh, 0>>>(dd, INT_MAX, INT_MAX, meta, 0, nullptr, 0);
     } else {
-      cgl_gemm_f32<1, 1><<<grid, 256, sh, 0>>>(dd, 1);
+      cgl_gemm_f32<1, 1><<<grid, 256, sh, 0>>>(dd, INT_MAX, INT_MAX, meta, 0, nullptr, 0);
     }
   };
   for (int i = 0; i < 10; ++i) go();
