@@ -158,7 +158,7 @@ def traffic_per_gemm_launch():
     newest committed FETCH_SIZE / WRITE_SIZE passes (tools/gpu_session.sh traffic -> tools/pmc_traffic.py).
     A static, labelled measurement: PMC passes cannot run inside the timed bench, so roofline.traffic
     names the profile file and the commit it was measured at (traffic_source).  None when absent."""
-    name, d = _latest_profile(["r05_traffic.json", "r04_traffic.json", "r03_traffic.json", "r02_traffic.json"])
+    name, d = _latest_profile(["r06_traffic.json", "r05_traffic.json", "r04_traffic.json", "r03_traffic.json", "r02_traffic.json"])
     if d is None:
         return None, None
     src = {"file": f"profiles/{name}", "commit": (d.get("_meta") or {}).get("commit"),
@@ -176,7 +176,7 @@ def traffic_per_launch():
     """Per-launch PMC traffic of the round's GEMM launches against each launch's own compulsory bytes
     (A + B + C of its descriptors, f32), from the newest committed per-launch pass (tools/pmc_traffic.py
     --plan): [{"i": position in the round, "bytes", "algorithmic", "ratio"}], plus the launch-summed ratio."""
-    name, d = _latest_profile(["r05_traffic.json", "r04_traffic.json"])
+    name, d = _latest_profile(["r06_traffic.json", "r05_traffic.json", "r04_traffic.json"])
     if not d or "per_launch" not in d:
         return {}
     rows = [{"i": e["i"], "kernel": e["kernel"].split("<")[0], "bytes": round(e["bytes"]),
