@@ -371,7 +371,7 @@ def conv_cpu_baseline(a, threads=None):
 def conv_traffic():
     """HBM-side traffic of the dominant conv op per dispatch from the newest committed PMC passes
     (tools/conv_traffic.py: FETCH_SIZE x2 + WRITE_SIZE; None when absent), labelled with its source."""
-    name, p = _latest_profile(["r04_conv_dominant_traffic.json", "r03_conv_dominant_traffic.json",
+    name, p = _latest_profile(["r06_conv_dominant_traffic.json", "r04_conv_dominant_traffic.json", "r03_conv_dominant_traffic.json",
                                "r02_conv_dominant_traffic.json"])
     if p is None:
         return {"traffic": None}
