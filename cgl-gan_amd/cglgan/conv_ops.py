@@ -223,11 +223,11 @@ def conv3x3_bwd_weight(dy, x, dw, db, n, h, wd, cin, cout, stride=1, up=0, bn_in
     gradient at the block's output, the LeakyReLU + Dropout2d backward applied per loaded value
     (cgl_conv3x3_bwd_weight_actdrop, bitwise act_drop_bwd + this).  ``ws``: a uint8 workspace of its own
     (inside wgrad_defer: the deferred reduction reads its partials from it), else the stream's shared one."""
+    if ws is None and _WDEFER:
+        raise RuntimeError("conv3x3_bwd_weight inside wgrad_defer: pass a workspace of its own (ws=)")
     _chk(dy, x, dw, db)
     need = conv_ws_bytes(n, h, wd, cin, cout, stride, up)
     if ws is None:
-        if _WDEFER:
-            raise RuntimeError("conv3x3_bwd_weight inside wgrad_defer: pass a workspace of its own (ws=)")
         ws = workspace(need, dy.device)
     elif ws.numel() < need or ws.dtype != torch.uint8:
         raise RuntimeError(f"conv3x3_bwd_weight: workspace of {need} bytes (uint8) needed")

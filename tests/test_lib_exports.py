@@ -160,6 +160,30 @@ def test_open_launch_batch_refuses_other_launches():
     assert lib.cgl_gather_rows(None, None, 0, 1, 4, None, None) == E_ARG
 
 
+def test_wgrad_defer_state():
+    """cgl_conv_wgrad_defer_begin / _end (round 6): a nested begin and an end without begin return CGL_E_STATE; an
+    empty batch launches nothing (so this runs on CPU); and the Python wrapper refuses a weight gradient without a
+    workspace of its own inside the block (its partials would be overwritten before the deferred reduction)."""
+    import torch
+    from cglgan import conv_ops as O
+    E_STATE = -2
+    lib = C.lib
+    assert lib.cgl_conv_wgrad_defer_end(None) == E_STATE
+    assert lib.cgl_conv_wgrad_defer_begin() == 0
+    try:
+        assert lib.cgl_conv_wgrad_defer_begin() == E_STATE
+    finally:
+        assert lib.cgl_conv_wgrad_defer_end(None) == 0
+    assert lib.cgl_conv_wgrad_defer_end(None) == E_STATE
+    O._WDEFER = True          # (the wrapper's check runs before any device work)
+    try:
+        t = torch.empty(0)
+        with pytest.raises(RuntimeError, match="of its own"):
+            O.conv3x3_bwd_weight(t, t, t, None, 1, 4, 4, 4, 4)
+    finally:
+        O._WDEFER = False
+
+
 def test_one_hip_runtime_whatever_the_import_order():
     """Importing cglgan before torch must not map a second HIP runtime: the library has to bind to torch's
     libamdhip64 (one device context, torch's streams, graph capture).  Round 5 found the GPU suite failing
