@@ -36,7 +36,7 @@ EXPORTS = [
     "cgl_dense_fwd", "cgl_dense_bwd_data", "cgl_dense_bwd_weight", "cgl_gather_rows", "cgl_weights_scale",
     "cgl_conv_packed_floats", "cgl_conv_pack_multi", "cgl_conv_batch_begin", "cgl_conv_batch_end", "cgl_conv_wgrad_defer_begin", "cgl_conv_wgrad_defer_end", "cgl_conv3x3_bias_by_colsum", "cgl_conv3x3_fwd_packed", "cgl_conv3x3_bwd_data_packed",
     "cgl_dense_fwd_packed", "cgl_dense_bwd_data_packed", "cgl_conv3x3_stat_chunks", "cgl_conv3x3_fwd_packed_stats",
-    "cgl_bn2d_fwd_stats", "cgl_bn2d_fwd_stats_coef", "cgl_conv3x3_fwd_packed_bnin", "cgl_bn2d_stats_scratch_bytes", "cgl_linear_desc_bytes", "cgl_linear_prepare",
+    "cgl_bn2d_fwd_stats", "cgl_bn2d_fwd_stats_coef", "cgl_conv3x3_fwd_packed_bnin", "cgl_bn2d_stats_scratch_bytes", "cgl_linear_desc_bytes", "cgl_linear_prepare", "cgl_linear_prepare_gather", "cgl_linear_prepare_wgrad_nhwc",
     "cgl_linear_launch", "cgl_conv3x3_bwd_stat_chunks", "cgl_conv3x3_bwd_data_packed_stats", "cgl_conv3x3_bwd_data_stats", "cgl_bn2d_bwd_stats",
     "cgl_normal_fill_dev", "cgl_dropout2d_masks_dev", "cgl_adam_multi_dev", "cgl_sample_rows_dev", "cgl_counters_add",
     # evaluation (CGLGAN/2DMG/main.py plot_2d KL score)
@@ -201,6 +201,8 @@ def _load():
         "cgl_bn2d_bwd_stats": (ci, [vp, ci, vp, vp, vp, ci, ci, ci, ci, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, ci, vp,
                                     vp, vp, i64, vp]),
         "cgl_linear_prepare": (ci, [ci, vp, vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, P(LinearLaunch)]),
+        "cgl_linear_prepare_gather": (ci, [vp, vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, P(LinearLaunch)]),
+        "cgl_linear_prepare_wgrad_nhwc": (ci, [vp, vp, vp, vp, ci, ci, ci, ci, vp, P(LinearLaunch)]),
         "cgl_linear_launch": (ci, [vp, P(LinearLaunch), vp]),
         "cgl_dense_fwd_packed": (ci, [vp, vp, vp, vp, ci, ci, ci, ci, cf, vp, i64, vp]),
         "cgl_dense_bwd_data_packed": (ci, [vp, vp, vp, ci, ci, ci, vp, i64, vp]),

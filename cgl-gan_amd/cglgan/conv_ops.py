@@ -293,11 +293,29 @@ class PreparedLinear:
     fused-MLP GEMM kernel (cgl_linear_prepare) and launched stream-ordered, capturable, without a
     descriptor upload: the operand tensors given here are the ones every launch reads."""
 
-    def __init__(self, op, a, b, bias, c, db, M, N, K, act=ACT_NONE, slope=0.2):
+    def __init__(self, op, a, b, bias, c, db, M, N, K, act=ACT_NONE, slope=0.2, b_rows=None, nhwc=None):
         _chk(a, b, bias, c, db)
-        self._keep = (a, b, bias, c, db)
+        self._keep = (a, b, bias, c, db, b_rows)
         self.desc = torch.zeros(int(C.lib.cgl_linear_desc_bytes()), dtype=torch.uint8, device=a.device)
         self.launch = C.LinearLaunch()
+        if nhwc is not None:     # op 2 with A an NHWC [M][HW][C] gradient (cgl_linear_prepare_wgrad_nhwc)
+            ch, hw = nhwc
+            if op != 2 or bias is not None or ch * hw != N or act != ACT_NONE or b_rows is not None:
+                raise ValueError("PreparedLinear: nhwc=(C, HW) is for op 2 with N = C * HW")
+            C.check(C.lib.cgl_linear_prepare_wgrad_nhwc(_p(a), _p(b), _p(c), _p(db), M, ch, hw, K, _p(self.desc),
+                                                        ctypes.byref(self.launch)), "cgl_linear_prepare_wgrad_nhwc")
+            return
+        if b_rows is not None:   # op 0 with gathered B rows (cgl_linear_prepare_gather)
+            if op != 0 or db is not None:
+                raise ValueError("PreparedLinear: b_rows is for op 0 only")
+            if b_rows.dtype != torch.int32 or b_rows.numel() != N or not b_rows.is_contiguous():
+                raise ValueError("PreparedLinear: b_rows must be a contiguous int32 tensor of N row indices")
+            if int(b_rows.min()) < 0 or int(b_rows.max()) >= b.numel() // K:
+                raise ValueError("PreparedLinear: b_rows index outside B's rows")
+            C.check(C.lib.cgl_linear_prepare_gather(_p(a), _p(b), _p(b_rows), _p(bias), _p(c), M, N, K, act,
+                                                    float(slope), _p(self.desc), ctypes.byref(self.launch)),
+                    "cgl_linear_prepare_gather")
+            return
         C.check(C.lib.cgl_linear_prepare(int(op), _p(a), _p(b), _p(bias), _p(c), _p(db), M, N, K, act, float(slope),
                                          _p(self.desc), ctypes.byref(self.launch)), "cgl_linear_prepare")
 

@@ -211,6 +211,13 @@ class ConvGanStep:
         pk.add("G", "c5f", PG["conv_blocks.5.weight"], 16, 16, 128, 64, 1, 1)
         pk.add("G", "c5b", PG["conv_blocks.5.weight"], 16, 16, 128, 64, 1, 1, dir=1)
         pk.add("G", "c8f", PG["conv_blocks.8.weight"], 32, 32, 64, 1, 1, 0)
+        # the Linear(100, 8192) works on the NHWC activation directly (CGL_CONV_L1NHWC): forward output column
+        # n = hw * 128 + c gathers W row c * 64 + hw, and its bias is packed in that order with the G operands
+        # (the 1x1 input-gradient pack of a [128][64] "weight" is its transpose); the weight gradient reads the
+        # NHWC gradient and stores its rows in the reference's order -- no transpose launch either way
+        self.l1nhwc = os.environ.get("CGL_CONV_L1NHWC", "1") != "0"
+        if self.l1nhwc:
+            pk.add("G", "l1b", PG["l1.0.bias"], 1, 1, 64, 128, 1, 0, ks=1, dir=1)
         for ck, _, ci, co, hw in D_CONVS:
             pk.add("D", ck + "f", PD[ck + ".weight"], hw, hw, ci, co, 2, 0)
             pk.add("D", ck + "b", PD[ck + ".weight"], hw, hw, ci, co, 2, 0, dir=1)
@@ -218,8 +225,19 @@ class ConvGanStep:
         # G's nn.Linear(100, 8192) (model/lsgan.py:8) on the fused-MLP GEMM kernel, prepared once:
         # forward on [z1; z2] and its weight + bias gradient on the z2 rows
         GG = self.G.grads
-        self.l1_fwd = O.PreparedLinear(0, self.z, PG["l1.0.weight"], PG["l1.0.bias"], self.h, None, B2, 8192, 100)
-        self.l1_wgrad = O.PreparedLinear(2, self.dh, self.z[B:], None, GG["l1.0.weight"], GG["l1.0.bias"], B, 8192, 100)
+        if self.l1nhwc:
+            n = torch.arange(8192, dtype=torch.int32, device=dev)
+            self.l1_rows = ((n % 128) * 64 + n // 128).to(torch.int32).contiguous()
+            self.l1_fwd = O.PreparedLinear(0, self.z, PG["l1.0.weight"], self.pk["l1b"], self.h0, None, B2, 8192, 100,
+                                           b_rows=self.l1_rows)
+        else:
+            self.l1_fwd = O.PreparedLinear(0, self.z, PG["l1.0.weight"], PG["l1.0.bias"], self.h, None, B2, 8192, 100)
+        if self.l1nhwc:   # its weight + bias gradient read the NHWC gradient dh0 (output rows permuted at the store)
+            self.l1_wgrad = O.PreparedLinear(2, self.dh0, self.z[B:], None, GG["l1.0.weight"], GG["l1.0.bias"], B, 8192,
+                                             100, nhwc=(128, 64))
+        else:
+            self.l1_wgrad = O.PreparedLinear(2, self.dh, self.z[B:], None, GG["l1.0.weight"], GG["l1.0.bias"], B, 8192,
+                                             100)
         # BatchNorm2d statistics written by the producing conv's epilogue (cgl_conv3x3_fwd_packed_stats):
         # one float64 partial buffer per BatchNorm, sized for its largest call (the D step's 2B rows)
         sc = lambda n, h, ci, co, st, up, grp: O.stat_chunks(n, h, h, ci, co, st, up, grp)
@@ -404,7 +422,8 @@ class ConvGanStep:
     def _g_forward(self):
         P, B2 = self.G.params, 2 * self.B
         self.l1_fwd()
-        O.nchw_to_nhwc(self.h, self.h0, B2, 128, 64)      # out.view(B, 128, 8, 8), model/lsgan.py:25
+        if not self.l1nhwc:
+            O.nchw_to_nhwc(self.h, self.h0, B2, 128, 64)      # out.view(B, 128, 8, 8), model/lsgan.py:25
         O.conv3x3_fwd(self.h0, P["conv_blocks.1.weight"], P["conv_blocks.1.bias"], self.y1, B2, 8, 8, 128, 128, 1, 1,
                       wp=self.pk["c1f"], stats=self._stats("conv_blocks.2", 2))
         # BatchNorm2d + LeakyReLU of y1 (bit 0) / y2 (bit 1) folded into the next conv's operand load (the finalize
@@ -661,7 +680,8 @@ class ConvGanStep:
         if c2:
             O.colsum_finalize(self.bcs["conv_blocks.2"], B * 256 // 256, 128, G["conv_blocks.1.bias"])
         O.conv3x3_bwd_data(self.dy1, P["conv_blocks.1.weight"], self.dh0, B, 8, 8, 128, 128, 1, 1, wp=self.pk["c1b"])
-        O.nhwc_to_nchw(self.dh0, self.dh, B, 128, 64)
+        if not self.l1nhwc:
+            O.nhwc_to_nchw(self.dh0, self.dh, B, 128, 64)
         self.l1_wgrad()
 
     # ------------------------------------------------------------------ round

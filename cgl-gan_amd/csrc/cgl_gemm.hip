@@ -350,6 +350,11 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   const CglRowSrc h_a = d->a, h_b = d->b;
   // the epilogue's fields too (they would otherwise cost one more scalar round trip after the k-loop)
   const int e_act = d->act, e_ldc = d->ldc, e_gr = d->stat_gr;
+#ifndef CGL_GEMM_NO_CPERM
+  const int e_cperm = d->c_perm;
+#else
+  const int e_cperm = 0;     // (A/B builds: the output-row permutation compiled out)
+#endif
   const float e_slope = d->slope;
   float* const e_C = d->C;
   float* const e_bout = d->bias_out;
@@ -360,7 +365,8 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("" ::"s"(M), "s"(N), "s"(K), "s"(WN), "s"(WK), "s"(WM), "s"(h_tm), "s"(h_tn), "s"(h_wg0), "s"(h_ks),
                "s"(h_xcd), "s"(h_tab), "s"(h_gen), "s"(h_abn), "s"(h_ones), "s"(h_apk), "s"(h_bpk));
-  asm volatile("" ::"s"(e_act), "s"(e_ldc), "s"(e_gr), "s"(e_slope), "s"(e_C), "s"(e_bout), "s"(e_stat), "s"(e_bnb));
+  asm volatile("" ::"s"(e_act), "s"(e_ldc), "s"(e_gr), "s"(e_slope), "s"(e_C), "s"(e_bout), "s"(e_stat), "s"(e_bnb),
+               "s"(e_cperm));
   asm volatile("" ::"s"(h_bias), "s"(h_mref), "s"(h_tref), "s"(h_mld), "s"(h_tld), "s"(h_crow0), "s"(h_copy),
                "s"(h_a.p0), "s"(h_a.p1), "s"(h_a.idx0), "s"(h_a.idx_off), "s"(h_a.split), "s"(h_a.ld), "s"(h_b.p0),
                "s"(h_b.p1), "s"(h_b.idx0), "s"(h_b.idx_off), "s"(h_b.split), "s"(h_b.ld));
@@ -955,6 +961,9 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 
   // the tile's stores first: they drain while the BatchNorm partials below are reduced (the partials only
   // read the accumulators)
+  // (stored row of result row r: ((r & pmask) << pq) + (r >> pl); the identity without a permutation)
+  const int pl = e_cperm ? (e_cperm & 255) : 31, pq = e_cperm ? (e_cperm >> 8) : 0;
+  const int pmask = e_cperm ? (1 << pl) - 1 : 0x7fffffff;
   if (owner) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -969,7 +978,7 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
-              if (row < M) gst(e_bout + row, v[r]);
+              if (row < M) gst(e_bout + (((row & pmask) << pq) + (row >> pl)), v[r]);
             }
             if constexpr (ADAM) cgl_epi_adam(d, d->ad_pb, d->ad_mb, d->ad_vb, rbase + 32 * i, M, 0, 1, v);
           }
@@ -978,17 +987,19 @@ __device__ __forceinline__ void cgl_gemm_body(const CglGemmDesc* __restrict__ d,
           const int ldc = e_ldc;
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int row = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
+            const int row0 = rbase + 32 * i + (r & 3) + 8 * (r >> 2);
+            const bool rok = row0 < M;
+            const int row = ((row0 & pmask) << pq) + (row0 >> pl);
 #ifndef CGL_C_STORE_WB
             // write-through (agent-scope) output stores: no dirty C lines are left in the XCD's L2 for the
             // end-of-kernel write-back, and the next launch (on any XCD) reads them from MALL either way.
             // Measured -1.0 us per B = 256 round, interleaved x3 twice (profiles/r04_store_wt_ab.txt); making
             // every plain store write-through (CGL_GST_WT) gave nothing.  -DCGL_C_STORE_WB: plain stores.
-            if (row < M)
+            if (rok)
               __hip_atomic_store((CGL_GLOBAL float*)(C + (long)row * ldc + col), v[r], __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
 #else
-            if (row < M) gst(C + (long)row * ldc + col, v[r]);
+            if (rok) gst(C + (long)row * ldc + col, v[r]);
 #endif
           }
           if constexpr (ADAM) cgl_epi_adam(d, d->ad_p, d->ad_m, d->ad_v, rbase + 32 * i, M, col, ldc, v);

@@ -139,6 +139,10 @@ struct CglGemmDesc {
   const float* tanh_ref; int tanh_ld;     // v *= 1 - t*t
   float* stat_part; int stat_gr;          // forward BatchNorm partials of the stored output
   float* bias_out;                     // with b_ones_col: column N-1 of C goes here
+  // output row permutation (0: none): with lp = c_perm & 255, lq = c_perm >> 8, row r of the result is stored as
+  // row ((r & (2^lp - 1)) << lq) + (r >> lp) of C (and of bias_out) -- the NHWC -> NCHW feature order of a weight
+  // gradient whose A operand is an NHWC activation gradient (cgl_linear_prepare_wgrad_nhwc); plain stores only
+  int c_perm;
   // cross-workgroup split-K (ksplit > 1): the K range is cut into ksplit slices, one workgroup per
   // (tile, slice); every slice stores its tile partial write-through (sc1) to kpart, the workgroup
   // that draws the last ticket of kcount[tile] sums the partials in slice order (deterministic),

@@ -2533,17 +2533,20 @@ int cgl_linear_bwd_weight(const float* dY, const float* X, float* dW, float* db,
 // and no stream synchronisation, unlike the cgl_linear_* ops above.
 int64_t cgl_linear_desc_bytes(void) { return (int64_t)((sizeof(CglGemmDesc) + 255) & ~size_t(255)); }
 
-int cgl_linear_prepare(int op, const float* A, const float* B, const float* bias, float* C, float* db, int M, int N,
-                       int K, int act, float slope, void* desc, CglLinearLaunch* launch) {
-  CGL_BATCH_GUARD();
+}  // extern "C"
+namespace {
+int linear_prepare(int op, const float* A, const float* B, const int* b_rows, const float* bias, float* C, float* db,
+                   int M, int N, int K, int act, float slope, void* desc, CglLinearLaunch* launch, int c_perm = 0) {
   if (!A || !B || !C || !desc || !launch || M < 1 || N < 1 || K < 1 || act < 0 || act > 3 || !al16(desc))
     return CGL_E_ARG;
+  if ((b_rows && op != 0) || (c_perm && op != 2)) return CGL_E_ARG;
   CglGemmDesc d;
   if (op == 0) {            // Y[M][N] = act(X[M][K] W[N][K]^T + b)
     d = make_gemm(0, M, N, K);
     d.a = rows(A, K);
     d.a_vec = (K % 4 == 0) && al16(A);
     d.b = rows(B, K);
+    d.b.idx0 = b_rows;      // (gathered W rows: output column n is W row b_rows[n])
     d.b_vec = (K % 4 == 0) && al16(B);
     d.bias = bias;
     d.act = act;
@@ -2565,6 +2568,7 @@ int cgl_linear_prepare(int op, const float* A, const float* B, const float* bias
     d.C = C;
     d.ldc = K;
     d.bias_out = db;
+    d.c_perm = c_perm;
   } else {
     return CGL_E_ARG;
   }
@@ -2581,6 +2585,30 @@ int cgl_linear_prepare(int op, const float* A, const float* B, const float* bias
   launch->shmem = cgl_gemm_stage_bytes(d);
   launch->flags = 0x100 | d.layout | ((d.a_vec && d.b_vec) ? 4 : 0);   // the kernel's problem selection (CglGemmSel)
   return 0;
+}
+}  // namespace
+extern "C" {
+
+int cgl_linear_prepare(int op, const float* A, const float* B, const float* bias, float* C, float* db, int M, int N,
+                       int K, int act, float slope, void* desc, CglLinearLaunch* launch) {
+  CGL_BATCH_GUARD();
+  return linear_prepare(op, A, B, nullptr, bias, C, db, M, N, K, act, slope, desc, launch);
+}
+
+int cgl_linear_prepare_wgrad_nhwc(const float* dY, const float* X, float* dW, float* db, int M, int C, int HW, int K,
+                                  void* desc, CglLinearLaunch* launch) {
+  CGL_BATCH_GUARD();
+  auto lg = [](int v) { return (v >= 2 && v <= (1 << 16) && (v & (v - 1)) == 0) ? __builtin_ctz(v) : -1; };
+  const int lc = lg(C), lh = HW == 1 ? 0 : lg(HW);
+  if (lc < 0 || lh < 0) return CGL_E_ARG;
+  return linear_prepare(2, dY, X, nullptr, nullptr, dW, db, M, C * HW, K, 0, 0.f, desc, launch, lc | lh << 8);
+}
+
+int cgl_linear_prepare_gather(const float* X, const float* W, const int* w_rows, const float* bias, float* Y, int M,
+                              int N, int K, int act, float slope, void* desc, CglLinearLaunch* launch) {
+  CGL_BATCH_GUARD();
+  if (!w_rows) return CGL_E_ARG;
+  return linear_prepare(0, X, W, w_rows, bias, Y, nullptr, M, N, K, act, slope, desc, launch);
 }
 
 int cgl_linear_launch(const void* desc, const CglLinearLaunch* launch, void* stream) {

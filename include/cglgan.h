@@ -267,6 +267,19 @@ int64_t cgl_linear_desc_bytes(void);
 int cgl_linear_prepare(int op, const float* A, const float* B, const float* bias, float* C, float* db, int M, int N,
                        int K, int act, float slope, void* desc, CglLinearLaunch* launch);
 int cgl_linear_launch(const void* desc, const CglLinearLaunch* launch, void* stream);
+/* op 0 with gathered weight rows: Y[M][N] = act(X[M][K] W[w_rows[n]][:]^T + bias[n]); w_rows is a device
+ * int array of N row indices, each a valid row of W (read at every launch, not checked there).  The conv
+ * round's Linear(100, 8192) uses it with the NCHW -> NHWC feature permutation (and the bias packed in the
+ * same order), so its output is the NHWC activation of out.view(B, 128, 8, 8) (model/lsgan.py:25)
+ * directly, bit for bit the plain op 0 output transposed. */
+int cgl_linear_prepare_gather(const float* X, const float* W, const int* w_rows, const float* bias, float* Y, int M,
+                              int N, int K, int act, float slope, void* desc, CglLinearLaunch* launch);
+/* op 2 on an NHWC activation gradient: dW[c * HW + p][k] = sum_m dY[m][p][c] X[m][k] and db[c * HW + p] =
+ * sum_m dY[m][p][c] (db may be null), dY [M][HW][C] -- the reference's NCHW feature order in dW / db, read
+ * straight from the NHWC tensor (the GEMM's output rows are permuted at the store); C and HW powers of two
+ * (C >= 2).  Bit for bit op 2 on the NCHW transpose of dY. */
+int cgl_linear_prepare_wgrad_nhwc(const float* dY, const float* X, float* dW, float* db, int M, int C, int HW, int K,
+                                  void* desc, CglLinearLaunch* launch);
 
 /* ---------------- conv GAN ops (model/lsgan.py) ----------------
  * Activations are NHWC (torch channels_last memory of the reference's NCHW tensors); weights are

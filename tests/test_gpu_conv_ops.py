@@ -292,6 +292,51 @@ def test_layout_and_gather():
     assert torch.equal(dst, src[10:14])
 
 
+@pytest.mark.parametrize("M", [16, 512])
+def test_linear_gather_nhwc(M):
+    """cgl_linear_prepare_gather with the conv round's NCHW -> NHWC feature permutation (model/lsgan.py:23-25):
+    bit for bit the plain prepared Linear's output transposed to NHWC, and close to the fp64 torch Linear;
+    the bias packed in that order by the 1x1 input-gradient pack (PackSet dir 1) is its exact transpose.
+    cgl_linear_prepare_wgrad_nhwc: the weight / bias gradient of the same Linear from an NHWC gradient."""
+    O = ops()
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = torch.randn(M, 100, device=DEV, generator=g)
+    w = torch.randn(8192, 100, device=DEV, generator=g) * 0.1
+    b = torch.randn(8192, device=DEV, generator=g)
+    ps = O.PackSet()
+    ps.add("G", "l1b", b, 1, 1, 64, 128, 1, 0, ks=1, dir=1)
+    ps = ps.finalize(torch.device(DEV))
+    ps.run()
+    n = torch.arange(8192, dtype=torch.int32, device=DEV)
+    rows = ((n % 128) * 64 + n // 128).to(torch.int32).contiguous()
+    y0 = torch.empty(M, 8192, device=DEV)
+    y1 = torch.empty(M, 8, 8, 128, device=DEV)
+    O.PreparedLinear(0, x, w, b, y0, None, M, 8192, 100)()
+    O.PreparedLinear(0, x, w, ps["l1b"], y1, None, M, 8192, 100, b_rows=rows)()
+    torch.cuda.synchronize()
+    assert torch.equal(ps["l1b"].view(64, 128), b.view(128, 64).t())
+    assert torch.equal(y1, y0.view(M, 128, 8, 8).permute(0, 2, 3, 1))
+    ref = (x.double() @ w.double().t() + b.double()).view(M, 128, 8, 8).permute(0, 2, 3, 1)
+    assert (y1.double() - ref).abs().max() <= 2e-5 * ref.abs().max()
+    with pytest.raises(ValueError):
+        O.PreparedLinear(0, x, w, b, y1, None, M, 8192, 100, b_rows=rows + 8192)
+    # the weight + bias gradient from the NHWC gradient (cgl_linear_prepare_wgrad_nhwc): bit for bit op 2 on
+    # the NCHW transpose, close to fp64
+    dy = torch.randn(M, 8, 8, 128, device=DEV, generator=g)
+    dyc = dy.permute(0, 3, 1, 2).contiguous().view(M, 8192)
+    dw0, db0 = torch.empty(8192, 100, device=DEV), torch.empty(8192, device=DEV)
+    dw1, db1 = torch.full((8192, 100), float("nan"), device=DEV), torch.full((8192,), float("nan"), device=DEV)
+    O.PreparedLinear(2, dyc, x, None, dw0, db0, M, 8192, 100)()
+    O.PreparedLinear(2, dy, x, None, dw1, db1, M, 8192, 100, nhwc=(128, 64))()
+    torch.cuda.synchronize()
+    assert torch.equal(dw1, dw0) and torch.equal(db1, db0)
+    rw = dyc.double().t() @ x.double()
+    assert (dw1.double() - rw).abs().max() <= 2e-5 * rw.abs().max()
+    assert (db1.double() - dyc.double().sum(0)).abs().max() <= 2e-5 * dyc.double().sum(0).abs().max()
+    with pytest.raises(ValueError):
+        O.PreparedLinear(2, dy, x, None, dw1, db1, M, 8192, 100, nhwc=(128, 32))
+
+
 def test_adam_multi_matches_torch_single_tensor():
     O = ops()
     from oracle.gan_oracle import Adam

@@ -246,6 +246,7 @@ int main(int argc, char** argv) {
       {"G1 dA", 1, 256, 128, 256},   {"D gV1", 2, 256, 513, 512},   {"D gV0", 2, 512, 785, 512},
       {"G gW4", 2, 784, 1025, 256},  {"G gW3", 2, 1024, 513, 256},  {"G gW2", 2, 512, 257, 256},
       {"G gW1", 2, 256, 129, 256},   {"G gW0", 2, 128, 101, 256},
+      {"L1 conv", 0, 512, 8192, 100},   // (index 23: the conv round's Linear(100, 8192) on [z1; z2])
   };
   const int cfgs[8][4] = {{2, 2, 1, 1}, {2, 1, 2, 1}, {1, 2, 2, 1}, {1, 1, 4, 1},
                           {2, 2, 1, 2}, {2, 1, 2, 2}, {1, 2, 2, 2}, {1, 1, 4, 2}};
@@ -262,12 +263,12 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&A, big * 4));
   CK(hipMalloc(&B, big * 4));
   CK(hipMalloc(&C, big * 4));
-  CK(hipMalloc(&bias, 4096 * 4));
+  CK(hipMalloc(&bias, 16384 * 4));
   std::vector<float> h(big);
   for (size_t i = 0; i < big; ++i) h[i] = (float)((i * 2654435761u) % 2001) / 1000.f - 1.f;
   CK(hipMemcpy(A, h.data(), big * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(B, h.data(), big * 4, hipMemcpyHostToDevice));
-  CK(hipMemset(bias, 0, 4096 * 4));
+  CK(hipMemset(bias, 0, 16384 * 4));
   CglGemmDesc* dd;
   CK(hipMalloc(&dd, sizeof(CglGemmDesc)));
   hipEvent_t e0, e1;
