@@ -34,7 +34,7 @@ EXPORTS = [
     "cgl_bn2d_workspace_bytes", "cgl_bn2d_fwd", "cgl_bn2d_bwd", "cgl_act_drop_bwd", "cgl_act_drop_bwd_colsum", "cgl_colsum_finalize", "cgl_dropout2d_mask", "cgl_dropout2d_masks",
     "cgl_nchw_to_nhwc", "cgl_nhwc_to_nchw", "cgl_dense1_bwd_data_nhwc", "cgl_dense1_fwd_nhwc", "cgl_dense1_head_nhwc", "cgl_adv_loss", "cgl_adam_multi", "cgl_dense_workspace_bytes",
     "cgl_dense_fwd", "cgl_dense_bwd_data", "cgl_dense_bwd_weight", "cgl_gather_rows", "cgl_weights_scale",
-    "cgl_conv_packed_floats", "cgl_conv_pack_multi", "cgl_conv_batch_begin", "cgl_conv_batch_end", "cgl_conv_wgrad_defer_begin", "cgl_conv_wgrad_defer_end", "cgl_conv3x3_bias_by_colsum", "cgl_conv3x3_fwd_packed", "cgl_conv3x3_bwd_data_packed",
+    "cgl_conv_packed_floats", "cgl_conv_pack_multi", "cgl_conv_batch_begin", "cgl_conv_batch_end", "cgl_conv_wgrad_defer_begin", "cgl_conv_wgrad_defer_end", "cgl_conv_wgrad_defer_counters", "cgl_conv3x3_bias_by_colsum", "cgl_conv3x3_fwd_packed", "cgl_conv3x3_bwd_data_packed",
     "cgl_dense_fwd_packed", "cgl_dense_bwd_data_packed", "cgl_conv3x3_stat_chunks", "cgl_conv3x3_fwd_packed_stats",
     "cgl_bn2d_fwd_stats", "cgl_bn2d_fwd_stats_coef", "cgl_conv3x3_fwd_packed_bnin", "cgl_bn2d_stats_scratch_bytes", "cgl_linear_desc_bytes", "cgl_linear_prepare", "cgl_linear_prepare_gather", "cgl_linear_prepare_wgrad_nhwc",
     "cgl_linear_launch", "cgl_conv3x3_bwd_stat_chunks", "cgl_conv3x3_bwd_data_packed_stats", "cgl_conv3x3_bwd_data_stats", "cgl_bn2d_bwd_stats",
@@ -183,6 +183,7 @@ def _load():
         "cgl_conv3x3_bias_by_colsum": (ci, [ci, ci, ci, ci, ci, ci, ci]),
         "cgl_conv_wgrad_defer_begin": (ci, []),
         "cgl_conv_wgrad_defer_end": (ci, [vp]),
+        "cgl_conv_wgrad_defer_counters": (ci, [vp, ci, ci, vp, ci]),
         "cgl_conv3x3_fwd_packed": (ci, [vp, vp, vp, vp] + [ci] * 8 + [cf, vp, vp, i64, vp]),
         "cgl_conv3x3_bwd_data_packed": (ci, [vp, vp, vp, vp] + [ci] * 7 + [vp, i64, vp]),
         "cgl_conv3x3_stat_chunks": (i64, [ci] * 8),

@@ -528,6 +528,17 @@ def sample_rows_dev(src, nrows, seed, round_dev, dst, nv_out=None):
     return dst
 
 
+def defer_counters(counters, snap, snap_index, v=1):
+    """Inside wgrad_defer: the deferred launch also snapshots counters[snap_index] into snap and adds v to every
+    counter (cgl_conv_wgrad_defer_counters) -- counters_add without a launch of its own."""
+    if not _WDEFER:
+        raise RuntimeError("defer_counters outside wgrad_defer")
+    if not (counters.is_cuda and snap.is_cuda and counters.dtype == torch.int32 and snap.dtype == torch.int32):
+        raise ValueError("defer_counters: int32 device tensors")
+    C.check(C.lib.cgl_conv_wgrad_defer_counters(_p(counters), counters.numel(), int(v), _p(snap), int(snap_index)),
+            "cgl_conv_wgrad_defer_counters")
+
+
 def counters_add(counters, v=1):
     """counters (device int32) += v, stream-ordered."""
     C.check(C.lib.cgl_counters_add(_p(counters), counters.numel(), int(v), _s()), "cgl_counters_add")

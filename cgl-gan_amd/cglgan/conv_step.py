@@ -189,7 +189,9 @@ class ConvGanStep:
         # real batch through the device sampler (cgl_sample_rows_dev) -- and run() replays one
         # captured round as a hipGraph (N = 1; phases stay eager for the multi-worker exchange)
         self.graph = bool(graph)
-        self.dstate = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.dstate = torch.zeros(5, dtype=torch.int32, device=dev)
+        # dstate[4]: the G steps completed before this round's G Adam (written by the G backward's deferred launch
+        # when it also advances the counters: CGL_CONV_CNTFOLD, one cgl_counters_add launch fewer per round)
         # dstate[3]: real images of this round's D-step real call (DataLoader's short final batch of a pass,
         # capgan.py:282,326-331: a shard of n rows gives ceil(n / B) batches per pass, the last n mod B rows);
         # the D-step kernels leave the padding images of a short call out (nvalid)
@@ -323,6 +325,7 @@ class ConvGanStep:
             if self.bnb_col and C.lib.cgl_conv3x3_bias_by_colsum(*geo) == 1:
                 self.bcs[k] = torch.zeros(B * hw // 256 * c * 2, dtype=torch.float64, device=dev)
         self.wdefer = os.environ.get("CGL_CONV_WDEFER", "1") != "0"
+        self.cnt_fold = os.environ.get("CGL_CONV_CNTFOLD", "1") != "0"
         self.wws = {}
         if self.wdefer:
             geoms = {ck: (B2, hw, hw, ci, co, 2, 0) for ck, _, ci, co, hw in D_CONVS}
@@ -612,9 +615,11 @@ class ConvGanStep:
             elif dx is not None:
                 O.conv3x3_bwd_data(self.dc[0], P[ck + ".weight"], dx, n, hw, hw, ci, co, 2, 0, wp=self.pk[ck + "b"])
 
-    def _g_backward(self):
+    def _g_backward(self, counters=False):
         with O.wgrad_defer(self.wdefer):
             self._g_backward_ops()
+            if counters:     # round, G steps, D steps += 1 in the deferred launch; G's completed steps -> dstate[4]
+                O.defer_counters(self.dstate[0:3], self.dstate[4:5], 1)
 
     def _g_backward_ops(self):
         P, G, B = self.G.params, self.G.grads, self.B
@@ -755,11 +760,14 @@ class ConvGanStep:
 
     def phase_b(self):
         """Replicated G backward from the (exchanged) image gradient, lambda SGD, Adam G (capgan.py:258-260)."""
+        fold = self.graph and self.wdefer and self.cnt_fold
         with O.stream_cache():
-            self._g_backward()
-            self.G.adam(self.lr, self.betas, self.eps, step_dev=self.dstate[1:2] if self.graph else None)
+            self._g_backward(counters=fold)
+            self.G.adam(self.lr, self.betas, self.eps,
+                        step_dev=(self.dstate[4:5] if fold else self.dstate[1:2]) if self.graph else None)
             if self.graph:
-                O.counters_add(self.dstate[0:3], 1)     # round, G steps, D steps (epoch = 1)
+                if not fold:
+                    O.counters_add(self.dstate[0:3], 1)     # round, G steps, D steps (epoch = 1)
                 self._dstate_host = (self.round + 1, self.G.step, self.D.step)
         self._lam_step()
         self.round += 1

@@ -2832,12 +2832,23 @@ struct CglWgradReduceMulti {
   CglBnFinArgs fin[CGL_WDEFER_FIN];   // deferred column-sum finishes (bias gradients: cgl_colsum_finalize, col_sum)
   // a deferred one-output dense weight gradient (cgl_dense1_wgrad_k: the D head's adv_layer), d1_blocks > 0
   const float* d1_dy; const float* d1_x; float* d1_dw; float* d1_db; int d1_M, d1_K, d1_blocks;
+  // the round's device counters (cgl_conv_wgrad_defer_counters), one extra last block when cnt != null:
+  // *cnt_snap = cnt[cnt_si], then cnt[0 .. cnt_n) += cnt_v (nothing else in the launch reads them)
+  int* cnt; int* cnt_snap; int cnt_n, cnt_v, cnt_si;
 };
 
 __global__ __launch_bounds__(256) void cgl_conv_wgrad_reduce_multi(CglWgradReduceMulti m) {
   __shared__ double red[256];
   const int b = blockIdx.x, n = m.n;
   const int fend = m.begin[n] + m.c1_blocks + m.fbeg[m.nfin];
+  if (b >= fend + m.d1_blocks) {     // the counters block
+    const int t = threadIdx.x;
+    const int snap = m.cnt[m.cnt_si];
+    __syncthreads();                 // (every lane has read the snapshot value before lane 0..n-1 add)
+    if (t == 0) *m.cnt_snap = snap;
+    if (t < m.cnt_n) m.cnt[t] += m.cnt_v;
+    return;
+  }
   if (b >= fend) {
     cgl_dense1_wgrad_at(m.d1_dy, m.d1_x, m.d1_dw, m.d1_db, m.d1_M, m.d1_K, b - fend, m.d1_blocks, red);
     return;
@@ -4353,12 +4364,20 @@ int cgl_conv_wgrad_defer_begin(void) {
   return CGL_OK;
 }
 
+int cgl_conv_wgrad_defer_counters(int* counters, int n, int v, int* snap, int snap_index) {
+  if (!t_wdefer.on || t_wdefer.m.cnt) return CGL_E_STATE;
+  if (!counters || !snap || n < 1 || n > 64 || snap_index < 0 || snap_index >= n) return CGL_E_ARG;
+  CglWgradReduceMulti& m = t_wdefer.m;
+  m.cnt = counters; m.cnt_snap = snap; m.cnt_n = n; m.cnt_v = v; m.cnt_si = snap_index;
+  return CGL_OK;
+}
+
 int cgl_conv_wgrad_defer_end(void* stream) {
   if (!t_wdefer.on) return CGL_E_STATE;
   t_wdefer.on = false;
   CglWgradReduceMulti& m = t_wdefer.m;
   if (!t_wdefer.has_c1) m.c1_blocks = 0;
-  const int blocks = m.begin[m.n] + m.c1_blocks + m.fbeg[m.nfin] + m.d1_blocks;
+  const int blocks = m.begin[m.n] + m.c1_blocks + m.fbeg[m.nfin] + m.d1_blocks + (m.cnt ? 1 : 0);
   if (blocks == 0) return CGL_OK;
   hipLaunchKernelGGL(cgl_conv_wgrad_reduce_multi, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, m);
   return (int)hipGetLastError();

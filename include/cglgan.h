@@ -373,6 +373,12 @@ int cgl_conv_batch_end(void* stream);
  * Returns CGL_E_STATE for a nested begin or an end without begin. */
 int cgl_conv_wgrad_defer_begin(void);
 int cgl_conv_wgrad_defer_end(void* stream);
+/* Inside an open deferral: the deferred launch also carries the round's device counters (one extra block, after
+ * every other deferred step of the launch): *snap = counters[snap_index], then counters[0 .. n) += v, n <= 64 --
+ * cgl_counters_add folded into the G backward's deferred launch of the conv round (its G Adam then reads the
+ * completed-step count from *snap).  Nothing else in the launch may read the counters.  At most once per
+ * deferral (CGL_E_STATE otherwise, or outside a deferral). */
+int cgl_conv_wgrad_defer_counters(int* counters, int n, int v, int* snap, int snap_index);
 int cgl_conv3x3_fwd_packed(const float* X, const float* Wp, const float* bias, float* Y, int n, int h, int w, int cin,
                            int cout, int stride, int up, int act, float slope, const float* drop, void* workspace,
                            int64_t ws_bytes, void* stream);

@@ -23,6 +23,8 @@
     bias gradients, cgl_bn2d_bwd_stats colsum_part) instead of the weight gradient's own pass.
   * CGL_CONV_L1NHWC: G's Linear(100, 8192) gathers its weight rows in NHWC feature order (with the bias packed in
     that order) and writes the NHWC activation directly, instead of the NCHW output + a transpose launch.
+  * CGL_CONV_CNTFOLD: graph rounds advance the device round / step counters in the G backward's deferred launch
+    (cgl_conv_wgrad_defer_counters) instead of a cgl_counters_add launch; G Adam reads the snapshot.
   * CGL_CONV_HEADBN: D's last BatchNorm (model.14) applied in the fused head's loads instead of by cgl_eltwise.
   * CGL_CONV_HEADFUSE: the discriminator head (adv_layer forward, the loss head(s), adv_layer's input gradient) as
     one launch per pass (cgl_dense1_head_nhwc), its batch-mean losses reduced by the last workgroup."""
@@ -63,7 +65,8 @@ CASES = [("CGL_CONV_POSTCOEF", 8, False, "2"), ("CGL_CONV_POSTCOEF", 256, False,
          ("CGL_CONV_WDEFER", 8, False, "3"), ("CGL_CONV_WDEFER", 256, True, "3"), ("CGL_CONV_WDEFER", 256, False, "0"),
          ("CGL_CONV_HEADBN", 8, False, "3"), ("CGL_CONV_HEADBN", 256, True, "3"),
          ("CGL_CONV_BNBCOL", 8, False, "3"), ("CGL_CONV_BNBCOL", 256, True, "3"), ("CGL_CONV_BNBCOL", 256, False, "0"),
-         ("CGL_CONV_L1NHWC", 8, False, "3"), ("CGL_CONV_L1NHWC", 256, True, "3")]
+         ("CGL_CONV_L1NHWC", 8, False, "3"), ("CGL_CONV_L1NHWC", 256, True, "3"),
+         ("CGL_CONV_CNTFOLD", 8, True, "3"), ("CGL_CONV_CNTFOLD", 256, True, "3")]
 
 
 @pytest.mark.parametrize("var,B,graph,fold", CASES)
@@ -100,6 +103,10 @@ def test_conv_round_fusion_bitwise(var, B, graph, fold):
     elif var == "CGL_CONV_L1NHWC":
         assert a.l1nhwc and not b.l1nhwc
         assert torch.equal(a.h0, b.h0)
+    elif var == "CGL_CONV_CNTFOLD":
+        assert a.cnt_fold and not b.cnt_fold
+        assert torch.equal(a.dstate[:4], b.dstate[:4]) and a.dstate[:3].tolist() == [3, 3, 3]
+        assert a.dstate[4].item() == 2      # the G steps completed before the third round's G Adam
     elif var == "CGL_CONV_HEADBN":
         assert a.head_bn and not b.head_bn
         assert torch.equal(a.v, b.v) and torch.equal(a.dv, b.dv) and torch.equal(a.dr[3], b.dr[3])

@@ -162,7 +162,8 @@ def test_open_launch_batch_refuses_other_launches():
 
 def test_wgrad_defer_state():
     """cgl_conv_wgrad_defer_begin / _end (round 6): a nested begin and an end without begin return CGL_E_STATE; an
-    empty batch launches nothing (so this runs on CPU); and the Python wrapper refuses a weight gradient without a
+    empty batch launches nothing (so this runs on CPU); cgl_conv_wgrad_defer_counters checks its state and
+    arguments; and the Python wrapper refuses a weight gradient without a
     workspace of its own inside the block (its partials would be overwritten before the deferred reduction)."""
     import torch
     from cglgan import conv_ops as O
@@ -175,6 +176,20 @@ def test_wgrad_defer_state():
     finally:
         assert lib.cgl_conv_wgrad_defer_end(None) == 0
     assert lib.cgl_conv_wgrad_defer_end(None) == E_STATE
+    # the counters fold: outside a deferral CGL_E_STATE; inside, bad arguments CGL_E_ARG (nothing recorded, so the
+    # end launches nothing); the addresses are only checked for null, never dereferenced here
+    import ctypes
+    fake = ctypes.c_void_p(256)
+    assert lib.cgl_conv_wgrad_defer_counters(fake, 3, 1, fake, 0) == E_STATE
+    assert lib.cgl_conv_wgrad_defer_begin() == 0
+    try:
+        assert lib.cgl_conv_wgrad_defer_counters(fake, 0, 1, fake, 0) == -1
+        assert lib.cgl_conv_wgrad_defer_counters(fake, 3, 1, fake, 3) == -1
+        assert lib.cgl_conv_wgrad_defer_counters(None, 3, 1, fake, 0) == -1
+    finally:
+        assert lib.cgl_conv_wgrad_defer_end(None) == 0
+    with pytest.raises(RuntimeError, match="outside wgrad_defer"):
+        O.defer_counters(torch.zeros(3, dtype=torch.int32), torch.zeros(1, dtype=torch.int32), 0)
     O._WDEFER = True          # (the wrapper's check runs before any device work)
     try:
         t = torch.empty(0)
