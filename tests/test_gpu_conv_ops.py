@@ -320,6 +320,13 @@ def test_linear_gather_nhwc(M):
     assert (y1.double() - ref).abs().max() <= 2e-5 * ref.abs().max()
     with pytest.raises(ValueError):
         O.PreparedLinear(0, x, w, b, y1, None, M, 8192, 100, b_rows=rows + 8192)
+    # a table of no shift form goes through the per-launch index load: bitwise the Linear on the gathered W
+    rnd = torch.randperm(8192, device=DEV, generator=g).to(torch.int32)
+    y2, y3 = torch.empty(M, 8192, device=DEV), torch.empty(M, 8192, device=DEV)
+    O.PreparedLinear(0, x, w, b, y2, None, M, 8192, 100, b_rows=rnd)()
+    O.PreparedLinear(0, x, w[rnd.long()].contiguous(), b, y3, None, M, 8192, 100)()
+    torch.cuda.synchronize()
+    assert torch.equal(y2, y3)
     # the weight + bias gradient from the NHWC gradient (cgl_linear_prepare_wgrad_nhwc): bit for bit op 2 on
     # the NCHW transpose, close to fp64
     dy = torch.randn(M, 8, 8, 128, device=DEV, generator=g)
